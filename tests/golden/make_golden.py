@@ -1,0 +1,606 @@
+"""Generate the golden fixtures under tests/golden/ by running the REFERENCE on CPU.
+
+This is the only file in the repository that imports /root/reference, and it only
+runs in the build container (the reference never travels to the GPU box).  What it
+writes is data: seeded inputs and the reference's outputs, as small .npz files.
+
+Loading recipe: stub the absent third-party modules
+(icecream, telegram, the git-ignored pretrained CIFAR package, torchvision-backed
+data loaders), map hard-coded 'cuda' devices to CPU for the functions that use
+them, and import the reference's own quant/ modules unmodified.
+
+Run:  PYTHONDONTWRITEBYTECODE=1 python tests/golden/make_golden.py
+"""
+import os
+import sys
+import types
+
+os.environ["PYTHONDONTWRITEBYTECODE"] = "1"
+sys.dont_write_bytecode = True
+
+import numpy as np
+import torch
+import torch.nn as nn
+
+REF = "/root/reference"
+OUT = os.path.dirname(os.path.abspath(__file__))
+
+
+# --------------------------------------------------------------------------- stubs
+def _install_stubs():
+    ic_mod = types.ModuleType("icecream")
+
+    class _IC:
+        def configureOutput(self, **k):
+            pass
+
+        def disable(self):
+            pass
+
+        def __call__(self, *a, **k):
+            return a[0] if a else None
+
+    ic_mod.ic = _IC()
+    sys.modules["icecream"] = ic_mod
+
+    for name in ["pretrained", "pretrained.PyTorch_CIFAR10",
+                 "pretrained.PyTorch_CIFAR10.cifar10_models"]:
+        sys.modules[name] = types.ModuleType(name)
+    res = types.ModuleType("pretrained.PyTorch_CIFAR10.cifar10_models.resnet")
+
+    class BasicBlockCIFAR(nn.Module):
+        pass
+
+    def _absent(*a, **k):
+        raise RuntimeError("CIFAR pretrained models are absent")
+
+    res.BasicBlockCIFAR = BasicBlockCIFAR
+    res.resnet18 = res.resnet34 = res.resnet50 = _absent
+    sys.modules[res.__name__] = res
+
+    tg = types.ModuleType("telegram")
+    tg.Bot = object
+    sys.modules["telegram"] = tg
+
+
+def _install_cpu_device_shim():
+    """Map 'cuda' device requests to CPU (reference hard-codes them at
+    layer_recon_shiftedScale.py:268, block_recon.py:88, layer_recon.py:78)."""
+    orig_to = torch.Tensor.to
+
+    def _map(a):
+        if isinstance(a, str) and a.startswith("cuda"):
+            return "cpu"
+        if isinstance(a, torch.device) and a.type == "cuda":
+            return torch.device("cpu")
+        return a
+
+    def to(self, *args, **kw):
+        args = tuple(_map(a) for a in args)
+        if "device" in kw:
+            kw["device"] = _map(kw["device"])
+        return orig_to(self, *args, **kw)
+
+    torch.Tensor.to = to
+    orig_device = torch.device
+
+    class _DevMeta(type):
+        def __instancecheck__(cls, inst):
+            return isinstance(inst, orig_device)
+
+        def __call__(cls, *a, **k):
+            if a and isinstance(a[0], str) and a[0].startswith("cuda"):
+                a = ("cpu",) + a[1:]
+            return orig_device(*a, **k)
+
+    class device(metaclass=_DevMeta):
+        pass
+
+    torch.device = device
+
+
+_install_stubs()
+sys.path.insert(0, REF)
+from quant.quant_layer import UniformAffineQuantizer, lp_loss, QuantModule  # noqa: E402
+from quant.channelQuant import ChannelQuant  # noqa: E402
+from quant.channelQuantMSE import ChannelQuantMSE  # noqa: E402
+from quant.adaptive_rounding import AdaRoundQuantizer  # noqa: E402
+from quant import layer_recon_fused_shiftedScale as LRF  # noqa: E402
+from quant import layer_recon_shiftedScale as LRS  # noqa: E402
+from quant import block_recon as BR  # noqa: E402
+from quant.quant_model import QuantModel  # noqa: E402
+from models.resnet import resnet18  # noqa: E402
+import myScaledMethods as MSM  # noqa: E402
+
+_install_cpu_device_shim()
+
+
+def f32(x):
+    return np.ascontiguousarray(np.asarray(x, dtype=np.float32))
+
+
+def t2n(t):
+    if t is None:
+        return np.zeros(0, np.float32)
+    return f32(t.detach().cpu().numpy()).copy()  # never alias a tensor mutated later
+
+
+def save(name, **arrays):
+    path = os.path.join(OUT, name + ".npz")
+    np.savez_compressed(path, **{k: np.asarray(v) for k, v in arrays.items()})
+    print(f"wrote {path} ({os.path.getsize(path)} B)")
+
+
+def edge_tensor(g, shape, scale=1.0):
+    """Gaussian values plus exact .5 ties and clamp edges after scaling."""
+    x = torch.randn(shape, generator=g) * scale
+    flat = x.view(-1)
+    n = flat.numel()
+    k = max(1, n // 16)
+    flat[0::16] = (flat[0::16] * 4 / scale).round() * 0.125 * scale  # exact multiples of scale/8
+    flat[5::16] = 0.0
+    return x
+
+
+# --------------------------------------------------------------------------- K1-K4 UAQ
+def gen_uaq():
+    g = torch.Generator().manual_seed(1005)
+    out = {}
+    for bits in (2, 3, 4, 8):
+        for sym in (False, True):
+            for cw in (False, True):
+                for method in ("max", "mse"):
+                    tag = f"b{bits}_{'sym' if sym else 'asym'}_{'cw' if cw else 'pt'}_{method}"
+                    if not cw and (method == "max" or sym):
+                        # per-tensor 'max' and per-tensor symmetric return a Python int
+                        # zero_point that nn.Parameter rejects (quant_layer.py:88,140,161):
+                        # broken in the reference, so no golden exists for them.
+                        continue
+                    shape = (12, 5, 3, 3) if cw else (4, 6, 7, 7)
+                    x = edge_tensor(g, shape, 0.2 if cw else 1.0)
+                    if not cw:
+                        x = torch.relu(x) if not sym else x
+                    q = UniformAffineQuantizer(n_bits=bits, symmetric=sym, channel_wise=cw,
+                                               scale_method=method, leaf_param=not cw,
+                                               ch=shape)
+                    xr = x.clone().requires_grad_(True)
+                    y = q(xr)
+                    gy = torch.randn(shape, generator=g)
+                    (y * gy).sum().backward()
+                    out[tag + "_x"] = t2n(x)
+                    out[tag + "_y"] = t2n(y)
+                    out[tag + "_delta"] = t2n(q.delta.reshape(-1))
+                    out[tag + "_zp"] = t2n(q.zero_point.reshape(-1))
+                    rz = q.raw_zero_point
+                    out[tag + "_rawzp"] = f32(rz.detach().reshape(-1).numpy() if torch.is_tensor(rz) else [rz])
+                    out[tag + "_gy"] = t2n(gy)
+                    out[tag + "_gx"] = t2n(xr.grad)
+                    out[tag + "_gdelta"] = t2n(q.delta.grad.reshape(-1))
+                    out[tag + "_gzp"] = t2n(q.zero_point.grad.reshape(-1))
+    # zero-range channel -> delta clamps to 1e-8 (quant_layer.py:136-138)
+    x = torch.zeros(3, 4, 3, 3)
+    x[1] = 0.5
+    q = UniformAffineQuantizer(n_bits=2, channel_wise=True, scale_method="max", ch=x.shape)
+    y = q(x)
+    out["zero_x"], out["zero_y"] = t2n(x), t2n(y)
+    out["zero_delta"], out["zero_zp"] = t2n(q.delta.reshape(-1)), t2n(q.zero_point.reshape(-1))
+    save("uaq", **out)
+
+
+# --------------------------------------------------------------------------- K5-K9 ChannelQuant
+def _mk_uaq(w, bits=2, method="max"):
+    q = UniformAffineQuantizer(n_bits=bits, channel_wise=True, scale_method=method, ch=w.shape)
+    q(w)
+    return q
+
+
+def gen_channelquant():
+    g = torch.Generator().manual_seed(1005)
+    out = {}
+    shapes = {"conv": (8, 6, 3, 3), "fc": (10, 12), "dw": (6, 1, 3, 3)}
+    shift = [31 / 32, 33 / 32, 1.0]
+    for name, shape in shapes.items():
+        for bits in (2, 4):
+            tag = f"{name}_b{bits}"
+            w = torch.randn(shape, generator=g) * 0.05
+            uaq = _mk_uaq(w, bits)
+            cq = ChannelQuant(1.0, uaq=uaq, weight_tensor=w, shiftTarget=shift, name=tag)
+            cq.init_v_beta(w.clone())
+            cq.opt_mode = "adaShift"
+            out[tag + "_w"] = t2n(w)
+            out[tag + "_delta"] = t2n(cq.delta.reshape(-1))
+            out[tag + "_zp"] = t2n(cq.zero_point.reshape(-1))
+            out[tag + "_xq"] = np.stack([t2n(t) for t in cq.x_q])
+            out[tag + "_alpha0"] = t2n(cq.alpha)
+            out[tag + "_beta"] = t2n(cq.beta)
+            # perturb alpha so soft targets are not all at init
+            with torch.no_grad():
+                cq.alpha.add_(torch.randn(cq.alpha.shape, generator=g) * 0.5)
+            out[tag + "_alpha"] = t2n(cq.alpha)
+            gy = torch.randn(shape, generator=g)
+            out[tag + "_gy"] = t2n(gy)
+            for hard_t, hard_r in ((False, False), (True, True), (False, True), (True, False)):
+                cq.hard_targets, cq.hard_round = hard_t, hard_r
+                cq.alpha.grad = None
+                cq.beta.grad = None
+                y = cq(w)
+                k = f"{tag}_t{int(hard_t)}r{int(hard_r)}"
+                out[k + "_y"] = t2n(y)
+                if y.requires_grad:
+                    (y * gy).sum().backward()
+                    out[k + "_galpha"] = t2n(cq.alpha.grad) if cq.alpha.grad is not None else np.zeros(0, np.float32)
+                    out[k + "_gbeta"] = t2n(cq.beta.grad) if cq.beta.grad is not None else np.zeros(0, np.float32)
+            cq.hard_targets = cq.hard_round = False
+            out[tag + "_p"] = t2n(cq.get_sig_soft_targets())
+            out[tag + "_h"] = t2n(cq.get_soft_round())
+            out[tag + "_delta_sel"] = t2n(cq.get_delta())
+
+            # learned_hard_sigmoid path (init_v, channelQuant.py:201-213)
+            uaq2 = _mk_uaq(w, bits)
+            cq2 = ChannelQuant(1.0, uaq=uaq2, weight_tensor=w, shiftTarget=shift, name=tag)
+            cq2.init_v(w.clone())
+            out[tag + "_lhs_xq"] = np.stack([t2n(t) for t in cq2.x_q])
+            out[tag + "_lhs_alpha0"] = t2n(cq2.alpha)
+            with torch.no_grad():
+                cq2.alpha.add_(torch.randn(cq2.alpha.shape, generator=g) * 0.5)
+            out[tag + "_lhs_alpha"] = t2n(cq2.alpha)
+            for hard_t in (False, True):
+                cq2.hard_targets = hard_t
+                cq2.alpha.grad = None
+                y = cq2(w)
+                out[f"{tag}_lhs_t{int(hard_t)}_y"] = t2n(y)
+                if y.requires_grad:
+                    (y * gy).sum().backward()
+                    out[f"{tag}_lhs_t{int(hard_t)}_galpha"] = t2n(cq2.alpha.grad)
+            # adaround phase (layer_recon_shiftedScale.py:270-276): update_delta + init_beta
+            cq2.hard_targets = False
+            cq2.update_delta()
+            cq2.init_beta(w.clone())
+            cq2.opt_mode = "adaround"
+            out[tag + "_ar_delta"] = t2n(cq2.delta)
+            out[tag + "_ar_beta0"] = t2n(cq2.beta)
+            with torch.no_grad():
+                cq2.beta.add_(torch.randn(cq2.beta.shape, generator=g) * 0.5)
+            out[tag + "_ar_beta"] = t2n(cq2.beta)
+            for hard_r in (False, True):
+                cq2.hard_round = hard_r
+                cq2.beta.grad = None
+                y = cq2(w)
+                out[f"{tag}_ar_r{int(hard_r)}_y"] = t2n(y)
+                if y.requires_grad:
+                    (y * gy).sum().backward()
+                    out[f"{tag}_ar_r{int(hard_r)}_gbeta"] = t2n(cq2.beta.grad)
+            cq2.opt_mode = "none"
+            out[tag + "_none_y"] = t2n(cq2(w))
+    save("channelquant", **out)
+
+
+def gen_adaround():
+    g = torch.Generator().manual_seed(1005)
+    out = {}
+    for name, shape in {"conv": (8, 6, 3, 3), "fc": (10, 12)}.items():
+        w = torch.randn(shape, generator=g) * 0.05
+        uaq = _mk_uaq(w, 2)
+        ar = AdaRoundQuantizer(uaq=uaq, round_mode="learned_hard_sigmoid", weight_tensor=w)
+        out[name + "_w"] = t2n(w)
+        out[name + "_delta"] = t2n(ar.delta.reshape(-1))
+        out[name + "_zp"] = t2n(ar.zero_point.reshape(-1))
+        out[name + "_alpha0"] = t2n(ar.alpha)
+        with torch.no_grad():
+            ar.alpha.add_(torch.randn(shape, generator=g) * 0.5)
+        out[name + "_alpha"] = t2n(ar.alpha)
+        gy = torch.randn(shape, generator=g)
+        out[name + "_gy"] = t2n(gy)
+        for soft in (True, False):
+            ar.soft_targets = soft
+            ar.alpha.grad = None
+            y = ar(w)
+            out[f"{name}_s{int(soft)}_y"] = t2n(y)
+            if y.requires_grad:
+                (y * gy).sum().backward()
+                out[f"{name}_s{int(soft)}_galpha"] = t2n(ar.alpha.grad)
+        out[name + "_h"] = t2n(ar.get_soft_targets())
+    save("adaround", **out)
+
+
+# --------------------------------------------------------------------------- K10
+def gen_inpscale():
+    g = torch.Generator().manual_seed(1005)
+    out = {}
+    for bits in (2, 4):
+        w = torch.randn(16, 8, 3, 3, generator=g) * 0.05
+        for level in (1, 2, 8, 64):
+            for thr in (1.0, 2.0):
+                tag = f"b{bits}_l{level}_t{int(thr)}"
+                uaq = _mk_uaq(w, bits)
+                m = ChannelQuantMSE(1.0, uaq=uaq, weight_tensor=w, shiftTarget=[1.0], opt_mode="max",
+                                    level=level, threshold=thr, name=tag)
+                m.init_scale(w)
+                out[tag + "_inp"] = t2n(m.inp_scale)
+                out[tag + "_y"] = t2n(m(w))
+        out[f"b{bits}_w"] = t2n(w)
+        out[f"b{bits}_delta"] = t2n(uaq.delta.reshape(-1))
+        out[f"b{bits}_rawzp"] = t2n(uaq.raw_zero_point.reshape(-1))
+    # FC variant
+    w = torch.randn(10, 12, generator=g) * 0.05
+    uaq = _mk_uaq(w, 2)
+    m = ChannelQuantMSE(1.0, uaq=uaq, weight_tensor=w, shiftTarget=[1.0], opt_mode="max", level=8,
+                        threshold=2.0, name="fc")
+    m.init_scale(w)
+    out["fc_w"], out["fc_inp"], out["fc_y"] = t2n(w), t2n(m.inp_scale), t2n(m(w))
+    out["fc_delta"], out["fc_rawzp"] = t2n(uaq.delta.reshape(-1)), t2n(uaq.raw_zero_point.reshape(-1))
+    save("inpscale", **out)
+
+
+# --------------------------------------------------------------------------- K11/K12
+def gen_loss():
+    g = torch.Generator().manual_seed(1005)
+    out = {}
+    pred = torch.randn(4, 6, 5, 5, generator=g)
+    tgt = torch.randn(4, 6, 5, 5, generator=g)
+    out["pred"], out["tgt"] = t2n(pred), t2n(tgt)
+    for p in (1.0, 2.0, 2.4):
+        for red in ("none", "all"):
+            pr = pred.clone().requires_grad_(True)
+            l = lp_loss(pr, tgt, p=p, reduction=red)
+            l.backward()
+            out[f"p{p}_{red}_loss"] = f32([l.item()])
+            out[f"p{p}_{red}_grad"] = t2n(pr.grad)
+    # regularizers (layer_recon_fused_shiftedScale.py:277-282, layer_recon_shiftedScale.py:393,
+    # block_recon.py:171-174)
+    v = torch.randn(6, 3, generator=g) * 2
+    beta = torch.randn(8, 6, 3, 3, generator=g) * 2
+    out["reg_alpha"], out["reg_beta"] = t2n(v), t2n(beta)
+    gam, zet = -0.1, 1.1
+    for b in (0.0, 20.0, 11.3, 2.0):
+        a = v.clone().requires_grad_(True)
+        pS = torch.clamp(torch.softmax(a, dim=-1) * (zet - gam) + gam, 0, 1)
+        lS = 0.1 * (1 - ((pS - .5).abs() * 2).pow(b)).sum()
+        lS.backward()
+        out[f"regS_b{b}_loss"], out[f"regS_b{b}_grad"] = f32([lS.item()]), t2n(a.grad)
+        bb = beta.clone().requires_grad_(True)
+        hR = torch.clamp(torch.sigmoid(bb) * (zet - gam) + gam, 0, 1)
+        lR = 0.01 * (1 - ((hR - .5).abs() * 2).pow(b)).sum()
+        lR.backward()
+        out[f"regR_b{b}_loss"], out[f"regR_b{b}_grad"] = f32([lR.item()]), t2n(bb.grad)
+    a = v.clone().requires_grad_(True)
+    pS = torch.clamp(torch.softmax(a, dim=-1) * (zet - gam) + gam, 0, 1)
+    lE = 0.1 * (-torch.sum(pS * torch.log(pS + 1e-10)))
+    lE.backward()
+    out["regE_loss"], out["regE_grad"] = f32([lE.item()]), t2n(a.grad)
+    # schedules
+    ts = np.arange(0, 101, dtype=np.int64)
+    fused = LRF.FusedLinearTempDecayShift(100, rel_start_decay=0.2, start_b=20, end_b=2)
+    fused_s = LRF.FusedLinearTempDecayShift(100 * 3 / 4, rel_start_decay=0.2, start_b=20, end_b=2)
+    lin = BR.LinearTempDecay(100, rel_start_decay=0.2, start_b=20, end_b=2)
+    lsh = LRS.LinearTempDecayShift(100, rel_start_decay=0.2, start_b=20, end_b=2)
+    out["sched_t"] = ts
+    out["sched_fused"] = np.array([fused(t) for t in ts], np.float64)
+    out["sched_fused_shift"] = np.array([fused_s(t) for t in ts], np.float64)
+    out["sched_lin"] = np.array([lin(t) for t in ts], np.float64)
+    out["sched_lsh"] = np.array([lsh(t) for t in ts], np.float64)
+    save("loss", **out)
+
+
+# --------------------------------------------------------------------------- loop golden
+def _tiny_net():
+    """stem conv -> BN -> ReLU -> BasicBlock(16->32, stride 2, downsample) -> pool -> fc.
+    Small enough that the block's weights and features fit a sub-MB fixture; built from
+    the reference's own BasicBlock so QuantModel wraps it as a QuantBasicBlock."""
+    from models.resnet import BasicBlock
+    torch.manual_seed(1005)
+    ds = nn.Sequential(nn.Conv2d(16, 32, 1, stride=2, bias=False), nn.BatchNorm2d(32))
+    net = nn.Sequential(nn.Conv2d(3, 16, 3, padding=1, bias=False), nn.BatchNorm2d(16), nn.ReLU(),
+                        BasicBlock(16, 32, stride=2, downsample=ds, norm_layer=nn.BatchNorm2d),
+                        nn.AdaptiveAvgPool2d(1), nn.Flatten(), nn.Linear(32, 10))
+    g = torch.Generator().manual_seed(7)
+    for m in net.modules():
+        if isinstance(m, nn.Conv2d):
+            nn.init.kaiming_normal_(m.weight, mode="fan_out", nonlinearity="relu")
+        if isinstance(m, nn.BatchNorm2d):  # non-trivial folded statistics
+            m.running_mean.copy_(torch.randn(m.num_features, generator=g) * 0.1)
+            m.running_var.copy_(torch.rand(m.num_features, generator=g) + 0.5)
+            m.weight.data.copy_(torch.rand(m.num_features, generator=g) + 0.5)
+            m.bias.data.copy_(torch.randn(m.num_features, generator=g) * 0.1)
+    return net.eval()
+
+
+def _build_tiny_qnn(bits_w=2, bits_a=4):
+    wq = {"n_bits": bits_w, "channel_wise": True, "scale_method": "max", "tune_delta_zero": False,
+          "symmetric": False}
+    aq = {"n_bits": bits_a, "channel_wise": False, "scale_method": "mse", "tune_delta_zero": False,
+          "leaf_param": True, "symmetric": False}
+    qnn = QuantModel(model=_tiny_net(), weight_quant_params=wq, act_quant_params=aq)
+    qnn.eval()
+    qnn.set_first_last_layer_to_8bit()
+    return qnn
+
+
+BLOCK = ".model.3"
+CONVS = ("conv1", "conv2", "downsample")
+
+
+def _cache(qnn, names, cali, bs):
+    MSM.set_cache_state(qnn, names, prv_name="", state="if")
+    with torch.no_grad():
+        for i in range(len(cali) // bs):
+            qnn(cali[i * bs:(i + 1) * bs])
+    qnn.store_quantization_state()
+    qnn.set_quant_state(False, False)
+    MSM.set_cache_state(qnn, names, prv_name="", state="of")
+    with torch.no_grad():
+        for i in range(len(cali) // bs):
+            qnn(cali[i * bs:(i + 1) * bs])
+    qnn.restore_quantization_state()
+    MSM.set_cache_state(qnn, names, prv_name="", state="none")
+
+
+class _Spy:
+    """Records randperm draws and per-iteration loss values of a reference loop."""
+
+    def __init__(self, loss_cls):
+        self.loss_cls, self.perms, self.rec = loss_cls, [], []
+
+    def __enter__(self):
+        self.orig_call, self.orig_rp = self.loss_cls.__call__, torch.randperm
+        spy = self
+
+        def call(lf, pred, tgt, grad=None):
+            r = spy.orig_call(lf, pred, tgt, grad)
+            rl = getattr(lf, "rec_loss", 0.0)
+            spy.rec.append((float(rl) if not isinstance(rl, str) else float("nan"), float(r.item())))
+            return r
+
+        def rp(n, *a, **k):
+            r = spy.orig_rp(n, *a, **k)
+            spy.perms.append(r.clone())
+            return r
+
+        self.loss_cls.__call__ = call
+        torch.randperm = rp
+        return self
+
+    def __exit__(self, *exc):
+        self.loss_cls.__call__ = self.orig_call
+        torch.randperm = self.orig_rp
+
+
+def _dump_block(out, block, prefix=""):
+    for n in CONVS:
+        m = getattr(block, n)
+        out[prefix + n + "_w"] = t2n(m.org_weight)
+        out[prefix + n + "_b"] = t2n(m.org_bias)
+
+
+def gen_recon_fused(iters=30, n_cali=16, res=16):
+    qnn = _build_tiny_qnn()
+    torch.manual_seed(1005)
+    cali = torch.randn(n_cali, 3, res, res)
+    qnn.set_quant_state(True, False)
+    with torch.no_grad():
+        qnn(cali[:8])
+    shift = [31 / 32, 33 / 32, 1.0]
+    MSM.build_ShiftedChannelQuant(qnn, [BLOCK], "", shiftTarget=shift, skipShiftLayer=[])
+    qnn.set_quant_state(False, False)
+    _cache(qnn, [BLOCK], cali, 8)
+    MSM.set_quant_state_block(qnn, [BLOCK], "", True)
+    block = qnn.model[3]
+    out = {}
+    _dump_block(out, block)
+    for n in CONVS:
+        q = getattr(block, n).weight_quantizer
+        out[n + "_delta"] = t2n(q.delta.reshape(-1))
+        out[n + "_zp"] = t2n(q.zero_point.reshape(-1))
+    out["cached_inp"] = t2n(torch.cat(block.cached_inp_features))
+    out["cached_out"] = t2n(torch.cat(block.cached_out_features))
+    torch.manual_seed(1005)
+    with _Spy(LRF.FusedScaleLossFunction) as spy:
+        res_loss = LRF.block_recon_fused_shiftedScale(block, iters, (0.01, 0.1), qnn, None)
+    out["perms"] = np.stack([p.numpy() for p in spy.perms]).astype(np.int64)
+    out["rec_loss"] = np.array([r[0] for r in spy.rec], np.float64)
+    out["total_loss"] = np.array([r[1] for r in spy.rec], np.float64)
+    out["final_losses"] = np.array(res_loss, np.float64)
+    for n in CONVS:
+        m = getattr(block, n)
+        q = m.weight_quantizer
+        out[n + "_alpha"] = t2n(q.alpha)
+        out[n + "_beta0"] = t2n(q.beta)  # beta is never optimised in the fused loop
+        with torch.no_grad():
+            out[n + "_what_hard"] = t2n(q(m.weight))
+    out["iters"] = np.array([iters])
+    save("recon_fused", **out)
+
+
+def gen_recon_layer_shift(iters=20, n_cali=16, res=16):
+    """layer_recon_shiftedScale: shift phase then adaround phase on one conv."""
+    qnn = _build_tiny_qnn(bits_w=4, bits_a=8)
+    torch.manual_seed(1005)
+    cali = torch.randn(n_cali, 3, res, res)
+    qnn.set_quant_state(True, False)
+    with torch.no_grad():
+        qnn(cali[:8])
+    layer = BLOCK + ".conv1"
+    MSM.build_ShiftedChannelQuant(qnn, [BLOCK], "", shiftTarget=[31 / 32, 33 / 32, 1.0],
+                                  skipShiftLayer=[])
+    qnn.set_quant_state(False, False)
+    _cache(qnn, [layer], cali, 8)
+    m = qnn.model[3].conv1
+    m.use_weight_quant = True
+    out = {"w": t2n(m.org_weight), "b": t2n(m.org_bias),
+           "delta": t2n(m.weight_quantizer.delta.reshape(-1)),
+           "zp": t2n(m.weight_quantizer.zero_point.reshape(-1)),
+           "cached_inp": t2n(torch.cat(m.cached_inp_features)),
+           "cached_out": t2n(torch.cat(m.cached_out_features))}
+    torch.manual_seed(1005)
+    with _Spy(LRS.ScaleLossFunction) as spy:
+        l1 = LRS.layer_recon_shiftedScale(m, iters, 0.1, qnn, None)
+    out["shift_perms"] = np.stack([p.numpy() for p in spy.perms]).astype(np.int64)
+    out["shift_total_loss"] = np.array([r[1] for r in spy.rec], np.float64)
+    out["shift_rec_loss"] = np.array([r[0] for r in spy.rec], np.float64)
+    out["shift_final"] = np.array(l1, np.float64)
+    out["shift_alpha"] = t2n(m.weight_quantizer.alpha)
+    out["shift_xq"] = np.stack([t2n(t) for t in m.weight_quantizer.x_q])
+    m.weight_quantizer.hard_targets = False
+    with _Spy(LRS.ScaleLossFunction) as spy:
+        l2 = LRS.layer_recon_shiftedScale(m, iters, 0.01, qnn, None, adaround=True)
+    out["ar_perms"] = np.stack([p.numpy() for p in spy.perms]).astype(np.int64)
+    out["ar_total_loss"] = np.array([r[1] for r in spy.rec], np.float64)
+    out["ar_rec_loss"] = np.array([r[0] for r in spy.rec], np.float64)
+    out["ar_final"] = np.array(l2, np.float64)
+    out["ar_delta"] = t2n(m.weight_quantizer.delta)
+    out["ar_beta"] = t2n(m.weight_quantizer.beta)
+    with torch.no_grad():
+        out["ar_what"] = t2n(m.weight_quantizer(m.weight))
+    out["iters"] = np.array([iters])
+    save("recon_layer_shift", **out)
+
+
+def gen_recon_brecq(iters=10, n_cali=16, res=16):
+    """BRECQ block_reconstruction (AdaRound weights), then the act-delta (LSQ) branch."""
+    qnn = _build_tiny_qnn()
+    torch.manual_seed(1005)
+    cali = torch.randn(n_cali, 3, res, res)
+    qnn.set_quant_state(True, False)
+    with torch.no_grad():
+        qnn(cali[:8])
+    block = qnn.model[3]
+    out = {"cali": t2n(cali)}
+    _dump_block(out, block)
+    for n in CONVS:
+        q = getattr(block, n).weight_quantizer
+        out[n + "_delta"] = t2n(q.delta.reshape(-1))
+        out[n + "_zp"] = t2n(q.zero_point.reshape(-1))
+    torch.manual_seed(1005)
+    with _Spy(BR.LossFunction) as spy:
+        BR.block_reconstruction(qnn, block, cali, batch_size=8, iters=iters, weight=0.01,
+                                asym=True, b_range=(20, 2), warmup=0.2, act_quant=False, opt_mode="mse")
+    out["w_perms"] = np.stack([p.numpy() for p in spy.perms]).astype(np.int64)
+    out["w_total_loss"] = np.array([r[1] for r in spy.rec], np.float64)
+    for n in CONVS:
+        m = getattr(block, n)
+        out[n + "_alpha"] = t2n(m.weight_quantizer.alpha)
+        with torch.no_grad():
+            out[n + "_what_hard"] = t2n(m.weight_quantizer(m.weight))
+    save("recon_brecq", **out)
+
+
+if __name__ == "__main__":
+    which = sys.argv[1:] or ["uaq", "channelquant", "adaround", "inpscale", "loss", "recon",
+                             "layershift", "brecq"]
+    torch.set_num_threads(4)
+    if "uaq" in which:
+        gen_uaq()
+    if "channelquant" in which:
+        gen_channelquant()
+    if "adaround" in which:
+        gen_adaround()
+    if "inpscale" in which:
+        gen_inpscale()
+    if "loss" in which:
+        gen_loss()
+    if "recon" in which:
+        gen_recon_fused()
+    if "layershift" in which:
+        gen_recon_layer_shift()
+    if "brecq" in which:
+        gen_recon_brecq()
