@@ -1,0 +1,208 @@
+"""Benchmark of the shifted-scale calibration hot path on MI355X (BASELINE.json metric).
+
+    python bench.py [--gpus N] [--steps K] [--warmup W]
+    python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N ...
+
+One step (configs[1], ResNet-18 W2A4, 1024 calibration samples, synthetic data) =
+  * A4 per-tensor q/dq of the block-input activation cache [1024,64,56,56] fp32
+    (205.5 M elements, 822 MB >> the 256 MB Infinity Cache), delta/zp from the 'mse'
+    init on the first 64 samples, and
+  * W2 per-channel q/dq of every ResNet-18 conv/fc weight (11.68 M elements, 8-bit
+    stem/head) in ONE multi-tensor launch.
+value = elements processed by all ranks / max-over-ranks wall time (Gelem/s, weak
+scaling: every rank owns its own calibration shard; no data-path collective).
+The reconstruction iteration rate (block_recon_fused_shiftedScale, batch 32) is
+reported beside it as `recon`.
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+import torch
+import torch.distributed as dist
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+from shiftedscalequantization_amd import kernels as K  # noqa: E402
+
+HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec peak (MI355X_MICROARCH.md)
+RESNET18_SHAPES = ([(64, 3, 7, 7)] + [(64, 64, 3, 3)] * 4 +
+                   [(128, 64, 3, 3), (128, 128, 3, 3), (128, 64, 1, 1), (128, 128, 3, 3),
+                    (128, 128, 3, 3)] +
+                   [(256, 128, 3, 3), (256, 256, 3, 3), (256, 128, 1, 1), (256, 256, 3, 3),
+                    (256, 256, 3, 3)] +
+                   [(512, 256, 3, 3), (512, 512, 3, 3), (512, 256, 1, 1), (512, 512, 3, 3),
+                    (512, 512, 3, 3)] + [(1000, 512)])
+
+
+def parse():
+    p = argparse.ArgumentParser()
+    p.add_argument("--gpus", type=int, default=1)
+    p.add_argument("--steps", type=int, default=20)
+    p.add_argument("--warmup", type=int, default=5)
+    p.add_argument("--n-cali", type=int, default=1024)
+    p.add_argument("--no-cpu-baseline", action="store_true")
+    p.add_argument("--cpu-seconds", type=float, default=10.0)
+    p.add_argument("--no-recon", action="store_true")
+    p.add_argument("--recon-iters", type=int, default=200)
+    p.add_argument("--variant", type=int, default=-1, help="streaming cache policy A/B")
+    return p.parse_args()
+
+
+def setup():
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    torch.cuda.set_device(local)
+    if world > 1:
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    return rank, world, torch.device("cuda", local)
+
+
+def barrier(world):
+    if world > 1:
+        dist.barrier()
+
+
+def max_over_ranks(v, world, dev):
+    if world == 1:
+        return v
+    t = torch.tensor([v], dtype=torch.float64, device=dev)
+    dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    return t.item()
+
+
+def make_workload(dev, rank, n_cali):
+    g = torch.Generator(device=dev).manual_seed(1005 + rank)
+    act = torch.empty(n_cali, 64, 56, 56, device=dev)
+    act.normal_(generator=g).relu_()
+    d_a, z_a, _ = K.scale_init(act[:64], 4, False, False, "mse")
+    weights, dws, zws, bits = [], [], [], []
+    for i, s in enumerate(RESNET18_SHAPES):
+        w = torch.empty(s, device=dev).normal_(0.0, 0.02, generator=g)
+        b = 8 if i in (0, len(RESNET18_SHAPES) - 1) else 2
+        d, z, _ = K.scale_init(w, b, False, True, "max")
+        weights.append(w)
+        dws.append(d)
+        zws.append(z)
+        bits.append(b)
+    return act, d_a, z_a, weights, dws, zws, bits
+
+
+def time_events(fn, reps, dev):
+    start, end = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    start.record()
+    for _ in range(reps):
+        fn()
+    end.record()
+    torch.cuda.synchronize(dev)
+    return start.elapsed_time(end) / reps  # ms
+
+
+def cpu_baseline(act_dev, d_a, z_a, seconds):
+    """The plain-C oracle (scalar port, 1 thread) on a bounded sample of the same
+    workload: the first 16 calibration samples of the activation cache, repeated for
+    about `seconds` of CPU time."""
+    from oracle import c_oracle
+    sample = act_dev[:16].cpu().numpy()
+    d, z = d_a.cpu().numpy(), z_a.cpu().numpy()
+    c_oracle.fake_quant(sample[:1], d, z, 4)  # load / warm
+    n, t0 = 0, time.perf_counter()
+    while True:
+        c_oracle.fake_quant(sample, d, z, 4)
+        n += 1
+        el = time.perf_counter() - t0
+        if el >= seconds:
+            break
+    return {"value": round(n * sample.size / el / 1e9, 4), "unit": "Gelem/s", "cores": 1,
+            "kind": "port",
+            "sample": f"oracle/c ssqo_fake_quant, A4 per-tensor q/dq of act[:16] "
+                      f"({sample.size} elems) x{n} reps, {el:.1f}s, 1 thread, "
+                      f"{os.cpu_count()} host CPUs visible"}
+
+
+def main():
+    args = parse()
+    rank, world, dev = setup()
+    if args.variant >= 0:
+        K.set_variant(args.variant)
+    act, d_a, z_a, weights, dws, zws, bits = make_workload(dev, rank, args.n_cali)
+    y_act = torch.empty_like(act)
+    n_act = act.numel()
+    n_w = sum(w.numel() for w in weights)
+    elems_per_step = n_act + n_w
+
+    def step():
+        K.fake_quant_fwd(act, d_a, z_a, 4)
+        K.fake_quant_multi(weights, dws, zws, bits)
+
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize(dev)
+    barrier(world)
+    torch.cuda.synchronize(dev)
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        step()
+    torch.cuda.synchronize(dev)
+    barrier(world)
+    elapsed = max_over_ranks(time.perf_counter() - t0, world, dev)
+    value = world * elems_per_step * args.steps / elapsed / 1e9
+
+    # dominant kernel: the A4 activation q/dq, timed alone with HIP events on the stream
+    # it is launched on (torch's current stream)
+    ms_fq = time_events(lambda: K.fake_quant_fwd(act, d_a, z_a, 4), 20, dev)
+    alg_bytes = 8.0 * n_act
+    achieved = alg_bytes / (ms_fq * 1e-3) / 1e9
+    ms_copy = time_events(lambda: K.stream_copy(act, y_act), 20, dev)
+    copy_gbs = 8.0 * n_act / (ms_copy * 1e-3) / 1e9
+    ms_w = time_events(lambda: K.fake_quant_multi(weights, dws, zws, bits), 20, dev)
+
+    recon = None
+    if not args.no_recon:
+        try:
+            from shiftedscalequantization_amd.recon_bench import run_recon_bench
+            recon = run_recon_bench(dev, world, rank, iters=args.recon_iters)
+        except ImportError:
+            recon = None
+
+    out = {
+        "metric": "Gelem/s shifted-scale q/dq + recon iters/s, ResNet-18 W2A4; top-1 vs ref",
+        "value": round(value, 3),
+        "unit": "Gelem/s",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": round(elapsed / args.steps * 1e3, 4),
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "f32",
+        "data": "synthetic (ReLU(N(0,1)) activation cache, N(0,0.02^2) ResNet-18-shaped weights)",
+        "config": {"workload": "resnet18 W2A4 bias_cal+bias_ch_quant, 1024 calib samples: A4 "
+                               "per-tensor q/dq of act [1024,64,56,56] + W2 per-channel q/dq of "
+                               "all 21 conv/fc weights (8-bit stem/head)",
+                   "elems_per_step_per_rank": elems_per_step, "parallelism": f"dp{world}"},
+        "roofline": {"bound": "hbm", "kernel": "fq_fwd_pt (ssq_fq_fwd, per-tensor A4)",
+                     "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                     "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": None,
+                     "kernel_ms": round(ms_fq, 4), "alg_bytes_per_launch": int(alg_bytes),
+                     "stream_copy_gbs": round(copy_gbs, 1),
+                     "frac_of_stream_copy": round(achieved / copy_gbs, 4)},
+        "weights_multi_ms": round(ms_w, 4),
+    }
+    if recon is not None:
+        out["recon"] = recon
+    if world == 1 and rank == 0 and not args.no_cpu_baseline:
+        out["cpu_baseline"] = cpu_baseline(act, d_a, z_a, args.cpu_seconds)
+    if rank == 0:
+        print(json.dumps(out), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

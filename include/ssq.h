@@ -1,0 +1,209 @@
+/*
+ * ssq.h -- C ABI of libssq.so, the MI355X (gfx950) kernels of the shifted-scale
+ * PTQ calibration path.  Plain pointers and sizes only: every pointer is DEVICE
+ * memory owned by the caller (PyTorch's caching allocator in the Python host layer),
+ * borrowed for the duration of the call.  Launches are asynchronous on `stream`
+ * (a hipStream_t passed as void*); no entry point allocates, synchronizes or keeps
+ * state, so every call is graph-capturable.
+ *
+ * Return value: 0 on success; a negative SSQ_E* code for an argument error; otherwise
+ * the hipError_t of a failed launch.  ssq_last_error() returns a thread-local message.
+ *
+ * The reference (jai1215snu/ShiftedScaleQuantization) is pure PyTorch: it has no FFI.
+ * Each entry point below replaces the eager-op sequence cited beside it; the reference
+ * "binding" that calls it is the quantizer module's forward/backward, whose Python
+ * mirror (shiftedscalequantization_amd.quant) calls this ABI through ctypes
+ * (INTEGRATION.md shows the binding).
+ *
+ * Common geometry: a weight tensor is viewed as (Co, Ci, K) with K = kh*kw (K = 1 for
+ * Linear).  "delta_per_ci" selects a delta of shape (Co,) (0) or (Co, Ci) (1, after
+ * ChannelQuant.update_delta).  Quantized codes are written as one byte per element:
+ * uint8 for asymmetric ranges, int8 (two's complement) for symmetric ones.
+ */
+#ifndef SSQ_H_
+#define SSQ_H_
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define SSQ_OK 0
+#define SSQ_E_ARG (-1)      /* invalid size / pointer / enum */
+#define SSQ_E_WS (-2)       /* workspace too small */
+
+typedef void* ssq_stream_t; /* hipStream_t */
+
+const char* ssq_last_error(void);
+int ssq_version(void);
+/* Cache-policy variant of the streaming kernels (0 plain, 1 non-temporal); returns the
+ * previous value.  Used by bench.py for A/B measurements only.                        */
+int ssq_set_variant(int variant);
+
+/* ---------------------------------------------------------------- K1/K2 uniform affine q/dq
+ * UniformAffineQuantizer.forward (quant_layer.py:77-98), ChannelQuant opt_mode 'none'
+ * (channelQuant.py:79-94) and ChannelQuantAct 'none' (channelQuantAct.py:56-67):
+ *   d = delta[c]*scale; q = clamp(rint(x/d) + zp[c], qmin, qmax); y = (q - zp[c]) * d
+ * Element i belongs to channel c = (i / inner) % nch   (nch == 1: per-tensor).     */
+int ssq_fq_fwd(const float* x, float* y, void* codes_or_null, const float* delta,
+               const float* zp, int64_t n, int64_t inner, int64_t nch, float scale,
+               int qmin, int qmax, ssq_stream_t stream);
+
+/* Several tensors in ONE launch (e.g. every conv weight of a network): segment s is
+ * the tensor x[s] (n[s] elements, inner[s] per channel, nch[s] channels). Per-channel
+ * delta/zp of the tile a workgroup covers are staged in LDS. Arrays are HOST arrays of
+ * length nseg; the pointers they hold are device pointers.                          */
+int ssq_fq_fwd_multi(int nseg, const float* const* x, float* const* y,
+                     const float* const* delta, const float* const* zp,
+                     const int64_t* n, const int64_t* inner, const int64_t* nch,
+                     const int* qmin, const int* qmax, ssq_stream_t stream);
+
+/* STE backward of ssq_fq_fwd (autograd of quant_layer.py:92-98):
+ *   gx = where(qmin <= rint(x/d)+zp <= qmax, gy*d, 0) / d
+ *   gdelta[c] = sum gy*(q-zp) - sum g_int*((x/d)/d) ; gzp[c] = sum g_int - sum gy*d
+ * gx / gdelta / gzp may each be NULL. Channel reductions are deterministic (fixed
+ * order partials in `ws`, reduced in double).                                         */
+size_t ssq_fq_bwd_workspace_size(int64_t n, int64_t inner, int64_t nch);
+int ssq_fq_bwd(const float* x, const float* gy, const float* delta, const float* zp,
+               int64_t n, int64_t inner, int64_t nch, int qmin, int qmax,
+               float* gx, float* gdelta, float* gzp, void* ws, size_t ws_bytes,
+               ssq_stream_t stream);
+
+/* ---------------------------------------------------------------- K3/K4 scale init
+ * init_quantization_scale (quant_layer.py:100-166) for `rows` independent rows of
+ * `inner` elements (rows = Co for channel-wise weights, 1 for a per-tensor activation).
+ * method 0 = 'max' (fp64 finalize exactly as the host Python; scale_flag = 'scale' in
+ * scale_method), 1 = 'mse' (80 shrink candidates, mean |x-q|^2.4, first strict min).
+ * Outputs delta, zp, raw_zp: `rows` floats each.  `scores_or_null` receives the
+ * rows x 80 candidate scores (mse only) for inspection.                                */
+size_t ssq_scale_init_workspace_size(int64_t rows, int64_t inner, int method);
+int ssq_scale_init(const float* x, int64_t rows, int64_t inner, int n_bits, int sym,
+                   int method, int scale_flag, float* delta, float* zp, float* raw_zp,
+                   double* scores_or_null, void* ws, size_t ws_bytes, ssq_stream_t stream);
+
+/* ---------------------------------------------------------------- K5-K9 ChannelQuant
+ * Shift-candidate floors are recomputed in-kernel from W:  F_i = floor(W / (delta*s_i)).
+ * alpha layout: conv (Ci, S); Linear (Co, Ci, S)  (is_fc = 1).  S <= 8.
+ * `shifts` (the shiftTarget list) is a HOST array of S floats; every other pointer is
+ * device memory.                                                                      */
+
+/* ChannelQuant.init_v_beta (channelQuant.py:279-294) + init_alpha (:158-199) +
+ * get_delta (:221-237): writes alpha (init logits), beta (W-shaped), and the per-(Ci,S)
+ * (conv) / per-element (fc) squared-error table mse_out (may be NULL).                 */
+size_t ssq_shift_init_workspace_size(int64_t Co, int64_t Ci, int64_t K, int S, int is_fc);
+int ssq_shift_init(const float* W, const float* delta, const float* shifts, int S,
+                   int64_t Co, int64_t Ci, int64_t K, int is_fc, float* alpha, float* beta,
+                   float* mse_out, void* ws, size_t ws_bytes, ssq_stream_t stream);
+
+/* ChannelQuant.init_beta (channelQuant.py:300-307) / AdaRoundQuantizer.init_alpha
+ * (adaptive_rounding.py:66-74): beta = -log((zeta-gamma)/(rest-gamma) - 1).           */
+int ssq_rect_init(const float* W, const float* delta, int delta_per_ci, int64_t Co,
+                  int64_t Ci, int64_t K, float* beta, ssq_stream_t stream);
+
+/* ChannelQuant.get_delta (channelQuant.py:221-237): out (Co, Ci) = delta * s[argmax p].*/
+int ssq_get_delta(const float* delta, const float* alpha, const float* shifts, int S,
+                  int64_t Co, int64_t Ci, int is_fc, float* out, ssq_stream_t stream);
+
+/* ChannelQuant.forward 'adaShift' (channelQuant.py:51-64, shifted_x_quant :96-118):
+ *   Xf = hard_targets ? F_{argmax p} : sum_i F_i * p_i   (separate fp32 roundings)
+ *   Q  = clamp(Xf + (hard_round ? [beta>=0] : h(beta)) + zp, qmin, qmax)
+ *   What = (Q - zp) * delta                                                           */
+int ssq_adashift_fwd(const float* W, const float* alpha, const float* beta,
+                     const float* delta, const float* zp, const float* shifts, int S,
+                     int64_t Co, int64_t Ci, int64_t K, int is_fc, int hard_targets,
+                     int hard_round, int qmin, int qmax, float* What, void* codes_or_null,
+                     ssq_stream_t stream);
+
+/* Backward of the soft-target adaShift forward wrt alpha (and beta if gbeta != NULL).
+ * Conv alpha gradients are reduced over (Co, K) deterministically through `ws`.
+ * Fused shift regulariser (layer_recon_fused_shiftedScale.py:281-282), applied when
+ * reg_lambda != 0:  reg = lambda * sum(1 - |2p-1|^b);  its gradient is added to
+ * galpha and per-alpha-row values are written to reg_vals (may be NULL).
+ * galpha is OVERWRITTEN (not accumulated).                                             */
+size_t ssq_adashift_bwd_workspace_size(int64_t Co, int64_t Ci, int64_t K, int S, int is_fc);
+int ssq_adashift_bwd(const float* gWhat, const float* W, const float* alpha,
+                     const float* beta, const float* delta, const float* zp,
+                     const float* shifts, int S, int64_t Co, int64_t Ci, int64_t K,
+                     int is_fc, int hard_round, int qmin, int qmax, float reg_lambda,
+                     float reg_b, float* galpha, float* gbeta, float* reg_vals, void* ws,
+                     size_t ws_bytes, ssq_stream_t stream);
+
+/* Shift-regulariser alone (value + gradient wrt alpha), for iterations where the
+ * reconstruction gradient is not wanted.  mode 0: lambda*sum(1-|2p-1|^b)
+ * (fused loss); mode 1: entropy lambda*-sum(p log(p+1e-10))
+ * (layer_recon_shiftedScale.py:393,467).  galpha is ACCUMULATED (+=) if not NULL.     */
+int ssq_shift_reg(const float* alpha, int S, int64_t rows, int mode, float lambda, float b,
+                  float* galpha, float* reg_vals, ssq_stream_t stream);
+
+/* 'learned_hard_sigmoid' (channelQuant.py:81-82): What = sum_i Xq_i * p_i (or Xq_{argmax})
+ * where Xq_i are the DEQUANTIZED candidates of init_v (channelQuant.py:201-213), i.e.
+ * 'none'-mode q/dq of W at delta*s_i, recomputed in-kernel.  galpha OVERWRITTEN.      */
+int ssq_lhs_fwd(const float* W, const float* alpha, const float* delta, const float* zp,
+                const float* shifts, int S, int64_t Co, int64_t Ci, int64_t K, int is_fc,
+                int hard_targets, int qmin, int qmax, float* What, ssq_stream_t stream);
+int ssq_lhs_bwd(const float* gWhat, const float* W, const float* alpha, const float* delta,
+                const float* zp, const float* shifts, int S, int64_t Co, int64_t Ci,
+                int64_t K, int is_fc, int qmin, int qmax, float* galpha, void* ws,
+                size_t ws_bytes, ssq_stream_t stream);
+
+/* 'adaround' mode (channelQuant.py:65-78) and AdaRoundQuantizer 'learned_hard_sigmoid'
+ * (adaptive_rounding.py:38-67):  Q = clamp(floor(W/d) + (hard ? [beta>=0] : h(beta)) + zp)
+ * What = (Q - zp)*d, d = delta*scale.  Backward gives gbeta (W-shaped, OVERWRITTEN).  */
+int ssq_adaround_fwd(const float* W, const float* beta, const float* delta, int delta_per_ci,
+                     const float* zp, float scale, int64_t Co, int64_t Ci, int64_t K,
+                     int hard_round, int qmin, int qmax, float* What, void* codes_or_null,
+                     ssq_stream_t stream);
+int ssq_adaround_bwd(const float* gWhat, const float* W, const float* beta,
+                     const float* delta, int delta_per_ci, const float* zp, float scale,
+                     int64_t Co, int64_t Ci, int64_t K, int qmin, int qmax, float* gbeta,
+                     ssq_stream_t stream);
+
+/* Rounding regulariser lambda*sum(1-|2h(v)-1|^b) over h = rect_sigmoid(v)
+ * (layer_recon_fused_shiftedScale.py:278-279, block_recon.py:171-174,
+ * layer_recon_shiftedScale.py:386-387).  loss_out: one float (deterministic).
+ * gv (may be NULL) is ACCUMULATED (+=).                                               */
+size_t ssq_round_reg_workspace_size(int64_t n);
+int ssq_round_reg(const float* v, int64_t n, float lambda, float b, float* loss_out,
+                  float* gv, void* ws, size_t ws_bytes, ssq_stream_t stream);
+
+/* ---------------------------------------------------------------- K10 ChannelQuantMSE
+ * init_scale 'max' mode (channelQuantMSE.py:203-241): per column j of W viewed as
+ * (Co, J) keep the LAST candidate c = k/level (k = level..1) whose normalized codes
+ * ((W/c)/delta + zero)/(2^b-1), zero = rint(raw_zp/delta), lie in the open range
+ * (-0.5*thr/(2^b-1), 1+0.5*thr/(2^b-1)) over all Co.  inp_scale: J floats.           */
+int ssq_inpscale_search(const float* W, const float* delta, const float* raw_zp,
+                        int64_t Co, int64_t J, int n_bits, int level, float threshold,
+                        float* inp_scale, ssq_stream_t stream);
+/* ChannelQuantMSE.forward (channelQuantMSE.py:267-276). */
+int ssq_inpscale_fwd(const float* W, const float* inp_scale, const float* delta,
+                     const float* raw_zp, int64_t Co, int64_t J, int n_bits, float* What,
+                     ssq_stream_t stream);
+
+/* ---------------------------------------------------------------- K11 reconstruction loss
+ * lp_loss (quant_layer.py:25-32) value and its gradient wrt pred in one pass:
+ *   loss = sum |pred-tgt|^p / M ;  grad = gscale * ((1/M) * (p*|d|^(p-1)) * sgn(d))
+ * M = n / C for reduction 'none' (sum over dim 1, mean over the rest), n for 'all'.
+ * loss_out / grad / gscale (a DEVICE scalar, the upstream gradient) may each be NULL.
+ * The loss reduction is deterministic.                                                */
+size_t ssq_lp_loss_workspace_size(int64_t n);
+int ssq_lp_loss(const float* pred, const float* tgt, int64_t n, int64_t M, float p,
+                float* loss_out, float* grad, const float* gscale, void* ws, size_t ws_bytes,
+                ssq_stream_t stream);
+
+/* ---------------------------------------------------------------- K14 batch gather
+ * dst_k[r] = src_k[idx[r]] for two sources at once (cached block input and output,
+ * layer_recon_fused_shiftedScale.py:95-97). src1/dst1 may be NULL.                    */
+int ssq_gather_rows2(const float* src0, float* dst0, int64_t row0, const float* src1,
+                     float* dst1, int64_t row1, const int64_t* idx, int64_t nidx,
+                     ssq_stream_t stream);
+
+/* ---------------------------------------------------------------- bandwidth probe
+ * float4 device copy, used by bench.py to report the measured stream bandwidth.      */
+int ssq_stream_copy(const float* src, float* dst, int64_t n, ssq_stream_t stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* SSQ_H_ */

@@ -1,0 +1,140 @@
+"""ctypes binding of libssq.so (include/ssq.h) plus tensor helpers.
+
+This is the ONLY way the Python host layer reaches the HIP kernels.  There is no CPU
+fallback: if the library is missing, or a tensor is not on the HIP device, the call
+raises.  torch is imported before the library is loaded so that libssq.so binds to the
+HIP runtime already mapped by PyTorch (same soname, one runtime per process).
+"""
+import ctypes as C
+import os
+
+import torch
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.environ.get("SSQ_LIB", os.path.join(_HERE, "libssq.so"))
+
+_p = C.c_void_p
+_i64 = C.c_int64
+_i = C.c_int
+_f = C.c_float
+_sz = C.c_size_t
+
+# name -> (restype, argtypes)
+SIGNATURES = {
+    "ssq_last_error": (C.c_char_p, []),
+    "ssq_version": (_i, []),
+    "ssq_set_variant": (_i, [_i]),
+    "ssq_fq_fwd": (_i, [_p, _p, _p, _p, _p, _i64, _i64, _i64, _f, _i, _i, _p]),
+    "ssq_fq_fwd_multi": (_i, [_i, _p, _p, _p, _p, _p, _p, _p, _p, _p, _p]),
+    "ssq_fq_bwd_workspace_size": (_sz, [_i64, _i64, _i64]),
+    "ssq_fq_bwd": (_i, [_p, _p, _p, _p, _i64, _i64, _i64, _i, _i, _p, _p, _p, _p, _sz, _p]),
+    "ssq_scale_init_workspace_size": (_sz, [_i64, _i64, _i]),
+    "ssq_scale_init": (_i, [_p, _i64, _i64, _i, _i, _i, _i, _p, _p, _p, _p, _p, _sz, _p]),
+    "ssq_shift_init_workspace_size": (_sz, [_i64, _i64, _i64, _i, _i]),
+    "ssq_shift_init": (_i, [_p, _p, _p, _i, _i64, _i64, _i64, _i, _p, _p, _p, _p, _sz, _p]),
+    "ssq_rect_init": (_i, [_p, _p, _i, _i64, _i64, _i64, _p, _p]),
+    "ssq_get_delta": (_i, [_p, _p, _p, _i, _i64, _i64, _i, _p, _p]),
+    "ssq_adashift_fwd": (_i, [_p, _p, _p, _p, _p, _p, _i, _i64, _i64, _i64, _i, _i, _i, _i, _i,
+                              _p, _p, _p]),
+    "ssq_adashift_bwd_workspace_size": (_sz, [_i64, _i64, _i64, _i, _i]),
+    "ssq_adashift_bwd": (_i, [_p, _p, _p, _p, _p, _p, _p, _i, _i64, _i64, _i64, _i, _i, _i, _i,
+                              _f, _f, _p, _p, _p, _p, _sz, _p]),
+    "ssq_shift_reg": (_i, [_p, _i, _i64, _i, _f, _f, _p, _p, _p]),
+    "ssq_lhs_fwd": (_i, [_p, _p, _p, _p, _p, _i, _i64, _i64, _i64, _i, _i, _i, _i, _p, _p]),
+    "ssq_lhs_bwd": (_i, [_p, _p, _p, _p, _p, _p, _i, _i64, _i64, _i64, _i, _i, _i, _p, _p, _sz,
+                         _p]),
+    "ssq_adaround_fwd": (_i, [_p, _p, _p, _i, _p, _f, _i64, _i64, _i64, _i, _i, _i, _p, _p, _p]),
+    "ssq_adaround_bwd": (_i, [_p, _p, _p, _p, _i, _p, _f, _i64, _i64, _i64, _i, _i, _p, _p]),
+    "ssq_round_reg_workspace_size": (_sz, [_i64]),
+    "ssq_round_reg": (_i, [_p, _i64, _f, _f, _p, _p, _p, _sz, _p]),
+    "ssq_inpscale_search": (_i, [_p, _p, _p, _i64, _i64, _i, _i, _f, _p, _p]),
+    "ssq_inpscale_fwd": (_i, [_p, _p, _p, _p, _i64, _i64, _i, _p, _p]),
+    "ssq_lp_loss_workspace_size": (_sz, [_i64]),
+    "ssq_lp_loss": (_i, [_p, _p, _i64, _i64, _f, _p, _p, _p, _p, _sz, _p]),
+    "ssq_gather_rows2": (_i, [_p, _p, _i64, _p, _p, _i64, _p, _i64, _p]),
+    "ssq_stream_copy": (_i, [_p, _p, _i64, _p]),
+}
+
+_lib = None
+
+
+class SSQError(RuntimeError):
+    pass
+
+
+def load():
+    """Load libssq.so once; raise loudly if it is missing (no fallback path exists)."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(LIB_PATH):
+        raise SSQError(f"libssq.so not found at {LIB_PATH}; build it with "
+                       "`python -m shiftedscalequantization_amd.build` (hipcc, gfx950)")
+    lib = C.CDLL(LIB_PATH)
+    for name, (res, args) in SIGNATURES.items():
+        fn = getattr(lib, name)
+        fn.restype = res
+        fn.argtypes = args
+    _lib = lib
+    return lib
+
+
+def call(name, *args):
+    lib = load()
+    rc = getattr(lib, name)(*args)
+    if rc != 0:
+        msg = lib.ssq_last_error().decode(errors="replace")
+        raise SSQError(f"{name} failed (rc={rc}): {msg}")
+
+
+def query(name, *args):
+    return getattr(load(), name)(*args)
+
+
+# ------------------------------------------------------------------ tensor helpers
+def check(t, name="tensor"):
+    """Kernels run on the HIP device only (no CPU fallback)."""
+    if not isinstance(t, torch.Tensor):
+        raise TypeError(f"{name}: expected a torch.Tensor")
+    if t.device.type != "cuda":
+        raise SSQError(f"{name}: ssq kernels run on the MI355X (HIP) device only; got {t.device}")
+    if t.dtype != torch.float32:
+        raise SSQError(f"{name}: expected float32, got {t.dtype}")
+    return t
+
+
+def ptr(t):
+    return None if t is None else C.c_void_p(t.data_ptr())
+
+
+def fptr(t, name="tensor"):
+    """Device pointer of a contiguous fp32 tensor (made contiguous if needed)."""
+    if t is None:
+        return None, None
+    check(t, name)
+    t = t.contiguous()
+    return t, C.c_void_p(t.data_ptr())
+
+
+def stream_of(t):
+    return C.c_void_p(torch.cuda.current_stream(t.device).cuda_stream)
+
+
+_ws_cache = {}
+
+
+def workspace(nbytes, device):
+    """Per-(device, stream) scratch buffer for kernel partials (grown, never shrunk)."""
+    if nbytes == 0:
+        return None, 0
+    key = (device.index, torch.cuda.current_stream(device).cuda_stream)
+    buf = _ws_cache.get(key)
+    if buf is None or buf.numel() < nbytes:
+        buf = torch.empty(max(int(nbytes), 1 << 16), dtype=torch.uint8, device=device)
+        _ws_cache[key] = buf
+    return C.c_void_p(buf.data_ptr()), buf.numel()
+
+
+def shifts_arg(shifts):
+    arr = (C.c_float * len(shifts))(*[float(s) for s in shifts])
+    return arr

@@ -1,0 +1,723 @@
+// K5-K9, K12: ChannelQuant / AdaRound kernels.
+//
+// A weight is viewed as (Co, Ci, K), K = kh*kw (1 for Linear).  Shift-candidate floors
+// F_i = floor(W / (delta[co]*s_i)) are recomputed from W in every kernel instead of being
+// materialized as S W-sized tensors (the reference's self.x_q list, channelQuant.py:284-286),
+// so the adaShift forward reads W + beta (8 B/elem) and writes What (4 B/elem).
+//
+// alpha-gradient reductions over (Co, K) per input channel are two-stage and
+// deterministic: stage 1 sums a chunk of Co rows per column j = ci*K + k in registers
+// (double) and writes [chunk][j][S] partials; stage 2 (one thread per alpha row) sums the
+// partials in fixed order and applies the softmax/clamp chain + the shift regulariser.
+#include "ssq_common.h"
+
+namespace ssq {
+
+constexpr int kMaxS = 8;
+
+struct Shifts {
+  float s[kMaxS];
+  int n;
+};
+
+struct Geo {
+  uint32_t Co, Ci, K, CiK;
+  int is_fc;
+};
+
+__device__ __forceinline__ void decompose(uint32_t e, const Geo& g, uint32_t& co, uint32_t& ci) {
+  co = e / g.CiK;
+  ci = (e - co * g.CiK) / g.K;
+}
+
+__device__ __forceinline__ uint32_t alpha_row(const Geo& g, uint32_t co, uint32_t ci) {
+  return g.is_fc ? co * g.Ci + ci : ci;
+}
+
+__device__ __forceinline__ void load_row(const float* __restrict__ a, uint32_t row, int S,
+                                         float* out) {
+  for (int i = 0; i < S; ++i) out[i] = a[(size_t)row * S + i];
+}
+
+// soft shifted floor  sum_i F_i * p_i  (x_out = x_q0*p0; x_out += x_q1*p1; ...)
+__device__ __forceinline__ float soft_floor(float w, float d, const Shifts& sh, const float* p,
+                                            float* F) {
+  float acc = 0.0f;
+  for (int i = 0; i < sh.n; ++i) {
+    F[i] = floorf(w / __fmul_rn(d, sh.s[i]));
+    const float t = __fmul_rn(F[i], p[i]);
+    acc = i == 0 ? t : __fadd_rn(acc, t);
+  }
+  return acc;
+}
+
+// ------------------------------------------------------------------ adaShift forward
+__global__ __launch_bounds__(kBlock) void adashift_fwd_kernel(
+    const float* __restrict__ W, const float* __restrict__ alpha, const float* __restrict__ beta,
+    const float* __restrict__ delta, const float* __restrict__ zp, Shifts sh, Geo g, uint32_t n,
+    int hard_t, int hard_r, float lo, float hi, float* __restrict__ What,
+    uint8_t* __restrict__ codes) {
+  const uint32_t stride = gridDim.x * blockDim.x;
+  for (uint32_t e = blockIdx.x * blockDim.x + threadIdx.x; e < n; e += stride) {
+    uint32_t co, ci;
+    decompose(e, g, co, ci);
+    float a[kMaxS], p[kMaxS], F[kMaxS];
+    load_row(alpha, alpha_row(g, co, ci), sh.n, a);
+    soft_targets<kMaxS>(a, sh.n, nullptr, p);
+    const float d = delta[co], z = zp[co], w = W[e];
+    float xf;
+    if (hard_t) {
+      const int sel = argmax_first(p, sh.n);
+      xf = floorf(w / __fmul_rn(d, sh.s[sel]));
+    } else {
+      xf = soft_floor(w, d, sh, p, F);
+    }
+    const float b = beta[e];
+    const float hr = hard_r ? (b >= 0.0f ? 1.0f : 0.0f) : rect_sigmoid(b);
+    const float q = clampf(__fadd_rn(__fadd_rn(xf, hr), z), lo, hi);
+    What[e] = __fmul_rn(__fsub_rn(q, z), __fmul_rn(d, 1.0f));
+    if (codes) codes[e] = (uint8_t)((int)q & 0xff);
+  }
+}
+
+// ------------------------------------------------------------------ shared stage-2 helper
+// Backward through p = clamp(softmax(a)*c + gamma, 0, 1), plus the optional shift
+// regulariser lambda*sum(1-|2p-1|^b) (value returned, gradient folded into g_p).
+__device__ __forceinline__ float alpha_chain(const float* a, int S, double* g_p, float reg_lambda,
+                                             float reg_b, int reg_mode, float* ga_out) {
+  float s[kMaxS], p[kMaxS];
+  soft_targets<kMaxS>(a, S, s, p);
+  float reg = 0.0f;
+  if (reg_lambda != 0.0f) {
+    double acc = 0.0;
+    for (int i = 0; i < S; ++i) {
+      if (reg_mode == 0) {
+        const double r = fabs((double)p[i] - 0.5) * 2.0;
+        acc += 1.0 - pow(r, (double)reg_b);
+        if (reg_b != 0.0f) {
+          const double sg = p[i] > 0.5f ? 1.0 : (p[i] < 0.5f ? -1.0 : 0.0);
+          g_p[i] += -(double)reg_lambda * (double)reg_b * pow(r, (double)reg_b - 1.0) * 2.0 * sg;
+        }
+      } else {  // entropy: -lambda * sum p log(p + 1e-10)
+        const double pp = p[i];
+        acc += -(pp * log(pp + 1e-10));
+        g_p[i] += -(double)reg_lambda * (log(pp + 1e-10) + pp / (pp + 1e-10));
+      }
+    }
+    reg = (float)((double)reg_lambda * acc);
+  }
+  double gs[kMaxS], dot = 0.0;
+  for (int i = 0; i < S; ++i) {
+    const float u = __fadd_rn(__fmul_rn(s[i], kZmG), kGamma);
+    gs[i] = (u >= 0.0f && u <= 1.0f) ? g_p[i] * (double)kZmG : 0.0;
+    dot += gs[i] * (double)s[i];
+  }
+  for (int i = 0; i < S; ++i) ga_out[i] = (float)((double)s[i] * (gs[i] - dot));
+  return reg;
+}
+
+// ------------------------------------------------------------------ adaShift backward
+// MODE 0: adaShift (floors), MODE 1: learned_hard_sigmoid (dequantized 'none' candidates)
+template <int MODE>
+__device__ __forceinline__ float cand_value(float w, float d, float z, float s, float lo, float hi) {
+  if (MODE == 0) return floorf(w / __fmul_rn(d, s));
+  const float ds = __fmul_rn(d, s);
+  const float q = clampf(__fadd_rn(rintf(w / ds), z), lo, hi);
+  return __fmul_rn(__fsub_rn(q, z), ds);
+}
+
+// Stage 1 (conv): column j = ci*K + k, rows co in [co0, co0 + chunk).
+template <int MODE>
+__global__ __launch_bounds__(kBlock) void alpha_grad_stage1(
+    const float* __restrict__ gWhat, const float* __restrict__ W, const float* __restrict__ alpha,
+    const float* __restrict__ beta, const float* __restrict__ delta, const float* __restrict__ zp,
+    Shifts sh, Geo g, uint32_t chunk, int hard_r, float lo, float hi, double* __restrict__ part,
+    float* __restrict__ gbeta) {
+  const uint32_t j = blockIdx.x * blockDim.x + threadIdx.x;
+  if (j >= g.CiK) return;
+  const uint32_t ci = j / g.K;
+  const uint32_t co0 = blockIdx.y * chunk, co1 = min(co0 + chunk, g.Co);
+  float a[kMaxS], p[kMaxS], F[kMaxS];
+  load_row(alpha, ci, sh.n, a);
+  soft_targets<kMaxS>(a, sh.n, nullptr, p);
+  double acc[kMaxS];
+  for (int i = 0; i < sh.n; ++i) acc[i] = 0.0;
+  for (uint32_t co = co0; co < co1; ++co) {
+    const uint32_t e = co * g.CiK + j;
+    const float w = W[e], d = delta[co], z = zp[co], gy = gWhat[e];
+    float gi;
+    if (MODE == 0) {
+      const float xf = soft_floor(w, d, sh, p, F);
+      const float b = beta[e];
+      const float hr = hard_r ? (b >= 0.0f ? 1.0f : 0.0f) : rect_sigmoid(b);
+      const float u = __fadd_rn(__fadd_rn(xf, hr), z);
+      gi = (u >= lo && u <= hi) ? __fmul_rn(gy, __fmul_rn(d, 1.0f)) : 0.0f;
+      if (gbeta) gbeta[e] = hard_r ? 0.0f : rect_sigmoid_grad(b, gi);
+    } else {
+      for (int i = 0; i < sh.n; ++i) F[i] = cand_value<1>(w, d, z, sh.s[i], lo, hi);
+      gi = gy;
+    }
+    for (int i = 0; i < sh.n; ++i) acc[i] += (double)gi * (double)F[i];
+  }
+  double* o = part + ((size_t)blockIdx.y * g.CiK + j) * sh.n;
+  for (int i = 0; i < sh.n; ++i) o[i] = acc[i];
+}
+
+// Stage 2 (conv): one thread per input channel.
+__global__ __launch_bounds__(kBlock) void alpha_grad_stage2(
+    const double* __restrict__ part, const float* __restrict__ alpha, int S, Geo g,
+    uint32_t nchunk, float reg_lambda, float reg_b, float* __restrict__ galpha,
+    float* __restrict__ reg_vals) {
+  const uint32_t ci = blockIdx.x * blockDim.x + threadIdx.x;
+  if (ci >= g.Ci) return;
+  double gp[kMaxS];
+  for (int i = 0; i < S; ++i) gp[i] = 0.0;
+  for (uint32_t c = 0; c < nchunk; ++c)
+    for (uint32_t k = 0; k < g.K; ++k) {
+      const double* q = part + ((size_t)c * g.CiK + (size_t)ci * g.K + k) * S;
+      for (int i = 0; i < S; ++i) gp[i] += q[i];
+    }
+  float a[kMaxS], ga[kMaxS];
+  load_row(alpha, ci, S, a);
+  const float reg = alpha_chain(a, S, gp, reg_lambda, reg_b, 0, ga);
+  for (int i = 0; i < S; ++i) galpha[(size_t)ci * S + i] = ga[i];
+  if (reg_vals) reg_vals[ci] = reg;
+}
+
+// Linear: alpha is per element, no reduction.
+template <int MODE>
+__global__ __launch_bounds__(kBlock) void alpha_grad_fc(
+    const float* __restrict__ gWhat, const float* __restrict__ W, const float* __restrict__ alpha,
+    const float* __restrict__ beta, const float* __restrict__ delta, const float* __restrict__ zp,
+    Shifts sh, Geo g, uint32_t n, int hard_r, float lo, float hi, float reg_lambda, float reg_b,
+    float* __restrict__ galpha, float* __restrict__ gbeta, float* __restrict__ reg_vals) {
+  const uint32_t stride = gridDim.x * blockDim.x;
+  for (uint32_t e = blockIdx.x * blockDim.x + threadIdx.x; e < n; e += stride) {
+    const uint32_t co = e / g.CiK;
+    float a[kMaxS], p[kMaxS], F[kMaxS], ga[kMaxS];
+    load_row(alpha, e, sh.n, a);
+    soft_targets<kMaxS>(a, sh.n, nullptr, p);
+    const float w = W[e], d = delta[co], z = zp[co], gy = gWhat[e];
+    float gi;
+    if (MODE == 0) {
+      const float xf = soft_floor(w, d, sh, p, F);
+      const float b = beta[e];
+      const float hr = hard_r ? (b >= 0.0f ? 1.0f : 0.0f) : rect_sigmoid(b);
+      const float u = __fadd_rn(__fadd_rn(xf, hr), z);
+      gi = (u >= lo && u <= hi) ? __fmul_rn(gy, __fmul_rn(d, 1.0f)) : 0.0f;
+      if (gbeta) gbeta[e] = hard_r ? 0.0f : rect_sigmoid_grad(b, gi);
+    } else {
+      for (int i = 0; i < sh.n; ++i) F[i] = cand_value<1>(w, d, z, sh.s[i], lo, hi);
+      gi = gy;
+    }
+    double gp[kMaxS];
+    for (int i = 0; i < sh.n; ++i) gp[i] = (double)gi * (double)F[i];
+    const float reg = alpha_chain(a, sh.n, gp, reg_lambda, reg_b, 0, ga);
+    for (int i = 0; i < sh.n; ++i) galpha[(size_t)e * sh.n + i] = ga[i];
+    if (reg_vals) reg_vals[e] = reg;
+  }
+}
+
+// ------------------------------------------------------------------ shift regulariser alone
+__global__ __launch_bounds__(kBlock) void shift_reg_kernel(const float* __restrict__ alpha, int S,
+                                                           uint32_t rows, int mode, float lambda,
+                                                           float b, float* __restrict__ galpha,
+                                                           float* __restrict__ reg_vals) {
+  const uint32_t r = blockIdx.x * blockDim.x + threadIdx.x;
+  if (r >= rows) return;
+  float a[kMaxS], ga[kMaxS];
+  double gp[kMaxS];
+  load_row(alpha, r, S, a);
+  for (int i = 0; i < S; ++i) gp[i] = 0.0;
+  const float reg = alpha_chain(a, S, gp, lambda, b, mode, ga);
+  if (galpha)
+    for (int i = 0; i < S; ++i) galpha[(size_t)r * S + i] += ga[i];
+  if (reg_vals) reg_vals[r] = reg;
+}
+
+// ------------------------------------------------------------------ learned_hard_sigmoid fwd
+__global__ __launch_bounds__(kBlock) void lhs_fwd_kernel(
+    const float* __restrict__ W, const float* __restrict__ alpha, const float* __restrict__ delta,
+    const float* __restrict__ zp, Shifts sh, Geo g, uint32_t n, int hard_t, float lo, float hi,
+    float* __restrict__ What) {
+  const uint32_t stride = gridDim.x * blockDim.x;
+  for (uint32_t e = blockIdx.x * blockDim.x + threadIdx.x; e < n; e += stride) {
+    uint32_t co, ci;
+    decompose(e, g, co, ci);
+    float a[kMaxS], p[kMaxS];
+    load_row(alpha, alpha_row(g, co, ci), sh.n, a);
+    soft_targets<kMaxS>(a, sh.n, nullptr, p);
+    const float w = W[e], d = delta[co], z = zp[co];
+    float out;
+    if (hard_t) {
+      out = cand_value<1>(w, d, z, sh.s[argmax_first(p, sh.n)], lo, hi);
+    } else {
+      out = 0.0f;
+      for (int i = 0; i < sh.n; ++i) {
+        const float t = __fmul_rn(cand_value<1>(w, d, z, sh.s[i], lo, hi), p[i]);
+        out = i == 0 ? t : __fadd_rn(out, t);
+      }
+    }
+    What[e] = out;
+  }
+}
+
+// ------------------------------------------------------------------ adaround fwd / bwd
+__device__ __forceinline__ float delta_at(const float* delta, int per_ci, const Geo& g,
+                                          uint32_t co, uint32_t ci) {
+  return per_ci ? delta[(size_t)co * g.Ci + ci] : delta[co];
+}
+
+__global__ __launch_bounds__(kBlock) void adaround_fwd_kernel(
+    const float* __restrict__ W, const float* __restrict__ beta, const float* __restrict__ delta,
+    int per_ci, const float* __restrict__ zp, float scale, Geo g, uint32_t n, int hard_r, float lo,
+    float hi, float* __restrict__ What, uint8_t* __restrict__ codes) {
+  const uint32_t stride = gridDim.x * blockDim.x;
+  for (uint32_t e = blockIdx.x * blockDim.x + threadIdx.x; e < n; e += stride) {
+    uint32_t co, ci;
+    decompose(e, g, co, ci);
+    const float d = __fmul_rn(delta_at(delta, per_ci, g, co, ci), scale), z = zp[co];
+    const float b = beta[e];
+    const float hr = hard_r ? (b >= 0.0f ? 1.0f : 0.0f) : rect_sigmoid(b);
+    const float q = clampf(__fadd_rn(__fadd_rn(floorf(W[e] / d), hr), z), lo, hi);
+    What[e] = __fmul_rn(__fsub_rn(q, z), d);
+    if (codes) codes[e] = (uint8_t)((int)q & 0xff);
+  }
+}
+
+__global__ __launch_bounds__(kBlock) void adaround_bwd_kernel(
+    const float* __restrict__ gWhat, const float* __restrict__ W, const float* __restrict__ beta,
+    const float* __restrict__ delta, int per_ci, const float* __restrict__ zp, float scale, Geo g,
+    uint32_t n, float lo, float hi, float* __restrict__ gbeta) {
+  const uint32_t stride = gridDim.x * blockDim.x;
+  for (uint32_t e = blockIdx.x * blockDim.x + threadIdx.x; e < n; e += stride) {
+    uint32_t co, ci;
+    decompose(e, g, co, ci);
+    const float d = __fmul_rn(delta_at(delta, per_ci, g, co, ci), scale), z = zp[co];
+    const float b = beta[e];
+    const float u = __fadd_rn(__fadd_rn(floorf(W[e] / d), rect_sigmoid(b)), z);
+    const float gi = (u >= lo && u <= hi) ? __fmul_rn(gWhat[e], d) : 0.0f;
+    gbeta[e] = rect_sigmoid_grad(b, gi);
+  }
+}
+
+// ------------------------------------------------------------------ inits
+// -log((zeta-gamma)/(rest-gamma) - 1); python_float/tensor == reciprocal(tensor)*float
+__device__ __forceinline__ float rect_inverse(float w, float d) {
+  const float t = w / d;
+  const float rest = __fsub_rn(t, floorf(t));
+  const float r = __fmul_rn(1.0f / __fsub_rn(rest, kGamma), kZmG);
+  return -logf(__fsub_rn(r, 1.0f));
+}
+
+__global__ __launch_bounds__(kBlock) void rect_init_kernel(const float* __restrict__ W,
+                                                           const float* __restrict__ delta,
+                                                           int per_ci, Geo g, uint32_t n,
+                                                           float* __restrict__ beta) {
+  const uint32_t stride = gridDim.x * blockDim.x;
+  for (uint32_t e = blockIdx.x * blockDim.x + threadIdx.x; e < n; e += stride) {
+    uint32_t co, ci;
+    decompose(e, g, co, ci);
+    beta[e] = rect_inverse(W[e], delta_at(delta, per_ci, g, co, ci));
+  }
+}
+
+__device__ __forceinline__ float delta_sel(const float* __restrict__ alpha, const float* delta,
+                                           const Shifts& sh, const Geo& g, uint32_t co,
+                                           uint32_t ci) {
+  float a[kMaxS], p[kMaxS];
+  load_row(alpha, alpha_row(g, co, ci), sh.n, a);
+  soft_targets<kMaxS>(a, sh.n, nullptr, p);
+  return __fmul_rn(delta[co], sh.s[argmax_first(p, sh.n)]);
+}
+
+__global__ __launch_bounds__(kBlock) void get_delta_kernel(const float* __restrict__ delta,
+                                                           const float* __restrict__ alpha,
+                                                           Shifts sh, Geo g,
+                                                           float* __restrict__ out) {
+  const uint32_t e = blockIdx.x * blockDim.x + threadIdx.x;
+  if (e >= g.Co * g.Ci) return;
+  const uint32_t co = e / g.Ci, ci = e - co * g.Ci;
+  out[e] = delta_sel(alpha, delta, sh, g, co, ci);
+}
+
+__global__ __launch_bounds__(kBlock) void beta_from_alpha_kernel(const float* __restrict__ W,
+                                                                 const float* __restrict__ delta,
+                                                                 const float* __restrict__ alpha,
+                                                                 Shifts sh, Geo g, uint32_t n,
+                                                                 float* __restrict__ beta) {
+  const uint32_t stride = gridDim.x * blockDim.x;
+  for (uint32_t e = blockIdx.x * blockDim.x + threadIdx.x; e < n; e += stride) {
+    uint32_t co, ci;
+    decompose(e, g, co, ci);
+    beta[e] = rect_inverse(W[e], delta_sel(alpha, delta, sh, g, co, ci));
+  }
+}
+
+// init_alpha (channelQuant.py:158-199) from per-row squared errors.
+__device__ __forceinline__ void init_alpha_row(const double* mse, int S, float* a_out) {
+  int mi = 0;
+  for (int i = 1; i < S; ++i)
+    if (mse[i] < mse[mi]) mi = i;  // torch.min(dim) -> first index of the minimum
+  const float clip = S == 1 ? 1.0f : 0.33f;
+  const float remain = S == 1 ? 0.0f : (float)((1.0 - 0.33) / (double)(S - 1));
+  float lg[kMaxS];
+  float sum = 0.0f;
+  for (int i = 0; i < S; ++i) {
+    const float pr = i == mi ? clip : remain;
+    const float x = __fsub_rn(pr, kGamma) / kZmG;   // (x - gamma) / (zeta - gamma)
+    lg[i] = logf(x);
+    sum = i == 0 ? lg[i] : __fadd_rn(sum, lg[i]);
+  }
+  const float avg = __fmul_rn(sum, 1.0f / (float)S);  // torch mean: sum * (1/N)
+  for (int i = 0; i < S; ++i) a_out[i] = __fsub_rn(lg[i], avg);
+}
+
+// stage 1 of shift init (conv): column partials of sum (w - F_i)^2 over a chunk of Co.
+__global__ __launch_bounds__(kBlock) void shift_mse_stage1(const float* __restrict__ W,
+                                                           const float* __restrict__ delta,
+                                                           Shifts sh, Geo g, uint32_t chunk,
+                                                           double* __restrict__ part) {
+  const uint32_t j = blockIdx.x * blockDim.x + threadIdx.x;
+  if (j >= g.CiK) return;
+  const uint32_t co0 = blockIdx.y * chunk, co1 = min(co0 + chunk, g.Co);
+  double acc[kMaxS];
+  for (int i = 0; i < sh.n; ++i) acc[i] = 0.0;
+  for (uint32_t co = co0; co < co1; ++co) {
+    const float w = W[co * g.CiK + j], d = delta[co];
+    for (int i = 0; i < sh.n; ++i) {
+      const float r = __fsub_rn(w, floorf(w / __fmul_rn(d, sh.s[i])));
+      acc[i] += (double)__fmul_rn(r, r);
+    }
+  }
+  double* o = part + ((size_t)blockIdx.y * g.CiK + j) * sh.n;
+  for (int i = 0; i < sh.n; ++i) o[i] = acc[i];
+}
+
+__global__ __launch_bounds__(kBlock) void shift_mse_stage2(const double* __restrict__ part, int S,
+                                                           Geo g, uint32_t nchunk,
+                                                           float* __restrict__ alpha,
+                                                           float* __restrict__ mse_out) {
+  const uint32_t ci = blockIdx.x * blockDim.x + threadIdx.x;
+  if (ci >= g.Ci) return;
+  double m[kMaxS];
+  for (int i = 0; i < S; ++i) m[i] = 0.0;
+  for (uint32_t c = 0; c < nchunk; ++c)
+    for (uint32_t k = 0; k < g.K; ++k) {
+      const double* q = part + ((size_t)c * g.CiK + (size_t)ci * g.K + k) * S;
+      for (int i = 0; i < S; ++i) m[i] += q[i];
+    }
+  float a[kMaxS];
+  init_alpha_row(m, S, a);
+  for (int i = 0; i < S; ++i) {
+    alpha[(size_t)ci * S + i] = a[i];
+    if (mse_out) mse_out[(size_t)ci * S + i] = (float)m[i];
+  }
+}
+
+__global__ __launch_bounds__(kBlock) void shift_init_fc(const float* __restrict__ W,
+                                                        const float* __restrict__ delta, Shifts sh,
+                                                        Geo g, uint32_t n, float* __restrict__ alpha,
+                                                        float* __restrict__ mse_out) {
+  const uint32_t stride = gridDim.x * blockDim.x;
+  for (uint32_t e = blockIdx.x * blockDim.x + threadIdx.x; e < n; e += stride) {
+    const uint32_t co = e / g.CiK;
+    const float w = W[e], d = delta[co];
+    double m[kMaxS];
+    for (int i = 0; i < sh.n; ++i) {
+      const float r = __fsub_rn(w, floorf(w / __fmul_rn(d, sh.s[i])));
+      m[i] = (double)__fmul_rn(r, r);
+    }
+    float a[kMaxS];
+    init_alpha_row(m, sh.n, a);
+    for (int i = 0; i < sh.n; ++i) {
+      alpha[(size_t)e * sh.n + i] = a[i];
+      if (mse_out) mse_out[(size_t)e * sh.n + i] = (float)m[i];
+    }
+  }
+}
+
+// ------------------------------------------------------------------ rounding regulariser
+__global__ __launch_bounds__(kBlock) void round_reg_kernel(const float* __restrict__ v, int64_t n,
+                                                           float lambda, float b,
+                                                           float* __restrict__ gv,
+                                                           double* __restrict__ part) {
+  __shared__ double red[16];
+  double acc = 0.0;
+  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+  for (int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; e < n; e += stride) {
+    const float h = rect_sigmoid(v[e]);
+    const float r = __fmul_rn(fabsf(__fsub_rn(h, 0.5f)), 2.0f);
+    acc += 1.0 - (double)powf(r, b);
+    if (gv && b != 0.0f) {
+      const float sg = h > 0.5f ? 1.0f : (h < 0.5f ? -1.0f : 0.0f);
+      const float gh = -lambda * b * powf(r, b - 1.0f) * 2.0f * sg;
+      gv[e] += rect_sigmoid_grad(v[e], gh);
+    }
+  }
+  acc = block_sum(acc, red);
+  if (threadIdx.x == 0) part[blockIdx.x] = acc;
+}
+
+__global__ void reduce_partials(const double* __restrict__ part, int nblk, double scale,
+                                float* __restrict__ out) {
+  __shared__ double red[16];
+  double a = 0.0;
+  for (int i = threadIdx.x; i < nblk; i += blockDim.x) a += part[i];
+  a = block_sum(a, red);
+  if (threadIdx.x == 0) out[0] = (float)(a * scale);
+}
+
+// ------------------------------------------------------------------ host helpers
+static int make_geo(int64_t Co, int64_t Ci, int64_t K, int is_fc, Geo& g) {
+  SSQ_REQUIRE(Co >= 1 && Ci >= 1 && K >= 1, SSQ_E_ARG, "bad geometry (%lld,%lld,%lld)",
+              (long long)Co, (long long)Ci, (long long)K);
+  SSQ_REQUIRE(Co * Ci * K < (1ll << 31), SSQ_E_ARG, "weight too large for 32-bit indexing");
+  SSQ_REQUIRE(!is_fc || K == 1, SSQ_E_ARG, "Linear weights must have K == 1");
+  g.Co = (uint32_t)Co;
+  g.Ci = (uint32_t)Ci;
+  g.K = (uint32_t)K;
+  g.CiK = (uint32_t)(Ci * K);
+  g.is_fc = is_fc;
+  return SSQ_OK;
+}
+
+static int make_shifts(const float* shifts, int S, Shifts& sh) {
+  SSQ_REQUIRE(S >= 1 && S <= kMaxS && shifts, SSQ_E_ARG, "1 <= S <= %d shifts required", kMaxS);
+  sh.n = S;
+  for (int i = 0; i < kMaxS; ++i) sh.s[i] = i < S ? shifts[i] : 1.0f;
+  return SSQ_OK;
+}
+
+// Co-chunking for the two-stage column reductions: aim for ~512 workgroups.
+static void chunking(const Geo& g, uint32_t& chunk, uint32_t& nchunk) {
+  const uint32_t colblk = (g.CiK + kBlock - 1) / kBlock;
+  uint32_t want = 512 / colblk;
+  if (want < 1) want = 1;
+  if (want > g.Co) want = g.Co;
+  chunk = (g.Co + want - 1) / want;
+  nchunk = (g.Co + chunk - 1) / chunk;
+}
+
+static size_t colred_ws(int64_t Co, int64_t Ci, int64_t K, int S) {
+  Geo g;
+  if (make_geo(Co, Ci, K, 0, g) != SSQ_OK) return 0;
+  uint32_t chunk, nchunk;
+  chunking(g, chunk, nchunk);
+  return (size_t)nchunk * g.CiK * S * sizeof(double);
+}
+
+}  // namespace ssq
+
+using namespace ssq;
+
+#define SSQ_GEO(Co, Ci, K, fc, g)                      \
+  Geo g;                                               \
+  {                                                    \
+    int _r = make_geo(Co, Ci, K, fc, g);               \
+    if (_r) return _r;                                 \
+  }
+#define SSQ_SHIFTS(p, S, sh)                           \
+  Shifts sh;                                           \
+  {                                                    \
+    int _r = make_shifts(p, S, sh);                    \
+    if (_r) return _r;                                 \
+  }
+
+extern "C" int ssq_adashift_fwd(const float* W, const float* alpha, const float* beta,
+                                const float* delta, const float* zp, const float* shifts, int S,
+                                int64_t Co, int64_t Ci, int64_t K, int is_fc, int hard_targets,
+                                int hard_round, int qmin, int qmax, float* What, void* codes,
+                                ssq_stream_t stream) {
+  SSQ_GEO(Co, Ci, K, is_fc, g);
+  SSQ_SHIFTS(shifts, S, sh);
+  SSQ_REQUIRE(W && alpha && beta && delta && zp && What, SSQ_E_ARG, "ssq_adashift_fwd: null");
+  const uint32_t n = g.Co * g.CiK;
+  hipLaunchKernelGGL(adashift_fwd_kernel, dim3(grid_for(n, kBlock)), dim3(kBlock), 0,
+                     (hipStream_t)stream, W, alpha, beta, delta, zp, sh, g, n, hard_targets,
+                     hard_round, (float)qmin, (float)qmax, What, (uint8_t*)codes);
+  return check_launch("ssq_adashift_fwd");
+}
+
+extern "C" size_t ssq_adashift_bwd_workspace_size(int64_t Co, int64_t Ci, int64_t K, int S,
+                                                  int is_fc) {
+  return is_fc ? 0 : colred_ws(Co, Ci, K, S);
+}
+
+extern "C" int ssq_adashift_bwd(const float* gWhat, const float* W, const float* alpha,
+                                const float* beta, const float* delta, const float* zp,
+                                const float* shifts, int S, int64_t Co, int64_t Ci, int64_t K,
+                                int is_fc, int hard_round, int qmin, int qmax, float reg_lambda,
+                                float reg_b, float* galpha, float* gbeta, float* reg_vals,
+                                void* ws, size_t ws_bytes, ssq_stream_t stream) {
+  SSQ_GEO(Co, Ci, K, is_fc, g);
+  SSQ_SHIFTS(shifts, S, sh);
+  SSQ_REQUIRE(gWhat && W && alpha && beta && delta && zp && galpha, SSQ_E_ARG,
+              "ssq_adashift_bwd: null");
+  hipStream_t s = (hipStream_t)stream;
+  const uint32_t n = g.Co * g.CiK;
+  if (is_fc) {
+    hipLaunchKernelGGL(alpha_grad_fc<0>, dim3(grid_for(n, kBlock)), dim3(kBlock), 0, s, gWhat, W,
+                       alpha, beta, delta, zp, sh, g, n, hard_round, (float)qmin, (float)qmax,
+                       reg_lambda, reg_b, galpha, gbeta, reg_vals);
+    return check_launch("ssq_adashift_bwd(fc)");
+  }
+  SSQ_REQUIRE(ws && ws_bytes >= colred_ws(Co, Ci, K, S), SSQ_E_WS,
+              "ssq_adashift_bwd: workspace too small");
+  uint32_t chunk, nchunk;
+  chunking(g, chunk, nchunk);
+  hipLaunchKernelGGL(alpha_grad_stage1<0>, dim3((g.CiK + kBlock - 1) / kBlock, nchunk),
+                     dim3(kBlock), 0, s, gWhat, W, alpha, beta, delta, zp, sh, g, chunk,
+                     hard_round, (float)qmin, (float)qmax, (double*)ws, gbeta);
+  hipLaunchKernelGGL(alpha_grad_stage2, dim3((g.Ci + kBlock - 1) / kBlock), dim3(kBlock), 0, s,
+                     (const double*)ws, alpha, S, g, nchunk, reg_lambda, reg_b, galpha, reg_vals);
+  return check_launch("ssq_adashift_bwd");
+}
+
+extern "C" int ssq_shift_reg(const float* alpha, int S, int64_t rows, int mode, float lambda,
+                             float b, float* galpha, float* reg_vals, ssq_stream_t stream) {
+  SSQ_REQUIRE(alpha && rows >= 1 && S >= 1 && S <= kMaxS && (mode == 0 || mode == 1), SSQ_E_ARG,
+              "ssq_shift_reg: bad args");
+  hipLaunchKernelGGL(shift_reg_kernel, dim3((unsigned)((rows + kBlock - 1) / kBlock)),
+                     dim3(kBlock), 0, (hipStream_t)stream, alpha, S, (uint32_t)rows, mode, lambda,
+                     b, galpha, reg_vals);
+  return check_launch("ssq_shift_reg");
+}
+
+extern "C" int ssq_lhs_fwd(const float* W, const float* alpha, const float* delta,
+                           const float* zp, const float* shifts, int S, int64_t Co, int64_t Ci,
+                           int64_t K, int is_fc, int hard_targets, int qmin, int qmax,
+                           float* What, ssq_stream_t stream) {
+  SSQ_GEO(Co, Ci, K, is_fc, g);
+  SSQ_SHIFTS(shifts, S, sh);
+  SSQ_REQUIRE(W && alpha && delta && zp && What, SSQ_E_ARG, "ssq_lhs_fwd: null");
+  const uint32_t n = g.Co * g.CiK;
+  hipLaunchKernelGGL(lhs_fwd_kernel, dim3(grid_for(n, kBlock)), dim3(kBlock), 0,
+                     (hipStream_t)stream, W, alpha, delta, zp, sh, g, n, hard_targets,
+                     (float)qmin, (float)qmax, What);
+  return check_launch("ssq_lhs_fwd");
+}
+
+extern "C" int ssq_lhs_bwd(const float* gWhat, const float* W, const float* alpha,
+                           const float* delta, const float* zp, const float* shifts, int S,
+                           int64_t Co, int64_t Ci, int64_t K, int is_fc, int qmin, int qmax,
+                           float* galpha, void* ws, size_t ws_bytes, ssq_stream_t stream) {
+  SSQ_GEO(Co, Ci, K, is_fc, g);
+  SSQ_SHIFTS(shifts, S, sh);
+  SSQ_REQUIRE(gWhat && W && alpha && delta && zp && galpha, SSQ_E_ARG, "ssq_lhs_bwd: null");
+  hipStream_t s = (hipStream_t)stream;
+  const uint32_t n = g.Co * g.CiK;
+  if (is_fc) {
+    hipLaunchKernelGGL(alpha_grad_fc<1>, dim3(grid_for(n, kBlock)), dim3(kBlock), 0, s, gWhat, W,
+                       alpha, nullptr, delta, zp, sh, g, n, 0, (float)qmin, (float)qmax, 0.0f,
+                       0.0f, galpha, nullptr, nullptr);
+    return check_launch("ssq_lhs_bwd(fc)");
+  }
+  SSQ_REQUIRE(ws && ws_bytes >= colred_ws(Co, Ci, K, S), SSQ_E_WS,
+              "ssq_lhs_bwd: workspace too small");
+  uint32_t chunk, nchunk;
+  chunking(g, chunk, nchunk);
+  hipLaunchKernelGGL(alpha_grad_stage1<1>, dim3((g.CiK + kBlock - 1) / kBlock, nchunk),
+                     dim3(kBlock), 0, s, gWhat, W, alpha, nullptr, delta, zp, sh, g, chunk, 0,
+                     (float)qmin, (float)qmax, (double*)ws, nullptr);
+  hipLaunchKernelGGL(alpha_grad_stage2, dim3((g.Ci + kBlock - 1) / kBlock), dim3(kBlock), 0, s,
+                     (const double*)ws, alpha, S, g, nchunk, 0.0f, 0.0f, galpha, nullptr);
+  return check_launch("ssq_lhs_bwd");
+}
+
+extern "C" int ssq_adaround_fwd(const float* W, const float* beta, const float* delta,
+                                int delta_per_ci, const float* zp, float scale, int64_t Co,
+                                int64_t Ci, int64_t K, int hard_round, int qmin, int qmax,
+                                float* What, void* codes, ssq_stream_t stream) {
+  SSQ_GEO(Co, Ci, K, 0, g);
+  SSQ_REQUIRE(W && beta && delta && zp && What, SSQ_E_ARG, "ssq_adaround_fwd: null");
+  const uint32_t n = g.Co * g.CiK;
+  hipLaunchKernelGGL(adaround_fwd_kernel, dim3(grid_for(n, kBlock)), dim3(kBlock), 0,
+                     (hipStream_t)stream, W, beta, delta, delta_per_ci, zp, scale, g, n,
+                     hard_round, (float)qmin, (float)qmax, What, (uint8_t*)codes);
+  return check_launch("ssq_adaround_fwd");
+}
+
+extern "C" int ssq_adaround_bwd(const float* gWhat, const float* W, const float* beta,
+                                const float* delta, int delta_per_ci, const float* zp, float scale,
+                                int64_t Co, int64_t Ci, int64_t K, int qmin, int qmax,
+                                float* gbeta, ssq_stream_t stream) {
+  SSQ_GEO(Co, Ci, K, 0, g);
+  SSQ_REQUIRE(gWhat && W && beta && delta && zp && gbeta, SSQ_E_ARG, "ssq_adaround_bwd: null");
+  const uint32_t n = g.Co * g.CiK;
+  hipLaunchKernelGGL(adaround_bwd_kernel, dim3(grid_for(n, kBlock)), dim3(kBlock), 0,
+                     (hipStream_t)stream, gWhat, W, beta, delta, delta_per_ci, zp, scale, g, n,
+                     (float)qmin, (float)qmax, gbeta);
+  return check_launch("ssq_adaround_bwd");
+}
+
+extern "C" int ssq_rect_init(const float* W, const float* delta, int delta_per_ci, int64_t Co,
+                             int64_t Ci, int64_t K, float* beta, ssq_stream_t stream) {
+  SSQ_GEO(Co, Ci, K, 0, g);
+  SSQ_REQUIRE(W && delta && beta, SSQ_E_ARG, "ssq_rect_init: null");
+  const uint32_t n = g.Co * g.CiK;
+  hipLaunchKernelGGL(rect_init_kernel, dim3(grid_for(n, kBlock)), dim3(kBlock), 0,
+                     (hipStream_t)stream, W, delta, delta_per_ci, g, n, beta);
+  return check_launch("ssq_rect_init");
+}
+
+extern "C" int ssq_get_delta(const float* delta, const float* alpha, const float* shifts, int S,
+                             int64_t Co, int64_t Ci, int is_fc, float* out, ssq_stream_t stream) {
+  SSQ_GEO(Co, Ci, 1, is_fc, g);
+  SSQ_SHIFTS(shifts, S, sh);
+  SSQ_REQUIRE(delta && alpha && out, SSQ_E_ARG, "ssq_get_delta: null");
+  hipLaunchKernelGGL(get_delta_kernel, dim3((g.Co * g.Ci + kBlock - 1) / kBlock), dim3(kBlock), 0,
+                     (hipStream_t)stream, delta, alpha, sh, g, out);
+  return check_launch("ssq_get_delta");
+}
+
+extern "C" size_t ssq_shift_init_workspace_size(int64_t Co, int64_t Ci, int64_t K, int S,
+                                                int is_fc) {
+  return is_fc ? 0 : colred_ws(Co, Ci, K, S);
+}
+
+extern "C" int ssq_shift_init(const float* W, const float* delta, const float* shifts, int S,
+                              int64_t Co, int64_t Ci, int64_t K, int is_fc, float* alpha,
+                              float* beta, float* mse_out, void* ws, size_t ws_bytes,
+                              ssq_stream_t stream) {
+  SSQ_GEO(Co, Ci, K, is_fc, g);
+  SSQ_SHIFTS(shifts, S, sh);
+  SSQ_REQUIRE(W && delta && alpha && beta, SSQ_E_ARG, "ssq_shift_init: null");
+  hipStream_t s = (hipStream_t)stream;
+  const uint32_t n = g.Co * g.CiK;
+  if (is_fc) {
+    hipLaunchKernelGGL(shift_init_fc, dim3(grid_for(n, kBlock)), dim3(kBlock), 0, s, W, delta, sh,
+                       g, n, alpha, mse_out);
+  } else {
+    SSQ_REQUIRE(ws && ws_bytes >= colred_ws(Co, Ci, K, S), SSQ_E_WS,
+                "ssq_shift_init: workspace too small");
+    uint32_t chunk, nchunk;
+    chunking(g, chunk, nchunk);
+    hipLaunchKernelGGL(shift_mse_stage1, dim3((g.CiK + kBlock - 1) / kBlock, nchunk), dim3(kBlock),
+                       0, s, W, delta, sh, g, chunk, (double*)ws);
+    hipLaunchKernelGGL(shift_mse_stage2, dim3((g.Ci + kBlock - 1) / kBlock), dim3(kBlock), 0, s,
+                       (const double*)ws, S, g, nchunk, alpha, mse_out);
+  }
+  hipLaunchKernelGGL(beta_from_alpha_kernel, dim3(grid_for(n, kBlock)), dim3(kBlock), 0, s, W,
+                     delta, alpha, sh, g, n, beta);
+  return check_launch("ssq_shift_init");
+}
+
+extern "C" size_t ssq_round_reg_workspace_size(int64_t n) {
+  (void)n;
+  return 1024 * sizeof(double);
+}
+
+extern "C" int ssq_round_reg(const float* v, int64_t n, float lambda, float b, float* loss_out,
+                             float* gv, void* ws, size_t ws_bytes, ssq_stream_t stream) {
+  SSQ_REQUIRE(v && n >= 1 && loss_out, SSQ_E_ARG, "ssq_round_reg: bad args");
+  SSQ_REQUIRE(ws && ws_bytes >= ssq_round_reg_workspace_size(n), SSQ_E_WS,
+              "ssq_round_reg: workspace too small");
+  hipStream_t s = (hipStream_t)stream;
+  const int grid = grid_for(n, kBlock, 1024);
+  hipLaunchKernelGGL(round_reg_kernel, dim3(grid), dim3(kBlock), 0, s, v, n, lambda, b, gv,
+                     (double*)ws);
+  hipLaunchKernelGGL(reduce_partials, dim3(1), dim3(kBlock), 0, s, (const double*)ws, grid,
+                     (double)lambda, loss_out);
+  return check_launch("ssq_round_reg");
+}

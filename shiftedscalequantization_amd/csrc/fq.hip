@@ -1,0 +1,455 @@
+// K1/K2: uniform affine fake-quant forward / STE backward, multi-tensor forward,
+// error plumbing and the bandwidth probe.
+//
+// Replaces the eager sequence of UniformAffineQuantizer.forward
+// (quant_layer.py:92-98): round_ste(x/delta) + zp -> clamp -> (q - zp)*delta
+// (5-6 launches, 4 temporaries) with one HBM pass: 8 B/elem (fp32 in, fp32 out),
+// +1 B/elem when int codes are emitted.
+#include <stdarg.h>
+#include <stdio.h>
+
+#include "ssq_common.h"
+
+namespace ssq {
+
+static thread_local char g_err[512] = "";
+
+void set_error(const char* fmt, ...) {
+  va_list ap;
+  va_start(ap, fmt);
+  vsnprintf(g_err, sizeof(g_err), fmt, ap);
+  va_end(ap);
+}
+
+int check_launch(const char* what) {
+  hipError_t e = hipGetLastError();
+  if (e != hipSuccess) {
+    set_error("%s: launch failed: %s", what, hipGetErrorString(e));
+    return (int)e;
+  }
+  return SSQ_OK;
+}
+
+// ------------------------------------------------------------------ element op
+struct QParams {
+  float d, z, lo, hi;
+};
+
+__device__ __forceinline__ float fq1(float x, const QParams& p, float* qout) {
+  float t = x / p.d;                       // IEEE fp32 divide (x / delta)
+  float v = __fadd_rn(rintf(t), p.z);      // round_ste fwd == round half-even, + zp
+  float q = clampf(v, p.lo, p.hi);         // clamp(x_int, lo, hi)
+  *qout = q;
+  return __fmul_rn(__fsub_rn(q, p.z), p.d);  // (x_quant - zp) * delta
+}
+
+__device__ __forceinline__ uint32_t pack4(float a, float b, float c, float d) {
+  return (uint32_t)((int)a & 0xff) | ((uint32_t)((int)b & 0xff) << 8) |
+         ((uint32_t)((int)c & 0xff) << 16) | ((uint32_t)((int)d & 0xff) << 24);
+}
+
+// Per-tensor: delta/zp are wave-uniform scalars.  Each thread keeps UNROLL 16-B loads
+// in flight (1 KiB per wave-instruction); NT selects the streaming cache policy.
+template <bool CODES, int UNROLL, bool NT>
+__global__ __launch_bounds__(kBlock) void fq_fwd_pt(const f32x4* __restrict__ x,
+                                                    f32x4* __restrict__ y,
+                                                    uint32_t* __restrict__ codes,
+                                                    const float* __restrict__ delta,
+                                                    const float* __restrict__ zp,
+                                                    int64_t n4, float scale, float lo,
+                                                    float hi) {
+  QParams p;
+  p.d = __fmul_rn(delta[0], scale);
+  p.z = zp[0];
+  p.lo = lo;
+  p.hi = hi;
+  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+  int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  for (; i + (UNROLL - 1) * stride < n4; i += UNROLL * stride) {
+    f32x4 v[UNROLL];
+#pragma unroll
+    for (int u = 0; u < UNROLL; ++u) v[u] = ld4<NT>(&x[i + u * stride]);
+#pragma unroll
+    for (int u = 0; u < UNROLL; ++u) {
+      f32x4 o;
+      float q0, q1, q2, q3;
+      o.x = fq1(v[u].x, p, &q0);
+      o.y = fq1(v[u].y, p, &q1);
+      o.z = fq1(v[u].z, p, &q2);
+      o.w = fq1(v[u].w, p, &q3);
+      st4<NT>(o, &y[i + u * stride]);
+      if (CODES) codes[i + u * stride] = pack4(q0, q1, q2, q3);
+    }
+  }
+  for (; i < n4; i += stride) {
+    f32x4 v = x[i], o;
+    float q0, q1, q2, q3;
+    o.x = fq1(v.x, p, &q0);
+    o.y = fq1(v.y, p, &q1);
+    o.z = fq1(v.z, p, &q2);
+    o.w = fq1(v.w, p, &q3);
+    y[i] = o;
+    if (CODES) codes[i] = pack4(q0, q1, q2, q3);
+  }
+}
+
+// General scalar path: any alignment, per-channel c = (i / inner) % nch.
+__global__ __launch_bounds__(kBlock) void fq_fwd_scalar(const float* __restrict__ x,
+                                                        float* __restrict__ y,
+                                                        uint8_t* __restrict__ codes,
+                                                        const float* __restrict__ delta,
+                                                        const float* __restrict__ zp,
+                                                        int64_t n, int64_t start, int64_t inner,
+                                                        int64_t nch, float scale, float lo,
+                                                        float hi) {
+  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+  for (int64_t i = start + (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
+    int64_t c = nch == 1 ? 0 : (i / inner) % nch;
+    QParams p;
+    p.d = __fmul_rn(delta[c], scale);
+    p.z = zp[c];
+    p.lo = lo;
+    p.hi = hi;
+    float q;
+    y[i] = fq1(x[i], p, &q);
+    if (codes) codes[i] = (uint8_t)((int)q & 0xff);
+  }
+}
+
+// Per-channel vector path (rows of `inner` elements, 16-B aligned): one float4 may
+// straddle a channel boundary when inner % 4 != 0, so the channel is tracked per lane.
+template <bool CODES>
+__global__ __launch_bounds__(kBlock) void fq_fwd_pc(const f32x4* __restrict__ x,
+                                                    f32x4* __restrict__ y,
+                                                    uint32_t* __restrict__ codes,
+                                                    const float* __restrict__ delta,
+                                                    const float* __restrict__ zp,
+                                                    int64_t n4, uint32_t inner, uint32_t nch,
+                                                    float scale, float lo, float hi) {
+  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n4; i += stride) {
+    f32x4 v = x[i], o;
+    float in[4] = {v.x, v.y, v.z, v.w}, out[4], q[4];
+    uint64_t e = (uint64_t)i * 4;
+    uint64_t c = e / inner;
+    uint64_t next = (c + 1) * inner;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      while (e + j >= next) {
+        ++c;
+        next += inner;
+      }
+      uint32_t cc = (uint32_t)(c % nch);
+      QParams p;
+      p.d = __fmul_rn(delta[cc], scale);
+      p.z = zp[cc];
+      p.lo = lo;
+      p.hi = hi;
+      out[j] = fq1(in[j], p, &q[j]);
+    }
+    o.x = out[0];
+    o.y = out[1];
+    o.z = out[2];
+    o.w = out[3];
+    y[i] = o;
+    if (CODES) codes[i] = pack4(q[0], q[1], q[2], q[3]);
+  }
+}
+
+// ------------------------------------------------------------------ multi-tensor forward
+struct Seg {
+  const float* x;
+  float* y;
+  const float* delta;
+  const float* zp;
+  int64_t n;
+  int64_t blk0;  // first workgroup of this segment
+  uint32_t inner, nch;
+  float lo, hi;
+};
+constexpr int kMaxSeg = 64;
+constexpr int kTile = 4096;  // elements per workgroup (16 per thread)
+struct SegTable {
+  Seg s[kMaxSeg];
+  int nseg;
+};
+
+// One workgroup = one tile of one segment.  The (delta, zp) of every channel the tile
+// touches are staged in LDS once, then each element reads its pair from LDS.
+__global__ __launch_bounds__(kBlock) void fq_fwd_multi_kernel(SegTable tab) {
+  __shared__ float sd[kTile + 2], sz[kTile + 2];
+  int si = 0;
+  while (si + 1 < tab.nseg && (int64_t)blockIdx.x >= tab.s[si + 1].blk0) ++si;
+  const Seg sg = tab.s[si];
+  const int64_t t0 = ((int64_t)blockIdx.x - sg.blk0) * kTile;
+  const int64_t t1 = min(t0 + (int64_t)kTile, sg.n);
+  const int64_t c0 = t0 / sg.inner, c1 = (t1 - 1) / sg.inner;
+  for (int64_t c = c0 + threadIdx.x; c <= c1; c += blockDim.x) {
+    sd[c - c0] = sg.delta[c % sg.nch];
+    sz[c - c0] = sg.zp[c % sg.nch];
+  }
+  __syncthreads();
+  for (int64_t e = t0 + threadIdx.x; e < t1; e += blockDim.x) {
+    const int64_t cl = e / sg.inner - c0;
+    QParams p{sd[cl], sz[cl], sg.lo, sg.hi};
+    float q;
+    sg.y[e] = fq1(sg.x[e], p, &q);
+  }
+}
+
+// ------------------------------------------------------------------ backward
+// partial layout in ws: per block 4 doubles {sum gy*(q-zp), sum g_int*((x/d)/d), sum g_int, sum gy*d}
+__global__ __launch_bounds__(kBlock) void fq_bwd_pt(const float* __restrict__ x,
+                                                    const float* __restrict__ gy,
+                                                    const float* __restrict__ delta,
+                                                    const float* __restrict__ zp, int64_t n,
+                                                    float lo, float hi, float* __restrict__ gx,
+                                                    double* __restrict__ part) {
+  __shared__ double red[16];
+  const float d = delta[0], z = zp[0];
+  double a0 = 0, a1 = 0, a2 = 0, a3 = 0;
+  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
+    const float xv = x[i], g = gy[i];
+    const float t = xv / d;
+    const float v = __fadd_rn(rintf(t), z);
+    const bool m = (v >= lo) && (v <= hi);
+    const float q = clampf(v, lo, hi);
+    const float gq = __fmul_rn(g, d);
+    const float gi = m ? gq : 0.0f;
+    if (gx) gx[i] = gi / d;
+    if (part) {
+      a0 += (double)g * (double)__fsub_rn(q, z);
+      a1 += (double)gi * (double)(t / d);
+      a2 += (double)gi;
+      a3 += (double)gq;
+    }
+  }
+  if (!part) return;
+  a0 = block_sum(a0, red);
+  a1 = block_sum(a1, red);
+  a2 = block_sum(a2, red);
+  a3 = block_sum(a3, red);
+  if (threadIdx.x == 0) {
+    double* o = part + 4 * (int64_t)blockIdx.x;
+    o[0] = a0;
+    o[1] = a1;
+    o[2] = a2;
+    o[3] = a3;
+  }
+}
+
+// one workgroup per channel row (rows are contiguous: n == nch * inner)
+__global__ __launch_bounds__(kBlock) void fq_bwd_rows(const float* __restrict__ x,
+                                                      const float* __restrict__ gy,
+                                                      const float* __restrict__ delta,
+                                                      const float* __restrict__ zp,
+                                                      int64_t inner, float lo, float hi,
+                                                      float* __restrict__ gx,
+                                                      float* __restrict__ gdelta,
+                                                      float* __restrict__ gzp) {
+  __shared__ double red[16];
+  const int64_t c = blockIdx.x;
+  const float d = delta[c], z = zp[c];
+  double a0 = 0, a1 = 0, a2 = 0, a3 = 0;
+  for (int64_t k = threadIdx.x; k < inner; k += blockDim.x) {
+    const int64_t i = c * inner + k;
+    const float xv = x[i], g = gy[i];
+    const float t = xv / d;
+    const float v = __fadd_rn(rintf(t), z);
+    const bool m = (v >= lo) && (v <= hi);
+    const float q = clampf(v, lo, hi);
+    const float gq = __fmul_rn(g, d);
+    const float gi = m ? gq : 0.0f;
+    if (gx) gx[i] = gi / d;
+    a0 += (double)g * (double)__fsub_rn(q, z);
+    a1 += (double)gi * (double)(t / d);
+    a2 += (double)gi;
+    a3 += (double)gq;
+  }
+  if (!gdelta && !gzp) return;
+  a0 = block_sum(a0, red);
+  a1 = block_sum(a1, red);
+  a2 = block_sum(a2, red);
+  a3 = block_sum(a3, red);
+  if (threadIdx.x == 0) {
+    if (gdelta) gdelta[c] = (float)(a0 - a1);
+    if (gzp) gzp[c] = (float)(a2 - a3);
+  }
+}
+
+__global__ void fq_bwd_finalize(const double* __restrict__ part, int nblk,
+                                float* __restrict__ gdelta, float* __restrict__ gzp) {
+  __shared__ double red[16];
+  double a[4] = {0, 0, 0, 0};
+  for (int b = threadIdx.x; b < nblk; b += blockDim.x)
+    for (int k = 0; k < 4; ++k) a[k] += part[4 * (int64_t)b + k];
+  for (int k = 0; k < 4; ++k) a[k] = block_sum(a[k], red);
+  if (threadIdx.x == 0) {
+    if (gdelta) gdelta[0] = (float)(a[0] - a[1]);
+    if (gzp) gzp[0] = (float)(a[2] - a[3]);
+  }
+}
+
+constexpr int kBwdBlocks = 1024;
+
+template <bool NT>
+__global__ __launch_bounds__(kBlock) void copy_kernel(const f32x4* __restrict__ s,
+                                                      f32x4* __restrict__ d, int64_t n4) {
+  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+  int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  for (; i + 3 * stride < n4; i += 4 * stride) {
+    f32x4 v0 = ld4<NT>(&s[i]);
+    f32x4 v1 = ld4<NT>(&s[i + stride]);
+    f32x4 v2 = ld4<NT>(&s[i + 2 * stride]);
+    f32x4 v3 = ld4<NT>(&s[i + 3 * stride]);
+    st4<NT>(v0, &d[i]);
+    st4<NT>(v1, &d[i + stride]);
+    st4<NT>(v2, &d[i + 2 * stride]);
+    st4<NT>(v3, &d[i + 3 * stride]);
+  }
+  for (; i < n4; i += stride) d[i] = s[i];
+}
+
+// Tuning variant for the per-tensor forward / copy (bench A/B): 0 plain, 1 non-temporal.
+static int g_variant = 1;
+
+static bool aligned16(const void* p) { return ((uintptr_t)p & 15u) == 0; }
+
+}  // namespace ssq
+
+using namespace ssq;
+
+extern "C" const char* ssq_last_error(void) { return g_err; }
+extern "C" int ssq_version(void) { return 1; }
+extern "C" int ssq_set_variant(int v) {
+  int old = g_variant;
+  g_variant = v;
+  return old;
+}
+
+extern "C" int ssq_fq_fwd(const float* x, float* y, void* codes, const float* delta,
+                          const float* zp, int64_t n, int64_t inner, int64_t nch, float scale,
+                          int qmin, int qmax, ssq_stream_t stream) {
+  SSQ_REQUIRE(n >= 0 && inner >= 1 && nch >= 1, SSQ_E_ARG, "ssq_fq_fwd: bad sizes");
+  SSQ_REQUIRE(qmin < qmax, SSQ_E_ARG, "ssq_fq_fwd: qmin >= qmax");
+  if (n == 0) return SSQ_OK;
+  SSQ_REQUIRE(x && y && delta && zp, SSQ_E_ARG, "ssq_fq_fwd: null pointer");
+  hipStream_t s = (hipStream_t)stream;
+  const float lo = (float)qmin, hi = (float)qmax;
+  const bool vec = aligned16(x) && aligned16(y) && (!codes || ((uintptr_t)codes & 3u) == 0);
+  const int64_t n4 = vec ? n / 4 : 0;
+  if (n4 > 0) {
+    if (nch == 1) {
+      // persistent-style grid: 8 workgroups per CU, grid-stride over the tensor
+      const int grid = grid_for(n4, kBlock * 4, 2048);
+      const f32x4* xv = (const f32x4*)x;
+      f32x4* yv = (f32x4*)y;
+      uint32_t* cv = (uint32_t*)codes;
+      if (codes && g_variant)
+        hipLaunchKernelGGL((fq_fwd_pt<true, 4, true>), dim3(grid), dim3(kBlock), 0, s, xv, yv, cv,
+                           delta, zp, n4, scale, lo, hi);
+      else if (codes)
+        hipLaunchKernelGGL((fq_fwd_pt<true, 4, false>), dim3(grid), dim3(kBlock), 0, s, xv, yv,
+                           cv, delta, zp, n4, scale, lo, hi);
+      else if (g_variant)
+        hipLaunchKernelGGL((fq_fwd_pt<false, 4, true>), dim3(grid), dim3(kBlock), 0, s, xv, yv,
+                           nullptr, delta, zp, n4, scale, lo, hi);
+      else
+        hipLaunchKernelGGL((fq_fwd_pt<false, 4, false>), dim3(grid), dim3(kBlock), 0, s, xv, yv,
+                           nullptr, delta, zp, n4, scale, lo, hi);
+    } else {
+      SSQ_REQUIRE(inner < (1ll << 31) && nch < (1ll << 31), SSQ_E_ARG, "ssq_fq_fwd: dims");
+      const int grid = grid_for(n4, kBlock, 4096);
+      if (codes)
+        hipLaunchKernelGGL((fq_fwd_pc<true>), dim3(grid), dim3(kBlock), 0, s, (const f32x4*)x,
+                           (f32x4*)y, (uint32_t*)codes, delta, zp, n4, (uint32_t)inner,
+                           (uint32_t)nch, scale, lo, hi);
+      else
+        hipLaunchKernelGGL((fq_fwd_pc<false>), dim3(grid), dim3(kBlock), 0, s, (const f32x4*)x,
+                           (f32x4*)y, nullptr, delta, zp, n4, (uint32_t)inner, (uint32_t)nch,
+                           scale, lo, hi);
+    }
+  }
+  const int64_t start = n4 * 4;
+  if (start < n) {
+    hipLaunchKernelGGL(fq_fwd_scalar, dim3(grid_for(n - start, kBlock)), dim3(kBlock), 0, s, x,
+                       y, (uint8_t*)codes, delta, zp, n, start, inner, nch, scale, lo, hi);
+  }
+  return check_launch("ssq_fq_fwd");
+}
+
+extern "C" int ssq_fq_fwd_multi(int nseg, const float* const* x, float* const* y,
+                                const float* const* delta, const float* const* zp,
+                                const int64_t* n, const int64_t* inner, const int64_t* nch,
+                                const int* qmin, const int* qmax, ssq_stream_t stream) {
+  SSQ_REQUIRE(nseg >= 1 && nseg <= kMaxSeg, SSQ_E_ARG, "ssq_fq_fwd_multi: 1 <= nseg <= %d",
+              kMaxSeg);
+  SegTable tab;
+  tab.nseg = nseg;
+  int64_t blk = 0;
+  for (int i = 0; i < nseg; ++i) {
+    SSQ_REQUIRE(n[i] >= 1 && inner[i] >= 1 && nch[i] >= 1 && qmin[i] < qmax[i], SSQ_E_ARG,
+                "ssq_fq_fwd_multi: bad segment %d", i);
+    SSQ_REQUIRE(x[i] && y[i] && delta[i] && zp[i], SSQ_E_ARG,
+                "ssq_fq_fwd_multi: null pointer in segment %d", i);
+    SSQ_REQUIRE(inner[i] < (1ll << 31) && nch[i] < (1ll << 31), SSQ_E_ARG,
+                "ssq_fq_fwd_multi: dims");
+    tab.s[i] = Seg{x[i], y[i], delta[i], zp[i], n[i], blk, (uint32_t)inner[i], (uint32_t)nch[i],
+                   (float)qmin[i], (float)qmax[i]};
+    blk += (n[i] + kTile - 1) / kTile;
+  }
+  SSQ_REQUIRE(blk < (1ll << 31), SSQ_E_ARG, "ssq_fq_fwd_multi: too many tiles");
+  hipLaunchKernelGGL(fq_fwd_multi_kernel, dim3((unsigned)blk), dim3(kBlock), 0,
+                     (hipStream_t)stream, tab);
+  return check_launch("ssq_fq_fwd_multi");
+}
+
+extern "C" size_t ssq_fq_bwd_workspace_size(int64_t n, int64_t inner, int64_t nch) {
+  (void)n;
+  (void)inner;
+  return nch == 1 ? (size_t)kBwdBlocks * 4 * sizeof(double) : 0;
+}
+
+extern "C" int ssq_fq_bwd(const float* x, const float* gy, const float* delta, const float* zp,
+                          int64_t n, int64_t inner, int64_t nch, int qmin, int qmax, float* gx,
+                          float* gdelta, float* gzp, void* ws, size_t ws_bytes,
+                          ssq_stream_t stream) {
+  SSQ_REQUIRE(n >= 1 && inner >= 1 && nch >= 1 && qmin < qmax, SSQ_E_ARG, "ssq_fq_bwd: sizes");
+  SSQ_REQUIRE(x && gy && delta && zp, SSQ_E_ARG, "ssq_fq_bwd: null pointer");
+  hipStream_t s = (hipStream_t)stream;
+  const float lo = (float)qmin, hi = (float)qmax;
+  const bool want_red = gdelta || gzp;
+  if (nch == 1) {
+    if (want_red)
+      SSQ_REQUIRE(ws && ws_bytes >= ssq_fq_bwd_workspace_size(n, inner, nch), SSQ_E_WS,
+                  "ssq_fq_bwd: workspace too small");
+    const int grid = grid_for(n, kBlock, kBwdBlocks);
+    hipLaunchKernelGGL(fq_bwd_pt, dim3(grid), dim3(kBlock), 0, s, x, gy, delta, zp, n, lo, hi, gx,
+                       want_red ? (double*)ws : nullptr);
+    if (want_red)
+      hipLaunchKernelGGL(fq_bwd_finalize, dim3(1), dim3(kBlock), 0, s, (const double*)ws, grid,
+                         gdelta, gzp);
+  } else {
+    SSQ_REQUIRE(n == nch * inner, SSQ_E_ARG,
+                "ssq_fq_bwd: per-channel reduction needs contiguous rows (n == nch*inner)");
+    hipLaunchKernelGGL(fq_bwd_rows, dim3((unsigned)nch), dim3(kBlock), 0, s, x, gy, delta, zp,
+                       inner, lo, hi, gx, gdelta, gzp);
+  }
+  return check_launch("ssq_fq_bwd");
+}
+
+extern "C" int ssq_stream_copy(const float* src, float* dst, int64_t n, ssq_stream_t stream) {
+  SSQ_REQUIRE(src && dst && n >= 0 && aligned16(src) && aligned16(dst) && n % 4 == 0, SSQ_E_ARG,
+              "ssq_stream_copy: needs 16-B aligned float4 buffers");
+  if (n == 0) return SSQ_OK;
+  const int64_t n4 = n / 4;
+  const dim3 grid(grid_for(n4, kBlock * 4, 2048));
+  if (g_variant)
+    hipLaunchKernelGGL((copy_kernel<true>), grid, dim3(kBlock), 0, (hipStream_t)stream,
+                       (const f32x4*)src, (f32x4*)dst, n4);
+  else
+    hipLaunchKernelGGL((copy_kernel<false>), grid, dim3(kBlock), 0, (hipStream_t)stream,
+                       (const f32x4*)src, (f32x4*)dst, n4);
+  return check_launch("ssq_stream_copy");
+}

@@ -1,0 +1,144 @@
+// Shared helpers for the ssq HIP kernels (gfx950 / CDNA4).
+//
+// Numerics contract (see DESIGN.md "bit-exactness"): every kernel reproduces the
+// reference's fp32 operation order with IEEE division (hipcc default: correctly
+// rounded fp32 divide), round-half-even (rintf), and no FMA contraction
+// (-ffp-contract=off on the build line, plus explicit __fmul_rn/__fadd_rn where the
+// reference does separate tensor ops).
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+#include <stddef.h>
+
+#include "../../include/ssq.h"
+
+namespace ssq {
+
+typedef float f32x4 __attribute__((ext_vector_type(4)));  // native 16-B vector
+
+constexpr int kWave = 64;          // CDNA wavefront
+constexpr int kBlock = 256;        // 4 waves per workgroup
+constexpr float kGamma = -0.1f;    // channelQuant.py:35 (gamma, zeta) = (-0.1, 1.1)
+constexpr float kZmG = 1.2f;       // fp32((1.1) - (-0.1)) = fp32(1.2000000000000002)
+
+// ---------------------------------------------------------------- error plumbing
+void set_error(const char* fmt, ...);
+int check_launch(const char* what);
+
+#define SSQ_REQUIRE(cond, code, ...)         \
+  do {                                       \
+    if (!(cond)) {                           \
+      ::ssq::set_error(__VA_ARGS__);         \
+      return (code);                         \
+    }                                        \
+  } while (0)
+
+inline int grid_for(int64_t work_items, int block, int max_blocks = 4096) {
+  int64_t g = (work_items + block - 1) / block;
+  if (g < 1) g = 1;
+  if (g > max_blocks) g = max_blocks;
+  return (int)g;
+}
+
+// Streaming loads/stores: NT=true uses the non-temporal (streaming) cache policy.
+template <bool NT>
+__device__ __forceinline__ f32x4 ld4(const f32x4* p) {
+  if constexpr (NT) return __builtin_nontemporal_load(p);
+  else return *p;
+}
+template <bool NT>
+__device__ __forceinline__ void st4(f32x4 v, f32x4* p) {
+  if constexpr (NT) __builtin_nontemporal_store(v, p);
+  else *p = v;
+}
+
+// ---------------------------------------------------------------- device math
+__device__ __forceinline__ float clampf(float v, float lo, float hi) {
+  // torch.clamp semantics on finite values: min(max(v, lo), hi)
+  return fminf(fmaxf(v, lo), hi);
+}
+
+// torch.sigmoid in fp32 (1 / (1 + exp(-x))).
+__device__ __forceinline__ float sigmoidf(float x) { return 1.0f / (1.0f + expf(-x)); }
+
+// rectified sigmoid h(v) = clamp(sigmoid(v)*(zeta-gamma) + gamma, 0, 1)
+// (channelQuant.py:123-127, adaptive_rounding.py:63-64)
+__device__ __forceinline__ float rect_sigmoid(float v) {
+  return clampf(__fadd_rn(__fmul_rn(sigmoidf(v), kZmG), kGamma), 0.0f, 1.0f);
+}
+
+// d h / d v  (clamp mask inclusive) * upstream
+__device__ __forceinline__ float rect_sigmoid_grad(float v, float g) {
+  float s = sigmoidf(v);
+  float u = __fadd_rn(__fmul_rn(s, kZmG), kGamma);
+  if (!(u >= 0.0f && u <= 1.0f)) return 0.0f;
+  return __fmul_rn(__fmul_rn(__fmul_rn(g, kZmG), __fsub_rn(1.0f, s)), s);
+}
+
+// p = clamp(softmax(a)*(zeta-gamma)+gamma, 0, 1) over S logits (channelQuant.py:120-121)
+template <int MAXS>
+__device__ __forceinline__ void soft_targets(const float* a, int S, float* s_out, float* p_out) {
+  float m = a[0];
+  for (int i = 1; i < S; ++i) m = fmaxf(m, a[i]);
+  float e[MAXS];
+  float sum = 0.0f;
+  for (int i = 0; i < S; ++i) {
+    e[i] = expf(__fsub_rn(a[i], m));
+    sum = __fadd_rn(sum, e[i]);
+  }
+  for (int i = 0; i < S; ++i) {
+    float s = e[i] / sum;
+    if (s_out) s_out[i] = s;
+    p_out[i] = clampf(__fadd_rn(__fmul_rn(s, kZmG), kGamma), 0.0f, 1.0f);
+  }
+}
+
+// first index of the maximum (torch.argmax tie rule)
+__device__ __forceinline__ int argmax_first(const float* p, int S) {
+  int best = 0;
+  for (int i = 1; i < S; ++i)
+    if (p[i] > p[best]) best = i;
+  return best;
+}
+
+// ---------------------------------------------------------------- wave / block reductions
+__device__ __forceinline__ double wave_sum(double v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, kWave);
+  return v;
+}
+__device__ __forceinline__ float wave_sum(float v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, kWave);
+  return v;
+}
+__device__ __forceinline__ float wave_min(float v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v = fminf(v, __shfl_xor(v, o, kWave));
+  return v;
+}
+__device__ __forceinline__ float wave_max(float v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v = fmaxf(v, __shfl_xor(v, o, kWave));
+  return v;
+}
+
+// Deterministic block sum of one double per thread (blockDim multiple of 64, <= 1024).
+__device__ __forceinline__ double block_sum(double v, double* lds /* >= 16 */) {
+  v = wave_sum(v);
+  const int lane = threadIdx.x & (kWave - 1), w = threadIdx.x / kWave;
+  __syncthreads();
+  if (lane == 0) lds[w] = v;
+  __syncthreads();
+  double t = 0.0;
+  const int nw = blockDim.x / kWave;
+  if (threadIdx.x == 0) {
+    for (int i = 0; i < nw; ++i) t += lds[i];
+    lds[0] = t;
+  }
+  __syncthreads();
+  return lds[0];
+}
+
+}  // namespace ssq

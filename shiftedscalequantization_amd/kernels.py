@@ -1,0 +1,518 @@
+"""Tensor-level wrappers and autograd Functions over libssq.so.
+
+Each function states the reference op sequence it replaces.  All of them require fp32
+tensors on the HIP device; nothing here falls back to eager PyTorch arithmetic.
+Weight geometry: W is (Co, Ci, kh, kw) -> (Co, Ci, K=kh*kw), Linear (Co, Ci) -> K = 1.
+"""
+import ctypes as C
+
+import torch
+
+from . import _capi as A
+from ._capi import call, fptr, query, stream_of, workspace
+
+
+def qrange(n_bits, sym):
+    n = 2 ** n_bits
+    return (-(n // 2), n // 2 - 1) if sym else (0, n - 1)
+
+
+def geometry(w):
+    if w.dim() == 4:
+        return int(w.shape[0]), int(w.shape[1]), int(w.shape[2] * w.shape[3]), 0
+    if w.dim() == 2:
+        return int(w.shape[0]), int(w.shape[1]), 1, 1
+    raise ValueError(f"weight must be 2-D (Linear) or 4-D (Conv2d), got {tuple(w.shape)}")
+
+
+def _codes_buf(x, want):
+    return torch.empty(x.shape, dtype=torch.uint8, device=x.device) if want else None
+
+
+def _vp(t):
+    return None if t is None else C.c_void_p(t.data_ptr())
+
+
+# ------------------------------------------------------------------ K1/K2
+def _channel_layout(x, delta):
+    """(inner, nch) for ssq_fq_fwd from the broadcast shape of delta."""
+    nd = delta.numel()
+    if nd == 1:
+        return 1, 1
+    if delta.shape[0] == x.shape[0] and nd == x.shape[0]:
+        return x[0].numel(), nd          # per output channel (dim 0)
+    raise ValueError(f"unsupported delta shape {tuple(delta.shape)} for x {tuple(x.shape)}")
+
+
+def fake_quant_fwd(x, delta, zp, n_bits, sym=False, scale=1.0, codes=False):
+    """UniformAffineQuantizer.forward (quant_layer.py:92-98). Returns (y, codes|None)."""
+    x, xp = fptr(x, "x")
+    delta, dp = fptr(delta.detach(), "delta")
+    zp, zpp = fptr(zp.detach(), "zero_point")
+    inner, nch = _channel_layout(x, delta)
+    lo, hi = qrange(n_bits, sym)
+    y = torch.empty_like(x)
+    cb = _codes_buf(x, codes)
+    call("ssq_fq_fwd", xp, _vp(y), _vp(cb), dp, zpp, x.numel(), inner, nch, float(scale), lo, hi,
+         stream_of(x))
+    return y, cb
+
+
+class FakeQuantFn(torch.autograd.Function):
+    """round_ste fake-quant with the reference's autograd: STE for x, exact chain for
+    delta / zero_point (used by the act-delta LSQ recon, block_recon.py:62-73)."""
+
+    @staticmethod
+    def forward(ctx, x, delta, zp, n_bits, sym):
+        y, _ = fake_quant_fwd(x, delta, zp, n_bits, sym)
+        ctx.save_for_backward(x, delta, zp)
+        ctx.q = (n_bits, sym)
+        return y
+
+    @staticmethod
+    def backward(ctx, gy):
+        x, delta, zp = ctx.saved_tensors
+        n_bits, sym = ctx.q
+        x = x.contiguous()
+        gy = gy.contiguous()
+        d, z = delta.detach().contiguous(), zp.detach().contiguous()
+        inner, nch = _channel_layout(x, d)
+        lo, hi = qrange(n_bits, sym)
+        need_x, need_d, need_z = ctx.needs_input_grad[0], ctx.needs_input_grad[1], ctx.needs_input_grad[2]
+        gx = torch.empty_like(x) if need_x else None
+        gd = torch.empty(d.numel(), dtype=torch.float32, device=x.device) if need_d else None
+        gz = torch.empty(z.numel(), dtype=torch.float32, device=x.device) if need_z else None
+        wsb = query("ssq_fq_bwd_workspace_size", x.numel(), inner, nch)
+        ws, wsn = workspace(wsb, x.device)
+        call("ssq_fq_bwd", _vp(x), _vp(gy), _vp(d), _vp(z), x.numel(), inner, nch, lo, hi,
+             _vp(gx), _vp(gd), _vp(gz), ws, wsn, stream_of(x))
+        return (gx, None if gd is None else gd.view(delta.shape),
+                None if gz is None else gz.view(zp.shape), None, None)
+
+
+def fake_quant(x, delta, zp, n_bits, sym=False):
+    return FakeQuantFn.apply(x, delta, zp, n_bits, sym)
+
+
+def fake_quant_multi(xs, deltas, zps, n_bits, sym=False):
+    """Every tensor of a list in one launch (per-channel params staged in LDS)."""
+    n = len(xs)
+    ys = [torch.empty_like(x) for x in xs]
+    keep = []
+    P = C.c_void_p * n
+    xa, ya, da, za = P(), P(), P(), P()
+    na, ia, ca = (C.c_int64 * n)(), (C.c_int64 * n)(), (C.c_int64 * n)()
+    lo_a, hi_a = (C.c_int * n)(), (C.c_int * n)()
+    nb = n_bits if isinstance(n_bits, (list, tuple)) else [n_bits] * n
+    for k, (x, d, z, y) in enumerate(zip(xs, deltas, zps, ys)):
+        x, xp = fptr(x)
+        d, dp = fptr(d.detach())
+        z, zpp = fptr(z.detach())
+        keep += [x, d, z]
+        inner, nch = _channel_layout(x, d)
+        xa[k], ya[k], da[k], za[k] = xp.value, y.data_ptr(), dp.value, zpp.value
+        na[k], ia[k], ca[k] = x.numel(), inner, nch
+        lo_a[k], hi_a[k] = qrange(nb[k], sym)
+    call("ssq_fq_fwd_multi", n, xa, ya, da, za, na, ia, ca, lo_a, hi_a, stream_of(xs[0]))
+    return ys
+
+
+# ------------------------------------------------------------------ K3/K4
+def scale_init(x, n_bits, sym=False, channel_wise=False, method="max", return_scores=False):
+    """init_quantization_scale (quant_layer.py:100-166) on the device.
+    Returns (delta, zero_point, raw_zero_point) shaped like the reference's:
+    (Co,1,1,1)/(Co,1) for channel_wise, 0-dim otherwise."""
+    x, xp = fptr(x.detach(), "x")
+    if "max" in method:
+        m, sflag = 0, int("scale" in method)
+    elif method == "mse":
+        m, sflag = 1, 0
+    else:
+        raise NotImplementedError(method)
+    rows = x.shape[0] if channel_wise else 1
+    inner = x.numel() // rows
+    d = torch.empty(rows, dtype=torch.float32, device=x.device)
+    z = torch.empty_like(d)
+    r = torch.empty_like(d)
+    sc = torch.empty(rows, 80, dtype=torch.float64, device=x.device) if (return_scores and m == 1) else None
+    wsb = query("ssq_scale_init_workspace_size", rows, inner, m)
+    ws, wsn = workspace(wsb, x.device)
+    call("ssq_scale_init", xp, rows, inner, n_bits, int(sym), m, sflag, _vp(d), _vp(z), _vp(r),
+         _vp(sc), ws, wsn, stream_of(x))
+    if channel_wise:
+        shape = (-1,) + (1,) * (x.dim() - 1)
+        out = d.view(shape), z.view(shape), r.view(shape)
+    else:
+        out = d.view(()), z.view(()), r.view(())
+    return out + (sc,) if return_scores else out
+
+
+# ------------------------------------------------------------------ K9 inits
+def shift_init(w, delta, shifts):
+    """ChannelQuant.init_v_beta (channelQuant.py:279-294): returns (alpha, beta, mse)."""
+    w, wp = fptr(w.detach(), "weight")
+    delta, dp = fptr(delta.detach(), "delta")
+    Co, Ci, K, is_fc = geometry(w)
+    S = len(shifts)
+    alpha = torch.empty((Co, Ci, S) if is_fc else (Ci, S), dtype=torch.float32, device=w.device)
+    if not is_fc and Ci == 1:
+        alpha = alpha.view(1, S)
+    mse = torch.empty_like(alpha)
+    beta = torch.empty_like(w)
+    wsb = query("ssq_shift_init_workspace_size", Co, Ci, K, S, is_fc)
+    ws, wsn = workspace(wsb, w.device)
+    call("ssq_shift_init", wp, dp, A.shifts_arg(shifts), S, Co, Ci, K, is_fc, _vp(alpha), _vp(beta),
+         _vp(mse), ws, wsn, stream_of(w))
+    return alpha, beta, mse
+
+
+def rect_init(w, delta):
+    """beta = -log((zeta-gamma)/(rest-gamma) - 1) (channelQuant.py:300-307,
+    adaptive_rounding.py:72-78); delta per output row or per (row, in-channel)."""
+    w, wp = fptr(w.detach(), "weight")
+    delta, dp = fptr(delta.detach(), "delta")
+    Co, Ci, K, _ = geometry(w)
+    per_ci = _delta_per_ci(delta, Co, Ci)
+    beta = torch.empty_like(w)
+    call("ssq_rect_init", wp, dp, per_ci, Co, Ci, K, _vp(beta), stream_of(w))
+    return beta
+
+
+def _delta_per_ci(delta, Co, Ci):
+    if delta.numel() == Co:
+        return 0
+    if delta.numel() == Co * Ci:
+        return 1
+    raise ValueError(f"delta with {delta.numel()} entries for ({Co},{Ci}) weight")
+
+
+def get_delta(delta, alpha, shifts, w_shape):
+    """ChannelQuant.get_delta (channelQuant.py:221-237) -> (Co,Ci,1,1) conv / (Co,Ci) fc."""
+    delta, dp = fptr(delta.detach(), "delta")
+    alpha, ap = fptr(alpha.detach(), "alpha")
+    Co, Ci = int(w_shape[0]), int(w_shape[1])
+    is_fc = int(len(w_shape) == 2)
+    out = torch.empty(Co, Ci, dtype=torch.float32, device=delta.device)
+    call("ssq_get_delta", dp, ap, A.shifts_arg(shifts), len(shifts), Co, Ci, is_fc, _vp(out),
+         stream_of(delta))
+    return out if is_fc else out.view(Co, Ci, 1, 1)
+
+
+# ------------------------------------------------------------------ K5/K6 adaShift
+class AdaShiftFn(torch.autograd.Function):
+    """ChannelQuant.forward 'adaShift' (channelQuant.py:51-64).  Gradients flow to alpha
+    (soft targets only) and beta (soft rounding only), as in the reference's autograd.
+    ctx.reg carries an optional fused shift regulariser (lambda, b) whose gradient is
+    added to alpha's inside the same backward kernel."""
+
+    @staticmethod
+    def forward(ctx, alpha, beta, w, delta, zp, shifts, n_bits, sym, hard_t, hard_r, reg):
+        w, wp = fptr(w.detach(), "weight")
+        a, ap = fptr(alpha.detach(), "alpha")
+        b, bp = fptr(beta.detach(), "beta")
+        d, dp = fptr(delta.detach(), "delta")
+        z, zpp = fptr(zp.detach(), "zero_point")
+        Co, Ci, K, is_fc = geometry(w)
+        lo, hi = qrange(n_bits, sym)
+        out = torch.empty_like(w)
+        call("ssq_adashift_fwd", wp, ap, bp, dp, zpp, A.shifts_arg(shifts), len(shifts), Co, Ci, K,
+             is_fc, int(hard_t), int(hard_r), lo, hi, _vp(out), None, stream_of(w))
+        ctx.save_for_backward(a, b, w, d, z)
+        ctx.cfg = (tuple(shifts), n_bits, sym, hard_t, hard_r, reg)
+        return out
+
+    @staticmethod
+    def backward(ctx, g):
+        a, b, w, d, z = ctx.saved_tensors
+        shifts, n_bits, sym, hard_t, hard_r, reg = ctx.cfg
+        need_a = ctx.needs_input_grad[0] and not hard_t
+        need_b = ctx.needs_input_grad[1] and not hard_r
+        if not (need_a or need_b):
+            return (None,) * 11
+        g = g.contiguous()
+        Co, Ci, K, is_fc = geometry(w)
+        lo, hi = qrange(n_bits, sym)
+        ga = torch.empty_like(a)
+        gb = torch.empty_like(w) if need_b else None
+        lam, bb, reg_vals = (0.0, 0.0, None) if reg is None else reg
+        S = len(shifts)
+        wsb = query("ssq_adashift_bwd_workspace_size", Co, Ci, K, S, is_fc)
+        ws, wsn = workspace(wsb, w.device)
+        call("ssq_adashift_bwd", _vp(g), _vp(w), _vp(a), _vp(b), _vp(d), _vp(z),
+             A.shifts_arg(shifts), S, Co, Ci, K, is_fc, int(hard_r), lo, hi, float(lam), float(bb),
+             _vp(ga), _vp(gb), _vp(reg_vals), ws, wsn, stream_of(w))
+        return (ga if need_a else None, gb, None, None, None, None, None, None, None, None, None)
+
+
+def adashift(alpha, beta, w, delta, zp, shifts, n_bits, sym, hard_t, hard_r, reg=None):
+    return AdaShiftFn.apply(alpha, beta, w, delta, zp, tuple(shifts), n_bits, sym, bool(hard_t),
+                            bool(hard_r), reg)
+
+
+def adashift_codes(alpha, beta, w, delta, zp, shifts, n_bits, sym):
+    """Hard/hard adaShift: dequantized weight and the integer codes (uint8/int8)."""
+    w, wp = fptr(w.detach())
+    a, ap = fptr(alpha.detach())
+    b, bp = fptr(beta.detach())
+    d, dp = fptr(delta.detach())
+    z, zpp = fptr(zp.detach())
+    Co, Ci, K, is_fc = geometry(w)
+    lo, hi = qrange(n_bits, sym)
+    out = torch.empty_like(w)
+    codes = torch.empty(w.shape, dtype=torch.uint8, device=w.device)
+    call("ssq_adashift_fwd", wp, ap, bp, dp, zpp, A.shifts_arg(shifts), len(shifts), Co, Ci, K,
+         is_fc, 1, 1, lo, hi, _vp(out), _vp(codes), stream_of(w))
+    return out, (codes.view(torch.int8) if sym else codes)
+
+
+# ------------------------------------------------------------------ K7 learned_hard_sigmoid
+class LhsFn(torch.autograd.Function):
+    """ChannelQuant 'learned_hard_sigmoid' (channelQuant.py:81-82, :96-118) with the
+    dequantized candidates of init_v (channelQuant.py:201-213) recomputed in-kernel."""
+
+    @staticmethod
+    def forward(ctx, alpha, w, delta, zp, shifts, n_bits, sym, hard_t):
+        w, wp = fptr(w.detach())
+        a, ap = fptr(alpha.detach())
+        d, dp = fptr(delta.detach())
+        z, zpp = fptr(zp.detach())
+        Co, Ci, K, is_fc = geometry(w)
+        lo, hi = qrange(n_bits, sym)
+        out = torch.empty_like(w)
+        call("ssq_lhs_fwd", wp, ap, dp, zpp, A.shifts_arg(shifts), len(shifts), Co, Ci, K, is_fc,
+             int(hard_t), lo, hi, _vp(out), stream_of(w))
+        ctx.save_for_backward(a, w, d, z)
+        ctx.cfg = (tuple(shifts), n_bits, sym, hard_t)
+        return out
+
+    @staticmethod
+    def backward(ctx, g):
+        a, w, d, z = ctx.saved_tensors
+        shifts, n_bits, sym, hard_t = ctx.cfg
+        if hard_t or not ctx.needs_input_grad[0]:
+            return (None,) * 8
+        g = g.contiguous()
+        Co, Ci, K, is_fc = geometry(w)
+        lo, hi = qrange(n_bits, sym)
+        ga = torch.empty_like(a)
+        S = len(shifts)
+        wsb = query("ssq_adashift_bwd_workspace_size", Co, Ci, K, S, is_fc)
+        ws, wsn = workspace(wsb, w.device)
+        call("ssq_lhs_bwd", _vp(g), _vp(w), _vp(a), _vp(d), _vp(z), A.shifts_arg(shifts), S, Co, Ci,
+             K, is_fc, lo, hi, _vp(ga), ws, wsn, stream_of(w))
+        return (ga, None, None, None, None, None, None, None)
+
+
+def lhs(alpha, w, delta, zp, shifts, n_bits, sym, hard_t):
+    return LhsFn.apply(alpha, w, delta, zp, tuple(shifts), n_bits, sym, bool(hard_t))
+
+
+# ------------------------------------------------------------------ K8 adaround
+class AdaRoundFn(torch.autograd.Function):
+    """floor(W/d) + h(beta) (soft) or [beta>=0] (hard), clamp, dequant
+    (channelQuant.py:65-78, adaptive_rounding.py:55-67)."""
+
+    @staticmethod
+    def forward(ctx, beta, w, delta, zp, n_bits, sym, hard_r, scale):
+        w, wp = fptr(w.detach())
+        b, bp = fptr(beta.detach())
+        d, dp = fptr(delta.detach())
+        z, zpp = fptr(zp.detach())
+        Co, Ci, K, _ = geometry(w)
+        per_ci = _delta_per_ci(d, Co, Ci)
+        lo, hi = qrange(n_bits, sym)
+        out = torch.empty_like(w)
+        call("ssq_adaround_fwd", wp, bp, dp, per_ci, zpp, float(scale), Co, Ci, K, int(hard_r), lo,
+             hi, _vp(out), None, stream_of(w))
+        ctx.save_for_backward(b, w, d, z)
+        ctx.cfg = (n_bits, sym, hard_r, scale, per_ci)
+        return out
+
+    @staticmethod
+    def backward(ctx, g):
+        b, w, d, z = ctx.saved_tensors
+        n_bits, sym, hard_r, scale, per_ci = ctx.cfg
+        if hard_r or not ctx.needs_input_grad[0]:
+            return (None,) * 8
+        g = g.contiguous()
+        Co, Ci, K, _ = geometry(w)
+        lo, hi = qrange(n_bits, sym)
+        gb = torch.empty_like(w)
+        call("ssq_adaround_bwd", _vp(g), _vp(w), _vp(b), _vp(d), per_ci, _vp(z), float(scale), Co,
+             Ci, K, lo, hi, _vp(gb), stream_of(w))
+        return (gb, None, None, None, None, None, None, None)
+
+
+def adaround(beta, w, delta, zp, n_bits, sym, hard_r, scale=1.0):
+    return AdaRoundFn.apply(beta, w, delta, zp, n_bits, sym, bool(hard_r), float(scale))
+
+
+# ------------------------------------------------------------------ K12 regularisers
+class ShiftRegFn(torch.autograd.Function):
+    """lambda*sum(1-|2p-1|^b) (mode 0) or lambda*-sum p log(p+1e-10) (mode 1) of
+    p = get_sig_soft_targets(alpha) (layer_recon_fused_shiftedScale.py:281-282,
+    layer_recon_shiftedScale.py:393)."""
+
+    @staticmethod
+    def forward(ctx, alpha, lam, b, mode):
+        a, ap = fptr(alpha.detach())
+        S = a.shape[-1]
+        rows = a.numel() // S
+        vals = torch.empty(rows, dtype=torch.float32, device=a.device)
+        call("ssq_shift_reg", ap, S, rows, int(mode), float(lam), float(b), None, _vp(vals),
+             stream_of(a))
+        ctx.save_for_backward(a)
+        ctx.cfg = (lam, b, mode)
+        return vals.sum()
+
+    @staticmethod
+    def backward(ctx, g):
+        (a,) = ctx.saved_tensors
+        lam, b, mode = ctx.cfg
+        S = a.shape[-1]
+        ga = torch.zeros_like(a)
+        call("ssq_shift_reg", _vp(a), S, a.numel() // S, int(mode), float(lam), float(b), _vp(ga),
+             None, stream_of(a))
+        return ga * g, None, None, None
+
+
+def shift_reg(alpha, lam, b, mode=0):
+    return ShiftRegFn.apply(alpha, lam, b, mode)
+
+
+class RoundRegFn(torch.autograd.Function):
+    """lambda*sum(1-|2h(v)-1|^b) with h the rectified sigmoid (block_recon.py:171-174,
+    layer_recon_fused_shiftedScale.py:278-279)."""
+
+    @staticmethod
+    def forward(ctx, v, lam, b):
+        v, vp = fptr(v.detach())
+        loss = torch.empty(1, dtype=torch.float32, device=v.device)
+        ws, wsn = workspace(query("ssq_round_reg_workspace_size", v.numel()), v.device)
+        call("ssq_round_reg", vp, v.numel(), float(lam), float(b), _vp(loss), None, ws, wsn,
+             stream_of(v))
+        ctx.save_for_backward(v)
+        ctx.cfg = (lam, b)
+        return loss[0]
+
+    @staticmethod
+    def backward(ctx, g):
+        (v,) = ctx.saved_tensors
+        lam, b = ctx.cfg
+        gv = torch.zeros_like(v)
+        tmp = torch.empty(1, dtype=torch.float32, device=v.device)
+        ws, wsn = workspace(query("ssq_round_reg_workspace_size", v.numel()), v.device)
+        call("ssq_round_reg", _vp(v), v.numel(), float(lam), float(b), _vp(tmp), _vp(gv), ws, wsn,
+             stream_of(v))
+        return gv * g, None, None
+
+
+def round_reg(v, lam, b):
+    return RoundRegFn.apply(v, lam, b)
+
+
+def round_reg_value(v, lam, b, out=None):
+    """Value only (no autograd), written to a 1-element device tensor."""
+    v, vp = fptr(v.detach())
+    out = torch.empty(1, dtype=torch.float32, device=v.device) if out is None else out
+    ws, wsn = workspace(query("ssq_round_reg_workspace_size", v.numel()), v.device)
+    call("ssq_round_reg", vp, v.numel(), float(lam), float(b), _vp(out), None, ws, wsn, stream_of(v))
+    return out
+
+
+# ------------------------------------------------------------------ K10
+def inpscale_search(w, delta, raw_zp, n_bits, level, threshold):
+    """ChannelQuantMSE.init_scale 'max' (channelQuantMSE.py:203-241) -> inp_scale
+    shaped (1, Ci, kh, kw) / (1, Ci)."""
+    w, wp = fptr(w.detach())
+    d, dp = fptr(delta.detach())
+    r, rp = fptr(raw_zp.detach())
+    Co = w.shape[0]
+    J = w.numel() // Co
+    inp = torch.empty((1,) + tuple(w.shape[1:]), dtype=torch.float32, device=w.device)
+    call("ssq_inpscale_search", wp, dp, rp, Co, J, n_bits, int(level), float(threshold), _vp(inp),
+         stream_of(w))
+    return inp
+
+
+def inpscale_fwd(w, inp, delta, raw_zp, n_bits):
+    """ChannelQuantMSE.forward (channelQuantMSE.py:267-276)."""
+    w, wp = fptr(w.detach())
+    i, ip = fptr(inp.detach())
+    d, dp = fptr(delta.detach())
+    r, rp = fptr(raw_zp.detach())
+    Co = w.shape[0]
+    out = torch.empty_like(w)
+    call("ssq_inpscale_fwd", wp, ip, dp, rp, Co, w.numel() // Co, n_bits, _vp(out), stream_of(w))
+    return out
+
+
+# ------------------------------------------------------------------ K11 / K14
+def _lp_M(pred, reduction):
+    if reduction == "none":
+        return pred.numel() // pred.shape[1]
+    return pred.numel()
+
+
+def lp_loss_and_grad(pred, tgt, p=2.0, reduction="none", want_grad=True, loss_out=None):
+    """lp_loss value (1-element device tensor) and d/d pred in one fused pass."""
+    pred, pp = fptr(pred.detach(), "pred")
+    tgt, tp = fptr(tgt.detach(), "tgt")
+    loss = torch.empty(1, dtype=torch.float32, device=pred.device) if loss_out is None else loss_out
+    grad = torch.empty_like(pred) if want_grad else None
+    ws, wsn = workspace(query("ssq_lp_loss_workspace_size", pred.numel()), pred.device)
+    call("ssq_lp_loss", pp, tp, pred.numel(), _lp_M(pred, reduction), float(p), _vp(loss),
+         _vp(grad), None, ws, wsn, stream_of(pred))
+    return loss, grad
+
+
+class LpLossFn(torch.autograd.Function):
+    """lp_loss (quant_layer.py:25-32): forward = value only; backward = one pass that
+    writes (1/M)*(p|d|^(p-1))*sgn(d) scaled by the upstream gradient (device scalar)."""
+
+    @staticmethod
+    def forward(ctx, pred, tgt, p, reduction):
+        loss, _ = lp_loss_and_grad(pred, tgt, p, reduction, want_grad=False)
+        ctx.save_for_backward(pred, tgt)
+        ctx.cfg = (p, reduction)
+        return loss[0]
+
+    @staticmethod
+    def backward(ctx, g):
+        pred, tgt = ctx.saved_tensors
+        p, reduction = ctx.cfg
+        pred, tgt = pred.contiguous(), tgt.contiguous()
+        grad = torch.empty_like(pred)
+        gs = g.detach().reshape(1).to(torch.float32).contiguous()
+        call("ssq_lp_loss", _vp(pred), _vp(tgt), pred.numel(), _lp_M(pred, reduction), float(p),
+             None, _vp(grad), _vp(gs), None, 0, stream_of(pred))
+        return grad, None, None, None
+
+
+def lp_loss(pred, tgt, p=2.0, reduction="none"):
+    return LpLossFn.apply(pred, tgt, float(p), reduction)
+
+
+def gather_rows2(src0, idx, src1=None, out0=None, out1=None):
+    """src[idx] for one or two row-major sources (the cached block input / output)."""
+    s0, p0 = fptr(src0, "src0")
+    idx = idx.to(device=s0.device, dtype=torch.int64).contiguous()
+    n = idx.numel()
+    row0 = s0[0].numel()
+    d0 = torch.empty((n,) + tuple(s0.shape[1:]), dtype=s0.dtype, device=s0.device) if out0 is None else out0
+    if src1 is not None:
+        s1, p1 = fptr(src1, "src1")
+        row1 = s1[0].numel()
+        d1 = torch.empty((n,) + tuple(s1.shape[1:]), dtype=s1.dtype, device=s1.device) if out1 is None else out1
+    else:
+        s1, p1, row1, d1 = None, None, 0, None
+    call("ssq_gather_rows2", p0, _vp(d0), row0, p1, _vp(d1), row1, _vp(idx), n, stream_of(s0))
+    return d0, d1
+
+
+def stream_copy(src, dst):
+    call("ssq_stream_copy", _vp(src), _vp(dst), src.numel(), stream_of(src))
+
+
+def set_variant(v):
+    return query("ssq_set_variant", int(v))
