@@ -49,26 +49,41 @@ __device__ __forceinline__ uint32_t pack4(float a, float b, float c, float d) {
 }
 
 // Per-tensor: delta/zp are wave-uniform scalars.  Each thread keeps UNROLL 16-B loads
-// in flight (1 KiB per wave-instruction); NT selects the streaming cache policy.
-template <bool CODES, int UNROLL, bool NT>
-__global__ __launch_bounds__(kBlock) void fq_fwd_pt(const f32x4* __restrict__ x,
-                                                    f32x4* __restrict__ y,
-                                                    uint32_t* __restrict__ codes,
-                                                    const float* __restrict__ delta,
-                                                    const float* __restrict__ zp,
-                                                    int64_t n4, float scale, float lo,
-                                                    float hi) {
+// in flight (1 KiB per wave-instruction); NTL/NTS select the streaming cache policy of
+// loads/stores.  chunk == 0: grid-stride; chunk > 0: workgroup b owns float4s
+// [b*chunk, (b+1)*chunk) and its threads stride through them.
+__device__ __forceinline__ void stream_range(int64_t n4, int64_t chunk, int64_t& i, int64_t& end,
+                                             int64_t& stride) {
+  if (chunk > 0) {
+    i = (int64_t)blockIdx.x * chunk + threadIdx.x;
+    end = min((int64_t)(blockIdx.x + 1) * chunk, n4);
+    stride = blockDim.x;
+  } else {
+    i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    end = n4;
+    stride = (int64_t)gridDim.x * blockDim.x;
+  }
+}
+
+template <bool CODES, int UNROLL, bool NTL, bool NTS>
+__global__ __launch_bounds__(1024) void fq_fwd_pt(const f32x4* __restrict__ x,
+                                                  f32x4* __restrict__ y,
+                                                  uint32_t* __restrict__ codes,
+                                                  const float* __restrict__ delta,
+                                                  const float* __restrict__ zp, int64_t n4,
+                                                  float scale, float lo, float hi,
+                                                  int64_t chunk) {
   QParams p;
   p.d = __fmul_rn(delta[0], scale);
   p.z = zp[0];
   p.lo = lo;
   p.hi = hi;
-  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
-  int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  for (; i + (UNROLL - 1) * stride < n4; i += UNROLL * stride) {
+  int64_t i, end, stride;
+  stream_range(n4, chunk, i, end, stride);
+  for (; i + (UNROLL - 1) * stride < end; i += UNROLL * stride) {
     f32x4 v[UNROLL];
 #pragma unroll
-    for (int u = 0; u < UNROLL; ++u) v[u] = ld4<NT>(&x[i + u * stride]);
+    for (int u = 0; u < UNROLL; ++u) v[u] = ld4<NTL>(&x[i + u * stride]);
 #pragma unroll
     for (int u = 0; u < UNROLL; ++u) {
       f32x4 o;
@@ -77,11 +92,11 @@ __global__ __launch_bounds__(kBlock) void fq_fwd_pt(const f32x4* __restrict__ x,
       o.y = fq1(v[u].y, p, &q1);
       o.z = fq1(v[u].z, p, &q2);
       o.w = fq1(v[u].w, p, &q3);
-      st4<NT>(o, &y[i + u * stride]);
+      st4<NTS>(o, &y[i + u * stride]);
       if (CODES) codes[i + u * stride] = pack4(q0, q1, q2, q3);
     }
   }
-  for (; i < n4; i += stride) {
+  for (; i < end; i += stride) {
     f32x4 v = x[i], o;
     float q0, q1, q2, q3;
     o.x = fq1(v.x, p, &q0);
@@ -293,26 +308,106 @@ __global__ void fq_bwd_finalize(const double* __restrict__ part, int nblk,
 
 constexpr int kBwdBlocks = 1024;
 
-template <bool NT>
-__global__ __launch_bounds__(kBlock) void copy_kernel(const f32x4* __restrict__ s,
-                                                      f32x4* __restrict__ d, int64_t n4) {
-  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
-  int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  for (; i + 3 * stride < n4; i += 4 * stride) {
-    f32x4 v0 = ld4<NT>(&s[i]);
-    f32x4 v1 = ld4<NT>(&s[i + stride]);
-    f32x4 v2 = ld4<NT>(&s[i + 2 * stride]);
-    f32x4 v3 = ld4<NT>(&s[i + 3 * stride]);
-    st4<NT>(v0, &d[i]);
-    st4<NT>(v1, &d[i + stride]);
-    st4<NT>(v2, &d[i + 2 * stride]);
-    st4<NT>(v3, &d[i + 3 * stride]);
+template <int UNROLL, bool NTL, bool NTS>
+__global__ __launch_bounds__(1024) void copy_kernel(const f32x4* __restrict__ s,
+                                                    f32x4* __restrict__ d, int64_t n4,
+                                                    int64_t chunk) {
+  int64_t i, end, stride;
+  stream_range(n4, chunk, i, end, stride);
+  for (; i + (UNROLL - 1) * stride < end; i += UNROLL * stride) {
+    f32x4 v[UNROLL];
+#pragma unroll
+    for (int u = 0; u < UNROLL; ++u) v[u] = ld4<NTL>(&s[i + u * stride]);
+#pragma unroll
+    for (int u = 0; u < UNROLL; ++u) st4<NTS>(v[u], &d[i + u * stride]);
   }
-  for (; i < n4; i += stride) d[i] = s[i];
+  for (; i < end; i += stride) d[i] = s[i];
 }
 
-// Tuning variant for the per-tensor forward / copy (bench A/B): 0 plain, 1 non-temporal.
-static int g_variant = 1;
+// Tuning variant of the streaming kernels (bench A/B only):
+//   bits 0-1 cache policy: 0 plain, 1 NT load+store, 2 NT load only, 3 NT store only
+//   bits 4-7 unroll: 0 -> 4, 1 -> 1, 2 -> 2, 3 -> 8
+//   bits 8-23 grid size in workgroups (0 -> 2048)
+//   bit  24   chunked (workgroup-contiguous) instead of grid-stride
+//   bits 25-26 workgroup size: 0 -> 256, 1 -> 512, 2 -> 1024
+static int g_variant = 1 | (256 << 8);  // NT load+store, unroll 4, 1 workgroup per CU (sweep: tools/sweep_stream.py)
+
+struct Variant {
+  bool ntl, nts, chunked;
+  int unroll, grid, block;
+};
+static Variant decode_variant(int v) {
+  Variant r;
+  const int pol = v & 3;
+  r.ntl = pol == 1 || pol == 2;
+  r.nts = pol == 1 || pol == 3;
+  const int u = (v >> 4) & 0xF;
+  r.unroll = u == 1 ? 1 : u == 2 ? 2 : u == 3 ? 8 : 4;
+  r.grid = (v >> 8) & 0xFFFF;
+  if (r.grid == 0) r.grid = 2048;
+  r.chunked = (v >> 24) & 1;
+  const int b = (v >> 25) & 3;
+  r.block = b == 1 ? 512 : b == 2 ? 1024 : 256;
+  return r;
+}
+
+// Launch geometry of a streaming kernel over n4 float4s.
+static void stream_geometry(const Variant& v, int64_t n4, dim3& grid, dim3& block,
+                            int64_t& chunk) {
+  block = dim3(v.block);
+  int64_t g = (n4 + (int64_t)v.block * v.unroll - 1) / ((int64_t)v.block * v.unroll);
+  if (g > v.grid) g = v.grid;
+  if (g < 1) g = 1;
+  chunk = 0;
+  if (v.chunked) {
+    const int64_t per = (int64_t)v.block * v.unroll;
+    chunk = ((n4 + g - 1) / g + per - 1) / per * per;  // multiple of one unrolled sweep
+    g = (n4 + chunk - 1) / chunk;
+  }
+  grid = dim3((unsigned)g);
+}
+
+// Instantiate a streaming kernel template over (UNROLL, NTL, NTS) and launch it.
+template <template <int, bool, bool> class L, typename... Args>
+static void launch_stream(const Variant& v, dim3 grid, dim3 block, hipStream_t s,
+                          Args... args) {
+#define SSQ_CASE(U)                                                                   \
+  if (v.unroll == U) {                                                                \
+    if (v.ntl && v.nts) L<U, true, true>::go(grid, block, s, args...);                \
+    else if (v.ntl) L<U, true, false>::go(grid, block, s, args...);                   \
+    else if (v.nts) L<U, false, true>::go(grid, block, s, args...);                   \
+    else L<U, false, false>::go(grid, block, s, args...);                             \
+    return;                                                                           \
+  }
+  SSQ_CASE(1) SSQ_CASE(2) SSQ_CASE(4) SSQ_CASE(8)
+#undef SSQ_CASE
+}
+
+template <int U, bool NTL, bool NTS>
+struct FqPtCodes {
+  static void go(dim3 g, dim3 b, hipStream_t s, const f32x4* x, f32x4* y, uint32_t* c,
+                 const float* d, const float* z, int64_t n4, float sc, float lo, float hi,
+                 int64_t chunk) {
+    hipLaunchKernelGGL((fq_fwd_pt<true, U, NTL, NTS>), g, b, 0, s, x, y, c, d, z, n4, sc, lo, hi,
+                       chunk);
+  }
+};
+template <int U, bool NTL, bool NTS>
+struct FqPt {
+  static void go(dim3 g, dim3 b, hipStream_t s, const f32x4* x, f32x4* y, uint32_t* c,
+                 const float* d, const float* z, int64_t n4, float sc, float lo, float hi,
+                 int64_t chunk) {
+    hipLaunchKernelGGL((fq_fwd_pt<false, U, NTL, NTS>), g, b, 0, s, x, y, c, d, z, n4, sc, lo, hi,
+                       chunk);
+  }
+};
+template <int U, bool NTL, bool NTS>
+struct Copy {
+  static void go(dim3 g, dim3 b, hipStream_t s, const f32x4* x, f32x4* y, int64_t n4,
+                 int64_t chunk) {
+    hipLaunchKernelGGL((copy_kernel<U, NTL, NTS>), g, b, 0, s, x, y, n4, chunk);
+  }
+};
 
 static bool aligned16(const void* p) { return ((uintptr_t)p & 15u) == 0; }
 
@@ -341,23 +436,19 @@ extern "C" int ssq_fq_fwd(const float* x, float* y, void* codes, const float* de
   const int64_t n4 = vec ? n / 4 : 0;
   if (n4 > 0) {
     if (nch == 1) {
-      // persistent-style grid: 8 workgroups per CU, grid-stride over the tensor
-      const int grid = grid_for(n4, kBlock * 4, 2048);
+      // persistent-style grid (default 8 workgroups per CU), grid-stride over the tensor
+      const Variant v = decode_variant(g_variant);
+      dim3 grid, block;
+      int64_t chunk;
+      stream_geometry(v, n4, grid, block, chunk);
       const f32x4* xv = (const f32x4*)x;
       f32x4* yv = (f32x4*)y;
       uint32_t* cv = (uint32_t*)codes;
-      if (codes && g_variant)
-        hipLaunchKernelGGL((fq_fwd_pt<true, 4, true>), dim3(grid), dim3(kBlock), 0, s, xv, yv, cv,
-                           delta, zp, n4, scale, lo, hi);
-      else if (codes)
-        hipLaunchKernelGGL((fq_fwd_pt<true, 4, false>), dim3(grid), dim3(kBlock), 0, s, xv, yv,
-                           cv, delta, zp, n4, scale, lo, hi);
-      else if (g_variant)
-        hipLaunchKernelGGL((fq_fwd_pt<false, 4, true>), dim3(grid), dim3(kBlock), 0, s, xv, yv,
-                           nullptr, delta, zp, n4, scale, lo, hi);
+      if (codes)
+        launch_stream<FqPtCodes>(v, grid, block, s, xv, yv, cv, delta, zp, n4, scale, lo, hi,
+                                 chunk);
       else
-        hipLaunchKernelGGL((fq_fwd_pt<false, 4, false>), dim3(grid), dim3(kBlock), 0, s, xv, yv,
-                           nullptr, delta, zp, n4, scale, lo, hi);
+        launch_stream<FqPt>(v, grid, block, s, xv, yv, cv, delta, zp, n4, scale, lo, hi, chunk);
     } else {
       SSQ_REQUIRE(inner < (1ll << 31) && nch < (1ll << 31), SSQ_E_ARG, "ssq_fq_fwd: dims");
       const int grid = grid_for(n4, kBlock, 4096);
@@ -444,12 +535,11 @@ extern "C" int ssq_stream_copy(const float* src, float* dst, int64_t n, ssq_stre
               "ssq_stream_copy: needs 16-B aligned float4 buffers");
   if (n == 0) return SSQ_OK;
   const int64_t n4 = n / 4;
-  const dim3 grid(grid_for(n4, kBlock * 4, 2048));
-  if (g_variant)
-    hipLaunchKernelGGL((copy_kernel<true>), grid, dim3(kBlock), 0, (hipStream_t)stream,
-                       (const f32x4*)src, (f32x4*)dst, n4);
-  else
-    hipLaunchKernelGGL((copy_kernel<false>), grid, dim3(kBlock), 0, (hipStream_t)stream,
-                       (const f32x4*)src, (f32x4*)dst, n4);
+  const Variant v = decode_variant(g_variant);
+  dim3 grid, block;
+  int64_t chunk;
+  stream_geometry(v, n4, grid, block, chunk);
+  launch_stream<Copy>(v, grid, block, (hipStream_t)stream, (const f32x4*)src, (f32x4*)dst, n4,
+                      chunk);
   return check_launch("ssq_stream_copy");
 }

@@ -181,8 +181,8 @@ def test_adashift_golden(K, golden, tag):
                 close(host(b.grad), g[k + "_gbeta"], rtol=1e-4, atol=1e-7)
     y, codes = K.adashift_codes(dev(alpha), dev(beta), dev(w), dev(d), dev(z), SHIFTS, bits, False)
     np.testing.assert_array_equal(host(y), g[tag + "_t1r1_y"])
-    np.testing.assert_array_equal(codes.cpu().numpy().astype(np.float32),
-                                  g[tag + "_t1r1_y"] / d + z)
+    c = codes.cpu().numpy().astype(np.float32)
+    np.testing.assert_array_equal((c - z) * d, g[tag + "_t1r1_y"])   # What = (q - zp) * delta
 
 
 @pytest.mark.parametrize("tag", CQ_TAGS)
