@@ -89,13 +89,17 @@ int ssq_scale_init(const float* x, int64_t rows, int64_t inner, int n_bits, int 
  * `shifts` (the shiftTarget list) is a HOST array of S floats; every other pointer is
  * device memory.                                                                      */
 
-/* ChannelQuant.init_v_beta (channelQuant.py:279-294) + init_alpha (:158-199) +
- * get_delta (:221-237): writes alpha (init logits), beta (W-shaped), and the per-(Ci,S)
- * (conv) / per-element (fc) squared-error table mse_out (may be NULL).                 */
+/* ChannelQuant.init_v_beta (channelQuant.py:279-294, mode 0) / init_v (:201-213, mode 1)
+ * + init_alpha (:158-199) + get_delta (:221-237).  init_alpha's squared error compares W
+ * with the integer floors F_i (mode 0, the reference's quirk) or with the dequantized
+ * 'none'-mode candidates at delta*s_i (mode 1, uses zp/qmin/qmax).  Writes alpha (init
+ * logits), beta (W-shaped, mode 0; may be NULL) and the per-(Ci,S) (conv) / per-element
+ * (fc) squared-error table mse_out (may be NULL).                                      */
 size_t ssq_shift_init_workspace_size(int64_t Co, int64_t Ci, int64_t K, int S, int is_fc);
-int ssq_shift_init(const float* W, const float* delta, const float* shifts, int S,
-                   int64_t Co, int64_t Ci, int64_t K, int is_fc, float* alpha, float* beta,
-                   float* mse_out, void* ws, size_t ws_bytes, ssq_stream_t stream);
+int ssq_shift_init(const float* W, const float* delta, const float* zp, const float* shifts,
+                   int S, int64_t Co, int64_t Ci, int64_t K, int is_fc, int mode, int qmin,
+                   int qmax, float* alpha, float* beta, float* mse_out, void* ws,
+                   size_t ws_bytes, ssq_stream_t stream);
 
 /* ChannelQuant.init_beta (channelQuant.py:300-307) / AdaRoundQuantizer.init_alpha
  * (adaptive_rounding.py:66-74): beta = -log((zeta-gamma)/(rest-gamma) - 1).           */

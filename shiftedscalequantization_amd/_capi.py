@@ -31,7 +31,8 @@ SIGNATURES = {
     "ssq_scale_init_workspace_size": (_sz, [_i64, _i64, _i]),
     "ssq_scale_init": (_i, [_p, _i64, _i64, _i, _i, _i, _i, _p, _p, _p, _p, _p, _sz, _p]),
     "ssq_shift_init_workspace_size": (_sz, [_i64, _i64, _i64, _i, _i]),
-    "ssq_shift_init": (_i, [_p, _p, _p, _i, _i64, _i64, _i64, _i, _p, _p, _p, _p, _sz, _p]),
+    "ssq_shift_init": (_i, [_p, _p, _p, _p, _i, _i64, _i64, _i64, _i, _i, _i, _i, _p, _p, _p, _p,
+                            _sz, _p]),
     "ssq_rect_init": (_i, [_p, _p, _i, _i64, _i64, _i64, _p, _p]),
     "ssq_get_delta": (_i, [_p, _p, _p, _i, _i64, _i64, _i, _p, _p]),
     "ssq_adashift_fwd": (_i, [_p, _p, _p, _p, _p, _p, _i, _i64, _i64, _i64, _i, _i, _i, _i, _i,

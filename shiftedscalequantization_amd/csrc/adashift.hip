@@ -373,10 +373,27 @@ __device__ __forceinline__ void init_alpha_row(const double* mse, int S, float* 
   for (int i = 0; i < S; ++i) a_out[i] = __fsub_rn(lg[i], avg);
 }
 
-// stage 1 of shift init (conv): column partials of sum (w - F_i)^2 over a chunk of Co.
+// Candidate error w - X_i for init_alpha: mode 0 (init_v_beta) X_i = floor(w/(d*s_i))
+// (integer floors, the reference's quirk, channelQuant.py:286); mode 1 (init_v) X_i =
+// the dequantized 'none'-mode value at d*s_i (channelQuant.py:206-208).
+struct CandCfg {
+  const float* zp;
+  int mode;
+  float lo, hi;
+};
+__device__ __forceinline__ float cand_err(float w, float d, uint32_t co, float s,
+                                          const CandCfg& c) {
+  const float x = c.mode == 0 ? floorf(w / __fmul_rn(d, s))
+                              : cand_value<1>(w, d, c.zp[co], s, c.lo, c.hi);
+  const float r = __fsub_rn(w, x);
+  return __fmul_rn(r, r);
+}
+
+// stage 1 of shift init (conv): column partials of sum (w - X_i)^2 over a chunk of Co.
 __global__ __launch_bounds__(kBlock) void shift_mse_stage1(const float* __restrict__ W,
                                                            const float* __restrict__ delta,
                                                            Shifts sh, Geo g, uint32_t chunk,
+                                                           CandCfg cc,
                                                            double* __restrict__ part) {
   const uint32_t j = blockIdx.x * blockDim.x + threadIdx.x;
   if (j >= g.CiK) return;
@@ -385,10 +402,7 @@ __global__ __launch_bounds__(kBlock) void shift_mse_stage1(const float* __restri
   for (int i = 0; i < sh.n; ++i) acc[i] = 0.0;
   for (uint32_t co = co0; co < co1; ++co) {
     const float w = W[co * g.CiK + j], d = delta[co];
-    for (int i = 0; i < sh.n; ++i) {
-      const float r = __fsub_rn(w, floorf(w / __fmul_rn(d, sh.s[i])));
-      acc[i] += (double)__fmul_rn(r, r);
-    }
+    for (int i = 0; i < sh.n; ++i) acc[i] += (double)cand_err(w, d, co, sh.s[i], cc);
   }
   double* o = part + ((size_t)blockIdx.y * g.CiK + j) * sh.n;
   for (int i = 0; i < sh.n; ++i) o[i] = acc[i];
@@ -417,17 +431,15 @@ __global__ __launch_bounds__(kBlock) void shift_mse_stage2(const double* __restr
 
 __global__ __launch_bounds__(kBlock) void shift_init_fc(const float* __restrict__ W,
                                                         const float* __restrict__ delta, Shifts sh,
-                                                        Geo g, uint32_t n, float* __restrict__ alpha,
+                                                        Geo g, uint32_t n, CandCfg cc,
+                                                        float* __restrict__ alpha,
                                                         float* __restrict__ mse_out) {
   const uint32_t stride = gridDim.x * blockDim.x;
   for (uint32_t e = blockIdx.x * blockDim.x + threadIdx.x; e < n; e += stride) {
     const uint32_t co = e / g.CiK;
     const float w = W[e], d = delta[co];
     double m[kMaxS];
-    for (int i = 0; i < sh.n; ++i) {
-      const float r = __fsub_rn(w, floorf(w / __fmul_rn(d, sh.s[i])));
-      m[i] = (double)__fmul_rn(r, r);
-    }
+    for (int i = 0; i < sh.n; ++i) m[i] = (double)cand_err(w, d, co, sh.s[i], cc);
     float a[kMaxS];
     init_alpha_row(m, sh.n, a);
     for (int i = 0; i < sh.n; ++i) {
@@ -676,30 +688,33 @@ extern "C" size_t ssq_shift_init_workspace_size(int64_t Co, int64_t Ci, int64_t 
   return is_fc ? 0 : colred_ws(Co, Ci, K, S);
 }
 
-extern "C" int ssq_shift_init(const float* W, const float* delta, const float* shifts, int S,
-                              int64_t Co, int64_t Ci, int64_t K, int is_fc, float* alpha,
-                              float* beta, float* mse_out, void* ws, size_t ws_bytes,
-                              ssq_stream_t stream) {
+extern "C" int ssq_shift_init(const float* W, const float* delta, const float* zp,
+                              const float* shifts, int S, int64_t Co, int64_t Ci, int64_t K,
+                              int is_fc, int mode, int qmin, int qmax, float* alpha, float* beta,
+                              float* mse_out, void* ws, size_t ws_bytes, ssq_stream_t stream) {
   SSQ_GEO(Co, Ci, K, is_fc, g);
   SSQ_SHIFTS(shifts, S, sh);
-  SSQ_REQUIRE(W && delta && alpha && beta, SSQ_E_ARG, "ssq_shift_init: null");
+  SSQ_REQUIRE(W && delta && alpha && (mode == 0 || mode == 1), SSQ_E_ARG, "ssq_shift_init: args");
+  SSQ_REQUIRE(mode == 0 || zp, SSQ_E_ARG, "ssq_shift_init: mode 1 needs zero_point");
   hipStream_t s = (hipStream_t)stream;
   const uint32_t n = g.Co * g.CiK;
+  const CandCfg cc{zp, mode, (float)qmin, (float)qmax};
   if (is_fc) {
     hipLaunchKernelGGL(shift_init_fc, dim3(grid_for(n, kBlock)), dim3(kBlock), 0, s, W, delta, sh,
-                       g, n, alpha, mse_out);
+                       g, n, cc, alpha, mse_out);
   } else {
     SSQ_REQUIRE(ws && ws_bytes >= colred_ws(Co, Ci, K, S), SSQ_E_WS,
                 "ssq_shift_init: workspace too small");
     uint32_t chunk, nchunk;
     chunking(g, chunk, nchunk);
     hipLaunchKernelGGL(shift_mse_stage1, dim3((g.CiK + kBlock - 1) / kBlock, nchunk), dim3(kBlock),
-                       0, s, W, delta, sh, g, chunk, (double*)ws);
+                       0, s, W, delta, sh, g, chunk, cc, (double*)ws);
     hipLaunchKernelGGL(shift_mse_stage2, dim3((g.Ci + kBlock - 1) / kBlock), dim3(kBlock), 0, s,
                        (const double*)ws, S, g, nchunk, alpha, mse_out);
   }
-  hipLaunchKernelGGL(beta_from_alpha_kernel, dim3(grid_for(n, kBlock)), dim3(kBlock), 0, s, W,
-                     delta, alpha, sh, g, n, beta);
+  if (beta)  // init_v_beta: beta from delta * s[argmax p(alpha)] (channelQuant.py:289-292)
+    hipLaunchKernelGGL(beta_from_alpha_kernel, dim3(grid_for(n, kBlock)), dim3(kBlock), 0, s, W,
+                       delta, alpha, sh, g, n, beta);
   return check_launch("ssq_shift_init");
 }
 

@@ -35,20 +35,31 @@ def _vp(t):
 
 # ------------------------------------------------------------------ K1/K2
 def _channel_layout(x, delta):
-    """(inner, nch) for ssq_fq_fwd from the broadcast shape of delta."""
+    """(inner, nch) for ssq_fq_fwd: delta broadcasts over x as x.shape[:k] + (1,)*rest,
+    channel c of element i = (i // inner) % nch."""
     nd = delta.numel()
     if nd == 1:
         return 1, 1
-    if delta.shape[0] == x.shape[0] and nd == x.shape[0]:
-        return x[0].numel(), nd          # per output channel (dim 0)
+    ds = tuple(delta.shape) + (1,) * (x.dim() - delta.dim())
+    for k in range(1, x.dim() + 1):
+        if ds[:k] == tuple(x.shape[:k]) and all(d == 1 for d in ds[k:]):
+            return x.numel() // nd, nd
     raise ValueError(f"unsupported delta shape {tuple(delta.shape)} for x {tuple(x.shape)}")
+
+
+def _zp_like(zp, delta):
+    """Expand a per-row zero point to delta's per-(row, in-channel) layout if needed."""
+    if zp.numel() == delta.numel() or zp.numel() == 1 and delta.numel() == 1:
+        return zp
+    return zp.expand(delta.shape).contiguous() if zp.dim() == delta.dim() else \
+        zp.reshape(zp.shape + (1,) * (delta.dim() - zp.dim())).expand(delta.shape).contiguous()
 
 
 def fake_quant_fwd(x, delta, zp, n_bits, sym=False, scale=1.0, codes=False):
     """UniformAffineQuantizer.forward (quant_layer.py:92-98). Returns (y, codes|None)."""
     x, xp = fptr(x, "x")
     delta, dp = fptr(delta.detach(), "delta")
-    zp, zpp = fptr(zp.detach(), "zero_point")
+    zp, zpp = fptr(_zp_like(zp.detach(), delta), "zero_point")
     inner, nch = _channel_layout(x, delta)
     lo, hi = qrange(n_bits, sym)
     y = torch.empty_like(x)
@@ -148,21 +159,22 @@ def scale_init(x, n_bits, sym=False, channel_wise=False, method="max", return_sc
 
 
 # ------------------------------------------------------------------ K9 inits
-def shift_init(w, delta, shifts):
-    """ChannelQuant.init_v_beta (channelQuant.py:279-294): returns (alpha, beta, mse)."""
+def shift_init(w, delta, shifts, zp=None, n_bits=None, sym=False, mode=0):
+    """ChannelQuant.init_v_beta (mode 0, channelQuant.py:279-294) -> (alpha, beta, mse) or
+    init_v's alpha (mode 1, channelQuant.py:201-213; beta is None)."""
     w, wp = fptr(w.detach(), "weight")
     delta, dp = fptr(delta.detach(), "delta")
+    z, zpp = fptr(zp.detach(), "zero_point") if zp is not None else (None, None)
     Co, Ci, K, is_fc = geometry(w)
     S = len(shifts)
+    lo, hi = qrange(n_bits, sym) if mode == 1 else (0, 1)
     alpha = torch.empty((Co, Ci, S) if is_fc else (Ci, S), dtype=torch.float32, device=w.device)
-    if not is_fc and Ci == 1:
-        alpha = alpha.view(1, S)
     mse = torch.empty_like(alpha)
-    beta = torch.empty_like(w)
+    beta = torch.empty_like(w) if mode == 0 else None
     wsb = query("ssq_shift_init_workspace_size", Co, Ci, K, S, is_fc)
     ws, wsn = workspace(wsb, w.device)
-    call("ssq_shift_init", wp, dp, A.shifts_arg(shifts), S, Co, Ci, K, is_fc, _vp(alpha), _vp(beta),
-         _vp(mse), ws, wsn, stream_of(w))
+    call("ssq_shift_init", wp, dp, zpp, A.shifts_arg(shifts), S, Co, Ci, K, is_fc, int(mode), lo, hi,
+         _vp(alpha), _vp(beta), _vp(mse), ws, wsn, stream_of(w))
     return alpha, beta, mse
 
 

@@ -1,0 +1,86 @@
+"""Shared machinery of the reconstruction loops.
+
+BatchFeeder: the loop's `cached[torch.randperm(N)[:batch]]` (layer_recon_fused_shiftedScale.py:
+95-97) with the permutation drawn from the SAME torch CPU generator stream as the
+reference, the indices staged through a ring of pinned host buffers (no host sync), and
+both cached tensors gathered by one ssq_gather_rows2 launch into reused device buffers.
+
+LazyValue: the reference calls .item() on the loss every iteration (a device->host sync,
+layer_recon_fused_shiftedScale.py:296-298); here loss values stay on the device and are
+read only when reported.
+"""
+import torch
+
+from .. import kernels as K
+
+
+class BatchFeeder:
+    RING = 4
+
+    def __init__(self, cached_inp, cached_out, batch_size, device):
+        self.inp = cached_inp.to(device).contiguous()
+        self.out = cached_out.to(device).contiguous()
+        self.N = self.inp.shape[0]
+        self.bs = min(batch_size, self.N)
+        self.device = device
+        pin = torch.cuda.is_available()
+        self.ring = [torch.empty(self.bs, dtype=torch.int64, pin_memory=pin) for _ in range(self.RING)]
+        self.done = [None] * self.RING
+        self.k = 0
+        self.didx = torch.empty(self.bs, dtype=torch.int64, device=device)
+        self.cur_inp = torch.empty((self.bs,) + tuple(self.inp.shape[1:]), device=device)
+        self.cur_out = torch.empty((self.bs,) + tuple(self.out.shape[1:]), device=device)
+
+    def draw(self):
+        """One reference-identical draw: torch.randperm(N)[:batch_size] on the CPU."""
+        return torch.randperm(self.N)[:self.bs]
+
+    def next(self, perm=None):
+        perm = self.draw() if perm is None else perm
+        slot = self.k % self.RING
+        if self.done[slot] is not None:
+            self.done[slot].synchronize()
+        self.ring[slot].copy_(perm)
+        self.didx.copy_(self.ring[slot], non_blocking=True)
+        ev = torch.cuda.Event()
+        ev.record()
+        self.done[slot] = ev
+        self.k += 1
+        K.gather_rows2(self.inp, self.didx, self.out, out0=self.cur_inp, out1=self.cur_out)
+        return self.cur_inp, self.cur_out
+
+    def head(self, n):
+        """cached[:n] (the final soft/hard evaluation batch)."""
+        return self.inp[:n], self.out[:n]
+
+
+class LazyValue:
+    """A device scalar (or a thunk producing one) read on demand."""
+
+    def __init__(self, v):
+        self._v = v
+
+    def get(self):
+        v = self._v() if callable(self._v) else self._v
+        if isinstance(v, torch.Tensor):
+            return float(v.detach().reshape(-1)[0].item()) if v.numel() == 1 else float(v.sum().item())
+        return float(v)
+
+    def __float__(self):
+        return self.get()
+
+    def __format__(self, spec):
+        return format(self.get(), spec)
+
+    def __str__(self):
+        return str(self.get())
+
+    def __lt__(self, o):
+        return self.get() < float(o)
+
+    def __gt__(self, o):
+        return self.get() > float(o)
+
+
+def as_float(v):
+    return v.get() if isinstance(v, LazyValue) else float(v)

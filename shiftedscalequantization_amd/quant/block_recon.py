@@ -1,0 +1,164 @@
+"""BRECQ block reconstruction (reference: quant/block_recon.py).
+
+Weight phase: every QuantModule's quantizer becomes an AdaRoundQuantizer
+('learned_hard_sigmoid', ssq_adaround_fwd/bwd) and its W-sized alpha is learned with
+loss = lp(p) + weight * sum(1 - |2h(alpha)-1|^b).  Act phase: the activation deltas
+(ssq_fq_fwd/bwd STE, LSQ-style) are learned with Adam(lr) + cosine schedule.
+multi_gpu=True all-reduces (SUM, as the reference's link.allreduce) every optimised
+gradient each iteration -- here as ONE flat RCCL bucket (parallel_dp.GradBucket); the
+reference's call crashes because `link` is never imported (block_recon.py:2,102).
+"""
+import torch
+
+from .. import kernels as K
+from ..parallel_dp import GradBucket, world
+from ._engine import BatchFeeder, LazyValue, as_float
+from .adaptive_rounding import AdaRoundQuantizer
+from .data_utils import save_grad_data, save_inp_oup_data
+from .quant_block import BaseQuantBlock
+from .quant_layer import QuantModule, StraightThrough
+from .quant_model import QuantModel
+
+
+def block_reconstruction(model: QuantModel, block: BaseQuantBlock, cali_data: torch.Tensor,
+                         batch_size: int = 32, iters: int = 20000, weight: float = 0.01,
+                         opt_mode: str = 'mse', asym: bool = False, include_act_func: bool = True,
+                         b_range: tuple = (20, 2), warmup: float = 0.0, act_quant: bool = False,
+                         lr: float = 4e-5, p: float = 2.0, multi_gpu: bool = False,
+                         eval: bool = False, dp_average: bool = False):
+    """block_recon.py:10-116."""
+    return _reconstruct(model, block, [m for m in block.modules() if isinstance(m, QuantModule)],
+                        cali_data, batch_size, iters, weight, opt_mode, asym, include_act_func,
+                        b_range, warmup, act_quant, lr, p, multi_gpu, eval, dp_average,
+                        block_level=True)
+
+
+def _reconstruct(model, block, qmodules, cali_data, batch_size, iters, weight, opt_mode, asym,
+                 include_act_func, b_range, warmup, act_quant, lr, p, multi_gpu, eval, dp_average,
+                 block_level):
+    if eval:
+        iters = 0
+    model.set_quant_state(False, False)
+    block.set_quant_state(True, act_quant)
+    round_mode = 'learned_hard_sigmoid'
+    if not include_act_func:
+        org_act_func = block.activation_function
+        block.activation_function = StraightThrough()
+
+    if not act_quant:
+        for m in qmodules:
+            m.weight_quantizer = AdaRoundQuantizer(uaq=m.weight_quantizer, round_mode=round_mode,
+                                                   weight_tensor=m.org_weight.data)
+            m.weight_quantizer.soft_targets = True
+        opt_params = [m.weight_quantizer.alpha for m in qmodules]
+        optimizer = torch.optim.Adam(opt_params)
+        scheduler = None
+    else:
+        if block_level:   # block_recon.py:64-71
+            opt_params = [block.act_quantizer.delta] + [
+                m.act_quantizer.delta for m in qmodules if m.act_quantizer.delta is not None]
+        else:             # layer_recon.py:61
+            opt_params = [block.act_quantizer.delta]
+        optimizer = torch.optim.Adam(opt_params, lr=lr)
+        scheduler = torch.optim.lr_scheduler.CosineAnnealingLR(optimizer, T_max=max(iters, 1),
+                                                               eta_min=0.)
+
+    loss_func = LossFunction(block, round_loss='none' if act_quant else 'relaxation', weight=weight,
+                             max_count=iters, rec_loss=opt_mode, b_range=b_range, decay_start=0,
+                             warmup=warmup, p=p, quant_modules=qmodules)
+    if iters > 0:
+        cached_inps, cached_outs = save_inp_oup_data(model, block, cali_data, asym, act_quant,
+                                                     batch_size)
+        device = next(model.parameters()).device
+        cached_grads = save_grad_data(model, block, cali_data, act_quant, batch_size=batch_size) \
+            if opt_mode != 'mse' else None
+        feeder = BatchFeeder(cached_inps, cached_outs, batch_size, device)
+        bucket = GradBucket(opt_params, average=dp_average) if (multi_gpu or world() > 1) else None
+        for i in range(iters):
+            perm = feeder.draw()
+            cur_inp, cur_out = feeder.next(perm)
+            cur_grad = cached_grads[perm.to(cached_grads.device)] if cached_grads is not None else None
+            optimizer.zero_grad()
+            out_quant = block(cur_inp)
+            err = loss_func(out_quant, cur_out, cur_grad)
+            err.backward()
+            if bucket is not None:
+                bucket.allreduce_()
+            optimizer.step()
+            if scheduler:
+                scheduler.step()
+    for m in qmodules:
+        if isinstance(m.weight_quantizer, AdaRoundQuantizer):
+            m.weight_quantizer.soft_targets = False
+    if not include_act_func:
+        block.activation_function = org_act_func
+
+
+class LossFunction:
+    """block_recon.py:119-182 (count incremented BEFORE the schedule, unlike the fused
+    loss).  The report line every 500 counts is the only host sync."""
+
+    def __init__(self, block, round_loss: str = 'relaxation', weight: float = 1., rec_loss: str = 'mse',
+                 max_count: int = 2000, b_range: tuple = (10, 2), decay_start: float = 0.0,
+                 warmup: float = 0.0, p: float = 2., quant_modules=None):
+        self.block = block
+        self.round_loss = round_loss
+        self.weight = weight
+        self.rec_loss = rec_loss
+        self.loss_start = max_count * warmup
+        self.p = p
+        self.temp_decay = LinearTempDecay(max_count, rel_start_decay=warmup + (1 - warmup) * decay_start,
+                                          start_b=b_range[0], end_b=b_range[1])
+        self.count = 0
+        self._qmodules = quant_modules
+        self.last_total = None
+
+    def _modules(self):
+        if self._qmodules is not None:
+            return self._qmodules
+        return [m for m in self.block.modules() if isinstance(m, QuantModule)]
+
+    def __call__(self, pred, tgt, grad=None):
+        self.count += 1
+        if self.rec_loss == 'mse':
+            rec_loss = K.lp_loss(pred, tgt, self.p)
+        elif self.rec_loss == 'fisher_diag':
+            rec_loss = ((pred - tgt).pow(2) * grad.pow(2)).sum(1).mean()
+        elif self.rec_loss == 'fisher_full':
+            a = (pred - tgt).abs()
+            g = grad.abs()
+            batch_dotprod = torch.sum(a * g, (1, 2, 3)).view(-1, 1, 1, 1)
+            rec_loss = (batch_dotprod * a * g).mean() / 100
+        else:
+            raise ValueError('Not supported reconstruction loss function: {}'.format(self.rec_loss))
+        b = self.temp_decay(self.count)
+        if self.count < self.loss_start or self.round_loss == 'none':
+            b = round_loss = 0
+        elif self.round_loss == 'relaxation':
+            round_loss = 0
+            for m in self._modules():
+                round_loss = round_loss + K.round_reg(m.weight_quantizer.alpha, self.weight, b)
+        else:
+            raise NotImplementedError
+        total_loss = rec_loss + round_loss
+        self.last_total = LazyValue(total_loss.detach())
+        if self.count % 500 == 0:
+            print('Total loss:\t{:.3f} (rec:{:.3f}, round:{:.3f})\tb={:.2f}\tcount={}'.format(
+                float(total_loss), float(rec_loss), float(round_loss), b, self.count))
+        return total_loss
+
+
+class LinearTempDecay:
+    """block_recon.py:185-202."""
+
+    def __init__(self, t_max: int, rel_start_decay: float = 0.2, start_b: int = 10, end_b: int = 2):
+        self.t_max = t_max
+        self.start_decay = rel_start_decay * t_max
+        self.start_b = start_b
+        self.end_b = end_b
+
+    def __call__(self, t):
+        if t < self.start_decay:
+            return self.start_b
+        rel_t = (t - self.start_decay) / (self.t_max - self.start_decay)
+        return self.end_b + (self.start_b - self.end_b) * max(0.0, (1 - rel_t))

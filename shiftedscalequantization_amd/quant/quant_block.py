@@ -1,0 +1,203 @@
+"""Quantized residual blocks (reference: quant/quant_block.py).
+
+Branch structure, activation and block-level act quant after the element-wise add are
+kept as in the reference.  setPathName is defined on BaseQuantBlock so every block type
+works with QuantModel (the reference defines it only on QuantBasicBlock, so QuantModel
+crashes on ResNet-50 / MobileNetV2 / RegNetX: quant_model.py:30 vs quant_block.py:119).
+"""
+import torch.nn as nn
+
+from .. import nets
+from .quant_layer import QuantModule, StraightThrough, UniformAffineQuantizer
+
+
+class BaseQuantBlock(nn.Module):
+    def __init__(self, act_quant_params: dict = {}):
+        super().__init__()
+        self.use_weight_quant = False
+        self.use_act_quant = False
+        act_quant_params = dict(act_quant_params)
+        act_quant_params['disable_act_quant'] = False
+        self.act_quantizer = UniformAffineQuantizer(**act_quant_params)
+        self.activation_function = StraightThrough()
+        self.ignore_reconstruction = False
+        self.cache_features = 'none'
+        self.cached_inp_features = []
+        self.cached_out_features = []
+        self.cache_to_host = False
+        self.selectionInited = False
+        self.pathName = ''
+
+    def set_quant_state(self, weight_quant: bool = False, act_quant: bool = False):
+        self.use_weight_quant = weight_quant
+        self.use_act_quant = act_quant
+        for m in self.modules():
+            if isinstance(m, QuantModule):
+                m.set_quant_state(weight_quant, act_quant)
+
+    def set_quant_init_state(self):
+        for m in self.modules():
+            if isinstance(m, QuantModule):
+                m.set_quant_init_state()
+
+    def set_quant_state_block(self, state, act=False):
+        for m in self.modules():
+            if isinstance(m, QuantModule):
+                if act:
+                    m.use_act_quant = state
+                else:
+                    m.use_weight_quant = state
+
+    # the reference defines these twice; the second (block-level) definition wins
+    def disable_cache_features(self):
+        self.cache_features = 'none'
+
+    def clear_cached_features(self):
+        self.cached_inp_features = []
+        self.cached_out_features = []
+
+    def _cache(self, t):
+        t = t.detach()
+        return t.cpu().clone() if self.cache_to_host else t.clone()
+
+    def setPathName(self, curName):
+        self.pathName = curName
+        for n, m in self.named_modules():
+            if isinstance(m, QuantModule) and n:
+                m.pathName = curName + '.' + n
+
+    def _finish(self, out):
+        out = self.activation_function(out)
+        if self.use_act_quant:
+            out = self.act_quantizer(out)
+        return out
+
+
+class QuantBasicBlock(BaseQuantBlock):
+    """ResNet-18/34 block (quant_block.py:76-130)."""
+
+    def __init__(self, basic_block, weight_quant_params: dict = {}, act_quant_params: dict = {}):
+        super().__init__(act_quant_params)
+        self.conv1 = QuantModule(basic_block.conv1, weight_quant_params, act_quant_params)
+        self.conv1.activation_function = basic_block.relu1
+        self.conv2 = QuantModule(basic_block.conv2, weight_quant_params, act_quant_params,
+                                 disable_act_quant=True)
+        self.activation_function = basic_block.relu2
+        self.downsample = None if basic_block.downsample is None else QuantModule(
+            basic_block.downsample[0], weight_quant_params, act_quant_params, disable_act_quant=True)
+        self.stride = basic_block.stride
+
+    def forward(self, x):
+        if self.cache_features == 'if':
+            self.cached_inp_features += [self._cache(x)]
+        residual = x if self.downsample is None else self.downsample(x)
+        out = self.conv1(x)
+        out = self.conv2(out)
+        out = out + residual
+        out = self._finish(out)
+        if self.cache_features == 'of':
+            self.cached_out_features += [self._cache(out)]
+        return out
+
+    def toggleHardTarget(self):
+        for m in (self.conv1, self.conv2, self.downsample):
+            if m is not None:
+                m.weight_quantizer.hard_targets = not m.weight_quantizer.hard_targets
+
+
+class QuantBottleneck(BaseQuantBlock):
+    """ResNet-50 block (quant_block.py:133-166)."""
+
+    def __init__(self, bottleneck, weight_quant_params: dict = {}, act_quant_params: dict = {}):
+        super().__init__(act_quant_params)
+        self.conv1 = QuantModule(bottleneck.conv1, weight_quant_params, act_quant_params)
+        self.conv1.activation_function = bottleneck.relu1
+        self.conv2 = QuantModule(bottleneck.conv2, weight_quant_params, act_quant_params)
+        self.conv2.activation_function = bottleneck.relu2
+        self.conv3 = QuantModule(bottleneck.conv3, weight_quant_params, act_quant_params,
+                                 disable_act_quant=True)
+        self.activation_function = bottleneck.relu3
+        self.downsample = None if bottleneck.downsample is None else QuantModule(
+            bottleneck.downsample[0], weight_quant_params, act_quant_params, disable_act_quant=True)
+        self.stride = bottleneck.stride
+
+    def forward(self, x):
+        if self.cache_features == 'if':
+            self.cached_inp_features += [self._cache(x)]
+        residual = x if self.downsample is None else self.downsample(x)
+        out = self.conv3(self.conv2(self.conv1(x)))
+        out = self._finish(out + residual)
+        if self.cache_features == 'of':
+            self.cached_out_features += [self._cache(out)]
+        return out
+
+
+class QuantResBottleneckBlock(BaseQuantBlock):
+    """RegNetX block without SE (quant_block.py:169-202): f.a / f.b / f.c + optional proj."""
+
+    def __init__(self, bottleneck, weight_quant_params: dict = {}, act_quant_params: dict = {}):
+        super().__init__(act_quant_params)
+        self.conv1 = QuantModule(bottleneck.f.a, weight_quant_params, act_quant_params)
+        self.conv1.activation_function = bottleneck.f.a_relu
+        self.conv2 = QuantModule(bottleneck.f.b, weight_quant_params, act_quant_params)
+        self.conv2.activation_function = bottleneck.f.b_relu
+        self.conv3 = QuantModule(bottleneck.f.c, weight_quant_params, act_quant_params,
+                                 disable_act_quant=True)
+        self.activation_function = bottleneck.relu
+        self.downsample = QuantModule(bottleneck.proj, weight_quant_params, act_quant_params,
+                                      disable_act_quant=True) if bottleneck.proj_block else None
+        self.proj_block = bottleneck.proj_block
+
+    def forward(self, x):
+        if self.cache_features == 'if':
+            self.cached_inp_features += [self._cache(x)]
+        residual = self.downsample(x) if self.proj_block else x
+        out = self.conv3(self.conv2(self.conv1(x)))
+        out = self._finish(out + residual)
+        if self.cache_features == 'of':
+            self.cached_out_features += [self._cache(out)]
+        return out
+
+
+class QuantInvertedResidual(BaseQuantBlock):
+    """MobileNetV2 block (quant_block.py:205-239); no activation after the residual add."""
+
+    def __init__(self, inv_res, weight_quant_params: dict = {}, act_quant_params: dict = {}):
+        super().__init__(act_quant_params)
+        self.use_res_connect = inv_res.use_res_connect
+        self.expand_ratio = inv_res.expand_ratio
+        if self.expand_ratio == 1:
+            self.conv = nn.Sequential(
+                QuantModule(inv_res.conv[0], weight_quant_params, act_quant_params),
+                QuantModule(inv_res.conv[3], weight_quant_params, act_quant_params,
+                            disable_act_quant=True))
+            self.conv[0].activation_function = nn.ReLU6()
+        else:
+            self.conv = nn.Sequential(
+                QuantModule(inv_res.conv[0], weight_quant_params, act_quant_params),
+                QuantModule(inv_res.conv[3], weight_quant_params, act_quant_params),
+                QuantModule(inv_res.conv[6], weight_quant_params, act_quant_params,
+                            disable_act_quant=True))
+            self.conv[0].activation_function = nn.ReLU6()
+            self.conv[1].activation_function = nn.ReLU6()
+
+    def forward(self, x):
+        if self.cache_features == 'if':
+            self.cached_inp_features += [self._cache(x)]
+        out = x + self.conv(x) if self.use_res_connect else self.conv(x)
+        out = self._finish(out)
+        if self.cache_features == 'of':
+            self.cached_out_features += [self._cache(out)]
+        return out
+
+
+specials = {
+    nets.BasicBlock: QuantBasicBlock,
+    nets.Bottleneck: QuantBottleneck,
+    nets.InvertedResidual: QuantInvertedResidual,
+}
+
+
+def register_block(fp_block_type, quant_block_type):
+    """Map another FP block class (e.g. a model zoo's own BasicBlock) to a quant block."""
+    specials[fp_block_type] = quant_block_type

@@ -1,0 +1,212 @@
+"""UniformAffineQuantizer and QuantModule (reference: quant/quant_layer.py).
+
+Same class names, constructor arguments, attributes and forward semantics as the
+reference; the arithmetic runs in the HIP kernels of libssq.so:
+  * UniformAffineQuantizer.forward        -> ssq_fq_fwd / ssq_fq_bwd (K1/K2)
+  * UniformAffineQuantizer.init_quantization_scale -> ssq_scale_init (K3/K4; no per-channel
+    Python loop, no .item() syncs)
+  * lp_loss                               -> ssq_lp_loss (K11)
+Feature caching keeps tensors on the device by default (the reference moves every batch
+to the host with .cpu(); quant_layer.py:247,278) -- identical values, no PCIe round trip.
+"""
+from typing import Union
+
+import torch
+import torch.nn as nn
+import torch.nn.functional as F
+
+from .. import kernels as K
+
+
+class StraightThrough(nn.Module):
+    """quant_layer.py:10-15."""
+
+    def __init__(self, channel_num: int = 1):
+        super().__init__()
+
+    def forward(self, input):
+        return input
+
+
+def round_ste(x: torch.Tensor):
+    """quant_layer.py:18-22 (API mirror; the q/dq kernels fold it in)."""
+    return (x.round() - x).detach() + x
+
+
+def lp_loss(pred, tgt, p=2.0, reduction='none'):
+    """quant_layer.py:25-32: (pred-tgt).abs().pow(p).sum(1).mean() ('none') or .mean()."""
+    return K.lp_loss(pred, tgt, p, reduction)
+
+
+class UniformAffineQuantizer(nn.Module):
+    """quant_layer.py:35-185.  Asymmetric/symmetric fake quantization, per tensor or per
+    output channel; delta/zero_point initialised by 'max' or the 80-candidate 'mse' search."""
+
+    def __init__(self, n_bits: int = 8, symmetric: bool = False, channel_wise: bool = False,
+                 scale_method: str = 'max', leaf_param: bool = False, tune_delta_zero: bool = False,
+                 ch: int = 64, disable_act_quant: bool = False):
+        super().__init__()
+        self.sym = symmetric
+        assert 1 <= n_bits <= 8, 'bitwidth not supported'
+        self.n_bits = n_bits
+        self.n_levels = 2 ** self.n_bits
+        self.delta = None
+        self.zero_point = None
+        self.raw_zero_point = None
+        self.inited = False
+        self.leaf_param = leaf_param
+        self.channel_wise = channel_wise
+        self.scale_method = scale_method
+        self.disable_act_quant = disable_act_quant
+        if not tune_delta_zero and not disable_act_quant:
+            if leaf_param:
+                self.delta = nn.Parameter(torch.tensor(0.0))
+                self.zero_point = nn.Parameter(torch.tensor(0.0))
+            elif type(ch) is int:
+                self.delta = nn.Parameter(torch.zeros(size=(ch, 1)))
+                self.zero_point = nn.Parameter(torch.zeros(size=(ch, 1)))
+            elif len(ch) == 2:
+                self.delta = nn.Parameter(torch.zeros(size=(ch[0], 1)))
+                self.zero_point = nn.Parameter(torch.zeros(size=(ch[0], 1)))
+            else:
+                self.delta = nn.Parameter(torch.zeros(size=(ch[0], 1, 1, 1)))
+                self.zero_point = nn.Parameter(torch.zeros(size=(ch[0], 1, 1, 1)))
+
+    def forward(self, x: torch.Tensor):
+        if self.inited is False:
+            delta, zero_point, self.raw_zero_point = self.init_quantization_scale(x, self.channel_wise)
+            self.delta = nn.Parameter(delta)
+            self.zero_point = nn.Parameter(zero_point)
+            self.inited = True
+        return K.fake_quant(x, self.delta, self.zero_point, self.n_bits, self.sym)
+
+    @torch.no_grad()
+    def init_quantization_scale(self, x: torch.Tensor, channel_wise: bool = False):
+        """quant_layer.py:100-166 on the device.  For per-tensor 'max' the reference returns
+        a Python int zero point that nn.Parameter rejects (quant_layer.py:88,140); the
+        evident intent (a 0-dim tensor) is implemented here."""
+        d, z, r = K.scale_init(x, self.n_bits, self.sym, channel_wise, self.scale_method)
+        return d.clone(), z.clone(), r.clone()
+
+    def quantize(self, x, max, min):
+        """quant_layer.py:168-175 (API mirror, used only for inspection)."""
+        delta = (max - min) / (2 ** self.n_bits - 1)
+        zero_point = (- min / delta).round()
+        x_int = torch.round(x / delta)
+        x_quant = torch.clamp(x_int + zero_point, 0, self.n_levels - 1)
+        return (x_quant - zero_point) * delta
+
+    def bitwidth_refactor(self, refactored_bit: int):
+        assert 2 <= refactored_bit <= 8, 'bitwidth not supported'
+        self.n_bits = refactored_bit
+        self.n_levels = 2 ** self.n_bits
+
+    def extra_repr(self):
+        s = 'bit={n_bits}, scale_method={scale_method}, symmetric={sym}, channel_wise={channel_wise},' \
+            ' leaf_param={leaf_param}'
+        return s.format(**self.__dict__)
+
+
+class QuantModule(nn.Module):
+    """quant_layer.py:188-280: a Conv2d / Linear whose weight goes through
+    `weight_quantizer` (any module: UAQ, ChannelQuant, AdaRoundQuantizer, ...), followed by
+    the output-channel affine gamma^z=alpha_out / phi^z=beta_out, the activation and the
+    activation quantizer.  The research-only greedy search methods (quant_layer.py:325-528)
+    are out of scope."""
+
+    def __init__(self, org_module: Union[nn.Conv2d, nn.Linear], weight_quant_params: dict = {},
+                 act_quant_params: dict = {}, disable_act_quant: bool = False, se_module=None):
+        super().__init__()
+        if isinstance(org_module, nn.Conv2d):
+            self.fwd_kwargs = dict(stride=org_module.stride, padding=org_module.padding,
+                                   dilation=org_module.dilation, groups=org_module.groups)
+            self.fwd_func = F.conv2d
+        else:
+            self.fwd_kwargs = dict()
+            self.fwd_func = F.linear
+        self.weight = org_module.weight
+        self.org_weight = org_module.weight.data.clone()
+        if org_module.bias is not None:
+            self.bias = org_module.bias
+            self.org_bias = org_module.bias.data.clone()
+        else:
+            self.bias = None
+            self.org_bias = None
+        self.use_weight_quant = False
+        self.use_act_quant = False
+        self.disable_act_quant = disable_act_quant
+        weight_quant_params = dict(weight_quant_params)
+        weight_quant_params['ch'] = self.weight.shape
+        self.weight_quantizer = UniformAffineQuantizer(**weight_quant_params)
+        act_quant_params = dict(act_quant_params)
+        act_quant_params['disable_act_quant'] = disable_act_quant
+        self.act_quantizer = UniformAffineQuantizer(**act_quant_params)
+
+        self.activation_function = StraightThrough()
+        self.ignore_reconstruction = False
+        self.se_module = se_module
+        self.extra_repr = org_module.extra_repr
+
+        self.cache_features = 'none'
+        self.cached_inp_features = []
+        self.cached_out_features = []
+        self.cache_to_host = False      # True: reference behaviour (.cpu() per batch)
+
+        n_ch = self.weight.shape[0]
+        if self.weight.dim() == 4:
+            self.alpha_out = nn.Parameter(torch.ones(n_ch).view(1, n_ch, 1, 1))
+            self.beta_out = nn.Parameter(torch.zeros(n_ch).view(1, n_ch, 1, 1))
+        else:
+            self.alpha_out = nn.Parameter(torch.ones(n_ch).view(1, n_ch))
+            self.beta_out = nn.Parameter(torch.zeros(n_ch).view(1, n_ch))
+        self.selection = None
+        self.selectionInited = False
+        self.pathName = ''
+
+    def _cache(self, t):
+        t = t.detach()
+        return t.cpu().clone() if self.cache_to_host else t.clone()
+
+    def forward(self, input: torch.Tensor):
+        if self.cache_features == 'if':
+            self.cached_inp_features += [self._cache(input)]
+        if self.use_weight_quant and self.cache_features == 'none':
+            weight = self.weight_quantizer(self.weight)
+            bias = self.bias
+        else:
+            weight = self.org_weight
+            bias = self.org_bias
+        out = self.fwd_func(input, weight, bias, **self.fwd_kwargs)
+        if self.use_weight_quant and self.cache_features == 'none':
+            out = out * self.alpha_out + self.beta_out
+        if self.se_module is not None:
+            out = self.se_module(out)
+        out = self.activation_function(out)
+        if not self.disable_act_quant:
+            if self.use_act_quant:
+                out = self.act_quantizer(out)
+        if self.cache_features == 'of':
+            self.cached_out_features += [self._cache(out)]
+        return out
+
+    def set_quant_init_state(self):
+        self.weight_quantizer.inited = True
+        self.act_quantizer.inited = True
+
+    def set_quant_state(self, weight_quant: bool = False, act_quant: bool = False):
+        self.use_weight_quant = weight_quant
+        self.use_act_quant = act_quant
+
+    def disable_cache_features(self):
+        self.cache_features = 'none'
+
+    def clear_cached_features(self):
+        self.cached_inp_features = []
+        self.cached_out_features = []
+
+    def getLoss(self, A, B, p=2.0):
+        """quant_layer.py:319-323 (host-side report)."""
+        loss = 0.0
+        for i in range(len(B)):
+            loss += lp_loss(A[i], B[i], p).detach()
+        return float(loss)

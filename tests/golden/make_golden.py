@@ -566,6 +566,12 @@ def gen_recon_brecq(iters=10, n_cali=16, res=16):
     block = qnn.model[3]
     out = {"cali": t2n(cali)}
     _dump_block(out, block)
+    qms = [m for m in qnn.modules() if isinstance(m, QuantModule)]
+    for k, m in enumerate(qms):   # whole-network state: asym capture runs the stem too
+        out[f"qm{k}_w"], out[f"qm{k}_b"] = t2n(m.org_weight), t2n(m.org_bias)
+        out[f"qm{k}_delta"] = t2n(m.weight_quantizer.delta.reshape(-1))
+        out[f"qm{k}_zp"] = t2n(m.weight_quantizer.zero_point.reshape(-1))
+        out[f"qm{k}_bits"] = np.array([m.weight_quantizer.n_bits])
     for n in CONVS:
         q = getattr(block, n).weight_quantizer
         out[n + "_delta"] = t2n(q.delta.reshape(-1))
@@ -581,6 +587,22 @@ def gen_recon_brecq(iters=10, n_cali=16, res=16):
         out[n + "_alpha"] = t2n(m.weight_quantizer.alpha)
         with torch.no_grad():
             out[n + "_what_hard"] = t2n(m.weight_quantizer(m.weight))
+    # act phase (Brecq/main_imagenet.py:231-241): act-delta init on 8 samples, then LSQ recon
+    qnn.set_quant_state(True, True)
+    with torch.no_grad():
+        qnn(cali[:8])
+    qnn.disable_network_output_quantization()
+    aqs = [block.act_quantizer] + [m.act_quantizer for m in (block.conv1, block.conv2, block.downsample)
+                                   if m.act_quantizer.delta is not None]
+    out["a_delta0"] = np.array([float(q.delta) for q in aqs], np.float32)
+    out["a_zp0"] = np.array([float(q.zero_point) for q in aqs], np.float32)
+    torch.manual_seed(1005)
+    with _Spy(BR.LossFunction) as spy:
+        BR.block_reconstruction(qnn, block, cali, batch_size=8, iters=iters, act_quant=True,
+                                opt_mode="mse", lr=4e-4, p=2.4)
+    out["a_perms"] = np.stack([p.numpy() for p in spy.perms]).astype(np.int64)
+    out["a_total_loss"] = np.array([r[1] for r in spy.rec], np.float64)
+    out["a_delta"] = np.array([float(q.delta) for q in aqs], np.float32)
     save("recon_brecq", **out)
 
 

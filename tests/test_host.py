@@ -1,0 +1,150 @@
+"""CPU-side checks: the C ABI library loads and exports every declared symbol, the
+host-side schedules / argument handling mirror the reference, the product path refuses
+CPU tensors (no silent fallback), and the data-parallel bucket all-reduce (gloo, 2 ranks)."""
+import os
+import re
+import socket
+
+import numpy as np
+import pytest
+import torch
+import torch.multiprocessing as mp
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def declared_symbols():
+    src = open(os.path.join(ROOT, "include", "ssq.h")).read()
+    src = re.sub(r"/\*.*?\*/", "", src, flags=re.S)
+    return sorted(set(re.findall(r"\b(ssq_[a-z0-9_]+)\s*\(", src)))
+
+
+def test_header_declares_abi():
+    syms = declared_symbols()
+    for s in ("ssq_fq_fwd", "ssq_fq_bwd", "ssq_scale_init", "ssq_adashift_fwd", "ssq_adashift_bwd",
+              "ssq_shift_init", "ssq_lp_loss", "ssq_gather_rows2", "ssq_inpscale_search"):
+        assert s in syms
+
+
+def test_library_exports_every_declared_symbol():
+    from shiftedscalequantization_amd import _capi
+    lib = _capi.load()
+    missing = [s for s in declared_symbols() if not hasattr(lib, s)]
+    assert not missing, missing
+    # every declared symbol has a ctypes signature, and vice versa
+    assert set(declared_symbols()) == set(_capi.SIGNATURES)
+    assert lib.ssq_version() == 1
+    assert lib.ssq_fq_bwd_workspace_size(10, 1, 1) > 0
+
+
+def test_abi_argument_errors_without_gpu():
+    """Argument validation happens on the host before any launch."""
+    from shiftedscalequantization_amd import _capi
+    lib = _capi.load()
+    rc = lib.ssq_fq_fwd(None, None, None, None, None, 16, 1, 1, 1.0, 0, 3, None)
+    assert rc == -1
+    assert b"null" in lib.ssq_last_error()
+    rc = lib.ssq_fq_fwd(None, None, None, None, None, 16, 1, 1, 1.0, 3, 3, None)
+    assert rc == -1 and b"qmin" in lib.ssq_last_error()
+
+
+def test_product_path_refuses_cpu_tensors():
+    from shiftedscalequantization_amd import kernels as K
+    from shiftedscalequantization_amd._capi import SSQError
+    x = torch.randn(4, 4)
+    with pytest.raises(SSQError):
+        K.fake_quant_fwd(x, torch.tensor(0.1), torch.tensor(0.0), 4)
+
+
+def test_schedules_match_reference(golden):
+    from shiftedscalequantization_amd.quant.block_recon import LinearTempDecay
+    from shiftedscalequantization_amd.quant.layer_recon_fused_shiftedScale import FusedLinearTempDecayShift
+    from shiftedscalequantization_amd.quant.layer_recon_shiftedScale import LinearTempDecayShift
+    g = golden("loss")
+    f = FusedLinearTempDecayShift(100, 0.2, 20, 2)
+    fs = FusedLinearTempDecayShift(100 * 3 / 4, 0.2, 20, 2)
+    lin = LinearTempDecay(100, 0.2, 20, 2)
+    lsh = LinearTempDecayShift(100, 0.2, 20, 2)
+    for t in g["sched_t"]:
+        t = int(t)
+        assert f(t) == g["sched_fused"][t]
+        assert fs(t) == g["sched_fused_shift"][t]
+        assert lin(t) == g["sched_lin"][t]
+        assert lsh(t) == g["sched_lsh"][t]
+
+
+def test_quant_model_structure_resnet18():
+    """QuantModel wraps the 21 conv/fc layers, 8 BasicBlocks, sets 8-bit stem/head and
+    path names exactly as the reference (quant_model.py:15-69)."""
+    from shiftedscalequantization_amd import nets
+    from shiftedscalequantization_amd.quant import QuantBasicBlock, QuantModel, QuantModule
+    torch.manual_seed(0)
+    qnn = QuantModel(nets.resnet18(), {"n_bits": 2, "channel_wise": True, "scale_method": "max"},
+                     {"n_bits": 4, "channel_wise": False, "scale_method": "mse", "leaf_param": True})
+    qms = [m for m in qnn.modules() if isinstance(m, QuantModule)]
+    assert len(qms) == 21
+    assert sum(m.weight.numel() for m in qms) == 11678912
+    assert len([m for m in qnn.modules() if isinstance(m, QuantBasicBlock)]) == 8
+    qnn.set_first_last_layer_to_8bit()
+    assert qms[0].weight_quantizer.n_bits == 8 and qms[-1].weight_quantizer.n_bits == 8
+    assert qms[0].ignore_reconstruction
+    assert qnn.model.layer2[0].pathName == ".layer2.0"
+    assert qnn.model.layer2[0].downsample.pathName == ".layer2.0.downsample"
+
+
+@pytest.mark.parametrize("arch,nq", [("resnet50", 54), ("mobilenetv2", 53)])
+def test_quant_model_other_archs(arch, nq):
+    """The reference crashes here (setPathName missing on non-basic blocks)."""
+    from shiftedscalequantization_amd import nets
+    from shiftedscalequantization_amd.quant import QuantModel, QuantModule
+    qnn = QuantModel(nets.ARCHS[arch](), {"n_bits": 2, "channel_wise": True, "scale_method": "max"},
+                     {"n_bits": 4, "channel_wise": False, "scale_method": "mse", "leaf_param": True})
+    assert len([m for m in qnn.modules() if isinstance(m, QuantModule)]) == nq
+
+
+def test_driver_flag_parsing():
+    from shiftedscalequantization_amd.cli import parse_args
+    a = parse_args(["--arch", "resnet18", "--n_bits_w", "2", "--n_bits_a", "4", "--bias_cal=True",
+                    "--bias_ch_quant=True", "--weight=1.0", "--device_gpu=0"])
+    assert a.bias_cal and a.bias_ch_quant and a.weight == 1.0 and a.n_bits_w == 2
+    # the reference's argparse type=bool quirk: any non-empty string is True
+    b = parse_args(["--bias_cal=False"])
+    assert b.bias_cal is True
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _dp_worker(rank, world, port, out):
+    import torch.distributed as dist
+    from shiftedscalequantization_amd.parallel_dp import GradBucket, shard_rows
+    dist.init_process_group("gloo", init_method=f"tcp://127.0.0.1:{port}", rank=rank, world_size=world)
+    a = torch.nn.Parameter(torch.zeros(3, 4))
+    b = torch.nn.Parameter(torch.zeros(5))
+    a.grad = torch.full((3, 4), float(rank + 1))
+    b.grad = torch.arange(5, dtype=torch.float32) * (rank + 1)
+    GradBucket([a, b], average=False).allreduce_()
+    c = torch.nn.Parameter(torch.zeros(2))
+    c.grad = torch.full((2,), float(rank))
+    GradBucket([c], average=True).allreduce_()
+    out[rank] = (a.grad.clone(), b.grad.clone(), c.grad.clone(), shard_rows(1024))
+    dist.destroy_process_group()
+
+
+def test_grad_bucket_allreduce_gloo():
+    world = 2
+    port = _free_port()
+    mgr = mp.Manager()
+    out = mgr.dict()
+    mp.spawn(_dp_worker, args=(world, port, out), nprocs=world, join=True)
+    for r in range(world):
+        a, b, c, sh = out[r]
+        assert torch.equal(a, torch.full((3, 4), 3.0))          # sum of 1 and 2
+        assert torch.equal(b, torch.arange(5, dtype=torch.float32) * 3)
+        assert torch.equal(c, torch.full((2,), 0.5))            # average of 0 and 1
+    assert out[0][3] == (0, 512) and out[1][3] == (512, 1024)

@@ -1,0 +1,193 @@
+"""Reconstruction loops on the GPU against the reference's own trajectories
+(tests/golden/recon_*.npz, produced by make_golden.py from the reference on CPU).
+
+The loops are seeded exactly like the reference (torch.manual_seed(1005), CPU randperm),
+so every batch drawn is identical (checked); per-iteration losses and the learned
+parameters then agree up to conv/summation rounding (MIOpen vs mkldnn), which is what
+the tolerances below bound.  Hard decisions that ride on near-ties of two shift
+probabilities may flip: their count is bounded explicitly.
+"""
+import numpy as np
+import pytest
+import torch
+import torch.nn as nn
+
+pytestmark = pytest.mark.gpu
+SHIFTS = [31 / 32, 33 / 32, 1.0]
+
+
+@pytest.fixture(scope="module")
+def Q():
+    if not torch.cuda.is_available():
+        pytest.skip("no HIP device")
+    from shiftedscalequantization_amd import quant
+    return quant
+
+
+def dev(a):
+    return torch.as_tensor(np.asarray(a)).cuda()
+
+
+def tiny_net():
+    """Same topology as make_golden._tiny_net (weights are loaded from the fixture)."""
+    from shiftedscalequantization_amd import nets
+    ds = nn.Sequential(nn.Conv2d(16, 32, 1, stride=2, bias=False), nn.BatchNorm2d(32))
+    return nn.Sequential(nn.Conv2d(3, 16, 3, padding=1, bias=False), nn.BatchNorm2d(16), nn.ReLU(),
+                         nets.BasicBlock(16, 32, stride=2, downsample=ds),
+                         nn.AdaptiveAvgPool2d(1), nn.Flatten(), nn.Linear(32, 10)).eval()
+
+
+def build_qnn(Q, g, bits_w=2, bits_a=4):
+    wq = {"n_bits": bits_w, "channel_wise": True, "scale_method": "max"}
+    aq = {"n_bits": bits_a, "channel_wise": False, "scale_method": "mse", "leaf_param": True}
+    qnn = Q.QuantModel(tiny_net(), wq, aq).cuda().eval()
+    qnn.set_first_last_layer_to_8bit()
+    qms = [m for m in qnn.modules() if isinstance(m, Q.QuantModule)]
+    for k, m in enumerate(qms):
+        if f"qm{k}_w" not in g:
+            continue
+        w, b = dev(g[f"qm{k}_w"]), dev(g[f"qm{k}_b"])
+        m.org_weight = w.clone()
+        m.weight.data = w.clone()
+        m.org_bias = b.clone()
+        m.bias.data = b.clone()
+        shape = (-1,) + (1,) * (w.dim() - 1)
+        m.weight_quantizer.delta = nn.Parameter(dev(g[f"qm{k}_delta"]).view(shape))
+        m.weight_quantizer.zero_point = nn.Parameter(dev(g[f"qm{k}_zp"]).view(shape))
+        m.weight_quantizer.inited = True
+    return qnn
+
+
+def load_block(Q, g, block):
+    for n in ("conv1", "conv2", "downsample"):
+        m = getattr(block, n)
+        w, b = dev(g[n + "_w"]), dev(g[n + "_b"])
+        m.org_weight, m.org_bias = w.clone(), b.clone()
+        m.weight.data = w.clone()
+        m.bias = nn.Parameter(b.clone())
+        uaq = Q.UniformAffineQuantizer(n_bits=2, channel_wise=True, ch=w.shape).cuda()
+        uaq.delta = nn.Parameter(dev(g[n + "_delta"]).view(-1, 1, 1, 1))
+        uaq.zero_point = nn.Parameter(dev(g[n + "_zp"]).view(-1, 1, 1, 1))
+        uaq.inited = True
+        m.weight_quantizer = Q.ChannelQuant(1.0, uaq=uaq, weight_tensor=m.org_weight, shiftTarget=SHIFTS,
+                                            name="." + n)
+        m.use_weight_quant = True
+
+
+def test_block_recon_fused_matches_reference(Q, golden):
+    g = golden("recon_fused")
+    qnn = build_qnn(Q, {})
+    block = qnn.model[3]
+    load_block(Q, g, block)
+    block.cached_inp_features = [dev(g["cached_inp"])]
+    block.cached_out_features = [dev(g["cached_out"])]
+    iters = int(g["iters"][0])
+
+    from shiftedscalequantization_amd.quant import layer_recon_fused_shiftedScale as LRF
+    seen_perms, seen_rec = [], []
+    orig_draw = LRF.BatchFeeder.draw
+    orig_fused = LRF.FusedScaleLossFunction.fused
+
+    def draw(self):
+        p = orig_draw(self)
+        seen_perms.append(p.clone())
+        return p
+
+    def fused(self, pred, tgt):
+        r = orig_fused(self, pred, tgt)
+        seen_rec.append(r)
+        return r
+
+    LRF.BatchFeeder.draw, LRF.FusedScaleLossFunction.fused = draw, fused
+    try:
+        torch.manual_seed(1005)
+        res = LRF.block_recon_fused_shiftedScale(block, iters, (0.01, 0.1), qnn, None, verbose=False)
+    finally:
+        LRF.BatchFeeder.draw, LRF.FusedScaleLossFunction.fused = orig_draw, orig_fused
+    # identical batches (same CPU RNG stream as the reference)
+    np.testing.assert_array_equal(np.stack([p.numpy() for p in seen_perms]), g["perms"])
+    rec = np.array([float(r.item()) for r in seen_rec])
+    np.testing.assert_allclose(rec, g["rec_loss"][:iters], rtol=2e-4)
+    np.testing.assert_allclose(res, g["final_losses"], rtol=5e-3)
+    for n in ("conv1", "conv2", "downsample"):
+        q = getattr(block, n).weight_quantizer
+        np.testing.assert_allclose(q.alpha.detach().cpu().numpy(), g[n + "_alpha"], atol=2e-4)
+        np.testing.assert_allclose(q.beta.detach().cpu().numpy(), g[n + "_beta0"], rtol=1e-5, atol=1e-5)
+        with torch.no_grad():
+            what = q(getattr(block, n).weight).cpu().numpy()
+        mism = np.mean(what != g[n + "_what_hard"])
+        assert mism <= 0.01, f"{n}: {mism:.4f} of hard weights differ"
+
+
+def test_layer_recon_shiftedScale_matches_reference(Q, golden):
+    g = golden("recon_layer_shift")
+    qnn = build_qnn(Q, {}, bits_w=4, bits_a=8)
+    m = qnn.model[3].conv1
+    w, b = dev(g["w"]), dev(g["b"])
+    m.org_weight, m.org_bias = w.clone(), b.clone()
+    m.weight.data = w.clone()
+    m.bias = nn.Parameter(b.clone())
+    uaq = Q.UniformAffineQuantizer(n_bits=4, channel_wise=True, ch=w.shape).cuda()
+    uaq.delta = nn.Parameter(dev(g["delta"]).view(-1, 1, 1, 1))
+    uaq.zero_point = nn.Parameter(dev(g["zp"]).view(-1, 1, 1, 1))
+    uaq.inited = True
+    m.weight_quantizer = Q.ChannelQuant(1.0, uaq=uaq, weight_tensor=w, shiftTarget=SHIFTS, name="c1")
+    m.use_weight_quant = True
+    m.cached_inp_features = [dev(g["cached_inp"])]
+    m.cached_out_features = [dev(g["cached_out"])]
+    iters = int(g["iters"][0])
+    torch.manual_seed(1005)
+    l1 = Q.layer_recon_shiftedScale(m, iters, 0.1, qnn, None, verbose=False)
+    np.testing.assert_allclose(l1, g["shift_final"], rtol=5e-3)
+    np.testing.assert_allclose(m.weight_quantizer.alpha.detach().cpu().numpy(), g["shift_alpha"], atol=2e-4)
+    m.weight_quantizer.hard_targets = False
+    l2 = Q.layer_recon_shiftedScale(m, iters, 0.01, qnn, None, adaround=True, verbose=False)
+    np.testing.assert_allclose(l2, g["ar_final"], rtol=5e-3)
+    d = m.weight_quantizer.delta.detach().cpu().numpy()
+    assert np.mean(d != g["ar_delta"]) <= 0.02
+    np.testing.assert_allclose(m.weight_quantizer.beta.detach().cpu().numpy(), g["ar_beta"], atol=5e-3)
+
+
+def test_brecq_block_reconstruction_matches_reference(Q, golden):
+    g = golden("recon_brecq")
+    qnn = build_qnn(Q, g)
+    block = qnn.model[3]
+    cali = dev(g["cali"])
+    from shiftedscalequantization_amd.quant import block_recon as BR
+    seen = []
+    orig = BR.LossFunction.__call__
+
+    def spy(self, pred, tgt, grad=None):
+        r = orig(self, pred, tgt, grad)
+        seen.append(float(r.item()))
+        return r
+
+    BR.LossFunction.__call__ = spy
+    try:
+        torch.manual_seed(1005)
+        Q.block_reconstruction(qnn, block, cali, batch_size=8, iters=len(g["w_total_loss"]),
+                               weight=0.01, asym=True, b_range=(20, 2), warmup=0.2,
+                               act_quant=False, opt_mode="mse")
+        np.testing.assert_allclose(seen, g["w_total_loss"], rtol=2e-4)
+        for n in ("conv1", "conv2", "downsample"):
+            q = getattr(block, n).weight_quantizer
+            np.testing.assert_allclose(q.alpha.detach().cpu().numpy(), g[n + "_alpha"], atol=1e-4)
+            with torch.no_grad():
+                what = q(getattr(block, n).weight).cpu().numpy()
+            assert np.mean(what != g[n + "_what_hard"]) <= 0.002
+        # act phase
+        qnn.set_quant_state(True, True)
+        with torch.no_grad():
+            qnn(cali[:8])
+        qnn.disable_network_output_quantization()
+        aqs = [block.act_quantizer] + [m.act_quantizer for m in (block.conv1, block.conv2, block.downsample)
+                                       if m.act_quantizer.delta is not None]
+        np.testing.assert_allclose([float(q.delta) for q in aqs], g["a_delta0"], rtol=1e-6)
+        seen.clear()
+        torch.manual_seed(1005)
+        Q.block_reconstruction(qnn, block, cali, batch_size=8, iters=len(g["a_total_loss"]),
+                               act_quant=True, opt_mode="mse", lr=4e-4, p=2.4)
+        np.testing.assert_allclose(seen, g["a_total_loss"], rtol=1e-4)
+        np.testing.assert_allclose([float(q.delta) for q in aqs], g["a_delta"], rtol=1e-5)
+    finally:
+        BR.LossFunction.__call__ = orig
