@@ -42,7 +42,7 @@ def _weight_quantizers(module):
 
 
 def _fused_loop(block, modules, iters, lmda, model, p, lr, bias_cal, batch_size, dp_average,
-                verbose):
+                verbose, iter_hook=None):
     device = next(model.parameters()).device
     quantizers, opt_params = [], []
     for m in modules:
@@ -70,6 +70,8 @@ def _fused_loop(block, modules, iters, lmda, model, p, lr, bias_cal, batch_size,
     start_loss = 0.0
     t = tqdm(range(iters), desc='', dynamic_ncols=True, disable=not verbose)
     for i in t:
+        if iter_hook is not None:
+            iter_hook(i)
         cur_inp, cur_out = feeder.next()
         optimizer.zero_grad()
         loss_func.arm()
@@ -84,6 +86,8 @@ def _fused_loop(block, modules, iters, lmda, model, p, lr, bias_cal, batch_size,
             t.set_description(f"{start_loss:.6f} -> {as_float(loss_func.rec_loss):.6f} "
                               f"{loss_func.round_loss_val} ")
     loss_func.disarm()
+    if iter_hook is not None:
+        iter_hook(iters)
 
     rec_loss_out = []
     cur_inp, cur_out = feeder.head(batch_size)
@@ -115,7 +119,7 @@ def _fused_loop(block, modules, iters, lmda, model, p, lr, bias_cal, batch_size,
 def block_recon_fused_shiftedScale(block: BaseQuantBlock, iters: int = 20000, lmda: list = [1., 1.],
                                    model=None, test_loader=None, act=False, adaround=False,
                                    useShiftedScale=True, bias_cal=False, batch_size=32,
-                                   dp_average=False, verbose=True):
+                                   dp_average=False, verbose=True, iter_hook=None):
     """layer_recon_fused_shiftedScale.py:23-141 -> [soft rec loss, hard rec loss]."""
     if act:
         # the reference's act branch builds ChannelQuantAct and calls its init_v, which
@@ -123,7 +127,7 @@ def block_recon_fused_shiftedScale(block: BaseQuantBlock, iters: int = 20000, lm
         raise NotImplementedError("block_recon_fused_shiftedScale(act=True) is broken in the reference")
     block.train()
     return _fused_loop(block, _weight_quantizers(block), iters, lmda, model, 2.0, 0.001, bias_cal,
-                       batch_size, dp_average, verbose)
+                       batch_size, dp_average, verbose, iter_hook)
 
 
 def layer_recon_fused_shiftedScale(layer: QuantModule, iters: int = 20000, lmda: list = [1., 1.],

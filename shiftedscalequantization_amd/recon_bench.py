@@ -1,0 +1,80 @@
+"""Reconstruction-iteration benchmark used by bench.py (the "recon iters/s" half of the
+BASELINE metric): block_recon_fused_shiftedScale on ResNet-18 blocks, batch 32 per rank,
+W2 shifted-scale (S=3 shifts [31/32, 33/32, 1]), lmda (0.01, 0.1), cached features of
+1024 synthetic calibration samples per rank, gradients all-reduced over RCCL for N > 1.
+"""
+import time
+
+import torch
+
+from . import nets
+from .quant import ChannelQuant, QuantModel, QuantModule
+from .quant.layer_recon_fused_shiftedScale import block_recon_fused_shiftedScale
+
+SHIFTS = [31 / 32, 33 / 32, 1.0]
+# block -> (input shape per sample)
+BLOCKS = {"layer1.0": (64, 56, 56), "layer2.0": (64, 56, 56), "layer3.0": (128, 28, 28),
+          "layer4.0": (256, 14, 14)}
+
+
+def _block(qnn, name):
+    m = qnn.model
+    for part in name.split("."):
+        m = m[int(part)] if part.isdigit() else getattr(m, part)
+    return m
+
+
+def run_block(dev, name, n_cali=1024, iters=200, warmup=20, rank=0):
+    torch.manual_seed(1005 + rank)
+    cnn = nets.resnet18().to(dev).eval()
+    qnn = QuantModel(cnn, {"n_bits": 2, "channel_wise": True, "scale_method": "max"},
+                     {"n_bits": 4, "channel_wise": False, "scale_method": "mse", "leaf_param": True})
+    qnn.to(dev).eval()
+    qnn.set_first_last_layer_to_8bit()
+    block = _block(qnn, name)
+    for m in block.modules():
+        if isinstance(m, QuantModule):
+            m.weight_quantizer.channel_wise = True
+            with torch.no_grad():
+                m.weight_quantizer(m.org_weight)           # 'max' init on the device
+            m.weight_quantizer = ChannelQuant(1.0, uaq=m.weight_quantizer, weight_tensor=m.org_weight,
+                                              shiftTarget=SHIFTS, name=name)
+    g = torch.Generator(device=dev).manual_seed(1005 + rank)
+    inp = torch.empty((n_cali,) + BLOCKS[name], device=dev).normal_(generator=g).relu_()
+    with torch.no_grad():
+        block.set_quant_state(False, False)
+        out = torch.cat([block(inp[i:i + 64]) for i in range(0, n_cali, 64)])
+    block.set_quant_state_block(True)
+    block.cached_inp_features, block.cached_out_features = [inp], [out]
+    stamps = {}
+
+    def hook(i):
+        if i in (warmup, warmup + iters):
+            torch.cuda.synchronize(dev)
+            stamps[i] = time.perf_counter()
+
+    import builtins
+    _print = builtins.print
+    builtins.print = lambda *a, **k: None       # silence the loop's init prints
+    try:
+        block_recon_fused_shiftedScale(block, warmup + iters, (0.01, 0.1), qnn, None, verbose=False,
+                                       iter_hook=hook)
+    finally:
+        builtins.print = _print
+    dt = stamps[warmup + iters] - stamps[warmup]
+    return iters / dt
+
+
+def run_recon_bench(dev, world, rank, iters=200, blocks=("layer1.0", "layer4.0")):
+    res = {}
+    for b in blocks:
+        ips = run_block(dev, b, iters=iters, rank=rank)
+        if world > 1:
+            import torch.distributed as dist
+            t = torch.tensor([1.0 / ips], dtype=torch.float64, device=dev)
+            dist.all_reduce(t, op=dist.ReduceOp.MAX)     # slowest rank sets the pace
+            ips = 1.0 / t.item()
+        res[b] = round(ips, 2)
+    return {"metric": "block_recon_fused_shiftedScale iters/s (batch 32 per rank, W2, S=3)",
+            "iters_per_s": res, "timed_iters": iters, "n_gpus": world,
+            "samples_per_s": {k: round(v * 32 * world, 1) for k, v in res.items()}}
