@@ -163,20 +163,33 @@ __global__ __launch_bounds__(kBlock) void alpha_grad_stage1(
   for (int i = 0; i < sh.n; ++i) o[i] = acc[i];
 }
 
-// Stage 2 (conv): one thread per input channel.
+// Stage-2 partial sum for one input channel, one WAVE per channel: lane l sums the
+// (chunk, k) partials l, l+64, ... in a fixed order, then a fixed shuffle tree combines
+// the lanes (deterministic).  Result valid in every lane.
+__device__ __forceinline__ void wave_colsum(const double* __restrict__ part, const Geo& g,
+                                            uint32_t ci, uint32_t nchunk, int S, double* out) {
+  const uint32_t lane = threadIdx.x & (kWave - 1);
+  double acc[kMaxS];
+  for (int i = 0; i < S; ++i) acc[i] = 0.0;
+  const uint32_t npairs = nchunk * g.K;
+  for (uint32_t t = lane; t < npairs; t += kWave) {
+    const uint32_t c = t / g.K, k = t - c * g.K;
+    const double* q = part + ((size_t)c * g.CiK + (size_t)ci * g.K + k) * S;
+    for (int i = 0; i < S; ++i) acc[i] += q[i];
+  }
+  for (int i = 0; i < S; ++i) out[i] = wave_sum(acc[i]);
+}
+
+// Stage 2 (conv): one wave per input channel (4 channels per 256-thread workgroup).
 __global__ __launch_bounds__(kBlock) void alpha_grad_stage2(
     const double* __restrict__ part, const float* __restrict__ alpha, int S, Geo g,
     uint32_t nchunk, float reg_lambda, float reg_b, float* __restrict__ galpha,
     float* __restrict__ reg_vals) {
-  const uint32_t ci = blockIdx.x * blockDim.x + threadIdx.x;
+  const uint32_t ci = blockIdx.x * (kBlock / kWave) + threadIdx.x / kWave;
   if (ci >= g.Ci) return;
   double gp[kMaxS];
-  for (int i = 0; i < S; ++i) gp[i] = 0.0;
-  for (uint32_t c = 0; c < nchunk; ++c)
-    for (uint32_t k = 0; k < g.K; ++k) {
-      const double* q = part + ((size_t)c * g.CiK + (size_t)ci * g.K + k) * S;
-      for (int i = 0; i < S; ++i) gp[i] += q[i];
-    }
+  wave_colsum(part, g, ci, nchunk, S, gp);
+  if ((threadIdx.x & (kWave - 1)) != 0) return;
   float a[kMaxS], ga[kMaxS];
   load_row(alpha, ci, S, a);
   const float reg = alpha_chain(a, S, gp, reg_lambda, reg_b, 0, ga);
@@ -412,15 +425,11 @@ __global__ __launch_bounds__(kBlock) void shift_mse_stage2(const double* __restr
                                                            Geo g, uint32_t nchunk,
                                                            float* __restrict__ alpha,
                                                            float* __restrict__ mse_out) {
-  const uint32_t ci = blockIdx.x * blockDim.x + threadIdx.x;
+  const uint32_t ci = blockIdx.x * (kBlock / kWave) + threadIdx.x / kWave;
   if (ci >= g.Ci) return;
   double m[kMaxS];
-  for (int i = 0; i < S; ++i) m[i] = 0.0;
-  for (uint32_t c = 0; c < nchunk; ++c)
-    for (uint32_t k = 0; k < g.K; ++k) {
-      const double* q = part + ((size_t)c * g.CiK + (size_t)ci * g.K + k) * S;
-      for (int i = 0; i < S; ++i) m[i] += q[i];
-    }
+  wave_colsum(part, g, ci, nchunk, S, m);
+  if ((threadIdx.x & (kWave - 1)) != 0) return;
   float a[kMaxS];
   init_alpha_row(m, S, a);
   for (int i = 0; i < S; ++i) {
@@ -505,8 +514,9 @@ static int make_shifts(const float* shifts, int S, Shifts& sh) {
 static void chunking(const Geo& g, uint32_t& chunk, uint32_t& nchunk) {
   const uint32_t colblk = (g.CiK + kBlock - 1) / kBlock;
   uint32_t want = 512 / colblk;
+  const uint32_t max_chunks = (g.Co + 7) / 8;   // >= 8 rows per thread: few stage-2 partials
+  if (want > max_chunks) want = max_chunks;
   if (want < 1) want = 1;
-  if (want > g.Co) want = g.Co;
   chunk = (g.Co + want - 1) / want;
   nchunk = (g.Co + chunk - 1) / chunk;
 }
@@ -581,7 +591,7 @@ extern "C" int ssq_adashift_bwd(const float* gWhat, const float* W, const float*
   hipLaunchKernelGGL(alpha_grad_stage1<0>, dim3((g.CiK + kBlock - 1) / kBlock, nchunk),
                      dim3(kBlock), 0, s, gWhat, W, alpha, beta, delta, zp, sh, g, chunk,
                      hard_round, (float)qmin, (float)qmax, (double*)ws, gbeta);
-  hipLaunchKernelGGL(alpha_grad_stage2, dim3((g.Ci + kBlock - 1) / kBlock), dim3(kBlock), 0, s,
+  hipLaunchKernelGGL(alpha_grad_stage2, dim3((g.Ci + 3) / 4), dim3(kBlock), 0, s,
                      (const double*)ws, alpha, S, g, nchunk, reg_lambda, reg_b, galpha, reg_vals);
   return check_launch("ssq_adashift_bwd");
 }
@@ -632,7 +642,7 @@ extern "C" int ssq_lhs_bwd(const float* gWhat, const float* W, const float* alph
   hipLaunchKernelGGL(alpha_grad_stage1<1>, dim3((g.CiK + kBlock - 1) / kBlock, nchunk),
                      dim3(kBlock), 0, s, gWhat, W, alpha, nullptr, delta, zp, sh, g, chunk, 0,
                      (float)qmin, (float)qmax, (double*)ws, nullptr);
-  hipLaunchKernelGGL(alpha_grad_stage2, dim3((g.Ci + kBlock - 1) / kBlock), dim3(kBlock), 0, s,
+  hipLaunchKernelGGL(alpha_grad_stage2, dim3((g.Ci + 3) / 4), dim3(kBlock), 0, s,
                      (const double*)ws, alpha, S, g, nchunk, 0.0f, 0.0f, galpha, nullptr);
   return check_launch("ssq_lhs_bwd");
 }
@@ -709,7 +719,7 @@ extern "C" int ssq_shift_init(const float* W, const float* delta, const float* z
     chunking(g, chunk, nchunk);
     hipLaunchKernelGGL(shift_mse_stage1, dim3((g.CiK + kBlock - 1) / kBlock, nchunk), dim3(kBlock),
                        0, s, W, delta, sh, g, chunk, cc, (double*)ws);
-    hipLaunchKernelGGL(shift_mse_stage2, dim3((g.Ci + kBlock - 1) / kBlock), dim3(kBlock), 0, s,
+    hipLaunchKernelGGL(shift_mse_stage2, dim3((g.Ci + 3) / 4), dim3(kBlock), 0, s,
                        (const double*)ws, S, g, nchunk, alpha, mse_out);
   }
   if (beta)  // init_v_beta: beta from delta * s[argmax p(alpha)] (channelQuant.py:289-292)

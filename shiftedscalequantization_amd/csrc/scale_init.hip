@@ -148,8 +148,19 @@ __global__ void finalize_mse(const double* __restrict__ part, const float* __res
                              int nslice, int n_bits, int sym, float* __restrict__ delta,
                              float* __restrict__ zp, float* __restrict__ raw_zp,
                              double* __restrict__ scores) {
-  const int64_t row = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (row >= rows) return;
+  // one workgroup per row: wave w sums the slice partials of candidates w, w+4, ...
+  // (lanes over slices, fixed shuffle tree), then thread 0 picks the first strict minimum
+  __shared__ double sc[kCand];
+  const int64_t row = blockIdx.x;
+  const int lane = threadIdx.x & (kWave - 1), wv = threadIdx.x / kWave;
+  for (int c = wv; c < kCand; c += blockDim.x / kWave) {
+    double sum = 0.0;
+    for (int s = lane; s < nslice; s += kWave) sum += part[((size_t)row * nslice + s) * kCand + c];
+    sum = wave_sum(sum);
+    if (lane == 0) sc[c] = sum / (double)inner;
+  }
+  __syncthreads();
+  if (threadIdx.x != 0) return;
   float mn, mx;
   row_minmax(pmin, pmax, row, nslice, mn, mx);
   if (sym) {
@@ -160,9 +171,7 @@ __global__ void finalize_mse(const double* __restrict__ part, const float* __res
   double best = 1e10;
   float bd = NAN, bz = NAN, br = NAN;
   for (int c = 0; c < kCand; ++c) {
-    double sum = 0.0;
-    for (int s = 0; s < nslice; ++s) sum += part[((size_t)row * nslice + s) * kCand + c];
-    const double score = sum / (double)inner;
+    const double score = sc[c];
     if (scores) scores[(size_t)row * kCand + c] = score;
     if (score < best) {
       best = score;
@@ -254,7 +263,7 @@ extern "C" int ssq_scale_init(const float* x, int64_t rows, int64_t inner, int n
     double* part = (double*)((char*)ws + off);
     hipLaunchKernelGGL(mse_stage, dim3(ns, (unsigned)rows), dim3(kBlock), 0, s, x, inner, ns, pmin,
                        pmax, n_bits, sym, part);
-    hipLaunchKernelGGL(finalize_mse, fin, dim3(64), 0, s, part, pmin, pmax, rows, inner, ns,
+    hipLaunchKernelGGL(finalize_mse, dim3((unsigned)rows), dim3(kBlock), 0, s, part, pmin, pmax, rows, inner, ns,
                        n_bits, sym, delta, zp, raw_zp, scores);
   }
   return check_launch("ssq_scale_init");

@@ -112,10 +112,18 @@ def test_block_recon_fused_matches_reference(Q, golden):
     np.testing.assert_allclose(res, g["final_losses"], rtol=5e-3)
     for n in ("conv1", "conv2", "downsample"):
         q = getattr(block, n).weight_quantizer
-        # Adam turns a near-zero gradient into a full +-lr step, so logits whose gradient
-        # sits at the rounding level can drift by a few lr-steps: bound those separately
+        # Input channels whose shift candidates are all identical (floor(W/(d*s_i)) equal
+        # for every shift, common in 1x1 convs) have an analytically ZERO alpha gradient;
+        # Adam turns the rounding noise left there into full +-lr steps in both the
+        # reference and here, so those rows are a random walk of a few lr-steps.  Every
+        # other row must follow the reference trajectory.
+        from oracle import ssq_ref as R
+        w = g[n + "_w"]
+        fl = np.stack(R.shift_floors(w, g[n + "_delta"].reshape(-1, 1, 1, 1), SHIFTS))
+        degenerate = np.all(fl == fl[:1], axis=(0, 1, 3, 4))          # per input channel
         da = np.abs(q.alpha.detach().cpu().numpy() - g[n + "_alpha"])
-        assert np.mean(da <= 2e-4) >= 0.95 and da.max() <= 3e-3, (n, da.max())
+        assert da[~degenerate].max() <= 2e-4, (n, da[~degenerate].max())
+        assert da[degenerate].max(initial=0.0) <= 30 * 1e-3 * 2, n      # <= iters * 2 lr
         np.testing.assert_allclose(q.beta.detach().cpu().numpy(), g[n + "_beta0"], rtol=1e-5, atol=1e-5)
         with torch.no_grad():
             what = q(getattr(block, n).weight).cpu().numpy()
