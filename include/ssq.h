@@ -123,16 +123,18 @@ int ssq_adashift_fwd(const float* W, const float* alpha, const float* beta,
 /* Backward of the soft-target adaShift forward wrt alpha (and beta if gbeta != NULL).
  * Conv alpha gradients are reduced over (Co, K) deterministically through `ws`.
  * Fused shift regulariser (layer_recon_fused_shiftedScale.py:281-282), applied when
- * reg_lambda != 0:  reg = lambda * sum(1 - |2p-1|^b);  its gradient is added to
- * galpha and per-alpha-row values are written to reg_vals (may be NULL).
+ * lambda != 0:  reg = lambda * sum(1 - |2p-1|^b);  its gradient is added to galpha and
+ * per-alpha-row values are written to reg_vals (may be NULL).  (lambda, b) come from
+ * reg_lambda/reg_b, or from the DEVICE pair reg_dev[0..1] when reg_dev != NULL (the
+ * graph-capturable form: the schedule changes every iteration).
  * galpha is OVERWRITTEN (not accumulated).                                             */
 size_t ssq_adashift_bwd_workspace_size(int64_t Co, int64_t Ci, int64_t K, int S, int is_fc);
 int ssq_adashift_bwd(const float* gWhat, const float* W, const float* alpha,
                      const float* beta, const float* delta, const float* zp,
                      const float* shifts, int S, int64_t Co, int64_t Ci, int64_t K,
                      int is_fc, int hard_round, int qmin, int qmax, float reg_lambda,
-                     float reg_b, float* galpha, float* gbeta, float* reg_vals, void* ws,
-                     size_t ws_bytes, ssq_stream_t stream);
+                     float reg_b, const float* reg_dev, float* galpha, float* gbeta,
+                     float* reg_vals, void* ws, size_t ws_bytes, ssq_stream_t stream);
 
 /* Shift-regulariser alone (value + gradient wrt alpha), for iterations where the
  * reconstruction gradient is not wanted.  mode 0: lambda*sum(1-|2p-1|^b)

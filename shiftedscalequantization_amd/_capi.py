@@ -39,7 +39,7 @@ SIGNATURES = {
                               _p, _p, _p]),
     "ssq_adashift_bwd_workspace_size": (_sz, [_i64, _i64, _i64, _i, _i]),
     "ssq_adashift_bwd": (_i, [_p, _p, _p, _p, _p, _p, _p, _i, _i64, _i64, _i64, _i, _i, _i, _i,
-                              _f, _f, _p, _p, _p, _p, _sz, _p]),
+                              _f, _f, _p, _p, _p, _p, _p, _sz, _p]),
     "ssq_shift_reg": (_i, [_p, _i, _i64, _i, _f, _f, _p, _p, _p]),
     "ssq_lhs_fwd": (_i, [_p, _p, _p, _p, _p, _i, _i64, _i64, _i64, _i, _i, _i, _i, _p, _p]),
     "ssq_lhs_bwd": (_i, [_p, _p, _p, _p, _p, _p, _i, _i64, _i64, _i64, _i, _i, _i, _p, _p, _sz,
@@ -124,15 +124,36 @@ def stream_of(t):
 _ws_cache = {}
 
 
+_ws_scope = None
+
+
+class workspace_scope:
+    """Route workspace() to a private cache, e.g. for one captured HIP graph: the buffers
+    allocated during capture belong to that graph and must never be resized under it."""
+
+    def __init__(self, cache=None):
+        self.cache = {} if cache is None else cache
+
+    def __enter__(self):
+        global _ws_scope
+        self.prev, _ws_scope = _ws_scope, self.cache
+        return self.cache
+
+    def __exit__(self, *exc):
+        global _ws_scope
+        _ws_scope = self.prev
+
+
 def workspace(nbytes, device):
     """Per-(device, stream) scratch buffer for kernel partials (grown, never shrunk)."""
     if nbytes == 0:
         return None, 0
+    cache = _ws_cache if _ws_scope is None else _ws_scope
     key = (device.index, torch.cuda.current_stream(device).cuda_stream)
-    buf = _ws_cache.get(key)
+    buf = cache.get(key)
     if buf is None or buf.numel() < nbytes:
         buf = torch.empty(max(int(nbytes), 1 << 16), dtype=torch.uint8, device=device)
-        _ws_cache[key] = buf
+        cache[key] = buf
     return C.c_void_p(buf.data_ptr()), buf.numel()
 
 

@@ -183,8 +183,12 @@ __device__ __forceinline__ void wave_colsum(const double* __restrict__ part, con
 // Stage 2 (conv): one wave per input channel (4 channels per 256-thread workgroup).
 __global__ __launch_bounds__(kBlock) void alpha_grad_stage2(
     const double* __restrict__ part, const float* __restrict__ alpha, int S, Geo g,
-    uint32_t nchunk, float reg_lambda, float reg_b, float* __restrict__ galpha,
-    float* __restrict__ reg_vals) {
+    uint32_t nchunk, float reg_lambda, float reg_b, const float* __restrict__ reg_dev,
+    float* __restrict__ galpha, float* __restrict__ reg_vals) {
+  if (reg_dev) {  // graph-capturable form: (lambda, b) read from device memory
+    reg_lambda = reg_dev[0];
+    reg_b = reg_dev[1];
+  }
   const uint32_t ci = blockIdx.x * (kBlock / kWave) + threadIdx.x / kWave;
   if (ci >= g.Ci) return;
   double gp[kMaxS];
@@ -203,7 +207,12 @@ __global__ __launch_bounds__(kBlock) void alpha_grad_fc(
     const float* __restrict__ gWhat, const float* __restrict__ W, const float* __restrict__ alpha,
     const float* __restrict__ beta, const float* __restrict__ delta, const float* __restrict__ zp,
     Shifts sh, Geo g, uint32_t n, int hard_r, float lo, float hi, float reg_lambda, float reg_b,
-    float* __restrict__ galpha, float* __restrict__ gbeta, float* __restrict__ reg_vals) {
+    const float* __restrict__ reg_dev, float* __restrict__ galpha, float* __restrict__ gbeta,
+    float* __restrict__ reg_vals) {
+  if (reg_dev) {
+    reg_lambda = reg_dev[0];
+    reg_b = reg_dev[1];
+  }
   const uint32_t stride = gridDim.x * blockDim.x;
   for (uint32_t e = blockIdx.x * blockDim.x + threadIdx.x; e < n; e += stride) {
     const uint32_t co = e / g.CiK;
@@ -570,8 +579,9 @@ extern "C" int ssq_adashift_bwd(const float* gWhat, const float* W, const float*
                                 const float* beta, const float* delta, const float* zp,
                                 const float* shifts, int S, int64_t Co, int64_t Ci, int64_t K,
                                 int is_fc, int hard_round, int qmin, int qmax, float reg_lambda,
-                                float reg_b, float* galpha, float* gbeta, float* reg_vals,
-                                void* ws, size_t ws_bytes, ssq_stream_t stream) {
+                                float reg_b, const float* reg_dev, float* galpha, float* gbeta,
+                                float* reg_vals, void* ws, size_t ws_bytes,
+                                ssq_stream_t stream) {
   SSQ_GEO(Co, Ci, K, is_fc, g);
   SSQ_SHIFTS(shifts, S, sh);
   SSQ_REQUIRE(gWhat && W && alpha && beta && delta && zp && galpha, SSQ_E_ARG,
@@ -581,7 +591,7 @@ extern "C" int ssq_adashift_bwd(const float* gWhat, const float* W, const float*
   if (is_fc) {
     hipLaunchKernelGGL(alpha_grad_fc<0>, dim3(grid_for(n, kBlock)), dim3(kBlock), 0, s, gWhat, W,
                        alpha, beta, delta, zp, sh, g, n, hard_round, (float)qmin, (float)qmax,
-                       reg_lambda, reg_b, galpha, gbeta, reg_vals);
+                       reg_lambda, reg_b, reg_dev, galpha, gbeta, reg_vals);
     return check_launch("ssq_adashift_bwd(fc)");
   }
   SSQ_REQUIRE(ws && ws_bytes >= colred_ws(Co, Ci, K, S), SSQ_E_WS,
@@ -592,7 +602,8 @@ extern "C" int ssq_adashift_bwd(const float* gWhat, const float* W, const float*
                      dim3(kBlock), 0, s, gWhat, W, alpha, beta, delta, zp, sh, g, chunk,
                      hard_round, (float)qmin, (float)qmax, (double*)ws, gbeta);
   hipLaunchKernelGGL(alpha_grad_stage2, dim3((g.Ci + 3) / 4), dim3(kBlock), 0, s,
-                     (const double*)ws, alpha, S, g, nchunk, reg_lambda, reg_b, galpha, reg_vals);
+                     (const double*)ws, alpha, S, g, nchunk, reg_lambda, reg_b, reg_dev, galpha,
+                     reg_vals);
   return check_launch("ssq_adashift_bwd");
 }
 
@@ -632,7 +643,7 @@ extern "C" int ssq_lhs_bwd(const float* gWhat, const float* W, const float* alph
   if (is_fc) {
     hipLaunchKernelGGL(alpha_grad_fc<1>, dim3(grid_for(n, kBlock)), dim3(kBlock), 0, s, gWhat, W,
                        alpha, nullptr, delta, zp, sh, g, n, 0, (float)qmin, (float)qmax, 0.0f,
-                       0.0f, galpha, nullptr, nullptr);
+                       0.0f, nullptr, galpha, nullptr, nullptr);
     return check_launch("ssq_lhs_bwd(fc)");
   }
   SSQ_REQUIRE(ws && ws_bytes >= colred_ws(Co, Ci, K, S), SSQ_E_WS,
@@ -643,7 +654,7 @@ extern "C" int ssq_lhs_bwd(const float* gWhat, const float* W, const float* alph
                      dim3(kBlock), 0, s, gWhat, W, alpha, nullptr, delta, zp, sh, g, chunk, 0,
                      (float)qmin, (float)qmax, (double*)ws, nullptr);
   hipLaunchKernelGGL(alpha_grad_stage2, dim3((g.Ci + 3) / 4), dim3(kBlock), 0, s,
-                     (const double*)ws, alpha, S, g, nchunk, 0.0f, 0.0f, galpha, nullptr);
+                     (const double*)ws, alpha, S, g, nchunk, 0.0f, 0.0f, nullptr, galpha, nullptr);
   return check_launch("ssq_lhs_bwd");
 }
 

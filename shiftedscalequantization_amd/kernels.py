@@ -214,8 +214,9 @@ def get_delta(delta, alpha, shifts, w_shape):
 class AdaShiftFn(torch.autograd.Function):
     """ChannelQuant.forward 'adaShift' (channelQuant.py:51-64).  Gradients flow to alpha
     (soft targets only) and beta (soft rounding only), as in the reference's autograd.
-    ctx.reg carries an optional fused shift regulariser (lambda, b) whose gradient is
-    added to alpha's inside the same backward kernel."""
+    `reg` = (lambda, b, reg_vals, reg_dev) optionally fuses the shift regulariser: its
+    gradient is added to alpha's inside the same backward kernel, (lambda, b) taken from
+    the device pair reg_dev when given (graph-capturable)."""
 
     @staticmethod
     def forward(ctx, alpha, beta, w, delta, zp, shifts, n_bits, sym, hard_t, hard_r, reg):
@@ -246,13 +247,13 @@ class AdaShiftFn(torch.autograd.Function):
         lo, hi = qrange(n_bits, sym)
         ga = torch.empty_like(a)
         gb = torch.empty_like(w) if need_b else None
-        lam, bb, reg_vals = (0.0, 0.0, None) if reg is None else reg
+        lam, bb, reg_vals, reg_dev = (0.0, 0.0, None, None) if reg is None else reg
         S = len(shifts)
         wsb = query("ssq_adashift_bwd_workspace_size", Co, Ci, K, S, is_fc)
         ws, wsn = workspace(wsb, w.device)
         call("ssq_adashift_bwd", _vp(g), _vp(w), _vp(a), _vp(b), _vp(d), _vp(z),
              A.shifts_arg(shifts), S, Co, Ci, K, is_fc, int(hard_r), lo, hi, float(lam), float(bb),
-             _vp(ga), _vp(gb), _vp(reg_vals), ws, wsn, stream_of(w))
+             _vp(reg_dev), _vp(ga), _vp(gb), _vp(reg_vals), ws, wsn, stream_of(w))
         return (ga if need_a else None, gb, None, None, None, None, None, None, None, None, None)
 
 

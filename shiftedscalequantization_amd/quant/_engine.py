@@ -35,8 +35,8 @@ class BatchFeeder:
         """One reference-identical draw: torch.randperm(N)[:batch_size] on the CPU."""
         return torch.randperm(self.N)[:self.bs]
 
-    def next(self, perm=None):
-        perm = self.draw() if perm is None else perm
+    def stage(self, perm):
+        """Host -> device copy of the batch indices into the static index buffer."""
         slot = self.k % self.RING
         if self.done[slot] is not None:
             self.done[slot].synchronize()
@@ -46,8 +46,15 @@ class BatchFeeder:
         ev.record()
         self.done[slot] = ev
         self.k += 1
+
+    def gather(self):
+        """One ssq_gather_rows2 launch from the static indices into the static batch."""
         K.gather_rows2(self.inp, self.didx, self.out, out0=self.cur_inp, out1=self.cur_out)
         return self.cur_inp, self.cur_out
+
+    def next(self, perm=None):
+        self.stage(self.draw() if perm is None else perm)
+        return self.gather()
 
     def head(self, n):
         """cached[:n] (the final soft/hard evaluation batch)."""

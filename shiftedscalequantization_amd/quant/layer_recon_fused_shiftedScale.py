@@ -41,8 +41,11 @@ def _weight_quantizers(module):
     return mods
 
 
+GRAPH_WARMUP = 3     # eager iterations before the iteration body is captured
+
+
 def _fused_loop(block, modules, iters, lmda, model, p, lr, bias_cal, batch_size, dp_average,
-                verbose, iter_hook=None):
+                verbose, iter_hook=None, graph=True):
     device = next(model.parameters()).device
     quantizers, opt_params = [], []
     for m in modules:
@@ -57,7 +60,11 @@ def _fused_loop(block, modules, iters, lmda, model, p, lr, bias_cal, batch_size,
         m.beta_out.requires_grad_(bias_cal)
         if bias_cal:
             opt_params += [m.alpha_out, m.beta_out]
-    optimizer = torch.optim.Adam(opt_params, lr=lr)
+    on_gpu = opt_params[0].is_cuda
+    use_graph = bool(graph and on_gpu and world() == 1 and iters > GRAPH_WARMUP + 1)
+    # one fused Adam kernel for all parameters (capturable: its step count lives on the
+    # device, so the whole iteration can be replayed from a HIP graph)
+    optimizer = torch.optim.Adam(opt_params, lr=lr, fused=on_gpu, capturable=use_graph)
     if verbose:
         print("number of elements in opt_params: {}".format(sum(t.numel() for t in opt_params)))
     loss_func = FusedScaleLossFunction(block, quantizers, round_loss='relaxation', lmda=lmda,
@@ -66,25 +73,50 @@ def _fused_loop(block, modules, iters, lmda, model, p, lr, bias_cal, batch_size,
     feeder = BatchFeeder(torch.cat(block.cached_inp_features), torch.cat(block.cached_out_features),
                          batch_size, device)
     bucket = GradBucket(opt_params, average=dp_average) if world() > 1 else None
+    regp = loss_func.arm(device)    # device (lambda_S, b2) read by the adaShift backward
+    last = {}
 
+    def body():
+        """One iteration on the device: gather -> forward -> fused loss+grad -> backward
+        (+ RCCL bucket) -> Adam.  No host sync, no host-side state: graph-capturable."""
+        cur_inp, cur_out = feeder.gather()
+        quant_out = block(cur_inp)
+        rec, g_out = loss_func.loss_and_grad(quant_out, cur_out)
+        quant_out.backward(g_out)
+        if bucket is not None:
+            bucket.allreduce_()
+        optimizer.step()
+        last['rec'] = rec
+
+    graph_obj, ws_cache = None, {}
     start_loss = 0.0
     t = tqdm(range(iters), desc='', dynamic_ncols=True, disable=not verbose)
     for i in t:
         if iter_hook is not None:
             iter_hook(i)
-        cur_inp, cur_out = feeder.next()
-        optimizer.zero_grad()
-        loss_func.arm()
-        quant_out = block(cur_inp)
-        err = loss_func.fused(quant_out, cur_out)
-        err.backward()
-        if bucket is not None:
-            bucket.allreduce_()
-        optimizer.step()
+        feeder.stage(feeder.draw())            # reference-identical CPU randperm draw
+        loss_func.upload_schedule(regp)        # this iteration's (lambda_S, b2)
+        if use_graph and i == GRAPH_WARMUP:
+            optimizer.zero_grad(set_to_none=True)
+            graph_obj = torch.cuda.CUDAGraph()
+            with K.A.workspace_scope(ws_cache):
+                with torch.cuda.graph(graph_obj):
+                    body()
+        if graph_obj is not None:
+            graph_obj.replay()
+        else:
+            optimizer.zero_grad()
+            body()
+        loss_func.bookkeep(last['rec'])
         if i % 500 == 0 and verbose:
             start_loss = max(start_loss, as_float(loss_func.rec_loss))
             t.set_description(f"{start_loss:.6f} -> {as_float(loss_func.rec_loss):.6f} "
                               f"{loss_func.round_loss_val} ")
+    if graph_obj is not None:
+        torch.cuda.current_stream().synchronize()
+        for p_ in opt_params:       # detach the grads from the graph's private pool
+            p_.grad = None if p_.grad is None else p_.grad.clone()
+        del graph_obj
     loss_func.disarm()
     if iter_hook is not None:
         iter_hook(iters)
@@ -119,27 +151,29 @@ def _fused_loop(block, modules, iters, lmda, model, p, lr, bias_cal, batch_size,
 def block_recon_fused_shiftedScale(block: BaseQuantBlock, iters: int = 20000, lmda: list = [1., 1.],
                                    model=None, test_loader=None, act=False, adaround=False,
                                    useShiftedScale=True, bias_cal=False, batch_size=32,
-                                   dp_average=False, verbose=True, iter_hook=None):
-    """layer_recon_fused_shiftedScale.py:23-141 -> [soft rec loss, hard rec loss]."""
+                                   dp_average=False, verbose=True, iter_hook=None, graph=True):
+    """layer_recon_fused_shiftedScale.py:23-141 -> [soft rec loss, hard rec loss].
+    graph=True replays the iteration body from a HIP graph after GRAPH_WARMUP eager
+    iterations (single GPU); the arithmetic and the batch draws are unchanged."""
     if act:
         # the reference's act branch builds ChannelQuantAct and calls its init_v, which
         # crashes (channelQuantAct.py:126-134): no working semantics exist to reproduce
         raise NotImplementedError("block_recon_fused_shiftedScale(act=True) is broken in the reference")
     block.train()
     return _fused_loop(block, _weight_quantizers(block), iters, lmda, model, 2.0, 0.001, bias_cal,
-                       batch_size, dp_average, verbose, iter_hook)
+                       batch_size, dp_average, verbose, iter_hook, graph)
 
 
 def layer_recon_fused_shiftedScale(layer: QuantModule, iters: int = 20000, lmda: list = [1., 1.],
                                    model=None, test_loader=None, act=False, adaround=False,
                                    useShiftedScale=True, bias_cal=False, batch_size=32,
-                                   dp_average=False, verbose=True):
+                                   dp_average=False, verbose=True, graph=True):
     """layer_recon_fused_shiftedScale.py:144-221.  The reference raises UnboundLocalError
     (`opt_params += ...` before assignment, :156); this implements its evident intent: the
     block loop on one layer with p = 1.0 (:165) and Adam's default lr."""
     model.train()
     return _fused_loop(layer, [layer], iters, lmda, model, 1.0, 0.001, bias_cal, batch_size,
-                       dp_average, verbose)
+                       dp_average, verbose, None, graph)
 
 
 class FusedScaleLossFunction:
@@ -195,27 +229,57 @@ class FusedScaleLossFunction:
         return total
 
     # ---------------------------------------------------------------- fused fast path
-    def arm(self):
-        """Before the block forward: hand this iteration's shift-regulariser (lambda, b2)
-        to each quantizer's adaShift backward."""
-        (b, b2), active = self._schedule()
+    def arm(self, device):
+        """Give every quantizer's adaShift backward the shift regulariser, with
+        (lambda_S, b2) read from a device pair that upload_schedule() refreshes before each
+        iteration (lambda_S = 0 during warm-up).  Returns that device pair."""
+        self._regp = torch.zeros(2, dtype=torch.float32, device=device)
+        self._regp_host = [torch.zeros(2, dtype=torch.float32, pin_memory=torch.cuda.is_available())
+                           for _ in range(4)]
+        self._regp_done = [None] * 4
+        self._regp_k = 0
         for qt in self.quantizer:
-            if active:
-                vals = self._reg_vals.get(id(qt))
-                rows = qt.alpha.numel() // qt.alpha.shape[-1]
-                if vals is None or vals.numel() != rows:
-                    vals = torch.zeros(rows, device=qt.alpha.device)
-                    self._reg_vals[id(qt)] = vals
-                qt._fused_reg = (self.lmdaS, b2, vals)
-            else:
-                qt._fused_reg = None
+            rows = qt.alpha.numel() // qt.alpha.shape[-1]
+            vals = torch.zeros(rows, device=qt.alpha.device)
+            self._reg_vals[id(qt)] = vals
+            qt._fused_reg = (0.0, 0.0, vals, self._regp)
+        return self._regp
+
+    def upload_schedule(self, regp=None):
+        """H2D (non-blocking, pinned ring) of this iteration's (lambda_S, b2)."""
+        regp = self._regp if regp is None else regp
+        (b, b2), active = self._schedule()
+        slot = self._regp_k % len(self._regp_host)
+        if self._regp_done[slot] is not None:
+            self._regp_done[slot].synchronize()
+        h = self._regp_host[slot]
+        h[0], h[1] = (float(self.lmdaS), float(b2)) if active else (0.0, 0.0)
+        regp.copy_(h, non_blocking=True)
+        ev = torch.cuda.Event()
+        ev.record()
+        self._regp_done[slot] = ev
+        self._regp_k += 1
 
     def disarm(self):
         for qt in self.quantizer:
             qt._fused_reg = None
 
+    def loss_and_grad(self, pred, tgt):
+        """One ssq_lp_loss pass: the loss value AND d loss / d pred (device only).  The
+        caller back-propagates `grad` from `pred` -- exactly what total_loss.backward()
+        delivers there; the regulariser terms reach alpha through the armed adaShift
+        backward, and beta is never optimised by this loop."""
+        rec_loss, grad = K.lp_loss_and_grad(pred, tgt, self.p)
+        return rec_loss[0], grad
+
     def fused(self, pred, tgt):
-        rec_loss = K.lp_loss(pred, tgt, self.p)
+        """loss_and_grad + the host bookkeeping of one iteration."""
+        rec_loss, grad = self.loss_and_grad(pred, tgt)
+        self.bookkeep(rec_loss)
+        return rec_loss, grad
+
+    def bookkeep(self, rec_loss):
+        """Host side of one iteration: lazy report values and count += 1."""
         (b, b2), active = self._schedule()
         if active:
             quants, lR = list(self.quantizer), self.lmdaR
@@ -228,7 +292,6 @@ class FusedScaleLossFunction:
             total = rec_loss
         self._record(rec_loss, R, S, total, b)
         self.count += 1
-        return rec_loss
 
     def _record(self, rec, R, S, total, b):
         self.rec_loss = LazyValue(rec.detach())

@@ -159,6 +159,12 @@ class QuantModule(nn.Module):
         else:
             self.alpha_out = nn.Parameter(torch.ones(n_ch).view(1, n_ch))
             self.beta_out = nn.Parameter(torch.zeros(n_ch).view(1, n_ch))
+        # gamma^z / phi^z are learned only with bias_cal: until then they need no grad
+        self.alpha_out.requires_grad_(False)
+        self.beta_out.requires_grad_(False)
+        self._affine_key = None
+        self._affine_identity = False
+        self.train_bias = False
         self.selection = None
         self.selectionInited = False
         self.pathName = ''
@@ -167,17 +173,33 @@ class QuantModule(nn.Module):
         t = t.detach()
         return t.cpu().clone() if self.cache_to_host else t.clone()
 
+    def _affine_is_identity(self):
+        """True while gamma^z / phi^z are still their untouched initial (1, 0) tensors
+        and nothing needs their gradient: then out*1+0 == out and the two passes (plus
+        their backward) are skipped.  Any in-place update bumps the tensor version."""
+        a, b = self.alpha_out, self.beta_out
+        if a.requires_grad or b.requires_grad:
+            return False
+        key = (id(a), id(b), a._version, b._version, a.device)
+        if key != self._affine_key:
+            # first use on this device / after any change: check the values once
+            self._affine_identity = bool(torch.all(a == 1).item() and torch.all(b == 0).item())
+            self._affine_key = key
+        return self._affine_identity
+
     def forward(self, input: torch.Tensor):
         if self.cache_features == 'if':
             self.cached_inp_features += [self._cache(input)]
         if self.use_weight_quant and self.cache_features == 'none':
             weight = self.weight_quantizer(self.weight)
-            bias = self.bias
+            # no reconstruction ever optimises the conv bias: its gradient (a full
+            # reduction over N,H,W per launch) is not requested
+            bias = self.bias if (self.bias is None or self.train_bias) else self.bias.detach()
         else:
             weight = self.org_weight
             bias = self.org_bias
         out = self.fwd_func(input, weight, bias, **self.fwd_kwargs)
-        if self.use_weight_quant and self.cache_features == 'none':
+        if self.use_weight_quant and self.cache_features == 'none' and not self._affine_is_identity():
             out = out * self.alpha_out + self.beta_out
         if self.se_module is not None:
             out = self.se_module(out)

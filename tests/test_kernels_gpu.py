@@ -319,6 +319,18 @@ def test_fused_bwd_with_reg_matches_separate(K, golden):
     a3 = dev(alpha).requires_grad_(True)
     vals = torch.empty(alpha.shape[0], device="cuda")
     y = K.adashift(a3, dev(beta), dev(w), dev(d), dev(z), SHIFTS, bits, False, False, False,
-                   reg=(0.1, 11.3, vals))
+                   reg=(0.1, 11.3, vals, None))
+    (y * gy).sum().backward()
+    close(host(a3.grad), host(a1.grad) + host(a2.grad), rtol=1e-5, atol=1e-7)
+    # device-side (lambda, b) form used under HIP-graph capture
+    a4 = dev(alpha).requires_grad_(True)
+    regp = torch.tensor([0.1, 11.3], device="cuda")
+    y = K.adashift(a4, dev(beta), dev(w), dev(d), dev(z), SHIFTS, bits, False, False, False,
+                   reg=(0.0, 0.0, vals, regp))
+    (y * gy).sum().backward()
+    close(host(a4.grad), host(a3.grad), rtol=1e-6, atol=1e-9)
+    a3 = dev(alpha).requires_grad_(True)
+    y = K.adashift(a3, dev(beta), dev(w), dev(d), dev(z), SHIFTS, bits, False, False, False,
+                   reg=(0.1, 11.3, vals, None))
     (y * gy).sum().backward()
     close(host(a3.grad), host(a1.grad) + host(a2.grad), rtol=1e-5, atol=1e-7)

@@ -74,7 +74,8 @@ def load_block(Q, g, block):
         m.use_weight_quant = True
 
 
-def test_block_recon_fused_matches_reference(Q, golden):
+@pytest.mark.parametrize("graph", [False, True])
+def test_block_recon_fused_matches_reference(Q, golden, graph):
     g = golden("recon_fused")
     qnn = build_qnn(Q, {})
     block = qnn.model[3]
@@ -87,27 +88,27 @@ def test_block_recon_fused_matches_reference(Q, golden):
     LRF = importlib.import_module("shiftedscalequantization_amd.quant.layer_recon_fused_shiftedScale")
     seen_perms, seen_rec = [], []
     orig_draw = LRF.BatchFeeder.draw
-    orig_fused = LRF.FusedScaleLossFunction.fused
+    orig_keep = LRF.FusedScaleLossFunction.bookkeep
 
     def draw(self):
         p = orig_draw(self)
         seen_perms.append(p.clone())
         return p
 
-    def fused(self, pred, tgt):
-        r = orig_fused(self, pred, tgt)
-        seen_rec.append(r)
-        return r
+    def bookkeep(self, rec):
+        seen_rec.append(float(rec.item()))     # read now: a graph replay overwrites it
+        return orig_keep(self, rec)
 
-    LRF.BatchFeeder.draw, LRF.FusedScaleLossFunction.fused = draw, fused
+    LRF.BatchFeeder.draw, LRF.FusedScaleLossFunction.bookkeep = draw, bookkeep
     try:
         torch.manual_seed(1005)
-        res = LRF.block_recon_fused_shiftedScale(block, iters, (0.01, 0.1), qnn, None, verbose=False)
+        res = LRF.block_recon_fused_shiftedScale(block, iters, (0.01, 0.1), qnn, None, verbose=False,
+                                                 graph=graph)
     finally:
-        LRF.BatchFeeder.draw, LRF.FusedScaleLossFunction.fused = orig_draw, orig_fused
+        LRF.BatchFeeder.draw, LRF.FusedScaleLossFunction.bookkeep = orig_draw, orig_keep
     # identical batches (same CPU RNG stream as the reference)
     np.testing.assert_array_equal(np.stack([p.numpy() for p in seen_perms]), g["perms"])
-    rec = np.array([float(r.item()) for r in seen_rec])
+    rec = np.array(seen_rec)
     np.testing.assert_allclose(rec, g["rec_loss"][:iters], rtol=2e-4)
     np.testing.assert_allclose(res, g["final_losses"], rtol=5e-3)
     for n in ("conv1", "conv2", "downsample"):
