@@ -5,10 +5,10 @@
 // materialized as S W-sized tensors (the reference's self.x_q list, channelQuant.py:284-286),
 // so the adaShift forward reads W + beta (8 B/elem) and writes What (4 B/elem).
 //
-// alpha-gradient reductions over (Co, K) per input channel are two-stage and
-// deterministic: stage 1 sums a chunk of Co rows per column j = ci*K + k in registers
-// (double) and writes [chunk][j][S] partials; stage 2 (one thread per alpha row) sums the
-// partials in fixed order and applies the softmax/clamp chain + the shift regulariser.
+// alpha-gradient reductions over (Co, K) per input channel run one workgroup per input
+// channel (alpha_ci_kernel): S double accumulators per thread, a fixed shuffle tree, then
+// the waves in fixed order -- deterministic, one launch, no workspace -- followed by the
+// softmax/clamp chain and the shift regulariser.
 #include "ssq_common.h"
 
 namespace ssq {
@@ -124,81 +124,6 @@ __device__ __forceinline__ float cand_value(float w, float d, float z, float s, 
   const float ds = __fmul_rn(d, s);
   const float q = clampf(__fadd_rn(rintf(w / ds), z), lo, hi);
   return __fmul_rn(__fsub_rn(q, z), ds);
-}
-
-// Stage 1 (conv): column j = ci*K + k, rows co in [co0, co0 + chunk).
-template <int MODE>
-__global__ __launch_bounds__(kBlock) void alpha_grad_stage1(
-    const float* __restrict__ gWhat, const float* __restrict__ W, const float* __restrict__ alpha,
-    const float* __restrict__ beta, const float* __restrict__ delta, const float* __restrict__ zp,
-    Shifts sh, Geo g, uint32_t chunk, int hard_r, float lo, float hi, double* __restrict__ part,
-    float* __restrict__ gbeta) {
-  const uint32_t j = blockIdx.x * blockDim.x + threadIdx.x;
-  if (j >= g.CiK) return;
-  const uint32_t ci = j / g.K;
-  const uint32_t co0 = blockIdx.y * chunk, co1 = min(co0 + chunk, g.Co);
-  float a[kMaxS], p[kMaxS], F[kMaxS];
-  load_row(alpha, ci, sh.n, a);
-  soft_targets<kMaxS>(a, sh.n, nullptr, p);
-  double acc[kMaxS];
-  for (int i = 0; i < sh.n; ++i) acc[i] = 0.0;
-  for (uint32_t co = co0; co < co1; ++co) {
-    const uint32_t e = co * g.CiK + j;
-    const float w = W[e], d = delta[co], z = zp[co], gy = gWhat[e];
-    float gi;
-    if (MODE == 0) {
-      const float xf = soft_floor(w, d, sh, p, F);
-      const float b = beta[e];
-      const float hr = hard_r ? (b >= 0.0f ? 1.0f : 0.0f) : rect_sigmoid(b);
-      const float u = __fadd_rn(__fadd_rn(xf, hr), z);
-      gi = (u >= lo && u <= hi) ? __fmul_rn(gy, __fmul_rn(d, 1.0f)) : 0.0f;
-      if (gbeta) gbeta[e] = hard_r ? 0.0f : rect_sigmoid_grad(b, gi);
-    } else {
-      for (int i = 0; i < sh.n; ++i) F[i] = cand_value<1>(w, d, z, sh.s[i], lo, hi);
-      gi = gy;
-    }
-    for (int i = 0; i < sh.n; ++i) acc[i] += (double)gi * (double)F[i];
-  }
-  double* o = part + ((size_t)blockIdx.y * g.CiK + j) * sh.n;
-  for (int i = 0; i < sh.n; ++i) o[i] = acc[i];
-}
-
-// Stage-2 partial sum for one input channel, one WAVE per channel: lane l sums the
-// (chunk, k) partials l, l+64, ... in a fixed order, then a fixed shuffle tree combines
-// the lanes (deterministic).  Result valid in every lane.
-__device__ __forceinline__ void wave_colsum(const double* __restrict__ part, const Geo& g,
-                                            uint32_t ci, uint32_t nchunk, int S, double* out) {
-  const uint32_t lane = threadIdx.x & (kWave - 1);
-  double acc[kMaxS];
-  for (int i = 0; i < S; ++i) acc[i] = 0.0;
-  const uint32_t npairs = nchunk * g.K;
-  for (uint32_t t = lane; t < npairs; t += kWave) {
-    const uint32_t c = t / g.K, k = t - c * g.K;
-    const double* q = part + ((size_t)c * g.CiK + (size_t)ci * g.K + k) * S;
-    for (int i = 0; i < S; ++i) acc[i] += q[i];
-  }
-  for (int i = 0; i < S; ++i) out[i] = wave_sum(acc[i]);
-}
-
-// Stage 2 (conv): one wave per input channel (4 channels per 256-thread workgroup).
-__global__ __launch_bounds__(kBlock) void alpha_grad_stage2(
-    const double* __restrict__ part, const float* __restrict__ alpha, int S, Geo g,
-    uint32_t nchunk, float reg_lambda, float reg_b, const float* __restrict__ reg_dev,
-    float* __restrict__ galpha, float* __restrict__ reg_vals) {
-  if (reg_dev) {  // graph-capturable form: (lambda, b) read from device memory
-    reg_lambda = reg_dev[0];
-    reg_b = reg_dev[1];
-  }
-  const uint32_t ci = blockIdx.x * (kBlock / kWave) + threadIdx.x / kWave;
-  if (ci >= g.Ci) return;
-  double gp[kMaxS];
-  wave_colsum(part, g, ci, nchunk, S, gp);
-  if ((threadIdx.x & (kWave - 1)) != 0) return;
-  float a[kMaxS], ga[kMaxS];
-  load_row(alpha, ci, S, a);
-  const float reg = alpha_chain(a, S, gp, reg_lambda, reg_b, 0, ga);
-  for (int i = 0; i < S; ++i) galpha[(size_t)ci * S + i] = ga[i];
-  if (reg_vals) reg_vals[ci] = reg;
 }
 
 // Linear: alpha is per element, no reduction.
@@ -411,42 +336,6 @@ __device__ __forceinline__ float cand_err(float w, float d, uint32_t co, float s
   return __fmul_rn(r, r);
 }
 
-// stage 1 of shift init (conv): column partials of sum (w - X_i)^2 over a chunk of Co.
-__global__ __launch_bounds__(kBlock) void shift_mse_stage1(const float* __restrict__ W,
-                                                           const float* __restrict__ delta,
-                                                           Shifts sh, Geo g, uint32_t chunk,
-                                                           CandCfg cc,
-                                                           double* __restrict__ part) {
-  const uint32_t j = blockIdx.x * blockDim.x + threadIdx.x;
-  if (j >= g.CiK) return;
-  const uint32_t co0 = blockIdx.y * chunk, co1 = min(co0 + chunk, g.Co);
-  double acc[kMaxS];
-  for (int i = 0; i < sh.n; ++i) acc[i] = 0.0;
-  for (uint32_t co = co0; co < co1; ++co) {
-    const float w = W[co * g.CiK + j], d = delta[co];
-    for (int i = 0; i < sh.n; ++i) acc[i] += (double)cand_err(w, d, co, sh.s[i], cc);
-  }
-  double* o = part + ((size_t)blockIdx.y * g.CiK + j) * sh.n;
-  for (int i = 0; i < sh.n; ++i) o[i] = acc[i];
-}
-
-__global__ __launch_bounds__(kBlock) void shift_mse_stage2(const double* __restrict__ part, int S,
-                                                           Geo g, uint32_t nchunk,
-                                                           float* __restrict__ alpha,
-                                                           float* __restrict__ mse_out) {
-  const uint32_t ci = blockIdx.x * (kBlock / kWave) + threadIdx.x / kWave;
-  if (ci >= g.Ci) return;
-  double m[kMaxS];
-  wave_colsum(part, g, ci, nchunk, S, m);
-  if ((threadIdx.x & (kWave - 1)) != 0) return;
-  float a[kMaxS];
-  init_alpha_row(m, S, a);
-  for (int i = 0; i < S; ++i) {
-    alpha[(size_t)ci * S + i] = a[i];
-    if (mse_out) mse_out[(size_t)ci * S + i] = (float)m[i];
-  }
-}
-
 __global__ __launch_bounds__(kBlock) void shift_init_fc(const float* __restrict__ W,
                                                         const float* __restrict__ delta, Shifts sh,
                                                         Geo g, uint32_t n, CandCfg cc,
@@ -519,25 +408,6 @@ static int make_shifts(const float* shifts, int S, Shifts& sh) {
   return SSQ_OK;
 }
 
-// Co-chunking for the two-stage column reductions: aim for ~512 workgroups.
-static void chunking(const Geo& g, uint32_t& chunk, uint32_t& nchunk) {
-  const uint32_t colblk = (g.CiK + kBlock - 1) / kBlock;
-  uint32_t want = 512 / colblk;
-  const uint32_t max_chunks = (g.Co + 7) / 8;   // >= 8 rows per thread: few stage-2 partials
-  if (want > max_chunks) want = max_chunks;
-  if (want < 1) want = 1;
-  chunk = (g.Co + want - 1) / want;
-  nchunk = (g.Co + chunk - 1) / chunk;
-}
-
-static size_t colred_ws(int64_t Co, int64_t Ci, int64_t K, int S) {
-  Geo g;
-  if (make_geo(Co, Ci, K, 0, g) != SSQ_OK) return 0;
-  uint32_t chunk, nchunk;
-  chunking(g, chunk, nchunk);
-  return (size_t)nchunk * g.CiK * S * sizeof(double);
-}
-
 }  // namespace ssq
 
 using namespace ssq;
@@ -572,7 +442,93 @@ extern "C" int ssq_adashift_fwd(const float* W, const float* alpha, const float*
 
 extern "C" size_t ssq_adashift_bwd_workspace_size(int64_t Co, int64_t Ci, int64_t K, int S,
                                                   int is_fc) {
-  return is_fc ? 0 : colred_ws(Co, Ci, K, S);
+  (void)Co; (void)Ci; (void)K; (void)S; (void)is_fc;
+  return 0;  // per-input-channel reductions need no workspace
+}
+
+// ------------------------------------------------------------------ per-input-channel reduction
+// One workgroup per input channel ci: its threads sweep the (co, k) pairs of that channel
+// (Co*K elements, stride Ci*K between output rows -- the weight is L2/MALL resident), keep
+// S double accumulators, and reduce them deterministically (wave shuffle tree, then the
+// waves in fixed order).  One launch, no workspace.
+//   MODE 0: adaShift backward   sum g_int * F_i           -> softmax chain + regulariser
+//   MODE 1: lhs backward        sum gy * Xq_i             -> softmax chain
+//   MODE 2: shift init          sum (w - X_i)^2 (cc.mode) -> init_alpha logits (+ mse table)
+template <int MODE>
+__global__ __launch_bounds__(kBlock) void alpha_ci_kernel(
+    const float* __restrict__ gWhat, const float* __restrict__ W, const float* __restrict__ alpha,
+    const float* __restrict__ beta, const float* __restrict__ delta, const float* __restrict__ zp,
+    Shifts sh, Geo g, int hard_r, float lo, float hi, CandCfg cc, float reg_lambda, float reg_b,
+    const float* __restrict__ reg_dev, float* __restrict__ out_alpha, float* __restrict__ gbeta,
+    float* __restrict__ side) {
+  __shared__ double red[kBlock / kWave][kMaxS];
+  const uint32_t ci = blockIdx.x;
+  float p[kMaxS], F[kMaxS];
+  if (MODE != 2) {
+    float a[kMaxS];
+    load_row(alpha, ci, sh.n, a);
+    soft_targets<kMaxS>(a, sh.n, nullptr, p);
+  }
+  double acc[kMaxS];
+  for (int i = 0; i < sh.n; ++i) acc[i] = 0.0;
+  const uint32_t npairs = g.Co * g.K;
+  for (uint32_t t = threadIdx.x; t < npairs; t += blockDim.x) {
+    const uint32_t co = t / g.K, k = t - co * g.K;
+    const uint32_t e = co * g.CiK + ci * g.K + k;
+    const float w = W[e], d = delta[co];
+    if (MODE == 0) {
+      const float z = zp[co];
+      const float xf = soft_floor(w, d, sh, p, F);
+      const float b = beta[e];
+      const float hr = hard_r ? (b >= 0.0f ? 1.0f : 0.0f) : rect_sigmoid(b);
+      const float u = __fadd_rn(__fadd_rn(xf, hr), z);
+      const float gi = (u >= lo && u <= hi) ? __fmul_rn(gWhat[e], __fmul_rn(d, 1.0f)) : 0.0f;
+      if (gbeta) gbeta[e] = hard_r ? 0.0f : rect_sigmoid_grad(b, gi);
+      for (int i = 0; i < sh.n; ++i) acc[i] += (double)gi * (double)F[i];
+    } else if (MODE == 1) {
+      const float z = zp[co], gy = gWhat[e];
+      for (int i = 0; i < sh.n; ++i)
+        acc[i] += (double)gy * (double)cand_value<1>(w, d, z, sh.s[i], lo, hi);
+    } else {
+      for (int i = 0; i < sh.n; ++i) acc[i] += (double)cand_err(w, d, co, sh.s[i], cc);
+    }
+  }
+  const int lane = threadIdx.x & (kWave - 1), wv = threadIdx.x / kWave;
+  for (int i = 0; i < sh.n; ++i) {
+    const double v = wave_sum(acc[i]);
+    if (lane == 0) red[wv][i] = v;
+  }
+  __syncthreads();
+  if (threadIdx.x != 0) return;
+  double tot[kMaxS];
+  for (int i = 0; i < sh.n; ++i) {
+    tot[i] = 0.0;
+    for (int w2 = 0; w2 < (int)(blockDim.x / kWave); ++w2) tot[i] += red[w2][i];
+  }
+  if (MODE == 2) {
+    float a[kMaxS];
+    init_alpha_row(tot, sh.n, a);
+    for (int i = 0; i < sh.n; ++i) {
+      out_alpha[(size_t)ci * sh.n + i] = a[i];
+      if (side) side[(size_t)ci * sh.n + i] = (float)tot[i];
+    }
+    return;
+  }
+  if (reg_dev) {
+    reg_lambda = reg_dev[0];
+    reg_b = reg_dev[1];
+  }
+  float a[kMaxS], ga[kMaxS];
+  load_row(alpha, ci, sh.n, a);
+  const float reg = alpha_chain(a, sh.n, tot, MODE == 0 ? reg_lambda : 0.0f, reg_b, 0, ga);
+  for (int i = 0; i < sh.n; ++i) out_alpha[(size_t)ci * sh.n + i] = ga[i];
+  if (side && MODE == 0) side[ci] = reg;
+}
+
+static unsigned ci_threads(const Geo& g) {
+  const uint32_t pairs = g.Co * g.K;
+  const uint32_t t = (pairs + kWave - 1) / kWave * kWave;
+  return t >= (uint32_t)kBlock ? (unsigned)kBlock : (unsigned)t;
 }
 
 extern "C" int ssq_adashift_bwd(const float* gWhat, const float* W, const float* alpha,
@@ -594,16 +550,12 @@ extern "C" int ssq_adashift_bwd(const float* gWhat, const float* W, const float*
                        reg_lambda, reg_b, reg_dev, galpha, gbeta, reg_vals);
     return check_launch("ssq_adashift_bwd(fc)");
   }
-  SSQ_REQUIRE(ws && ws_bytes >= colred_ws(Co, Ci, K, S), SSQ_E_WS,
-              "ssq_adashift_bwd: workspace too small");
-  uint32_t chunk, nchunk;
-  chunking(g, chunk, nchunk);
-  hipLaunchKernelGGL(alpha_grad_stage1<0>, dim3((g.CiK + kBlock - 1) / kBlock, nchunk),
-                     dim3(kBlock), 0, s, gWhat, W, alpha, beta, delta, zp, sh, g, chunk,
-                     hard_round, (float)qmin, (float)qmax, (double*)ws, gbeta);
-  hipLaunchKernelGGL(alpha_grad_stage2, dim3((g.Ci + 3) / 4), dim3(kBlock), 0, s,
-                     (const double*)ws, alpha, S, g, nchunk, reg_lambda, reg_b, reg_dev, galpha,
-                     reg_vals);
+  (void)ws;
+  (void)ws_bytes;
+  const CandCfg cc{nullptr, 0, 0.0f, 0.0f};
+  hipLaunchKernelGGL(alpha_ci_kernel<0>, dim3(g.Ci), dim3(ci_threads(g)), 0, s, gWhat, W, alpha,
+                     beta, delta, zp, sh, g, hard_round, (float)qmin, (float)qmax, cc, reg_lambda,
+                     reg_b, reg_dev, galpha, gbeta, reg_vals);
   return check_launch("ssq_adashift_bwd");
 }
 
@@ -646,15 +598,12 @@ extern "C" int ssq_lhs_bwd(const float* gWhat, const float* W, const float* alph
                        0.0f, nullptr, galpha, nullptr, nullptr);
     return check_launch("ssq_lhs_bwd(fc)");
   }
-  SSQ_REQUIRE(ws && ws_bytes >= colred_ws(Co, Ci, K, S), SSQ_E_WS,
-              "ssq_lhs_bwd: workspace too small");
-  uint32_t chunk, nchunk;
-  chunking(g, chunk, nchunk);
-  hipLaunchKernelGGL(alpha_grad_stage1<1>, dim3((g.CiK + kBlock - 1) / kBlock, nchunk),
-                     dim3(kBlock), 0, s, gWhat, W, alpha, nullptr, delta, zp, sh, g, chunk, 0,
-                     (float)qmin, (float)qmax, (double*)ws, nullptr);
-  hipLaunchKernelGGL(alpha_grad_stage2, dim3((g.Ci + 3) / 4), dim3(kBlock), 0, s,
-                     (const double*)ws, alpha, S, g, nchunk, 0.0f, 0.0f, nullptr, galpha, nullptr);
+  (void)ws;
+  (void)ws_bytes;
+  const CandCfg cc{nullptr, 0, 0.0f, 0.0f};
+  hipLaunchKernelGGL(alpha_ci_kernel<1>, dim3(g.Ci), dim3(ci_threads(g)), 0, s, gWhat, W, alpha,
+                     nullptr, delta, zp, sh, g, 0, (float)qmin, (float)qmax, cc, 0.0f, 0.0f,
+                     nullptr, galpha, nullptr, nullptr);
   return check_launch("ssq_lhs_bwd");
 }
 
@@ -706,7 +655,8 @@ extern "C" int ssq_get_delta(const float* delta, const float* alpha, const float
 
 extern "C" size_t ssq_shift_init_workspace_size(int64_t Co, int64_t Ci, int64_t K, int S,
                                                 int is_fc) {
-  return is_fc ? 0 : colred_ws(Co, Ci, K, S);
+  (void)Co; (void)Ci; (void)K; (void)S; (void)is_fc;
+  return 0;  // per-input-channel reductions need no workspace
 }
 
 extern "C" int ssq_shift_init(const float* W, const float* delta, const float* zp,
@@ -724,14 +674,11 @@ extern "C" int ssq_shift_init(const float* W, const float* delta, const float* z
     hipLaunchKernelGGL(shift_init_fc, dim3(grid_for(n, kBlock)), dim3(kBlock), 0, s, W, delta, sh,
                        g, n, cc, alpha, mse_out);
   } else {
-    SSQ_REQUIRE(ws && ws_bytes >= colred_ws(Co, Ci, K, S), SSQ_E_WS,
-                "ssq_shift_init: workspace too small");
-    uint32_t chunk, nchunk;
-    chunking(g, chunk, nchunk);
-    hipLaunchKernelGGL(shift_mse_stage1, dim3((g.CiK + kBlock - 1) / kBlock, nchunk), dim3(kBlock),
-                       0, s, W, delta, sh, g, chunk, cc, (double*)ws);
-    hipLaunchKernelGGL(shift_mse_stage2, dim3((g.Ci + 3) / 4), dim3(kBlock), 0, s,
-                       (const double*)ws, S, g, nchunk, alpha, mse_out);
+    (void)ws;
+    (void)ws_bytes;
+    hipLaunchKernelGGL(alpha_ci_kernel<2>, dim3(g.Ci), dim3(ci_threads(g)), 0, s, nullptr, W,
+                       nullptr, nullptr, delta, nullptr, sh, g, 0, 0.0f, 0.0f, cc, 0.0f, 0.0f,
+                       nullptr, alpha, nullptr, mse_out);
   }
   if (beta)  // init_v_beta: beta from delta * s[argmax p(alpha)] (channelQuant.py:289-292)
     hipLaunchKernelGGL(beta_from_alpha_kernel, dim3(grid_for(n, kBlock)), dim3(kBlock), 0, s, W,
