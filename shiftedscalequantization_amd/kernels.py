@@ -55,14 +55,20 @@ def _zp_like(zp, delta):
         zp.reshape(zp.shape + (1,) * (delta.dim() - zp.dim())).expand(delta.shape).contiguous()
 
 
-def fake_quant_fwd(x, delta, zp, n_bits, sym=False, scale=1.0, codes=False):
-    """UniformAffineQuantizer.forward (quant_layer.py:92-98). Returns (y, codes|None)."""
+def fake_quant_fwd(x, delta, zp, n_bits, sym=False, scale=1.0, codes=False, out=None):
+    """UniformAffineQuantizer.forward (quant_layer.py:92-98). Returns (y, codes|None);
+    `out` (same shape, fp32, on the device) receives y when given."""
     x, xp = fptr(x, "x")
     delta, dp = fptr(delta.detach(), "delta")
     zp, zpp = fptr(_zp_like(zp.detach(), delta), "zero_point")
     inner, nch = _channel_layout(x, delta)
     lo, hi = qrange(n_bits, sym)
-    y = torch.empty_like(x)
+    if out is not None:
+        y, _ = fptr(out, "out")
+        if y.shape != x.shape or y is not out:
+            raise A.SSQError("fake_quant_fwd: out must be a contiguous tensor shaped like x")
+    else:
+        y = torch.empty_like(x)
     cb = _codes_buf(x, codes)
     call("ssq_fq_fwd", xp, _vp(y), _vp(cb), dp, zpp, x.numel(), inner, nch, float(scale), lo, hi,
          stream_of(x))

@@ -112,6 +112,40 @@ def test_fq_ragged_sizes(K, n):
     np.testing.assert_array_equal(c.cpu().numpy(), rq.astype(np.uint8))
 
 
+def _boundary_inputs(d, n_per=4096, seed=5):
+    """Values x whose quotient x/d lands on or one ulp either side of the rounding
+    boundaries k+0.5 (rint) and k (floor), plus zeros, subnormals and huge values."""
+    gen = np.random.default_rng(seed)
+    k = gen.integers(-300, 300, n_per).astype(np.float32)
+    base = np.concatenate([(k + np.float32(0.5)) * np.float32(d), k * np.float32(d)]).astype(np.float32)
+    xs = [base, np.nextafter(base, np.float32(np.inf)), np.nextafter(base, np.float32(-np.inf)),
+          np.array([0.0, -0.0, 1e-45, -1e-45, 1e-40, -3e-39, 1e30, -1e30, 3e38], np.float32),
+          (gen.standard_normal(n_per) * 10).astype(np.float32)]
+    x = np.concatenate(xs).astype(np.float32)
+    return x[: len(x) // 4 * 4]
+
+
+@pytest.mark.parametrize("d", [0.05, 0.3, 1e-8, 7.0e-3, 2.0 ** -70, 3.0e20])
+def test_fq_division_is_ieee_exact(K, d):
+    """div_rn (reciprocal + two fma corrections) must equal the IEEE quotient bit for bit:
+    the fq kernel run with div_rn and with the compiler's divide (variant bit 27) agree,
+    and both match the oracle, on inputs sitting on the rint/floor boundaries."""
+    x = torch.from_numpy(_boundary_inputs(d))
+    dd, z = torch.tensor(np.float32(d)), torch.tensor(2.0)
+    old = K.set_variant(1 | (256 << 8))
+    try:
+        a, ca = K.fake_quant_fwd(x.cuda(), dd.cuda(), z.cuda(), 8, codes=True)
+        K.set_variant(1 | (256 << 8) | (1 << 27))
+        b, cb = K.fake_quant_fwd(x.cuda(), dd.cuda(), z.cuda(), 8, codes=True)
+    finally:
+        K.set_variant(old)
+    np.testing.assert_array_equal(host(a).view(np.int32), host(b).view(np.int32))
+    np.testing.assert_array_equal(ca.cpu().numpy(), cb.cpu().numpy())
+    ry, rq = R.fake_quant(x.numpy(), dd.numpy(), z.numpy(), 8)
+    np.testing.assert_array_equal(host(a), ry)
+    np.testing.assert_array_equal(ca.cpu().numpy(), rq.astype(np.uint8))
+
+
 def test_fq_per_channel_unaligned(K):
     # conv1-like rows of 147 elements: float4 vectors straddle channel boundaries
     gen = torch.Generator().manual_seed(3)
