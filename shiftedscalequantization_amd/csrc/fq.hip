@@ -32,13 +32,11 @@ int check_launch(const char* what) {
 
 // ------------------------------------------------------------------ element op
 struct QParams {
-  float d, z, lo, hi, r;   // r = recip_for_div(d)
+  float d, z, lo, hi;
 };
 
-template <bool IEEE = false>
 __device__ __forceinline__ float fq1(float x, const QParams& p, float* qout) {
-  // x / delta, correctly rounded (div_rn == the IEEE divide bit for bit)
-  const float t = IEEE ? x / p.d : div_rn(x, p.d, p.r);
+  float t = x / p.d;                       // IEEE fp32 divide (x / delta)
   float v = __fadd_rn(rintf(t), p.z);      // round_ste fwd == round half-even, + zp
   float q = clampf(v, p.lo, p.hi);         // clamp(x_int, lo, hi)
   *qout = q;
@@ -50,8 +48,10 @@ __device__ __forceinline__ uint32_t pack4(float a, float b, float c, float d) {
          ((uint32_t)((int)c & 0xff) << 16) | ((uint32_t)((int)d & 0xff) << 24);
 }
 
-// chunk == 0: grid-stride; chunk > 0: workgroup b owns float4s [b*chunk, (b+1)*chunk)
-// and its threads stride through them.
+// Per-tensor: delta/zp are wave-uniform scalars.  Each thread keeps UNROLL 16-B loads
+// in flight (1 KiB per wave-instruction); NTL/NTS select the streaming cache policy of
+// loads/stores.  chunk == 0: grid-stride; chunk > 0: workgroup b owns float4s
+// [b*chunk, (b+1)*chunk) and its threads stride through them.
 __device__ __forceinline__ void stream_range(int64_t n4, int64_t chunk, int64_t& i, int64_t& end,
                                              int64_t& stride) {
   if (chunk > 0) {
@@ -65,10 +65,21 @@ __device__ __forceinline__ void stream_range(int64_t n4, int64_t chunk, int64_t&
   }
 }
 
-template <bool CODES, int UNROLL, bool NTL, bool NTS, bool IEEE>
-__device__ __forceinline__ void fq_pt_body(const f32x4* __restrict__ x, f32x4* __restrict__ y,
-                                           uint32_t* __restrict__ codes, const QParams& p,
-                                           int64_t i, int64_t end, int64_t stride) {
+template <bool CODES, int UNROLL, bool NTL, bool NTS>
+__global__ __launch_bounds__(1024) void fq_fwd_pt(const f32x4* __restrict__ x,
+                                                  f32x4* __restrict__ y,
+                                                  uint32_t* __restrict__ codes,
+                                                  const float* __restrict__ delta,
+                                                  const float* __restrict__ zp, int64_t n4,
+                                                  float scale, float lo, float hi,
+                                                  int64_t chunk) {
+  QParams p;
+  p.d = __fmul_rn(delta[0], scale);
+  p.z = zp[0];
+  p.lo = lo;
+  p.hi = hi;
+  int64_t i, end, stride;
+  stream_range(n4, chunk, i, end, stride);
   for (; i + (UNROLL - 1) * stride < end; i += UNROLL * stride) {
     f32x4 v[UNROLL];
 #pragma unroll
@@ -77,10 +88,10 @@ __device__ __forceinline__ void fq_pt_body(const f32x4* __restrict__ x, f32x4* _
     for (int u = 0; u < UNROLL; ++u) {
       f32x4 o;
       float q0, q1, q2, q3;
-      o.x = fq1<IEEE>(v[u].x, p, &q0);
-      o.y = fq1<IEEE>(v[u].y, p, &q1);
-      o.z = fq1<IEEE>(v[u].z, p, &q2);
-      o.w = fq1<IEEE>(v[u].w, p, &q3);
+      o.x = fq1(v[u].x, p, &q0);
+      o.y = fq1(v[u].y, p, &q1);
+      o.z = fq1(v[u].z, p, &q2);
+      o.w = fq1(v[u].w, p, &q3);
       st4<NTS>(o, &y[i + u * stride]);
       if (CODES) codes[i + u * stride] = pack4(q0, q1, q2, q3);
     }
@@ -88,38 +99,13 @@ __device__ __forceinline__ void fq_pt_body(const f32x4* __restrict__ x, f32x4* _
   for (; i < end; i += stride) {
     f32x4 v = x[i], o;
     float q0, q1, q2, q3;
-    o.x = fq1<IEEE>(v.x, p, &q0);
-    o.y = fq1<IEEE>(v.y, p, &q1);
-    o.z = fq1<IEEE>(v.z, p, &q2);
-    o.w = fq1<IEEE>(v.w, p, &q3);
+    o.x = fq1(v.x, p, &q0);
+    o.y = fq1(v.y, p, &q1);
+    o.z = fq1(v.z, p, &q2);
+    o.w = fq1(v.w, p, &q3);
     y[i] = o;
     if (CODES) codes[i] = pack4(q0, q1, q2, q3);
   }
-}
-
-// Per-tensor: delta/zp are wave-uniform scalars.  Each thread keeps UNROLL 16-B loads
-// in flight (1 KiB per wave-instruction); NTL/NTS select the streaming cache policy of
-// loads/stores.  chunk == 0: grid-stride; chunk > 0: workgroup b owns float4s
-// [b*chunk, (b+1)*chunk) and its threads stride through them.  ieee != 0 selects the
-// compiler's IEEE divide instead of div_rn (A/B only; both are bit-identical).
-template <bool CODES, int UNROLL, bool NTL, bool NTS>
-__global__ __launch_bounds__(1024) void fq_fwd_pt(const f32x4* __restrict__ x,
-                                                  f32x4* __restrict__ y,
-                                                  uint32_t* __restrict__ codes,
-                                                  const float* __restrict__ delta,
-                                                  const float* __restrict__ zp, int64_t n4,
-                                                  float scale, float lo, float hi,
-                                                  int64_t chunk, int ieee) {
-  QParams p;
-  p.d = __fmul_rn(delta[0], scale);
-  p.z = zp[0];
-  p.lo = lo;
-  p.hi = hi;
-  p.r = recip_for_div(p.d);
-  int64_t i, end, stride;
-  stream_range(n4, chunk, i, end, stride);
-  if (ieee) fq_pt_body<CODES, UNROLL, NTL, NTS, true>(x, y, codes, p, i, end, stride);
-  else fq_pt_body<CODES, UNROLL, NTL, NTS, false>(x, y, codes, p, i, end, stride);
 }
 
 // General scalar path: any alignment, per-channel c = (i / inner) % nch.
@@ -139,7 +125,6 @@ __global__ __launch_bounds__(kBlock) void fq_fwd_scalar(const float* __restrict_
     p.z = zp[c];
     p.lo = lo;
     p.hi = hi;
-    p.r = recip_for_div(p.d);
     float q;
     y[i] = fq1(x[i], p, &q);
     if (codes) codes[i] = (uint8_t)((int)q & 0xff);
@@ -175,7 +160,6 @@ __global__ __launch_bounds__(kBlock) void fq_fwd_pc(const f32x4* __restrict__ x,
       p.z = zp[cc];
       p.lo = lo;
       p.hi = hi;
-      p.r = recip_for_div(p.d);
       out[j] = fq1(in[j], p, &q[j]);
     }
     o.x = out[0];
@@ -208,7 +192,7 @@ struct SegTable {
 // One workgroup = one tile of one segment.  The (delta, zp) of every channel the tile
 // touches are staged in LDS once, then each element reads its pair from LDS.
 __global__ __launch_bounds__(kBlock) void fq_fwd_multi_kernel(SegTable tab) {
-  __shared__ float sd[kTile + 2], sz[kTile + 2], sr[kTile + 2];
+  __shared__ float sd[kTile + 2], sz[kTile + 2];
   int si = 0;
   while (si + 1 < tab.nseg && (int64_t)blockIdx.x >= tab.s[si + 1].blk0) ++si;
   const Seg sg = tab.s[si];
@@ -216,15 +200,13 @@ __global__ __launch_bounds__(kBlock) void fq_fwd_multi_kernel(SegTable tab) {
   const int64_t t1 = min(t0 + (int64_t)kTile, sg.n);
   const int64_t c0 = t0 / sg.inner, c1 = (t1 - 1) / sg.inner;
   for (int64_t c = c0 + threadIdx.x; c <= c1; c += blockDim.x) {
-    const float d = sg.delta[c % sg.nch];
-    sd[c - c0] = d;
+    sd[c - c0] = sg.delta[c % sg.nch];
     sz[c - c0] = sg.zp[c % sg.nch];
-    sr[c - c0] = recip_for_div(d);
   }
   __syncthreads();
   for (int64_t e = t0 + threadIdx.x; e < t1; e += blockDim.x) {
     const int64_t cl = e / sg.inner - c0;
-    QParams p{sd[cl], sz[cl], sg.lo, sg.hi, sr[cl]};
+    QParams p{sd[cl], sz[cl], sg.lo, sg.hi};
     float q;
     sg.y[e] = fq1(sg.x[e], p, &q);
   }
@@ -344,15 +326,14 @@ __global__ __launch_bounds__(1024) void copy_kernel(const f32x4* __restrict__ s,
 
 // Tuning variant of the streaming kernels (bench A/B only):
 //   bits 0-1 cache policy: 0 plain, 1 NT load+store, 2 NT load only, 3 NT store only
-//   bits 4-7 unroll: 0 -> 4, 1 -> 1, 2 -> 2, 3 -> 8
+//   bits 4-7 unroll: 0 -> 4, 1 -> 1, 2 -> 2, 3 -> 8, 4 -> 16
 //   bits 8-23 grid size in workgroups (0 -> 2048)
 //   bit  24   chunked (workgroup-contiguous) instead of grid-stride
 //   bits 25-26 workgroup size: 0 -> 256, 1 -> 512, 2 -> 1024
-//   bit  27   q/dq divides with the compiler's IEEE divide instead of div_rn
 static int g_variant = 1 | (256 << 8);  // NT load+store, unroll 4, 1 workgroup per CU (sweep: tools/sweep_stream.py)
 
 struct Variant {
-  bool ntl, nts, chunked, ieee;
+  bool ntl, nts, chunked;
   int unroll, grid, block;
 };
 static Variant decode_variant(int v) {
@@ -361,13 +342,12 @@ static Variant decode_variant(int v) {
   r.ntl = pol == 1 || pol == 2;
   r.nts = pol == 1 || pol == 3;
   const int u = (v >> 4) & 0xF;
-  r.unroll = u == 1 ? 1 : u == 2 ? 2 : u == 3 ? 8 : 4;
+  r.unroll = u == 1 ? 1 : u == 2 ? 2 : u == 3 ? 8 : u == 4 ? 16 : 4;
   r.grid = (v >> 8) & 0xFFFF;
   if (r.grid == 0) r.grid = 2048;
   r.chunked = (v >> 24) & 1;
   const int b = (v >> 25) & 3;
   r.block = b == 1 ? 512 : b == 2 ? 1024 : 256;
-  r.ieee = (v >> 27) & 1;
   return r;
 }
 
@@ -399,7 +379,7 @@ static void launch_stream(const Variant& v, dim3 grid, dim3 block, hipStream_t s
     else L<U, false, false>::go(grid, block, s, args...);                             \
     return;                                                                           \
   }
-  SSQ_CASE(1) SSQ_CASE(2) SSQ_CASE(4) SSQ_CASE(8)
+  SSQ_CASE(1) SSQ_CASE(2) SSQ_CASE(4) SSQ_CASE(8) SSQ_CASE(16)
 #undef SSQ_CASE
 }
 
@@ -407,18 +387,18 @@ template <int U, bool NTL, bool NTS>
 struct FqPtCodes {
   static void go(dim3 g, dim3 b, hipStream_t s, const f32x4* x, f32x4* y, uint32_t* c,
                  const float* d, const float* z, int64_t n4, float sc, float lo, float hi,
-                 int64_t chunk, int ieee) {
+                 int64_t chunk) {
     hipLaunchKernelGGL((fq_fwd_pt<true, U, NTL, NTS>), g, b, 0, s, x, y, c, d, z, n4, sc, lo, hi,
-                       chunk, ieee);
+                       chunk);
   }
 };
 template <int U, bool NTL, bool NTS>
 struct FqPt {
   static void go(dim3 g, dim3 b, hipStream_t s, const f32x4* x, f32x4* y, uint32_t* c,
                  const float* d, const float* z, int64_t n4, float sc, float lo, float hi,
-                 int64_t chunk, int ieee) {
+                 int64_t chunk) {
     hipLaunchKernelGGL((fq_fwd_pt<false, U, NTL, NTS>), g, b, 0, s, x, y, c, d, z, n4, sc, lo, hi,
-                       chunk, ieee);
+                       chunk);
   }
 };
 template <int U, bool NTL, bool NTS>
@@ -466,10 +446,9 @@ extern "C" int ssq_fq_fwd(const float* x, float* y, void* codes, const float* de
       uint32_t* cv = (uint32_t*)codes;
       if (codes)
         launch_stream<FqPtCodes>(v, grid, block, s, xv, yv, cv, delta, zp, n4, scale, lo, hi,
-                                 chunk, (int)v.ieee);
+                                 chunk);
       else
-        launch_stream<FqPt>(v, grid, block, s, xv, yv, cv, delta, zp, n4, scale, lo, hi, chunk,
-                            (int)v.ieee);
+        launch_stream<FqPt>(v, grid, block, s, xv, yv, cv, delta, zp, n4, scale, lo, hi, chunk);
     } else {
       SSQ_REQUIRE(inner < (1ll << 31) && nch < (1ll << 31), SSQ_E_ARG, "ssq_fq_fwd: dims");
       const int grid = grid_for(n4, kBlock, 4096);

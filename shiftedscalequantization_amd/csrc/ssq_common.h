@@ -54,28 +54,6 @@ __device__ __forceinline__ void st4(f32x4 v, f32x4* p) {
 }
 
 // ---------------------------------------------------------------- device math
-// Correctly rounded x / d from a precomputed reciprocal r = RN(1/d): q0 = x*r is within
-// 1.5 ulp, one fma residual/correction step makes it faithful, and a second one
-// (Markstein: r within 1/2 ulp of 1/d, q1 faithful => RN(q1 + RN(x - d*q1)*r) == RN(x/d))
-// yields the IEEE quotient bit for bit -- the same sequence the compiler's divide runs
-// after its rcp refinement, minus the per-element div_scale/rcp/div_fixup.  The premise
-// needs the residuals to stay normal: outside |x|, |d| in [2^-60, 2^60] (r == 0 marks a
-// bad d, see recip_for_div) the IEEE divide runs instead.  Zero x (ReLU activations) is
-// on the fast path: x*r carries the sign of x/d.
-__device__ __forceinline__ float recip_for_div(float d) {
-  const float a = fabsf(d);
-  return (a >= 0x1p-60f && a <= 0x1p60f) ? 1.0f / d : 0.0f;
-}
-__device__ __forceinline__ float div_rn(float x, float d, float r) {
-  const float q0 = __fmul_rn(x, r);
-  const float q1 = __fmaf_rn(__fmaf_rn(-q0, d, x), r, q0);
-  const float q2 = __fmaf_rn(__fmaf_rn(-q1, d, x), r, q1);
-  const float ax = fabsf(x);
-  if (__builtin_expect(r == 0.0f || !(ax <= 0x1p60f) || (ax < 0x1p-60f && ax != 0.0f), 0))
-    return x / d;
-  return ax == 0.0f ? q0 : q2;
-}
-
 __device__ __forceinline__ float clampf(float v, float lo, float hi) {
   // torch.clamp semantics on finite values: min(max(v, lo), hi)
   return fminf(fmaxf(v, lo), hi);

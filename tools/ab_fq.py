@@ -1,7 +1,7 @@
-"""Focused A/B of the per-tensor q/dq kernel: division form (div_rn vs IEEE divide) x a
-few launch geometries, against the float4 copy of the same tensor; interleaved rounds in
-one process (cdna_hip_programming.md §5.4 rule 24).  Also checks that both division
-forms give bit-identical outputs on the full tensor."""
+"""Focused A/B of the per-tensor q/dq kernel over launch geometries (grid, block,
+unroll, chunked, cache policy), each against the float4 copy of the same tensor with
+the same geometry; interleaved rounds in one process (cdna_hip_programming.md §5.4
+rule 24).  Prints rows sorted by median q/dq GB/s."""
 import json
 import os
 import sys
@@ -16,18 +16,24 @@ x = torch.empty(1024, 64, 56, 56, device=dev).normal_().relu_()
 y = torch.empty_like(x)
 d, z, _ = K.scale_init(x[:64], 4, False, False, "mse")
 n = x.numel()
-IEEE = 1 << 27
-base = 1 | (256 << 8)                       # NT, unroll 4, grid 256, block 256
+U = {1: 1, 2: 2, 4: 0, 8: 3, 16: 4}
+B = {256: 0, 512: 1, 1024: 2}
 
-# bit-identical check
-K.set_variant(base)
-a = K.fake_quant_fwd(x, d, z, 4)[0]
-K.set_variant(base | IEEE)
-b = K.fake_quant_fwd(x, d, z, 4)[0]
-torch.cuda.synchronize()
-same = bool(torch.equal(a.view(torch.int32), b.view(torch.int32)))
-print(json.dumps({"bit_identical_div_rn_vs_ieee": same}))
-assert same
+
+def var(grid, block=256, unroll=4, chunked=0, pol=1):
+    return pol | (U[unroll] << 4) | (grid << 8) | (chunked << 24) | (B[block] << 25)
+
+
+geoms = {}
+for grid in (256, 512, 1024):
+    for block in (256, 512):
+        for unroll in (4, 8, 16):
+            for ch in (0, 1):
+                if block * unroll > 4096:
+                    continue
+                geoms[f"g{grid}b{block}u{unroll}c{ch}"] = var(grid, block, unroll, ch)
+geoms["g256b256u8c0_plain"] = var(256, 256, 8, 0, pol=0)
+geoms["g256b256u8c0_ntstore"] = var(256, 256, 8, 0, pol=3)
 
 
 def t(fn, reps=20):
@@ -41,21 +47,15 @@ def t(fn, reps=20):
     return s.elapsed_time(e) / reps
 
 
-geoms = {"g256b256": 1 | (256 << 8), "g512b256": 1 | (512 << 8), "g1024b256": 1 | (1024 << 8),
-         "g512b512": 1 | (512 << 8) | (1 << 25), "g256b1024ch": 1 | (256 << 8) | (1 << 24) | (2 << 25),
-         "g1024b1024ch": 1 | (1024 << 8) | (1 << 24) | (2 << 25),
-         "g2048b256u2": 1 | (2 << 4) | (2048 << 8), "g256b256u8": 1 | (3 << 4) | (256 << 8)}
 res = {}
 for rnd in range(5):
     for name, v in geoms.items():
-        for div in ("rn", "ieee"):
-            K.set_variant(v | (IEEE if div == "ieee" else 0))
-            res.setdefault((name, div), []).append(8 * n / t(lambda: K.fake_quant_fwd(x, d, z, 4, out=y)) / 1e6)
         K.set_variant(v)
+        res.setdefault((name, "fq"), []).append(8 * n / t(lambda: K.fake_quant_fwd(x, d, z, 4, out=y)) / 1e6)
         res.setdefault((name, "copy"), []).append(8 * n / t(lambda: K.stream_copy(x, y)) / 1e6)
-K.set_variant(base)
-rows = [{"geom": k[0], "kind": k[1], "gbs_med": round(sorted(v)[len(v) // 2], 1),
-         "gbs_max": round(max(v), 1)} for k, v in res.items()]
+K.set_variant(var(256))
+rows = [{"geom": k[0], "kind": k[1], "variant": geoms[k[0]], "gbs_med": round(sorted(v)[len(v) // 2], 1),
+         "gbs_min": round(min(v), 1)} for k, v in res.items()]
 rows.sort(key=lambda r: -r["gbs_med"])
 for r in rows:
     print(json.dumps(r))
