@@ -172,41 +172,99 @@ __global__ __launch_bounds__(kBlock) void fq_fwd_pc(const f32x4* __restrict__ x,
 }
 
 // ------------------------------------------------------------------ multi-tensor forward
+// n / d for 0 <= n < 2^31 as (umulhi(n, m) + n) >> s (round-up magic number, exact).
+struct FastDiv {
+  uint32_t m, s;
+};
+static FastDiv make_fastdiv(uint32_t d) {
+  uint32_t s = 0;
+  while (s < 32 && (1ull << s) < d) ++s;
+  const uint64_t m = ((1ull << 32) * ((1ull << s) - d)) / d + 1;
+  return FastDiv{(uint32_t)m, s};
+}
+__device__ __forceinline__ uint32_t fdiv(uint32_t n, FastDiv f) {
+  return (__umulhi(n, f.m) + n) >> f.s;
+}
+
 struct Seg {
   const float* x;
   float* y;
   const float* delta;
   const float* zp;
-  int64_t n;
-  int64_t blk0;  // first workgroup of this segment
+  uint32_t n;     // elements (< 2^31)
+  uint32_t blk0;  // first workgroup of this segment
   uint32_t inner, nch;
   float lo, hi;
+  FastDiv div_inner;
+  uint32_t vec;   // x and y 16-B aligned: float4 path
 };
-constexpr int kMaxSeg = 64;
-constexpr int kTile = 4096;  // elements per workgroup (16 per thread)
+constexpr int kMaxSeg = 48;      // keeps the by-value table under 4 KiB of kernel arguments
+constexpr int kTile = 4096;      // elements per workgroup: 4 float4 per thread
 struct SegTable {
   Seg s[kMaxSeg];
   int nseg;
 };
 
 // One workgroup = one tile of one segment.  The (delta, zp) of every channel the tile
-// touches are staged in LDS once, then each element reads its pair from LDS.
+// touches are staged in LDS once; each thread then issues its 4 float4 loads before any
+// math (16 B/lane, 4 KiB per wave in flight) and finds channels with a magic-number
+// division (no 64-bit divides).  A float4 may straddle a channel boundary (inner % 4).
 __global__ __launch_bounds__(kBlock) void fq_fwd_multi_kernel(SegTable tab) {
   __shared__ float sd[kTile + 2], sz[kTile + 2];
   int si = 0;
-  while (si + 1 < tab.nseg && (int64_t)blockIdx.x >= tab.s[si + 1].blk0) ++si;
-  const Seg sg = tab.s[si];
-  const int64_t t0 = ((int64_t)blockIdx.x - sg.blk0) * kTile;
-  const int64_t t1 = min(t0 + (int64_t)kTile, sg.n);
-  const int64_t c0 = t0 / sg.inner, c1 = (t1 - 1) / sg.inner;
-  for (int64_t c = c0 + threadIdx.x; c <= c1; c += blockDim.x) {
+  while (si + 1 < tab.nseg && blockIdx.x >= tab.s[si + 1].blk0) ++si;
+  const Seg& sg = tab.s[si];
+  const uint32_t t0 = (blockIdx.x - sg.blk0) * (uint32_t)kTile;
+  const uint32_t t1 = min(t0 + (uint32_t)kTile, sg.n);
+  const uint32_t c0 = fdiv(t0, sg.div_inner), c1 = fdiv(t1 - 1, sg.div_inner);
+  for (uint32_t c = c0 + threadIdx.x; c <= c1; c += blockDim.x) {
     sd[c - c0] = sg.delta[c % sg.nch];
     sz[c - c0] = sg.zp[c % sg.nch];
   }
   __syncthreads();
-  for (int64_t e = t0 + threadIdx.x; e < t1; e += blockDim.x) {
-    const int64_t cl = e / sg.inner - c0;
-    QParams p{sd[cl], sz[cl], sg.lo, sg.hi};
+  const float lo = sg.lo, hi = sg.hi;
+  uint32_t e_tail = t0;
+  if (sg.vec) {
+    constexpr int U = kTile / 4 / kBlock;
+    const uint32_t v0 = t0 / 4, v1 = t1 / 4;  // whole float4s of the tile
+    const f32x4* xv = (const f32x4*)sg.x;
+    f32x4* yv = (f32x4*)sg.y;
+    f32x4 in[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const uint32_t v = v0 + threadIdx.x + u * kBlock;
+      if (v < v1) in[u] = __builtin_nontemporal_load(&xv[v]);
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const uint32_t v = v0 + threadIdx.x + u * kBlock;
+      if (v >= v1) continue;
+      const uint32_t e = v * 4;
+      uint32_t c = fdiv(e, sg.div_inner);
+      uint32_t next = (c + 1) * sg.inner;
+      float a[4] = {in[u].x, in[u].y, in[u].z, in[u].w}, o[4];
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        while (e + j >= next) {
+          ++c;
+          next += sg.inner;
+        }
+        QParams p{sd[c - c0], sz[c - c0], lo, hi};
+        float q;
+        o[j] = fq1(a[j], p, &q);
+      }
+      f32x4 r;
+      r.x = o[0];
+      r.y = o[1];
+      r.z = o[2];
+      r.w = o[3];
+      __builtin_nontemporal_store(r, &yv[v]);
+    }
+    e_tail = v1 * 4;
+  }
+  for (uint32_t e = e_tail + threadIdx.x; e < t1; e += blockDim.x) {
+    const uint32_t cl = fdiv(e, sg.div_inner) - c0;
+    QParams p{sd[cl], sz[cl], lo, hi};
     float q;
     sg.y[e] = fq1(sg.x[e], p, &q);
   }
@@ -474,26 +532,36 @@ extern "C" int ssq_fq_fwd_multi(int nseg, const float* const* x, float* const* y
                                 const float* const* delta, const float* const* zp,
                                 const int64_t* n, const int64_t* inner, const int64_t* nch,
                                 const int* qmin, const int* qmax, ssq_stream_t stream) {
-  SSQ_REQUIRE(nseg >= 1 && nseg <= kMaxSeg, SSQ_E_ARG, "ssq_fq_fwd_multi: 1 <= nseg <= %d",
-              kMaxSeg);
-  SegTable tab;
-  tab.nseg = nseg;
-  int64_t blk = 0;
+  SSQ_REQUIRE(nseg >= 1 && x && y && delta && zp && n && inner && nch && qmin && qmax,
+              SSQ_E_ARG, "ssq_fq_fwd_multi: nseg >= 1 and non-null arrays required");
   for (int i = 0; i < nseg; ++i) {
     SSQ_REQUIRE(n[i] >= 1 && inner[i] >= 1 && nch[i] >= 1 && qmin[i] < qmax[i], SSQ_E_ARG,
                 "ssq_fq_fwd_multi: bad segment %d", i);
     SSQ_REQUIRE(x[i] && y[i] && delta[i] && zp[i], SSQ_E_ARG,
                 "ssq_fq_fwd_multi: null pointer in segment %d", i);
-    SSQ_REQUIRE(inner[i] < (1ll << 31) && nch[i] < (1ll << 31), SSQ_E_ARG,
-                "ssq_fq_fwd_multi: dims");
-    tab.s[i] = Seg{x[i], y[i], delta[i], zp[i], n[i], blk, (uint32_t)inner[i], (uint32_t)nch[i],
-                   (float)qmin[i], (float)qmax[i]};
-    blk += (n[i] + kTile - 1) / kTile;
+    SSQ_REQUIRE(n[i] < (1ll << 31) && inner[i] < (1ll << 31) && nch[i] < (1ll << 31), SSQ_E_ARG,
+                "ssq_fq_fwd_multi: segment %d exceeds 2^31 elements", i);
   }
-  SSQ_REQUIRE(blk < (1ll << 31), SSQ_E_ARG, "ssq_fq_fwd_multi: too many tiles");
-  hipLaunchKernelGGL(fq_fwd_multi_kernel, dim3((unsigned)blk), dim3(kBlock), 0,
-                     (hipStream_t)stream, tab);
-  return check_launch("ssq_fq_fwd_multi");
+  // kMaxSeg segments per launch
+  for (int base = 0; base < nseg; base += kMaxSeg) {
+    SegTable tab;
+    tab.nseg = nseg - base < kMaxSeg ? nseg - base : kMaxSeg;
+    int64_t blk = 0;
+    for (int k = 0; k < tab.nseg; ++k) {
+      const int i = base + k;
+      const bool vec = aligned16(x[i]) && aligned16(y[i]);
+      tab.s[k] = Seg{x[i], y[i], delta[i], zp[i], (uint32_t)n[i], (uint32_t)blk,
+                     (uint32_t)inner[i], (uint32_t)nch[i], (float)qmin[i], (float)qmax[i],
+                     make_fastdiv((uint32_t)inner[i]), vec ? 1u : 0u};
+      blk += (n[i] + kTile - 1) / kTile;
+    }
+    SSQ_REQUIRE(blk < (1ll << 31), SSQ_E_ARG, "ssq_fq_fwd_multi: too many tiles");
+    hipLaunchKernelGGL(fq_fwd_multi_kernel, dim3((unsigned)blk), dim3(kBlock), 0,
+                       (hipStream_t)stream, tab);
+    const int rc = check_launch("ssq_fq_fwd_multi");
+    if (rc) return rc;
+  }
+  return SSQ_OK;
 }
 
 extern "C" size_t ssq_fq_bwd_workspace_size(int64_t n, int64_t inner, int64_t nch) {

@@ -162,6 +162,24 @@ def test_fq_multi_segment(K):
         np.testing.assert_array_equal(host(y), R.fake_quant(w.numpy(), p[0], p[1], 2)[0])
 
 
+def test_fq_multi_many_ragged_segments(K):
+    """More segments than one launch holds (ResNet-50 has 54 layers), rows of 1-3 and
+    odd lengths (float4s straddling channels), an unaligned view, tiles crossing rows."""
+    gen = torch.Generator().manual_seed(12)
+    shapes = []
+    for i in range(61):
+        shapes.append([(7, 1), (5, 2), (9, 3), (33, 3, 7, 7), (16, 5, 1, 1), (1000, 512),
+                       (64, 64, 3, 3), (3, 4099)][i % 8])
+    ws = [torch.randn(s, generator=gen) * 0.05 for s in shapes]
+    params = [R.init_scale(w.numpy(), 4, False, True, "max") for w in ws]
+    xs = [w.cuda() for w in ws]
+    big = torch.randn(1 + ws[5].numel(), generator=gen).cuda()
+    xs[5] = big[1:].view(ws[5].shape)           # not 16-B aligned -> scalar path
+    ys = K.fake_quant_multi(xs, [dev(p[0]) for p in params], [dev(p[1]) for p in params], 4)
+    for x, p, y in zip(xs, params, ys):
+        np.testing.assert_array_equal(host(y), R.fake_quant(host(x), p[0], p[1], 4)[0])
+
+
 # ------------------------------------------------------------------ K5-K9 on goldens
 def _cq(g, tag):
     w = g[tag + "_w"]
