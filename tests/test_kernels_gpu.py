@@ -112,6 +112,25 @@ def test_fq_ragged_sizes(K, n):
     np.testing.assert_array_equal(c.cpu().numpy(), rq.astype(np.uint8))
 
 
+@pytest.mark.parametrize("variant", [1 | (256 << 8) | (1 << 27), 1 | (3 << 4) | (512 << 8) | (1 << 27),
+                                     (2 << 4) | (64 << 8) | (1 << 24), 3 | (4 << 4) | (128 << 8)])
+def test_fq_streaming_variants(K, variant):
+    """Every launch-geometry / pipelining variant of the per-tensor kernel is bit-exact,
+    including sizes that end mid-step, mid-pipeline and inside the scalar tail."""
+    old = K.set_variant(variant)
+    try:
+        for n in (4, 1020, 65536 * 4 + 12, 256 * 256 * 4 * 9 + 3, 3 << 20):
+            gen = torch.Generator().manual_seed(n)
+            x = torch.randn(n, generator=gen)
+            d, z = torch.tensor(0.11), torch.tensor(7.0)
+            y, c = K.fake_quant_fwd(x.cuda(), d.cuda(), z.cuda(), 4, codes=True)
+            ry, rq = R.fake_quant(x.numpy(), d.numpy(), z.numpy(), 4)
+            np.testing.assert_array_equal(host(y), ry)
+            np.testing.assert_array_equal(c.cpu().numpy(), rq.astype(np.uint8))
+    finally:
+        K.set_variant(old)
+
+
 def _boundary_inputs(d, n_per=4096, seed=5):
     """Values x whose quotient x/d lands on or one ulp either side of the rounding
     boundaries k+0.5 (rint) and k (floor), plus zeros, subnormals and huge values."""

@@ -20,20 +20,19 @@ U = {1: 1, 2: 2, 4: 0, 8: 3, 16: 4}
 B = {256: 0, 512: 1, 1024: 2}
 
 
-def var(grid, block=256, unroll=4, chunked=0, pol=1):
-    return pol | (U[unroll] << 4) | (grid << 8) | (chunked << 24) | (B[block] << 25)
+def var(grid, block=256, unroll=4, chunked=0, pol=1, pipe=0):
+    return pol | (U[unroll] << 4) | (grid << 8) | (chunked << 24) | (B[block] << 25) | (pipe << 27)
 
 
 geoms = {}
-for grid in (256, 512, 1024):
+for grid in (256, 512):
     for block in (256, 512):
-        for unroll in (4, 8, 16):
-            for ch in (0, 1):
+        for unroll in (2, 4, 8):
+            for pipe in (0, 1):
                 if block * unroll > 4096:
                     continue
-                geoms[f"g{grid}b{block}u{unroll}c{ch}"] = var(grid, block, unroll, ch)
-geoms["g256b256u8c0_plain"] = var(256, 256, 8, 0, pol=0)
-geoms["g256b256u8c0_ntstore"] = var(256, 256, 8, 0, pol=3)
+                geoms[f"g{grid}b{block}u{unroll}p{pipe}"] = var(grid, block, unroll, 0, pipe=pipe)
+geoms["g256b256u4p1_plain"] = var(256, 256, 4, 0, pol=0, pipe=1)
 
 
 def t(fn, reps=20):
