@@ -92,6 +92,21 @@ def make_workload(dev, rank, n_cali):
     return act, d_a, z_a, weights, dws, zws, bits
 
 
+PMC_FILE = "profiles/pmc_traffic.json"
+
+
+def pmc_traffic():
+    """HBM bytes per fq_fwd_pt launch from the committed rocprofv3 PMC passes
+    (tools/pmc_session.sh: FETCH_SIZE and WRITE_SIZE in separate passes, read side
+    doubled per the gfx950 correction), or None if they were not collected."""
+    path = os.path.join(os.path.dirname(os.path.abspath(__file__)), PMC_FILE)
+    try:
+        with open(path) as f:
+            return float(json.load(f)["fq_fwd_pt"]["hbm_bytes_per_launch"])
+    except (OSError, KeyError, ValueError):
+        return None
+
+
 def time_events(fn, reps, dev):
     start, end = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     start.record()
@@ -157,8 +172,14 @@ def main():
     ms_fq = time_events(lambda: K.fake_quant_fwd(act, d_a, z_a, 4), 20, dev)
     alg_bytes = 8.0 * n_act
     achieved = alg_bytes / (ms_fq * 1e-3) / 1e9
-    ms_copy = time_events(lambda: K.stream_copy(act, y_act), 20, dev)
-    copy_gbs = 8.0 * n_act / (ms_copy * 1e-3) / 1e9
+    # stream-copy ceiling of this box: the best of the copy geometries the q/dq kernel
+    # is tuned over (1 workgroup/CU x unroll 4 / 8), same tensor, same bytes
+    copy_gbs, default_variant = 0.0, K.set_variant(0)
+    for v in (1 | (256 << 8), 1 | (3 << 4) | (256 << 8)):
+        K.set_variant(v)
+        ms_copy = time_events(lambda: K.stream_copy(act, y_act), 20, dev)
+        copy_gbs = max(copy_gbs, 8.0 * n_act / (ms_copy * 1e-3) / 1e9)
+    K.set_variant(default_variant)
     ms_w = time_events(lambda: K.fake_quant_multi(weights, dws, zws, bits), 20, dev)
 
     recon = None
@@ -188,7 +209,8 @@ def main():
                    "elems_per_step_per_rank": elems_per_step, "parallelism": f"dp{world}"},
         "roofline": {"bound": "hbm", "kernel": "fq_fwd_pt (ssq_fq_fwd, per-tensor A4)",
                      "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                     "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": None,
+                     "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": pmc_traffic(),
+                     "traffic_source": PMC_FILE if pmc_traffic() is not None else None,
                      "kernel_ms": round(ms_fq, 4), "alg_bytes_per_launch": int(alg_bytes),
                      "stream_copy_gbs": round(copy_gbs, 1),
                      "frac_of_stream_copy": round(achieved / copy_gbs, 4)},

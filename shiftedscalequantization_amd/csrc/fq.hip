@@ -78,9 +78,10 @@ __device__ __forceinline__ void fq_store4(f32x4 v, const QParams& p, f32x4* __re
   if (CODES) codes[k] = pack4(q0, q1, q2, q3);
 }
 
-// pipe == 0: each unrolled step loads UNROLL float4s, then computes and stores them.
-// pipe == 1: software pipelined -- the next step's UNROLL loads are issued before the
-// current step's math, so a wave keeps 2*UNROLL 16-B loads in flight across its ALU work.
+// Per-tensor: delta/zp are wave-uniform scalars.  Each step loads UNROLL float4s per
+// thread (issued back to back), then computes and stores them.  A software-pipelined form
+// (next step's loads issued before this step's math) measured no faster: the default
+// geometry (1 workgroup/CU, UNROLL 8) already keeps 8 KiB per wave in flight.
 template <bool CODES, int UNROLL, bool NTL, bool NTS>
 __global__ __launch_bounds__(1024) void fq_fwd_pt(const f32x4* __restrict__ x,
                                                   f32x4* __restrict__ y,
@@ -88,7 +89,7 @@ __global__ __launch_bounds__(1024) void fq_fwd_pt(const f32x4* __restrict__ x,
                                                   const float* __restrict__ delta,
                                                   const float* __restrict__ zp, int64_t n4,
                                                   float scale, float lo, float hi,
-                                                  int64_t chunk, int pipe) {
+                                                  int64_t chunk) {
   QParams p;
   p.d = __fmul_rn(delta[0], scale);
   p.z = zp[0];
@@ -96,35 +97,12 @@ __global__ __launch_bounds__(1024) void fq_fwd_pt(const f32x4* __restrict__ x,
   p.hi = hi;
   int64_t i, end, stride;
   stream_range(n4, chunk, i, end, stride);
-  const int64_t step = UNROLL * stride;
-  if (pipe) {
-    if (i + (UNROLL - 1) * stride < end) {
-      f32x4 cur[UNROLL];
+  for (; i + (UNROLL - 1) * stride < end; i += UNROLL * stride) {
+    f32x4 v[UNROLL];
 #pragma unroll
-      for (int u = 0; u < UNROLL; ++u) cur[u] = ld4<NTL>(&x[i + u * stride]);
-      for (;;) {
-        const bool more = i + step + (UNROLL - 1) * stride < end;
-        f32x4 nxt[UNROLL];
-        if (more) {
+    for (int u = 0; u < UNROLL; ++u) v[u] = ld4<NTL>(&x[i + u * stride]);
 #pragma unroll
-          for (int u = 0; u < UNROLL; ++u) nxt[u] = ld4<NTL>(&x[i + step + u * stride]);
-        }
-#pragma unroll
-        for (int u = 0; u < UNROLL; ++u) fq_store4<CODES, NTS>(cur[u], p, y, codes, i + u * stride);
-        i += step;
-        if (!more) break;
-#pragma unroll
-        for (int u = 0; u < UNROLL; ++u) cur[u] = nxt[u];
-      }
-    }
-  } else {
-    for (; i + (UNROLL - 1) * stride < end; i += step) {
-      f32x4 v[UNROLL];
-#pragma unroll
-      for (int u = 0; u < UNROLL; ++u) v[u] = ld4<NTL>(&x[i + u * stride]);
-#pragma unroll
-      for (int u = 0; u < UNROLL; ++u) fq_store4<CODES, NTS>(v[u], p, y, codes, i + u * stride);
-    }
+    for (int u = 0; u < UNROLL; ++u) fq_store4<CODES, NTS>(v[u], p, y, codes, i + u * stride);
   }
   for (; i < end; i += stride) fq_store4<CODES, false>(x[i], p, y, codes, i);
 }
@@ -409,11 +387,10 @@ __global__ __launch_bounds__(1024) void copy_kernel(const f32x4* __restrict__ s,
 //   bits 8-23 grid size in workgroups (0 -> 2048)
 //   bit  24   chunked (workgroup-contiguous) instead of grid-stride
 //   bits 25-26 workgroup size: 0 -> 256, 1 -> 512, 2 -> 1024
-//   bit  27   software-pipelined q/dq loop (next step's loads issued before the math)
-static int g_variant = 1 | (256 << 8);  // NT load+store, unroll 4, 1 workgroup per CU (sweep: tools/sweep_stream.py)
+static int g_variant = 1 | (3 << 4) | (256 << 8);  // NT load+store, unroll 8, 1 workgroup per CU (tools/ab_fq.py)
 
 struct Variant {
-  bool ntl, nts, chunked, pipe;
+  bool ntl, nts, chunked;
   int unroll, grid, block;
 };
 static Variant decode_variant(int v) {
@@ -428,7 +405,6 @@ static Variant decode_variant(int v) {
   r.chunked = (v >> 24) & 1;
   const int b = (v >> 25) & 3;
   r.block = b == 1 ? 512 : b == 2 ? 1024 : 256;
-  r.pipe = (v >> 27) & 1;
   return r;
 }
 
@@ -468,18 +444,18 @@ template <int U, bool NTL, bool NTS>
 struct FqPtCodes {
   static void go(dim3 g, dim3 b, hipStream_t s, const f32x4* x, f32x4* y, uint32_t* c,
                  const float* d, const float* z, int64_t n4, float sc, float lo, float hi,
-                 int64_t chunk, int pipe) {
+                 int64_t chunk) {
     hipLaunchKernelGGL((fq_fwd_pt<true, U, NTL, NTS>), g, b, 0, s, x, y, c, d, z, n4, sc, lo, hi,
-                       chunk, pipe);
+                       chunk);
   }
 };
 template <int U, bool NTL, bool NTS>
 struct FqPt {
   static void go(dim3 g, dim3 b, hipStream_t s, const f32x4* x, f32x4* y, uint32_t* c,
                  const float* d, const float* z, int64_t n4, float sc, float lo, float hi,
-                 int64_t chunk, int pipe) {
+                 int64_t chunk) {
     hipLaunchKernelGGL((fq_fwd_pt<false, U, NTL, NTS>), g, b, 0, s, x, y, c, d, z, n4, sc, lo, hi,
-                       chunk, pipe);
+                       chunk);
   }
 };
 template <int U, bool NTL, bool NTS>
@@ -527,10 +503,9 @@ extern "C" int ssq_fq_fwd(const float* x, float* y, void* codes, const float* de
       uint32_t* cv = (uint32_t*)codes;
       if (codes)
         launch_stream<FqPtCodes>(v, grid, block, s, xv, yv, cv, delta, zp, n4, scale, lo, hi,
-                                 chunk, (int)v.pipe);
+                                 chunk);
       else
-        launch_stream<FqPt>(v, grid, block, s, xv, yv, cv, delta, zp, n4, scale, lo, hi, chunk,
-                            (int)v.pipe);
+        launch_stream<FqPt>(v, grid, block, s, xv, yv, cv, delta, zp, n4, scale, lo, hi, chunk);
     } else {
       SSQ_REQUIRE(inner < (1ll << 31) && nch < (1ll << 31), SSQ_E_ARG, "ssq_fq_fwd: dims");
       const int grid = grid_for(n4, kBlock, 4096);
