@@ -121,8 +121,8 @@ int ssq_adashift_fwd(const float* W, const float* alpha, const float* beta,
                      ssq_stream_t stream);
 
 /* Backward of the soft-target adaShift forward wrt alpha (and beta if gbeta != NULL).
- * Conv alpha gradients are reduced over (Co, K) deterministically, one workgroup per
- * input channel (the workspace size is 0; ws/ws_bytes are kept for ABI stability).
+ * Conv alpha gradients are reduced over (Co, K) deterministically in two fixed-order
+ * stages through `ws` (ssq_adashift_bwd_workspace_size bytes; 0 for Linear).
  * Fused shift regulariser (layer_recon_fused_shiftedScale.py:281-282), applied when
  * lambda != 0:  reg = lambda * sum(1 - |2p-1|^b);  its gradient is added to galpha and
  * per-alpha-row values are written to reg_vals (may be NULL).  (lambda, b) come from

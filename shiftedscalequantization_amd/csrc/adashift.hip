@@ -5,10 +5,9 @@
 // materialized as S W-sized tensors (the reference's self.x_q list, channelQuant.py:284-286),
 // so the adaShift forward reads W + beta (8 B/elem) and writes What (4 B/elem).
 //
-// alpha-gradient reductions over (Co, K) per input channel run one workgroup per input
-// channel (alpha_ci_kernel): S double accumulators per thread, a fixed shuffle tree, then
-// the waves in fixed order -- deterministic, one launch, no workspace -- followed by the
-// softmax/clamp chain and the shift regulariser.
+// Conv kernels are column-tiled (see "column-tiled conv kernels"): the softmax of an
+// input channel's alpha row is computed once per thread, rows are coalesced sweeps, and
+// the alpha-gradient reductions over (Co, K) are two fixed-order stages (deterministic).
 #include "ssq_common.h"
 
 namespace ssq {
@@ -425,86 +424,160 @@ using namespace ssq;
     if (_r) return _r;                                 \
   }
 
-extern "C" int ssq_adashift_fwd(const float* W, const float* alpha, const float* beta,
-                                const float* delta, const float* zp, const float* shifts, int S,
-                                int64_t Co, int64_t Ci, int64_t K, int is_fc, int hard_targets,
-                                int hard_round, int qmin, int qmax, float* What, void* codes,
-                                ssq_stream_t stream) {
-  SSQ_GEO(Co, Ci, K, is_fc, g);
-  SSQ_SHIFTS(shifts, S, sh);
-  SSQ_REQUIRE(W && alpha && beta && delta && zp && What, SSQ_E_ARG, "ssq_adashift_fwd: null");
-  const uint32_t n = g.Co * g.CiK;
-  hipLaunchKernelGGL(adashift_fwd_kernel, dim3(grid_for(n, kBlock)), dim3(kBlock), 0,
-                     (hipStream_t)stream, W, alpha, beta, delta, zp, sh, g, n, hard_targets,
-                     hard_round, (float)qmin, (float)qmax, What, (uint8_t*)codes);
-  return check_launch("ssq_adashift_fwd");
+// ------------------------------------------------------------------ column-tiled conv kernels
+// A conv weight (Co, Ci, K) is tiled as [chunk of R output channels] x [column block of
+// ncb whole input channels = ncb*K contiguous columns].  Thread t owns column
+// j = ci0*K + t of every row of the chunk, so its input channel ci = ci0 + t/K is fixed:
+// the softmax p(alpha[ci]) is computed once per thread (not once per element), and each
+// row is one coalesced sweep of ncb*K contiguous floats.  delta/zp are per row (wave
+// uniform).  The alpha reductions write one fixed-order partial per (chunk, ci) and a
+// second launch sums the chunks with one wave per input channel (fixed shuffle tree):
+// deterministic, no atomics.
+struct ColTiling {
+  uint32_t ncb, ncolblk, R, nchunk, threads;
+};
+constexpr uint32_t kMaxChunks = 64;  // stage 2: one lane per chunk
+
+static ColTiling col_tiling(const Geo& g) {
+  ColTiling t;
+  t.ncb = g.K >= (uint32_t)kBlock ? 1u : (uint32_t)kBlock / g.K;
+  if (t.ncb > g.Ci) t.ncb = g.Ci;
+  t.ncolblk = (g.Ci + t.ncb - 1) / t.ncb;
+  t.threads = (t.ncb * g.K + kWave - 1) / kWave * kWave;
+  uint32_t want = 2048 / t.ncolblk;  // ~8 workgroups per CU
+  if (want < 1) want = 1;
+  if (want > kMaxChunks) want = kMaxChunks;
+  if (want > g.Co) want = g.Co;
+  t.R = (g.Co + want - 1) / want;
+  t.nchunk = (g.Co + t.R - 1) / t.R;
+  return t;
+}
+static size_t col_ws_bytes(const Geo& g, int S) {
+  const ColTiling t = col_tiling(g);
+  return (size_t)t.nchunk * g.Ci * S * sizeof(double);
 }
 
-extern "C" size_t ssq_adashift_bwd_workspace_size(int64_t Co, int64_t Ci, int64_t K, int S,
-                                                  int is_fc) {
-  (void)Co; (void)Ci; (void)K; (void)S; (void)is_fc;
-  return 0;  // per-input-channel reductions need no workspace
-}
-
-// ------------------------------------------------------------------ per-input-channel reduction
-// One workgroup per input channel ci: its threads sweep the (co, k) pairs of that channel
-// (Co*K elements, stride Ci*K between output rows -- the weight is L2/MALL resident), keep
-// S double accumulators, and reduce them deterministically (wave shuffle tree, then the
-// waves in fixed order).  One launch, no workspace.
-//   MODE 0: adaShift backward   sum g_int * F_i           -> softmax chain + regulariser
-//   MODE 1: lhs backward        sum gy * Xq_i             -> softmax chain
-//   MODE 2: shift init          sum (w - X_i)^2 (cc.mode) -> init_alpha logits (+ mse table)
+// MODE 0: adaShift forward (floors + h(beta)); MODE 1: learned_hard_sigmoid forward.
 template <int MODE>
-__global__ __launch_bounds__(kBlock) void alpha_ci_kernel(
-    const float* __restrict__ gWhat, const float* __restrict__ W, const float* __restrict__ alpha,
-    const float* __restrict__ beta, const float* __restrict__ delta, const float* __restrict__ zp,
-    Shifts sh, Geo g, int hard_r, float lo, float hi, CandCfg cc, float reg_lambda, float reg_b,
-    const float* __restrict__ reg_dev, float* __restrict__ out_alpha, float* __restrict__ gbeta,
-    float* __restrict__ side) {
-  __shared__ double red[kBlock / kWave][kMaxS];
-  const uint32_t ci = blockIdx.x;
-  float p[kMaxS], F[kMaxS];
-  if (MODE != 2) {
-    float a[kMaxS];
-    load_row(alpha, ci, sh.n, a);
-    soft_targets<kMaxS>(a, sh.n, nullptr, p);
-  }
-  double acc[kMaxS];
-  for (int i = 0; i < sh.n; ++i) acc[i] = 0.0;
-  const uint32_t npairs = g.Co * g.K;
-  for (uint32_t t = threadIdx.x; t < npairs; t += blockDim.x) {
-    const uint32_t co = t / g.K, k = t - co * g.K;
-    const uint32_t e = co * g.CiK + ci * g.K + k;
-    const float w = W[e], d = delta[co];
+__global__ __launch_bounds__(1024) void shift_fwd_col(
+    const float* __restrict__ W, const float* __restrict__ alpha, const float* __restrict__ beta,
+    const float* __restrict__ delta, const float* __restrict__ zp, Shifts sh, Geo g,
+    ColTiling tl, int hard_t, int hard_r, float lo, float hi, float* __restrict__ What,
+    uint8_t* __restrict__ codes) {
+  const uint32_t ci0 = blockIdx.x * tl.ncb;
+  const uint32_t nci = min(tl.ncb, g.Ci - ci0);
+  const uint32_t t = threadIdx.x;
+  if (t >= nci * g.K) return;
+  const uint32_t ci = ci0 + t / g.K, j = ci0 * g.K + t;
+  float a[kMaxS], p[kMaxS], F[kMaxS];
+  load_row(alpha, ci, sh.n, a);
+  soft_targets<kMaxS>(a, sh.n, nullptr, p);
+  const float s_sel = sh.s[argmax_first(p, sh.n)];
+  const uint32_t co0 = blockIdx.y * tl.R, co1 = min(co0 + tl.R, g.Co);
+#pragma unroll 4
+  for (uint32_t co = co0; co < co1; ++co) {
+    const uint32_t e = co * g.CiK + j;
+    const float w = W[e], d = delta[co], z = zp[co];
     if (MODE == 0) {
-      const float z = zp[co];
-      const float xf = soft_floor(w, d, sh, p, F);
+      const float xf = hard_t ? floorf(w / __fmul_rn(d, s_sel)) : soft_floor(w, d, sh, p, F);
       const float b = beta[e];
       const float hr = hard_r ? (b >= 0.0f ? 1.0f : 0.0f) : rect_sigmoid(b);
-      const float u = __fadd_rn(__fadd_rn(xf, hr), z);
-      const float gi = (u >= lo && u <= hi) ? __fmul_rn(gWhat[e], __fmul_rn(d, 1.0f)) : 0.0f;
-      if (gbeta) gbeta[e] = hard_r ? 0.0f : rect_sigmoid_grad(b, gi);
-      for (int i = 0; i < sh.n; ++i) acc[i] += (double)gi * (double)F[i];
-    } else if (MODE == 1) {
-      const float z = zp[co], gy = gWhat[e];
-      for (int i = 0; i < sh.n; ++i)
-        acc[i] += (double)gy * (double)cand_value<1>(w, d, z, sh.s[i], lo, hi);
+      const float q = clampf(__fadd_rn(__fadd_rn(xf, hr), z), lo, hi);
+      What[e] = __fmul_rn(__fsub_rn(q, z), __fmul_rn(d, 1.0f));
+      if (codes) codes[e] = (uint8_t)((int)q & 0xff);
     } else {
-      for (int i = 0; i < sh.n; ++i) acc[i] += (double)cand_err(w, d, co, sh.s[i], cc);
+      float out;
+      if (hard_t) {
+        out = cand_value<1>(w, d, z, s_sel, lo, hi);
+      } else {
+        out = 0.0f;
+        for (int i = 0; i < sh.n; ++i) {
+          const float v = __fmul_rn(cand_value<1>(w, d, z, sh.s[i], lo, hi), p[i]);
+          out = i == 0 ? v : __fadd_rn(out, v);
+        }
+      }
+      What[e] = out;
     }
   }
-  const int lane = threadIdx.x & (kWave - 1), wv = threadIdx.x / kWave;
-  for (int i = 0; i < sh.n; ++i) {
-    const double v = wave_sum(acc[i]);
-    if (lane == 0) red[wv][i] = v;
+}
+
+// Stage 1 of the per-input-channel reductions over (Co, K):
+//   MODE 0: adaShift backward   sum g_int * F_i   (and gbeta, elementwise)
+//   MODE 1: lhs backward        sum gy * Xq_i
+//   MODE 2: shift init          sum (w - X_i)^2   (cc.mode selects X_i)
+// part[(chunk*Ci + ci)*S + i] = this chunk's sum, accumulated in double in a fixed order.
+template <int MODE>
+__global__ __launch_bounds__(1024) void alpha_col_stage1(
+    const float* __restrict__ gWhat, const float* __restrict__ W, const float* __restrict__ alpha,
+    const float* __restrict__ beta, const float* __restrict__ delta, const float* __restrict__ zp,
+    Shifts sh, Geo g, ColTiling tl, int hard_r, float lo, float hi, CandCfg cc,
+    float* __restrict__ gbeta, double* __restrict__ part) {
+  extern __shared__ double red[];  // [threads][S]
+  const uint32_t ci0 = blockIdx.x * tl.ncb;
+  const uint32_t nci = min(tl.ncb, g.Ci - ci0);
+  const uint32_t t = threadIdx.x;
+  const bool active = t < nci * g.K;
+  double acc[kMaxS];
+  for (int i = 0; i < sh.n; ++i) acc[i] = 0.0;
+  if (active) {
+    const uint32_t ci = ci0 + t / g.K, j = ci0 * g.K + t;
+    float p[kMaxS], F[kMaxS];
+    if (MODE == 0) {
+      float a[kMaxS];
+      load_row(alpha, ci, sh.n, a);
+      soft_targets<kMaxS>(a, sh.n, nullptr, p);
+    }
+    const uint32_t co0 = blockIdx.y * tl.R, co1 = min(co0 + tl.R, g.Co);
+#pragma unroll 4
+    for (uint32_t co = co0; co < co1; ++co) {
+      const uint32_t e = co * g.CiK + j;
+      const float w = W[e], d = delta[co];
+      if (MODE == 0) {
+        const float z = zp[co];
+        const float xf = soft_floor(w, d, sh, p, F);
+        const float b = beta[e];
+        const float hr = hard_r ? (b >= 0.0f ? 1.0f : 0.0f) : rect_sigmoid(b);
+        const float u = __fadd_rn(__fadd_rn(xf, hr), z);
+        const float gi = (u >= lo && u <= hi) ? __fmul_rn(gWhat[e], __fmul_rn(d, 1.0f)) : 0.0f;
+        if (gbeta) gbeta[e] = hard_r ? 0.0f : rect_sigmoid_grad(b, gi);
+        for (int i = 0; i < sh.n; ++i) acc[i] += (double)gi * (double)F[i];
+      } else if (MODE == 1) {
+        const float z = zp[co], gy = gWhat[e];
+        for (int i = 0; i < sh.n; ++i)
+          acc[i] += (double)gy * (double)cand_value<1>(w, d, z, sh.s[i], lo, hi);
+      } else {
+        for (int i = 0; i < sh.n; ++i) acc[i] += (double)cand_err(w, d, co, sh.s[i], cc);
+      }
+    }
   }
+  for (int i = 0; i < sh.n; ++i) red[t * sh.n + i] = acc[i];
   __syncthreads();
-  if (threadIdx.x != 0) return;
+  if (t < nci) {
+    for (int i = 0; i < sh.n; ++i) {
+      double s = 0.0;
+      for (uint32_t k = 0; k < g.K; ++k) s += red[(t * g.K + k) * sh.n + i];
+      part[((size_t)blockIdx.y * g.Ci + ci0 + t) * sh.n + i] = s;
+    }
+  }
+}
+
+// Stage 2: one wave per input channel; lane c loads chunk c's partial, a fixed shuffle
+// tree sums them, lane 0 applies the softmax/clamp chain (+ regulariser, MODE 0) or the
+// init_alpha logits (MODE 2).
+template <int MODE>
+__global__ __launch_bounds__(kBlock) void alpha_col_stage2(
+    const double* __restrict__ part, uint32_t nchunk, const float* __restrict__ alpha, Shifts sh,
+    Geo g, float reg_lambda, float reg_b, const float* __restrict__ reg_dev,
+    float* __restrict__ out_alpha, float* __restrict__ side) {
+  const uint32_t ci = blockIdx.x * (blockDim.x / kWave) + threadIdx.x / kWave;
+  const uint32_t lane = threadIdx.x & (kWave - 1);
+  if (ci >= g.Ci) return;
   double tot[kMaxS];
   for (int i = 0; i < sh.n; ++i) {
-    tot[i] = 0.0;
-    for (int w2 = 0; w2 < (int)(blockDim.x / kWave); ++w2) tot[i] += red[w2][i];
+    const double v = lane < nchunk ? part[((size_t)lane * g.Ci + ci) * sh.n + i] : 0.0;
+    tot[i] = wave_sum(v);
   }
+  if (lane != 0) return;
   if (MODE == 2) {
     float a[kMaxS];
     init_alpha_row(tot, sh.n, a);
@@ -525,10 +598,55 @@ __global__ __launch_bounds__(kBlock) void alpha_ci_kernel(
   if (side && MODE == 0) side[ci] = reg;
 }
 
-static unsigned ci_threads(const Geo& g) {
-  const uint32_t pairs = g.Co * g.K;
-  const uint32_t t = (pairs + kWave - 1) / kWave * kWave;
-  return t >= (uint32_t)kBlock ? (unsigned)kBlock : (unsigned)t;
+template <int MODE>
+static int launch_alpha_col(const Geo& g, const Shifts& sh, const float* gWhat, const float* W,
+                            const float* alpha, const float* beta, const float* delta,
+                            const float* zp, int hard_r, float lo, float hi, const CandCfg& cc,
+                            float reg_lambda, float reg_b, const float* reg_dev, float* out_alpha,
+                            float* gbeta, float* side, void* ws, size_t ws_bytes, hipStream_t s,
+                            const char* what) {
+  const ColTiling tl = col_tiling(g);
+  SSQ_REQUIRE(tl.threads <= 1024, SSQ_E_ARG, "%s: kernel window K > 1024 unsupported", what);
+  SSQ_REQUIRE(ws && ws_bytes >= col_ws_bytes(g, sh.n), SSQ_E_WS, "%s: workspace too small", what);
+  const size_t lds = (size_t)tl.threads * sh.n * sizeof(double);
+  hipLaunchKernelGGL(alpha_col_stage1<MODE>, dim3(tl.ncolblk, tl.nchunk), dim3(tl.threads), lds, s,
+                     gWhat, W, alpha, beta, delta, zp, sh, g, tl, hard_r, lo, hi, cc, gbeta,
+                     (double*)ws);
+  const uint32_t waves = kBlock / kWave;
+  hipLaunchKernelGGL(alpha_col_stage2<MODE>, dim3((g.Ci + waves - 1) / waves), dim3(kBlock), 0, s,
+                     (const double*)ws, tl.nchunk, alpha, sh, g, reg_lambda, reg_b, reg_dev,
+                     out_alpha, side);
+  return check_launch(what);
+}
+
+extern "C" int ssq_adashift_fwd(const float* W, const float* alpha, const float* beta,
+                                const float* delta, const float* zp, const float* shifts, int S,
+                                int64_t Co, int64_t Ci, int64_t K, int is_fc, int hard_targets,
+                                int hard_round, int qmin, int qmax, float* What, void* codes,
+                                ssq_stream_t stream) {
+  SSQ_GEO(Co, Ci, K, is_fc, g);
+  SSQ_SHIFTS(shifts, S, sh);
+  SSQ_REQUIRE(W && alpha && beta && delta && zp && What, SSQ_E_ARG, "ssq_adashift_fwd: null");
+  const uint32_t n = g.Co * g.CiK;
+  if (is_fc) {
+    hipLaunchKernelGGL(adashift_fwd_kernel, dim3(grid_for(n, kBlock)), dim3(kBlock), 0,
+                       (hipStream_t)stream, W, alpha, beta, delta, zp, sh, g, n, hard_targets,
+                       hard_round, (float)qmin, (float)qmax, What, (uint8_t*)codes);
+  } else {
+    const ColTiling tl = col_tiling(g);
+    SSQ_REQUIRE(tl.threads <= 1024, SSQ_E_ARG, "ssq_adashift_fwd: kernel window K > 1024");
+    hipLaunchKernelGGL(shift_fwd_col<0>, dim3(tl.ncolblk, tl.nchunk), dim3(tl.threads), 0,
+                       (hipStream_t)stream, W, alpha, beta, delta, zp, sh, g, tl, hard_targets,
+                       hard_round, (float)qmin, (float)qmax, What, (uint8_t*)codes);
+  }
+  return check_launch("ssq_adashift_fwd");
+}
+
+extern "C" size_t ssq_adashift_bwd_workspace_size(int64_t Co, int64_t Ci, int64_t K, int S,
+                                                  int is_fc) {
+  Geo g;
+  if (is_fc || S < 1 || S > kMaxS || make_geo(Co, Ci, K, 0, g) != SSQ_OK) return 0;
+  return col_ws_bytes(g, S);
 }
 
 extern "C" int ssq_adashift_bwd(const float* gWhat, const float* W, const float* alpha,
@@ -550,13 +668,10 @@ extern "C" int ssq_adashift_bwd(const float* gWhat, const float* W, const float*
                        reg_lambda, reg_b, reg_dev, galpha, gbeta, reg_vals);
     return check_launch("ssq_adashift_bwd(fc)");
   }
-  (void)ws;
-  (void)ws_bytes;
   const CandCfg cc{nullptr, 0, 0.0f, 0.0f};
-  hipLaunchKernelGGL(alpha_ci_kernel<0>, dim3(g.Ci), dim3(ci_threads(g)), 0, s, gWhat, W, alpha,
-                     beta, delta, zp, sh, g, hard_round, (float)qmin, (float)qmax, cc, reg_lambda,
-                     reg_b, reg_dev, galpha, gbeta, reg_vals);
-  return check_launch("ssq_adashift_bwd");
+  return launch_alpha_col<0>(g, sh, gWhat, W, alpha, beta, delta, zp, hard_round, (float)qmin,
+                             (float)qmax, cc, reg_lambda, reg_b, reg_dev, galpha, gbeta, reg_vals,
+                             ws, ws_bytes, s, "ssq_adashift_bwd");
 }
 
 extern "C" int ssq_shift_reg(const float* alpha, int S, int64_t rows, int mode, float lambda,
@@ -577,9 +692,17 @@ extern "C" int ssq_lhs_fwd(const float* W, const float* alpha, const float* delt
   SSQ_SHIFTS(shifts, S, sh);
   SSQ_REQUIRE(W && alpha && delta && zp && What, SSQ_E_ARG, "ssq_lhs_fwd: null");
   const uint32_t n = g.Co * g.CiK;
-  hipLaunchKernelGGL(lhs_fwd_kernel, dim3(grid_for(n, kBlock)), dim3(kBlock), 0,
-                     (hipStream_t)stream, W, alpha, delta, zp, sh, g, n, hard_targets,
-                     (float)qmin, (float)qmax, What);
+  if (is_fc) {
+    hipLaunchKernelGGL(lhs_fwd_kernel, dim3(grid_for(n, kBlock)), dim3(kBlock), 0,
+                       (hipStream_t)stream, W, alpha, delta, zp, sh, g, n, hard_targets,
+                       (float)qmin, (float)qmax, What);
+  } else {
+    const ColTiling tl = col_tiling(g);
+    SSQ_REQUIRE(tl.threads <= 1024, SSQ_E_ARG, "ssq_lhs_fwd: kernel window K > 1024");
+    hipLaunchKernelGGL(shift_fwd_col<1>, dim3(tl.ncolblk, tl.nchunk), dim3(tl.threads), 0,
+                       (hipStream_t)stream, W, alpha, nullptr, delta, zp, sh, g, tl, hard_targets,
+                       0, (float)qmin, (float)qmax, What, nullptr);
+  }
   return check_launch("ssq_lhs_fwd");
 }
 
@@ -598,13 +721,10 @@ extern "C" int ssq_lhs_bwd(const float* gWhat, const float* W, const float* alph
                        0.0f, nullptr, galpha, nullptr, nullptr);
     return check_launch("ssq_lhs_bwd(fc)");
   }
-  (void)ws;
-  (void)ws_bytes;
   const CandCfg cc{nullptr, 0, 0.0f, 0.0f};
-  hipLaunchKernelGGL(alpha_ci_kernel<1>, dim3(g.Ci), dim3(ci_threads(g)), 0, s, gWhat, W, alpha,
-                     nullptr, delta, zp, sh, g, 0, (float)qmin, (float)qmax, cc, 0.0f, 0.0f,
-                     nullptr, galpha, nullptr, nullptr);
-  return check_launch("ssq_lhs_bwd");
+  return launch_alpha_col<1>(g, sh, gWhat, W, alpha, nullptr, delta, zp, 0, (float)qmin,
+                             (float)qmax, cc, 0.0f, 0.0f, nullptr, galpha, nullptr, nullptr, ws,
+                             ws_bytes, s, "ssq_lhs_bwd");
 }
 
 extern "C" int ssq_adaround_fwd(const float* W, const float* beta, const float* delta,
@@ -655,8 +775,7 @@ extern "C" int ssq_get_delta(const float* delta, const float* alpha, const float
 
 extern "C" size_t ssq_shift_init_workspace_size(int64_t Co, int64_t Ci, int64_t K, int S,
                                                 int is_fc) {
-  (void)Co; (void)Ci; (void)K; (void)S; (void)is_fc;
-  return 0;  // per-input-channel reductions need no workspace
+  return ssq_adashift_bwd_workspace_size(Co, Ci, K, S, is_fc);
 }
 
 extern "C" int ssq_shift_init(const float* W, const float* delta, const float* zp,
@@ -674,11 +793,10 @@ extern "C" int ssq_shift_init(const float* W, const float* delta, const float* z
     hipLaunchKernelGGL(shift_init_fc, dim3(grid_for(n, kBlock)), dim3(kBlock), 0, s, W, delta, sh,
                        g, n, cc, alpha, mse_out);
   } else {
-    (void)ws;
-    (void)ws_bytes;
-    hipLaunchKernelGGL(alpha_ci_kernel<2>, dim3(g.Ci), dim3(ci_threads(g)), 0, s, nullptr, W,
-                       nullptr, nullptr, delta, nullptr, sh, g, 0, 0.0f, 0.0f, cc, 0.0f, 0.0f,
-                       nullptr, alpha, nullptr, mse_out);
+    const int rc = launch_alpha_col<2>(g, sh, nullptr, W, nullptr, nullptr, delta, nullptr, 0, 0.0f,
+                                       0.0f, cc, 0.0f, 0.0f, nullptr, alpha, nullptr, mse_out, ws,
+                                       ws_bytes, s, "ssq_shift_init");
+    if (rc) return rc;
   }
   if (beta)  // init_v_beta: beta from delta * s[argmax p(alpha)] (channelQuant.py:289-292)
     hipLaunchKernelGGL(beta_from_alpha_kernel, dim3(grid_for(n, kBlock)), dim3(kBlock), 0, s, W,
