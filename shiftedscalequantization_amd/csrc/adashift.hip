@@ -39,10 +39,10 @@ __device__ __forceinline__ void load_row(const float* __restrict__ a, uint32_t r
 }
 
 // soft shifted floor  sum_i F_i * p_i  (x_out = x_q0*p0; x_out += x_q1*p1; ...)
-__device__ __forceinline__ float soft_floor(float w, float d, const Shifts& sh, const float* p,
-                                            float* F) {
+__device__ __forceinline__ float soft_floor(float w, float d, const Shifts& sh, int S,
+                                            const float* p, float* F) {
   float acc = 0.0f;
-  for (int i = 0; i < sh.n; ++i) {
+  for (int i = 0; i < S; ++i) {
     F[i] = floorf(w / __fmul_rn(d, sh.s[i]));
     const float t = __fmul_rn(F[i], p[i]);
     acc = i == 0 ? t : __fadd_rn(acc, t);
@@ -69,7 +69,7 @@ __global__ __launch_bounds__(kBlock) void adashift_fwd_kernel(
       const int sel = argmax_first(p, sh.n);
       xf = floorf(w / __fmul_rn(d, sh.s[sel]));
     } else {
-      xf = soft_floor(w, d, sh, p, F);
+      xf = soft_floor(w, d, sh, sh.n, p, F);
     }
     const float b = beta[e];
     const float hr = hard_r ? (b >= 0.0f ? 1.0f : 0.0f) : rect_sigmoid(b);
@@ -86,21 +86,24 @@ __device__ __forceinline__ float alpha_chain(const float* a, int S, double* g_p,
                                              float reg_b, int reg_mode, float* ga_out) {
   float s[kMaxS], p[kMaxS];
   soft_targets<kMaxS>(a, S, s, p);
+  // the regulariser in fp32 like the reference's tensor ops (pow / log and their
+  // autograd), summed in double for a deterministic value
   float reg = 0.0f;
   if (reg_lambda != 0.0f) {
     double acc = 0.0;
     for (int i = 0; i < S; ++i) {
-      if (reg_mode == 0) {
-        const double r = fabs((double)p[i] - 0.5) * 2.0;
-        acc += 1.0 - pow(r, (double)reg_b);
+      if (reg_mode == 0) {  // lambda * sum(1 - ((p - 0.5).abs() * 2).pow(b))
+        const float r = __fmul_rn(fabsf(__fsub_rn(p[i], 0.5f)), 2.0f);
+        acc += (double)__fsub_rn(1.0f, powf(r, reg_b));
         if (reg_b != 0.0f) {
-          const double sg = p[i] > 0.5f ? 1.0 : (p[i] < 0.5f ? -1.0 : 0.0);
-          g_p[i] += -(double)reg_lambda * (double)reg_b * pow(r, (double)reg_b - 1.0) * 2.0 * sg;
+          const float sg = p[i] > 0.5f ? 1.0f : (p[i] < 0.5f ? -1.0f : 0.0f);
+          const float gr = __fmul_rn(__fmul_rn(-reg_lambda, reg_b), powf(r, __fsub_rn(reg_b, 1.0f)));
+          g_p[i] += (double)__fmul_rn(__fmul_rn(gr, 2.0f), sg);
         }
       } else {  // entropy: -lambda * sum p log(p + 1e-10)
-        const double pp = p[i];
-        acc += -(pp * log(pp + 1e-10));
-        g_p[i] += -(double)reg_lambda * (log(pp + 1e-10) + pp / (pp + 1e-10));
+        const float lg = logf(__fadd_rn(p[i], 1e-10f));
+        acc += -(double)__fmul_rn(p[i], lg);
+        g_p[i] += (double)(-reg_lambda * __fadd_rn(lg, p[i] / __fadd_rn(p[i], 1e-10f)));
       }
     }
     reg = (float)((double)reg_lambda * acc);
@@ -146,7 +149,7 @@ __global__ __launch_bounds__(kBlock) void alpha_grad_fc(
     const float w = W[e], d = delta[co], z = zp[co], gy = gWhat[e];
     float gi;
     if (MODE == 0) {
-      const float xf = soft_floor(w, d, sh, p, F);
+      const float xf = soft_floor(w, d, sh, sh.n, p, F);
       const float b = beta[e];
       const float hr = hard_r ? (b >= 0.0f ? 1.0f : 0.0f) : rect_sigmoid(b);
       const float u = __fadd_rn(__fadd_rn(xf, hr), z);
@@ -457,30 +460,35 @@ static size_t col_ws_bytes(const Geo& g, int S) {
   return (size_t)t.nchunk * g.Ci * S * sizeof(double);
 }
 
+// Rows are processed RB at a time with every load of the batch issued before any math
+// (the row stride is Ci*K floats, so each load is its own cache line: latency, not
+// bandwidth, bounds a row-at-a-time loop).  NS > 0 fixes the shift count at compile time
+// so the per-shift loops unroll; NS == 0 takes it from sh.n.
+constexpr int kRB = 4;
+
 // MODE 0: adaShift forward (floors + h(beta)); MODE 1: learned_hard_sigmoid forward.
-template <int MODE>
+template <int MODE, int NS>
 __global__ __launch_bounds__(1024) void shift_fwd_col(
     const float* __restrict__ W, const float* __restrict__ alpha, const float* __restrict__ beta,
     const float* __restrict__ delta, const float* __restrict__ zp, Shifts sh, Geo g,
     ColTiling tl, int hard_t, int hard_r, float lo, float hi, float* __restrict__ What,
     uint8_t* __restrict__ codes) {
+  const int S = NS > 0 ? NS : sh.n;
   const uint32_t ci0 = blockIdx.x * tl.ncb;
   const uint32_t nci = min(tl.ncb, g.Ci - ci0);
   const uint32_t t = threadIdx.x;
   if (t >= nci * g.K) return;
   const uint32_t ci = ci0 + t / g.K, j = ci0 * g.K + t;
-  float a[kMaxS], p[kMaxS], F[kMaxS];
-  load_row(alpha, ci, sh.n, a);
-  soft_targets<kMaxS>(a, sh.n, nullptr, p);
-  const float s_sel = sh.s[argmax_first(p, sh.n)];
+  float a[kMaxS], p[kMaxS];
+  load_row(alpha, ci, S, a);
+  soft_targets<kMaxS>(a, S, nullptr, p);
+  const float s_sel = sh.s[argmax_first(p, S)];
   const uint32_t co0 = blockIdx.y * tl.R, co1 = min(co0 + tl.R, g.Co);
-#pragma unroll 4
-  for (uint32_t co = co0; co < co1; ++co) {
+  auto one = [&](uint32_t co, float w, float d, float z, float b) {
     const uint32_t e = co * g.CiK + j;
-    const float w = W[e], d = delta[co], z = zp[co];
+    float F[kMaxS];
     if (MODE == 0) {
-      const float xf = hard_t ? floorf(w / __fmul_rn(d, s_sel)) : soft_floor(w, d, sh, p, F);
-      const float b = beta[e];
+      const float xf = hard_t ? floorf(w / __fmul_rn(d, s_sel)) : soft_floor(w, d, sh, S, p, F);
       const float hr = hard_r ? (b >= 0.0f ? 1.0f : 0.0f) : rect_sigmoid(b);
       const float q = clampf(__fadd_rn(__fadd_rn(xf, hr), z), lo, hi);
       What[e] = __fmul_rn(__fsub_rn(q, z), __fmul_rn(d, 1.0f));
@@ -491,13 +499,31 @@ __global__ __launch_bounds__(1024) void shift_fwd_col(
         out = cand_value<1>(w, d, z, s_sel, lo, hi);
       } else {
         out = 0.0f;
-        for (int i = 0; i < sh.n; ++i) {
+        for (int i = 0; i < S; ++i) {
           const float v = __fmul_rn(cand_value<1>(w, d, z, sh.s[i], lo, hi), p[i]);
           out = i == 0 ? v : __fadd_rn(out, v);
         }
       }
       What[e] = out;
     }
+  };
+  uint32_t co = co0;
+  for (; co + kRB <= co1; co += kRB) {
+    float w[kRB], d[kRB], z[kRB], b[kRB];
+#pragma unroll
+    for (int r = 0; r < kRB; ++r) {
+      const uint32_t e = (co + r) * g.CiK + j;
+      w[r] = W[e];
+      d[r] = delta[co + r];
+      z[r] = zp[co + r];
+      b[r] = MODE == 0 ? beta[e] : 0.0f;
+    }
+#pragma unroll
+    for (int r = 0; r < kRB; ++r) one(co + r, w[r], d[r], z[r], b[r]);
+  }
+  for (; co < co1; ++co) {
+    const uint32_t e = co * g.CiK + j;
+    one(co, W[e], delta[co], zp[co], MODE == 0 ? beta[e] : 0.0f);
   }
 }
 
@@ -506,57 +532,73 @@ __global__ __launch_bounds__(1024) void shift_fwd_col(
 //   MODE 1: lhs backward        sum gy * Xq_i
 //   MODE 2: shift init          sum (w - X_i)^2   (cc.mode selects X_i)
 // part[(chunk*Ci + ci)*S + i] = this chunk's sum, accumulated in double in a fixed order.
-template <int MODE>
+template <int MODE, int NS>
 __global__ __launch_bounds__(1024) void alpha_col_stage1(
     const float* __restrict__ gWhat, const float* __restrict__ W, const float* __restrict__ alpha,
     const float* __restrict__ beta, const float* __restrict__ delta, const float* __restrict__ zp,
     Shifts sh, Geo g, ColTiling tl, int hard_r, float lo, float hi, CandCfg cc,
     float* __restrict__ gbeta, double* __restrict__ part) {
   extern __shared__ double red[];  // [threads][S]
+  const int S = NS > 0 ? NS : sh.n;
   const uint32_t ci0 = blockIdx.x * tl.ncb;
   const uint32_t nci = min(tl.ncb, g.Ci - ci0);
   const uint32_t t = threadIdx.x;
   const bool active = t < nci * g.K;
   double acc[kMaxS];
-  for (int i = 0; i < sh.n; ++i) acc[i] = 0.0;
+  for (int i = 0; i < S; ++i) acc[i] = 0.0;
   if (active) {
     const uint32_t ci = ci0 + t / g.K, j = ci0 * g.K + t;
-    float p[kMaxS], F[kMaxS];
+    float p[kMaxS];
     if (MODE == 0) {
       float a[kMaxS];
-      load_row(alpha, ci, sh.n, a);
-      soft_targets<kMaxS>(a, sh.n, nullptr, p);
+      load_row(alpha, ci, S, a);
+      soft_targets<kMaxS>(a, S, nullptr, p);
     }
-    const uint32_t co0 = blockIdx.y * tl.R, co1 = min(co0 + tl.R, g.Co);
-#pragma unroll 4
-    for (uint32_t co = co0; co < co1; ++co) {
-      const uint32_t e = co * g.CiK + j;
-      const float w = W[e], d = delta[co];
+    auto one = [&](uint32_t co, float w, float d, float z, float b, float gy) {
       if (MODE == 0) {
-        const float z = zp[co];
-        const float xf = soft_floor(w, d, sh, p, F);
-        const float b = beta[e];
+        float F[kMaxS];
+        const float xf = soft_floor(w, d, sh, S, p, F);
         const float hr = hard_r ? (b >= 0.0f ? 1.0f : 0.0f) : rect_sigmoid(b);
         const float u = __fadd_rn(__fadd_rn(xf, hr), z);
-        const float gi = (u >= lo && u <= hi) ? __fmul_rn(gWhat[e], __fmul_rn(d, 1.0f)) : 0.0f;
-        if (gbeta) gbeta[e] = hard_r ? 0.0f : rect_sigmoid_grad(b, gi);
-        for (int i = 0; i < sh.n; ++i) acc[i] += (double)gi * (double)F[i];
+        const float gi = (u >= lo && u <= hi) ? __fmul_rn(gy, __fmul_rn(d, 1.0f)) : 0.0f;
+        if (gbeta) gbeta[co * g.CiK + j] = hard_r ? 0.0f : rect_sigmoid_grad(b, gi);
+        for (int i = 0; i < S; ++i) acc[i] += (double)gi * (double)F[i];
       } else if (MODE == 1) {
-        const float z = zp[co], gy = gWhat[e];
-        for (int i = 0; i < sh.n; ++i)
+        for (int i = 0; i < S; ++i)
           acc[i] += (double)gy * (double)cand_value<1>(w, d, z, sh.s[i], lo, hi);
       } else {
-        for (int i = 0; i < sh.n; ++i) acc[i] += (double)cand_err(w, d, co, sh.s[i], cc);
+        for (int i = 0; i < S; ++i) acc[i] += (double)cand_err(w, d, co, sh.s[i], cc);
       }
+    };
+    const uint32_t co0 = blockIdx.y * tl.R, co1 = min(co0 + tl.R, g.Co);
+    uint32_t co = co0;
+    for (; co + kRB <= co1; co += kRB) {
+      float w[kRB], d[kRB], z[kRB], b[kRB], gy[kRB];
+#pragma unroll
+      for (int r = 0; r < kRB; ++r) {
+        const uint32_t e = (co + r) * g.CiK + j;
+        w[r] = W[e];
+        d[r] = delta[co + r];
+        z[r] = MODE != 2 ? zp[co + r] : 0.0f;
+        b[r] = MODE == 0 ? beta[e] : 0.0f;
+        gy[r] = MODE != 2 ? gWhat[e] : 0.0f;
+      }
+#pragma unroll
+      for (int r = 0; r < kRB; ++r) one(co + r, w[r], d[r], z[r], b[r], gy[r]);
+    }
+    for (; co < co1; ++co) {
+      const uint32_t e = co * g.CiK + j;
+      one(co, W[e], delta[co], MODE != 2 ? zp[co] : 0.0f, MODE == 0 ? beta[e] : 0.0f,
+          MODE != 2 ? gWhat[e] : 0.0f);
     }
   }
-  for (int i = 0; i < sh.n; ++i) red[t * sh.n + i] = acc[i];
+  for (int i = 0; i < S; ++i) red[t * S + i] = acc[i];
   __syncthreads();
   if (t < nci) {
-    for (int i = 0; i < sh.n; ++i) {
-      double s = 0.0;
-      for (uint32_t k = 0; k < g.K; ++k) s += red[(t * g.K + k) * sh.n + i];
-      part[((size_t)blockIdx.y * g.Ci + ci0 + t) * sh.n + i] = s;
+    for (int i = 0; i < S; ++i) {
+      double sum = 0.0;
+      for (uint32_t k = 0; k < g.K; ++k) sum += red[(t * g.K + k) * S + i];
+      part[((size_t)blockIdx.y * g.Ci + ci0 + t) * S + i] = sum;
     }
   }
 }
@@ -609,14 +651,41 @@ static int launch_alpha_col(const Geo& g, const Shifts& sh, const float* gWhat, 
   SSQ_REQUIRE(tl.threads <= 1024, SSQ_E_ARG, "%s: kernel window K > 1024 unsupported", what);
   SSQ_REQUIRE(ws && ws_bytes >= col_ws_bytes(g, sh.n), SSQ_E_WS, "%s: workspace too small", what);
   const size_t lds = (size_t)tl.threads * sh.n * sizeof(double);
-  hipLaunchKernelGGL(alpha_col_stage1<MODE>, dim3(tl.ncolblk, tl.nchunk), dim3(tl.threads), lds, s,
-                     gWhat, W, alpha, beta, delta, zp, sh, g, tl, hard_r, lo, hi, cc, gbeta,
-                     (double*)ws);
+#define SSQ_STAGE1(NS)                                                                        \
+  hipLaunchKernelGGL((alpha_col_stage1<MODE, NS>), dim3(tl.ncolblk, tl.nchunk), dim3(tl.threads), \
+                     lds, s, gWhat, W, alpha, beta, delta, zp, sh, g, tl, hard_r, lo, hi, cc,      \
+                     gbeta, (double*)ws)
+  switch (sh.n) {
+    case 1: SSQ_STAGE1(1); break;
+    case 2: SSQ_STAGE1(2); break;
+    case 3: SSQ_STAGE1(3); break;
+    case 4: SSQ_STAGE1(4); break;
+    default: SSQ_STAGE1(0); break;
+  }
+#undef SSQ_STAGE1
   const uint32_t waves = kBlock / kWave;
   hipLaunchKernelGGL(alpha_col_stage2<MODE>, dim3((g.Ci + waves - 1) / waves), dim3(kBlock), 0, s,
                      (const double*)ws, tl.nchunk, alpha, sh, g, reg_lambda, reg_b, reg_dev,
                      out_alpha, side);
   return check_launch(what);
+}
+
+template <int MODE>
+static void launch_shift_fwd_col(const Geo& g, const Shifts& sh, const ColTiling& tl,
+                                 const float* W, const float* alpha, const float* beta,
+                                 const float* delta, const float* zp, int hard_t, int hard_r,
+                                 float lo, float hi, float* What, uint8_t* codes, hipStream_t s) {
+#define SSQ_FWD(NS)                                                                         \
+  hipLaunchKernelGGL((shift_fwd_col<MODE, NS>), dim3(tl.ncolblk, tl.nchunk), dim3(tl.threads), 0, \
+                     s, W, alpha, beta, delta, zp, sh, g, tl, hard_t, hard_r, lo, hi, What, codes)
+  switch (sh.n) {
+    case 1: SSQ_FWD(1); break;
+    case 2: SSQ_FWD(2); break;
+    case 3: SSQ_FWD(3); break;
+    case 4: SSQ_FWD(4); break;
+    default: SSQ_FWD(0); break;
+  }
+#undef SSQ_FWD
 }
 
 extern "C" int ssq_adashift_fwd(const float* W, const float* alpha, const float* beta,
@@ -635,9 +704,8 @@ extern "C" int ssq_adashift_fwd(const float* W, const float* alpha, const float*
   } else {
     const ColTiling tl = col_tiling(g);
     SSQ_REQUIRE(tl.threads <= 1024, SSQ_E_ARG, "ssq_adashift_fwd: kernel window K > 1024");
-    hipLaunchKernelGGL(shift_fwd_col<0>, dim3(tl.ncolblk, tl.nchunk), dim3(tl.threads), 0,
-                       (hipStream_t)stream, W, alpha, beta, delta, zp, sh, g, tl, hard_targets,
-                       hard_round, (float)qmin, (float)qmax, What, (uint8_t*)codes);
+    launch_shift_fwd_col<0>(g, sh, tl, W, alpha, beta, delta, zp, hard_targets, hard_round,
+                            (float)qmin, (float)qmax, What, (uint8_t*)codes, (hipStream_t)stream);
   }
   return check_launch("ssq_adashift_fwd");
 }
@@ -699,9 +767,8 @@ extern "C" int ssq_lhs_fwd(const float* W, const float* alpha, const float* delt
   } else {
     const ColTiling tl = col_tiling(g);
     SSQ_REQUIRE(tl.threads <= 1024, SSQ_E_ARG, "ssq_lhs_fwd: kernel window K > 1024");
-    hipLaunchKernelGGL(shift_fwd_col<1>, dim3(tl.ncolblk, tl.nchunk), dim3(tl.threads), 0,
-                       (hipStream_t)stream, W, alpha, nullptr, delta, zp, sh, g, tl, hard_targets,
-                       0, (float)qmin, (float)qmax, What, nullptr);
+    launch_shift_fwd_col<1>(g, sh, tl, W, alpha, nullptr, delta, zp, hard_targets, 0,
+                            (float)qmin, (float)qmax, What, nullptr, (hipStream_t)stream);
   }
   return check_launch("ssq_lhs_fwd");
 }
