@@ -603,29 +603,27 @@ __global__ __launch_bounds__(1024) void alpha_col_stage1(
   }
 }
 
-// Stage 2: one wave per input channel; lane c loads chunk c's partial, a fixed shuffle
-// tree sums them, lane 0 applies the softmax/clamp chain (+ regulariser, MODE 0) or the
-// init_alpha logits (MODE 2).
-template <int MODE>
+// Stage 2: one thread per input channel sums the chunk partials in chunk order (the
+// loads of a chunk are coalesced across the wave), then applies the softmax/clamp chain
+// (+ regulariser, MODE 0) or the init_alpha logits (MODE 2) -- every lane in parallel.
+template <int MODE, int NS>
 __global__ __launch_bounds__(kBlock) void alpha_col_stage2(
     const double* __restrict__ part, uint32_t nchunk, const float* __restrict__ alpha, Shifts sh,
     Geo g, float reg_lambda, float reg_b, const float* __restrict__ reg_dev,
     float* __restrict__ out_alpha, float* __restrict__ side) {
-  const uint32_t ci = blockIdx.x * (blockDim.x / kWave) + threadIdx.x / kWave;
-  const uint32_t lane = threadIdx.x & (kWave - 1);
+  const int S = NS > 0 ? NS : sh.n;
+  const uint32_t ci = blockIdx.x * blockDim.x + threadIdx.x;
   if (ci >= g.Ci) return;
   double tot[kMaxS];
-  for (int i = 0; i < sh.n; ++i) {
-    const double v = lane < nchunk ? part[((size_t)lane * g.Ci + ci) * sh.n + i] : 0.0;
-    tot[i] = wave_sum(v);
-  }
-  if (lane != 0) return;
+  for (int i = 0; i < S; ++i) tot[i] = 0.0;
+  for (uint32_t c = 0; c < nchunk; ++c)
+    for (int i = 0; i < S; ++i) tot[i] += part[((size_t)c * g.Ci + ci) * S + i];
   if (MODE == 2) {
     float a[kMaxS];
-    init_alpha_row(tot, sh.n, a);
-    for (int i = 0; i < sh.n; ++i) {
-      out_alpha[(size_t)ci * sh.n + i] = a[i];
-      if (side) side[(size_t)ci * sh.n + i] = (float)tot[i];
+    init_alpha_row(tot, S, a);
+    for (int i = 0; i < S; ++i) {
+      out_alpha[(size_t)ci * S + i] = a[i];
+      if (side) side[(size_t)ci * S + i] = (float)tot[i];
     }
     return;
   }
@@ -634,9 +632,9 @@ __global__ __launch_bounds__(kBlock) void alpha_col_stage2(
     reg_b = reg_dev[1];
   }
   float a[kMaxS], ga[kMaxS];
-  load_row(alpha, ci, sh.n, a);
-  const float reg = alpha_chain(a, sh.n, tot, MODE == 0 ? reg_lambda : 0.0f, reg_b, 0, ga);
-  for (int i = 0; i < sh.n; ++i) out_alpha[(size_t)ci * sh.n + i] = ga[i];
+  load_row(alpha, ci, S, a);
+  const float reg = alpha_chain(a, S, tot, MODE == 0 ? reg_lambda : 0.0f, reg_b, 0, ga);
+  for (int i = 0; i < S; ++i) out_alpha[(size_t)ci * S + i] = ga[i];
   if (side && MODE == 0) side[ci] = reg;
 }
 
@@ -663,10 +661,19 @@ static int launch_alpha_col(const Geo& g, const Shifts& sh, const float* gWhat, 
     default: SSQ_STAGE1(0); break;
   }
 #undef SSQ_STAGE1
-  const uint32_t waves = kBlock / kWave;
-  hipLaunchKernelGGL(alpha_col_stage2<MODE>, dim3((g.Ci + waves - 1) / waves), dim3(kBlock), 0, s,
-                     (const double*)ws, tl.nchunk, alpha, sh, g, reg_lambda, reg_b, reg_dev,
-                     out_alpha, side);
+  const unsigned blocks2 = (g.Ci + kBlock - 1) / kBlock;
+#define SSQ_STAGE2(NS)                                                                         \
+  hipLaunchKernelGGL((alpha_col_stage2<MODE, NS>), dim3(blocks2), dim3(kBlock), 0, s,             \
+                     (const double*)ws, tl.nchunk, alpha, sh, g, reg_lambda, reg_b, reg_dev,     \
+                     out_alpha, side)
+  switch (sh.n) {
+    case 1: SSQ_STAGE2(1); break;
+    case 2: SSQ_STAGE2(2); break;
+    case 3: SSQ_STAGE2(3); break;
+    case 4: SSQ_STAGE2(4); break;
+    default: SSQ_STAGE2(0); break;
+  }
+#undef SSQ_STAGE2
   return check_launch(what);
 }
 

@@ -47,12 +47,17 @@ GRAPH_WARMUP = 3     # eager iterations before the iteration body is captured
 def _fused_loop(block, modules, iters, lmda, model, p, lr, bias_cal, batch_size, dp_average,
                 verbose, iter_hook=None, graph=True):
     device = next(model.parameters()).device
-    quantizers, opt_params = [], []
+    quantizers, opt_params, beta_rg = [], [], {}
     for m in modules:
         q = m.weight_quantizer
         q.init_v_beta(x=m.org_weight.data.clone().detach())
         opt_params += [q.alpha]
         quantizers += [q]
+        # beta is not optimised here (the reference's opt_params line for it is commented
+        # out, :65): its gradient is never read, so it is not computed.  The reference's
+        # autograd would accumulate it into beta.grad; nothing observes that.
+        beta_rg[q] = q.beta.requires_grad
+        q.beta.requires_grad_(False)
         q.opt_mode = 'adaShift'
         # gamma^z / phi^z: learned only with --bias_cal (the reference's commented-out
         # opt_params lines :67-68); otherwise their gradient is not computed at all
@@ -118,6 +123,8 @@ def _fused_loop(block, modules, iters, lmda, model, p, lr, bias_cal, batch_size,
             p_.grad = None if p_.grad is None else p_.grad.clone()
         del graph_obj
     loss_func.disarm()
+    for q, rg in beta_rg.items():
+        q.beta.requires_grad_(rg)
     if iter_hook is not None:
         iter_hook(iters)
 
