@@ -206,6 +206,16 @@ int ssq_gather_rows2(const float* src0, float* dst0, int64_t row0, const float* 
                      float* dst1, int64_t row1, const int64_t* idx, int64_t nidx,
                      ssq_stream_t stream);
 
+/* ---------------------------------------------------------------- K13 fused epilogue
+ * QuantModule conv bias add (quant_layer.py:250), the block's residual add and ReLU
+ * (quant_block.py:99-117) in one pass, in the reference's op order:
+ *   out = act((y + bias[c]) + res),  c = (i / hw) % C,  act = ReLU if relu else identity.
+ * bias / res may be NULL.  ssq_relu_bwd: gin = out > 0 ? g : 0 (ReLU backward on its
+ * output).  n < 2^31.                                                                 */
+int ssq_bias_act(const float* y, const float* bias, const float* res, float* out, int64_t n,
+                 int64_t hw, int64_t C, int relu, ssq_stream_t stream);
+int ssq_relu_bwd(const float* g, const float* out, float* gin, int64_t n, ssq_stream_t stream);
+
 /* ---------------------------------------------------------------- bandwidth probe
  * float4 device copy, used by bench.py to report the measured stream bandwidth.      */
 int ssq_stream_copy(const float* src, float* dst, int64_t n, ssq_stream_t stream);

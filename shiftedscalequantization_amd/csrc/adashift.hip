@@ -616,7 +616,19 @@ __global__ __launch_bounds__(kBlock) void alpha_col_stage2(
   if (ci >= g.Ci) return;
   double tot[kMaxS];
   for (int i = 0; i < S; ++i) tot[i] = 0.0;
-  for (uint32_t c = 0; c < nchunk; ++c)
+  // batches of 8 chunks: all loads of a batch in flight before the in-order adds
+  constexpr int CB = 8;
+  uint32_t c = 0;
+  for (; c + CB <= nchunk; c += CB) {
+    double v[CB][kMaxS];
+#pragma unroll
+    for (int k = 0; k < CB; ++k)
+      for (int i = 0; i < S; ++i) v[k][i] = part[((size_t)(c + k) * g.Ci + ci) * S + i];
+#pragma unroll
+    for (int k = 0; k < CB; ++k)
+      for (int i = 0; i < S; ++i) tot[i] += v[k][i];
+  }
+  for (; c < nchunk; ++c)
     for (int i = 0; i < S; ++i) tot[i] += part[((size_t)c * g.Ci + ci) * S + i];
   if (MODE == 2) {
     float a[kMaxS];

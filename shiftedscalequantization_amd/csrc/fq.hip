@@ -171,20 +171,6 @@ __global__ __launch_bounds__(kBlock) void fq_fwd_pc(const f32x4* __restrict__ x,
 }
 
 // ------------------------------------------------------------------ multi-tensor forward
-// n / d for 0 <= n < 2^31 as (umulhi(n, m) + n) >> s (round-up magic number, exact).
-struct FastDiv {
-  uint32_t m, s;
-};
-static FastDiv make_fastdiv(uint32_t d) {
-  uint32_t s = 0;
-  while (s < 32 && (1ull << s) < d) ++s;
-  const uint64_t m = ((1ull << 32) * ((1ull << s) - d)) / d + 1;
-  return FastDiv{(uint32_t)m, s};
-}
-__device__ __forceinline__ uint32_t fdiv(uint32_t n, FastDiv f) {
-  return (__umulhi(n, f.m) + n) >> f.s;
-}
-
 struct Seg {
   const float* x;
   float* y;

@@ -5,6 +5,8 @@
 // one pass reads pred and tgt and writes d loss/d pred (12 B/elem), with a deterministic
 // two-stage reduction of the loss value.  For p == 2 the gradient is bit-identical to
 // PyTorch's: (1/M) * (2*|d|) * sgn(d).
+#include <type_traits>
+
 #include "ssq_common.h"
 
 namespace ssq {
@@ -56,34 +58,92 @@ __global__ void lp_loss_finalize(const double* __restrict__ part, int nblk, doub
   if (threadIdx.x == 0) out[0] = (float)(a / m);
 }
 
-// dst_k[r, :] = src_k[idx[r], :], 16-B vectors when rows allow it.
+// dst_k[r, :] = src_k[idx[r], :], 16-B vectors when rows allow it.  blockIdx.y is the
+// batch row (its source row index is one scalar load), blockIdx.x strides over the
+// concatenated row of both sources: no per-element integer division.
 template <bool VEC>
 __global__ __launch_bounds__(kBlock) void gather2_kernel(const float* __restrict__ s0,
                                                          float* __restrict__ d0, int64_t row0,
                                                          const float* __restrict__ s1,
                                                          float* __restrict__ d1, int64_t row1,
-                                                         const int64_t* __restrict__ idx,
-                                                         int64_t nidx) {
+                                                         const int64_t* __restrict__ idx) {
+  typedef typename std::conditional<VEC, f32x4, float>::type T;
   const int64_t w = VEC ? 4 : 1;
   const int64_t r0 = row0 / w, r1 = s1 ? row1 / w : 0;
-  const int64_t per = r0 + r1;
-  const int64_t total = per * nidx;
+  const int64_t r = blockIdx.y;
+  const int64_t src = idx[r];
+  const T* a0 = (const T*)s0 + src * r0;
+  T* b0 = (T*)d0 + r * r0;
   const int64_t stride = (int64_t)gridDim.x * blockDim.x;
-  for (int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; e < total; e += stride) {
-    const int64_t r = e / per, k = e - r * per;
-    const int64_t src_row = idx[r];
-    if (VEC) {
-      if (k < r0)
-        ((f32x4*)d0)[r * r0 + k] = ((const f32x4*)s0)[src_row * r0 + k];
-      else
-        ((f32x4*)d1)[r * r1 + (k - r0)] = ((const f32x4*)s1)[src_row * r1 + (k - r0)];
-    } else {
-      if (k < r0)
-        d0[r * r0 + k] = s0[src_row * r0 + k];
-      else
-        d1[r * r1 + (k - r0)] = s1[src_row * r1 + (k - r0)];
-    }
+  for (int64_t k = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; k < r0; k += stride) b0[k] = a0[k];
+  if (s1) {
+    const T* a1 = (const T*)s1 + src * r1;
+    T* b1 = (T*)d1 + r * r1;
+    for (int64_t k = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; k < r1; k += stride)
+      b1[k] = a1[k];
   }
+}
+
+// ------------------------------------------------------------------ K13 fused epilogue
+// out = act(y + bias[c] (+ res)),  c = (i / hw) % C, in the reference's op order (conv
+// bias add, residual add, ReLU: three separate fp32 roundings -> bit-identical to the
+// eager sequence), one pass instead of three.
+template <bool RES, bool RELU>
+__global__ __launch_bounds__(kBlock) void bias_act_kernel(const float* __restrict__ y,
+                                                          const float* __restrict__ bias,
+                                                          const float* __restrict__ res,
+                                                          float* __restrict__ out, uint32_t n,
+                                                          FastDiv div_hw, FastDiv div_c,
+                                                          uint32_t C, int vec) {
+  const uint32_t stride = gridDim.x * blockDim.x;
+  auto one = [&](uint32_t i, float v, float rv) {
+    const uint32_t q = fdiv(i, div_hw);
+    const uint32_t c = q - fdiv(q, div_c) * C;
+    float t = bias ? __fadd_rn(v, bias[c]) : v;
+    if (RES) t = __fadd_rn(t, rv);
+    if (RELU) t = t < 0.0f ? 0.0f : t;  // torch clamp_min: std::max(t, 0) keeps -0 and NaN
+    return t;
+  };
+  if (vec) {
+    const uint32_t n4 = n / 4;
+    for (uint32_t v = blockIdx.x * blockDim.x + threadIdx.x; v < n4; v += stride) {
+      const f32x4 a = ((const f32x4*)y)[v];
+      f32x4 rr = {0.0f, 0.0f, 0.0f, 0.0f};
+      if (RES) rr = ((const f32x4*)res)[v];
+      f32x4 o;
+      o.x = one(4 * v, a.x, rr.x);
+      o.y = one(4 * v + 1, a.y, rr.y);
+      o.z = one(4 * v + 2, a.z, rr.z);
+      o.w = one(4 * v + 3, a.w, rr.w);
+      ((f32x4*)out)[v] = o;
+    }
+  } else {
+    for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride)
+      out[i] = one(i, y[i], RES ? res[i] : 0.0f);
+  }
+}
+
+// ReLU backward (threshold_backward on the output): gin = out > 0 ? g : 0
+__global__ __launch_bounds__(kBlock) void relu_bwd_kernel(const f32x4* __restrict__ g,
+                                                          const f32x4* __restrict__ out,
+                                                          f32x4* __restrict__ gin, uint32_t n4) {
+  const uint32_t stride = gridDim.x * blockDim.x;
+  for (uint32_t v = blockIdx.x * blockDim.x + threadIdx.x; v < n4; v += stride) {
+    const f32x4 a = g[v], o = out[v];
+    f32x4 r;
+    r.x = o.x > 0.0f ? a.x : 0.0f;
+    r.y = o.y > 0.0f ? a.y : 0.0f;
+    r.z = o.z > 0.0f ? a.z : 0.0f;
+    r.w = o.w > 0.0f ? a.w : 0.0f;
+    gin[v] = r;
+  }
+}
+__global__ __launch_bounds__(kBlock) void relu_bwd_tail(const float* __restrict__ g,
+                                                        const float* __restrict__ out,
+                                                        float* __restrict__ gin, uint32_t start,
+                                                        uint32_t n) {
+  const uint32_t i = start + blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < n) gin[i] = out[i] > 0.0f ? g[i] : 0.0f;
 }
 
 }  // namespace ssq
@@ -127,16 +187,62 @@ extern "C" int ssq_gather_rows2(const float* src0, float* dst0, int64_t row0, co
   SSQ_REQUIRE(src0 && dst0 && idx && row0 >= 1 && nidx >= 1, SSQ_E_ARG,
               "ssq_gather_rows2: bad args");
   SSQ_REQUIRE(!src1 || (dst1 && row1 >= 1), SSQ_E_ARG, "ssq_gather_rows2: bad second source");
+  SSQ_REQUIRE(nidx <= 65535, SSQ_E_ARG, "ssq_gather_rows2: at most 65535 rows per call");
   auto al = [](const void* q) { return ((uintptr_t)q & 15u) == 0; };
   const bool vec = row0 % 4 == 0 && al(src0) && al(dst0) &&
                    (!src1 || (row1 % 4 == 0 && al(src1) && al(dst1)));
-  const int64_t total = (row0 + (src1 ? row1 : 0)) * nidx / (vec ? 4 : 1);
-  const dim3 grid(grid_for(total, kBlock, 8192));
+  const int64_t per = (row0 > row1 ? row0 : row1) / (vec ? 4 : 1);
+  int64_t gx = 2048 / nidx;  // ~8 workgroups per CU in all
+  const int64_t need = (per + kBlock - 1) / kBlock;
+  if (gx > need) gx = need;
+  if (gx < 1) gx = 1;
+  const dim3 grid((unsigned)gx, (unsigned)nidx);
   if (vec)
     hipLaunchKernelGGL(gather2_kernel<true>, grid, dim3(kBlock), 0, (hipStream_t)stream, src0,
-                       dst0, row0, src1, dst1, row1, idx, nidx);
+                       dst0, row0, src1, dst1, row1, idx);
   else
     hipLaunchKernelGGL(gather2_kernel<false>, grid, dim3(kBlock), 0, (hipStream_t)stream, src0,
-                       dst0, row0, src1, dst1, row1, idx, nidx);
+                       dst0, row0, src1, dst1, row1, idx);
   return check_launch("ssq_gather_rows2");
+}
+
+extern "C" int ssq_bias_act(const float* y, const float* bias, const float* res, float* out,
+                            int64_t n, int64_t hw, int64_t C, int relu, ssq_stream_t stream) {
+  SSQ_REQUIRE(y && out && n >= 0 && hw >= 1 && C >= 1, SSQ_E_ARG, "ssq_bias_act: bad args");
+  SSQ_REQUIRE(n < (1ll << 31) && hw < (1ll << 31) && C < (1ll << 31), SSQ_E_ARG,
+              "ssq_bias_act: tensor exceeds 2^31 elements");
+  if (n == 0) return SSQ_OK;
+  auto al = [](const void* q) { return ((uintptr_t)q & 15u) == 0; };
+  const int vec = n % 4 == 0 && al(y) && al(out) && (!res || al(res));
+  const FastDiv dh = make_fastdiv((uint32_t)hw), dc = make_fastdiv((uint32_t)C);
+  const dim3 grid(grid_for(vec ? n / 4 : n, kBlock, 2048));
+  hipStream_t s = (hipStream_t)stream;
+#define SSQ_BA(R, A)                                                                      \
+  hipLaunchKernelGGL((bias_act_kernel<R, A>), grid, dim3(kBlock), 0, s, y, bias, res, out, \
+                     (uint32_t)n, dh, dc, (uint32_t)C, vec)
+  if (res) {
+    if (relu) SSQ_BA(true, true); else SSQ_BA(true, false);
+  } else {
+    if (relu) SSQ_BA(false, true); else SSQ_BA(false, false);
+  }
+#undef SSQ_BA
+  return check_launch("ssq_bias_act");
+}
+
+extern "C" int ssq_relu_bwd(const float* g, const float* out, float* gin, int64_t n,
+                            ssq_stream_t stream) {
+  SSQ_REQUIRE(g && out && gin && n >= 0 && n < (1ll << 31), SSQ_E_ARG, "ssq_relu_bwd: bad args");
+  if (n == 0) return SSQ_OK;
+  hipStream_t s = (hipStream_t)stream;
+  auto al = [](const void* q) { return ((uintptr_t)q & 15u) == 0; };
+  const bool vec = al(g) && al(out) && al(gin);
+  const int64_t n4 = vec ? n / 4 : 0;
+  if (n4 > 0)
+    hipLaunchKernelGGL(relu_bwd_kernel, dim3(grid_for(n4, kBlock, 2048)), dim3(kBlock), 0, s,
+                       (const f32x4*)g, (const f32x4*)out, (f32x4*)gin, (uint32_t)n4);
+  const int64_t start = n4 * 4;
+  if (start < n)
+    hipLaunchKernelGGL(relu_bwd_tail, dim3((unsigned)((n - start + kBlock - 1) / kBlock)),
+                       dim3(kBlock), 0, s, g, out, gin, (uint32_t)start, (uint32_t)n);
+  return check_launch("ssq_relu_bwd");
 }

@@ -53,6 +53,21 @@ __device__ __forceinline__ void st4(f32x4 v, f32x4* p) {
   else *p = v;
 }
 
+// n / d for 0 <= n < 2^31 as (umulhi(n, m) + n) >> s (round-up magic number, exact;
+// d >= 1).  Replaces 32/64-bit integer divides in per-element index math.
+struct FastDiv {
+  uint32_t m, s;
+};
+inline FastDiv make_fastdiv(uint32_t d) {
+  uint32_t s = 0;
+  while (s < 32 && (1ull << s) < d) ++s;
+  const uint64_t m = ((1ull << 32) * ((1ull << s) - d)) / d + 1;
+  return FastDiv{(uint32_t)m, s};
+}
+__device__ __forceinline__ uint32_t fdiv(uint32_t n, FastDiv f) {
+  return (__umulhi(n, f.m) + n) >> f.s;
+}
+
 // ---------------------------------------------------------------- device math
 __device__ __forceinline__ float clampf(float v, float lo, float hi) {
   // torch.clamp semantics on finite values: min(max(v, lo), hi)

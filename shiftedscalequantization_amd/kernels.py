@@ -529,6 +529,52 @@ def gather_rows2(src0, idx, src1=None, out0=None, out1=None):
     return d0, d1
 
 
+# ------------------------------------------------------------------ K13 fused epilogue
+class BiasActFn(torch.autograd.Function):
+    """act((y + bias[c]) + res) in one kernel (conv bias add quant_layer.py:250, residual
+    add + ReLU quant_block.py:99-117).  The bias is taken as a constant (no
+    reconstruction optimises it); gradients flow to y and res."""
+
+    @staticmethod
+    def forward(ctx, y, bias, res, relu):
+        y, yp = fptr(y.detach(), "conv output")
+        C = y.shape[1] if y.dim() > 1 else 1
+        hw = y[0, 0].numel() if y.dim() > 2 else 1
+        if bias is not None:
+            bias, bp = fptr(bias.detach().reshape(-1), "bias")
+            if bias.numel() != C:
+                raise A.SSQError("bias_act: bias must have one value per channel")
+        else:
+            bp = None
+        if res is not None:
+            res, rp = fptr(res.detach(), "residual")
+            if res.shape != y.shape:
+                raise A.SSQError("bias_act: residual shape mismatch")
+        else:
+            rp = None
+        out = torch.empty_like(y)
+        call("ssq_bias_act", yp, bp, rp, _vp(out), y.numel(), hw, C, int(relu), stream_of(y))
+        ctx.relu = bool(relu)
+        if relu:
+            ctx.save_for_backward(out)
+        return out
+
+    @staticmethod
+    def backward(ctx, g):
+        if ctx.relu:
+            (out,) = ctx.saved_tensors
+            g, gp = fptr(g.contiguous(), "grad")
+            gin = torch.empty_like(g)
+            call("ssq_relu_bwd", gp, _vp(out), _vp(gin), g.numel(), stream_of(g))
+        else:
+            gin = g
+        return gin, None, (gin if ctx.needs_input_grad[2] else None), None
+
+
+def bias_act(y, bias=None, res=None, relu=True):
+    return BiasActFn.apply(y, bias, res, bool(relu))
+
+
 def stream_copy(src, dst):
     call("ssq_stream_copy", _vp(src), _vp(dst), src.numel(), stream_of(src))
 

@@ -7,6 +7,7 @@ crashes on ResNet-50 / MobileNetV2 / RegNetX: quant_model.py:30 vs quant_block.p
 """
 import torch.nn as nn
 
+from .. import kernels as K
 from .. import nets
 from .quant_layer import QuantModule, StraightThrough, UniformAffineQuantizer
 
@@ -92,9 +93,19 @@ class QuantBasicBlock(BaseQuantBlock):
             self.cached_inp_features += [self._cache(x)]
         residual = x if self.downsample is None else self.downsample(x)
         out = self.conv1(x)
-        out = self.conv2(out)
-        out = out + residual
-        out = self._finish(out)
+        c2 = self.conv2
+        if (isinstance(self.activation_function, (nn.ReLU, StraightThrough))
+                and isinstance(c2.activation_function, StraightThrough)
+                and (c2.disable_act_quant or not c2.use_act_quant) and c2.epilogue_fusable(out)):
+            # conv2 bias + residual add + block ReLU as one K13 epilogue pass
+            raw, bias = c2.forward_raw(out)
+            out = K.bias_act(raw, bias, residual, isinstance(self.activation_function, nn.ReLU))
+            if self.use_act_quant:
+                out = self.act_quantizer(out)
+        else:
+            out = c2(out)
+            out = out + residual
+            out = self._finish(out)
         if self.cache_features == 'of':
             self.cached_out_features += [self._cache(out)]
         return out

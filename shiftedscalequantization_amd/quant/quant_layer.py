@@ -187,9 +187,7 @@ class QuantModule(nn.Module):
             self._affine_key = key
         return self._affine_identity
 
-    def forward(self, input: torch.Tensor):
-        if self.cache_features == 'if':
-            self.cached_inp_features += [self._cache(input)]
+    def _weight_bias(self):
         if self.use_weight_quant and self.cache_features == 'none':
             weight = self.weight_quantizer(self.weight)
             # no reconstruction ever optimises the conv bias: its gradient (a full
@@ -198,12 +196,42 @@ class QuantModule(nn.Module):
         else:
             weight = self.org_weight
             bias = self.org_bias
-        out = self.fwd_func(input, weight, bias, **self.fwd_kwargs)
-        if self.use_weight_quant and self.cache_features == 'none' and not self._affine_is_identity():
-            out = out * self.alpha_out + self.beta_out
-        if self.se_module is not None:
-            out = self.se_module(out)
-        out = self.activation_function(out)
+        return weight, bias
+
+    def epilogue_fusable(self, input):
+        """The conv bias add and a ReLU / identity activation can run as the fused K13
+        epilogue (bit-identical to the eager ops): a conv on the device, a constant
+        bias, no gamma^z/phi^z affine, no SE module, no feature caching."""
+        if not (input.is_cuda and self.fwd_func is F.conv2d and self.se_module is None
+                and self.cache_features == 'none'
+                and isinstance(self.activation_function, (nn.ReLU, StraightThrough))):
+            return False
+        if self.bias is not None and self.bias.requires_grad and self.train_bias:
+            return False
+        return not self.use_weight_quant or self._affine_is_identity()
+
+    def forward_raw(self, input):
+        """(conv(input, W_hat) without bias, bias): for a parent block that fuses this
+        module's bias add with its residual add and activation (see epilogue_fusable)."""
+        weight, bias = self._weight_bias()
+        return self.fwd_func(input, weight, None, **self.fwd_kwargs), bias
+
+    def forward(self, input: torch.Tensor):
+        if self.cache_features == 'if':
+            self.cached_inp_features += [self._cache(input)]
+        if self.epilogue_fusable(input):
+            out, bias = self.forward_raw(input)
+            relu = isinstance(self.activation_function, nn.ReLU)
+            if bias is not None or relu:
+                out = K.bias_act(out, bias, None, relu)
+        else:
+            weight, bias = self._weight_bias()
+            out = self.fwd_func(input, weight, bias, **self.fwd_kwargs)
+            if self.use_weight_quant and self.cache_features == 'none' and not self._affine_is_identity():
+                out = out * self.alpha_out + self.beta_out
+            if self.se_module is not None:
+                out = self.se_module(out)
+            out = self.activation_function(out)
         if not self.disable_act_quant:
             if self.use_act_quant:
                 out = self.act_quantizer(out)
