@@ -210,8 +210,8 @@ int ssq_gather_rows2(const float* src0, float* dst0, int64_t row0, const float* 
  * QuantModule conv bias add (quant_layer.py:250), the block's residual add and ReLU
  * (quant_block.py:99-117) in one pass, in the reference's op order:
  *   out = act((y + bias[c]) + res),  c = (i / hw) % C,  act = ReLU if relu else identity.
- * bias / res may be NULL.  ssq_relu_bwd: gin = out > 0 ? g : 0 (ReLU backward on its
- * output).  n < 2^31.                                                                 */
+ * bias / res may be NULL.  ssq_relu_bwd: gin = out <= 0 ? 0 : g (torch's ReLU backward on
+ * its output).  n < 2^31.                                                                */
 int ssq_bias_act(const float* y, const float* bias, const float* res, float* out, int64_t n,
                  int64_t hw, int64_t C, int relu, ssq_stream_t stream);
 int ssq_relu_bwd(const float* g, const float* out, float* gin, int64_t n, ssq_stream_t stream);

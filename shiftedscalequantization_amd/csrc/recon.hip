@@ -123,7 +123,8 @@ __global__ __launch_bounds__(kBlock) void bias_act_kernel(const float* __restric
   }
 }
 
-// ReLU backward (threshold_backward on the output): gin = out > 0 ? g : 0
+// ReLU backward (torch threshold_backward on the output): gin = out <= 0 ? 0 : g
+// (a NaN output passes its gradient, as in torch)
 __global__ __launch_bounds__(kBlock) void relu_bwd_kernel(const f32x4* __restrict__ g,
                                                           const f32x4* __restrict__ out,
                                                           f32x4* __restrict__ gin, uint32_t n4) {
@@ -131,10 +132,10 @@ __global__ __launch_bounds__(kBlock) void relu_bwd_kernel(const f32x4* __restric
   for (uint32_t v = blockIdx.x * blockDim.x + threadIdx.x; v < n4; v += stride) {
     const f32x4 a = g[v], o = out[v];
     f32x4 r;
-    r.x = o.x > 0.0f ? a.x : 0.0f;
-    r.y = o.y > 0.0f ? a.y : 0.0f;
-    r.z = o.z > 0.0f ? a.z : 0.0f;
-    r.w = o.w > 0.0f ? a.w : 0.0f;
+    r.x = o.x <= 0.0f ? 0.0f : a.x;
+    r.y = o.y <= 0.0f ? 0.0f : a.y;
+    r.z = o.z <= 0.0f ? 0.0f : a.z;
+    r.w = o.w <= 0.0f ? 0.0f : a.w;
     gin[v] = r;
   }
 }
@@ -143,7 +144,7 @@ __global__ __launch_bounds__(kBlock) void relu_bwd_tail(const float* __restrict_
                                                         float* __restrict__ gin, uint32_t start,
                                                         uint32_t n) {
   const uint32_t i = start + blockIdx.x * blockDim.x + threadIdx.x;
-  if (i < n) gin[i] = out[i] > 0.0f ? g[i] : 0.0f;
+  if (i < n) gin[i] = out[i] <= 0.0f ? 0.0f : g[i];
 }
 
 }  // namespace ssq
