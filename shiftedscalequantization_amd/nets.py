@@ -175,5 +175,111 @@ def mobilenetv2(**kw):
     return MobileNetV2(**kw)
 
 
+# ------------------------------------------------------------------ RegNetX (models/regnet.py)
+# The RegNet design space (Radosavovic et al. 2020): per-block widths u_j = w0 + wa*j are
+# snapped to w0 * wm^round(log(u_j/w0)/log(wm)), rounded to multiples of 8, grouped into
+# stages of equal width, then made compatible with the group width (bottleneck ratio 1).
+# Module names follow the reference (f.a/a_bn/a_relu, f.b, f.c, proj/bn, relu) so the
+# quant block mapping (QuantResBottleneckBlock) applies unchanged.
+REGNETX = {"regnetx_200m": (36.44, 24, 2.49, 13, 8), "regnetx_400m": (24.48, 24, 2.54, 22, 16),
+           "regnetx_600m": (36.97, 48, 2.24, 16, 24), "regnetx_800m": (35.73, 56, 2.28, 16, 16),
+           "regnetx_1600m": (34.01, 80, 2.25, 18, 24), "regnetx_3200m": (26.31, 88, 2.25, 25, 48),
+           "regnetx_4000m": (38.65, 96, 2.43, 23, 40), "regnetx_6400m": (60.83, 184, 2.07, 17, 56)}
+
+
+def regnet_stages(wa, w0, wm, depth, gw, q=8):
+    """(stage widths, stage depths, group widths) of a RegNetX configuration."""
+    widths = []
+    for j in range(depth):
+        k = round(math.log((w0 + wa * j) / w0) / math.log(wm))
+        widths.append(int(round(w0 * wm ** k / q) * q))
+    sw, sd = [], []
+    for w in widths:
+        if sw and sw[-1] == w:
+            sd[-1] += 1
+        else:
+            sw.append(w)
+            sd.append(1)
+    gs = [min(gw, w) for w in sw]
+    sw = [int(round(w / g) * g) for w, g in zip(sw, gs)]
+    return sw, sd, gs
+
+
+class _BottleneckTransform(nn.Module):
+    def __init__(self, w_in, w_out, stride, gw):
+        super().__init__()
+        self.a = nn.Conv2d(w_in, w_out, 1, 1, 0, bias=False)
+        self.a_bn = nn.BatchNorm2d(w_out)
+        self.a_relu = nn.ReLU(inplace=True)
+        self.b = nn.Conv2d(w_out, w_out, 3, stride, 1, groups=w_out // gw, bias=False)
+        self.b_bn = nn.BatchNorm2d(w_out)
+        self.b_relu = nn.ReLU(inplace=True)
+        self.c = nn.Conv2d(w_out, w_out, 1, 1, 0, bias=False)
+        self.c_bn = nn.BatchNorm2d(w_out)
+
+    def forward(self, x):
+        for m in self.children():
+            x = m(x)
+        return x
+
+
+class ResBottleneckBlock(nn.Module):
+    def __init__(self, w_in, w_out, stride, gw):
+        super().__init__()
+        self.proj_block = w_in != w_out or stride != 1
+        if self.proj_block:
+            self.proj = nn.Conv2d(w_in, w_out, 1, stride, 0, bias=False)
+            self.bn = nn.BatchNorm2d(w_out)
+        self.f = _BottleneckTransform(w_in, w_out, stride, gw)
+        self.relu = nn.ReLU(inplace=True)
+
+    def forward(self, x):
+        skip = self.bn(self.proj(x)) if self.proj_block else x
+        return self.relu(skip + self.f(x))
+
+
+class RegNet(nn.Module):
+    def __init__(self, wa, w0, wm, depth, gw, num_classes=1000, stem_w=32):
+        super().__init__()
+        sw, sd, gs = regnet_stages(wa, w0, wm, depth, gw)
+        self.stem = nn.Sequential(nn.Conv2d(3, stem_w, 3, 2, 1, bias=False), nn.BatchNorm2d(stem_w),
+                                  nn.ReLU(inplace=True))
+        prev = stem_w
+        for i, (w, d, g) in enumerate(zip(sw, sd, gs)):
+            stage = nn.Sequential()
+            for k in range(d):
+                stage.add_module(f"b{k + 1}", ResBottleneckBlock(prev if k == 0 else w, w,
+                                                                 2 if k == 0 else 1, g))
+            self.add_module(f"s{i + 1}", stage)
+            prev = w
+        self.avgpool = nn.AdaptiveAvgPool2d((1, 1))
+        self.fc = nn.Linear(prev, num_classes)
+        for m in self.modules():
+            if isinstance(m, nn.Conv2d):
+                fan_out = m.kernel_size[0] * m.kernel_size[1] * m.out_channels
+                m.weight.data.normal_(0.0, math.sqrt(2.0 / fan_out))
+            elif isinstance(m, nn.BatchNorm2d):
+                m.weight.data.fill_(1)
+                m.bias.data.zero_()
+            elif isinstance(m, nn.Linear):
+                m.weight.data.normal_(0, 1.0 / float(m.weight.size(1)))
+                m.bias.data.zero_()
+        self.stages = len(sw)
+
+    def forward(self, x):
+        x = self.stem(x)
+        for i in range(self.stages):
+            x = getattr(self, f"s{i + 1}")(x)
+        return self.fc(torch.flatten(self.avgpool(x), 1))
+
+
+def _regnet(name):
+    def build(**kw):
+        return RegNet(*REGNETX[name], **kw)
+    build.__name__ = name
+    return build
+
+
 ARCHS = {"resnet18": resnet18, "resnet34": resnet34, "resnet50": resnet50,
          "mobilenetv2": mobilenetv2}
+ARCHS.update({name: _regnet(name) for name in REGNETX})

@@ -73,6 +73,25 @@ class BaseQuantBlock(nn.Module):
             out = self.act_quantizer(out)
         return out
 
+    def _tail(self, last, inp, residual):
+        """last(inp) (+ residual) -> block activation -> block act quant.  When `last` has
+        no activation of its own and the block's is ReLU / identity, its bias add, the
+        residual add and the activation run as one K13 epilogue pass (bit-identical)."""
+        if (residual is not None
+                and isinstance(self.activation_function, (nn.ReLU, StraightThrough))
+                and isinstance(last.activation_function, StraightThrough)
+                and (last.disable_act_quant or not last.use_act_quant)
+                and last.epilogue_fusable(inp)):
+            raw, bias = last.forward_raw(inp)
+            out = K.bias_act(raw, bias, residual, isinstance(self.activation_function, nn.ReLU))
+            if self.use_act_quant:
+                out = self.act_quantizer(out)
+            return out
+        out = last(inp)
+        if residual is not None:
+            out = out + residual
+        return self._finish(out)
+
 
 class QuantBasicBlock(BaseQuantBlock):
     """ResNet-18/34 block (quant_block.py:76-130)."""
@@ -92,20 +111,7 @@ class QuantBasicBlock(BaseQuantBlock):
         if self.cache_features == 'if':
             self.cached_inp_features += [self._cache(x)]
         residual = x if self.downsample is None else self.downsample(x)
-        out = self.conv1(x)
-        c2 = self.conv2
-        if (isinstance(self.activation_function, (nn.ReLU, StraightThrough))
-                and isinstance(c2.activation_function, StraightThrough)
-                and (c2.disable_act_quant or not c2.use_act_quant) and c2.epilogue_fusable(out)):
-            # conv2 bias + residual add + block ReLU as one K13 epilogue pass
-            raw, bias = c2.forward_raw(out)
-            out = K.bias_act(raw, bias, residual, isinstance(self.activation_function, nn.ReLU))
-            if self.use_act_quant:
-                out = self.act_quantizer(out)
-        else:
-            out = c2(out)
-            out = out + residual
-            out = self._finish(out)
+        out = self._tail(self.conv2, self.conv1(x), residual)
         if self.cache_features == 'of':
             self.cached_out_features += [self._cache(out)]
         return out
@@ -136,8 +142,7 @@ class QuantBottleneck(BaseQuantBlock):
         if self.cache_features == 'if':
             self.cached_inp_features += [self._cache(x)]
         residual = x if self.downsample is None else self.downsample(x)
-        out = self.conv3(self.conv2(self.conv1(x)))
-        out = self._finish(out + residual)
+        out = self._tail(self.conv3, self.conv2(self.conv1(x)), residual)
         if self.cache_features == 'of':
             self.cached_out_features += [self._cache(out)]
         return out
@@ -163,8 +168,7 @@ class QuantResBottleneckBlock(BaseQuantBlock):
         if self.cache_features == 'if':
             self.cached_inp_features += [self._cache(x)]
         residual = self.downsample(x) if self.proj_block else x
-        out = self.conv3(self.conv2(self.conv1(x)))
-        out = self._finish(out + residual)
+        out = self._tail(self.conv3, self.conv2(self.conv1(x)), residual)
         if self.cache_features == 'of':
             self.cached_out_features += [self._cache(out)]
         return out
@@ -195,8 +199,11 @@ class QuantInvertedResidual(BaseQuantBlock):
     def forward(self, x):
         if self.cache_features == 'if':
             self.cached_inp_features += [self._cache(x)]
-        out = x + self.conv(x) if self.use_res_connect else self.conv(x)
-        out = self._finish(out)
+        h = x
+        for m in list(self.conv)[:-1]:
+            h = m(h)
+        # x + conv(x): fp32 addition commutes, so the fused (conv + bias) + x is bit-identical
+        out = self._tail(self.conv[-1], h, x if self.use_res_connect else None)
         if self.cache_features == 'of':
             self.cached_out_features += [self._cache(out)]
         return out
@@ -206,6 +213,7 @@ specials = {
     nets.BasicBlock: QuantBasicBlock,
     nets.Bottleneck: QuantBottleneck,
     nets.InvertedResidual: QuantInvertedResidual,
+    nets.ResBottleneckBlock: QuantResBottleneckBlock,
 }
 
 

@@ -92,14 +92,33 @@ def test_quant_model_structure_resnet18():
     assert qnn.model.layer2[0].downsample.pathName == ".layer2.0.downsample"
 
 
-@pytest.mark.parametrize("arch,nq", [("resnet50", 54), ("mobilenetv2", 53)])
-def test_quant_model_other_archs(arch, nq):
-    """The reference crashes here (setPathName missing on non-basic blocks)."""
+@pytest.mark.parametrize("arch,nq,nw", [("resnet50", 54, 25502912), ("mobilenetv2", 53, 3469760),
+                                        ("regnetx_3200m", 81, 15232992)])
+def test_quant_model_other_archs(arch, nq, nw):
+    """The reference crashes here (setPathName missing on non-basic blocks).  Layer and
+    weight counts are SURVEY §8(a)'s (RegNetX-3200M: 81 layers, 15.2 M weights)."""
     from shiftedscalequantization_amd import nets
-    from shiftedscalequantization_amd.quant import QuantModel, QuantModule
+    from shiftedscalequantization_amd.quant import QuantModel, QuantModule, BaseQuantBlock
     qnn = QuantModel(nets.ARCHS[arch](), {"n_bits": 2, "channel_wise": True, "scale_method": "max"},
                      {"n_bits": 4, "channel_wise": False, "scale_method": "mse", "leaf_param": True})
-    assert len([m for m in qnn.modules() if isinstance(m, QuantModule)]) == nq
+    qms = [m for m in qnn.modules() if isinstance(m, QuantModule)]
+    assert len(qms) == nq
+    assert sum(m.weight.numel() for m in qms) == nw
+    assert all(b.pathName for b in qnn.modules() if isinstance(b, BaseQuantBlock))
+
+
+def test_regnetx_design_space():
+    """RegNetX stage widths / depths / groups from the design-space generator: the
+    3200M model has 25 grouped 3x3 convs with g in {2, 4, 9, 21}."""
+    import torch.nn as nn
+    from shiftedscalequantization_amd import nets
+    assert nets.regnet_stages(*nets.REGNETX["regnetx_3200m"]) == ([96, 192, 432, 1008], [2, 6, 15, 2],
+                                                                   [48, 48, 48, 48])
+    assert nets.regnet_stages(*nets.REGNETX["regnetx_600m"]) == ([48, 96, 240, 528], [1, 3, 5, 7],
+                                                                  [24, 24, 24, 24])
+    m = nets.ARCHS["regnetx_3200m"]()
+    groups = [c.groups for c in m.modules() if isinstance(c, nn.Conv2d) and c.groups > 1]
+    assert len(groups) == 25 and set(groups) == {2, 4, 9, 21}
 
 
 def test_driver_flag_parsing():
