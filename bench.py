@@ -181,6 +181,14 @@ def main():
         copy_gbs = max(copy_gbs, 8.0 * n_act / (ms_copy * 1e-3) / 1e9)
     K.set_variant(default_variant)
     ms_w = time_events(lambda: K.fake_quant_multi(weights, dws, zws, bits), 20, dev)
+    # W2 per-channel q/dq of the large synthetic weight of BASELINE.md §2 ([8192,2048,3,3],
+    # per-output-channel delta/zp staged in LDS): the per-channel kernel's roofline line
+    big = torch.empty(8192, 2048, 3, 3, device=dev).normal_(0.0, 0.02)
+    d_big, z_big, _ = K.scale_init(big, 2, False, True, "max")
+    y_big = torch.empty_like(big)
+    ms_pc = time_events(lambda: K.fake_quant_fwd(big, d_big, z_big, 2, out=y_big), 10, dev)
+    pc_gbs = 8.0 * big.numel() / (ms_pc * 1e-3) / 1e9
+    del big, y_big
 
     recon = None
     if not args.no_recon:
@@ -215,6 +223,10 @@ def main():
                      "stream_copy_gbs": round(copy_gbs, 1),
                      "frac_of_stream_copy": round(achieved / copy_gbs, 4)},
         "weights_multi_ms": round(ms_w, 4),
+        "roofline_per_channel": {"kernel": "fq_fwd_multi_kernel (ssq_fq_fwd per-channel, 1 segment)",
+                                 "workload": "W2 per-channel q/dq of [8192,2048,3,3] (151 M elems)",
+                                 "achieved": round(pc_gbs, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                                 "frac": round(pc_gbs / HBM_PEAK_GBS, 4), "kernel_ms": round(ms_pc, 4)},
     }
     if recon is not None:
         out["recon"] = recon

@@ -193,11 +193,13 @@ int ssq_inpscale_fwd(const float* W, const float* inp_scale, const float* delta,
  *   loss = sum |pred-tgt|^p / M ;  grad = gscale * ((1/M) * (p*|d|^(p-1)) * sgn(d))
  * M = n / C for reduction 'none' (sum over dim 1, mean over the rest), n for 'all'.
  * loss_out / grad / gscale (a DEVICE scalar, the upstream gradient) may each be NULL.
- * The loss reduction is deterministic.                                                */
+ * relu_mask != 0: pred is the output of a ReLU and grad is written at the ReLU's input
+ * (grad = 0 where pred <= 0, torch's threshold_backward) -- the block's final ReLU
+ * backward folded into the loss pass.  The loss reduction is deterministic.          */
 size_t ssq_lp_loss_workspace_size(int64_t n);
 int ssq_lp_loss(const float* pred, const float* tgt, int64_t n, int64_t M, float p,
-                float* loss_out, float* grad, const float* gscale, void* ws, size_t ws_bytes,
-                ssq_stream_t stream);
+                float* loss_out, float* grad, const float* gscale, int relu_mask, void* ws,
+                size_t ws_bytes, ssq_stream_t stream);
 
 /* ---------------------------------------------------------------- K14 batch gather
  * dst_k[r] = src_k[idx[r]] for two sources at once (cached block input and output,

@@ -176,12 +176,13 @@ struct Seg {
   float* y;
   const float* delta;
   const float* zp;
-  uint32_t n;     // elements (< 2^31)
-  uint32_t blk0;  // first workgroup of this segment
+  uint8_t* codes;  // may be null
+  uint32_t n;      // elements (< 2^31)
+  uint32_t blk0;   // first workgroup of this segment
   uint32_t inner, nch;
-  float lo, hi;
+  float lo, hi, scale;
   FastDiv div_inner;
-  uint32_t vec;   // x and y 16-B aligned: float4 path
+  uint32_t vec;    // x, y 16-B (codes 4-B) aligned: float4 path
 };
 constexpr int kMaxSeg = 48;      // keeps the by-value table under 4 KiB of kernel arguments
 constexpr int kTile = 4096;      // elements per workgroup: 4 float4 per thread
@@ -203,7 +204,7 @@ __global__ __launch_bounds__(kBlock) void fq_fwd_multi_kernel(SegTable tab) {
   const uint32_t t1 = min(t0 + (uint32_t)kTile, sg.n);
   const uint32_t c0 = fdiv(t0, sg.div_inner), c1 = fdiv(t1 - 1, sg.div_inner);
   for (uint32_t c = c0 + threadIdx.x; c <= c1; c += blockDim.x) {
-    sd[c - c0] = sg.delta[c % sg.nch];
+    sd[c - c0] = __fmul_rn(sg.delta[c % sg.nch], sg.scale);
     sz[c - c0] = sg.zp[c % sg.nch];
   }
   __syncthreads();
@@ -227,7 +228,7 @@ __global__ __launch_bounds__(kBlock) void fq_fwd_multi_kernel(SegTable tab) {
       const uint32_t e = v * 4;
       uint32_t c = fdiv(e, sg.div_inner);
       uint32_t next = (c + 1) * sg.inner;
-      float a[4] = {in[u].x, in[u].y, in[u].z, in[u].w}, o[4];
+      float a[4] = {in[u].x, in[u].y, in[u].z, in[u].w}, o[4], q[4];
 #pragma unroll
       for (int j = 0; j < 4; ++j) {
         while (e + j >= next) {
@@ -235,8 +236,7 @@ __global__ __launch_bounds__(kBlock) void fq_fwd_multi_kernel(SegTable tab) {
           next += sg.inner;
         }
         QParams p{sd[c - c0], sz[c - c0], lo, hi};
-        float q;
-        o[j] = fq1(a[j], p, &q);
+        o[j] = fq1(a[j], p, &q[j]);
       }
       f32x4 r;
       r.x = o[0];
@@ -244,6 +244,7 @@ __global__ __launch_bounds__(kBlock) void fq_fwd_multi_kernel(SegTable tab) {
       r.z = o[2];
       r.w = o[3];
       __builtin_nontemporal_store(r, &yv[v]);
+      if (sg.codes) ((uint32_t*)sg.codes)[v] = pack4(q[0], q[1], q[2], q[3]);
     }
     e_tail = v1 * 4;
   }
@@ -252,6 +253,7 @@ __global__ __launch_bounds__(kBlock) void fq_fwd_multi_kernel(SegTable tab) {
     QParams p{sd[cl], sz[cl], lo, hi};
     float q;
     sg.y[e] = fq1(sg.x[e], p, &q);
+    if (sg.codes) sg.codes[e] = (uint8_t)((int)q & 0xff);
   }
 }
 
@@ -492,6 +494,15 @@ extern "C" int ssq_fq_fwd(const float* x, float* y, void* codes, const float* de
                                  chunk);
       else
         launch_stream<FqPt>(v, grid, block, s, xv, yv, cv, delta, zp, n4, scale, lo, hi, chunk);
+    } else if (n < (1ll << 31) && (n + kTile - 1) / kTile < (1ll << 31)) {
+      // per-channel: the LDS-staged tile kernel with one segment (no 64-bit divides)
+      SegTable tab;
+      tab.nseg = 1;
+      tab.s[0] = Seg{x, y, delta, zp, (uint8_t*)codes, (uint32_t)n, 0u, (uint32_t)inner,
+                     (uint32_t)nch, lo, hi, scale, make_fastdiv((uint32_t)inner), 1u};
+      hipLaunchKernelGGL(fq_fwd_multi_kernel, dim3((unsigned)((n + kTile - 1) / kTile)),
+                         dim3(kBlock), 0, s, tab);
+      return check_launch("ssq_fq_fwd");
     } else {
       SSQ_REQUIRE(inner < (1ll << 31) && nch < (1ll << 31), SSQ_E_ARG, "ssq_fq_fwd: dims");
       const int grid = grid_for(n4, kBlock, 4096);
@@ -535,8 +546,8 @@ extern "C" int ssq_fq_fwd_multi(int nseg, const float* const* x, float* const* y
     for (int k = 0; k < tab.nseg; ++k) {
       const int i = base + k;
       const bool vec = aligned16(x[i]) && aligned16(y[i]);
-      tab.s[k] = Seg{x[i], y[i], delta[i], zp[i], (uint32_t)n[i], (uint32_t)blk,
-                     (uint32_t)inner[i], (uint32_t)nch[i], (float)qmin[i], (float)qmax[i],
+      tab.s[k] = Seg{x[i], y[i], delta[i], zp[i], nullptr, (uint32_t)n[i], (uint32_t)blk,
+                     (uint32_t)inner[i], (uint32_t)nch[i], (float)qmin[i], (float)qmax[i], 1.0f,
                      make_fastdiv((uint32_t)inner[i]), vec ? 1u : 0u};
       blk += (n[i] + kTile - 1) / kTile;
     }

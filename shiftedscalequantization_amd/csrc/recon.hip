@@ -19,6 +19,7 @@ __global__ __launch_bounds__(kBlock) void lp_loss_kernel(const float* __restrict
                                                          float p, float inv_m,
                                                          float* __restrict__ grad,
                                                          const float* __restrict__ gscale,
+                                                         int relu_mask,
                                                          double* __restrict__ part) {
   __shared__ double red[16];
   double acc = 0.0;
@@ -41,7 +42,10 @@ __global__ __launch_bounds__(kBlock) void lp_loss_kernel(const float* __restrict
     acc += (double)pw;
     if (grad) {
       const float sg = d > 0.0f ? 1.0f : (d < 0.0f ? -1.0f : 0.0f);
-      grad[i] = __fmul_rn(__fmul_rn(__fmul_rn(inv_m, dp), sg), gs);
+      const float gv = __fmul_rn(__fmul_rn(__fmul_rn(inv_m, dp), sg), gs);
+      // relu_mask: pred is a ReLU output; write the gradient at the ReLU's input
+      // (torch threshold_backward: out <= 0 -> 0)
+      grad[i] = (relu_mask && pred[i] <= 0.0f) ? 0.0f : gv;
     }
   }
   if (!part) return;
@@ -157,8 +161,8 @@ extern "C" size_t ssq_lp_loss_workspace_size(int64_t n) {
 }
 
 extern "C" int ssq_lp_loss(const float* pred, const float* tgt, int64_t n, int64_t M, float p,
-                           float* loss_out, float* grad, const float* gscale, void* ws,
-                           size_t ws_bytes, ssq_stream_t stream) {
+                           float* loss_out, float* grad, const float* gscale, int relu_mask,
+                           void* ws, size_t ws_bytes, ssq_stream_t stream) {
   SSQ_REQUIRE(pred && tgt && n >= 1 && M >= 1 && (loss_out || grad), SSQ_E_ARG,
               "ssq_lp_loss: bad args");
   SSQ_REQUIRE(!loss_out || (ws && ws_bytes >= ssq_lp_loss_workspace_size(n)), SSQ_E_WS,
@@ -169,13 +173,13 @@ extern "C" int ssq_lp_loss(const float* pred, const float* tgt, int64_t n, int64
   double* part = loss_out ? (double*)ws : nullptr;
   if (p == 2.0f)
     hipLaunchKernelGGL(lp_loss_kernel<0>, dim3(grid), dim3(kBlock), 0, s, pred, tgt, n, p, inv_m,
-                       grad, gscale, part);
+                       grad, gscale, relu_mask, part);
   else if (p == 1.0f)
     hipLaunchKernelGGL(lp_loss_kernel<1>, dim3(grid), dim3(kBlock), 0, s, pred, tgt, n, p, inv_m,
-                       grad, gscale, part);
+                       grad, gscale, relu_mask, part);
   else
     hipLaunchKernelGGL(lp_loss_kernel<2>, dim3(grid), dim3(kBlock), 0, s, pred, tgt, n, p, inv_m,
-                       grad, gscale, part);
+                       grad, gscale, relu_mask, part);
   if (loss_out)
     hipLaunchKernelGGL(lp_loss_finalize, dim3(1), dim3(kBlock), 0, s, (const double*)part, grid,
                        (double)M, loss_out);

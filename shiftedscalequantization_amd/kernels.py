@@ -473,15 +473,17 @@ def _lp_M(pred, reduction):
     return pred.numel()
 
 
-def lp_loss_and_grad(pred, tgt, p=2.0, reduction="none", want_grad=True, loss_out=None):
-    """lp_loss value (1-element device tensor) and d/d pred in one fused pass."""
+def lp_loss_and_grad(pred, tgt, p=2.0, reduction="none", want_grad=True, loss_out=None,
+                     relu_mask=False):
+    """lp_loss value (1-element device tensor) and d/d pred in one fused pass.  With
+    relu_mask, pred is a ReLU output and the gradient is returned at the ReLU's input."""
     pred, pp = fptr(pred.detach(), "pred")
     tgt, tp = fptr(tgt.detach(), "tgt")
     loss = torch.empty(1, dtype=torch.float32, device=pred.device) if loss_out is None else loss_out
     grad = torch.empty_like(pred) if want_grad else None
     ws, wsn = workspace(query("ssq_lp_loss_workspace_size", pred.numel()), pred.device)
     call("ssq_lp_loss", pp, tp, pred.numel(), _lp_M(pred, reduction), float(p), _vp(loss),
-         _vp(grad), None, ws, wsn, stream_of(pred))
+         _vp(grad), None, int(bool(relu_mask)), ws, wsn, stream_of(pred))
     return loss, grad
 
 
@@ -504,7 +506,7 @@ class LpLossFn(torch.autograd.Function):
         grad = torch.empty_like(pred)
         gs = g.detach().reshape(1).to(torch.float32).contiguous()
         call("ssq_lp_loss", _vp(pred), _vp(tgt), pred.numel(), _lp_M(pred, reduction), float(p),
-             None, _vp(grad), _vp(gs), None, 0, stream_of(pred))
+             None, _vp(grad), _vp(gs), 0, None, 0, stream_of(pred))
         return grad, None, None, None
 
 
@@ -572,7 +574,12 @@ class BiasActFn(torch.autograd.Function):
 
 
 def bias_act(y, bias=None, res=None, relu=True):
-    return BiasActFn.apply(y, bias, res, bool(relu))
+    out = BiasActFn.apply(y, bias, res, bool(relu))
+    if relu:
+        # lets a loss that folds the ReLU backward into its own pass (lp_loss relu_mask)
+        # back-propagate from the ReLU's inputs directly
+        out._ssq_relu_inputs = tuple(t for t in (y, res) if t is not None and t.requires_grad)
+    return out
 
 
 def stream_copy(src, dst):

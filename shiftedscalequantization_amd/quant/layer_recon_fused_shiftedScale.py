@@ -86,8 +86,15 @@ def _fused_loop(block, modules, iters, lmda, model, p, lr, bias_cal, batch_size,
         (+ RCCL bucket) -> Adam.  No host sync, no host-side state: graph-capturable."""
         cur_inp, cur_out = feeder.gather()
         quant_out = block(cur_inp)
-        rec, g_out = loss_func.loss_and_grad(quant_out, cur_out)
-        quant_out.backward(g_out)
+        relu_in = getattr(quant_out, '_ssq_relu_inputs', None)
+        if relu_in:
+            # the block ends in the fused epilogue's ReLU: the loss pass writes the gradient
+            # at the ReLU's input and backward starts from the epilogue's inputs
+            rec, g_pre = loss_func.loss_and_grad(quant_out, cur_out, relu_mask=True)
+            torch.autograd.backward(list(relu_in), [g_pre] * len(relu_in))
+        else:
+            rec, g_out = loss_func.loss_and_grad(quant_out, cur_out)
+            quant_out.backward(g_out)
         if bucket is not None:
             bucket.allreduce_()
         optimizer.step()
@@ -271,12 +278,13 @@ class FusedScaleLossFunction:
         for qt in self.quantizer:
             qt._fused_reg = None
 
-    def loss_and_grad(self, pred, tgt):
-        """One ssq_lp_loss pass: the loss value AND d loss / d pred (device only).  The
-        caller back-propagates `grad` from `pred` -- exactly what total_loss.backward()
-        delivers there; the regulariser terms reach alpha through the armed adaShift
-        backward, and beta is never optimised by this loop."""
-        rec_loss, grad = K.lp_loss_and_grad(pred, tgt, self.p)
+    def loss_and_grad(self, pred, tgt, relu_mask=False):
+        """One ssq_lp_loss pass: the loss value AND d loss / d pred (device only) -- or,
+        with relu_mask, d loss / d (ReLU input) when pred is a ReLU output.  The caller
+        back-propagates it -- exactly what total_loss.backward() delivers there; the
+        regulariser terms reach alpha through the armed adaShift backward, and beta is
+        never optimised by this loop."""
+        rec_loss, grad = K.lp_loss_and_grad(pred, tgt, self.p, relu_mask=relu_mask)
         return rec_loss[0], grad
 
     def fused(self, pred, tgt):

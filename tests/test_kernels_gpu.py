@@ -497,3 +497,18 @@ def test_other_blocks_fused_epilogue_matches_unfused(K, kind):
         outs.append((host(y), host(xx.grad)))
     np.testing.assert_array_equal(outs[0][0], outs[1][0])
     np.testing.assert_array_equal(outs[0][1], outs[1][1])
+
+
+def test_lp_loss_relu_mask_folds_relu_backward(K):
+    """lp_loss(relu(t), tgt) with relu_mask: the gradient written is d loss / d t, equal
+    to torch autograd through the ReLU of the unmasked lp gradient, bit for bit."""
+    gen = torch.Generator().manual_seed(21)
+    t = torch.randn(8, 16, 9, 9, generator=gen).cuda()
+    t.view(-1)[:2] = torch.tensor([0.0, -0.0])
+    out = torch.relu(t)
+    tgt = torch.randn(8, 16, 9, 9, generator=gen).cuda()
+    l1, g_plain = K.lp_loss_and_grad(out, tgt, 2.0)
+    l2, g_mask = K.lp_loss_and_grad(out, tgt, 2.0, relu_mask=True)
+    assert host(l1) == host(l2)
+    ref = torch.where(out <= 0, torch.zeros_like(g_plain), g_plain)
+    np.testing.assert_array_equal(host(g_mask), host(ref))
