@@ -603,33 +603,23 @@ __global__ __launch_bounds__(1024) void alpha_col_stage1(
   }
 }
 
-// Stage 2: one thread per input channel sums the chunk partials in chunk order (the
-// loads of a chunk are coalesced across the wave), then applies the softmax/clamp chain
-// (+ regulariser, MODE 0) or the init_alpha logits (MODE 2) -- every lane in parallel.
+// Stage 2: one wave per input channel -- lane c loads chunk c's partials (one round of
+// loads), a fixed shuffle tree sums them (deterministic), and lane 0 applies the
+// softmax/clamp chain (+ regulariser, MODE 0) or the init_alpha logits (MODE 2).
 template <int MODE, int NS>
 __global__ __launch_bounds__(kBlock) void alpha_col_stage2(
     const double* __restrict__ part, uint32_t nchunk, const float* __restrict__ alpha, Shifts sh,
     Geo g, float reg_lambda, float reg_b, const float* __restrict__ reg_dev,
     float* __restrict__ out_alpha, float* __restrict__ side) {
   const int S = NS > 0 ? NS : sh.n;
-  const uint32_t ci = blockIdx.x * blockDim.x + threadIdx.x;
+  const uint32_t ci = blockIdx.x * (blockDim.x / kWave) + threadIdx.x / kWave;
+  const uint32_t lane = threadIdx.x & (kWave - 1);
   if (ci >= g.Ci) return;
   double tot[kMaxS];
-  for (int i = 0; i < S; ++i) tot[i] = 0.0;
-  // batches of 8 chunks: all loads of a batch in flight before the in-order adds
-  constexpr int CB = 8;
-  uint32_t c = 0;
-  for (; c + CB <= nchunk; c += CB) {
-    double v[CB][kMaxS];
-#pragma unroll
-    for (int k = 0; k < CB; ++k)
-      for (int i = 0; i < S; ++i) v[k][i] = part[((size_t)(c + k) * g.Ci + ci) * S + i];
-#pragma unroll
-    for (int k = 0; k < CB; ++k)
-      for (int i = 0; i < S; ++i) tot[i] += v[k][i];
-  }
-  for (; c < nchunk; ++c)
-    for (int i = 0; i < S; ++i) tot[i] += part[((size_t)c * g.Ci + ci) * S + i];
+  for (int i = 0; i < S; ++i)
+    tot[i] = lane < nchunk ? part[((size_t)lane * g.Ci + ci) * S + i] : 0.0;
+  for (int i = 0; i < S; ++i) tot[i] = wave_sum(tot[i]);
+  if (lane != 0) return;
   if (MODE == 2) {
     float a[kMaxS];
     init_alpha_row(tot, S, a);
@@ -673,7 +663,8 @@ static int launch_alpha_col(const Geo& g, const Shifts& sh, const float* gWhat, 
     default: SSQ_STAGE1(0); break;
   }
 #undef SSQ_STAGE1
-  const unsigned blocks2 = (g.Ci + kBlock - 1) / kBlock;
+  const unsigned waves = kBlock / kWave;
+  const unsigned blocks2 = (g.Ci + waves - 1) / waves;
 #define SSQ_STAGE2(NS)                                                                         \
   hipLaunchKernelGGL((alpha_col_stage2<MODE, NS>), dim3(blocks2), dim3(kBlock), 0, s,             \
                      (const double*)ws, tl.nchunk, alpha, sh, g, reg_lambda, reg_b, reg_dev,     \

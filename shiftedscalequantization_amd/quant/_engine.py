@@ -24,10 +24,15 @@ class BatchFeeder:
         self.bs = min(batch_size, self.N)
         self.device = device
         pin = torch.cuda.is_available()
-        self.ring = [torch.empty(self.bs, dtype=torch.int64, pin_memory=pin) for _ in range(self.RING)]
+        # one pinned slot = the batch indices + one 8-byte word carrying two fp32 values
+        # riding on the same H2D copy (the loop's (lambda_S, b2) schedule pair)
+        self.ring = [torch.zeros(self.bs + 1, dtype=torch.int64, pin_memory=pin)
+                     for _ in range(self.RING)]
         self.done = [None] * self.RING
         self.k = 0
-        self.didx = torch.empty(self.bs, dtype=torch.int64, device=device)
+        self._dev = torch.zeros(self.bs + 1, dtype=torch.int64, device=device)
+        self.didx = self._dev[:self.bs]
+        self.extra = self._dev[self.bs:].view(torch.float32)      # 2 floats on the device
         self.cur_inp = torch.empty((self.bs,) + tuple(self.inp.shape[1:]), device=device)
         self.cur_out = torch.empty((self.bs,) + tuple(self.out.shape[1:]), device=device)
 
@@ -35,13 +40,17 @@ class BatchFeeder:
         """One reference-identical draw: torch.randperm(N)[:batch_size] on the CPU."""
         return torch.randperm(self.N)[:self.bs]
 
-    def stage(self, perm):
-        """Host -> device copy of the batch indices into the static index buffer."""
+    def stage(self, perm, extra=None):
+        """One host -> device copy of the batch indices (and, optionally, two fp32 values
+        into self.extra) into the static device buffer."""
         slot = self.k % self.RING
         if self.done[slot] is not None:
             self.done[slot].synchronize()
-        self.ring[slot].copy_(perm)
-        self.didx.copy_(self.ring[slot], non_blocking=True)
+        h = self.ring[slot]
+        h[:self.bs].copy_(perm)
+        if extra is not None:
+            h[self.bs:].view(torch.float32).copy_(torch.as_tensor(extra, dtype=torch.float32))
+        self._dev.copy_(h, non_blocking=True)
         ev = torch.cuda.Event()
         ev.record()
         self.done[slot] = ev

@@ -78,7 +78,8 @@ def _fused_loop(block, modules, iters, lmda, model, p, lr, bias_cal, batch_size,
     feeder = BatchFeeder(torch.cat(block.cached_inp_features), torch.cat(block.cached_out_features),
                          batch_size, device)
     bucket = GradBucket(opt_params, average=dp_average) if world() > 1 else None
-    regp = loss_func.arm(device)    # device (lambda_S, b2) read by the adaShift backward
+    # device (lambda_S, b2) read by the adaShift backward; it rides on the index copy
+    regp = loss_func.arm(device, regp=feeder.extra)
     last = {}
 
     def body():
@@ -106,8 +107,8 @@ def _fused_loop(block, modules, iters, lmda, model, p, lr, bias_cal, batch_size,
     for i in t:
         if iter_hook is not None:
             iter_hook(i)
-        feeder.stage(feeder.draw())            # reference-identical CPU randperm draw
-        loss_func.upload_schedule(regp)        # this iteration's (lambda_S, b2)
+        # reference-identical CPU randperm draw + this iteration's (lambda_S, b2): one H2D copy
+        feeder.stage(feeder.draw(), extra=loss_func.schedule_pair())
         if use_graph and i == GRAPH_WARMUP:
             optimizer.zero_grad(set_to_none=True)
             graph_obj = torch.cuda.CUDAGraph()
@@ -243,11 +244,13 @@ class FusedScaleLossFunction:
         return total
 
     # ---------------------------------------------------------------- fused fast path
-    def arm(self, device):
+    def arm(self, device, regp=None):
         """Give every quantizer's adaShift backward the shift regulariser, with
-        (lambda_S, b2) read from a device pair that upload_schedule() refreshes before each
-        iteration (lambda_S = 0 during warm-up).  Returns that device pair."""
-        self._regp = torch.zeros(2, dtype=torch.float32, device=device)
+        (lambda_S, b2) read from a device pair refreshed before each iteration
+        (lambda_S = 0 during warm-up): `regp` (e.g. the BatchFeeder's extra word, which
+        rides on the index copy) or a pair of its own that upload_schedule() fills.
+        Returns that device pair."""
+        self._regp = torch.zeros(2, dtype=torch.float32, device=device) if regp is None else regp
         self._regp_host = [torch.zeros(2, dtype=torch.float32, pin_memory=torch.cuda.is_available())
                            for _ in range(4)]
         self._regp_done = [None] * 4
@@ -258,6 +261,11 @@ class FusedScaleLossFunction:
             self._reg_vals[id(qt)] = vals
             qt._fused_reg = (0.0, 0.0, vals, self._regp)
         return self._regp
+
+    def schedule_pair(self):
+        """This iteration's (lambda_S, b2) for the armed backward ((0, 0) in warm-up)."""
+        (b, b2), active = self._schedule()
+        return (float(self.lmdaS), float(b2)) if active else (0.0, 0.0)
 
     def upload_schedule(self, regp=None):
         """H2D (non-blocking, pinned ring) of this iteration's (lambda_S, b2)."""
