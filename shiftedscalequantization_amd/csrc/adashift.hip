@@ -82,32 +82,30 @@ __global__ __launch_bounds__(kBlock) void adashift_fwd_kernel(
 // ------------------------------------------------------------------ shared stage-2 helper
 // Backward through p = clamp(softmax(a)*c + gamma, 0, 1), plus the optional shift
 // regulariser lambda*sum(1-|2p-1|^b) (value returned, gradient folded into g_p).
-__device__ __forceinline__ float alpha_chain(const float* a, int S, double* g_p, float reg_lambda,
-                                             float reg_b, int reg_mode, float* ga_out) {
-  float s[kMaxS], p[kMaxS];
-  soft_targets<kMaxS>(a, S, s, p);
-  // the regulariser in fp32 like the reference's tensor ops (pow / log and their
-  // autograd), summed in double for a deterministic value
-  float reg = 0.0f;
-  if (reg_lambda != 0.0f) {
-    double acc = 0.0;
-    for (int i = 0; i < S; ++i) {
-      if (reg_mode == 0) {  // lambda * sum(1 - ((p - 0.5).abs() * 2).pow(b))
-        const float r = __fmul_rn(fabsf(__fsub_rn(p[i], 0.5f)), 2.0f);
-        acc += (double)__fsub_rn(1.0f, powf(r, reg_b));
-        if (reg_b != 0.0f) {
-          const float sg = p[i] > 0.5f ? 1.0f : (p[i] < 0.5f ? -1.0f : 0.0f);
-          const float gr = __fmul_rn(__fmul_rn(-reg_lambda, reg_b), powf(r, __fsub_rn(reg_b, 1.0f)));
-          g_p[i] += (double)__fmul_rn(__fmul_rn(gr, 2.0f), sg);
-        }
-      } else {  // entropy: -lambda * sum p log(p + 1e-10)
-        const float lg = logf(__fadd_rn(p[i], 1e-10f));
-        acc += -(double)__fmul_rn(p[i], lg);
-        g_p[i] += (double)(-reg_lambda * __fadd_rn(lg, p[i] / __fadd_rn(p[i], 1e-10f)));
-      }
+// One shift's regulariser term and its gradient wrt p_i, in fp32 like the reference's
+// tensor ops (pow / log and their autograd): mode 0 = lambda * (1 - |2p-1|^b) (without
+// lambda in the value), mode 1 = entropy -p log(p + 1e-10).
+__device__ __forceinline__ void reg_term(float p, float reg_lambda, float reg_b, int reg_mode,
+                                         double& val, double& grad) {
+  if (reg_mode == 0) {  // lambda * sum(1 - ((p - 0.5).abs() * 2).pow(b))
+    const float r = __fmul_rn(fabsf(__fsub_rn(p, 0.5f)), 2.0f);
+    val = (double)__fsub_rn(1.0f, powf(r, reg_b));
+    grad = 0.0;
+    if (reg_b != 0.0f) {
+      const float sg = p > 0.5f ? 1.0f : (p < 0.5f ? -1.0f : 0.0f);
+      const float gr = __fmul_rn(__fmul_rn(-reg_lambda, reg_b), powf(r, __fsub_rn(reg_b, 1.0f)));
+      grad = (double)__fmul_rn(__fmul_rn(gr, 2.0f), sg);
     }
-    reg = (float)((double)reg_lambda * acc);
+  } else {
+    const float lg = logf(__fadd_rn(p, 1e-10f));
+    val = -(double)__fmul_rn(p, lg);
+    grad = (double)(-reg_lambda * __fadd_rn(lg, p / __fadd_rn(p, 1e-10f)));
   }
+}
+
+// Backward through p = clamp(softmax(a)*c + gamma, 0, 1) given d/dp in g_p (double).
+__device__ __forceinline__ void softmax_clamp_bwd(const float* s, int S, const double* g_p,
+                                                  float* ga_out) {
   double gs[kMaxS], dot = 0.0;
   for (int i = 0; i < S; ++i) {
     const float u = __fadd_rn(__fmul_rn(s[i], kZmG), kGamma);
@@ -115,6 +113,26 @@ __device__ __forceinline__ float alpha_chain(const float* a, int S, double* g_p,
     dot += gs[i] * (double)s[i];
   }
   for (int i = 0; i < S; ++i) ga_out[i] = (float)((double)s[i] * (gs[i] - dot));
+}
+
+// g_p += regulariser gradient; returns the regulariser value (summed in double, fixed
+// order); then the softmax/clamp backward into ga_out.
+__device__ __forceinline__ float alpha_chain(const float* a, int S, double* g_p, float reg_lambda,
+                                             float reg_b, int reg_mode, float* ga_out) {
+  float s[kMaxS], p[kMaxS];
+  soft_targets<kMaxS>(a, S, s, p);
+  float reg = 0.0f;
+  if (reg_lambda != 0.0f) {
+    double acc = 0.0;
+    for (int i = 0; i < S; ++i) {
+      double v, gr;
+      reg_term(p[i], reg_lambda, reg_b, reg_mode, v, gr);
+      acc += v;
+      g_p[i] += gr;
+    }
+    reg = (float)((double)reg_lambda * acc);
+  }
+  softmax_clamp_bwd(s, S, g_p, ga_out);
   return reg;
 }
 
@@ -615,10 +633,37 @@ __global__ __launch_bounds__(kBlock) void alpha_col_stage2(
   const uint32_t ci = blockIdx.x * (blockDim.x / kWave) + threadIdx.x / kWave;
   const uint32_t lane = threadIdx.x & (kWave - 1);
   if (ci >= g.Ci) return;
+  // every load this wave needs is issued up front, so their latencies overlap
+  float a[kMaxS];
+  if (MODE != 2) {
+    load_row(alpha, ci, S, a);
+    if (reg_dev) {
+      reg_lambda = reg_dev[0];
+      reg_b = reg_dev[1];
+    }
+  }
   double tot[kMaxS];
   for (int i = 0; i < S; ++i)
     tot[i] = lane < nchunk ? part[((size_t)lane * g.Ci + ci) * S + i] : 0.0;
+  // MODE 0: lane i < S evaluates shift i's regulariser term while the partials are in
+  // flight; lane 0 gathers them (same values, same summation order as alpha_chain)
+  float sm[kMaxS], p[kMaxS];
+  double rv = 0.0, rg = 0.0;
+  if (MODE != 2) {
+    soft_targets<kMaxS>(a, S, sm, p);
+    if (MODE == 0 && reg_lambda != 0.0f && lane < (uint32_t)S) {
+      float pl = p[0];
+      for (int i = 1; i < S; ++i)
+        if ((uint32_t)i == lane) pl = p[i];
+      reg_term(pl, reg_lambda, reg_b, 0, rv, rg);
+    }
+  }
   for (int i = 0; i < S; ++i) tot[i] = wave_sum(tot[i]);
+  double rvs[kMaxS], rgs[kMaxS];
+  for (int i = 0; i < S; ++i) {
+    rvs[i] = __shfl(rv, i, kWave);
+    rgs[i] = __shfl(rg, i, kWave);
+  }
   if (lane != 0) return;
   if (MODE == 2) {
     float a[kMaxS];
@@ -629,13 +674,16 @@ __global__ __launch_bounds__(kBlock) void alpha_col_stage2(
     }
     return;
   }
-  if (reg_dev) {
-    reg_lambda = reg_dev[0];
-    reg_b = reg_dev[1];
+  float ga[kMaxS], reg = 0.0f;
+  if (MODE == 0 && reg_lambda != 0.0f) {
+    double acc = 0.0;
+    for (int i = 0; i < S; ++i) {
+      acc += rvs[i];
+      tot[i] += rgs[i];
+    }
+    reg = (float)((double)reg_lambda * acc);
   }
-  float a[kMaxS], ga[kMaxS];
-  load_row(alpha, ci, S, a);
-  const float reg = alpha_chain(a, S, tot, MODE == 0 ? reg_lambda : 0.0f, reg_b, 0, ga);
+  softmax_clamp_bwd(sm, S, tot, ga);
   for (int i = 0; i < S; ++i) out_alpha[(size_t)ci * S + i] = ga[i];
   if (side && MODE == 0) side[ci] = reg;
 }
