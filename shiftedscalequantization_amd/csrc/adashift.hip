@@ -457,9 +457,12 @@ using namespace ssq;
 struct ColTiling {
   uint32_t ncb, ncolblk, R, nchunk, threads;
 };
-constexpr uint32_t kMaxChunks = 64;  // stage 2: one lane per chunk
+constexpr uint32_t kMaxChunks = 256;  // stage 2: lane c sums chunks c, c+64, ... in order
 
-static ColTiling col_tiling(const Geo& g) {
+// max_chunks: kMaxChunks for the reductions (stage 2 has one lane per chunk); the
+// forward has no second stage and takes as many row chunks as keep ~8 workgroups per CU
+// (down to 4 rows = one load batch per thread: its time is load latency, not bandwidth).
+static ColTiling col_tiling(const Geo& g, uint32_t max_chunks = kMaxChunks) {
   ColTiling t;
   t.ncb = g.K >= (uint32_t)kBlock ? 1u : (uint32_t)kBlock / g.K;
   if (t.ncb > g.Ci) t.ncb = g.Ci;
@@ -467,7 +470,7 @@ static ColTiling col_tiling(const Geo& g) {
   t.threads = (t.ncb * g.K + kWave - 1) / kWave * kWave;
   uint32_t want = 2048 / t.ncolblk;  // ~8 workgroups per CU
   if (want < 1) want = 1;
-  if (want > kMaxChunks) want = kMaxChunks;
+  if (want > max_chunks) want = max_chunks;
   if (want > g.Co) want = g.Co;
   t.R = (g.Co + want - 1) / want;
   t.nchunk = (g.Co + t.R - 1) / t.R;
@@ -643,8 +646,19 @@ __global__ __launch_bounds__(kBlock) void alpha_col_stage2(
     }
   }
   double tot[kMaxS];
-  for (int i = 0; i < S; ++i)
-    tot[i] = lane < nchunk ? part[((size_t)lane * g.Ci + ci) * S + i] : 0.0;
+  {
+    double v[kMaxChunks / kWave][kMaxS];
+#pragma unroll
+    for (uint32_t r = 0; r < kMaxChunks / kWave; ++r) {
+      const uint32_t c = lane + r * kWave;
+      for (int i = 0; i < S; ++i) v[r][i] = c < nchunk ? part[((size_t)c * g.Ci + ci) * S + i] : 0.0;
+    }
+    for (int i = 0; i < S; ++i) {
+      tot[i] = v[0][i];
+#pragma unroll
+      for (uint32_t r = 1; r < kMaxChunks / kWave; ++r) tot[i] += v[r][i];
+    }
+  }
   // MODE 0: lane i < S evaluates shift i's regulariser term while the partials are in
   // flight; lane 0 gathers them (same values, same summation order as alpha_chain)
   float sm[kMaxS], p[kMaxS];
@@ -760,7 +774,7 @@ extern "C" int ssq_adashift_fwd(const float* W, const float* alpha, const float*
                        (hipStream_t)stream, W, alpha, beta, delta, zp, sh, g, n, hard_targets,
                        hard_round, (float)qmin, (float)qmax, What, (uint8_t*)codes);
   } else {
-    const ColTiling tl = col_tiling(g);
+    const ColTiling tl = col_tiling(g, (g.Co + 3) / 4);
     SSQ_REQUIRE(tl.threads <= 1024, SSQ_E_ARG, "ssq_adashift_fwd: kernel window K > 1024");
     launch_shift_fwd_col<0>(g, sh, tl, W, alpha, beta, delta, zp, hard_targets, hard_round,
                             (float)qmin, (float)qmax, What, (uint8_t*)codes, (hipStream_t)stream);
@@ -823,7 +837,7 @@ extern "C" int ssq_lhs_fwd(const float* W, const float* alpha, const float* delt
                        (hipStream_t)stream, W, alpha, delta, zp, sh, g, n, hard_targets,
                        (float)qmin, (float)qmax, What);
   } else {
-    const ColTiling tl = col_tiling(g);
+    const ColTiling tl = col_tiling(g, (g.Co + 3) / 4);
     SSQ_REQUIRE(tl.threads <= 1024, SSQ_E_ARG, "ssq_lhs_fwd: kernel window K > 1024");
     launch_shift_fwd_col<1>(g, sh, tl, W, alpha, nullptr, delta, zp, hard_targets, 0,
                             (float)qmin, (float)qmax, What, nullptr, (hipStream_t)stream);
