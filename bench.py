@@ -107,14 +107,21 @@ def pmc_traffic():
         return None
 
 
-def time_events(fn, reps, dev):
-    start, end = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-    start.record()
-    for _ in range(reps):
-        fn()
-    end.record()
-    torch.cuda.synchronize(dev)
-    return start.elapsed_time(end) / reps  # ms
+def time_events(fn, reps, dev, rounds=5):
+    """Average launch time (ms) of fn over `reps` back-to-back launches, measured with HIP
+    events on the current stream; the median of `rounds` such groups (after one untimed
+    warm-up launch) so that a clock ramp or one slow group does not set the number."""
+    fn()
+    times = []
+    for _ in range(rounds):
+        start, end = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        start.record()
+        for _ in range(reps):
+            fn()
+        end.record()
+        torch.cuda.synchronize(dev)
+        times.append(start.elapsed_time(end) / reps)
+    return sorted(times)[len(times) // 2]
 
 
 def cpu_baseline(act_dev, d_a, z_a, seconds):
