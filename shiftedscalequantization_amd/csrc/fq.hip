@@ -35,8 +35,10 @@ struct QParams {
   float d, z, lo, hi;
 };
 
-__device__ __forceinline__ float fq1(float x, const QParams& p, float* qout) {
-  float t = x / p.d;                       // IEEE fp32 divide (x / delta)
+template <bool FAST = false>
+__device__ __forceinline__ float fq1(float x, const QParams& p, float* qout, float r = 0.0f) {
+  // x / delta: IEEE fp32 divide, or its bit-identical reciprocal form (div_fast)
+  float t = FAST ? div_fast(x, p.d, r) : x / p.d;
   float v = __fadd_rn(rintf(t), p.z);      // round_ste fwd == round half-even, + zp
   float q = clampf(v, p.lo, p.hi);         // clamp(x_int, lo, hi)
   *qout = q;
@@ -65,15 +67,15 @@ __device__ __forceinline__ void stream_range(int64_t n4, int64_t chunk, int64_t&
   }
 }
 
-template <bool CODES, bool NTS>
+template <bool CODES, bool NTS, bool FAST = false>
 __device__ __forceinline__ void fq_store4(f32x4 v, const QParams& p, f32x4* __restrict__ y,
-                                          uint32_t* __restrict__ codes, int64_t k) {
+                                          uint32_t* __restrict__ codes, int64_t k, float r = 0.0f) {
   f32x4 o;
   float q0, q1, q2, q3;
-  o.x = fq1(v.x, p, &q0);
-  o.y = fq1(v.y, p, &q1);
-  o.z = fq1(v.z, p, &q2);
-  o.w = fq1(v.w, p, &q3);
+  o.x = fq1<FAST>(v.x, p, &q0, r);
+  o.y = fq1<FAST>(v.y, p, &q1, r);
+  o.z = fq1<FAST>(v.z, p, &q2, r);
+  o.w = fq1<FAST>(v.w, p, &q3, r);
   st4<NTS>(o, &y[k]);
   if (CODES) codes[k] = pack4(q0, q1, q2, q3);
 }
@@ -82,6 +84,9 @@ __device__ __forceinline__ void fq_store4(f32x4 v, const QParams& p, f32x4* __re
 // thread (issued back to back), then computes and stores them.  A software-pipelined form
 // (next step's loads issued before this step's math) measured no faster: the default
 // geometry (1 workgroup/CU, UNROLL 8) already keeps 8 KiB per wave in flight.
+// fastdiv: x/delta in the reciprocal form (div_fast, bit-identical) when every element
+// of the wave's step is in its range -- one wave-uniform branch per step; otherwise (and
+// for an out-of-range delta) the IEEE divide.
 template <bool CODES, int UNROLL, bool NTL, bool NTS>
 __global__ __launch_bounds__(1024) void fq_fwd_pt(const f32x4* __restrict__ x,
                                                   f32x4* __restrict__ y,
@@ -89,20 +94,33 @@ __global__ __launch_bounds__(1024) void fq_fwd_pt(const f32x4* __restrict__ x,
                                                   const float* __restrict__ delta,
                                                   const float* __restrict__ zp, int64_t n4,
                                                   float scale, float lo, float hi,
-                                                  int64_t chunk) {
+                                                  int64_t chunk, int fastdiv) {
   QParams p;
   p.d = __fmul_rn(delta[0], scale);
   p.z = zp[0];
   p.lo = lo;
   p.hi = hi;
+  const float r = fastdiv ? recip_for_div(p.d) : 0.0f;
   int64_t i, end, stride;
   stream_range(n4, chunk, i, end, stride);
   for (; i + (UNROLL - 1) * stride < end; i += UNROLL * stride) {
     f32x4 v[UNROLL];
 #pragma unroll
     for (int u = 0; u < UNROLL; ++u) v[u] = ld4<NTL>(&x[i + u * stride]);
+    // bitwise (not short-circuit) so the range test stays branch-free
+    unsigned ok = r != 0.0f;
 #pragma unroll
-    for (int u = 0; u < UNROLL; ++u) fq_store4<CODES, NTS>(v[u], p, y, codes, i + u * stride);
+    for (int u = 0; u < UNROLL; ++u)
+      ok &= (unsigned)div_fast_ok(v[u].x) & (unsigned)div_fast_ok(v[u].y) &
+            (unsigned)div_fast_ok(v[u].z) & (unsigned)div_fast_ok(v[u].w);
+    if (__all(ok)) {
+#pragma unroll
+      for (int u = 0; u < UNROLL; ++u)
+        fq_store4<CODES, NTS, true>(v[u], p, y, codes, i + u * stride, r);
+    } else {
+#pragma unroll
+      for (int u = 0; u < UNROLL; ++u) fq_store4<CODES, NTS>(v[u], p, y, codes, i + u * stride);
+    }
   }
   for (; i < end; i += stride) fq_store4<CODES, false>(x[i], p, y, codes, i);
 }
@@ -375,10 +393,11 @@ __global__ __launch_bounds__(1024) void copy_kernel(const f32x4* __restrict__ s,
 //   bits 8-23 grid size in workgroups (0 -> 2048)
 //   bit  24   chunked (workgroup-contiguous) instead of grid-stride
 //   bits 25-26 workgroup size: 0 -> 256, 1 -> 512, 2 -> 1024
+//   bit  27   1: IEEE divide only (no reciprocal fast path)
 static int g_variant = 1 | (3 << 4) | (256 << 8);  // NT load+store, unroll 8, 1 workgroup per CU (tools/ab_fq.py)
 
 struct Variant {
-  bool ntl, nts, chunked;
+  bool ntl, nts, chunked, ieee;
   int unroll, grid, block;
 };
 static Variant decode_variant(int v) {
@@ -393,6 +412,7 @@ static Variant decode_variant(int v) {
   r.chunked = (v >> 24) & 1;
   const int b = (v >> 25) & 3;
   r.block = b == 1 ? 512 : b == 2 ? 1024 : 256;
+  r.ieee = (v >> 27) & 1;
   return r;
 }
 
@@ -432,18 +452,18 @@ template <int U, bool NTL, bool NTS>
 struct FqPtCodes {
   static void go(dim3 g, dim3 b, hipStream_t s, const f32x4* x, f32x4* y, uint32_t* c,
                  const float* d, const float* z, int64_t n4, float sc, float lo, float hi,
-                 int64_t chunk) {
+                 int64_t chunk, int fastdiv) {
     hipLaunchKernelGGL((fq_fwd_pt<true, U, NTL, NTS>), g, b, 0, s, x, y, c, d, z, n4, sc, lo, hi,
-                       chunk);
+                       chunk, fastdiv);
   }
 };
 template <int U, bool NTL, bool NTS>
 struct FqPt {
   static void go(dim3 g, dim3 b, hipStream_t s, const f32x4* x, f32x4* y, uint32_t* c,
                  const float* d, const float* z, int64_t n4, float sc, float lo, float hi,
-                 int64_t chunk) {
+                 int64_t chunk, int fastdiv) {
     hipLaunchKernelGGL((fq_fwd_pt<false, U, NTL, NTS>), g, b, 0, s, x, y, c, d, z, n4, sc, lo, hi,
-                       chunk);
+                       chunk, fastdiv);
   }
 };
 template <int U, bool NTL, bool NTS>
@@ -491,9 +511,10 @@ extern "C" int ssq_fq_fwd(const float* x, float* y, void* codes, const float* de
       uint32_t* cv = (uint32_t*)codes;
       if (codes)
         launch_stream<FqPtCodes>(v, grid, block, s, xv, yv, cv, delta, zp, n4, scale, lo, hi,
-                                 chunk);
+                                 chunk, v.ieee ? 0 : 1);
       else
-        launch_stream<FqPt>(v, grid, block, s, xv, yv, cv, delta, zp, n4, scale, lo, hi, chunk);
+        launch_stream<FqPt>(v, grid, block, s, xv, yv, cv, delta, zp, n4, scale, lo, hi, chunk,
+                            v.ieee ? 0 : 1);
     } else if (n < (1ll << 31) && (n + kTile - 1) / kTile < (1ll << 31)) {
       // per-channel: the LDS-staged tile kernel with one segment (no 64-bit divides)
       SegTable tab;

@@ -69,6 +69,30 @@ __device__ __forceinline__ uint32_t fdiv(uint32_t n, FastDiv f) {
 }
 
 // ---------------------------------------------------------------- device math
+// Division by a loop-invariant d without the per-element divide sequence.  With
+// r = RN(1/d) (computed once), q0 = x*r is within 1.5 ulp of x/d, one fma residual /
+// correction makes it faithful, and a second one returns RN(x/d) -- Markstein's theorem
+// (r within 1/2 ulp of 1/d, q1 faithful => RN(q1 + RN(x - d*q1)*r) = RN(x/d)), the same
+// correction the compiler's IEEE divide ends with.  The premise needs every residual
+// normal: |d| and nonzero |x| in [2^-60, 2^60].  recip_for_div returns 0 for a d outside
+// that range and div_fast_ok tests x; callers take the IEEE divide when either fails.
+// x = +-0 returns x*r, the correctly signed zero.  Validated against the IEEE divide on
+// 3.4e9 random pairs (tools/divcheck.c) in addition to the boundary tests.
+__device__ __forceinline__ float recip_for_div(float d) {
+  const float a = fabsf(d);
+  return (a >= 0x1p-60f && a <= 0x1p60f) ? 1.0f / d : 0.0f;
+}
+__device__ __forceinline__ bool div_fast_ok(float x) {
+  const uint32_t b = __float_as_uint(x) & 0x7fffffffu;
+  return b == 0u || (b - 0x21800000u) <= (0x5d800000u - 0x21800000u);
+}
+__device__ __forceinline__ float div_fast(float x, float d, float r) {
+  const float q0 = __fmul_rn(x, r);
+  const float q1 = __fmaf_rn(__fmaf_rn(-q0, d, x), r, q0);
+  const float q2 = __fmaf_rn(__fmaf_rn(-q1, d, x), r, q1);
+  return x == 0.0f ? q0 : q2;
+}
+
 __device__ __forceinline__ float clampf(float v, float lo, float hi) {
   // torch.clamp semantics on finite values: min(max(v, lo), hi)
   return fminf(fmaxf(v, lo), hi);

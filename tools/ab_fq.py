@@ -25,14 +25,9 @@ def var(grid, block=256, unroll=4, chunked=0, pol=1, pipe=0):
 
 
 geoms = {}
-for grid in (256, 512):
-    for block in (256, 512):
-        for unroll in (2, 4, 8):
-            for pipe in (0, 1):
-                if block * unroll > 4096:
-                    continue
-                geoms[f"g{grid}b{block}u{unroll}p{pipe}"] = var(grid, block, unroll, 0, pipe=pipe)
-geoms["g256b256u4p1_plain"] = var(256, 256, 4, 0, pol=0, pipe=1)
+for grid, block, unroll in ((256, 256, 8), (256, 256, 4), (512, 256, 4), (256, 512, 4)):
+    for ieee in (0, 1):
+        geoms[f"g{grid}b{block}u{unroll}{'_ieee' if ieee else '_rcp'}"] = var(grid, block, unroll) | (ieee << 27)
 
 
 def t(fn, reps=20):
