@@ -393,11 +393,12 @@ __global__ __launch_bounds__(1024) void copy_kernel(const f32x4* __restrict__ s,
 //   bits 8-23 grid size in workgroups (0 -> 2048)
 //   bit  24   chunked (workgroup-contiguous) instead of grid-stride
 //   bits 25-26 workgroup size: 0 -> 256, 1 -> 512, 2 -> 1024
-//   bit  27   1: IEEE divide only (no reciprocal fast path)
+//   bit  27   1: reciprocal-form division fast path (div_fast); 0: IEEE divide.  A/B on
+//             MI355X boxes was mixed (+6 % at unroll 4, -7 % at unroll 8): IEEE stays default
 static int g_variant = 1 | (3 << 4) | (256 << 8);  // NT load+store, unroll 8, 1 workgroup per CU (tools/ab_fq.py)
 
 struct Variant {
-  bool ntl, nts, chunked, ieee;
+  bool ntl, nts, chunked, rcp;
   int unroll, grid, block;
 };
 static Variant decode_variant(int v) {
@@ -412,7 +413,7 @@ static Variant decode_variant(int v) {
   r.chunked = (v >> 24) & 1;
   const int b = (v >> 25) & 3;
   r.block = b == 1 ? 512 : b == 2 ? 1024 : 256;
-  r.ieee = (v >> 27) & 1;
+  r.rcp = (v >> 27) & 1;
   return r;
 }
 
@@ -511,10 +512,10 @@ extern "C" int ssq_fq_fwd(const float* x, float* y, void* codes, const float* de
       uint32_t* cv = (uint32_t*)codes;
       if (codes)
         launch_stream<FqPtCodes>(v, grid, block, s, xv, yv, cv, delta, zp, n4, scale, lo, hi,
-                                 chunk, v.ieee ? 0 : 1);
+                                 chunk, v.rcp ? 1 : 0);
       else
         launch_stream<FqPt>(v, grid, block, s, xv, yv, cv, delta, zp, n4, scale, lo, hi, chunk,
-                            v.ieee ? 0 : 1);
+                            v.rcp ? 1 : 0);
     } else if (n < (1ll << 31) && (n + kTile - 1) / kTile < (1ll << 31)) {
       // per-channel: the LDS-staged tile kernel with one segment (no 64-bit divides)
       SegTable tab;

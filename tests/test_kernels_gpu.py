@@ -144,16 +144,28 @@ def _boundary_inputs(d, n_per=4096, seed=5):
     return x[: len(x) // 4 * 4]
 
 
+@pytest.mark.parametrize("rcp", [0, 1])
 @pytest.mark.parametrize("d", [0.05, 0.3, 1e-8, 7.0e-3, 2.0 ** -70, 3.0e20])
-def test_fq_rounding_boundaries(K, d):
+def test_fq_rounding_boundaries(K, d, rcp):
     """Quotients on / one ulp beside the rint and floor boundaries, zeros, subnormals,
-    huge values: codes and dequantized values bit-exact against the oracle."""
+    huge values: codes and dequantized values bit-exact against the oracle, with the IEEE
+    divide and with the reciprocal-form fast path (variant bit 27)."""
     x = torch.from_numpy(_boundary_inputs(d))
     dd, z = torch.tensor(np.float32(d)), torch.tensor(2.0)
-    a, ca = K.fake_quant_fwd(x.cuda(), dd.cuda(), z.cuda(), 8, codes=True)
+    old = K.set_variant(1 | (3 << 4) | (256 << 8) | (rcp << 27))
+    try:
+        a, ca = K.fake_quant_fwd(x.cuda(), dd.cuda(), z.cuda(), 8, codes=True)
+        # a large ReLU-like tensor: whole waves take the fast path when rcp is on
+        big = torch.relu(torch.randn(1 << 22, generator=torch.Generator().manual_seed(9))) * float(d)
+        b, cb = K.fake_quant_fwd(big.cuda(), dd.cuda(), z.cuda(), 8, codes=True)
+    finally:
+        K.set_variant(old)
     ry, rq = R.fake_quant(x.numpy(), dd.numpy(), z.numpy(), 8)
     np.testing.assert_array_equal(host(a).view(np.int32), ry.view(np.int32))
     np.testing.assert_array_equal(ca.cpu().numpy(), rq.astype(np.uint8))
+    ry, rq = R.fake_quant(big.numpy(), dd.numpy(), z.numpy(), 8)
+    np.testing.assert_array_equal(host(b).view(np.int32), ry.view(np.int32))
+    np.testing.assert_array_equal(cb.cpu().numpy(), rq.astype(np.uint8))
 
 
 def test_fq_per_channel_unaligned(K):

@@ -26,8 +26,8 @@ def var(grid, block=256, unroll=4, chunked=0, pol=1, pipe=0):
 
 geoms = {}
 for grid, block, unroll in ((256, 256, 8), (256, 256, 4), (512, 256, 4), (256, 512, 4)):
-    for ieee in (0, 1):
-        geoms[f"g{grid}b{block}u{unroll}{'_ieee' if ieee else '_rcp'}"] = var(grid, block, unroll) | (ieee << 27)
+    for rcp in (0, 1):
+        geoms[f"g{grid}b{block}u{unroll}{'_rcp' if rcp else '_ieee'}"] = var(grid, block, unroll) | (rcp << 27)
 
 
 def t(fn, reps=20):
