@@ -49,17 +49,25 @@ def parse():
     p.add_argument("--no-recon", action="store_true")
     p.add_argument("--recon-iters", type=int, default=200)
     p.add_argument("--variant", type=int, default=-1, help="streaming cache policy A/B")
+    p.add_argument("--dist-backend", default="nccl",
+                   help="nccl (= RCCL over xGMI, the default) or gloo (rehearsing N > 1 ranks "
+                        "on fewer GPUs: ranks share devices round-robin)")
     return p.parse_args()
 
 
-def setup():
+def setup(backend="nccl"):
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
-    torch.cuda.set_device(local)
+    ndev = torch.cuda.device_count()
+    dev = torch.device("cuda", local % max(ndev, 1))
+    torch.cuda.set_device(dev)
     if world > 1:
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
-    return rank, world, torch.device("cuda", local)
+        if backend == "nccl":
+            dist.init_process_group("nccl", device_id=dev)
+        else:
+            dist.init_process_group(backend)
+    return rank, world, dev
 
 
 def barrier(world):
@@ -148,7 +156,7 @@ def cpu_baseline(act_dev, d_a, z_a, seconds):
 
 def main():
     args = parse()
-    rank, world, dev = setup()
+    rank, world, dev = setup(args.dist_backend)
     if args.variant >= 0:
         K.set_variant(args.variant)
     act, d_a, z_a, weights, dws, zws, bits = make_workload(dev, rank, args.n_cali)
