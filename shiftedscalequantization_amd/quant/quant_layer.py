@@ -173,6 +173,16 @@ class QuantModule(nn.Module):
         t = t.detach()
         return t.cpu().clone() if self.cache_to_host else t.clone()
 
+    def _apply(self, fn, *args, **kwargs):
+        """.to() / .cuda() also move the FP copies org_weight / org_bias (plain tensor
+        attributes, as in the reference, which leaves them behind on the old device)."""
+        out = super()._apply(fn, *args, **kwargs)
+        if isinstance(self.org_weight, torch.Tensor):
+            self.org_weight = fn(self.org_weight)
+        if isinstance(self.org_bias, torch.Tensor):
+            self.org_bias = fn(self.org_bias)
+        return out
+
     def _affine_is_identity(self):
         """True while gamma^z / phi^z are still their untouched initial (1, 0) tensors
         and nothing needs their gradient: then out*1+0 == out and the two passes (plus
