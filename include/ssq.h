@@ -157,15 +157,18 @@ int ssq_lhs_bwd(const float* gWhat, const float* W, const float* alpha, const fl
 
 /* 'adaround' mode (channelQuant.py:65-78) and AdaRoundQuantizer 'learned_hard_sigmoid'
  * (adaptive_rounding.py:38-67):  Q = clamp(floor(W/d) + (hard ? [beta>=0] : h(beta)) + zp)
- * What = (Q - zp)*d, d = delta*scale.  Backward gives gbeta (W-shaped, OVERWRITTEN).  */
+ * What = (Q - zp)*d, d = delta*scale.  Backward gives gbeta (W-shaped, OVERWRITTEN); with
+ * reg_lambda != 0 (or reg_dev != NULL: (lambda, b) read from that DEVICE pair, the
+ * graph-capturable form) the gradient of the rounding regulariser
+ * lambda*sum(1-|2h(beta)-1|^b) (block_recon.py:171-174) is added in the same pass.      */
 int ssq_adaround_fwd(const float* W, const float* beta, const float* delta, int delta_per_ci,
                      const float* zp, float scale, int64_t Co, int64_t Ci, int64_t K,
                      int hard_round, int qmin, int qmax, float* What, void* codes_or_null,
                      ssq_stream_t stream);
 int ssq_adaround_bwd(const float* gWhat, const float* W, const float* beta,
                      const float* delta, int delta_per_ci, const float* zp, float scale,
-                     int64_t Co, int64_t Ci, int64_t K, int qmin, int qmax, float* gbeta,
-                     ssq_stream_t stream);
+                     int64_t Co, int64_t Ci, int64_t K, int qmin, int qmax, float reg_lambda,
+                     float reg_b, const float* reg_dev, float* gbeta, ssq_stream_t stream);
 
 /* Rounding regulariser lambda*sum(1-|2h(v)-1|^b) over h = rect_sigmoid(v)
  * (layer_recon_fused_shiftedScale.py:278-279, block_recon.py:171-174,

@@ -252,10 +252,27 @@ __global__ __launch_bounds__(kBlock) void adaround_fwd_kernel(
   }
 }
 
+// d/dv of the rounding regulariser lambda*(1-|2h(v)-1|^b) (round_reg_kernel's gradient)
+__device__ __forceinline__ float round_reg_grad(float v, float lambda, float b) {
+  if (lambda == 0.0f || b == 0.0f) return 0.0f;
+  const float h = rect_sigmoid(v);
+  const float r = __fmul_rn(fabsf(__fsub_rn(h, 0.5f)), 2.0f);
+  const float sg = h > 0.5f ? 1.0f : (h < 0.5f ? -1.0f : 0.0f);
+  const float gh = -lambda * b * powf(r, b - 1.0f) * 2.0f * sg;
+  return rect_sigmoid_grad(v, gh);
+}
+
+// reg_dev != null: the rounding regulariser's gradient (lambda, b = reg_dev[0..1]) is added
+// (BRECQ's round loss, block_recon.py:171-174, folded into this backward).
 __global__ __launch_bounds__(kBlock) void adaround_bwd_kernel(
     const float* __restrict__ gWhat, const float* __restrict__ W, const float* __restrict__ beta,
     const float* __restrict__ delta, int per_ci, const float* __restrict__ zp, float scale, Geo g,
-    uint32_t n, float lo, float hi, float* __restrict__ gbeta) {
+    uint32_t n, float lo, float hi, float reg_lambda, float reg_b,
+    const float* __restrict__ reg_dev, float* __restrict__ gbeta) {
+  if (reg_dev) {
+    reg_lambda = reg_dev[0];
+    reg_b = reg_dev[1];
+  }
   const uint32_t stride = gridDim.x * blockDim.x;
   for (uint32_t e = blockIdx.x * blockDim.x + threadIdx.x; e < n; e += stride) {
     uint32_t co, ci;
@@ -264,7 +281,8 @@ __global__ __launch_bounds__(kBlock) void adaround_bwd_kernel(
     const float b = beta[e];
     const float u = __fadd_rn(__fadd_rn(floorf(W[e] / d), rect_sigmoid(b)), z);
     const float gi = (u >= lo && u <= hi) ? __fmul_rn(gWhat[e], d) : 0.0f;
-    gbeta[e] = rect_sigmoid_grad(b, gi);
+    const float ga = rect_sigmoid_grad(b, gi);
+    gbeta[e] = reg_lambda != 0.0f ? __fadd_rn(ga, round_reg_grad(b, reg_lambda, reg_b)) : ga;
   }
 }
 
@@ -882,13 +900,14 @@ extern "C" int ssq_adaround_fwd(const float* W, const float* beta, const float* 
 extern "C" int ssq_adaround_bwd(const float* gWhat, const float* W, const float* beta,
                                 const float* delta, int delta_per_ci, const float* zp, float scale,
                                 int64_t Co, int64_t Ci, int64_t K, int qmin, int qmax,
-                                float* gbeta, ssq_stream_t stream) {
+                                float reg_lambda, float reg_b, const float* reg_dev, float* gbeta,
+                                ssq_stream_t stream) {
   SSQ_GEO(Co, Ci, K, 0, g);
   SSQ_REQUIRE(gWhat && W && beta && delta && zp && gbeta, SSQ_E_ARG, "ssq_adaround_bwd: null");
   const uint32_t n = g.Co * g.CiK;
   hipLaunchKernelGGL(adaround_bwd_kernel, dim3(grid_for(n, kBlock)), dim3(kBlock), 0,
                      (hipStream_t)stream, gWhat, W, beta, delta, delta_per_ci, zp, scale, g, n,
-                     (float)qmin, (float)qmax, gbeta);
+                     (float)qmin, (float)qmax, reg_lambda, reg_b, reg_dev, gbeta);
   return check_launch("ssq_adaround_bwd");
 }
 

@@ -332,7 +332,7 @@ class AdaRoundFn(torch.autograd.Function):
     (channelQuant.py:65-78, adaptive_rounding.py:55-67)."""
 
     @staticmethod
-    def forward(ctx, beta, w, delta, zp, n_bits, sym, hard_r, scale):
+    def forward(ctx, beta, w, delta, zp, n_bits, sym, hard_r, scale, reg=None):
         w, wp = fptr(w.detach())
         b, bp = fptr(beta.detach())
         d, dp = fptr(delta.detach())
@@ -344,26 +344,29 @@ class AdaRoundFn(torch.autograd.Function):
         call("ssq_adaround_fwd", wp, bp, dp, per_ci, zpp, float(scale), Co, Ci, K, int(hard_r), lo,
              hi, _vp(out), None, stream_of(w))
         ctx.save_for_backward(b, w, d, z)
-        ctx.cfg = (n_bits, sym, hard_r, scale, per_ci)
+        ctx.cfg = (n_bits, sym, hard_r, scale, per_ci, reg)
         return out
 
     @staticmethod
     def backward(ctx, g):
         b, w, d, z = ctx.saved_tensors
-        n_bits, sym, hard_r, scale, per_ci = ctx.cfg
+        n_bits, sym, hard_r, scale, per_ci, reg = ctx.cfg
         if hard_r or not ctx.needs_input_grad[0]:
-            return (None,) * 8
+            return (None,) * 9
         g = g.contiguous()
         Co, Ci, K, _ = geometry(w)
         lo, hi = qrange(n_bits, sym)
         gb = torch.empty_like(w)
+        lam, bb, reg_dev = (0.0, 0.0, None) if reg is None else reg
         call("ssq_adaround_bwd", _vp(g), _vp(w), _vp(b), _vp(d), per_ci, _vp(z), float(scale), Co,
-             Ci, K, lo, hi, _vp(gb), stream_of(w))
-        return (gb, None, None, None, None, None, None, None)
+             Ci, K, lo, hi, float(lam), float(bb), _vp(reg_dev), _vp(gb), stream_of(w))
+        return (gb, None, None, None, None, None, None, None, None)
 
 
-def adaround(beta, w, delta, zp, n_bits, sym, hard_r, scale=1.0):
-    return AdaRoundFn.apply(beta, w, delta, zp, n_bits, sym, bool(hard_r), float(scale))
+def adaround(beta, w, delta, zp, n_bits, sym, hard_r, scale=1.0, reg=None):
+    """reg = (lambda, b, reg_dev) folds the rounding regulariser's gradient into the
+    backward ((lambda, b) from the device pair reg_dev when given)."""
+    return AdaRoundFn.apply(beta, w, delta, zp, n_bits, sym, bool(hard_r), float(scale), reg)
 
 
 # ------------------------------------------------------------------ K12 regularisers

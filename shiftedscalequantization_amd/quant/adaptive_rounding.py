@@ -24,6 +24,7 @@ class AdaRoundQuantizer(nn.Module):
         self.soft_targets = False
         self.gamma, self.zeta = -0.1, 1.1
         self.beta = 2 / 3
+        self._fused_reg = None      # (lambda, b, reg_dev): the BRECQ loop's folded round loss
         self.init_alpha(x=weight_tensor.clone())
 
     def forward(self, x):
@@ -42,7 +43,7 @@ class AdaRoundQuantizer(nn.Module):
         elif self.round_mode == 'learned_hard_sigmoid':
             # adaptive_rounding.py:64 clamps to [0, n_levels-1] regardless of sym
             return K.adaround(self.alpha, x, self.delta, self.zero_point, self.n_bits, False,
-                              not self.soft_targets)
+                              not self.soft_targets, reg=self._fused_reg)
         else:
             raise ValueError('Wrong rounding mode')
 

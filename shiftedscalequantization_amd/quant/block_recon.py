@@ -33,9 +33,12 @@ def block_reconstruction(model: QuantModel, block: BaseQuantBlock, cali_data: to
                         block_level=True)
 
 
+GRAPH_WARMUP = 3     # eager iterations before the iteration body is captured
+
+
 def _reconstruct(model, block, qmodules, cali_data, batch_size, iters, weight, opt_mode, asym,
                  include_act_func, b_range, warmup, act_quant, lr, p, multi_gpu, eval, dp_average,
-                 block_level):
+                 block_level, graph=True):
     if eval:
         iters = 0
     model.set_quant_state(False, False)
@@ -51,17 +54,12 @@ def _reconstruct(model, block, qmodules, cali_data, batch_size, iters, weight, o
                                                    weight_tensor=m.org_weight.data)
             m.weight_quantizer.soft_targets = True
         opt_params = [m.weight_quantizer.alpha for m in qmodules]
-        optimizer = torch.optim.Adam(opt_params)
-        scheduler = None
     else:
         if block_level:   # block_recon.py:64-71
             opt_params = [block.act_quantizer.delta] + [
                 m.act_quantizer.delta for m in qmodules if m.act_quantizer.delta is not None]
         else:             # layer_recon.py:61
             opt_params = [block.act_quantizer.delta]
-        optimizer = torch.optim.Adam(opt_params, lr=lr)
-        scheduler = torch.optim.lr_scheduler.CosineAnnealingLR(optimizer, T_max=max(iters, 1),
-                                                               eta_min=0.)
 
     loss_func = LossFunction(block, round_loss='none' if act_quant else 'relaxation', weight=weight,
                              max_count=iters, rec_loss=opt_mode, b_range=b_range, decay_start=0,
@@ -74,19 +72,12 @@ def _reconstruct(model, block, qmodules, cali_data, batch_size, iters, weight, o
             if opt_mode != 'mse' else None
         feeder = BatchFeeder(cached_inps, cached_outs, batch_size, device)
         bucket = GradBucket(opt_params, average=dp_average) if (multi_gpu or world() > 1) else None
-        for i in range(iters):
-            perm = feeder.draw()
-            cur_inp, cur_out = feeder.next(perm)
-            cur_grad = cached_grads[perm.to(cached_grads.device)] if cached_grads is not None else None
-            optimizer.zero_grad()
-            out_quant = block(cur_inp)
-            err = loss_func(out_quant, cur_out, cur_grad)
-            err.backward()
-            if bucket is not None:
-                bucket.allreduce_()
-            optimizer.step()
-            if scheduler:
-                scheduler.step()
+        if opt_mode == 'mse' and opt_params[0].is_cuda:
+            _fast_loop(block, qmodules, opt_params, loss_func, feeder, bucket, iters, act_quant, lr,
+                       p, graph and world() == 1 and not multi_gpu)
+        else:
+            _eager_loop(opt_params, loss_func, feeder, bucket, cached_grads, block, iters, act_quant,
+                        lr)
     for m in qmodules:
         if isinstance(m.weight_quantizer, AdaRoundQuantizer):
             m.weight_quantizer.soft_targets = False
@@ -94,9 +85,115 @@ def _reconstruct(model, block, qmodules, cali_data, batch_size, iters, weight, o
         block.activation_function = org_act_func
 
 
+def _eager_loop(opt_params, loss_func, feeder, bucket, cached_grads, block, iters, act_quant, lr):
+    """The reference's loop (block_recon.py:90-105) as written, for the Fisher losses and
+    host tensors."""
+    if not act_quant:
+        optimizer, scheduler = torch.optim.Adam(opt_params), None
+    else:
+        optimizer = torch.optim.Adam(opt_params, lr=lr)
+        scheduler = torch.optim.lr_scheduler.CosineAnnealingLR(optimizer, T_max=max(iters, 1),
+                                                               eta_min=0.)
+    for i in range(iters):
+        perm = feeder.draw()
+        cur_inp, cur_out = feeder.next(perm)
+        cur_grad = cached_grads[perm.to(cached_grads.device)] if cached_grads is not None else None
+        optimizer.zero_grad()
+        out_quant = block(cur_inp)
+        err = loss_func(out_quant, cur_out, cur_grad)
+        err.backward()
+        if bucket is not None:
+            bucket.allreduce_()
+        optimizer.step()
+        if scheduler:
+            scheduler.step()
+
+
+def _fast_loop(block, qmodules, opt_params, loss_func, feeder, bucket, iters, act_quant, lr, p,
+               graph):
+    """Same iteration, device only: one H2D copy (batch indices + this iteration's
+    (lambda, b)), gather, forward, one fused lp_loss value+gradient pass (at the input of a
+    final fused-epilogue ReLU), backward with the round loss's gradient folded into the
+    AdaRound backward, fused Adam.  After GRAPH_WARMUP eager iterations the body is
+    replayed from a HIP graph (single GPU).  The cosine LR schedule is stepped by the
+    reference's own torch scheduler on a shadow optimizer and copied into Adam's device lr."""
+    device = opt_params[0].device
+    use_graph = bool(graph and iters > GRAPH_WARMUP + 1)
+    kw = dict(fused=True, capturable=use_graph)
+    if act_quant:
+        lr_dev = torch.tensor(float(lr), dtype=torch.float32, device=device)
+        optimizer = torch.optim.Adam(opt_params, lr=lr_dev if use_graph else lr, **kw)
+        shadow_p = torch.zeros(1, requires_grad=True)
+        shadow = torch.optim.Adam([shadow_p], lr=lr)
+        scheduler = torch.optim.lr_scheduler.CosineAnnealingLR(shadow, T_max=max(iters, 1), eta_min=0.)
+    else:
+        optimizer, scheduler = torch.optim.Adam(opt_params, **kw), None
+    regp = feeder.extra
+    ada = [m.weight_quantizer for m in qmodules if isinstance(m.weight_quantizer, AdaRoundQuantizer)]
+    if not act_quant:
+        for q in ada:
+            q._fused_reg = (0.0, 0.0, regp)
+    last = {}
+
+    def body():
+        cur_inp, cur_out = feeder.gather()
+        out = block(cur_inp)
+        relu_in = getattr(out, '_ssq_relu_inputs', None)
+        if relu_in:
+            rec, g = K.lp_loss_and_grad(out, cur_out, p, relu_mask=True)
+            torch.autograd.backward(list(relu_in), [g] * len(relu_in))
+        else:
+            rec, g = K.lp_loss_and_grad(out, cur_out, p)
+            out.backward(g)
+        if bucket is not None:
+            bucket.allreduce_()
+        optimizer.step()
+        last['rec'] = rec
+
+    graph_obj, ws_cache = None, {}
+    try:
+        for i in range(iters):
+            b, lam, active = loss_func.schedule()
+            feeder.stage(feeder.draw(), extra=(lam, float(b)))
+            # the round-loss value (reporting only) from alpha before this step, as the
+            # reference's forward computes it
+            rnd = loss_func.round_value(b) if (active and loss_func.wants_value()) else 0.0
+            if use_graph and i == GRAPH_WARMUP:
+                optimizer.zero_grad(set_to_none=True)
+                graph_obj = torch.cuda.CUDAGraph()
+                with K.A.workspace_scope(ws_cache):
+                    with torch.cuda.graph(graph_obj):
+                        body()
+            if graph_obj is not None:
+                graph_obj.replay()
+            else:
+                optimizer.zero_grad()
+                body()
+            rec = last['rec'][0]
+            loss_func.record(rec, rnd, b)
+            if scheduler is not None:
+                shadow.step()
+                scheduler.step()
+                new_lr = shadow.param_groups[0]['lr']
+                if use_graph:
+                    lr_dev.fill_(new_lr)
+                else:
+                    for grp in optimizer.param_groups:
+                        grp['lr'] = new_lr
+    finally:
+        for q in ada:
+            q._fused_reg = None
+        if graph_obj is not None:
+            torch.cuda.current_stream().synchronize()
+            for p_ in opt_params:       # detach the grads from the graph's private pool
+                p_.grad = None if p_.grad is None else p_.grad.clone()
+            del graph_obj
+
+
 class LossFunction:
     """block_recon.py:119-182 (count incremented BEFORE the schedule, unlike the fused
-    loss).  The report line every 500 counts is the only host sync."""
+    loss).  The report line every 500 counts is the only host sync.  schedule() /
+    round_value() / record() are the same steps split for the device-only loop."""
 
     def __init__(self, block, round_loss: str = 'relaxation', weight: float = 1., rec_loss: str = 'mse',
                  max_count: int = 2000, b_range: tuple = (10, 2), decay_start: float = 0.0,
@@ -112,14 +209,45 @@ class LossFunction:
         self.count = 0
         self._qmodules = quant_modules
         self.last_total = None
+        self.track_values = False   # True: round_value() every iteration (tests)
 
     def _modules(self):
         if self._qmodules is not None:
             return self._qmodules
         return [m for m in self.block.modules() if isinstance(m, QuantModule)]
 
-    def __call__(self, pred, tgt, grad=None):
+    def schedule(self):
+        """count += 1; (b, lambda_eff, round loss active) for this iteration."""
         self.count += 1
+        b = self.temp_decay(self.count)
+        if self.count < self.loss_start or self.round_loss == 'none':
+            return 0, 0.0, False
+        if self.round_loss != 'relaxation':
+            raise NotImplementedError
+        return b, float(self.weight), True
+
+    def wants_value(self):
+        return self.track_values or self.count % 500 == 0
+
+    def round_value(self, b):
+        total = 0
+        for m in self._modules():
+            total = total + K.round_reg_value(m.weight_quantizer.alpha, self.weight, b)
+        return total
+
+    def record(self, rec_loss, round_loss, b):
+        # no tensor op when there is no round term (keeps the device loop launch-free)
+        total_loss = rec_loss if isinstance(round_loss, (int, float)) and round_loss == 0 \
+            else rec_loss + round_loss
+        self.last_total = LazyValue(total_loss.detach() if isinstance(total_loss, torch.Tensor)
+                                    else total_loss)
+        if self.count % 500 == 0:
+            print('Total loss:\t{:.3f} (rec:{:.3f}, round:{:.3f})\tb={:.2f}\tcount={}'.format(
+                float(total_loss), float(rec_loss), float(round_loss), b, self.count))
+        return total_loss
+
+    def __call__(self, pred, tgt, grad=None):
+        b, _, active = self.schedule()
         if self.rec_loss == 'mse':
             rec_loss = K.lp_loss(pred, tgt, self.p)
         elif self.rec_loss == 'fisher_diag':
@@ -131,21 +259,11 @@ class LossFunction:
             rec_loss = (batch_dotprod * a * g).mean() / 100
         else:
             raise ValueError('Not supported reconstruction loss function: {}'.format(self.rec_loss))
-        b = self.temp_decay(self.count)
-        if self.count < self.loss_start or self.round_loss == 'none':
-            b = round_loss = 0
-        elif self.round_loss == 'relaxation':
-            round_loss = 0
+        round_loss = 0
+        if active:
             for m in self._modules():
                 round_loss = round_loss + K.round_reg(m.weight_quantizer.alpha, self.weight, b)
-        else:
-            raise NotImplementedError
-        total_loss = rec_loss + round_loss
-        self.last_total = LazyValue(total_loss.detach())
-        if self.count % 500 == 0:
-            print('Total loss:\t{:.3f} (rec:{:.3f}, round:{:.3f})\tb={:.2f}\tcount={}'.format(
-                float(total_loss), float(rec_loss), float(round_loss), b, self.count))
-        return total_loss
+        return self.record(rec_loss, round_loss, b)
 
 
 class LinearTempDecay:
