@@ -221,6 +221,18 @@ int ssq_bias_act(const float* y, const float* bias, const float* res, float* out
                  int64_t hw, int64_t C, int relu, ssq_stream_t stream);
 int ssq_relu_bwd(const float* g, const float* out, float* gin, int64_t n, ssq_stream_t stream);
 
+/* ---------------------------------------------------------------- Adam
+ * torch.optim.Adam's single-tensor step (the reference's optimizer; block_recon.py:57-60,
+ * layer_recon_fused_shiftedScale.py:57/73) over nseg parameter tensors in one launch:
+ *   m = m + (1-b1)*(g-m);  v = v*b2 + ((1-b2)*g)*g;  p = p + (nss*m)/(sqrt(v)/bc2s + eps)
+ * with nss = -lr/(1-b1^t), bc2s = sqrt(1-b2^t) taken from the DEVICE pair `hyper` when it
+ * is not NULL (graph-capturable), else from the scalar arguments.  Arrays are HOST arrays
+ * of length nseg holding device pointers.                                               */
+int ssq_adam(int nseg, float* const* p, const float* const* g, float* const* m,
+             float* const* v, const int64_t* n, float one_minus_beta1, float beta2,
+             float one_minus_beta2, float eps, const float* hyper, float neg_step_size,
+             float bias_correction2_sqrt, ssq_stream_t stream);
+
 /* ---------------------------------------------------------------- bandwidth probe
  * float4 device copy, used by bench.py to report the measured stream bandwidth.      */
 int ssq_stream_copy(const float* src, float* dst, int64_t n, ssq_stream_t stream);

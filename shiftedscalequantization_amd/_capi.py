@@ -56,6 +56,7 @@ SIGNATURES = {
     "ssq_gather_rows2": (_i, [_p, _p, _i64, _p, _p, _i64, _p, _i64, _p]),
     "ssq_bias_act": (_i, [_p, _p, _p, _p, _i64, _i64, _i64, _i, _p]),
     "ssq_relu_bwd": (_i, [_p, _p, _p, _i64, _p]),
+    "ssq_adam": (_i, [_i, _p, _p, _p, _p, _p, _f, _f, _f, _f, _p, _f, _f, _p]),
     "ssq_stream_copy": (_i, [_p, _p, _i64, _p]),
 }
 

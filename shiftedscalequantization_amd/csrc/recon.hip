@@ -151,6 +151,52 @@ __global__ __launch_bounds__(kBlock) void relu_bwd_tail(const float* __restrict_
   if (i < n) gin[i] = out[i] <= 0.0f ? 0.0f : g[i];
 }
 
+// ------------------------------------------------------------------ Adam step
+// torch.optim.Adam's single-tensor update (the reference's optimizer) for several
+// parameter tensors in one launch, op for op in fp32:
+//   m = m + (1-b1)*(g - m)                       exp_avg.lerp_(grad, 1-beta1)
+//   v = v*b2 + ((1-b2)*g)*g                      exp_avg_sq.mul_(beta2).addcmul_(g, g, 1-beta2)
+//   p = p + (nss*m) / (sqrt(v)/bc2s + eps)       param.addcdiv_(exp_avg, denom, -step_size)
+// nss = -lr/(1-b1^t) and bc2s = sqrt(1-b2^t) are host doubles rounded to fp32, read from
+// `hyper` (device) when given so that a captured graph picks up each step's values.
+struct AdamSeg {
+  float* p;
+  const float* g;
+  float* m;
+  float* v;
+  uint32_t n, blk0;
+};
+constexpr int kMaxAdamSeg = 48;
+constexpr int kAdamTile = 2048;
+struct AdamTable {
+  AdamSeg s[kMaxAdamSeg];
+  int nseg;
+};
+
+__global__ __launch_bounds__(kBlock) void adam_kernel(AdamTable tab, float w1, float b2, float w2,
+                                                      float eps, const float* __restrict__ hyper,
+                                                      float nss, float bc2s) {
+  if (hyper) {
+    nss = hyper[0];
+    bc2s = hyper[1];
+  }
+  int si = 0;
+  while (si + 1 < tab.nseg && blockIdx.x >= tab.s[si + 1].blk0) ++si;
+  const AdamSeg& sg = tab.s[si];
+  const uint32_t t0 = (blockIdx.x - sg.blk0) * (uint32_t)kAdamTile;
+  const uint32_t t1 = min(t0 + (uint32_t)kAdamTile, sg.n);
+  for (uint32_t e = t0 + threadIdx.x; e < t1; e += blockDim.x) {
+    const float g = sg.g[e];
+    float m = sg.m[e], v = sg.v[e];
+    m = __fadd_rn(m, __fmul_rn(w1, __fsub_rn(g, m)));
+    v = __fadd_rn(__fmul_rn(v, b2), __fmul_rn(__fmul_rn(w2, g), g));
+    const float denom = __fadd_rn(__fdiv_rn(__fsqrt_rn(v), bc2s), eps);
+    sg.p[e] = __fadd_rn(sg.p[e], __fdiv_rn(__fmul_rn(nss, m), denom));
+    sg.m[e] = m;
+    sg.v[e] = v;
+  }
+}
+
 }  // namespace ssq
 
 using namespace ssq;
@@ -250,4 +296,30 @@ extern "C" int ssq_relu_bwd(const float* g, const float* out, float* gin, int64_
     hipLaunchKernelGGL(relu_bwd_tail, dim3((unsigned)((n - start + kBlock - 1) / kBlock)),
                        dim3(kBlock), 0, s, g, out, gin, (uint32_t)start, (uint32_t)n);
   return check_launch("ssq_relu_bwd");
+}
+
+extern "C" int ssq_adam(int nseg, float* const* p, const float* const* g, float* const* m,
+                        float* const* v, const int64_t* n, float one_minus_beta1, float beta2,
+                        float one_minus_beta2, float eps, const float* hyper, float neg_step_size,
+                        float bias_correction2_sqrt, ssq_stream_t stream) {
+  SSQ_REQUIRE(nseg >= 1 && p && g && m && v && n, SSQ_E_ARG, "ssq_adam: bad arrays");
+  for (int base = 0; base < nseg; base += kMaxAdamSeg) {
+    AdamTable tab;
+    tab.nseg = nseg - base < kMaxAdamSeg ? nseg - base : kMaxAdamSeg;
+    int64_t blk = 0;
+    for (int k = 0; k < tab.nseg; ++k) {
+      const int i = base + k;
+      SSQ_REQUIRE(p[i] && g[i] && m[i] && v[i] && n[i] >= 1 && n[i] < (1ll << 31), SSQ_E_ARG,
+                  "ssq_adam: bad segment %d", i);
+      tab.s[k] = AdamSeg{p[i], g[i], m[i], v[i], (uint32_t)n[i], (uint32_t)blk};
+      blk += (n[i] + kAdamTile - 1) / kAdamTile;
+    }
+    SSQ_REQUIRE(blk < (1ll << 31), SSQ_E_ARG, "ssq_adam: too many tiles");
+    hipLaunchKernelGGL(adam_kernel, dim3((unsigned)blk), dim3(kBlock), 0, (hipStream_t)stream, tab,
+                       one_minus_beta1, beta2, one_minus_beta2, eps, hyper, neg_step_size,
+                       bias_correction2_sqrt);
+    const int rc = check_launch("ssq_adam");
+    if (rc) return rc;
+  }
+  return SSQ_OK;
 }

@@ -585,6 +585,25 @@ def bias_act(y, bias=None, res=None, relu=True):
     return out
 
 
+def adam_step(params, grads, exp_avgs, exp_avg_sqs, beta1, beta2, eps, hyper=None,
+              neg_step_size=0.0, bc2_sqrt=1.0):
+    """One torch.optim.Adam (single-tensor form) step for every tensor, one launch.
+    hyper: device [neg_step_size, bias_correction2_sqrt] (graph-capturable) or None."""
+    n = len(params)
+    P = C.c_void_p * n
+    pa, ga, ma, va = P(), P(), P(), P()
+    na = (C.c_int64 * n)()
+    for k, (p_, g_, m_, v_) in enumerate(zip(params, grads, exp_avgs, exp_avg_sqs)):
+        for t, nm in ((p_, "param"), (g_, "grad"), (m_, "exp_avg"), (v_, "exp_avg_sq")):
+            A.check(t, nm)
+            if not t.is_contiguous():
+                raise A.SSQError(f"adam_step: {nm} must be contiguous")
+        pa[k], ga[k], ma[k], va[k] = p_.data_ptr(), g_.data_ptr(), m_.data_ptr(), v_.data_ptr()
+        na[k] = p_.numel()
+    call("ssq_adam", n, pa, ga, ma, va, na, float(1 - beta1), float(beta2), float(1 - beta2),
+         float(eps), _vp(hyper), float(neg_step_size), float(bc2_sqrt), stream_of(params[0]))
+
+
 def stream_copy(src, dst):
     call("ssq_stream_copy", _vp(src), _vp(dst), src.numel(), stream_of(src))
 

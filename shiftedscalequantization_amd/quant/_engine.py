@@ -17,7 +17,7 @@ from .. import kernels as K
 class BatchFeeder:
     RING = 4
 
-    def __init__(self, cached_inp, cached_out, batch_size, device):
+    def __init__(self, cached_inp, cached_out, batch_size, device, extra_words=1):
         self.inp = cached_inp.to(device).contiguous()
         self.out = cached_out.to(device).contiguous()
         self.N = self.inp.shape[0]
@@ -26,13 +26,13 @@ class BatchFeeder:
         pin = torch.cuda.is_available()
         # one pinned slot = the batch indices + one 8-byte word carrying two fp32 values
         # riding on the same H2D copy (the loop's (lambda_S, b2) schedule pair)
-        self.ring = [torch.zeros(self.bs + 1, dtype=torch.int64, pin_memory=pin)
+        self.ring = [torch.zeros(self.bs + extra_words, dtype=torch.int64, pin_memory=pin)
                      for _ in range(self.RING)]
         self.done = [None] * self.RING
         self.k = 0
-        self._dev = torch.zeros(self.bs + 1, dtype=torch.int64, device=device)
+        self._dev = torch.zeros(self.bs + extra_words, dtype=torch.int64, device=device)
         self.didx = self._dev[:self.bs]
-        self.extra = self._dev[self.bs:].view(torch.float32)      # 2 floats on the device
+        self.extra = self._dev[self.bs:].view(torch.float32)      # 2*extra_words floats
         self.cur_inp = torch.empty((self.bs,) + tuple(self.inp.shape[1:]), device=device)
         self.cur_out = torch.empty((self.bs,) + tuple(self.out.shape[1:]), device=device)
 
@@ -41,8 +41,8 @@ class BatchFeeder:
         return torch.randperm(self.N)[:self.bs]
 
     def stage(self, perm, extra=None):
-        """One host -> device copy of the batch indices (and, optionally, two fp32 values
-        into self.extra) into the static device buffer."""
+        """One host -> device copy of the batch indices (and, optionally, fp32 values into
+        self.extra) into the static device buffer."""
         slot = self.k % self.RING
         if self.done[slot] is not None:
             self.done[slot].synchronize()
@@ -100,3 +100,49 @@ class LazyValue:
 
 def as_float(v):
     return v.get() if isinstance(v, LazyValue) else float(v)
+
+
+class SsqAdam:
+    """torch.optim.Adam (default hyper-parameters, no weight decay / amsgrad) as one
+    ssq_adam launch over all parameters, following the single-tensor update the reference
+    runs.  The step count and the bias corrections live on the host; step(hyper=...)
+    reads this step's (-lr/bc1, sqrt(bc2)) from a device pair instead, so a captured HIP
+    graph replays with each iteration's values (next_hyper() advances the count)."""
+
+    def __init__(self, params, lr=1e-3, betas=(0.9, 0.999), eps=1e-8):
+        self.params = [p for p in params]
+        self.param_groups = [{"params": self.params, "lr": lr, "betas": betas, "eps": eps}]
+        self.state = {p: {"exp_avg": torch.zeros_like(p, memory_format=torch.contiguous_format),
+                          "exp_avg_sq": torch.zeros_like(p, memory_format=torch.contiguous_format)}
+                      for p in self.params}
+        self.t = 0
+
+    def zero_grad(self, set_to_none=True):
+        for p in self.params:
+            if p.grad is not None:
+                if set_to_none:
+                    p.grad = None
+                else:
+                    p.grad.zero_()
+
+    def next_hyper(self):
+        """Advance the step count; (-lr/(1-b1^t), sqrt(1-b2^t)) as the reference computes
+        them in double precision."""
+        self.t += 1
+        g = self.param_groups[0]
+        b1, b2 = g["betas"]
+        return -(g["lr"] / (1 - b1 ** self.t)), (1 - b2 ** self.t) ** 0.5
+
+    def step(self, hyper=None):
+        live = [p for p in self.params if p.grad is not None]
+        if not live:
+            return
+        g = self.param_groups[0]
+        b1, b2 = g["betas"]
+        if hyper is None:
+            nss, bc2s = self.next_hyper()
+        else:
+            nss, bc2s = 0.0, 1.0
+        K.adam_step(live, [p.grad for p in live], [self.state[p]["exp_avg"] for p in live],
+                    [self.state[p]["exp_avg_sq"] for p in live], b1, b2, g["eps"], hyper=hyper,
+                    neg_step_size=nss, bc2_sqrt=bc2s)

@@ -12,7 +12,7 @@ import torch
 
 from .. import kernels as K
 from ..parallel_dp import GradBucket, world
-from ._engine import BatchFeeder, LazyValue, as_float
+from ._engine import BatchFeeder, LazyValue, SsqAdam, as_float
 from .adaptive_rounding import AdaRoundQuantizer
 from .data_utils import save_grad_data, save_inp_oup_data
 from .quant_block import BaseQuantBlock
@@ -70,7 +70,7 @@ def _reconstruct(model, block, qmodules, cali_data, batch_size, iters, weight, o
         device = next(model.parameters()).device
         cached_grads = save_grad_data(model, block, cali_data, act_quant, batch_size=batch_size) \
             if opt_mode != 'mse' else None
-        feeder = BatchFeeder(cached_inps, cached_outs, batch_size, device)
+        feeder = BatchFeeder(cached_inps, cached_outs, batch_size, device, extra_words=2)
         bucket = GradBucket(opt_params, average=dp_average) if (multi_gpu or world() > 1) else None
         if opt_mode == 'mse' and opt_params[0].is_cuda:
             _fast_loop(block, qmodules, opt_params, loss_func, feeder, bucket, iters, act_quant, lr,
@@ -117,18 +117,16 @@ def _fast_loop(block, qmodules, opt_params, loss_func, feeder, bucket, iters, ac
     AdaRound backward, fused Adam.  After GRAPH_WARMUP eager iterations the body is
     replayed from a HIP graph (single GPU).  The cosine LR schedule is stepped by the
     reference's own torch scheduler on a shadow optimizer and copied into Adam's device lr."""
-    device = opt_params[0].device
     use_graph = bool(graph and iters > GRAPH_WARMUP + 1)
-    kw = dict(fused=True, capturable=use_graph)
     if act_quant:
-        lr_dev = torch.tensor(float(lr), dtype=torch.float32, device=device)
-        optimizer = torch.optim.Adam(opt_params, lr=lr_dev if use_graph else lr, **kw)
-        shadow_p = torch.zeros(1, requires_grad=True)
-        shadow = torch.optim.Adam([shadow_p], lr=lr)
+        optimizer = SsqAdam(opt_params, lr=lr)
+        # the reference's cosine schedule, stepped by torch's own scheduler on a shadow
+        # optimizer so every lr value is the one the reference uses
+        shadow = torch.optim.Adam([torch.zeros(1, requires_grad=True)], lr=lr)
         scheduler = torch.optim.lr_scheduler.CosineAnnealingLR(shadow, T_max=max(iters, 1), eta_min=0.)
     else:
-        optimizer, scheduler = torch.optim.Adam(opt_params, **kw), None
-    regp = feeder.extra
+        optimizer, scheduler = SsqAdam(opt_params), None
+    regp, hyper = feeder.extra[0:2], feeder.extra[2:4]
     ada = [m.weight_quantizer for m in qmodules if isinstance(m.weight_quantizer, AdaRoundQuantizer)]
     if not act_quant:
         for q in ada:
@@ -147,14 +145,14 @@ def _fast_loop(block, qmodules, opt_params, loss_func, feeder, bucket, iters, ac
             out.backward(g)
         if bucket is not None:
             bucket.allreduce_()
-        optimizer.step()
+        optimizer.step(hyper=hyper)
         last['rec'] = rec
 
     graph_obj, ws_cache = None, {}
     try:
         for i in range(iters):
             b, lam, active = loss_func.schedule()
-            feeder.stage(feeder.draw(), extra=(lam, float(b)))
+            feeder.stage(feeder.draw(), extra=(lam, float(b)) + optimizer.next_hyper())
             # the round-loss value (reporting only) from alpha before this step, as the
             # reference's forward computes it
             rnd = loss_func.round_value(b) if (active and loss_func.wants_value()) else 0.0
@@ -174,12 +172,7 @@ def _fast_loop(block, qmodules, opt_params, loss_func, feeder, bucket, iters, ac
             if scheduler is not None:
                 shadow.step()
                 scheduler.step()
-                new_lr = shadow.param_groups[0]['lr']
-                if use_graph:
-                    lr_dev.fill_(new_lr)
-                else:
-                    for grp in optimizer.param_groups:
-                        grp['lr'] = new_lr
+                optimizer.param_groups[0]['lr'] = shadow.param_groups[0]['lr']
     finally:
         for q in ada:
             q._fused_reg = None

@@ -19,7 +19,7 @@ from tqdm import tqdm
 
 from .. import kernels as K
 from ..parallel_dp import GradBucket, world
-from ._engine import BatchFeeder, LazyValue, as_float
+from ._engine import BatchFeeder, SsqAdam, LazyValue, as_float
 from .quant_block import BaseQuantBlock
 from .quant_layer import QuantModule
 
@@ -67,19 +67,21 @@ def _fused_loop(block, modules, iters, lmda, model, p, lr, bias_cal, batch_size,
             opt_params += [m.alpha_out, m.beta_out]
     on_gpu = opt_params[0].is_cuda
     use_graph = bool(graph and on_gpu and world() == 1 and iters > GRAPH_WARMUP + 1)
-    # one fused Adam kernel for all parameters (capturable: its step count lives on the
-    # device, so the whole iteration can be replayed from a HIP graph)
-    optimizer = torch.optim.Adam(opt_params, lr=lr, fused=on_gpu, capturable=use_graph)
+    # one ssq_adam launch for all parameters; its per-step scalars ride on the index copy,
+    # so the whole iteration can be replayed from a HIP graph
+    optimizer = SsqAdam(opt_params, lr=lr) if on_gpu else torch.optim.Adam(opt_params, lr=lr)
     if verbose:
         print("number of elements in opt_params: {}".format(sum(t.numel() for t in opt_params)))
     loss_func = FusedScaleLossFunction(block, quantizers, round_loss='relaxation', lmda=lmda,
                                        max_count=iters, b_range=(20, 2), decay_start=0,
                                        warmup=0.2, p=p)
+    # extra device words: [lambda_S, b2 | -lr/bc1, sqrt(bc2)] refreshed with every index copy
     feeder = BatchFeeder(torch.cat(block.cached_inp_features), torch.cat(block.cached_out_features),
-                         batch_size, device)
+                         batch_size, device, extra_words=2)
     bucket = GradBucket(opt_params, average=dp_average) if world() > 1 else None
     # device (lambda_S, b2) read by the adaShift backward; it rides on the index copy
-    regp = loss_func.arm(device, regp=feeder.extra)
+    regp = loss_func.arm(device, regp=feeder.extra[0:2])
+    hyper = feeder.extra[2:4]
     last = {}
 
     def body():
@@ -98,7 +100,10 @@ def _fused_loop(block, modules, iters, lmda, model, p, lr, bias_cal, batch_size,
             quant_out.backward(g_out)
         if bucket is not None:
             bucket.allreduce_()
-        optimizer.step()
+        if on_gpu:
+            optimizer.step(hyper=hyper)
+        else:
+            optimizer.step()
         last['rec'] = rec
 
     graph_obj, ws_cache = None, {}
@@ -108,7 +113,8 @@ def _fused_loop(block, modules, iters, lmda, model, p, lr, bias_cal, batch_size,
         if iter_hook is not None:
             iter_hook(i)
         # reference-identical CPU randperm draw + this iteration's (lambda_S, b2): one H2D copy
-        feeder.stage(feeder.draw(), extra=loss_func.schedule_pair())
+        feeder.stage(feeder.draw(), extra=loss_func.schedule_pair() +
+                     (optimizer.next_hyper() if on_gpu else (0.0, 0.0)))
         if use_graph and i == GRAPH_WARMUP:
             optimizer.zero_grad(set_to_none=True)
             graph_obj = torch.cuda.CUDAGraph()

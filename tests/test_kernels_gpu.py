@@ -524,3 +524,32 @@ def test_lp_loss_relu_mask_folds_relu_backward(K):
     assert host(l1) == host(l2)
     ref = torch.where(out <= 0, torch.zeros_like(g_plain), g_plain)
     np.testing.assert_array_equal(host(g_mask), host(ref))
+
+
+def test_ssq_adam_matches_torch_single_tensor_adam(K):
+    """SsqAdam (one ssq_adam launch) follows torch.optim.Adam's single-tensor update (the
+    reference's optimizer on CPU) over 50 steps, with host and device hyper-parameters."""
+    from shiftedscalequantization_amd.quant._engine import SsqAdam
+    gen = torch.Generator().manual_seed(4)
+    shapes = [(64, 3), (5,), (7, 9, 3)]
+    ref = [torch.randn(s, generator=gen).requires_grad_(True) for s in shapes]
+    mine = [p.detach().clone().cuda().requires_grad_(True) for p in ref]
+    mine2 = [p.detach().clone().cuda().requires_grad_(True) for p in ref]
+    topt = torch.optim.Adam(ref, lr=3e-3, foreach=False)
+    sopt, sopt2 = SsqAdam(mine, lr=3e-3), SsqAdam(mine2, lr=3e-3)
+    hyper = torch.zeros(2, device="cuda")
+    for it in range(50):
+        grads = [torch.randn(s, generator=gen) * (0.1 if it % 7 else 1e-6) for s in shapes]
+        for p, g in zip(ref, grads):
+            p.grad = g.clone()
+        for p, g in zip(mine, grads):
+            p.grad = g.cuda()
+        for p, g in zip(mine2, grads):
+            p.grad = g.cuda()
+        topt.step()
+        sopt.step()
+        hyper.copy_(torch.tensor(sopt2.next_hyper(), dtype=torch.float32))
+        sopt2.step(hyper=hyper)
+    for a, b, c in zip(ref, mine, mine2):
+        np.testing.assert_allclose(host(b), a.detach().numpy(), rtol=2e-6, atol=1e-7)
+        np.testing.assert_array_equal(host(b), host(c))
