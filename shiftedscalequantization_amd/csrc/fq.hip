@@ -317,6 +317,67 @@ __global__ __launch_bounds__(kBlock) void fq_bwd_pt(const float* __restrict__ x,
   }
 }
 
+// float4 form of fq_bwd_pt (x, gy, gx 16-B aligned): two float4 loads per 4 elements,
+// (x/d)/d as t * (1/d) (it only feeds the reduction), zp sums only when asked for.
+template <bool ZP>
+__global__ __launch_bounds__(kBlock) void fq_bwd_pt4(const f32x4* __restrict__ x,
+                                                     const f32x4* __restrict__ gy,
+                                                     const float* __restrict__ delta,
+                                                     const float* __restrict__ zp, int64_t n4,
+                                                     float lo, float hi, f32x4* __restrict__ gx,
+                                                     double* __restrict__ part) {
+  __shared__ double red[16];
+  const float d = delta[0], z = zp[0];
+  const float rd = 1.0f / d;
+  double a0 = 0, a1 = 0, a2 = 0, a3 = 0;
+  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n4; i += stride) {
+    const f32x4 xv = x[i], gv = gy[i];
+    const float xs[4] = {xv.x, xv.y, xv.z, xv.w}, gs[4] = {gv.x, gv.y, gv.z, gv.w};
+    float go[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const float t = xs[j] / d;
+      const float v = __fadd_rn(rintf(t), z);
+      const bool m = (v >= lo) && (v <= hi);
+      const float q = clampf(v, lo, hi);
+      const float gq = __fmul_rn(gs[j], d);
+      const float gi = m ? gq : 0.0f;
+      go[j] = gi / d;
+      if (part) {
+        a0 += (double)gs[j] * (double)__fsub_rn(q, z);
+        a1 += (double)gi * (double)__fmul_rn(t, rd);
+        if (ZP) {
+          a2 += (double)gi;
+          a3 += (double)gq;
+        }
+      }
+    }
+    if (gx) {
+      f32x4 o;
+      o.x = go[0];
+      o.y = go[1];
+      o.z = go[2];
+      o.w = go[3];
+      gx[i] = o;
+    }
+  }
+  if (!part) return;
+  a0 = block_sum(a0, red);
+  a1 = block_sum(a1, red);
+  if (ZP) {
+    a2 = block_sum(a2, red);
+    a3 = block_sum(a3, red);
+  }
+  if (threadIdx.x == 0) {
+    double* o = part + 4 * (int64_t)blockIdx.x;
+    o[0] = a0;
+    o[1] = a1;
+    o[2] = a2;
+    o[3] = a3;
+  }
+}
+
 // one workgroup per channel row (rows are contiguous: n == nch * inner)
 __global__ __launch_bounds__(kBlock) void fq_bwd_rows(const float* __restrict__ x,
                                                       const float* __restrict__ gy,
@@ -601,9 +662,21 @@ extern "C" int ssq_fq_bwd(const float* x, const float* gy, const float* delta, c
     if (want_red)
       SSQ_REQUIRE(ws && ws_bytes >= ssq_fq_bwd_workspace_size(n, inner, nch), SSQ_E_WS,
                   "ssq_fq_bwd: workspace too small");
-    const int grid = grid_for(n, kBlock, kBwdBlocks);
-    hipLaunchKernelGGL(fq_bwd_pt, dim3(grid), dim3(kBlock), 0, s, x, gy, delta, zp, n, lo, hi, gx,
-                       want_red ? (double*)ws : nullptr);
+    const bool vec4 = n % 4 == 0 && aligned16(x) && aligned16(gy) && (!gx || aligned16(gx));
+    const int grid = grid_for(vec4 ? n / 4 : n, kBlock, kBwdBlocks);
+    if (vec4) {
+      if (gzp)
+        hipLaunchKernelGGL(fq_bwd_pt4<true>, dim3(grid), dim3(kBlock), 0, s, (const f32x4*)x,
+                           (const f32x4*)gy, delta, zp, n / 4, lo, hi, (f32x4*)gx,
+                           want_red ? (double*)ws : nullptr);
+      else
+        hipLaunchKernelGGL(fq_bwd_pt4<false>, dim3(grid), dim3(kBlock), 0, s, (const f32x4*)x,
+                           (const f32x4*)gy, delta, zp, n / 4, lo, hi, (f32x4*)gx,
+                           want_red ? (double*)ws : nullptr);
+    } else {
+      hipLaunchKernelGGL(fq_bwd_pt, dim3(grid), dim3(kBlock), 0, s, x, gy, delta, zp, n, lo, hi,
+                         gx, want_red ? (double*)ws : nullptr);
+    }
     if (want_red)
       hipLaunchKernelGGL(fq_bwd_finalize, dim3(1), dim3(kBlock), 0, s, (const double*)ws, grid,
                          gdelta, gzp);

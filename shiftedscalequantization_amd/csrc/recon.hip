@@ -35,9 +35,10 @@ __global__ __launch_bounds__(kBlock) void lp_loss_kernel(const float* __restrict
     } else if (PMODE == 1) {
       pw = a;
       dp = 1.0f;
-    } else {
+    } else {  // |d|^(p-1) = |d|^p / |d|: one pow per element instead of two
       pw = powf(a, p);
-      dp = __fmul_rn(p, powf(a, p - 1.0f));
+      // (a == 0 keeps pow's own value: 0 for p > 1, inf -> NaN gradient for p < 1, as torch)
+      dp = a > 0.0f ? __fmul_rn(p, __fdiv_rn(pw, a)) : __fmul_rn(p, powf(a, p - 1.0f));
     }
     acc += (double)pw;
     if (grad) {

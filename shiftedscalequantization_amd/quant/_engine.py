@@ -146,3 +146,23 @@ class SsqAdam:
         K.adam_step(live, [p.grad for p in live], [self.state[p]["exp_avg"] for p in live],
                     [self.state[p]["exp_avg_sq"] for p in live], b1, b2, g["eps"], hyper=hyper,
                     neg_step_size=nss, bc2_sqrt=bc2s)
+
+
+class frozen_except:
+    """Context: every parameter of `module` that requires grad but is not in `keep` is
+    frozen for the loop's duration.  The reference's autograd also computes (and
+    accumulates) those gradients -- the FP conv weights under a UAQ weight quantizer, the
+    weight quantizers' delta / zero_point, the act zero_points -- but nothing reads them."""
+
+    def __init__(self, module, keep):
+        ids = {id(p) for p in keep}
+        self.frozen = [p for p in module.parameters() if p.requires_grad and id(p) not in ids]
+
+    def __enter__(self):
+        for p in self.frozen:
+            p.requires_grad_(False)
+        return self
+
+    def __exit__(self, *exc):
+        for p in self.frozen:
+            p.requires_grad_(True)

@@ -12,7 +12,7 @@ import torch
 
 from .. import kernels as K
 from ..parallel_dp import GradBucket, world
-from ._engine import BatchFeeder, LazyValue, SsqAdam, as_float
+from ._engine import BatchFeeder, LazyValue, SsqAdam, as_float, frozen_except
 from .adaptive_rounding import AdaRoundQuantizer
 from .data_utils import save_grad_data, save_inp_oup_data
 from .quant_block import BaseQuantBlock
@@ -73,8 +73,9 @@ def _reconstruct(model, block, qmodules, cali_data, batch_size, iters, weight, o
         feeder = BatchFeeder(cached_inps, cached_outs, batch_size, device, extra_words=2)
         bucket = GradBucket(opt_params, average=dp_average) if (multi_gpu or world() > 1) else None
         if opt_mode == 'mse' and opt_params[0].is_cuda:
-            _fast_loop(block, qmodules, opt_params, loss_func, feeder, bucket, iters, act_quant, lr,
-                       p, graph and world() == 1 and not multi_gpu)
+            with frozen_except(block, opt_params):
+                _fast_loop(block, qmodules, opt_params, loss_func, feeder, bucket, iters, act_quant,
+                           lr, p, graph and world() == 1 and not multi_gpu)
         else:
             _eager_loop(opt_params, loss_func, feeder, bucket, cached_grads, block, iters, act_quant,
                         lr)

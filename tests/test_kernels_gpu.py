@@ -553,3 +553,22 @@ def test_ssq_adam_matches_torch_single_tensor_adam(K):
     for a, b, c in zip(ref, mine, mine2):
         np.testing.assert_allclose(host(b), a.detach().numpy(), rtol=2e-6, atol=1e-7)
         np.testing.assert_array_equal(host(b), host(c))
+
+
+@pytest.mark.parametrize("n", [4096 * 33, 4099, 12])
+def test_fq_bwd_per_tensor_vs_oracle(K, n):
+    """Per-tensor STE backward (float4 and scalar forms): gx bit-exact, delta / zero_point
+    gradients within 1e-5 of the oracle's double sums."""
+    gen = torch.Generator().manual_seed(n)
+    x = torch.relu(torch.randn(n, generator=gen)) * 3
+    gy = torch.randn(n, generator=gen)
+    d, z = torch.tensor(0.21), torch.tensor(1.0)
+    xr = x.cuda().requires_grad_(True)
+    dd = d.cuda().requires_grad_(True)
+    zz = z.cuda().requires_grad_(True)
+    y = K.fake_quant(xr, dd, zz, 4, False)
+    y.backward(gy.cuda())
+    rgx, rgd, rgz = R.fake_quant_bwd(x.numpy(), d.numpy(), z.numpy(), 4, False, gy.numpy())
+    np.testing.assert_array_equal(host(xr.grad), rgx)
+    close(host(dd.grad).reshape(-1), np.reshape(rgd, -1), rtol=1e-5, atol=1e-6)
+    close(host(zz.grad).reshape(-1), np.reshape(rgz, -1), rtol=1e-5, atol=1e-6)
