@@ -138,6 +138,12 @@ def _fast_loop(block, qmodules, opt_params, loss_func, feeder, bucket, iters, ac
         cur_inp, cur_out = feeder.gather()
         out = block(cur_inp)
         relu_in = getattr(out, '_ssq_relu_inputs', None)
+        if not out.requires_grad:
+            # no optimised parameter reaches the output (e.g. the act delta of a layer whose
+            # act quantizer is disabled): the reference's backward yields no gradient for it
+            # and its Adam step skips it -- only the loss value remains
+            last['rec'], _ = K.lp_loss_and_grad(out, cur_out, p, want_grad=False)
+            return
         if relu_in:
             rec, g = K.lp_loss_and_grad(out, cur_out, p, relu_mask=True)
             torch.autograd.backward(list(relu_in), [g] * len(relu_in))
