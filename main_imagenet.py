@@ -72,6 +72,8 @@ def main(argv=None):
         qnn(cali[:64])
     bs = 32
     report = {}
+    phases = {'init': time.time() - t0}
+    t_phase = time.time()
     if args.bias_ch_quant:
         shifts = [float(s) for s in args.shift_targets.split(',')]
         blocks = D.block_paths(qnn)
@@ -95,6 +97,9 @@ def main(argv=None):
         D.recon_model(qnn, qnn, cali_data=cali, iters=args.iters_w, weight=args.weight, asym=True,
                       b_range=(args.b_start, args.b_end), warmup=args.warmup, act_quant=False,
                       opt_mode='mse', batch_size=bs)
+    torch.cuda.synchronize(device)
+    phases['weight_recon'] = time.time() - t_phase
+    t_phase = time.time()
     qnn.set_quant_state(weight_quant=True, act_quant=False)
     if loader is not None:
         print('Weight quantization accuracy: {}'.format(validate_model(loader, qnn)))
@@ -106,10 +111,13 @@ def main(argv=None):
         D.recon_model(qnn, qnn, cali_data=cali, iters=args.iters_a, act_quant=True, opt_mode='mse',
                       lr=args.lr, p=args.p, batch_size=bs)
         qnn.set_quant_state(weight_quant=True, act_quant=True)
+        torch.cuda.synchronize(device)
+        phases['act_recon'] = time.time() - t_phase
         if loader is not None:
             print('Full quantization (W{}A{}) accuracy: {}'.format(args.n_bits_w, args.n_bits_a,
                                                                    validate_model(loader, qnn)))
-    print(f'calibration finished in {time.time() - t0:.1f}s; block rec losses: '
+    print(f'calibration finished in {time.time() - t0:.1f}s '
+          f'({", ".join(f"{k} {v:.1f}s" for k, v in phases.items())}); block rec losses: '
           f'{ {k: v for k, v in report.items()} }')
     if world > 1:
         dist.destroy_process_group()
