@@ -61,7 +61,7 @@ def main(argv=None):
         device = torch.device('cuda', torch.cuda.current_device())
     else:
         device = torch.device(args.device_gpu)
-    seed_all(args.seed)
+    seed_all(args.seed, deterministic=bool(args.deterministic))
     cali, val = load_data(args, device)
     loader = val_loader(val)
     t0 = time.time()
