@@ -606,9 +606,133 @@ def gen_recon_brecq(iters=10, n_cali=16, res=16):
     save("recon_brecq", **out)
 
 
+# ------------------------------------------------------------------ other block types
+# ResNet-50 Bottleneck (config 3), MobileNetV2 InvertedResidual with a depthwise conv
+# (config 4) and RegNetX ResBottleneckBlock with a grouped conv (config 5), each as the
+# only block of a tiny net.  The reference's QuantModel needs setPathName on these block
+# types (it is only defined on QuantBasicBlock): oracle-side shim below.
+def _tiny_block_net(kind):
+    torch.manual_seed(1005)
+    if kind == "bottleneck":
+        from models.resnet import Bottleneck
+        ds = nn.Sequential(nn.Conv2d(16, 32, 1, stride=2, bias=False), nn.BatchNorm2d(32))
+        blk, cout = Bottleneck(16, 8, stride=2, downsample=ds, norm_layer=nn.BatchNorm2d), 32
+    elif kind == "inverted":
+        from models.mobilenetv2 import InvertedResidual
+        blk, cout = InvertedResidual(16, 16, 1, 2), 16
+    else:
+        from models.regnet import ResBottleneckBlock
+        blk, cout = ResBottleneckBlock(16, 32, 2, 1.0, 8), 32
+    net = nn.Sequential(nn.Conv2d(3, 16, 3, padding=1, bias=False), nn.BatchNorm2d(16), nn.ReLU(),
+                        blk, nn.AdaptiveAvgPool2d(1), nn.Flatten(), nn.Linear(cout, 10))
+    g = torch.Generator().manual_seed(7)
+    for m in net.modules():
+        if isinstance(m, nn.Conv2d):
+            nn.init.kaiming_normal_(m.weight, mode="fan_out", nonlinearity="relu")
+        if isinstance(m, nn.BatchNorm2d):
+            m.running_mean.copy_(torch.randn(m.num_features, generator=g) * 0.1)
+            m.running_var.copy_(torch.rand(m.num_features, generator=g) + 0.5)
+            m.weight.data.copy_(torch.rand(m.num_features, generator=g) + 0.5)
+            m.bias.data.copy_(torch.randn(m.num_features, generator=g) * 0.1)
+    return net.eval()
+
+
+def _block_qnn(kind):
+    from quant.quant_block import BaseQuantBlock
+    if not hasattr(BaseQuantBlock, "setPathName"):
+        BaseQuantBlock.setPathName = lambda self, n: setattr(self, "pathName", n)
+    wq = {"n_bits": 2, "channel_wise": True, "scale_method": "max", "tune_delta_zero": False,
+          "symmetric": False}
+    aq = {"n_bits": 4, "channel_wise": False, "scale_method": "mse", "tune_delta_zero": False,
+          "leaf_param": True, "symmetric": False}
+    qnn = QuantModel(model=_tiny_block_net(kind), weight_quant_params=wq, act_quant_params=aq)
+    qnn.eval()
+    qnn.set_first_last_layer_to_8bit()
+    return qnn
+
+
+def _named_qms(block):
+    return [(n, m) for n, m in block.named_modules() if isinstance(m, QuantModule)]
+
+
+def gen_recon_blocks(iters=30, brecq_iters=10, n_cali=16, res=16):
+    from quant.channelQuant import ChannelQuant
+    for kind in ("bottleneck", "inverted", "resbottleneck"):
+        out = {}
+        # fused shifted-scale reconstruction
+        qnn = _block_qnn(kind)
+        torch.manual_seed(1005)
+        cali = torch.randn(n_cali, 3, res, res)
+        qnn.set_quant_state(True, False)
+        with torch.no_grad():
+            qnn(cali[:8])
+        block = qnn.model[3]
+        shift = [31 / 32, 33 / 32, 1.0]
+        for n, m in _named_qms(block):
+            out[f"f_{n}_w"], out[f"f_{n}_b"] = t2n(m.org_weight), t2n(m.org_bias)
+            out[f"f_{n}_delta"] = t2n(m.weight_quantizer.delta.reshape(-1))
+            out[f"f_{n}_zp"] = t2n(m.weight_quantizer.zero_point.reshape(-1))
+            m.weight_quantizer = ChannelQuant(1.0, uaq=m.weight_quantizer, weight_tensor=m.org_weight.data,
+                                              shiftTarget=shift, name="." + n)
+            m.use_weight_quant = True
+            m.cache_features = "none"
+        qnn.set_quant_state(False, False)
+        # the reference caches features only inside QuantBasicBlock.forward: capture this
+        # block's FP input / output with a hook instead (same batches, same FP state)
+        ins, outs = [], []
+        def grab(mod, i, o):
+            ins.append(i[0].detach().clone())
+            outs.append(o.detach().clone())
+        h = block.register_forward_hook(grab)
+        with torch.no_grad():
+            for i in range(n_cali // 8):
+                qnn(cali[i * 8:(i + 1) * 8])
+        h.remove()
+        block.cached_inp_features, block.cached_out_features = [torch.cat(ins)], [torch.cat(outs)]
+        MSM.set_quant_state_block(qnn, [BLOCK], "", True)
+        out["f_cached_inp"] = t2n(torch.cat(block.cached_inp_features))
+        out["f_cached_out"] = t2n(torch.cat(block.cached_out_features))
+        torch.manual_seed(1005)
+        with _Spy(LRF.FusedScaleLossFunction) as spy:
+            res_loss = LRF.block_recon_fused_shiftedScale(block, iters, (0.01, 0.1), qnn, None)
+        out["f_perms"] = np.stack([p.numpy() for p in spy.perms]).astype(np.int64)
+        out["f_rec_loss"] = np.array([r[0] for r in spy.rec], np.float64)
+        out["f_final_losses"] = np.array(res_loss, np.float64)
+        for n, m in _named_qms(block):
+            out[f"f_{n}_alpha"] = t2n(m.weight_quantizer.alpha)
+            with torch.no_grad():
+                out[f"f_{n}_what_hard"] = t2n(m.weight_quantizer(m.weight))
+        # BRECQ AdaRound weight phase
+        qnn = _block_qnn(kind)
+        torch.manual_seed(1005)
+        cali = torch.randn(n_cali, 3, res, res)
+        qnn.set_quant_state(True, False)
+        with torch.no_grad():
+            qnn(cali[:8])
+        block = qnn.model[3]
+        out["b_cali"] = t2n(cali)
+        qms = [m for m in qnn.modules() if isinstance(m, QuantModule)]
+        for k, m in enumerate(qms):
+            out[f"b_qm{k}_w"], out[f"b_qm{k}_b"] = t2n(m.org_weight), t2n(m.org_bias)
+            out[f"b_qm{k}_delta"] = t2n(m.weight_quantizer.delta.reshape(-1))
+            out[f"b_qm{k}_zp"] = t2n(m.weight_quantizer.zero_point.reshape(-1))
+        torch.manual_seed(1005)
+        with _Spy(BR.LossFunction) as spy:
+            BR.block_reconstruction(qnn, block, cali, batch_size=8, iters=brecq_iters, weight=0.01,
+                                    asym=True, b_range=(20, 2), warmup=0.2, act_quant=False,
+                                    opt_mode="mse")
+        out["b_total_loss"] = np.array([r[1] for r in spy.rec], np.float64)
+        for n, m in _named_qms(block):
+            out[f"b_{n}_alpha"] = t2n(m.weight_quantizer.alpha)
+            with torch.no_grad():
+                out[f"b_{n}_what_hard"] = t2n(m.weight_quantizer(m.weight))
+        out["iters"] = np.array([iters, brecq_iters])
+        save(f"recon_block_{kind}", **out)
+
+
 if __name__ == "__main__":
     which = sys.argv[1:] or ["uaq", "channelquant", "adaround", "inpscale", "loss", "recon",
-                             "layershift", "brecq"]
+                             "layershift", "brecq", "blocks"]
     torch.set_num_threads(4)
     if "uaq" in which:
         gen_uaq()
@@ -626,3 +750,5 @@ if __name__ == "__main__":
         gen_recon_layer_shift()
     if "brecq" in which:
         gen_recon_brecq()
+    if "blocks" in which:
+        gen_recon_blocks()
