@@ -188,26 +188,45 @@ __global__ void finalize_mse(const double* __restrict__ part, const float* __res
 }
 
 // ------------------------------------------------------------------ K10
+// One wave per column j (4 columns per workgroup).  The reference scans c = k/level for
+// k = level..1 and keeps the LAST (smallest) c whose normalized codes fit.  Every op in
+// v(c) = ((W/c)/d + zero)/x_range is monotone (IEEE rounding is), so as c shrinks the
+// column max can only grow and the min only fall: the set of fitting c is upward closed,
+// and a binary search over k returns exactly the scan's answer in log2(level) passes of
+// the column instead of level passes.  Each pass: lanes sweep the Co rows, wave min/max.
 __global__ __launch_bounds__(kBlock) void inpscale_search_kernel(
     const float* __restrict__ W, const float* __restrict__ delta, const float* __restrict__ raw_zp,
     int64_t Co, int64_t J, float x_range, int level, float min_lim, float max_lim,
     float* __restrict__ inp) {
-  const int64_t j = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const int64_t j = (int64_t)blockIdx.x * (blockDim.x / kWave) + threadIdx.x / kWave;
+  const int lane = threadIdx.x & (kWave - 1);
   if (j >= J) return;
-  float cur = 1.0f;
-  for (int k = level; k >= 1; --k) {
-    const float c = (float)((double)k / (double)level);
+  auto cand = [&](int k) { return (float)((double)k / (double)level); };
+  auto fits = [&](int k) {
+    const float c = cand(k);
     float mn = INFINITY, mx = -INFINITY;
-    for (int64_t co = 0; co < Co; ++co) {
+    for (int64_t co = lane; co < Co; co += kWave) {
       const float d = delta[co];
       const float zero = rintf(raw_zp[co] / d);
       const float v = __fadd_rn((W[co * J + j] / c) / d, zero) / x_range;
       mn = fminf(mn, v);
       mx = fmaxf(mx, v);
     }
-    if (mn > min_lim && mx < max_lim) cur = c;
+    mn = wave_min(mn);
+    mx = wave_max(mx);
+    return mn > min_lim && mx < max_lim;
+  };
+  float cur = 1.0f;
+  if (fits(level)) {
+    int lo = 1, hi = level;  // fits(hi) holds
+    while (lo < hi) {
+      const int mid = lo + (hi - lo) / 2;
+      if (fits(mid)) hi = mid;
+      else lo = mid + 1;
+    }
+    cur = cand(hi);
   }
-  inp[j] = cur;
+  if (lane == 0) inp[j] = cur;
 }
 
 __global__ __launch_bounds__(kBlock) void inpscale_fwd_kernel(
@@ -276,7 +295,9 @@ extern "C" int ssq_inpscale_search(const float* W, const float* delta, const flo
               "ssq_inpscale_search: bad args");
   const int xr = (1 << n_bits) - 1;
   const double min_lim = 0.0 - 0.5 / xr * threshold, max_lim = 1.0 + 0.5 / xr * threshold;
-  hipLaunchKernelGGL(inpscale_search_kernel, dim3((unsigned)((J + kBlock - 1) / kBlock)),
+  const int64_t cols_per_block = kBlock / kWave;
+  hipLaunchKernelGGL(inpscale_search_kernel,
+                     dim3((unsigned)((J + cols_per_block - 1) / cols_per_block)),
                      dim3(kBlock), 0, (hipStream_t)stream, W, delta, raw_zp, Co, J, (float)xr,
                      level, (float)min_lim, (float)max_lim, inp);
   return check_launch("ssq_inpscale_search");

@@ -572,3 +572,18 @@ def test_fq_bwd_per_tensor_vs_oracle(K, n):
     np.testing.assert_array_equal(host(xr.grad), rgx)
     close(host(dd.grad).reshape(-1), np.reshape(rgd, -1), rtol=1e-5, atol=1e-6)
     close(host(zz.grad).reshape(-1), np.reshape(rgz, -1), rtol=1e-5, atol=1e-6)
+
+
+@pytest.mark.parametrize("level,threshold", [(1024, 2.0), (64, 1.0), (1, 1.5), (333, 0.5)])
+def test_inpscale_search_binary_search_equals_scan(K, level, threshold):
+    """The kernel's binary search over k returns exactly the reference's linear scan
+    (the oracle) -- every column, including ones where no candidate fits."""
+    gen = torch.Generator().manual_seed(level)
+    w = torch.randn(96, 32, 3, 3, generator=gen) * 0.05
+    w[:, 0] *= 40.0                                # columns where only c = 1 (or none) fits
+    d, z, raw = R.init_scale(w.numpy(), 2, False, True, "max")
+    inp = K.inpscale_search(w.cuda(), dev(d).view(-1, 1, 1, 1), dev(raw).view(-1, 1, 1, 1), 2, level,
+                            threshold)
+    ref = R.inpscale_search(w.numpy(), d.reshape(-1, 1, 1, 1), raw.reshape(-1, 1, 1, 1), 2, level,
+                            threshold)
+    np.testing.assert_array_equal(host(inp), ref)
