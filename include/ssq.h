@@ -70,6 +70,14 @@ int ssq_fq_bwd(const float* x, const float* gy, const float* delta, const float*
                int64_t n, int64_t inner, int64_t nch, int qmin, int qmax,
                float* gx, float* gdelta, float* gzp, void* ws, size_t ws_bytes,
                ssq_stream_t stream);
+/* Per-tensor ssq_fq_bwd for an x that is a ReLU output, with the ReLU backward folded in:
+ * gx is written at the ReLU's input (x <= 0 -> 0, torch threshold_backward on the output),
+ * bit-identical to ssq_fq_bwd followed by ssq_relu_bwd.  Workspace as ssq_fq_bwd with
+ * nch = 1.  Replaces the act quantizer's backward (quant_layer.py:92-98) + the ReLU's
+ * (quant_block.py:117, QuantModule activation quant_layer.py:270).                     */
+int ssq_fq_relu_bwd(const float* x, const float* gy, const float* delta, const float* zp,
+                    int64_t n, int qmin, int qmax, float* gx, float* gdelta, float* gzp,
+                    void* ws, size_t ws_bytes, ssq_stream_t stream);
 
 /* ---------------------------------------------------------------- K3/K4 scale init
  * init_quantization_scale (quant_layer.py:100-166) for `rows` independent rows of
@@ -220,6 +228,14 @@ int ssq_gather_rows2(const float* src0, float* dst0, int64_t row0, const float* 
 int ssq_bias_act(const float* y, const float* bias, const float* res, float* out, int64_t n,
                  int64_t hw, int64_t C, int relu, ssq_stream_t stream);
 int ssq_relu_bwd(const float* g, const float* out, float* gin, int64_t n, ssq_stream_t stream);
+/* ssq_bias_act with the following per-tensor activation fake-quant (quant_layer.py:92-98,
+ * applied at quant_layer.py:272 / quant_block.py:118) in the same pass:
+ *   yq = (clamp(rint(out/delta[0]) + zp[0], qmin, qmax) - zp[0]) * delta[0]
+ * bit-identical to ssq_bias_act + ssq_fq_fwd.  out (the pre-quant activation, needed only
+ * by the backward) may be NULL: then the pass reads y (+res) and writes yq alone.        */
+int ssq_bias_act_fq(const float* y, const float* bias, const float* res, float* out, float* yq,
+                    int64_t n, int64_t hw, int64_t C, int relu, const float* delta,
+                    const float* zp, int qmin, int qmax, ssq_stream_t stream);
 
 /* ---------------------------------------------------------------- Adam
  * torch.optim.Adam's single-tensor step (the reference's optimizer; block_recon.py:57-60,

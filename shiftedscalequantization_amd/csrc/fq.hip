@@ -30,21 +30,6 @@ int check_launch(const char* what) {
   return SSQ_OK;
 }
 
-// ------------------------------------------------------------------ element op
-struct QParams {
-  float d, z, lo, hi;
-};
-
-template <bool FAST = false>
-__device__ __forceinline__ float fq1(float x, const QParams& p, float* qout, float r = 0.0f) {
-  // x / delta: IEEE fp32 divide, or its bit-identical reciprocal form (div_fast)
-  float t = FAST ? div_fast(x, p.d, r) : x / p.d;
-  float v = __fadd_rn(rintf(t), p.z);      // round_ste fwd == round half-even, + zp
-  float q = clampf(v, p.lo, p.hi);         // clamp(x_int, lo, hi)
-  *qout = q;
-  return __fmul_rn(__fsub_rn(q, p.z), p.d);  // (x_quant - zp) * delta
-}
-
 __device__ __forceinline__ uint32_t pack4(float a, float b, float c, float d) {
   return (uint32_t)((int)a & 0xff) | ((uint32_t)((int)b & 0xff) << 8) |
          ((uint32_t)((int)c & 0xff) << 16) | ((uint32_t)((int)d & 0xff) << 24);
@@ -277,6 +262,9 @@ __global__ __launch_bounds__(kBlock) void fq_fwd_multi_kernel(SegTable tab) {
 
 // ------------------------------------------------------------------ backward
 // partial layout in ws: per block 4 doubles {sum gy*(q-zp), sum g_int*((x/d)/d), sum g_int, sum gy*d}
+// RELU: x is a ReLU output and gx is written at the ReLU's input (torch threshold_backward
+// on the output: x <= 0 -> 0), i.e. fq backward and relu_bwd in one pass.
+template <bool RELU>
 __global__ __launch_bounds__(kBlock) void fq_bwd_pt(const float* __restrict__ x,
                                                     const float* __restrict__ gy,
                                                     const float* __restrict__ delta,
@@ -295,7 +283,7 @@ __global__ __launch_bounds__(kBlock) void fq_bwd_pt(const float* __restrict__ x,
     const float q = clampf(v, lo, hi);
     const float gq = __fmul_rn(g, d);
     const float gi = m ? gq : 0.0f;
-    if (gx) gx[i] = gi / d;
+    if (gx) gx[i] = (RELU && xv <= 0.0f) ? 0.0f : gi / d;
     if (part) {
       a0 += (double)g * (double)__fsub_rn(q, z);
       a1 += (double)gi * (double)(t / d);
@@ -319,7 +307,7 @@ __global__ __launch_bounds__(kBlock) void fq_bwd_pt(const float* __restrict__ x,
 
 // float4 form of fq_bwd_pt (x, gy, gx 16-B aligned): two float4 loads per 4 elements,
 // (x/d)/d as t * (1/d) (it only feeds the reduction), zp sums only when asked for.
-template <bool ZP>
+template <bool ZP, bool RELU>
 __global__ __launch_bounds__(kBlock) void fq_bwd_pt4(const f32x4* __restrict__ x,
                                                      const f32x4* __restrict__ gy,
                                                      const float* __restrict__ delta,
@@ -343,7 +331,7 @@ __global__ __launch_bounds__(kBlock) void fq_bwd_pt4(const f32x4* __restrict__ x
       const float q = clampf(v, lo, hi);
       const float gq = __fmul_rn(gs[j], d);
       const float gi = m ? gq : 0.0f;
-      go[j] = gi / d;
+      go[j] = (RELU && xs[j] <= 0.0f) ? 0.0f : gi / d;
       if (part) {
         a0 += (double)gs[j] * (double)__fsub_rn(q, z);
         a1 += (double)gi * (double)__fmul_rn(t, rd);
@@ -649,44 +637,58 @@ extern "C" size_t ssq_fq_bwd_workspace_size(int64_t n, int64_t inner, int64_t nc
   return nch == 1 ? (size_t)kBwdBlocks * 4 * sizeof(double) : 0;
 }
 
-extern "C" int ssq_fq_bwd(const float* x, const float* gy, const float* delta, const float* zp,
-                          int64_t n, int64_t inner, int64_t nch, int qmin, int qmax, float* gx,
-                          float* gdelta, float* gzp, void* ws, size_t ws_bytes,
-                          ssq_stream_t stream) {
-  SSQ_REQUIRE(n >= 1 && inner >= 1 && nch >= 1 && qmin < qmax, SSQ_E_ARG, "ssq_fq_bwd: sizes");
-  SSQ_REQUIRE(x && gy && delta && zp, SSQ_E_ARG, "ssq_fq_bwd: null pointer");
-  hipStream_t s = (hipStream_t)stream;
+static int fq_bwd(const char* what, bool relu, const float* x, const float* gy,
+                  const float* delta, const float* zp, int64_t n, int64_t inner, int64_t nch,
+                  int qmin, int qmax, float* gx, float* gdelta, float* gzp, void* ws,
+                  size_t ws_bytes, hipStream_t s) {
+  SSQ_REQUIRE(n >= 1 && inner >= 1 && nch >= 1 && qmin < qmax, SSQ_E_ARG, "%s: sizes", what);
+  SSQ_REQUIRE(x && gy && delta && zp, SSQ_E_ARG, "%s: null pointer", what);
   const float lo = (float)qmin, hi = (float)qmax;
   const bool want_red = gdelta || gzp;
   if (nch == 1) {
     if (want_red)
       SSQ_REQUIRE(ws && ws_bytes >= ssq_fq_bwd_workspace_size(n, inner, nch), SSQ_E_WS,
-                  "ssq_fq_bwd: workspace too small");
+                  "%s: workspace too small", what);
     const bool vec4 = n % 4 == 0 && aligned16(x) && aligned16(gy) && (!gx || aligned16(gx));
     const int grid = grid_for(vec4 ? n / 4 : n, kBlock, kBwdBlocks);
+    double* part = want_red ? (double*)ws : nullptr;
     if (vec4) {
-      if (gzp)
-        hipLaunchKernelGGL(fq_bwd_pt4<true>, dim3(grid), dim3(kBlock), 0, s, (const f32x4*)x,
-                           (const f32x4*)gy, delta, zp, n / 4, lo, hi, (f32x4*)gx,
-                           want_red ? (double*)ws : nullptr);
-      else
-        hipLaunchKernelGGL(fq_bwd_pt4<false>, dim3(grid), dim3(kBlock), 0, s, (const f32x4*)x,
-                           (const f32x4*)gy, delta, zp, n / 4, lo, hi, (f32x4*)gx,
-                           want_red ? (double*)ws : nullptr);
+      auto k = gzp ? (relu ? fq_bwd_pt4<true, true> : fq_bwd_pt4<true, false>)
+                   : (relu ? fq_bwd_pt4<false, true> : fq_bwd_pt4<false, false>);
+      hipLaunchKernelGGL(k, dim3(grid), dim3(kBlock), 0, s, (const f32x4*)x, (const f32x4*)gy,
+                         delta, zp, n / 4, lo, hi, (f32x4*)gx, part);
     } else {
-      hipLaunchKernelGGL(fq_bwd_pt, dim3(grid), dim3(kBlock), 0, s, x, gy, delta, zp, n, lo, hi,
-                         gx, want_red ? (double*)ws : nullptr);
+      auto k = relu ? fq_bwd_pt<true> : fq_bwd_pt<false>;
+      hipLaunchKernelGGL(k, dim3(grid), dim3(kBlock), 0, s, x, gy, delta, zp, n, lo, hi, gx,
+                         part);
     }
     if (want_red)
       hipLaunchKernelGGL(fq_bwd_finalize, dim3(1), dim3(kBlock), 0, s, (const double*)ws, grid,
                          gdelta, gzp);
   } else {
+    SSQ_REQUIRE(!relu, SSQ_E_ARG, "%s: the ReLU-fused backward is per-tensor only", what);
     SSQ_REQUIRE(n == nch * inner, SSQ_E_ARG,
-                "ssq_fq_bwd: per-channel reduction needs contiguous rows (n == nch*inner)");
+                "%s: per-channel reduction needs contiguous rows (n == nch*inner)", what);
     hipLaunchKernelGGL(fq_bwd_rows, dim3((unsigned)nch), dim3(kBlock), 0, s, x, gy, delta, zp,
                        inner, lo, hi, gx, gdelta, gzp);
   }
-  return check_launch("ssq_fq_bwd");
+  return check_launch(what);
+}
+
+extern "C" int ssq_fq_bwd(const float* x, const float* gy, const float* delta, const float* zp,
+                          int64_t n, int64_t inner, int64_t nch, int qmin, int qmax, float* gx,
+                          float* gdelta, float* gzp, void* ws, size_t ws_bytes,
+                          ssq_stream_t stream) {
+  return fq_bwd("ssq_fq_bwd", false, x, gy, delta, zp, n, inner, nch, qmin, qmax, gx, gdelta,
+                gzp, ws, ws_bytes, (hipStream_t)stream);
+}
+
+extern "C" int ssq_fq_relu_bwd(const float* x, const float* gy, const float* delta,
+                               const float* zp, int64_t n, int qmin, int qmax, float* gx,
+                               float* gdelta, float* gzp, void* ws, size_t ws_bytes,
+                               ssq_stream_t stream) {
+  return fq_bwd("ssq_fq_relu_bwd", true, x, gy, delta, zp, n, n, 1, qmin, qmax, gx, gdelta,
+                gzp, ws, ws_bytes, (hipStream_t)stream);
 }
 
 extern "C" int ssq_stream_copy(const float* src, float* dst, int64_t n, ssq_stream_t stream) {

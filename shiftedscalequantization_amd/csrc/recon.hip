@@ -13,43 +13,70 @@ namespace ssq {
 
 constexpr int kLossBlocks = 1024;
 
+// |d|^p and its derivative p*|d|^(p-1) for one element.
 template <int PMODE>  // 0: p == 2, 1: p == 1, 2: general p
+__device__ __forceinline__ void lp_term(float a, float p, float& pw, float& dp) {
+  if (PMODE == 0) {
+    pw = __fmul_rn(a, a);
+    dp = __fmul_rn(2.0f, a);
+  } else if (PMODE == 1) {
+    pw = a;
+    dp = 1.0f;
+  } else {
+    // both powers from one hardware log2 and two hardware exp2 (about 1e-6 relative; the
+    // loss and gradient tolerance is 1e-5).  No divide and no ocml powf: those made this
+    // pass VALU-bound.  a == 0: log2 = -inf gives pow's own values (0 for p > 1; inf for
+    // p - 1 < 0, so the gradient is inf * sgn(0) = NaN, as torch's)
+    const float l = __builtin_amdgcn_logf(a);
+    pw = __builtin_amdgcn_exp2f(__fmul_rn(p, l));
+    dp = __fmul_rn(p, __builtin_amdgcn_exp2f(__fmul_rn(__fsub_rn(p, 1.0f), l)));
+  }
+}
+
+template <int PMODE>
+__device__ __forceinline__ float lp_elem(float x, float t, float p, float inv_m, float gs,
+                                         int relu_mask, double& acc) {
+  const float d = __fsub_rn(x, t);
+  float pw, dp;
+  lp_term<PMODE>(fabsf(d), p, pw, dp);
+  acc += (double)pw;
+  const float sg = d > 0.0f ? 1.0f : (d < 0.0f ? -1.0f : 0.0f);
+  const float gv = __fmul_rn(__fmul_rn(__fmul_rn(inv_m, dp), sg), gs);
+  // relu_mask: pred is a ReLU output; the gradient is written at the ReLU's input
+  // (torch threshold_backward: out <= 0 -> 0)
+  return (relu_mask && x <= 0.0f) ? 0.0f : gv;
+}
+
+// float4 body over the first n & ~3 elements (when aligned), scalar tail; one double partial per block.
+template <int PMODE>
 __global__ __launch_bounds__(kBlock) void lp_loss_kernel(const float* __restrict__ pred,
                                                          const float* __restrict__ tgt, int64_t n,
                                                          float p, float inv_m,
                                                          float* __restrict__ grad,
                                                          const float* __restrict__ gscale,
-                                                         int relu_mask,
+                                                         int relu_mask, int vec,
                                                          double* __restrict__ part) {
   __shared__ double red[16];
   double acc = 0.0;
   const float gs = gscale ? gscale[0] : 1.0f;
   const int64_t stride = (int64_t)gridDim.x * blockDim.x;
-  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
-    const float d = __fsub_rn(pred[i], tgt[i]);
-    const float a = fabsf(d);
-    float pw, dp;  // |d|^p and p*|d|^(p-1)
-    if (PMODE == 0) {
-      pw = __fmul_rn(a, a);
-      dp = __fmul_rn(2.0f, a);
-    } else if (PMODE == 1) {
-      pw = a;
-      dp = 1.0f;
-    } else {  // |d|^(p-1) = |d|^p / |d|: one pow per element instead of two
-      // |d|^p = exp2(p*log2|d|) on the hardware log/exp (about 1e-6 relative, the loss
-      // and gradient tolerance is 1e-5; the ocml powf made this pass VALU-bound)
-      pw = __builtin_amdgcn_exp2f(__fmul_rn(p, __builtin_amdgcn_logf(a)));
-      // (a == 0 keeps pow's own value: 0 for p > 1, inf -> NaN gradient for p < 1, as torch)
-      dp = a > 0.0f ? __fmul_rn(p, __fdiv_rn(pw, a)) : __fmul_rn(p, powf(a, p - 1.0f));
-    }
-    acc += (double)pw;
-    if (grad) {
-      const float sg = d > 0.0f ? 1.0f : (d < 0.0f ? -1.0f : 0.0f);
-      const float gv = __fmul_rn(__fmul_rn(__fmul_rn(inv_m, dp), sg), gs);
-      // relu_mask: pred is a ReLU output; write the gradient at the ReLU's input
-      // (torch threshold_backward: out <= 0 -> 0)
-      grad[i] = (relu_mask && pred[i] <= 0.0f) ? 0.0f : gv;
-    }
+  const int64_t tid = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const int64_t n4 = vec ? n >> 2 : 0;  // vec: every pointer 16-B aligned
+  const f32x4* P = (const f32x4*)pred;
+  const f32x4* T = (const f32x4*)tgt;
+  f32x4* G = (f32x4*)grad;
+  for (int64_t i = tid; i < n4; i += stride) {
+    const f32x4 x = __builtin_nontemporal_load(P + i), t = __builtin_nontemporal_load(T + i);
+    f32x4 g;
+    g.x = lp_elem<PMODE>(x.x, t.x, p, inv_m, gs, relu_mask, acc);
+    g.y = lp_elem<PMODE>(x.y, t.y, p, inv_m, gs, relu_mask, acc);
+    g.z = lp_elem<PMODE>(x.z, t.z, p, inv_m, gs, relu_mask, acc);
+    g.w = lp_elem<PMODE>(x.w, t.w, p, inv_m, gs, relu_mask, acc);
+    if (grad) __builtin_nontemporal_store(g, G + i);
+  }
+  for (int64_t i = (n4 << 2) + tid; i < n; i += stride) {
+    const float g = lp_elem<PMODE>(pred[i], tgt[i], p, inv_m, gs, relu_mask, acc);
+    if (grad) grad[i] = g;
   }
   if (!part) return;
   acc = block_sum(acc, red);
@@ -95,14 +122,23 @@ __global__ __launch_bounds__(kBlock) void gather2_kernel(const float* __restrict
 // out = act(y + bias[c] (+ res)),  c = (i / hw) % C, in the reference's op order (conv
 // bias add, residual add, ReLU: three separate fp32 roundings -> bit-identical to the
 // eager sequence), one pass instead of three.
-template <bool RES, bool RELU>
+template <bool RES, bool RELU, bool QUANT>
 __global__ __launch_bounds__(kBlock) void bias_act_kernel(const float* __restrict__ y,
                                                           const float* __restrict__ bias,
                                                           const float* __restrict__ res,
                                                           float* __restrict__ out, uint32_t n,
                                                           FastDiv div_hw, FastDiv div_c,
-                                                          uint32_t C, int vec) {
+                                                          uint32_t C, int vec,
+                                                          float* __restrict__ yq,
+                                                          const float* __restrict__ qdelta,
+                                                          const float* __restrict__ qzp,
+                                                          float qlo, float qhi) {
   const uint32_t stride = gridDim.x * blockDim.x;
+  QParams qp{1.0f, 0.0f, qlo, qhi};
+  if (QUANT) {
+    qp.d = qdelta[0];
+    qp.z = qzp[0];
+  }
   auto one = [&](uint32_t i, float v, float rv) {
     const uint32_t q = fdiv(i, div_hw);
     const uint32_t c = q - fdiv(q, div_c) * C;
@@ -110,6 +146,10 @@ __global__ __launch_bounds__(kBlock) void bias_act_kernel(const float* __restric
     if (RES) t = __fadd_rn(t, rv);
     if (RELU) t = t < 0.0f ? 0.0f : t;  // torch clamp_min: std::max(t, 0) keeps -0 and NaN
     return t;
+  };
+  auto fq = [&](float t) {
+    float q;
+    return fq1(t, qp, &q);
   };
   if (vec) {
     const uint32_t n4 = n / 4;
@@ -122,11 +162,22 @@ __global__ __launch_bounds__(kBlock) void bias_act_kernel(const float* __restric
       o.y = one(4 * v + 1, a.y, rr.y);
       o.z = one(4 * v + 2, a.z, rr.z);
       o.w = one(4 * v + 3, a.w, rr.w);
-      ((f32x4*)out)[v] = o;
+      if (!QUANT || out) ((f32x4*)out)[v] = o;
+      if (QUANT) {
+        f32x4 r;
+        r.x = fq(o.x);
+        r.y = fq(o.y);
+        r.z = fq(o.z);
+        r.w = fq(o.w);
+        ((f32x4*)yq)[v] = r;
+      }
     }
   } else {
-    for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride)
-      out[i] = one(i, y[i], RES ? res[i] : 0.0f);
+    for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
+      const float t = one(i, y[i], RES ? res[i] : 0.0f);
+      if (!QUANT || out) out[i] = t;
+      if (QUANT) yq[i] = fq(t);
+    }
   }
 }
 
@@ -220,15 +271,10 @@ extern "C" int ssq_lp_loss(const float* pred, const float* tgt, int64_t n, int64
   const int grid = grid_for(n, kBlock * 4, kLossBlocks);
   const float inv_m = 1.0f / (float)M;  // mean backward: 1.0 / numel in fp32
   double* part = loss_out ? (double*)ws : nullptr;
-  if (p == 2.0f)
-    hipLaunchKernelGGL(lp_loss_kernel<0>, dim3(grid), dim3(kBlock), 0, s, pred, tgt, n, p, inv_m,
-                       grad, gscale, relu_mask, part);
-  else if (p == 1.0f)
-    hipLaunchKernelGGL(lp_loss_kernel<1>, dim3(grid), dim3(kBlock), 0, s, pred, tgt, n, p, inv_m,
-                       grad, gscale, relu_mask, part);
-  else
-    hipLaunchKernelGGL(lp_loss_kernel<2>, dim3(grid), dim3(kBlock), 0, s, pred, tgt, n, p, inv_m,
-                       grad, gscale, relu_mask, part);
+  const int vec = ((((uintptr_t)pred) | ((uintptr_t)tgt) | ((uintptr_t)grad)) & 15) == 0;
+  auto k = p == 2.0f ? lp_loss_kernel<0> : (p == 1.0f ? lp_loss_kernel<1> : lp_loss_kernel<2>);
+  hipLaunchKernelGGL(k, dim3(grid), dim3(kBlock), 0, s, pred, tgt, n, p, inv_m, grad, gscale,
+                     relu_mask, vec, part);
   if (loss_out)
     hipLaunchKernelGGL(lp_loss_finalize, dim3(1), dim3(kBlock), 0, s, (const double*)part, grid,
                        (double)M, loss_out);
@@ -260,27 +306,48 @@ extern "C" int ssq_gather_rows2(const float* src0, float* dst0, int64_t row0, co
   return check_launch("ssq_gather_rows2");
 }
 
-extern "C" int ssq_bias_act(const float* y, const float* bias, const float* res, float* out,
-                            int64_t n, int64_t hw, int64_t C, int relu, ssq_stream_t stream) {
-  SSQ_REQUIRE(y && out && n >= 0 && hw >= 1 && C >= 1, SSQ_E_ARG, "ssq_bias_act: bad args");
+static int bias_act(const char* what, const float* y, const float* bias, const float* res,
+                    float* out, float* yq, int64_t n, int64_t hw, int64_t C, int relu,
+                    const float* qdelta, const float* qzp, int qmin, int qmax, hipStream_t s) {
+  SSQ_REQUIRE(y && n >= 0 && hw >= 1 && C >= 1, SSQ_E_ARG, "%s: bad args", what);
+  SSQ_REQUIRE(yq ? (qdelta && qzp && qmin < qmax) : out != nullptr, SSQ_E_ARG, "%s: bad outputs",
+              what);
   SSQ_REQUIRE(n < (1ll << 31) && hw < (1ll << 31) && C < (1ll << 31), SSQ_E_ARG,
-              "ssq_bias_act: tensor exceeds 2^31 elements");
+              "%s: tensor exceeds 2^31 elements", what);
   if (n == 0) return SSQ_OK;
   auto al = [](const void* q) { return ((uintptr_t)q & 15u) == 0; };
-  const int vec = n % 4 == 0 && al(y) && al(out) && (!res || al(res));
+  const int vec = n % 4 == 0 && al(y) && (!out || al(out)) && (!res || al(res)) && (!yq || al(yq));
   const FastDiv dh = make_fastdiv((uint32_t)hw), dc = make_fastdiv((uint32_t)C);
   const dim3 grid(grid_for(vec ? n / 4 : n, kBlock, 2048));
-  hipStream_t s = (hipStream_t)stream;
-#define SSQ_BA(R, A)                                                                      \
-  hipLaunchKernelGGL((bias_act_kernel<R, A>), grid, dim3(kBlock), 0, s, y, bias, res, out, \
-                     (uint32_t)n, dh, dc, (uint32_t)C, vec)
+  const float lo = (float)qmin, hi = (float)qmax;
+#define SSQ_BA(R, A, Q)                                                                       \
+  hipLaunchKernelGGL((bias_act_kernel<R, A, Q>), grid, dim3(kBlock), 0, s, y, bias, res, out,  \
+                     (uint32_t)n, dh, dc, (uint32_t)C, vec, yq, qdelta, qzp, lo, hi)
+#define SSQ_BA2(R, A) \
+  if (yq) SSQ_BA(R, A, true); else SSQ_BA(R, A, false);
   if (res) {
-    if (relu) SSQ_BA(true, true); else SSQ_BA(true, false);
+    if (relu) { SSQ_BA2(true, true) } else { SSQ_BA2(true, false) }
   } else {
-    if (relu) SSQ_BA(false, true); else SSQ_BA(false, false);
+    if (relu) { SSQ_BA2(false, true) } else { SSQ_BA2(false, false) }
   }
+#undef SSQ_BA2
 #undef SSQ_BA
-  return check_launch("ssq_bias_act");
+  return check_launch(what);
+}
+
+extern "C" int ssq_bias_act(const float* y, const float* bias, const float* res, float* out,
+                            int64_t n, int64_t hw, int64_t C, int relu, ssq_stream_t stream) {
+  return bias_act("ssq_bias_act", y, bias, res, out, nullptr, n, hw, C, relu, nullptr, nullptr,
+                  0, 1, (hipStream_t)stream);
+}
+
+extern "C" int ssq_bias_act_fq(const float* y, const float* bias, const float* res, float* out,
+                               float* yq, int64_t n, int64_t hw, int64_t C, int relu,
+                               const float* delta, const float* zp, int qmin, int qmax,
+                               ssq_stream_t stream) {
+  SSQ_REQUIRE(yq, SSQ_E_ARG, "ssq_bias_act_fq: yq is required");
+  return bias_act("ssq_bias_act_fq", y, bias, res, out, yq, n, hw, C, relu, delta, zp, qmin, qmax,
+                  (hipStream_t)stream);
 }
 
 extern "C" int ssq_relu_bwd(const float* g, const float* out, float* gin, int64_t n,

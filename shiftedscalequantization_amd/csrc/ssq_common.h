@@ -180,4 +180,19 @@ __device__ __forceinline__ double block_sum(double v, double* lds /* >= 16 */) {
   return lds[0];
 }
 
+// one element of the uniform affine fake-quant (quant_layer.py:92-98)
+struct QParams {
+  float d, z, lo, hi;
+};
+
+template <bool FAST = false>
+__device__ __forceinline__ float fq1(float x, const QParams& p, float* qout, float r = 0.0f) {
+  // x / delta: IEEE fp32 divide, or its bit-identical reciprocal form (div_fast)
+  float t = FAST ? div_fast(x, p.d, r) : x / p.d;
+  float v = __fadd_rn(rintf(t), p.z);      // round_ste fwd == round half-even, + zp
+  float q = clampf(v, p.lo, p.hi);         // clamp(x_int, lo, hi)
+  *qout = q;
+  return __fmul_rn(__fsub_rn(q, p.z), p.d);  // (x_quant - zp) * delta
+}
+
 }  // namespace ssq

@@ -585,6 +585,77 @@ def bias_act(y, bias=None, res=None, relu=True):
     return out
 
 
+def _epilogue_layout(y, bias, res):
+    y, yp = fptr(y.detach(), "conv output")
+    C = y.shape[1] if y.dim() > 1 else 1
+    hw = y[0, 0].numel() if y.dim() > 2 else 1
+    bp = rp = None
+    if bias is not None:
+        bias, bp = fptr(bias.detach().reshape(-1), "bias")
+        if bias.numel() != C:
+            raise A.SSQError("bias_act: bias must have one value per channel")
+    if res is not None:
+        res, rp = fptr(res.detach(), "residual")
+        if res.shape != y.shape:
+            raise A.SSQError("bias_act: residual shape mismatch")
+    return y, yp, bp, rp, C, hw, (bias, res)
+
+
+class BiasActQuantFn(torch.autograd.Function):
+    """K13 epilogue followed by the per-tensor activation fake-quant, one pass:
+    fq(act((y + bias[c]) + res)) (quant_layer.py:250,270-272; quant_block.py:99-118).
+    The pre-quant activation is written only when a backward will need it.  Backward:
+    the STE / delta / zero-point gradients of FakeQuantFn with the ReLU backward folded
+    into the same pass (ssq_fq_relu_bwd)."""
+
+    @staticmethod
+    def forward(ctx, y, bias, res, delta, zp, relu, n_bits, sym, keep):
+        y, yp, bp, rp, C_, hw, hold = _epilogue_layout(y, bias, res)
+        d, dp = fptr(delta.detach().reshape(-1), "delta")
+        z, zpp = fptr(zp.detach().reshape(-1), "zero_point")
+        if d.numel() != 1 or z.numel() != 1:
+            raise A.SSQError("bias_act_fq: per-tensor activation quantizer only")
+        lo, hi = qrange(n_bits, sym)
+        out = torch.empty_like(y) if keep else None
+        yq = torch.empty_like(y)
+        call("ssq_bias_act_fq", yp, bp, rp, _vp(out), _vp(yq), y.numel(), hw, C_, int(relu), dp,
+             zpp, lo, hi, stream_of(y))
+        ctx.relu, ctx.q = bool(relu), (lo, hi)
+        if keep:
+            ctx.save_for_backward(out, delta, zp)
+        return yq
+
+    @staticmethod
+    def backward(ctx, g):
+        out, delta, zp = ctx.saved_tensors
+        lo, hi = ctx.q
+        g, gp = fptr(g.contiguous(), "grad")
+        d, z = delta.detach().contiguous(), zp.detach().contiguous()
+        need_in = ctx.needs_input_grad[0] or ctx.needs_input_grad[2]
+        gin = torch.empty_like(g) if need_in else None
+        gd = torch.empty(1, dtype=torch.float32, device=g.device) if ctx.needs_input_grad[3] else None
+        gz = torch.empty(1, dtype=torch.float32, device=g.device) if ctx.needs_input_grad[4] else None
+        n = g.numel()
+        ws, wsn = workspace(query("ssq_fq_bwd_workspace_size", n, n, 1), g.device)
+        if ctx.relu:
+            call("ssq_fq_relu_bwd", _vp(out), gp, _vp(d), _vp(z), n, lo, hi, _vp(gin), _vp(gd),
+                 _vp(gz), ws, wsn, stream_of(g))
+        else:
+            call("ssq_fq_bwd", _vp(out), gp, _vp(d), _vp(z), n, n, 1, lo, hi, _vp(gin), _vp(gd),
+                 _vp(gz), ws, wsn, stream_of(g))
+        return (gin if ctx.needs_input_grad[0] else None, None,
+                gin if ctx.needs_input_grad[2] else None,
+                None if gd is None else gd.view(delta.shape),
+                None if gz is None else gz.view(zp.shape), None, None, None, None)
+
+
+def bias_act_quant(y, bias, res, relu, delta, zp, n_bits, sym=False):
+    """bias_act followed by fake_quant(delta, zp) in one pass (per-tensor quantizer)."""
+    keep = torch.is_grad_enabled() and any(
+        t is not None and t.requires_grad for t in (y, res, delta, zp))
+    return BiasActQuantFn.apply(y, bias, res, delta, zp, bool(relu), n_bits, sym, keep)
+
+
 def adam_step(params, grads, exp_avgs, exp_avg_sqs, beta1, beta2, eps, hyper=None,
               neg_step_size=0.0, bc2_sqrt=1.0):
     """One torch.optim.Adam (single-tensor form) step for every tensor, one launch.

@@ -9,7 +9,7 @@ import torch.nn as nn
 
 from .. import kernels as K
 from .. import nets
-from .quant_layer import QuantModule, StraightThrough, UniformAffineQuantizer
+from .quant_layer import QuantModule, StraightThrough, UniformAffineQuantizer, fusable_act_quantizer
 
 
 class BaseQuantBlock(nn.Module):
@@ -83,7 +83,12 @@ class BaseQuantBlock(nn.Module):
                 and (last.disable_act_quant or not last.use_act_quant)
                 and last.epilogue_fusable(inp)):
             raw, bias = last.forward_raw(inp)
-            out = K.bias_act(raw, bias, residual, isinstance(self.activation_function, nn.ReLU))
+            relu = isinstance(self.activation_function, nn.ReLU)
+            q = fusable_act_quantizer(self.act_quantizer, self.use_act_quant)
+            if q is not None:   # + the block's act quant in the same pass
+                return K.bias_act_quant(raw, bias, residual, relu, q.delta, q.zero_point,
+                                        q.n_bits, q.sym)
+            out = K.bias_act(raw, bias, residual, relu)
             if self.use_act_quant:
                 out = self.act_quantizer(out)
             return out

@@ -107,6 +107,19 @@ class UniformAffineQuantizer(nn.Module):
         return s.format(**self.__dict__)
 
 
+def fusable_act_quantizer(q, active):
+    """The act quantizer `q` if its per-tensor q/dq can run inside the K13 epilogue pass
+    (an initialised plain UniformAffineQuantizer with scalar delta/zp and no hooks), else
+    None."""
+    if not active or type(q) is not UniformAffineQuantizer or not q.inited:
+        return None
+    if q.delta is None or q.delta.numel() != 1 or q.zero_point.numel() != 1:
+        return None
+    if q._forward_hooks or q._forward_pre_hooks or not q.delta.is_cuda:
+        return None
+    return q
+
+
 class QuantModule(nn.Module):
     """quant_layer.py:188-280: a Conv2d / Linear whose weight goes through
     `weight_quantizer` (any module: UAQ, ChannelQuant, AdaRoundQuantizer, ...), followed by
@@ -229,10 +242,16 @@ class QuantModule(nn.Module):
     def forward(self, input: torch.Tensor):
         if self.cache_features == 'if':
             self.cached_inp_features += [self._cache(input)]
+        act_q = self.use_act_quant and not self.disable_act_quant
         if self.epilogue_fusable(input):
             out, bias = self.forward_raw(input)
             relu = isinstance(self.activation_function, nn.ReLU)
-            if bias is not None or relu:
+            q = fusable_act_quantizer(self.act_quantizer, act_q)
+            if q is not None:
+                out = K.bias_act_quant(out, bias, None, relu, q.delta, q.zero_point, q.n_bits,
+                                       q.sym)
+                act_q = False
+            elif bias is not None or relu:
                 out = K.bias_act(out, bias, None, relu)
         else:
             weight, bias = self._weight_bias()
@@ -242,9 +261,8 @@ class QuantModule(nn.Module):
             if self.se_module is not None:
                 out = self.se_module(out)
             out = self.activation_function(out)
-        if not self.disable_act_quant:
-            if self.use_act_quant:
-                out = self.act_quantizer(out)
+        if act_q:
+            out = self.act_quantizer(out)
         if self.cache_features == 'of':
             self.cached_out_features += [self._cache(out)]
         return out

@@ -447,9 +447,11 @@ def test_bias_act_matches_eager_ops(K, shape, res, relu):
         np.testing.assert_array_equal(host(rr.grad), host(re_.grad))
 
 
-def test_quant_block_fused_epilogue_matches_unfused(K):
+@pytest.mark.parametrize("act", [False, True])
+def test_quant_block_fused_epilogue_matches_unfused(K, act):
     """A QuantBasicBlock forward/backward through the fused epilogue equals the eager
-    path (fusion disabled) bit for bit."""
+    path (fusion disabled) bit for bit; with act quant on, the act q/dq runs inside the
+    epilogue pass and the act-delta gradients match too."""
     from shiftedscalequantization_amd import nets, quant as Q
     torch.manual_seed(3)
     ds = torch.nn.Sequential(torch.nn.Conv2d(16, 32, 1, stride=2, bias=False), torch.nn.BatchNorm2d(32))
@@ -457,26 +459,47 @@ def test_quant_block_fused_epilogue_matches_unfused(K):
     qnn = Q.QuantModel(torch.nn.Sequential(blk), {"n_bits": 4, "channel_wise": True, "scale_method": "max"},
                        {"n_bits": 8, "channel_wise": False, "scale_method": "max"}).cuda()
     qb = qnn.model[0]
-    qnn.set_quant_state(True, False)
+    qnn.set_quant_state(True, act)
     x = torch.randn(4, 16, 14, 14).cuda()
     with torch.no_grad():
         qnn(x)                                       # init the quantizers
+    _compare_fused_unfused(qb, x, act)
+
+
+def _act_deltas(qb):
+    from shiftedscalequantization_amd import quant as Q
+    ds = [qb.act_quantizer.delta]
+    ds += [m.act_quantizer.delta for m in qb.modules()
+           if isinstance(m, Q.QuantModule) and not m.disable_act_quant]
+    return [d for d in ds if d is not None]
+
+
+def _compare_fused_unfused(qb, x, act):
+    from shiftedscalequantization_amd import quant as Q
     outs = []
+    g = torch.randn(1, generator=torch.Generator().manual_seed(1))
     for fuse in (True, False):
         if not fuse:
             for m in qb.modules():
                 if isinstance(m, Q.QuantModule):
                     m.epilogue_fusable = lambda inp: False
+        for d in _act_deltas(qb):
+            d.grad = None
         xx = x.clone().requires_grad_(True)
         y = qb(xx)
-        y.backward(torch.ones_like(y))
-        outs.append((host(y), host(xx.grad)))
+        gy = torch.linspace(-1, 1, y.numel(), device=y.device).view_as(y) + g.item()
+        y.backward(gy)
+        outs.append((host(y), host(xx.grad), [host(d.grad) for d in _act_deltas(qb)] if act else []))
     np.testing.assert_array_equal(outs[0][0], outs[1][0])
     np.testing.assert_array_equal(outs[0][1], outs[1][1])
+    assert len(outs[0][2]) == len(outs[1][2])
+    for a, b in zip(outs[0][2], outs[1][2]):
+        np.testing.assert_array_equal(a, b)
 
 
+@pytest.mark.parametrize("act", [False, True])
 @pytest.mark.parametrize("kind", ["bottleneck", "resbottleneck", "inverted"])
-def test_other_blocks_fused_epilogue_matches_unfused(K, kind):
+def test_other_blocks_fused_epilogue_matches_unfused(K, kind, act):
     """ResNet-50 / RegNetX / MobileNetV2 blocks: the fused conv-bias + residual (+ReLU)
     tail equals the eager ops bit for bit, forward and backward."""
     import torch.nn as nn
@@ -493,22 +516,46 @@ def test_other_blocks_fused_epilogue_matches_unfused(K, kind):
                        {"n_bits": 8, "channel_wise": False, "scale_method": "max"}).cuda()
     qb = qnn.model[0]
     assert isinstance(qb, Q.BaseQuantBlock)
-    qnn.set_quant_state(True, False)
+    qnn.set_quant_state(True, act)
     x = torch.randn(4, cin, 14, 14).cuda()
     with torch.no_grad():
         qnn(x)
-    outs = []
-    for fuse in (True, False):
-        if not fuse:
-            for m in qb.modules():
-                if isinstance(m, Q.QuantModule):
-                    m.epilogue_fusable = lambda inp: False
-        xx = x.clone().requires_grad_(True)
-        y = qb(xx)
-        y.backward(torch.ones_like(y))
-        outs.append((host(y), host(xx.grad)))
-    np.testing.assert_array_equal(outs[0][0], outs[1][0])
-    np.testing.assert_array_equal(outs[0][1], outs[1][1])
+    _compare_fused_unfused(qb, x, act)
+
+
+@pytest.mark.parametrize("shape", [(4, 8, 7, 7), (2, 3, 5, 3), (32, 64, 56, 56)])
+@pytest.mark.parametrize("res", [False, True])
+@pytest.mark.parametrize("relu", [False, True])
+def test_bias_act_quant_matches_composed(K, shape, res, relu):
+    """K13 + act q/dq in one pass == bias_act then fake_quant, bit for bit: the output,
+    and the gradients of y, the residual, delta and zero_point (ReLU backward folded into
+    the STE pass)."""
+    gen = torch.Generator().manual_seed(sum(shape) + 7 * res + relu)
+    y = torch.randn(shape, generator=gen).cuda()
+    y.view(-1)[:3] = torch.tensor([-0.0, float("nan"), 0.0])
+    b = torch.randn(shape[1], generator=gen).cuda()
+    r = torch.randn(shape, generator=gen).cuda() if res else None
+    d = torch.tensor(0.21).cuda()
+    z = torch.tensor(3.0).cuda()
+    g = torch.randn(shape, generator=gen).cuda()
+    with torch.no_grad():
+        a = K.bias_act_quant(y, b, r, relu, d, z, 4)
+    results = []
+    for fused in (True, False):
+        yy = y.clone().requires_grad_(True)
+        rr = r.clone().requires_grad_(True) if res else None
+        dd = d.clone().requires_grad_(True)
+        zz = z.clone().requires_grad_(True)
+        if fused:
+            o = K.bias_act_quant(yy, b, rr, relu, dd, zz, 4)
+        else:
+            o = K.fake_quant(K.bias_act(yy, b, rr, relu), dd, zz, 4)
+        o.backward(g)
+        results.append([host(o), host(yy.grad), host(dd.grad), host(zz.grad)]
+                       + ([host(rr.grad)] if res else []))
+    np.testing.assert_array_equal(host(a).view(np.int32), results[0][0].view(np.int32))
+    for u, v in zip(*results):
+        np.testing.assert_array_equal(np.asarray(u).view(np.int32), np.asarray(v).view(np.int32))
 
 
 def test_lp_loss_relu_mask_folds_relu_backward(K):
