@@ -249,6 +249,25 @@ int ssq_adam(int nseg, float* const* p, const float* const* g, float* const* m,
              float one_minus_beta2, float eps, const float* hyper, float neg_step_size,
              float bias_correction2_sqrt, ssq_stream_t stream);
 
+/* ---------------------------------------------------------------- K15/K16 packed export
+ * Low-bit weight export (replaces the fp32 state_dict + pickled shift
+ * choice of main_cifar10.py:86 / myScaledMethods.py:204-205).  A hard weight quantizer's
+ * output is W_hat = ((q - zp[co]) * d1) (* d2[j]) with d1 per co (d1_per_ci = 0) or per
+ * (co, ci) (= 1) and the optional column scale d2 (ChannelQuantMSE's inp_scale, j in
+ * [0, Ci*K)).  Codes are stored as q - qmin in ssq_pack_bits(n_bits) = 2 / 4 / 8 bits each,
+ * little-endian, ssq_pack_bytes(n, n_bits) bytes for n codes.
+ * ssq_pack_encode recovers q from W_hat and ADDS to *mismatch (device u32, caller-zeroed)
+ * the number of elements whose decode is not bit-identical to W_hat (0 = exact export).
+ * ssq_pack_decode writes W_hat back.  Co*Ci*K < 2^31.                                    */
+int ssq_pack_bits(int n_bits);
+size_t ssq_pack_bytes(int64_t n, int n_bits);
+int ssq_pack_encode(const float* What, const float* zp, const float* d1, int d1_per_ci,
+                    const float* d2, int64_t Co, int64_t Ci, int64_t K, int n_bits, int qmin,
+                    int qmax, void* packed, uint32_t* mismatch, ssq_stream_t stream);
+int ssq_pack_decode(const void* packed, const float* zp, const float* d1, int d1_per_ci,
+                    const float* d2, int64_t Co, int64_t Ci, int64_t K, int n_bits, int qmin,
+                    float* What, ssq_stream_t stream);
+
 /* ---------------------------------------------------------------- bandwidth probe
  * float4 device copy, used by bench.py to report the measured stream bandwidth.      */
 int ssq_stream_copy(const float* src, float* dst, int64_t n, ssq_stream_t stream);

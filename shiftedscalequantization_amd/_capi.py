@@ -59,6 +59,10 @@ SIGNATURES = {
     "ssq_relu_bwd": (_i, [_p, _p, _p, _i64, _p]),
     "ssq_bias_act_fq": (_i, [_p, _p, _p, _p, _p, _i64, _i64, _i64, _i, _p, _p, _i, _i, _p]),
     "ssq_adam": (_i, [_i, _p, _p, _p, _p, _p, _f, _f, _f, _f, _p, _f, _f, _p]),
+    "ssq_pack_bits": (_i, [_i]),
+    "ssq_pack_bytes": (_sz, [_i64, _i]),
+    "ssq_pack_encode": (_i, [_p, _p, _p, _i, _p, _i64, _i64, _i64, _i, _i, _i, _p, _p, _p]),
+    "ssq_pack_decode": (_i, [_p, _p, _p, _i, _p, _i64, _i64, _i64, _i, _i, _p, _p]),
     "ssq_stream_copy": (_i, [_p, _p, _i64, _p]),
 }
 

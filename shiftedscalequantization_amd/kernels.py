@@ -681,3 +681,40 @@ def stream_copy(src, dst):
 
 def set_variant(v):
     return query("ssq_set_variant", int(v))
+
+
+# ------------------------------------------------------------------ K15/K16 packed export
+def pack_encode(what, zp, d1, per_ci, d2, n_bits, qmin, qmax):
+    """Hard W_hat -> (packed codes as a uint8 tensor, number of elements whose decode is not
+    bit-identical; 0 = exact).  W_hat = ((q - zp[co]) * d1) (* d2[j])."""
+    w, wp = fptr(what.detach(), "W_hat")
+    Co, Ci, Kk, _ = geometry(w)
+    z, zpp = fptr(zp.detach().reshape(-1), "zero_point")
+    a, ap = fptr(d1.detach().reshape(-1), "scale")
+    b, bp = fptr(d2.detach().reshape(-1), "col_scale") if d2 is not None else (None, None)
+    if z.numel() != Co or a.numel() != (Co * Ci if per_ci else Co) or \
+            (b is not None and b.numel() != Ci * Kk):
+        raise A.SSQError("pack_encode: zp / scale / col_scale sizes do not match the weight")
+    nbytes = query("ssq_pack_bytes", w.numel(), n_bits)
+    packed = torch.empty(max(nbytes, 1), dtype=torch.uint8, device=w.device)[:nbytes]
+    bad = torch.zeros(1, dtype=torch.int32, device=w.device)
+    call("ssq_pack_encode", wp, zpp, ap, int(per_ci), bp, Co, Ci, Kk, n_bits, qmin, qmax,
+         _vp(packed), _vp(bad), stream_of(w))
+    return packed, int(bad.item())
+
+
+def pack_decode(packed, shape, zp, d1, per_ci, d2, n_bits, qmin):
+    """Packed codes -> W_hat (fp32, `shape`)."""
+    if packed.device.type != "cuda" or packed.dtype != torch.uint8:
+        raise A.SSQError("pack_decode: packed codes must be a uint8 tensor on the HIP device")
+    out = torch.empty(shape, dtype=torch.float32, device=packed.device)
+    Co, Ci, Kk, _ = geometry(out)
+    if packed.numel() < query("ssq_pack_bytes", out.numel(), n_bits):
+        raise A.SSQError("pack_decode: packed buffer too small for the shape")
+    packed = packed.contiguous()
+    z, zpp = fptr(zp.reshape(-1), "zero_point")
+    a, ap = fptr(d1.reshape(-1), "scale")
+    b, bp = fptr(d2.reshape(-1), "col_scale") if d2 is not None else (None, None)
+    call("ssq_pack_decode", _vp(packed), zpp, ap, int(per_ci), bp, Co, Ci, Kk, n_bits, qmin,
+         _vp(out), stream_of(out))
+    return out

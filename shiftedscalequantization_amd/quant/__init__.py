@@ -17,3 +17,4 @@ from .layer_recon_shiftedScale import (LinearTempDecayShift, ScaleLossBlockFunct
                                        ScaleLossFunction, block_recon_shiftedScale,
                                        layer_recon_shiftedScale)
 from .data_utils import save_inp_oup_data, save_grad_data
+from .export import PackedWeight, dequant_form, export_quantized, load_quantized
