@@ -212,6 +212,15 @@ int ssq_lp_loss(const float* pred, const float* tgt, int64_t n, int64_t M, float
                 float* loss_out, float* grad, const float* gscale, int relu_mask, void* ws,
                 size_t ws_bytes, ssq_stream_t stream);
 
+/* ssq_lp_loss with the target rows read straight from the cached outputs: target element
+ * i is tgt_cache[idx[i / row] * row + i % row] (the loop's cached_outs[idx] batch,
+ * layer_recon_fused_shiftedScale.py:95-97, without materialising it).  n % row == 0,
+ * n < 2^31.  Same values as ssq_gather_rows2 + ssq_lp_loss.                             */
+int ssq_lp_loss_rows(const float* pred, const float* tgt_cache, const int64_t* idx, int64_t row,
+                     int64_t n, int64_t M, float p, float* loss_out, float* grad,
+                     const float* gscale, int relu_mask, void* ws, size_t ws_bytes,
+                     ssq_stream_t stream);
+
 /* ---------------------------------------------------------------- K14 batch gather
  * dst_k[r] = src_k[idx[r]] for two sources at once (cached block input and output,
  * layer_recon_fused_shiftedScale.py:95-97). src1/dst1 may be NULL.                    */

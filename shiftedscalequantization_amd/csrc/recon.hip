@@ -47,14 +47,31 @@ __device__ __forceinline__ float lp_elem(float x, float t, float p, float inv_m,
   return (relu_mask && x <= 0.0f) ? 0.0f : gv;
 }
 
-// float4 body over the first n & ~3 elements (when aligned), scalar tail; one double partial per block.
-template <int PMODE>
+// Target rows: tgt itself, or (GATHER) rows idx[r] of a [N, row] cache, r = i / row, so the
+// loop's batch target is never materialised.
+struct TgtRows {
+  const int64_t* idx;
+  uint32_t row;
+  FastDiv div_row;
+};
+
+template <bool GATHER>
+__device__ __forceinline__ int64_t tgt_index(uint32_t i, const TgtRows& tr) {
+  if (!GATHER) return i;
+  const uint32_t r = fdiv(i, tr.div_row);
+  return tr.idx[r] * (int64_t)tr.row + (i - r * tr.row);
+}
+
+// float4 body over the first n & ~3 elements (when aligned), scalar tail; one double
+// partial per block.  GATHER: tr is in float4 units in the body, in elements in the tail.
+template <int PMODE, bool GATHER>
 __global__ __launch_bounds__(kBlock) void lp_loss_kernel(const float* __restrict__ pred,
                                                          const float* __restrict__ tgt, int64_t n,
                                                          float p, float inv_m,
                                                          float* __restrict__ grad,
                                                          const float* __restrict__ gscale,
-                                                         int relu_mask, int vec,
+                                                         int relu_mask, int vec, TgtRows tr4,
+                                                         TgtRows tr1,
                                                          double* __restrict__ part) {
   __shared__ double red[16];
   double acc = 0.0;
@@ -66,7 +83,8 @@ __global__ __launch_bounds__(kBlock) void lp_loss_kernel(const float* __restrict
   const f32x4* T = (const f32x4*)tgt;
   f32x4* G = (f32x4*)grad;
   for (int64_t i = tid; i < n4; i += stride) {
-    const f32x4 x = __builtin_nontemporal_load(P + i), t = __builtin_nontemporal_load(T + i);
+    const f32x4 x = __builtin_nontemporal_load(P + i);
+    const f32x4 t = __builtin_nontemporal_load(T + tgt_index<GATHER>((uint32_t)i, tr4));
     f32x4 g;
     g.x = lp_elem<PMODE>(x.x, t.x, p, inv_m, gs, relu_mask, acc);
     g.y = lp_elem<PMODE>(x.y, t.y, p, inv_m, gs, relu_mask, acc);
@@ -75,7 +93,8 @@ __global__ __launch_bounds__(kBlock) void lp_loss_kernel(const float* __restrict
     if (grad) __builtin_nontemporal_store(g, G + i);
   }
   for (int64_t i = (n4 << 2) + tid; i < n; i += stride) {
-    const float g = lp_elem<PMODE>(pred[i], tgt[i], p, inv_m, gs, relu_mask, acc);
+    const float g = lp_elem<PMODE>(pred[i], tgt[tgt_index<GATHER>((uint32_t)i, tr1)], p, inv_m, gs,
+                                   relu_mask, acc);
     if (grad) grad[i] = g;
   }
   if (!part) return;
@@ -260,25 +279,52 @@ extern "C" size_t ssq_lp_loss_workspace_size(int64_t n) {
   return kLossBlocks * sizeof(double);
 }
 
-extern "C" int ssq_lp_loss(const float* pred, const float* tgt, int64_t n, int64_t M, float p,
-                           float* loss_out, float* grad, const float* gscale, int relu_mask,
-                           void* ws, size_t ws_bytes, ssq_stream_t stream) {
-  SSQ_REQUIRE(pred && tgt && n >= 1 && M >= 1 && (loss_out || grad), SSQ_E_ARG,
-              "ssq_lp_loss: bad args");
+static int lp_loss(const char* what, const float* pred, const float* tgt, const int64_t* idx,
+                   int64_t row, int64_t n, int64_t M, float p, float* loss_out, float* grad,
+                   const float* gscale, int relu_mask, void* ws, size_t ws_bytes, hipStream_t s) {
+  SSQ_REQUIRE(pred && tgt && n >= 1 && M >= 1 && (loss_out || grad), SSQ_E_ARG, "%s: bad args",
+              what);
   SSQ_REQUIRE(!loss_out || (ws && ws_bytes >= ssq_lp_loss_workspace_size(n)), SSQ_E_WS,
-              "ssq_lp_loss: workspace too small");
-  hipStream_t s = (hipStream_t)stream;
+              "%s: workspace too small", what);
+  const bool gather = idx != nullptr;
+  SSQ_REQUIRE(!gather || (row >= 1 && n % row == 0 && n < (1ll << 31)), SSQ_E_ARG,
+              "%s: n must be a whole number of target rows (< 2^31 elements)", what);
   const int grid = grid_for(n, kBlock * 4, kLossBlocks);
   const float inv_m = 1.0f / (float)M;  // mean backward: 1.0 / numel in fp32
   double* part = loss_out ? (double*)ws : nullptr;
-  const int vec = ((((uintptr_t)pred) | ((uintptr_t)tgt) | ((uintptr_t)grad)) & 15) == 0;
-  auto k = p == 2.0f ? lp_loss_kernel<0> : (p == 1.0f ? lp_loss_kernel<1> : lp_loss_kernel<2>);
+  int vec = ((((uintptr_t)pred) | ((uintptr_t)tgt) | ((uintptr_t)grad)) & 15) == 0;
+  if (gather && row % 4 != 0) vec = 0;  // float4s must not straddle target rows
+  TgtRows tr4{idx, 1, make_fastdiv(1)}, tr1 = tr4;
+  if (gather) {
+    tr1 = TgtRows{idx, (uint32_t)row, make_fastdiv((uint32_t)row)};
+    if (vec) tr4 = TgtRows{idx, (uint32_t)(row / 4), make_fastdiv((uint32_t)(row / 4))};
+  }
+  auto k = gather ? (p == 2.0f ? lp_loss_kernel<0, true>
+                               : (p == 1.0f ? lp_loss_kernel<1, true> : lp_loss_kernel<2, true>))
+                  : (p == 2.0f ? lp_loss_kernel<0, false>
+                               : (p == 1.0f ? lp_loss_kernel<1, false> : lp_loss_kernel<2, false>));
   hipLaunchKernelGGL(k, dim3(grid), dim3(kBlock), 0, s, pred, tgt, n, p, inv_m, grad, gscale,
-                     relu_mask, vec, part);
+                     relu_mask, vec, tr4, tr1, part);
   if (loss_out)
     hipLaunchKernelGGL(lp_loss_finalize, dim3(1), dim3(kBlock), 0, s, (const double*)part, grid,
                        (double)M, loss_out);
-  return check_launch("ssq_lp_loss");
+  return check_launch(what);
+}
+
+extern "C" int ssq_lp_loss(const float* pred, const float* tgt, int64_t n, int64_t M, float p,
+                           float* loss_out, float* grad, const float* gscale, int relu_mask,
+                           void* ws, size_t ws_bytes, ssq_stream_t stream) {
+  return lp_loss("ssq_lp_loss", pred, tgt, nullptr, 0, n, M, p, loss_out, grad, gscale,
+                 relu_mask, ws, ws_bytes, (hipStream_t)stream);
+}
+
+extern "C" int ssq_lp_loss_rows(const float* pred, const float* tgt_cache, const int64_t* idx,
+                                int64_t row, int64_t n, int64_t M, float p, float* loss_out,
+                                float* grad, const float* gscale, int relu_mask, void* ws,
+                                size_t ws_bytes, ssq_stream_t stream) {
+  SSQ_REQUIRE(idx, SSQ_E_ARG, "ssq_lp_loss_rows: idx is required");
+  return lp_loss("ssq_lp_loss_rows", pred, tgt_cache, idx, row, n, M, p, loss_out, grad, gscale,
+                 relu_mask, ws, ws_bytes, (hipStream_t)stream);
 }
 
 extern "C" int ssq_gather_rows2(const float* src0, float* dst0, int64_t row0, const float* src1,

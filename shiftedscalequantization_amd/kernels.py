@@ -476,16 +476,39 @@ def _lp_M(pred, reduction):
     return pred.numel()
 
 
+class Rows:
+    """cache[idx] as a lazy target: the loss pass reads the rows in place
+    (ssq_lp_loss_rows) instead of a gathered copy."""
+
+    def __init__(self, cache, idx):
+        self.cache, self.idx = cache, idx
+
+    def materialize(self):
+        return gather_rows2(self.cache, self.idx)[0]
+
+
 def lp_loss_and_grad(pred, tgt, p=2.0, reduction="none", want_grad=True, loss_out=None,
                      relu_mask=False):
     """lp_loss value (1-element device tensor) and d/d pred in one fused pass.  With
-    relu_mask, pred is a ReLU output and the gradient is returned at the ReLU's input."""
+    relu_mask, pred is a ReLU output and the gradient is returned at the ReLU's input.
+    tgt may be a Rows(cache, idx) target."""
     pred, pp = fptr(pred.detach(), "pred")
-    tgt, tp = fptr(tgt.detach(), "tgt")
     loss = torch.empty(1, dtype=torch.float32, device=pred.device) if loss_out is None else loss_out
     grad = torch.empty_like(pred) if want_grad else None
     ws, wsn = workspace(query("ssq_lp_loss_workspace_size", pred.numel()), pred.device)
-    call("ssq_lp_loss", pp, tp, pred.numel(), _lp_M(pred, reduction), float(p), _vp(loss),
+    M = _lp_M(pred, reduction)
+    if isinstance(tgt, Rows):
+        cache, cp = fptr(tgt.cache.detach(), "tgt cache")
+        idx = tgt.idx
+        row = cache[0].numel()
+        if idx.dtype != torch.int64 or idx.device != pred.device or \
+                idx.numel() * row != pred.numel() or tuple(cache.shape[1:]) != tuple(pred.shape[1:]):
+            raise A.SSQError("lp_loss: Rows target does not match pred")
+        call("ssq_lp_loss_rows", pp, cp, _vp(idx), row, pred.numel(), M, float(p), _vp(loss),
+             _vp(grad), None, int(bool(relu_mask)), ws, wsn, stream_of(pred))
+        return loss, grad
+    tgt, tp = fptr(tgt.detach(), "tgt")
+    call("ssq_lp_loss", pp, tp, pred.numel(), M, float(p), _vp(loss),
          _vp(grad), None, int(bool(relu_mask)), ws, wsn, stream_of(pred))
     return loss, grad
 

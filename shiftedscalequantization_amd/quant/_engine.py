@@ -61,6 +61,12 @@ class BatchFeeder:
         K.gather_rows2(self.inp, self.didx, self.out, out0=self.cur_inp, out1=self.cur_out)
         return self.cur_inp, self.cur_out
 
+    def gather_lazy(self):
+        """The batch input gathered (the conv needs it contiguous); the batch target as a
+        K.Rows view that the loss pass reads in place."""
+        K.gather_rows2(self.inp, self.didx, out0=self.cur_inp)
+        return self.cur_inp, K.Rows(self.out, self.didx)
+
     def next(self, perm=None):
         self.stage(self.draw() if perm is None else perm)
         return self.gather()

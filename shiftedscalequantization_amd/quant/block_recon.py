@@ -135,7 +135,7 @@ def _fast_loop(block, qmodules, opt_params, loss_func, feeder, bucket, iters, ac
     last = {}
 
     def body():
-        cur_inp, cur_out = feeder.gather()
+        cur_inp, cur_out = feeder.gather_lazy()
         out = block(cur_inp)
         relu_in = getattr(out, '_ssq_relu_inputs', None)
         if not out.requires_grad:

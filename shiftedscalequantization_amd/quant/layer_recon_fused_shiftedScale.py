@@ -87,7 +87,7 @@ def _fused_loop(block, modules, iters, lmda, model, p, lr, bias_cal, batch_size,
     def body():
         """One iteration on the device: gather -> forward -> fused loss+grad -> backward
         (+ RCCL bucket) -> Adam.  No host sync, no host-side state: graph-capturable."""
-        cur_inp, cur_out = feeder.gather()
+        cur_inp, cur_out = feeder.gather_lazy()
         quant_out = block(cur_inp)
         relu_in = getattr(quant_out, '_ssq_relu_inputs', None)
         if relu_in:

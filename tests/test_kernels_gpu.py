@@ -634,3 +634,20 @@ def test_inpscale_search_binary_search_equals_scan(K, level, threshold):
     ref = R.inpscale_search(w.numpy(), d.reshape(-1, 1, 1, 1), raw.reshape(-1, 1, 1, 1), 2, level,
                             threshold)
     np.testing.assert_array_equal(host(inp), ref)
+
+
+@pytest.mark.parametrize("row_shape", [(16, 7, 7), (3, 5, 3), (64, 14, 14)])
+@pytest.mark.parametrize("p", [2.0, 2.4, 1.0])
+def test_lp_loss_rows_equals_gathered(K, row_shape, p):
+    """Loss pass reading cache[idx] in place (ssq_lp_loss_rows) == gather + ssq_lp_loss,
+    bit for bit (value and gradient, with and without the ReLU mask)."""
+    gen = torch.Generator().manual_seed(len(row_shape) + int(p * 10))
+    cache = torch.randn((40,) + row_shape, generator=gen).cuda()
+    idx = torch.randperm(40, generator=gen)[:8].cuda()
+    pred = torch.relu(torch.randn((8,) + row_shape, generator=gen)).cuda()
+    tgt = K.gather_rows2(cache, idx)[0]
+    for relu_mask in (False, True):
+        l1, g1 = K.lp_loss_and_grad(pred, tgt, p, relu_mask=relu_mask)
+        l2, g2 = K.lp_loss_and_grad(pred, K.Rows(cache, idx), p, relu_mask=relu_mask)
+        assert host(l1).tobytes() == host(l2).tobytes()
+        np.testing.assert_array_equal(host(g1).view(np.int32), host(g2).view(np.int32))

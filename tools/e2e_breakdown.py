@@ -3,6 +3,7 @@
 timed with a device synchronize on both sides.  Arguments are main_imagenet.py's.
 Prints one line per call and a per-kind summary."""
 import collections
+import importlib
 import functools
 import os
 import sys
@@ -15,8 +16,8 @@ import main_imagenet  # noqa: E402
 from shiftedscalequantization_amd import drivers as D  # noqa: E402
 from shiftedscalequantization_amd.quant import block_recon as BR  # noqa: E402
 from shiftedscalequantization_amd.quant import data_utils as DU  # noqa: E402
-from shiftedscalequantization_amd.quant import layer_recon_fused_shiftedScale as LF  # noqa: E402
 
+LF = importlib.import_module("shiftedscalequantization_amd.quant.layer_recon_fused_shiftedScale")
 tot = collections.defaultdict(float)
 cnt = collections.Counter()
 
