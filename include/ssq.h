@@ -258,6 +258,20 @@ int ssq_adam(int nseg, float* const* p, const float* const* g, float* const* m,
              float one_minus_beta2, float eps, const float* hyper, float neg_step_size,
              float bias_correction2_sqrt, ssq_stream_t stream);
 
+/* ---------------------------------------------------------------- K17 conv weight gradient
+ * Deterministic fp32 conv weight gradient (NCHW, dilation 1) on the fp32 matrix cores:
+ *   dw[co, ci, r, s] = sum_{n,oh,ow} dy[n, co, oh, ow] * x[n, g*Cig + ci, oh*st + r - pad,
+ *                                                          ow*st + s - pad]
+ * (the autograd of the reconstruction loops' F.conv2d weight, quant_layer.py:250, under
+ * the reference's cudnn.deterministic = True, common.py:77-85).  Split-K partials in ws,
+ * summed in a fixed order: bit-identical run to run.  OW <= 128, tensors < 2^31 elements. */
+size_t ssq_conv_wgrad_workspace_size(int64_t Nb, int64_t C, int64_t H, int64_t W, int64_t Co,
+                                     int64_t R, int64_t S, int64_t stride, int64_t pad,
+                                     int64_t groups);
+int ssq_conv_wgrad(const float* x, const float* dy, int64_t Nb, int64_t C, int64_t H, int64_t W,
+                   int64_t Co, int64_t R, int64_t S, int64_t stride, int64_t pad, int64_t groups,
+                   float* dw, void* ws, size_t ws_bytes, ssq_stream_t stream);
+
 /* ---------------------------------------------------------------- K15/K16 packed export
  * Low-bit weight export (replaces the fp32 state_dict + pickled shift
  * choice of main_cifar10.py:86 / myScaledMethods.py:204-205).  A hard weight quantizer's

@@ -741,3 +741,87 @@ def pack_decode(packed, shape, zp, d1, per_ci, d2, n_bits, qmin):
     call("ssq_pack_decode", _vp(packed), zpp, ap, int(per_ci), bp, Co, Ci, Kk, n_bits, qmin,
          _vp(out), stream_of(out))
     return out
+
+
+# ------------------------------------------------------------------ K17 conv weight gradient
+def conv_wgrad_supported(x, weight, stride, padding, dilation, groups):
+    """Shapes ssq_conv_wgrad handles: 4-D fp32 NCHW on the device, square stride /
+    padding, dilation 1, output width <= 128."""
+    if x.dim() != 4 or weight.dim() != 4 or not x.is_cuda or x.dtype != torch.float32:
+        return False
+    st = stride if isinstance(stride, int) else stride[0]
+    pad = padding if isinstance(padding, int) else padding[0]
+    if not isinstance(stride, int) and len(set(stride)) != 1:
+        return False
+    if not isinstance(padding, int) and (isinstance(padding, str) or len(set(padding)) != 1):
+        return False
+    if (dilation if isinstance(dilation, int) else max(dilation)) != 1:
+        return False
+    ow = (x.shape[3] + 2 * pad - weight.shape[3]) // st + 1
+    return 1 <= ow <= 128
+
+
+def conv_wgrad(x, dy, w_shape, stride, padding, groups):
+    """d loss / d weight of F.conv2d(x, w, stride, padding, groups) given dy (K17)."""
+    st = stride if isinstance(stride, int) else stride[0]
+    pad = padding if isinstance(padding, int) else padding[0]
+    x, xp = fptr(x.detach(), "x")
+    dy, dp = fptr(dy.detach(), "dy")
+    Nb, C, H, W = (int(v) for v in x.shape)
+    Co, _, R, S = (int(v) for v in w_shape)
+    dims = (Nb, C, H, W, Co, R, S, int(st), int(pad), int(groups))
+    ws, wsn = workspace(query("ssq_conv_wgrad_workspace_size", *dims), x.device)
+    dw = torch.empty(tuple(w_shape), dtype=torch.float32, device=x.device)
+    call("ssq_conv_wgrad", xp, dp, *dims, _vp(dw), ws, wsn, stream_of(x))
+    return dw
+
+
+class Conv2dFn(torch.autograd.Function):
+    """F.conv2d whose weight gradient runs on K17 (deterministic, MFMA); the forward and
+    the input gradient stay on MIOpen."""
+
+    @staticmethod
+    def forward(ctx, x, weight, stride, padding, dilation, groups):
+        ctx.save_for_backward(x, weight)
+        ctx.cfg = (stride, padding, dilation, groups)
+        return torch.nn.functional.conv2d(x, weight, None, stride, padding, dilation, groups)
+
+    @staticmethod
+    def backward(ctx, g):
+        x, weight = ctx.saved_tensors
+        stride, padding, dilation, groups = ctx.cfg
+        g = g.contiguous()
+        gx = gw = None
+        if ctx.needs_input_grad[0]:
+            gx = torch.nn.grad.conv2d_input(x.shape, weight, g, stride, padding, dilation, groups)
+        if ctx.needs_input_grad[1]:
+            gw = conv_wgrad(x, g, weight.shape, stride, padding, groups)
+        return gx, gw, None, None, None, None
+
+
+# When the conv weight gradient runs on K17: 'deterministic' = whenever the reference's
+# torch.backends.cudnn.deterministic is set and the output plane has >= 400 pixels (there
+# MIOpen's deterministic weight-gradient solvers are 3-8x slower than K17; on 14x14 / 7x7
+# planes they are as fast: tools/wgrad_bench.py), 'always', or 'never' (MIOpen's choice).
+WGRAD_POLICY = "deterministic"
+
+
+def _use_k17(x, weight, stride, padding):
+    if WGRAD_POLICY == "always":
+        return True
+    if WGRAD_POLICY == "deterministic" and torch.backends.cudnn.deterministic:
+        st = stride if isinstance(stride, int) else stride[0]
+        pad = padding if isinstance(padding, int) else padding[0]
+        oh = (x.shape[2] + 2 * pad - weight.shape[2]) // st + 1
+        ow = (x.shape[3] + 2 * pad - weight.shape[3]) // st + 1
+        return oh * ow >= 400
+    return False
+
+
+def conv2d(x, weight, stride=1, padding=0, dilation=1, groups=1):
+    """F.conv2d without bias, K17 weight gradient when the weight needs one (policy above)."""
+    if weight.requires_grad and torch.is_grad_enabled() and \
+            conv_wgrad_supported(x, weight, stride, padding, dilation, groups) and \
+            _use_k17(x, weight, stride, padding):
+        return Conv2dFn.apply(x, weight, stride, padding, dilation, groups)
+    return torch.nn.functional.conv2d(x, weight, None, stride, padding, dilation, groups)

@@ -233,11 +233,19 @@ class QuantModule(nn.Module):
             return False
         return not self.use_weight_quant or self._affine_is_identity()
 
+    def _conv(self, input, weight, bias=None):
+        """The layer's conv / linear; a conv whose weight needs a gradient goes through
+        K.conv2d (deterministic K17 weight gradient, see kernels.WGRAD_POLICY)."""
+        if self.fwd_func is F.conv2d and input.is_cuda and weight.requires_grad:
+            out = K.conv2d(input, weight, **self.fwd_kwargs)
+            return out if bias is None else out + bias.view(1, -1, 1, 1)
+        return self.fwd_func(input, weight, bias, **self.fwd_kwargs)
+
     def forward_raw(self, input):
         """(conv(input, W_hat) without bias, bias): for a parent block that fuses this
         module's bias add with its residual add and activation (see epilogue_fusable)."""
         weight, bias = self._weight_bias()
-        return self.fwd_func(input, weight, None, **self.fwd_kwargs), bias
+        return self._conv(input, weight), bias
 
     def forward(self, input: torch.Tensor):
         if self.cache_features == 'if':
@@ -255,7 +263,7 @@ class QuantModule(nn.Module):
                 out = K.bias_act(out, bias, None, relu)
         else:
             weight, bias = self._weight_bias()
-            out = self.fwd_func(input, weight, bias, **self.fwd_kwargs)
+            out = self._conv(input, weight, bias)
             if self.use_weight_quant and self.cache_features == 'none' and not self._affine_is_identity():
                 out = out * self.alpha_out + self.beta_out
             if self.se_module is not None:

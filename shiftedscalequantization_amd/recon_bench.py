@@ -24,7 +24,7 @@ def _block(qnn, name):
     return m
 
 
-def run_block(dev, name, n_cali=1024, iters=200, warmup=20, rank=0):
+def run_block(dev, name, n_cali=1024, iters=200, warmup=20, rank=0, bias_cal=False):
     torch.manual_seed(1005 + rank)
     cnn = nets.resnet18().to(dev).eval()
     qnn = QuantModel(cnn, {"n_bits": 2, "channel_wise": True, "scale_method": "max"},
@@ -58,7 +58,7 @@ def run_block(dev, name, n_cali=1024, iters=200, warmup=20, rank=0):
     builtins.print = lambda *a, **k: None       # silence the loop's init prints
     try:
         block_recon_fused_shiftedScale(block, warmup + iters, (0.01, 0.1), qnn, None, verbose=False,
-                                       iter_hook=hook)
+                                       iter_hook=hook, bias_cal=bias_cal)
     finally:
         builtins.print = _print
     dt = stamps[warmup + iters] - stamps[warmup]

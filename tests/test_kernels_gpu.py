@@ -651,3 +651,35 @@ def test_lp_loss_rows_equals_gathered(K, row_shape, p):
         l2, g2 = K.lp_loss_and_grad(pred, K.Rows(cache, idx), p, relu_mask=relu_mask)
         assert host(l1).tobytes() == host(l2).tobytes()
         np.testing.assert_array_equal(host(g1).view(np.int32), host(g2).view(np.int32))
+
+
+@pytest.mark.parametrize("cfg", [
+    # (Nb, C, H, Co, k, stride, pad, groups)
+    (4, 64, 56, 64, 3, 1, 1, 1), (3, 16, 15, 24, 3, 2, 1, 1), (2, 32, 14, 48, 1, 2, 0, 1),
+    (2, 24, 9, 24, 3, 1, 1, 24), (2, 48, 12, 96, 3, 1, 1, 2), (5, 130, 7, 70, 3, 1, 1, 1),
+    (1, 3, 32, 16, 7, 2, 3, 1)])
+def test_conv_wgrad_matches_fp64(K, cfg):
+    """K17 weight gradient vs the fp64 CPU gradient: error within the fp32 accumulation
+    bound, bit-identical run to run, and the autograd wrapper equals the direct call."""
+    Nb, C, H, Co, k, st, pad, g = cfg
+    gen = torch.Generator().manual_seed(sum(cfg))
+    x = torch.randn(Nb, C, H, H, generator=gen)
+    w = torch.randn(Co, C // g, k, k, generator=gen)
+    y = torch.nn.functional.conv2d(x, w, None, st, pad, 1, g)
+    dy = torch.randn(y.shape, generator=gen)
+    ref = torch.nn.grad.conv2d_weight(x.double(), w.shape, dy.double(), st, pad, 1, g)
+    mag = torch.nn.grad.conv2d_weight(x.double().abs(), w.shape, dy.double().abs(), st, pad, 1, g)
+    xd, dyd = x.cuda(), dy.cuda()
+    dw1 = K.conv_wgrad(xd, dyd, w.shape, st, pad, g)
+    dw2 = K.conv_wgrad(xd, dyd, w.shape, st, pad, g)
+    np.testing.assert_array_equal(host(dw1).view(np.int32), host(dw2).view(np.int32))
+    err = (dw1.double().cpu() - ref).abs()
+    assert bool((err <= 1e-5 * mag + 1e-30).all()), float((err / mag.clamp_min(1e-30)).max())
+    wd = w.cuda().requires_grad_(True)
+    old, K.WGRAD_POLICY = K.WGRAD_POLICY, "always"
+    try:
+        out = K.conv2d(xd, wd, st, pad, 1, g)
+        out.backward(dyd)
+    finally:
+        K.WGRAD_POLICY = old
+    np.testing.assert_array_equal(host(wd.grad).view(np.int32), host(dw1).view(np.int32))

@@ -28,6 +28,15 @@ def dev(a):
     return torch.as_tensor(np.asarray(a)).cuda()
 
 
+@pytest.fixture(params=["never", "always"])
+def wgrad(request):
+    """Conv weight gradients from MIOpen ('never') or from K17 ssq_conv_wgrad ('always')."""
+    from shiftedscalequantization_amd import kernels
+    old, kernels.WGRAD_POLICY = kernels.WGRAD_POLICY, request.param
+    yield request.param
+    kernels.WGRAD_POLICY = old
+
+
 def tiny_net():
     """Same topology as make_golden._tiny_net (weights are loaded from the fixture)."""
     from shiftedscalequantization_amd import nets
@@ -75,7 +84,7 @@ def load_block(Q, g, block):
 
 
 @pytest.mark.parametrize("graph", [False, True])
-def test_block_recon_fused_matches_reference(Q, golden, graph):
+def test_block_recon_fused_matches_reference(Q, golden, graph, wgrad):
     g = golden("recon_fused")
     qnn = build_qnn(Q, {})
     block = qnn.model[3]
@@ -162,7 +171,7 @@ def test_layer_recon_shiftedScale_matches_reference(Q, golden):
 
 
 @pytest.mark.parametrize("graph", [False, True])
-def test_brecq_block_reconstruction_matches_reference(Q, golden, graph):
+def test_brecq_block_reconstruction_matches_reference(Q, golden, graph, wgrad):
     g = golden("recon_brecq")
     qnn = build_qnn(Q, g)
     block = qnn.model[3]
