@@ -246,6 +246,27 @@ int ssq_bias_act_fq(const float* y, const float* bias, const float* res, float* 
                     int64_t n, int64_t hw, int64_t C, int relu, const float* delta,
                     const float* zp, int qmin, int qmax, ssq_stream_t stream);
 
+/* The general epilogue: out = act(((y + bias[c]) * gamma[c] + phi[c]) + res), the
+ * QuantModule's gamma^z/phi^z affine (quant_layer.py:266-267, learned with --bias_cal)
+ * included, optionally followed by the per-tensor act fake-quant (yq; then out may be
+ * NULL).  gamma/phi (both or neither), bias, res, delta/zp may be NULL.  Bit-identical to
+ * the reference's separate fp32 ops.                                                     */
+int ssq_epilogue_fwd(const float* y, const float* bias, const float* gamma, const float* phi,
+                     const float* res, float* out, float* yq, int64_t n, int64_t hw, int64_t C,
+                     int relu, const float* delta, const float* zp, int qmin, int qmax,
+                     ssq_stream_t stream);
+/* Its backward from g = dL/d(output), recomputing the pre-activation from y (NCHW, N x C
+ * planes of hw): gy = g_t * gamma[c] (or g_t), gres = g_t, ggamma[c] = sum g_t*(y+bias[c]),
+ * gphi[c] = sum g_t, gdelta/gzp as ssq_fq_bwd, where g_t is the act quantizer's STE and the
+ * ReLU mask applied to g.  Outputs other than gy may be NULL.  Per-(n, c) partials in ws
+ * (ssq_epilogue_bwd_workspace_size(N*C)), reduced in a fixed order.                     */
+size_t ssq_epilogue_bwd_workspace_size(int64_t rows);
+int ssq_epilogue_bwd(const float* g, const float* y, const float* bias, const float* gamma,
+                     const float* phi, const float* res, int64_t N, int64_t C, int64_t hw,
+                     int relu, const float* delta, const float* zp, int qmin, int qmax, float* gy,
+                     float* gres, float* ggamma, float* gphi, float* gdelta, float* gzp, void* ws,
+                     size_t ws_bytes, ssq_stream_t stream);
+
 /* ---------------------------------------------------------------- Adam
  * torch.optim.Adam's single-tensor step (the reference's optimizer; block_recon.py:57-60,
  * layer_recon_fused_shiftedScale.py:57/73) over nseg parameter tensors in one launch:

@@ -59,6 +59,11 @@ SIGNATURES = {
     "ssq_bias_act": (_i, [_p, _p, _p, _p, _i64, _i64, _i64, _i, _p]),
     "ssq_relu_bwd": (_i, [_p, _p, _p, _i64, _p]),
     "ssq_bias_act_fq": (_i, [_p, _p, _p, _p, _p, _i64, _i64, _i64, _i, _p, _p, _i, _i, _p]),
+    "ssq_epilogue_fwd": (_i, [_p, _p, _p, _p, _p, _p, _p, _i64, _i64, _i64, _i, _p, _p, _i, _i,
+                              _p]),
+    "ssq_epilogue_bwd_workspace_size": (_sz, [_i64]),
+    "ssq_epilogue_bwd": (_i, [_p, _p, _p, _p, _p, _p, _i64, _i64, _i64, _i, _p, _p, _i, _i, _p,
+                              _p, _p, _p, _p, _p, _p, _sz, _p]),
     "ssq_adam": (_i, [_i, _p, _p, _p, _p, _p, _f, _f, _f, _f, _p, _f, _f, _p]),
     "ssq_conv_wgrad_workspace_size": (_sz, [_i64] * 10),
     "ssq_conv_wgrad": (_i, [_p, _p] + [_i64] * 10 + [_p, _p, _sz, _p]),

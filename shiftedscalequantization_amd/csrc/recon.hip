@@ -141,7 +141,7 @@ __global__ __launch_bounds__(kBlock) void gather2_kernel(const float* __restrict
 // out = act(y + bias[c] (+ res)),  c = (i / hw) % C, in the reference's op order (conv
 // bias add, residual add, ReLU: three separate fp32 roundings -> bit-identical to the
 // eager sequence), one pass instead of three.
-template <bool RES, bool RELU, bool QUANT>
+template <bool RES, bool RELU, bool QUANT, bool AFFINE>
 __global__ __launch_bounds__(kBlock) void bias_act_kernel(const float* __restrict__ y,
                                                           const float* __restrict__ bias,
                                                           const float* __restrict__ res,
@@ -151,7 +151,9 @@ __global__ __launch_bounds__(kBlock) void bias_act_kernel(const float* __restric
                                                           float* __restrict__ yq,
                                                           const float* __restrict__ qdelta,
                                                           const float* __restrict__ qzp,
-                                                          float qlo, float qhi) {
+                                                          float qlo, float qhi,
+                                                          const float* __restrict__ gamma,
+                                                          const float* __restrict__ phi) {
   const uint32_t stride = gridDim.x * blockDim.x;
   QParams qp{1.0f, 0.0f, qlo, qhi};
   if (QUANT) {
@@ -162,6 +164,7 @@ __global__ __launch_bounds__(kBlock) void bias_act_kernel(const float* __restric
     const uint32_t q = fdiv(i, div_hw);
     const uint32_t c = q - fdiv(q, div_c) * C;
     float t = bias ? __fadd_rn(v, bias[c]) : v;
+    if (AFFINE) t = __fadd_rn(__fmul_rn(t, gamma[c]), phi[c]);  // out*alpha_out + beta_out
     if (RES) t = __fadd_rn(t, rv);
     if (RELU) t = t < 0.0f ? 0.0f : t;  // torch clamp_min: std::max(t, 0) keeps -0 and NaN
     return t;
@@ -270,6 +273,132 @@ __global__ __launch_bounds__(kBlock) void adam_kernel(AdamTable tab, float w1, f
   }
 }
 
+// Backward of the K13 epilogue (optionally with gamma^z/phi^z and the act quantizer):
+// t = (y + bias[c]) [*gamma[c] + phi[c]] [+ res] [-> ReLU] [-> fq]; given g = dL/d(output)
+//   g_t = dL/d(pre-ReLU t): the STE of the act quantizer (fq_bwd_pt's formulas), then the
+//         ReLU mask (relu output <= 0 -> 0, torch threshold_backward);
+//   gy  = g_t * gamma[c] (mul backward) or g_t;   gres = g_t;
+//   per row (n, c): sum g_t*(y + bias[c]) -> dL/dgamma[c],  sum g_t -> dL/dphi[c],
+//   and the act quantizer's four sums -> dL/ddelta, dL/dzp.
+// One wave per (n, c) row; the pre-activation values are recomputed from y with the
+// forward's fp32 operations (bit-identical masks), nothing of the forward is stored.
+constexpr int kEpiParts = 6;
+
+template <bool RES, bool RELU, bool QUANT, bool AFFINE, bool VEC>
+__global__ __launch_bounds__(kBlock) void epilogue_bwd_rows(
+    const float* __restrict__ g, const float* __restrict__ y, const float* __restrict__ bias,
+    const float* __restrict__ gamma, const float* __restrict__ phi, const float* __restrict__ res,
+    uint32_t rows, uint32_t C, uint32_t hw, const float* __restrict__ qdelta,
+    const float* __restrict__ qzp, float lo, float hi, float* __restrict__ gy,
+    float* __restrict__ gres, double* __restrict__ part) {
+  const uint32_t lane = threadIdx.x & (kWave - 1);
+  const uint32_t r = blockIdx.x * (kBlock / kWave) + threadIdx.x / kWave;
+  if (r >= rows) return;
+  const uint32_t c = r % C;
+  const float b = bias ? bias[c] : 0.0f;
+  const float ga = AFFINE ? gamma[c] : 1.0f, ph = AFFINE ? phi[c] : 0.0f;
+  const float d = QUANT ? qdelta[0] : 1.0f, z = QUANT ? qzp[0] : 0.0f;
+  double sg = 0, sp = 0, a0 = 0, a1 = 0, a2 = 0, a3 = 0;
+  auto one = [&](float yv, float gv, float rv, float& oy, float& orr) {
+    const float pre = bias ? __fadd_rn(yv, b) : yv;
+    float t = AFFINE ? __fadd_rn(__fmul_rn(pre, ga), ph) : pre;
+    if (RES) t = __fadd_rn(t, rv);
+    if (RELU) t = t < 0.0f ? 0.0f : t;
+    float gt = gv;
+    if (QUANT) {
+      const float tq = t / d;
+      const float v = __fadd_rn(rintf(tq), z);
+      const bool m = (v >= lo) && (v <= hi);
+      const float q = clampf(v, lo, hi);
+      const float gq = __fmul_rn(gv, d);
+      const float gi = m ? gq : 0.0f;
+      gt = gi / d;
+      a0 += (double)gv * (double)__fsub_rn(q, z);
+      a1 += (double)gi * (double)(tq / d);
+      a2 += (double)gi;
+      a3 += (double)gq;
+    }
+    if (RELU) gt = t <= 0.0f ? 0.0f : gt;
+    oy = AFFINE ? __fmul_rn(gt, ga) : gt;
+    orr = gt;
+    sg += (double)gt * (double)pre;
+    sp += (double)gt;
+  };
+  const int64_t base = (int64_t)r * hw;
+  if (VEC) {
+    const f32x4* Y = (const f32x4*)(y + base);
+    const f32x4* G = (const f32x4*)(g + base);
+    const f32x4* R = RES ? (const f32x4*)(res + base) : nullptr;
+    f32x4* GY = (f32x4*)(gy + base);
+    f32x4* GR = gres ? (f32x4*)(gres + base) : nullptr;
+    for (uint32_t v = lane; v < hw / 4; v += kWave) {
+      const f32x4 yv = Y[v], gv = G[v];
+      f32x4 rv = {0.0f, 0.0f, 0.0f, 0.0f};
+      if (RES) rv = R[v];
+      float oy[4], orr[4];
+      one(yv.x, gv.x, rv.x, oy[0], orr[0]);
+      one(yv.y, gv.y, rv.y, oy[1], orr[1]);
+      one(yv.z, gv.z, rv.z, oy[2], orr[2]);
+      one(yv.w, gv.w, rv.w, oy[3], orr[3]);
+      GY[v] = f32x4{oy[0], oy[1], oy[2], oy[3]};
+      if (GR) GR[v] = f32x4{orr[0], orr[1], orr[2], orr[3]};
+    }
+  } else {
+    for (uint32_t j = lane; j < hw; j += kWave) {
+      float oy, orr;
+      one(y[base + j], g[base + j], RES ? res[base + j] : 0.0f, oy, orr);
+      gy[base + j] = oy;
+      if (gres) gres[base + j] = orr;
+    }
+  }
+  sg = wave_sum(sg);
+  sp = wave_sum(sp);
+  if (QUANT) {
+    a0 = wave_sum(a0);
+    a1 = wave_sum(a1);
+    a2 = wave_sum(a2);
+    a3 = wave_sum(a3);
+  }
+  if (lane == 0) {
+    double* o = part + (int64_t)r * kEpiParts;
+    o[0] = sg;
+    o[1] = sp;
+    o[2] = a0;
+    o[3] = a1;
+    o[4] = a2;
+    o[5] = a3;
+  }
+}
+
+// blocks [0, nb): per-channel gamma / phi gradients (sum over n in order); block nb: the
+// act quantizer's delta / zp gradients (rows in a fixed order, as fq_bwd_finalize).
+__global__ __launch_bounds__(kBlock) void epilogue_bwd_finalize(
+    const double* __restrict__ part, uint32_t N, uint32_t C, float* __restrict__ ggamma,
+    float* __restrict__ gphi, float* __restrict__ gdelta, float* __restrict__ gzp) {
+  __shared__ double red[16];
+  const uint32_t nb = (C + kBlock - 1) / kBlock;
+  if (blockIdx.x < nb) {
+    const uint32_t c = blockIdx.x * kBlock + threadIdx.x;
+    if (c >= C) return;
+    double sg = 0, sp = 0;
+    for (uint32_t n = 0; n < N; ++n) {
+      sg += part[((int64_t)n * C + c) * kEpiParts + 0];
+      sp += part[((int64_t)n * C + c) * kEpiParts + 1];
+    }
+    if (ggamma) ggamma[c] = (float)sg;
+    if (gphi) gphi[c] = (float)sp;
+    return;
+  }
+  double a[4] = {0, 0, 0, 0};
+  for (uint32_t r = threadIdx.x; r < N * C; r += blockDim.x)
+    for (int k = 0; k < 4; ++k) a[k] += part[(int64_t)r * kEpiParts + 2 + k];
+  for (int k = 0; k < 4; ++k) a[k] = block_sum(a[k], red);
+  if (threadIdx.x == 0) {
+    if (gdelta) gdelta[0] = (float)(a[0] - a[1]);
+    if (gzp) gzp[0] = (float)(a[2] - a[3]);
+  }
+}
+
 }  // namespace ssq
 
 using namespace ssq;
@@ -354,7 +483,9 @@ extern "C" int ssq_gather_rows2(const float* src0, float* dst0, int64_t row0, co
 
 static int bias_act(const char* what, const float* y, const float* bias, const float* res,
                     float* out, float* yq, int64_t n, int64_t hw, int64_t C, int relu,
-                    const float* qdelta, const float* qzp, int qmin, int qmax, hipStream_t s) {
+                    const float* qdelta, const float* qzp, int qmin, int qmax, hipStream_t s,
+                    const float* gamma = nullptr, const float* phi = nullptr) {
+  SSQ_REQUIRE(!gamma == !phi, SSQ_E_ARG, "%s: gamma and phi go together", what);
   SSQ_REQUIRE(y && n >= 0 && hw >= 1 && C >= 1, SSQ_E_ARG, "%s: bad args", what);
   SSQ_REQUIRE(yq ? (qdelta && qzp && qmin < qmax) : out != nullptr, SSQ_E_ARG, "%s: bad outputs",
               what);
@@ -366,17 +497,20 @@ static int bias_act(const char* what, const float* y, const float* bias, const f
   const FastDiv dh = make_fastdiv((uint32_t)hw), dc = make_fastdiv((uint32_t)C);
   const dim3 grid(grid_for(vec ? n / 4 : n, kBlock, 2048));
   const float lo = (float)qmin, hi = (float)qmax;
-#define SSQ_BA(R, A, Q)                                                                       \
-  hipLaunchKernelGGL((bias_act_kernel<R, A, Q>), grid, dim3(kBlock), 0, s, y, bias, res, out,  \
-                     (uint32_t)n, dh, dc, (uint32_t)C, vec, yq, qdelta, qzp, lo, hi)
+#define SSQ_BA(R, A, Q, F)                                                                    \
+  hipLaunchKernelGGL((bias_act_kernel<R, A, Q, F>), grid, dim3(kBlock), 0, s, y, bias, res, out, \
+                     (uint32_t)n, dh, dc, (uint32_t)C, vec, yq, qdelta, qzp, lo, hi, gamma, phi)
+#define SSQ_BA1(R, A, Q) \
+  if (gamma) SSQ_BA(R, A, Q, true); else SSQ_BA(R, A, Q, false);
 #define SSQ_BA2(R, A) \
-  if (yq) SSQ_BA(R, A, true); else SSQ_BA(R, A, false);
+  if (yq) { SSQ_BA1(R, A, true) } else { SSQ_BA1(R, A, false) }
   if (res) {
     if (relu) { SSQ_BA2(true, true) } else { SSQ_BA2(true, false) }
   } else {
     if (relu) { SSQ_BA2(false, true) } else { SSQ_BA2(false, false) }
   }
 #undef SSQ_BA2
+#undef SSQ_BA1
 #undef SSQ_BA
   return check_launch(what);
 }
@@ -394,6 +528,69 @@ extern "C" int ssq_bias_act_fq(const float* y, const float* bias, const float* r
   SSQ_REQUIRE(yq, SSQ_E_ARG, "ssq_bias_act_fq: yq is required");
   return bias_act("ssq_bias_act_fq", y, bias, res, out, yq, n, hw, C, relu, delta, zp, qmin, qmax,
                   (hipStream_t)stream);
+}
+
+extern "C" int ssq_epilogue_fwd(const float* y, const float* bias, const float* gamma,
+                                const float* phi, const float* res, float* out, float* yq,
+                                int64_t n, int64_t hw, int64_t C, int relu, const float* delta,
+                                const float* zp, int qmin, int qmax, ssq_stream_t stream) {
+  return bias_act("ssq_epilogue_fwd", y, bias, res, out, yq, n, hw, C, relu, delta, zp, qmin,
+                  qmax, (hipStream_t)stream, gamma, phi);
+}
+
+extern "C" size_t ssq_epilogue_bwd_workspace_size(int64_t rows) {
+  return (size_t)rows * kEpiParts * sizeof(double);
+}
+
+extern "C" int ssq_epilogue_bwd(const float* g, const float* y, const float* bias,
+                                const float* gamma, const float* phi, const float* res,
+                                int64_t N, int64_t C, int64_t hw, int relu, const float* delta,
+                                const float* zp, int qmin, int qmax, float* gy, float* gres,
+                                float* ggamma, float* gphi, float* gdelta, float* gzp, void* ws,
+                                size_t ws_bytes, ssq_stream_t stream) {
+  SSQ_REQUIRE(g && y && gy && N >= 1 && C >= 1 && hw >= 1, SSQ_E_ARG,
+              "ssq_epilogue_bwd: bad args");
+  SSQ_REQUIRE(!gamma == !phi && (!(ggamma || gphi) || gamma), SSQ_E_ARG,
+              "ssq_epilogue_bwd: gamma/phi gradients need gamma and phi");
+  SSQ_REQUIRE(!delta || (zp && qmin < qmax), SSQ_E_ARG, "ssq_epilogue_bwd: act quantizer");
+  SSQ_REQUIRE(!(gdelta || gzp) || delta, SSQ_E_ARG, "ssq_epilogue_bwd: delta/zp grads need delta");
+  SSQ_REQUIRE(N * C * hw < (1ll << 31) && N * C < (1ll << 31), SSQ_E_ARG,
+              "ssq_epilogue_bwd: tensor exceeds 2^31 elements");
+  const int64_t rows = N * C;
+  SSQ_REQUIRE(ws && ws_bytes >= ssq_epilogue_bwd_workspace_size(rows), SSQ_E_WS,
+              "ssq_epilogue_bwd: workspace too small");
+  hipStream_t s = (hipStream_t)stream;
+  auto al = [](const void* q) { return ((uintptr_t)q & 15u) == 0; };
+  const bool vec = hw % 4 == 0 && al(g) && al(y) && al(gy) && (!res || al(res)) &&
+                   (!gres || al(gres));
+  const dim3 grid((unsigned)((rows + kBlock / kWave - 1) / (kBlock / kWave)));
+  const float lo = (float)qmin, hi = (float)qmax;
+  double* part = (double*)ws;
+#define SSQ_EB(R, A, Q, F, V)                                                                  \
+  hipLaunchKernelGGL((epilogue_bwd_rows<R, A, Q, F, V>), grid, dim3(kBlock), 0, s, g, y, bias, \
+                     gamma, phi, res, (uint32_t)rows, (uint32_t)C, (uint32_t)hw, delta, zp, lo, \
+                     hi, gy, gres, part)
+#define SSQ_EB1(R, A, Q, F) \
+  if (vec) SSQ_EB(R, A, Q, F, true); else SSQ_EB(R, A, Q, F, false);
+#define SSQ_EB2(R, A, Q) \
+  if (gamma) { SSQ_EB1(R, A, Q, true) } else { SSQ_EB1(R, A, Q, false) }
+#define SSQ_EB3(R, A) \
+  if (delta) { SSQ_EB2(R, A, true) } else { SSQ_EB2(R, A, false) }
+  if (res) {
+    if (relu) { SSQ_EB3(true, true) } else { SSQ_EB3(true, false) }
+  } else {
+    if (relu) { SSQ_EB3(false, true) } else { SSQ_EB3(false, false) }
+  }
+#undef SSQ_EB3
+#undef SSQ_EB2
+#undef SSQ_EB1
+#undef SSQ_EB
+  if (ggamma || gphi || gdelta || gzp) {
+    const unsigned nb = (unsigned)((C + kBlock - 1) / kBlock);
+    hipLaunchKernelGGL(epilogue_bwd_finalize, dim3(nb + 1), dim3(kBlock), 0, s,
+                       (const double*)part, (uint32_t)N, (uint32_t)C, ggamma, gphi, gdelta, gzp);
+  }
+  return check_launch("ssq_epilogue_bwd");
 }
 
 extern "C" int ssq_relu_bwd(const float* g, const float* out, float* gin, int64_t n,

@@ -679,6 +679,75 @@ def bias_act_quant(y, bias, res, relu, delta, zp, n_bits, sym=False):
     return BiasActQuantFn.apply(y, bias, res, delta, zp, bool(relu), n_bits, sym, keep)
 
 
+class EpilogueFn(torch.autograd.Function):
+    """act(((y + bias[c]) * gamma[c] + phi[c]) (+ res)) [-> per-tensor act fake-quant] in one
+    pass (quant_layer.py:250,266-272; quant_block.py:99-118) -- the general K13 epilogue,
+    with the --bias_cal affine gamma^z/phi^z.  Backward (ssq_epilogue_bwd) recomputes the
+    pre-activation from the conv output y and returns the y / res / gamma / phi / delta /
+    zero_point gradients of the reference's op sequence."""
+
+    @staticmethod
+    def forward(ctx, y, bias, gamma, phi, res, delta, zp, relu, n_bits, sym):
+        y, yp, bp, rp, C_, hw, _ = _epilogue_layout(y, bias, res)
+        gm, gmp = fptr(gamma.detach().reshape(-1), "gamma") if gamma is not None else (None, None)
+        ph, php = fptr(phi.detach().reshape(-1), "phi") if phi is not None else (None, None)
+        if gm is not None and (gm.numel() != C_ or ph.numel() != C_):
+            raise A.SSQError("epilogue: gamma / phi must have one value per channel")
+        quant = delta is not None
+        if quant:
+            d, dp = fptr(delta.detach().reshape(-1), "delta")
+            z, zpp = fptr(zp.detach().reshape(-1), "zero_point")
+            if d.numel() != 1 or z.numel() != 1:
+                raise A.SSQError("epilogue: per-tensor activation quantizer only")
+            lo, hi = qrange(n_bits, sym)
+        else:
+            dp = zpp = None
+            lo, hi = 0, 1
+        out = torch.empty_like(y)
+        call("ssq_epilogue_fwd", yp, bp, gmp, php, rp, None if quant else _vp(out),
+             _vp(out) if quant else None, y.numel(), hw, C_, int(relu), dp, zpp, lo, hi,
+             stream_of(y))
+        ctx.cfg = (bool(relu), lo, hi, quant, C_, hw)
+        ctx.save_for_backward(y, bias, gamma, phi, res, delta, zp)
+        return out
+
+    @staticmethod
+    def backward(ctx, g):
+        y, bias, gamma, phi, res, delta, zp = ctx.saved_tensors
+        relu, lo, hi, quant, C_, hw = ctx.cfg
+        g, gp = fptr(g.contiguous(), "grad")
+        need = ctx.needs_input_grad
+        dev_ = g.device
+
+        def flat(t):
+            return None if t is None else t.detach().reshape(-1).contiguous()
+        b, gm, ph, r = flat(bias), flat(gamma), flat(phi), res
+        d, z = flat(delta), flat(zp)
+        gy = torch.empty_like(g)
+        gres = torch.empty_like(g) if (res is not None and need[4]) else None
+        ggm = torch.empty(C_, device=dev_) if (gamma is not None and need[2]) else None
+        gph = torch.empty(C_, device=dev_) if (phi is not None and need[3]) else None
+        gd = torch.empty(1, device=dev_) if (quant and need[5]) else None
+        gz = torch.empty(1, device=dev_) if (quant and need[6]) else None
+        N = g.numel() // (C_ * hw)
+        ws, wsn = workspace(query("ssq_epilogue_bwd_workspace_size", N * C_), dev_)
+        call("ssq_epilogue_bwd", gp, _vp(y), _vp(b), _vp(gm), _vp(ph),
+             _vp(r.contiguous() if r is not None else None), N, C_, hw, int(relu), _vp(d), _vp(z),
+             lo, hi, _vp(gy), _vp(gres), _vp(ggm), _vp(gph), _vp(gd), _vp(gz), ws, wsn,
+             stream_of(g))
+        shape = (lambda t, o: None if o is None else o.view(t.shape))
+        return (gy if need[0] else None, None, shape(gamma, ggm), shape(phi, gph), gres,
+                shape(delta, gd), shape(zp, gz), None, None, None)
+
+
+def epilogue(y, bias, gamma, phi, res, relu, q=None):
+    """EpilogueFn with q an (initialised, per-tensor) act quantizer or None."""
+    if q is None:
+        return EpilogueFn.apply(y, bias, gamma, phi, res, None, None, bool(relu), 8, False)
+    return EpilogueFn.apply(y, bias, gamma, phi, res, q.delta, q.zero_point, bool(relu), q.n_bits,
+                            q.sym)
+
+
 def adam_step(params, grads, exp_avgs, exp_avg_sqs, beta1, beta2, eps, hyper=None,
               neg_step_size=0.0, bc2_sqrt=1.0):
     """One torch.optim.Adam (single-tensor form) step for every tensor, one launch.

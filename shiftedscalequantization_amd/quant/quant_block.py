@@ -85,6 +85,12 @@ class BaseQuantBlock(nn.Module):
             raw, bias = last.forward_raw(inp)
             relu = isinstance(self.activation_function, nn.ReLU)
             q = fusable_act_quantizer(self.act_quantizer, self.use_act_quant)
+            gamma, phi = last.affine()
+            if gamma is not None:   # last's gamma^z/phi^z, residual, act (+ act quant)
+                out = K.epilogue(raw, bias, gamma, phi, residual, relu, q)
+                if q is None and self.use_act_quant:
+                    out = self.act_quantizer(out)
+                return out
             if q is not None:   # + the block's act quant in the same pass
                 return K.bias_act_quant(raw, bias, residual, relu, q.delta, q.zero_point,
                                         q.n_bits, q.sym)

@@ -222,16 +222,21 @@ class QuantModule(nn.Module):
         return weight, bias
 
     def epilogue_fusable(self, input):
-        """The conv bias add and a ReLU / identity activation can run as the fused K13
-        epilogue (bit-identical to the eager ops): a conv on the device, a constant
-        bias, no gamma^z/phi^z affine, no SE module, no feature caching."""
+        """The conv bias add, the gamma^z/phi^z affine and a ReLU / identity activation can
+        run as the fused K13 epilogue (bit-identical to the eager ops): a conv on the
+        device, a constant bias, no SE module, no feature caching."""
         if not (input.is_cuda and self.fwd_func is F.conv2d and self.se_module is None
                 and self.cache_features == 'none'
                 and isinstance(self.activation_function, (nn.ReLU, StraightThrough))):
             return False
-        if self.bias is not None and self.bias.requires_grad and self.train_bias:
-            return False
-        return not self.use_weight_quant or self._affine_is_identity()
+        return not (self.bias is not None and self.bias.requires_grad and self.train_bias)
+
+    def affine(self):
+        """(gamma^z, phi^z) when the forward applies them (quant_layer.py:266-267), else
+        (None, None)."""
+        if self.use_weight_quant and self.cache_features == 'none' and not self._affine_is_identity():
+            return self.alpha_out, self.beta_out
+        return None, None
 
     def _conv(self, input, weight, bias=None):
         """The layer's conv / linear; a conv whose weight needs a gradient goes through
@@ -255,7 +260,11 @@ class QuantModule(nn.Module):
             out, bias = self.forward_raw(input)
             relu = isinstance(self.activation_function, nn.ReLU)
             q = fusable_act_quantizer(self.act_quantizer, act_q)
-            if q is not None:
+            gamma, phi = self.affine()
+            if gamma is not None:
+                out = K.epilogue(out, bias, gamma, phi, None, relu, q)
+                act_q = act_q and q is None
+            elif q is not None:
                 out = K.bias_act_quant(out, bias, None, relu, q.delta, q.zero_point, q.n_bits,
                                        q.sym)
                 act_q = False

@@ -447,8 +447,9 @@ def test_bias_act_matches_eager_ops(K, shape, res, relu):
         np.testing.assert_array_equal(host(rr.grad), host(re_.grad))
 
 
+@pytest.mark.parametrize("affine", [False, True])
 @pytest.mark.parametrize("act", [False, True])
-def test_quant_block_fused_epilogue_matches_unfused(K, act):
+def test_quant_block_fused_epilogue_matches_unfused(K, act, affine):
     """A QuantBasicBlock forward/backward through the fused epilogue equals the eager
     path (fusion disabled) bit for bit; with act quant on, the act q/dq runs inside the
     epilogue pass and the act-delta gradients match too."""
@@ -463,7 +464,7 @@ def test_quant_block_fused_epilogue_matches_unfused(K, act):
     x = torch.randn(4, 16, 14, 14).cuda()
     with torch.no_grad():
         qnn(x)                                       # init the quantizers
-    _compare_fused_unfused(qb, x, act)
+    _compare_fused_unfused(qb, x, act, _set_affine(qb) if affine else ())
 
 
 def _act_deltas(qb):
@@ -474,7 +475,23 @@ def _act_deltas(qb):
     return [d for d in ds if d is not None]
 
 
-def _compare_fused_unfused(qb, x, act):
+def _set_affine(qb):
+    """Random learned gamma^z / phi^z on every QuantModule of the block (--bias_cal)."""
+    from shiftedscalequantization_amd import quant as Q
+    gen = torch.Generator().manual_seed(77)
+    ps = []
+    for m in qb.modules():
+        if isinstance(m, Q.QuantModule):
+            c = m.alpha_out.numel()
+            m.alpha_out.data = (1 + 0.1 * torch.randn(c, generator=gen)).view_as(m.alpha_out).cuda()
+            m.beta_out.data = (0.1 * torch.randn(c, generator=gen)).view_as(m.beta_out).cuda()
+            m.alpha_out.requires_grad_(True)
+            m.beta_out.requires_grad_(True)
+            ps += [m.alpha_out, m.beta_out]
+    return ps
+
+
+def _compare_fused_unfused(qb, x, act, affine=()):
     from shiftedscalequantization_amd import quant as Q
     outs = []
     g = torch.randn(1, generator=torch.Generator().manual_seed(1))
@@ -483,23 +500,33 @@ def _compare_fused_unfused(qb, x, act):
             for m in qb.modules():
                 if isinstance(m, Q.QuantModule):
                     m.epilogue_fusable = lambda inp: False
-        for d in _act_deltas(qb):
+        for d in list(_act_deltas(qb)) + list(affine):
             d.grad = None
         xx = x.clone().requires_grad_(True)
         y = qb(xx)
         gy = torch.linspace(-1, 1, y.numel(), device=y.device).view_as(y) + g.item()
         y.backward(gy)
-        outs.append((host(y), host(xx.grad), [host(d.grad) for d in _act_deltas(qb)] if act else []))
+        outs.append((host(y), host(xx.grad), [host(d.grad) for d in _act_deltas(qb)] if act else [],
+                     [host(p.grad) for p in affine]))
     np.testing.assert_array_equal(outs[0][0], outs[1][0])
     np.testing.assert_array_equal(outs[0][1], outs[1][1])
     assert len(outs[0][2]) == len(outs[1][2])
     for a, b in zip(outs[0][2], outs[1][2]):
-        np.testing.assert_array_equal(a, b)
+        if affine:
+            # the affine epilogue reduces the act-delta sums per (n, c) row and takes the
+            # (x/d)/d term exactly as torch's div backward; the float4 fq backward uses
+            # (x/d)*(1/d): one ulp per term of two sums of ~1e2 that cancel to ~1e-2
+            np.testing.assert_allclose(a, b, rtol=1e-4, atol=1e-3)
+        else:
+            np.testing.assert_array_equal(a, b)
+    for a, b in zip(outs[0][3], outs[1][3]):   # gamma / phi: double vs torch's fp32 sums
+        np.testing.assert_allclose(a, b, rtol=1e-4, atol=1e-4 * np.abs(b).max())
 
 
+@pytest.mark.parametrize("affine", [False, True])
 @pytest.mark.parametrize("act", [False, True])
 @pytest.mark.parametrize("kind", ["bottleneck", "resbottleneck", "inverted"])
-def test_other_blocks_fused_epilogue_matches_unfused(K, kind, act):
+def test_other_blocks_fused_epilogue_matches_unfused(K, kind, act, affine):
     """ResNet-50 / RegNetX / MobileNetV2 blocks: the fused conv-bias + residual (+ReLU)
     tail equals the eager ops bit for bit, forward and backward."""
     import torch.nn as nn
@@ -520,7 +547,7 @@ def test_other_blocks_fused_epilogue_matches_unfused(K, kind, act):
     x = torch.randn(4, cin, 14, 14).cuda()
     with torch.no_grad():
         qnn(x)
-    _compare_fused_unfused(qb, x, act)
+    _compare_fused_unfused(qb, x, act, _set_affine(qb) if affine else ())
 
 
 @pytest.mark.parametrize("shape", [(4, 8, 7, 7), (2, 3, 5, 3), (32, 64, 56, 56)])
