@@ -177,6 +177,7 @@ class QuantModule(nn.Module):
         self.beta_out.requires_grad_(False)
         self._affine_key = None
         self._affine_identity = False
+        self._affine_live = False
         self.train_bias = False
         self.selection = None
         self.selectionInited = False
@@ -199,9 +200,15 @@ class QuantModule(nn.Module):
     def _affine_is_identity(self):
         """True while gamma^z / phi^z are still their untouched initial (1, 0) tensors
         and nothing needs their gradient: then out*1+0 == out and the two passes (plus
-        their backward) are skipped.  Any in-place update bumps the tensor version."""
+        their backward) are skipped.  Once they have been trainable (--bias_cal) they
+        count as live for good: the fused Adam and HIP-graph replays update them without
+        bumping torch's version counter, so a version-keyed value check would go stale.
+        Other in-place edits (torch ops) bump the version and trigger a re-check."""
         a, b = self.alpha_out, self.beta_out
         if a.requires_grad or b.requires_grad:
+            self._affine_live = True
+            return False
+        if getattr(self, '_affine_live', False):
             return False
         key = (id(a), id(b), a._version, b._version, a.device)
         if key != self._affine_key:

@@ -710,3 +710,27 @@ def test_conv_wgrad_matches_fp64(K, cfg):
     finally:
         K.WGRAD_POLICY = old
     np.testing.assert_array_equal(host(wd.grad).view(np.int32), host(dw1).view(np.int32))
+
+
+def test_affine_stays_live_after_raw_device_updates(K):
+    """gamma^z/phi^z updated by a raw device write (fused Adam, graph replay: no torch
+    version bump) after being trainable must still be applied once frozen again."""
+    from shiftedscalequantization_amd import quant as Q
+    torch.manual_seed(8)
+    qm = Q.QuantModule(torch.nn.Conv2d(4, 8, 3, padding=1), {"n_bits": 4, "channel_wise": True},
+                       {"n_bits": 8}).cuda()
+    qm.set_quant_state(True, False)
+    x = torch.randn(2, 4, 6, 6).cuda()
+    with torch.no_grad():
+        y0 = qm(x)                                   # identity affine (cached check)
+    qm.alpha_out.requires_grad_(True)
+    qm(x)                                            # trainable once (bias_cal loop)
+    new = torch.linspace(0.5, 1.5, 8).view_as(qm.alpha_out).cuda()
+    K.stream_copy(new, qm.alpha_out.data)            # raw write, no version bump
+    qm.alpha_out.requires_grad_(False)
+    with torch.no_grad():
+        y1 = qm(x)
+        w = qm.weight_quantizer(qm.weight)
+        ref = torch.nn.functional.conv2d(x, w, qm.bias, 1, 1) * new + qm.beta_out
+    assert not torch.equal(y0, y1)
+    np.testing.assert_array_equal(host(y1).view(np.int32), host(ref).view(np.int32))
