@@ -34,6 +34,7 @@ def block_reconstruction(model: QuantModel, block: BaseQuantBlock, cali_data: to
 
 
 GRAPH_WARMUP = 3     # eager iterations before the iteration body is captured
+ITER_HOOK = None     # optional callable(i, iters) at the top of every device-loop iteration (tools)
 
 
 def _reconstruct(model, block, qmodules, cali_data, batch_size, iters, weight, opt_mode, asym,
@@ -118,6 +119,8 @@ def _fast_loop(block, qmodules, opt_params, loss_func, feeder, bucket, iters, ac
     AdaRound backward, fused Adam.  After GRAPH_WARMUP eager iterations the body is
     replayed from a HIP graph (single GPU).  The cosine LR schedule is stepped by the
     reference's own torch scheduler on a shadow optimizer and copied into Adam's device lr."""
+    if ITER_HOOK is not None:
+        ITER_HOOK(-1, iters)
     use_graph = bool(graph and iters > GRAPH_WARMUP + 1)
     if act_quant:
         optimizer = SsqAdam(opt_params, lr=lr)
@@ -158,6 +161,8 @@ def _fast_loop(block, qmodules, opt_params, loss_func, feeder, bucket, iters, ac
     graph_obj, ws_cache = None, {}
     try:
         for i in range(iters):
+            if ITER_HOOK is not None:
+                ITER_HOOK(i, iters)
             b, lam, active = loss_func.schedule()
             feeder.stage(feeder.draw(), extra=(lam, float(b)) + optimizer.next_hyper())
             # the round-loss value (reporting only) from alpha before this step, as the
@@ -180,6 +185,8 @@ def _fast_loop(block, qmodules, opt_params, loss_func, feeder, bucket, iters, ac
                 shadow.step()
                 scheduler.step()
                 optimizer.param_groups[0]['lr'] = shadow.param_groups[0]['lr']
+        if ITER_HOOK is not None:
+            ITER_HOOK(iters, iters)
     finally:
         for q in ada:
             q._fused_reg = None

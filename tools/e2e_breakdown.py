@@ -43,6 +43,26 @@ D.cache_block_features = timed("shift_cache", D.cache_block_features)
 D.block_recon_fused_shiftedScale = timed("shift_block_recon", D.block_recon_fused_shiftedScale)
 LF._fused_loop = timed("shift_loop", LF._fused_loop)
 
+_marks = {}
+
+
+def _hook(i, iters):
+    """Per-phase times of each BRECQ device loop: setup (entry .. i=0), eager warm-up
+    (0-3), capture + first replay (3-4), replays 4-20, steady state 20 .. iters-1, the last
+    iteration (iters-1 .. end)."""
+    if i in (-1, 0, 3, 4, 20, iters - 1, iters):
+        torch.cuda.synchronize()
+        _marks[i] = time.perf_counter()
+        if i == iters and 20 in _marks:
+            m = _marks
+            print(f"[breakdown] brecq setup {1e3 * (m[0] - m[-1]):.1f} ms, warmup {1e3 * (m[3] - m[0]):.1f} ms, "
+                  f"capture {1e3 * (m[4] - m[3]):.1f} ms, 4-20 {1e3 * (m[20] - m[4]):.1f} ms, "
+                  f"steady {1e6 * (m[iters - 1] - m[20]) / (iters - 21):.1f} us/iter, "
+                  f"last {1e3 * (m[iters] - m[iters - 1]):.1f} ms", flush=True)
+            _marks.clear()
+
+
+BR.ITER_HOOK = _hook
 t0 = time.perf_counter()
 main_imagenet.main(sys.argv[1:])
 torch.cuda.synchronize()
