@@ -18,10 +18,16 @@ import argparse
 import json
 import os
 import sys
+import tempfile
 import time
 
-import torch
-import torch.distributed as dist
+# MIOpen persists its solver choices in a per-user find-db that outlives the process: a
+# test run that convolved under cudnn.deterministic would otherwise hand its (slow,
+# deterministic) solvers to this bench's recon loops on the same box.  Fresh db per run.
+os.environ.setdefault("MIOPEN_USER_DB_PATH", tempfile.mkdtemp(prefix="ssq_bench_miopen_"))
+
+import torch  # noqa: E402
+import torch.distributed as dist  # noqa: E402
 
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)

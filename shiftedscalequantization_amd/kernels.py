@@ -868,22 +868,31 @@ class Conv2dFn(torch.autograd.Function):
         return gx, gw, None, None, None, None
 
 
-# When the conv weight gradient runs on K17: 'deterministic' = whenever the reference's
-# torch.backends.cudnn.deterministic is set and the output plane has >= 400 pixels (there
-# MIOpen's deterministic weight-gradient solvers are 3-8x slower than K17; on 14x14 / 7x7
-# planes they are as fast: tools/wgrad_bench.py), 'always', or 'never' (MIOpen's choice).
-WGRAD_POLICY = "deterministic"
+# When the conv weight gradient runs on K17 (tools/wgrad_bench.py, batch 32, MI355X):
+#   'auto'   grouped, non-depthwise convs always (MIOpen's grouped wrw is 4x slower: RegNetX
+#            g=2 956 vs 233 us); under the reference's torch.backends.cudnn.deterministic
+#            also every stride-2 conv and every output plane >= 400 pixels, where MIOpen's
+#            deterministic solvers are 3-8x slower than K17 (stride-1 14x14 / 7x7 planes are
+#            as fast on MIOpen).  Depthwise convs stay on MIOpen (K17 is 3-6x slower there).
+#   'always' / 'never' (MIOpen's choice) for A/B runs.
+WGRAD_POLICY = "auto"
 
 
-def _use_k17(x, weight, stride, padding):
+def _use_k17(x, weight, stride, padding, groups=1):
     if WGRAD_POLICY == "always":
         return True
-    if WGRAD_POLICY == "deterministic" and torch.backends.cudnn.deterministic:
+    if WGRAD_POLICY != "auto":
+        return False
+    if groups > 1 and weight.shape[1] == 1:
+        return False                      # depthwise
+    if groups > 1:
+        return True
+    if torch.backends.cudnn.deterministic:
         st = stride if isinstance(stride, int) else stride[0]
         pad = padding if isinstance(padding, int) else padding[0]
         oh = (x.shape[2] + 2 * pad - weight.shape[2]) // st + 1
         ow = (x.shape[3] + 2 * pad - weight.shape[3]) // st + 1
-        return oh * ow >= 400
+        return st > 1 or oh * ow >= 400
     return False
 
 
@@ -891,6 +900,6 @@ def conv2d(x, weight, stride=1, padding=0, dilation=1, groups=1):
     """F.conv2d without bias, K17 weight gradient when the weight needs one (policy above)."""
     if weight.requires_grad and torch.is_grad_enabled() and \
             conv_wgrad_supported(x, weight, stride, padding, dilation, groups) and \
-            _use_k17(x, weight, stride, padding):
+            _use_k17(x, weight, stride, padding, groups):
         return Conv2dFn.apply(x, weight, stride, padding, dilation, groups)
     return torch.nn.functional.conv2d(x, weight, None, stride, padding, dilation, groups)

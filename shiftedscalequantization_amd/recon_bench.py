@@ -65,16 +65,33 @@ def run_block(dev, name, n_cali=1024, iters=200, warmup=20, rank=0, bias_cal=Fal
     return iters / dt
 
 
+def _rate(dev, world, rank, name, iters):
+    ips = run_block(dev, name, iters=iters, rank=rank)
+    if world > 1:
+        import torch.distributed as dist
+        t = torch.tensor([1.0 / ips], dtype=torch.float64, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)     # slowest rank sets the pace
+        ips = 1.0 / t.item()
+    return round(ips, 2)
+
+
 def run_recon_bench(dev, world, rank, iters=200, blocks=("layer1.0", "layer4.0")):
-    res = {}
-    for b in blocks:
-        ips = run_block(dev, b, iters=iters, rank=rank)
-        if world > 1:
-            import torch.distributed as dist
-            t = torch.tensor([1.0 / ips], dtype=torch.float64, device=dev)
-            dist.all_reduce(t, op=dist.ReduceOp.MAX)     # slowest rank sets the pace
-            ips = 1.0 / t.item()
-        res[b] = round(ips, 2)
+    """iters/s per block with MIOpen's measured solver choice (cudnn.benchmark: miopenFind
+    once per shape, during the eager warm-up) and, beside it, under the reference's
+    seed_all setting (cudnn.deterministic, benchmark off: MIOpen's deterministic solvers,
+    K17 for the weight gradients where those are slow, kernels.WGRAD_POLICY)."""
+    cudnn = torch.backends.cudnn
+    saved = (cudnn.benchmark, cudnn.deterministic)
+    res, res_det = {}, {}
+    try:
+        for b in blocks:
+            cudnn.benchmark, cudnn.deterministic = True, False
+            res[b] = _rate(dev, world, rank, b, iters)
+            cudnn.benchmark, cudnn.deterministic = False, True
+            res_det[b] = _rate(dev, world, rank, b, iters)
+    finally:
+        cudnn.benchmark, cudnn.deterministic = saved
     return {"metric": "block_recon_fused_shiftedScale iters/s (batch 32 per rank, W2, S=3)",
-            "iters_per_s": res, "timed_iters": iters, "n_gpus": world,
+            "iters_per_s": res, "conv_solvers": "MIOpen find (cudnn.benchmark)",
+            "iters_per_s_deterministic": res_det, "timed_iters": iters, "n_gpus": world,
             "samples_per_s": {k: round(v * 32 * world, 1) for k, v in res.items()}}

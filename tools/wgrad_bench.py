@@ -13,7 +13,11 @@ dev = torch.device("cuda")
 SHAPES = {  # name: (C, H, Co, k, stride, pad, groups)
     "r18.l1.3x3": (64, 56, 64, 3, 1, 1, 1), "r18.l2.3x3s2": (64, 56, 128, 3, 2, 1, 1),
     "r18.l2.1x1s2": (64, 56, 128, 1, 2, 0, 1), "r18.l2.3x3": (128, 28, 128, 3, 1, 1, 1),
-    "r18.l3.3x3": (256, 14, 256, 3, 1, 1, 1), "r18.l4.3x3": (512, 7, 512, 3, 1, 1, 1),
+    "r18.l3.3x3s2": (128, 28, 256, 3, 2, 1, 1), "r18.l3.1x1s2": (128, 28, 256, 1, 2, 0, 1),
+    "r18.l3.3x3": (256, 14, 256, 3, 1, 1, 1), "r18.l4.3x3s2": (256, 14, 512, 3, 2, 1, 1),
+    "r18.l4.1x1s2": (256, 14, 512, 1, 2, 0, 1), "r18.l4.3x3": (512, 7, 512, 3, 1, 1, 1),
+    "mbv2.dw.3x3": (144, 56, 144, 3, 1, 1, 144), "mbv2.dw.3x3s2": (144, 56, 144, 3, 2, 1, 144),
+    "rgx.g2.3x3": (96, 56, 96, 3, 1, 1, 2),
     "r50.l1.1x1": (64, 56, 256, 1, 1, 0, 1), "r50.l1.1x1b": (256, 56, 64, 1, 1, 0, 1)}
 
 
