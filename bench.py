@@ -203,6 +203,12 @@ def main():
         ms_copy = time_events(lambda: K.stream_copy(act, y_act), 20, dev)
         copy_gbs = max(copy_gbs, 8.0 * n_act / (ms_copy * 1e-3) / 1e9)
     K.set_variant(default_variant)
+    # the HBM's read and write paths priced separately on the same bytes: K1 moves 4 B in
+    # and 4 B out per element, so its ceiling is the 1:1 harmonic mix of the two rates
+    sink = torch.empty(4, device=dev)
+    rd_gbs = 4.0 * n_act / (time_events(lambda: K.stream_read(act, sink), 20, dev) * 1e-3) / 1e9
+    wr_gbs = 4.0 * n_act / (time_events(lambda: K.stream_write(y_act), 20, dev) * 1e-3) / 1e9
+    mix_gbs = 2.0 / (1.0 / rd_gbs + 1.0 / wr_gbs)
     ms_w = time_events(lambda: K.fake_quant_multi(weights, dws, zws, bits), 20, dev)
     # W2 per-channel q/dq of the large synthetic weight of BASELINE.md §2 ([8192,2048,3,3],
     # per-output-channel delta/zp staged in LDS): the per-channel kernel's roofline line
@@ -244,7 +250,10 @@ def main():
                      "traffic_source": PMC_FILE if traffic is not None else None,
                      "kernel_ms": round(ms_fq, 4), "alg_bytes_per_launch": int(alg_bytes),
                      "stream_copy_gbs": round(copy_gbs, 1),
-                     "frac_of_stream_copy": round(achieved / copy_gbs, 4)},
+                     "frac_of_stream_copy": round(achieved / copy_gbs, 4),
+                     "read_only_gbs": round(rd_gbs, 1), "write_only_gbs": round(wr_gbs, 1),
+                     "mixed_rw_ceiling_gbs": round(mix_gbs, 1),
+                     "frac_of_mixed_rw_ceiling": round(achieved / mix_gbs, 4)},
         "weights_multi_ms": round(ms_w, 4),
         "roofline_per_channel": {"kernel": "fq_fwd_multi_kernel (ssq_fq_fwd per-channel, 1 segment)",
                                  "workload": "W2 per-channel q/dq of [8192,2048,3,3] (151 M elems)",

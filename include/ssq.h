@@ -315,6 +315,9 @@ int ssq_pack_decode(const void* packed, const float* zp, const float* d1, int d1
 /* ---------------------------------------------------------------- bandwidth probe
  * float4 device copy, used by bench.py to report the measured stream bandwidth.      */
 int ssq_stream_copy(const float* src, float* dst, int64_t n, ssq_stream_t stream);
+/* HBM read-only (kind 1: nt loads of src, dst receives nothing) / write-only (kind 2: nt
+ * stores into dst) probe over n floats, K1's geometry.  Bench context only. */
+int ssq_stream_probe(const float* src, float* dst, int64_t n, int kind, ssq_stream_t stream);
 
 #ifdef __cplusplus
 }

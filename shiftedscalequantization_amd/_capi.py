@@ -72,6 +72,7 @@ SIGNATURES = {
     "ssq_pack_encode": (_i, [_p, _p, _p, _i, _p, _i64, _i64, _i64, _i, _i, _i, _p, _p, _p]),
     "ssq_pack_decode": (_i, [_p, _p, _p, _i, _p, _i64, _i64, _i64, _i, _i, _p, _p]),
     "ssq_stream_copy": (_i, [_p, _p, _i64, _p]),
+    "ssq_stream_probe": (_i, [_p, _p, _i64, _i, _p]),
 }
 
 _lib = None

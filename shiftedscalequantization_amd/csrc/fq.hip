@@ -436,6 +436,38 @@ __global__ __launch_bounds__(1024) void copy_kernel(const f32x4* __restrict__ s,
   for (; i < end; i += stride) d[i] = s[i];
 }
 
+// Bandwidth probes for the bench's roofline context: a pure read (nt loads, reduced to
+// a value that is never stored unless it equals an impossible sentinel) and a pure write
+// (nt stores) over the same bytes, same geometry as the copy.  The read and write paths
+// of the HBM differ (tools/hbm_ceiling.hip); K1's 1:1 mix is priced against both.
+template <int UNROLL>
+__global__ __launch_bounds__(1024) void read_probe(const f32x4* __restrict__ s,
+                                                   float* __restrict__ sink, int64_t n4) {
+  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+  int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  f32x4 acc = {0.0f, 0.0f, 0.0f, 0.0f};
+  for (; i + (UNROLL - 1) * stride < n4; i += UNROLL * stride) {
+    f32x4 v[UNROLL];
+#pragma unroll
+    for (int u = 0; u < UNROLL; ++u) v[u] = ld4<true>(&s[i + u * stride]);
+#pragma unroll
+    for (int u = 0; u < UNROLL; ++u) acc += v[u];
+  }
+  if (acc.x + acc.y + acc.z + acc.w == -1234.5f) sink[0] = 1.0f;
+}
+
+template <int UNROLL>
+__global__ __launch_bounds__(1024) void write_probe(f32x4* __restrict__ d, int64_t n4) {
+  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+  int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const f32x4 v = {0.0f, 1.0f, 2.0f, (float)threadIdx.x};
+  for (; i + (UNROLL - 1) * stride < n4; i += UNROLL * stride) {
+#pragma unroll
+    for (int u = 0; u < UNROLL; ++u) st4<true>(v, &d[i + u * stride]);
+  }
+  for (; i < n4; i += stride) d[i] = v;
+}
+
 // Tuning variant of the streaming kernels (bench A/B only):
 //   bits 0-1 cache policy: 0 plain, 1 NT load+store, 2 NT load only, 3 NT store only
 //   bits 4-7 unroll: 0 -> 4, 1 -> 1, 2 -> 2, 3 -> 8, 4 -> 16
@@ -703,4 +735,22 @@ extern "C" int ssq_stream_copy(const float* src, float* dst, int64_t n, ssq_stre
   launch_stream<Copy>(v, grid, block, (hipStream_t)stream, (const f32x4*)src, (f32x4*)dst, n4,
                       chunk);
   return check_launch("ssq_stream_copy");
+}
+
+extern "C" int ssq_stream_probe(const float* src, float* dst, int64_t n, int kind,
+                                ssq_stream_t stream) {
+  SSQ_REQUIRE(n >= 0 && n % 4 == 0 && (kind == 1 || kind == 2), SSQ_E_ARG,
+              "ssq_stream_probe: kind 1 (read) / 2 (write), n a multiple of 4");
+  SSQ_REQUIRE((kind == 1 ? src != nullptr : true) && dst && aligned16(dst) &&
+                  (kind == 2 || aligned16(src)),
+              SSQ_E_ARG, "ssq_stream_probe: needs 16-B aligned buffers");
+  if (n == 0) return SSQ_OK;
+  const int64_t n4 = n / 4;
+  hipStream_t s = (hipStream_t)stream;
+  // the K1 default geometry: 1 workgroup of 256 per CU, 8 float4 in flight per thread
+  if (kind == 1)
+    hipLaunchKernelGGL(read_probe<8>, dim3(256), dim3(256), 0, s, (const f32x4*)src, dst, n4);
+  else
+    hipLaunchKernelGGL(write_probe<8>, dim3(256), dim3(256), 0, s, (f32x4*)dst, n4);
+  return check_launch("ssq_stream_probe");
 }

@@ -771,6 +771,16 @@ def stream_copy(src, dst):
     call("ssq_stream_copy", _vp(src), _vp(dst), src.numel(), stream_of(src))
 
 
+def stream_read(src, sink):
+    """HBM read-only probe over src (K1 geometry); sink is never written in practice."""
+    call("ssq_stream_probe", _vp(src), _vp(sink), src.numel(), 1, stream_of(src))
+
+
+def stream_write(dst):
+    """HBM write-only probe over dst (K1 geometry)."""
+    call("ssq_stream_probe", None, _vp(dst), dst.numel(), 2, stream_of(dst))
+
+
 def set_variant(v):
     return query("ssq_set_variant", int(v))
 
