@@ -195,15 +195,125 @@ __global__ __launch_bounds__(256, 2) void wgrad_stage1(const float* __restrict__
   }
 }
 
-// dW = sum over splits in split order
+// dW = the splits summed in a fixed order: wave w of a workgroup sums its quarter of the
+// splits in split order (8 loads in flight per lane), then the four wave sums are added
+// in wave order.  Same bits run to run; 4x the parallelism of one thread per element.
 __global__ __launch_bounds__(256) void wgrad_stage2(const float* __restrict__ part, int nsplit,
                                                     int64_t n, float* __restrict__ dw) {
-  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
-  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
-    float a = part[i];
-    for (int s = 1; s < nsplit; ++s) a = __fadd_rn(a, part[(int64_t)s * n + i]);
-    dw[i] = a;
+  __shared__ float red[4][64];
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int q = (nsplit + 3) >> 2;
+  const int s0 = min(w * q, nsplit), s1 = min(s0 + q, nsplit);
+  for (int64_t base = (int64_t)blockIdx.x * 64; base < n; base += (int64_t)gridDim.x * 64) {
+    const int64_t i = base + lane;
+    const int64_t ic = i < n ? i : n - 1;
+    float a = 0.0f;
+    int s = s0;
+    for (; s + 8 <= s1; s += 8) {
+      float v[8];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) v[u] = part[(int64_t)(s + u) * n + ic];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) a = __fadd_rn(a, v[u]);
+    }
+    for (; s < s1; ++s) a = __fadd_rn(a, part[(int64_t)s * n + ic]);
+    red[w][lane] = a;
+    __syncthreads();
+    if (w == 0 && i < n)
+      dw[i] = __fadd_rn(__fadd_rn(__fadd_rn(red[0][lane], red[1][lane]), red[2][lane]), red[3][lane]);
+    __syncthreads();
   }
+}
+
+// Depthwise convs (one input and one output channel per group): dW[c, r, s] is a
+// reduction of R*S products per output pixel over (n, oh, ow) -- no GEMM, a bandwidth-
+// bound pass over x and dy (MIOpen's deterministic path for these runs at < 1 TFLOP/s,
+// tools/wgrad_bench.py).  Workgroup (c, split) walks samples [n0, n0+spl) of channel c:
+// the zero-padded x plane is staged in LDS (no bounds tests in the product loop), threads
+// are laid over (output row, output column) once (no per-pixel division), each keeps R*S
+// fp32 partials over its pixels, and the workgroup reduces them in a fixed order (wave
+// shuffle tree, waves in order) into part[split][c][rs].
+template <int RSMAX>
+__global__ __launch_bounds__(256) void wgrad_dw_stage1(const float* __restrict__ x,
+                                                       const float* __restrict__ dy, int C, int H,
+                                                       int W, int OH, int OW, int R, int S,
+                                                       int st, int pad, int spl,
+                                                       float* __restrict__ part) {
+  extern __shared__ float xs[];  // [H + 2 pad][W + 2 pad]
+  __shared__ float red[4][RSMAX];
+  const int c = blockIdx.x, split = blockIdx.y;
+  const int n0 = split * spl;
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const int RS = R * S;
+  const int Hp = H + 2 * pad, Wp = W + 2 * pad;
+  // staging layout: thread -> (row r0 + k*rp, column cw) of the padded plane
+  const int scols = min(Wp, 256), srp = 256 / scols;
+  const int sr0 = tid / scols, scw = tid - sr0 * scols;
+  // product layout: thread -> (output row o0 + k*op, output column ocw)
+  const int ocols = min(OW, 256), orp = 256 / ocols;
+  const int or0 = tid / ocols, ocw = tid - or0 * ocols;
+  float acc[RSMAX];
+#pragma unroll
+  for (int j = 0; j < RSMAX; ++j) acc[j] = 0.0f;
+  const int OHW = OH * OW, HW = H * W;
+  for (int n = n0; n < n0 + spl; ++n) {
+    const float* xp = x + ((int64_t)n * C + c) * HW;
+    const float* dp = dy + ((int64_t)n * C + c) * OHW;
+    __syncthreads();  // the previous sample's products are done with the plane
+    if (sr0 < srp) {
+      for (int rr = sr0; rr < Hp; rr += srp) {
+        const int ih = rr - pad;
+        const bool rok = ih >= 0 && ih < H;
+        for (int cc = scw; cc < Wp; cc += scols) {
+          const int iw = cc - pad;
+          const bool ok = rok && iw >= 0 && iw < W;
+          const float v = xp[ok ? ih * W + iw : 0];
+          xs[rr * Wp + cc] = ok ? v : 0.0f;
+        }
+      }
+    }
+    __syncthreads();
+    if (or0 < orp) {
+      for (int oh = or0; oh < OH; oh += orp) {
+        for (int ow = ocw; ow < OW; ow += ocols) {
+          const float g = dp[oh * OW + ow];
+          const float* xr = xs + oh * st * Wp + ow * st;
+#pragma unroll
+          for (int j = 0; j < RSMAX; ++j) {
+            if (j < RS) {
+              const int r = j / S, q = j - r * S;
+              acc[j] = __fadd_rn(acc[j], __fmul_rn(g, xr[r * Wp + q]));
+            }
+          }
+        }
+      }
+    }
+  }
+#pragma unroll
+  for (int j = 0; j < RSMAX; ++j) {
+    float v = acc[j];
+#pragma unroll
+    for (int o = 32; o >= 1; o >>= 1) v = __fadd_rn(v, __shfl_xor(v, o));
+    if (lane == 0) red[w][j] = v;
+  }
+  __syncthreads();
+  if (tid < RS)
+    part[((int64_t)split * C + c) * RS + tid] =
+        __fadd_rn(__fadd_rn(__fadd_rn(red[0][tid], red[1][tid]), red[2][tid]), red[3][tid]);
+}
+
+static bool is_depthwise(int64_t C, int64_t Co, int64_t G) { return G == C && G == Co && G > 1; }
+static bool dw_lds_ok(int64_t H, int64_t W, int64_t pad) {
+  return (H + 2 * pad) * (W + 2 * pad) * (int64_t)sizeof(float) <= 128 * 1024;
+}
+
+// depthwise plan: samples per split so that C * nsplit fills the chip (~1024 workgroups)
+static int dw_splits(int64_t Nb, int64_t C, int* spl) {
+  int64_t ns = std::max<int64_t>(1, std::min<int64_t>(Nb, (1024 + C - 1) / C));
+  *spl = (int)((Nb + ns - 1) / ns);
+  // every split must hold exactly spl samples: shrink to a divisor of Nb
+  while (Nb % *spl) ++*spl;
+  return (int)(Nb / *spl);
 }
 
 static int wgrad_plan(int64_t Nb, int64_t C, int64_t H, int64_t W, int64_t Co, int64_t R,
@@ -263,6 +373,11 @@ using namespace ssq;
 extern "C" size_t ssq_conv_wgrad_workspace_size(int64_t Nb, int64_t C, int64_t H, int64_t W,
                                                 int64_t Co, int64_t R, int64_t S, int64_t stride,
                                                 int64_t pad, int64_t groups) {
+  if (is_depthwise(C, Co, groups) && R * S <= 25 && Nb >= 1 && dw_lds_ok(H, W, pad)) {
+    int spl;
+    const int ns = dw_splits(Nb, C, &spl);
+    return (size_t)ns * (size_t)C * (size_t)(R * S) * sizeof(float);
+  }
   WgradGeo g;
   size_t lds;
   if (wgrad_plan(Nb, C, H, W, Co, R, S, stride, pad, groups, g, &lds)) return 0;
@@ -274,13 +389,44 @@ extern "C" int ssq_conv_wgrad(const float* x, const float* dy, int64_t Nb, int64
                               int64_t pad, int64_t groups, float* dw, void* ws, size_t ws_bytes,
                               ssq_stream_t stream) {
   SSQ_REQUIRE(x && dy && dw, SSQ_E_ARG, "ssq_conv_wgrad: null pointer");
+  hipStream_t s = (hipStream_t)stream;
+  if (is_depthwise(C, Co, groups) && R * S <= 25 && dw_lds_ok(H, W, pad)) {
+    SSQ_REQUIRE(Nb >= 1 && H >= 1 && W >= 1 && stride >= 1 && pad >= 0, SSQ_E_ARG,
+                "ssq_conv_wgrad: bad geometry");
+    const int64_t OH = (H + 2 * pad - R) / stride + 1, OW = (W + 2 * pad - S) / stride + 1;
+    SSQ_REQUIRE(OH >= 1 && OW >= 1 && Nb * C * H * W < (1ll << 31) && Nb * C * OH * OW < (1ll << 31),
+                SSQ_E_ARG, "ssq_conv_wgrad: sizes");
+    int spl;
+    const int ns = dw_splits(Nb, C, &spl);
+    const size_t need = (size_t)ns * (size_t)C * (size_t)(R * S) * sizeof(float);
+    SSQ_REQUIRE(ws && ws_bytes >= need, SSQ_E_WS, "ssq_conv_wgrad: workspace too small");
+    const dim3 grid((unsigned)C, (unsigned)ns);
+    const size_t lds = (size_t)(H + 2 * pad) * (W + 2 * pad) * sizeof(float);
+    static bool dw_attr = false;
+    if (!dw_attr) {  // dynamic LDS beyond 64 KiB must be opted into
+      hipFuncSetAttribute((const void*)wgrad_dw_stage1<9>,
+                          hipFuncAttributeMaxDynamicSharedMemorySize, 128 * 1024);
+      hipFuncSetAttribute((const void*)wgrad_dw_stage1<25>,
+                          hipFuncAttributeMaxDynamicSharedMemorySize, 128 * 1024);
+      dw_attr = true;
+    }
+    if (R * S <= 9)
+      hipLaunchKernelGGL(wgrad_dw_stage1<9>, grid, dim3(256), lds, s, x, dy, (int)C, (int)H, (int)W,
+                         (int)OH, (int)OW, (int)R, (int)S, (int)stride, (int)pad, spl, (float*)ws);
+    else
+      hipLaunchKernelGGL(wgrad_dw_stage1<25>, grid, dim3(256), lds, s, x, dy, (int)C, (int)H, (int)W,
+                         (int)OH, (int)OW, (int)R, (int)S, (int)stride, (int)pad, spl, (float*)ws);
+    const int64_t n = C * R * S;
+    hipLaunchKernelGGL(wgrad_stage2, dim3((unsigned)std::min<int64_t>((n + 63) / 64, 4096)),
+                       dim3(256), 0, s, (const float*)ws, ns, n, dw);
+    return check_launch("ssq_conv_wgrad");
+  }
   WgradGeo g;
   size_t lds;
   int rc = wgrad_plan(Nb, C, H, W, Co, R, S, stride, pad, groups, g, &lds);
   if (rc) return rc;
   const size_t need = (size_t)g.nsplit * (size_t)Co * (size_t)g.Ncol * sizeof(float);
   SSQ_REQUIRE(ws && ws_bytes >= need, SSQ_E_WS, "ssq_conv_wgrad: workspace too small");
-  hipStream_t s = (hipStream_t)stream;
   static bool lds_attr = false;
   if (!lds_attr) {  // dynamic LDS beyond 64 KiB must be opted into
     hipFuncSetAttribute((const void*)wgrad_stage1, hipFuncAttributeMaxDynamicSharedMemorySize,
@@ -290,7 +436,7 @@ extern "C" int ssq_conv_wgrad(const float* x, const float* dy, int64_t Nb, int64
   const dim3 grid((g.Ncol + kTN - 1) / kTN, g.m_tiles * g.G, g.nsplit);
   hipLaunchKernelGGL(wgrad_stage1, grid, dim3(256), lds, s, x, dy, g, (float*)ws);
   const int64_t n = (int64_t)Co * g.Ncol;
-  hipLaunchKernelGGL(wgrad_stage2, dim3(grid_for(n, 256, 2048)), dim3(256), 0, s,
-                     (const float*)ws, g.nsplit, n, dw);
+  hipLaunchKernelGGL(wgrad_stage2, dim3((unsigned)std::min<int64_t>((n + 63) / 64, 4096)),
+                     dim3(256), 0, s, (const float*)ws, g.nsplit, n, dw);
   return check_launch("ssq_conv_wgrad");
 }

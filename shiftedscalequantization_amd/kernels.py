@@ -879,11 +879,12 @@ class Conv2dFn(torch.autograd.Function):
 
 
 # When the conv weight gradient runs on K17 (tools/wgrad_bench.py, batch 32, MI355X):
-#   'auto'   grouped, non-depthwise convs always (MIOpen's grouped wrw is 4x slower: RegNetX
-#            g=2 956 vs 233 us); under the reference's torch.backends.cudnn.deterministic
-#            also every stride-2 conv and every output plane >= 400 pixels, where MIOpen's
-#            deterministic solvers are 3-8x slower than K17 (stride-1 14x14 / 7x7 planes are
-#            as fast on MIOpen).  Depthwise convs stay on MIOpen (K17 is 3-6x slower there).
+#   'auto'   every grouped conv: depthwise ones on K17's LDS-staged reduction (MobileNetV2
+#            144x56x56 3x3: 74 vs 866 us on MIOpen, either mode), other grouped ones on
+#            its MFMA GEMM (RegNetX g=2: 217 vs 955 us); under the reference's
+#            torch.backends.cudnn.deterministic also every stride-2 conv and every output
+#            plane >= 400 pixels, where MIOpen's deterministic solvers are 3-8x slower than
+#            K17 (stride-1 14x14 / 7x7 planes are as fast on MIOpen).
 #   'always' / 'never' (MIOpen's choice) for A/B runs.
 WGRAD_POLICY = "auto"
 
@@ -893,8 +894,6 @@ def _use_k17(x, weight, stride, padding, groups=1):
         return True
     if WGRAD_POLICY != "auto":
         return False
-    if groups > 1 and weight.shape[1] == 1:
-        return False                      # depthwise
     if groups > 1:
         return True
     if torch.backends.cudnn.deterministic:

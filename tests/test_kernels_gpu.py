@@ -684,7 +684,10 @@ def test_lp_loss_rows_equals_gathered(K, row_shape, p):
     # (Nb, C, H, Co, k, stride, pad, groups)
     (4, 64, 56, 64, 3, 1, 1, 1), (3, 16, 15, 24, 3, 2, 1, 1), (2, 32, 14, 48, 1, 2, 0, 1),
     (2, 24, 9, 24, 3, 1, 1, 24), (2, 48, 12, 96, 3, 1, 1, 2), (5, 130, 7, 70, 3, 1, 1, 1),
-    (1, 3, 32, 16, 7, 2, 3, 1)])
+    (1, 3, 32, 16, 7, 2, 3, 1),
+    # depthwise path: stride 2, planes wider than a wave, 5x5, odd batch
+    (3, 32, 57, 32, 3, 2, 1, 32), (2, 144, 28, 144, 3, 1, 1, 144), (5, 16, 11, 16, 5, 1, 2, 16),
+    (32, 8, 7, 8, 3, 1, 1, 8)])
 def test_conv_wgrad_matches_fp64(K, cfg):
     """K17 weight gradient vs the fp64 CPU gradient: error within the fp32 accumulation
     bound, bit-identical run to run, and the autograd wrapper equals the direct call."""
