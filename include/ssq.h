@@ -293,6 +293,19 @@ int ssq_conv_wgrad(const float* x, const float* dy, int64_t Nb, int64_t C, int64
                    int64_t Co, int64_t R, int64_t S, int64_t stride, int64_t pad, int64_t groups,
                    float* dw, void* ws, size_t ws_bytes, ssq_stream_t stream);
 
+/* ---------------------------------------------------------------- K18 depthwise conv
+ * Depthwise (groups == C == Co) fp32 NCHW conv, dilation 1, R*S <= 25, zero padding:
+ *   y[n,c,oh,ow] = sum_{r,s} w[c,r,s] * x[n,c,oh*st+r-pad, ow*st+s-pad]
+ * and its input gradient dx (the same sum transposed).  The MobileNetV2 blocks' depthwise
+ * F.conv2d of QuantModule.forward (quant_layer.py:250) and its autograd; one plane per
+ * workgroup staged in LDS ((H+2pad)*(W+2pad)*4 <= 128 KiB).  Deterministic.           */
+int ssq_dwconv_fwd(const float* x, const float* w, float* y, int64_t Nb, int64_t C, int64_t H,
+                   int64_t W, int64_t R, int64_t S, int64_t stride, int64_t pad,
+                   ssq_stream_t stream);
+int ssq_dwconv_bwd_data(const float* dy, const float* w, float* dx, int64_t Nb, int64_t C,
+                        int64_t H, int64_t W, int64_t R, int64_t S, int64_t stride, int64_t pad,
+                        ssq_stream_t stream);
+
 /* ---------------------------------------------------------------- K15/K16 packed export
  * Low-bit weight export (replaces the fp32 state_dict + pickled shift
  * choice of main_cifar10.py:86 / myScaledMethods.py:204-205).  A hard weight quantizer's

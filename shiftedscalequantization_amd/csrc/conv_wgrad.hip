@@ -238,7 +238,7 @@ __global__ __launch_bounds__(256) void wgrad_dw_stage1(const float* __restrict__
                                                        const float* __restrict__ dy, int C, int H,
                                                        int W, int OH, int OW, int R, int S,
                                                        int st, int pad, int spl,
-                                                       float* __restrict__ part) {
+                                                       FastDiv dWp, float* __restrict__ part) {
   extern __shared__ float xs[];  // [H + 2 pad][W + 2 pad]
   __shared__ float red[4][RSMAX];
   const int c = blockIdx.x, split = blockIdx.y;
@@ -246,9 +246,7 @@ __global__ __launch_bounds__(256) void wgrad_dw_stage1(const float* __restrict__
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
   const int RS = R * S;
   const int Hp = H + 2 * pad, Wp = W + 2 * pad;
-  // staging layout: thread -> (row r0 + k*rp, column cw) of the padded plane
-  const int scols = min(Wp, 256), srp = 256 / scols;
-  const int sr0 = tid / scols, scw = tid - sr0 * scols;
+  const int HpWp = Hp * Wp;
   // product layout: thread -> (output row o0 + k*op, output column ocw)
   const int ocols = min(OW, 256), orp = 256 / ocols;
   const int or0 = tid / ocols, ocw = tid - or0 * ocols;
@@ -260,17 +258,21 @@ __global__ __launch_bounds__(256) void wgrad_dw_stage1(const float* __restrict__
     const float* xp = x + ((int64_t)n * C + c) * HW;
     const float* dp = dy + ((int64_t)n * C + c) * OHW;
     __syncthreads();  // the previous sample's products are done with the plane
-    if (sr0 < srp) {
-      for (int rr = sr0; rr < Hp; rr += srp) {
-        const int ih = rr - pad;
-        const bool rok = ih >= 0 && ih < H;
-        for (int cc = scw; cc < Wp; cc += scols) {
-          const int iw = cc - pad;
-          const bool ok = rok && iw >= 0 && iw < W;
-          const float v = xp[ok ? ih * W + iw : 0];
-          xs[rr * Wp + cc] = ok ? v : 0.0f;
-        }
+    // 8 loads in flight per thread, then the 8 LDS stores
+    for (int e0 = tid; e0 < HpWp; e0 += 256 * 8) {
+      float v[8];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) {
+        const int e = e0 + 256 * u;
+        const int rr = (int)fdiv((uint32_t)e, dWp), cc = e - rr * Wp;
+        const int ih = rr - pad, iw = cc - pad;
+        const bool ok = e < HpWp && ih >= 0 && ih < H && iw >= 0 && iw < W;
+        const float t = xp[ok ? ih * W + iw : 0];
+        v[u] = ok ? t : 0.0f;
       }
+#pragma unroll
+      for (int u = 0; u < 8; ++u)
+        if (e0 + 256 * u < HpWp) xs[e0 + 256 * u] = v[u];
     }
     __syncthreads();
     if (or0 < orp) {
@@ -412,10 +414,12 @@ extern "C" int ssq_conv_wgrad(const float* x, const float* dy, int64_t Nb, int64
     }
     if (R * S <= 9)
       hipLaunchKernelGGL(wgrad_dw_stage1<9>, grid, dim3(256), lds, s, x, dy, (int)C, (int)H, (int)W,
-                         (int)OH, (int)OW, (int)R, (int)S, (int)stride, (int)pad, spl, (float*)ws);
+                         (int)OH, (int)OW, (int)R, (int)S, (int)stride, (int)pad, spl,
+                         make_fastdiv((uint32_t)(W + 2 * pad)), (float*)ws);
     else
       hipLaunchKernelGGL(wgrad_dw_stage1<25>, grid, dim3(256), lds, s, x, dy, (int)C, (int)H, (int)W,
-                         (int)OH, (int)OW, (int)R, (int)S, (int)stride, (int)pad, spl, (float*)ws);
+                         (int)OH, (int)OW, (int)R, (int)S, (int)stride, (int)pad, spl,
+                         make_fastdiv((uint32_t)(W + 2 * pad)), (float*)ws);
     const int64_t n = C * R * S;
     hipLaunchKernelGGL(wgrad_stage2, dim3((unsigned)std::min<int64_t>((n + 63) / 64, 4096)),
                        dim3(256), 0, s, (const float*)ws, ns, n, dw);

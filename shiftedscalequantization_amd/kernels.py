@@ -855,6 +855,74 @@ def conv_wgrad(x, dy, w_shape, stride, padding, groups):
     return dw
 
 
+# ------------------------------------------------------------------ K18 depthwise conv
+def dwconv_supported(x, weight, stride, padding, dilation, groups):
+    """Depthwise shapes K18 handles: fp32 NCHW on the device, groups == C == Co, square
+    stride / padding, dilation 1, R*S <= 25, the padded input plane within 128 KiB."""
+    if x.dim() != 4 or weight.dim() != 4 or not x.is_cuda or x.dtype != torch.float32:
+        return False
+    if groups <= 1 or groups != x.shape[1] or groups != weight.shape[0] or weight.shape[1] != 1:
+        return False
+    if not isinstance(stride, int) and len(set(stride)) != 1:
+        return False
+    if not isinstance(padding, int) and (isinstance(padding, str) or len(set(padding)) != 1):
+        return False
+    if (dilation if isinstance(dilation, int) else max(dilation)) != 1:
+        return False
+    pad = padding if isinstance(padding, int) else padding[0]
+    R, S = int(weight.shape[2]), int(weight.shape[3])
+    return R * S <= 25 and (x.shape[2] + 2 * pad) * (x.shape[3] + 2 * pad) * 4 <= 128 * 1024
+
+
+def _dw_dims(x_shape, w_shape, stride, padding):
+    st = stride if isinstance(stride, int) else stride[0]
+    pad = padding if isinstance(padding, int) else padding[0]
+    Nb, C, H, W = (int(v) for v in x_shape)
+    return Nb, C, H, W, int(w_shape[2]), int(w_shape[3]), int(st), int(pad)
+
+
+def dwconv_fwd(x, weight, stride, padding):
+    Nb, C, H, W, R, S, st, pad = _dw_dims(x.shape, weight.shape, stride, padding)
+    x, xp = fptr(x.detach(), "x")
+    w, wp = fptr(weight.detach(), "weight")
+    y = torch.empty((Nb, C, (H + 2 * pad - R) // st + 1, (W + 2 * pad - S) // st + 1),
+                    dtype=torch.float32, device=x.device)
+    call("ssq_dwconv_fwd", xp, wp, _vp(y), Nb, C, H, W, R, S, st, pad, stream_of(x))
+    return y
+
+
+def dwconv_bwd_data(dy, weight, x_shape, stride, padding):
+    Nb, C, H, W, R, S, st, pad = _dw_dims(x_shape, weight.shape, stride, padding)
+    dy, dp = fptr(dy.detach(), "dy")
+    w, wp = fptr(weight.detach(), "weight")
+    dx = torch.empty(tuple(x_shape), dtype=torch.float32, device=dy.device)
+    call("ssq_dwconv_bwd_data", dp, wp, _vp(dx), Nb, C, H, W, R, S, st, pad, stream_of(dy))
+    return dx
+
+
+class DwConv2dFn(torch.autograd.Function):
+    """Depthwise F.conv2d on K18 (forward, input gradient) and K17's depthwise reduction
+    (weight gradient): deterministic, no MIOpen naive kernels."""
+
+    @staticmethod
+    def forward(ctx, x, weight, stride, padding):
+        ctx.save_for_backward(x, weight)
+        ctx.cfg = (stride, padding)
+        return dwconv_fwd(x, weight, stride, padding)
+
+    @staticmethod
+    def backward(ctx, g):
+        x, weight = ctx.saved_tensors
+        stride, padding = ctx.cfg
+        g = g.contiguous()
+        gx = gw = None
+        if ctx.needs_input_grad[0]:
+            gx = dwconv_bwd_data(g, weight, x.shape, stride, padding)
+        if ctx.needs_input_grad[1]:
+            gw = conv_wgrad(x, g, weight.shape, stride, padding, int(weight.shape[0]))
+        return gx, gw, None, None
+
+
 class Conv2dFn(torch.autograd.Function):
     """F.conv2d whose weight gradient runs on K17 (deterministic, MFMA); the forward and
     the input gradient stay on MIOpen."""
@@ -905,8 +973,19 @@ def _use_k17(x, weight, stride, padding, groups=1):
     return False
 
 
+# Depthwise convs on K18 + K17 ('auto'; MIOpen runs them on naive direct kernels) or on
+# MIOpen ('never').
+DWCONV_POLICY = "auto"
+
+
 def conv2d(x, weight, stride=1, padding=0, dilation=1, groups=1):
-    """F.conv2d without bias, K17 weight gradient when the weight needs one (policy above)."""
+    """F.conv2d without bias: depthwise convs on K18/K17 (DWCONV_POLICY), otherwise MIOpen
+    with the K17 weight gradient when the weight needs one (WGRAD_POLICY)."""
+    if DWCONV_POLICY == "auto" and dwconv_supported(x, weight, stride, padding, dilation, groups) \
+            and x.is_contiguous():
+        if torch.is_grad_enabled() and (x.requires_grad or weight.requires_grad):
+            return DwConv2dFn.apply(x, weight, stride, padding)
+        return dwconv_fwd(x, weight, stride, padding)
     if weight.requires_grad and torch.is_grad_enabled() and \
             conv_wgrad_supported(x, weight, stride, padding, dilation, groups) and \
             _use_k17(x, weight, stride, padding, groups):

@@ -18,15 +18,33 @@ BLOCKS = {"layer1.0": (64, 56, 56), "layer2.0": (64, 56, 56), "layer3.0": (128, 
 
 
 def _block(qnn, name):
-    m = qnn.model
+    m = qnn.model if hasattr(qnn, "model") else qnn
     for part in name.split("."):
         m = m[int(part)] if part.isdigit() else getattr(m, part)
     return m
 
 
-def run_block(dev, name, n_cali=1024, iters=200, warmup=20, rank=0, bias_cal=False):
+def _block_input_shape(cnn, name, dev):
+    """Per-sample input shape of block `name` of the FP model (one 224x224 forward)."""
+    shape = {}
+
+    def hook(m, i, o):
+        shape.setdefault("s", i[0].shape)
+
+    h = _block(cnn, name).register_forward_hook(hook)
+    with torch.no_grad():
+        cnn(torch.zeros(1, 3, 224, 224, device=dev))
+    h.remove()
+    return tuple(shape["s"][1:])
+
+
+def run_block(dev, name, n_cali=1024, iters=200, warmup=20, rank=0, bias_cal=False,
+              arch="resnet18"):
     torch.manual_seed(1005 + rank)
-    cnn = nets.resnet18().to(dev).eval()
+    cnn = nets.ARCHS[arch]().eval()
+    # (on the host: a device forward under cudnn.benchmark would tune every conv of the net)
+    in_shape = BLOCKS[name] if arch == "resnet18" else _block_input_shape(cnn, name, "cpu")
+    cnn = cnn.to(dev)
     qnn = QuantModel(cnn, {"n_bits": 2, "channel_wise": True, "scale_method": "max"},
                      {"n_bits": 4, "channel_wise": False, "scale_method": "mse", "leaf_param": True})
     qnn.to(dev).eval()
@@ -40,7 +58,7 @@ def run_block(dev, name, n_cali=1024, iters=200, warmup=20, rank=0, bias_cal=Fal
             m.weight_quantizer = ChannelQuant(1.0, uaq=m.weight_quantizer, weight_tensor=m.org_weight,
                                               shiftTarget=SHIFTS, name=name)
     g = torch.Generator(device=dev).manual_seed(1005 + rank)
-    inp = torch.empty((n_cali,) + BLOCKS[name], device=dev).normal_(generator=g).relu_()
+    inp = torch.empty((n_cali,) + in_shape, device=dev).normal_(generator=g).relu_()
     with torch.no_grad():
         block.set_quant_state(False, False)
         out = torch.cat([block(inp[i:i + 64]) for i in range(0, n_cali, 64)])

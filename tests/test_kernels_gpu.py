@@ -715,6 +715,42 @@ def test_conv_wgrad_matches_fp64(K, cfg):
     np.testing.assert_array_equal(host(wd.grad).view(np.int32), host(dw1).view(np.int32))
 
 
+@pytest.mark.parametrize("cfg", [
+    # (Nb, C, H, k, stride, pad): MobileNetV2's 3x3 s1 / s2, odd sizes, 5x5, wide plane
+    (4, 144, 56, 3, 1, 1), (3, 96, 57, 3, 2, 1), (2, 32, 112, 3, 1, 1), (5, 16, 11, 5, 1, 2),
+    (2, 24, 9, 3, 2, 0), (32, 8, 7, 3, 1, 1)])
+def test_dwconv_matches_fp64(K, cfg):
+    """K18 depthwise forward and input gradient vs fp64 torch: within the fp32 rounding
+    bound of an R*S-term sum, bit-identical run to run; K.conv2d's autograd routes the
+    depthwise conv through K18 (forward, dx) and K17 (dw)."""
+    Nb, C, H, k, st, pad = cfg
+    gen = torch.Generator().manual_seed(sum(cfg))
+    x = torch.randn(Nb, C, H, H, generator=gen)
+    w = torch.randn(C, 1, k, k, generator=gen)
+    y64 = torch.nn.functional.conv2d(x.double(), w.double(), None, st, pad, 1, C)
+    ymag = torch.nn.functional.conv2d(x.double().abs(), w.double().abs(), None, st, pad, 1, C)
+    dy = torch.randn(y64.shape, generator=gen)
+    dx64 = torch.nn.grad.conv2d_input(x.shape, w.double(), dy.double(), st, pad, 1, C)
+    dxmag = torch.nn.grad.conv2d_input(x.shape, w.double().abs(), dy.double().abs(), st, pad, 1, C)
+    xd, wd, dyd = x.cuda(), w.cuda(), dy.cuda()
+    y1 = K.dwconv_fwd(xd, wd, st, pad)
+    y2 = K.dwconv_fwd(xd, wd, st, pad)
+    np.testing.assert_array_equal(host(y1).view(np.int32), host(y2).view(np.int32))
+    err = (y1.double().cpu() - y64).abs()
+    assert bool((err <= 1e-6 * ymag + 1e-30).all()), float((err / ymag.clamp_min(1e-30)).max())
+    dx1 = K.dwconv_bwd_data(dyd, wd, x.shape, st, pad)
+    err = (dx1.double().cpu() - dx64).abs()
+    assert bool((err <= 1e-6 * dxmag + 1e-30).all()), float((err / dxmag.clamp_min(1e-30)).max())
+    xg = xd.clone().requires_grad_(True)
+    wg = wd.clone().requires_grad_(True)
+    out = K.conv2d(xg, wg, st, pad, 1, C)
+    np.testing.assert_array_equal(host(out).view(np.int32), host(y1).view(np.int32))
+    out.backward(dyd)
+    np.testing.assert_array_equal(host(xg.grad).view(np.int32), host(dx1).view(np.int32))
+    dw = K.conv_wgrad(xd, dyd, w.shape, st, pad, C)
+    np.testing.assert_array_equal(host(wg.grad).view(np.int32), host(dw).view(np.int32))
+
+
 def test_affine_stays_live_after_raw_device_updates(K):
     """gamma^z/phi^z updated by a raw device write (fused Adam, graph replay: no torch
     version bump) after being trainable must still be applied once frozen again."""
