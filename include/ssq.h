@@ -78,6 +78,11 @@ int ssq_fq_bwd(const float* x, const float* gy, const float* delta, const float*
 int ssq_fq_relu_bwd(const float* x, const float* gy, const float* delta, const float* zp,
                     int64_t n, int qmin, int qmax, float* gx, float* gdelta, float* gzp,
                     void* ws, size_t ws_bytes, ssq_stream_t stream);
+/* The same for x a ReLU6 output (MobileNetV2's QuantInvertedResidual, quant_block.py:
+ * 205-239): gx = 0 where x <= 0 or x >= 6 (torch hardtanh_backward).                  */
+int ssq_fq_relu6_bwd(const float* x, const float* gy, const float* delta, const float* zp,
+                     int64_t n, int qmin, int qmax, float* gx, float* gdelta, float* gzp,
+                     void* ws, size_t ws_bytes, ssq_stream_t stream);
 
 /* ---------------------------------------------------------------- K3/K4 scale init
  * init_quantization_scale (quant_layer.py:100-166) for `rows` independent rows of
@@ -231,12 +236,15 @@ int ssq_gather_rows2(const float* src0, float* dst0, int64_t row0, const float* 
 /* ---------------------------------------------------------------- K13 fused epilogue
  * QuantModule conv bias add (quant_layer.py:250), the block's residual add and ReLU
  * (quant_block.py:99-117) in one pass, in the reference's op order:
- *   out = act((y + bias[c]) + res),  c = (i / hw) % C,  act = ReLU if relu else identity.
- * bias / res may be NULL.  ssq_relu_bwd: gin = out <= 0 ? 0 : g (torch's ReLU backward on
- * its output).  n < 2^31.                                                                */
+ *   out = act((y + bias[c]) + res),  c = (i / hw) % C,
+ * act by the `relu` code of every K13 entry point: 0 identity, 1 ReLU, 2 ReLU6 (torch
+ * clamp semantics: -0.0 and NaN kept).  bias / res may be NULL.  ssq_relu_bwd: gin =
+ * out <= 0 ? 0 : g (torch's ReLU backward on its output); ssq_relu6_bwd: gin = 0 where
+ * out <= 0 or out >= 6 (hardtanh_backward).  n < 2^31.                                   */
 int ssq_bias_act(const float* y, const float* bias, const float* res, float* out, int64_t n,
                  int64_t hw, int64_t C, int relu, ssq_stream_t stream);
 int ssq_relu_bwd(const float* g, const float* out, float* gin, int64_t n, ssq_stream_t stream);
+int ssq_relu6_bwd(const float* g, const float* out, float* gin, int64_t n, ssq_stream_t stream);
 /* ssq_bias_act with the following per-tensor activation fake-quant (quant_layer.py:92-98,
  * applied at quant_layer.py:272 / quant_block.py:118) in the same pass:
  *   yq = (clamp(rint(out/delta[0]) + zp[0], qmin, qmax) - zp[0]) * delta[0]

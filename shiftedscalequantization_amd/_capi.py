@@ -29,6 +29,7 @@ SIGNATURES = {
     "ssq_fq_bwd_workspace_size": (_sz, [_i64, _i64, _i64]),
     "ssq_fq_bwd": (_i, [_p, _p, _p, _p, _i64, _i64, _i64, _i, _i, _p, _p, _p, _p, _sz, _p]),
     "ssq_fq_relu_bwd": (_i, [_p, _p, _p, _p, _i64, _i, _i, _p, _p, _p, _p, _sz, _p]),
+    "ssq_fq_relu6_bwd": (_i, [_p, _p, _p, _p, _i64, _i, _i, _p, _p, _p, _p, _sz, _p]),
     "ssq_scale_init_workspace_size": (_sz, [_i64, _i64, _i]),
     "ssq_scale_init": (_i, [_p, _i64, _i64, _i, _i, _i, _i, _p, _p, _p, _p, _p, _sz, _p]),
     "ssq_shift_init_workspace_size": (_sz, [_i64, _i64, _i64, _i, _i]),
@@ -58,6 +59,7 @@ SIGNATURES = {
     "ssq_gather_rows2": (_i, [_p, _p, _i64, _p, _p, _i64, _p, _i64, _p]),
     "ssq_bias_act": (_i, [_p, _p, _p, _p, _i64, _i64, _i64, _i, _p]),
     "ssq_relu_bwd": (_i, [_p, _p, _p, _i64, _p]),
+    "ssq_relu6_bwd": (_i, [_p, _p, _p, _i64, _p]),
     "ssq_bias_act_fq": (_i, [_p, _p, _p, _p, _p, _i64, _i64, _i64, _i, _p, _p, _i, _i, _p]),
     "ssq_epilogue_fwd": (_i, [_p, _p, _p, _p, _p, _p, _p, _i64, _i64, _i64, _i, _p, _p, _i, _i,
                               _p]),

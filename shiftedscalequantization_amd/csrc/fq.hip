@@ -264,7 +264,7 @@ __global__ __launch_bounds__(kBlock) void fq_fwd_multi_kernel(SegTable tab) {
 // partial layout in ws: per block 4 doubles {sum gy*(q-zp), sum g_int*((x/d)/d), sum g_int, sum gy*d}
 // RELU: x is a ReLU output and gx is written at the ReLU's input (torch threshold_backward
 // on the output: x <= 0 -> 0), i.e. fq backward and relu_bwd in one pass.
-template <bool RELU>
+template <int ACT>
 __global__ __launch_bounds__(kBlock) void fq_bwd_pt(const float* __restrict__ x,
                                                     const float* __restrict__ gy,
                                                     const float* __restrict__ delta,
@@ -283,7 +283,7 @@ __global__ __launch_bounds__(kBlock) void fq_bwd_pt(const float* __restrict__ x,
     const float q = clampf(v, lo, hi);
     const float gq = __fmul_rn(g, d);
     const float gi = m ? gq : 0.0f;
-    if (gx) gx[i] = (RELU && xv <= 0.0f) ? 0.0f : gi / d;
+    if (gx) gx[i] = (ACT && !act_pass<ACT>(xv)) ? 0.0f : gi / d;
     if (part) {
       a0 += (double)g * (double)__fsub_rn(q, z);
       a1 += (double)gi * (double)(t / d);
@@ -307,7 +307,7 @@ __global__ __launch_bounds__(kBlock) void fq_bwd_pt(const float* __restrict__ x,
 
 // float4 form of fq_bwd_pt (x, gy, gx 16-B aligned): two float4 loads per 4 elements,
 // (x/d)/d as t * (1/d) (it only feeds the reduction), zp sums only when asked for.
-template <bool ZP, bool RELU>
+template <bool ZP, int ACT>
 __global__ __launch_bounds__(kBlock) void fq_bwd_pt4(const f32x4* __restrict__ x,
                                                      const f32x4* __restrict__ gy,
                                                      const float* __restrict__ delta,
@@ -331,7 +331,7 @@ __global__ __launch_bounds__(kBlock) void fq_bwd_pt4(const f32x4* __restrict__ x
       const float q = clampf(v, lo, hi);
       const float gq = __fmul_rn(gs[j], d);
       const float gi = m ? gq : 0.0f;
-      go[j] = (RELU && xs[j] <= 0.0f) ? 0.0f : gi / d;
+      go[j] = (ACT && !act_pass<ACT>(xs[j])) ? 0.0f : gi / d;
       if (part) {
         a0 += (double)gs[j] * (double)__fsub_rn(q, z);
         a1 += (double)gi * (double)__fmul_rn(t, rd);
@@ -669,7 +669,7 @@ extern "C" size_t ssq_fq_bwd_workspace_size(int64_t n, int64_t inner, int64_t nc
   return nch == 1 ? (size_t)kBwdBlocks * 4 * sizeof(double) : 0;
 }
 
-static int fq_bwd(const char* what, bool relu, const float* x, const float* gy,
+static int fq_bwd(const char* what, int relu, const float* x, const float* gy,
                   const float* delta, const float* zp, int64_t n, int64_t inner, int64_t nch,
                   int qmin, int qmax, float* gx, float* gdelta, float* gzp, void* ws,
                   size_t ws_bytes, hipStream_t s) {
@@ -685,12 +685,14 @@ static int fq_bwd(const char* what, bool relu, const float* x, const float* gy,
     const int grid = grid_for(vec4 ? n / 4 : n, kBlock, kBwdBlocks);
     double* part = want_red ? (double*)ws : nullptr;
     if (vec4) {
-      auto k = gzp ? (relu ? fq_bwd_pt4<true, true> : fq_bwd_pt4<true, false>)
-                   : (relu ? fq_bwd_pt4<false, true> : fq_bwd_pt4<false, false>);
+      auto k = gzp ? (relu == 2 ? fq_bwd_pt4<true, 2> : relu ? fq_bwd_pt4<true, 1>
+                                                             : fq_bwd_pt4<true, 0>)
+                   : (relu == 2 ? fq_bwd_pt4<false, 2> : relu ? fq_bwd_pt4<false, 1>
+                                                              : fq_bwd_pt4<false, 0>);
       hipLaunchKernelGGL(k, dim3(grid), dim3(kBlock), 0, s, (const f32x4*)x, (const f32x4*)gy,
                          delta, zp, n / 4, lo, hi, (f32x4*)gx, part);
     } else {
-      auto k = relu ? fq_bwd_pt<true> : fq_bwd_pt<false>;
+      auto k = relu == 2 ? fq_bwd_pt<2> : relu ? fq_bwd_pt<1> : fq_bwd_pt<0>;
       hipLaunchKernelGGL(k, dim3(grid), dim3(kBlock), 0, s, x, gy, delta, zp, n, lo, hi, gx,
                          part);
     }
@@ -711,7 +713,7 @@ extern "C" int ssq_fq_bwd(const float* x, const float* gy, const float* delta, c
                           int64_t n, int64_t inner, int64_t nch, int qmin, int qmax, float* gx,
                           float* gdelta, float* gzp, void* ws, size_t ws_bytes,
                           ssq_stream_t stream) {
-  return fq_bwd("ssq_fq_bwd", false, x, gy, delta, zp, n, inner, nch, qmin, qmax, gx, gdelta,
+  return fq_bwd("ssq_fq_bwd", 0, x, gy, delta, zp, n, inner, nch, qmin, qmax, gx, gdelta,
                 gzp, ws, ws_bytes, (hipStream_t)stream);
 }
 
@@ -719,7 +721,15 @@ extern "C" int ssq_fq_relu_bwd(const float* x, const float* gy, const float* del
                                const float* zp, int64_t n, int qmin, int qmax, float* gx,
                                float* gdelta, float* gzp, void* ws, size_t ws_bytes,
                                ssq_stream_t stream) {
-  return fq_bwd("ssq_fq_relu_bwd", true, x, gy, delta, zp, n, n, 1, qmin, qmax, gx, gdelta,
+  return fq_bwd("ssq_fq_relu_bwd", 1, x, gy, delta, zp, n, n, 1, qmin, qmax, gx, gdelta,
+                gzp, ws, ws_bytes, (hipStream_t)stream);
+}
+
+extern "C" int ssq_fq_relu6_bwd(const float* x, const float* gy, const float* delta,
+                                const float* zp, int64_t n, int qmin, int qmax, float* gx,
+                                float* gdelta, float* gzp, void* ws, size_t ws_bytes,
+                                ssq_stream_t stream) {
+  return fq_bwd("ssq_fq_relu6_bwd", 2, x, gy, delta, zp, n, n, 1, qmin, qmax, gx, gdelta,
                 gzp, ws, ws_bytes, (hipStream_t)stream);
 }
 

@@ -141,7 +141,7 @@ __global__ __launch_bounds__(kBlock) void gather2_kernel(const float* __restrict
 // out = act(y + bias[c] (+ res)),  c = (i / hw) % C, in the reference's op order (conv
 // bias add, residual add, ReLU: three separate fp32 roundings -> bit-identical to the
 // eager sequence), one pass instead of three.
-template <bool RES, bool RELU, bool QUANT, bool AFFINE>
+template <bool RES, int ACT, bool QUANT, bool AFFINE>
 __global__ __launch_bounds__(kBlock) void bias_act_kernel(const float* __restrict__ y,
                                                           const float* __restrict__ bias,
                                                           const float* __restrict__ res,
@@ -166,8 +166,7 @@ __global__ __launch_bounds__(kBlock) void bias_act_kernel(const float* __restric
     float t = bias ? __fadd_rn(v, bias[c]) : v;
     if (AFFINE) t = __fadd_rn(__fmul_rn(t, gamma[c]), phi[c]);  // out*alpha_out + beta_out
     if (RES) t = __fadd_rn(t, rv);
-    if (RELU) t = t < 0.0f ? 0.0f : t;  // torch clamp_min: std::max(t, 0) keeps -0 and NaN
-    return t;
+    return act_fwd<ACT>(t);  // torch clamp: keeps -0 and NaN
   };
   auto fq = [&](float t) {
     float q;
@@ -203,8 +202,9 @@ __global__ __launch_bounds__(kBlock) void bias_act_kernel(const float* __restric
   }
 }
 
-// ReLU backward (torch threshold_backward on the output): gin = out <= 0 ? 0 : g
-// (a NaN output passes its gradient, as in torch)
+// Activation backward from the output (act_pass): ReLU = torch threshold_backward
+// (out <= 0 -> 0; a NaN output passes its gradient), ReLU6 = hardtanh_backward.
+template <int ACT>
 __global__ __launch_bounds__(kBlock) void relu_bwd_kernel(const f32x4* __restrict__ g,
                                                           const f32x4* __restrict__ out,
                                                           f32x4* __restrict__ gin, uint32_t n4) {
@@ -212,19 +212,20 @@ __global__ __launch_bounds__(kBlock) void relu_bwd_kernel(const f32x4* __restric
   for (uint32_t v = blockIdx.x * blockDim.x + threadIdx.x; v < n4; v += stride) {
     const f32x4 a = g[v], o = out[v];
     f32x4 r;
-    r.x = o.x <= 0.0f ? 0.0f : a.x;
-    r.y = o.y <= 0.0f ? 0.0f : a.y;
-    r.z = o.z <= 0.0f ? 0.0f : a.z;
-    r.w = o.w <= 0.0f ? 0.0f : a.w;
+    r.x = act_pass<ACT>(o.x) ? a.x : 0.0f;
+    r.y = act_pass<ACT>(o.y) ? a.y : 0.0f;
+    r.z = act_pass<ACT>(o.z) ? a.z : 0.0f;
+    r.w = act_pass<ACT>(o.w) ? a.w : 0.0f;
     gin[v] = r;
   }
 }
+template <int ACT>
 __global__ __launch_bounds__(kBlock) void relu_bwd_tail(const float* __restrict__ g,
                                                         const float* __restrict__ out,
                                                         float* __restrict__ gin, uint32_t start,
                                                         uint32_t n) {
   const uint32_t i = start + blockIdx.x * blockDim.x + threadIdx.x;
-  if (i < n) gin[i] = out[i] <= 0.0f ? 0.0f : g[i];
+  if (i < n) gin[i] = act_pass<ACT>(out[i]) ? g[i] : 0.0f;
 }
 
 // ------------------------------------------------------------------ Adam step
@@ -284,7 +285,7 @@ __global__ __launch_bounds__(kBlock) void adam_kernel(AdamTable tab, float w1, f
 // forward's fp32 operations (bit-identical masks), nothing of the forward is stored.
 constexpr int kEpiParts = 6;
 
-template <bool RES, bool RELU, bool QUANT, bool AFFINE, bool VEC>
+template <bool RES, int ACT, bool QUANT, bool AFFINE, bool VEC>
 __global__ __launch_bounds__(kBlock) void epilogue_bwd_rows(
     const float* __restrict__ g, const float* __restrict__ y, const float* __restrict__ bias,
     const float* __restrict__ gamma, const float* __restrict__ phi, const float* __restrict__ res,
@@ -303,7 +304,7 @@ __global__ __launch_bounds__(kBlock) void epilogue_bwd_rows(
     const float pre = bias ? __fadd_rn(yv, b) : yv;
     float t = AFFINE ? __fadd_rn(__fmul_rn(pre, ga), ph) : pre;
     if (RES) t = __fadd_rn(t, rv);
-    if (RELU) t = t < 0.0f ? 0.0f : t;
+    t = act_fwd<ACT>(t);
     float gt = gv;
     if (QUANT) {
       const float tq = t / d;
@@ -318,7 +319,7 @@ __global__ __launch_bounds__(kBlock) void epilogue_bwd_rows(
       a2 += (double)gi;
       a3 += (double)gq;
     }
-    if (RELU) gt = t <= 0.0f ? 0.0f : gt;
+    if (ACT) gt = act_pass<ACT>(t) ? gt : 0.0f;
     oy = AFFINE ? __fmul_rn(gt, ga) : gt;
     orr = gt;
     sg += (double)gt * (double)pre;
@@ -504,10 +505,11 @@ static int bias_act(const char* what, const float* y, const float* bias, const f
   if (gamma) SSQ_BA(R, A, Q, true); else SSQ_BA(R, A, Q, false);
 #define SSQ_BA2(R, A) \
   if (yq) { SSQ_BA1(R, A, true) } else { SSQ_BA1(R, A, false) }
+  SSQ_REQUIRE(relu >= 0 && relu <= 2, SSQ_E_ARG, "%s: activation code %d (0/1/2)", what, relu);
   if (res) {
-    if (relu) { SSQ_BA2(true, true) } else { SSQ_BA2(true, false) }
+    if (relu == 2) { SSQ_BA2(true, 2) } else if (relu) { SSQ_BA2(true, 1) } else { SSQ_BA2(true, 0) }
   } else {
-    if (relu) { SSQ_BA2(false, true) } else { SSQ_BA2(false, false) }
+    if (relu == 2) { SSQ_BA2(false, 2) } else if (relu) { SSQ_BA2(false, 1) } else { SSQ_BA2(false, 0) }
   }
 #undef SSQ_BA2
 #undef SSQ_BA1
@@ -576,10 +578,11 @@ extern "C" int ssq_epilogue_bwd(const float* g, const float* y, const float* bia
   if (gamma) { SSQ_EB1(R, A, Q, true) } else { SSQ_EB1(R, A, Q, false) }
 #define SSQ_EB3(R, A) \
   if (delta) { SSQ_EB2(R, A, true) } else { SSQ_EB2(R, A, false) }
+  SSQ_REQUIRE(relu >= 0 && relu <= 2, SSQ_E_ARG, "ssq_epilogue_bwd: activation code %d", relu);
   if (res) {
-    if (relu) { SSQ_EB3(true, true) } else { SSQ_EB3(true, false) }
+    if (relu == 2) { SSQ_EB3(true, 2) } else if (relu) { SSQ_EB3(true, 1) } else { SSQ_EB3(true, 0) }
   } else {
-    if (relu) { SSQ_EB3(false, true) } else { SSQ_EB3(false, false) }
+    if (relu == 2) { SSQ_EB3(false, 2) } else if (relu) { SSQ_EB3(false, 1) } else { SSQ_EB3(false, 0) }
   }
 #undef SSQ_EB3
 #undef SSQ_EB2
@@ -593,22 +596,32 @@ extern "C" int ssq_epilogue_bwd(const float* g, const float* y, const float* bia
   return check_launch("ssq_epilogue_bwd");
 }
 
-extern "C" int ssq_relu_bwd(const float* g, const float* out, float* gin, int64_t n,
-                            ssq_stream_t stream) {
-  SSQ_REQUIRE(g && out && gin && n >= 0 && n < (1ll << 31), SSQ_E_ARG, "ssq_relu_bwd: bad args");
+template <int ACT>
+static int act_bwd(const char* what, const float* g, const float* out, float* gin, int64_t n,
+                   hipStream_t s) {
+  SSQ_REQUIRE(g && out && gin && n >= 0 && n < (1ll << 31), SSQ_E_ARG, "%s: bad args", what);
   if (n == 0) return SSQ_OK;
-  hipStream_t s = (hipStream_t)stream;
   auto al = [](const void* q) { return ((uintptr_t)q & 15u) == 0; };
   const bool vec = al(g) && al(out) && al(gin);
   const int64_t n4 = vec ? n / 4 : 0;
   if (n4 > 0)
-    hipLaunchKernelGGL(relu_bwd_kernel, dim3(grid_for(n4, kBlock, 2048)), dim3(kBlock), 0, s,
+    hipLaunchKernelGGL(relu_bwd_kernel<ACT>, dim3(grid_for(n4, kBlock, 2048)), dim3(kBlock), 0, s,
                        (const f32x4*)g, (const f32x4*)out, (f32x4*)gin, (uint32_t)n4);
   const int64_t start = n4 * 4;
   if (start < n)
-    hipLaunchKernelGGL(relu_bwd_tail, dim3((unsigned)((n - start + kBlock - 1) / kBlock)),
+    hipLaunchKernelGGL(relu_bwd_tail<ACT>, dim3((unsigned)((n - start + kBlock - 1) / kBlock)),
                        dim3(kBlock), 0, s, g, out, gin, (uint32_t)start, (uint32_t)n);
-  return check_launch("ssq_relu_bwd");
+  return check_launch(what);
+}
+
+extern "C" int ssq_relu_bwd(const float* g, const float* out, float* gin, int64_t n,
+                            ssq_stream_t stream) {
+  return act_bwd<1>("ssq_relu_bwd", g, out, gin, n, (hipStream_t)stream);
+}
+
+extern "C" int ssq_relu6_bwd(const float* g, const float* out, float* gin, int64_t n,
+                             ssq_stream_t stream) {
+  return act_bwd<2>("ssq_relu6_bwd", g, out, gin, n, (hipStream_t)stream);
 }
 
 extern "C" int ssq_adam(int nseg, float* const* p, const float* const* g, float* const* m,

@@ -68,6 +68,25 @@ __device__ __forceinline__ uint32_t fdiv(uint32_t n, FastDiv f) {
   return (__umulhi(n, f.m) + n) >> f.s;
 }
 
+// ---------------------------------------------------------------- activations
+// Activation codes of the fused epilogues (ABI int `relu`): 0 none, 1 ReLU, 2 ReLU6.
+// Forward as torch's clamp (t < lo -> lo keeps -0.0 and NaN); the gradient passes unless
+// the activation's output sits on / beyond a clamp edge -- threshold_backward (out <= 0)
+// for ReLU, hardtanh_backward (x <= 0 || x >= 6, NaN passes) for ReLU6, evaluated on the
+// output, which equals the input strictly inside the edges.
+template <int ACT>
+__device__ __forceinline__ float act_fwd(float t) {
+  if (ACT >= 1) t = t < 0.0f ? 0.0f : t;
+  if (ACT == 2) t = t > 6.0f ? 6.0f : t;
+  return t;
+}
+template <int ACT>
+__device__ __forceinline__ bool act_pass(float o) {
+  if (ACT == 1) return !(o <= 0.0f);
+  if (ACT == 2) return !(o <= 0.0f || o >= 6.0f);
+  return true;
+}
+
 // ---------------------------------------------------------------- device math
 // Division by a loop-invariant d without the per-element divide sequence.  With
 // r = RN(1/d) (computed once), q0 = x*r is within 1.5 ulp of x/d, one fma residual /

@@ -582,7 +582,7 @@ class BiasActFn(torch.autograd.Function):
             rp = None
         out = torch.empty_like(y)
         call("ssq_bias_act", yp, bp, rp, _vp(out), y.numel(), hw, C, int(relu), stream_of(y))
-        ctx.relu = bool(relu)
+        ctx.relu = int(relu)
         if relu:
             ctx.save_for_backward(out)
         return out
@@ -593,15 +593,17 @@ class BiasActFn(torch.autograd.Function):
             (out,) = ctx.saved_tensors
             g, gp = fptr(g.contiguous(), "grad")
             gin = torch.empty_like(g)
-            call("ssq_relu_bwd", gp, _vp(out), _vp(gin), g.numel(), stream_of(g))
+            call("ssq_relu6_bwd" if ctx.relu == 2 else "ssq_relu_bwd", gp, _vp(out), _vp(gin),
+                 g.numel(), stream_of(g))
         else:
             gin = g
         return gin, None, (gin if ctx.needs_input_grad[2] else None), None
 
 
 def bias_act(y, bias=None, res=None, relu=True):
-    out = BiasActFn.apply(y, bias, res, bool(relu))
-    if relu:
+    """relu: activation code (False/0 identity, True/1 ReLU, 2 ReLU6)."""
+    out = BiasActFn.apply(y, bias, res, int(relu))
+    if int(relu) == 1:
         # lets a loss that folds the ReLU backward into its own pass (lp_loss relu_mask)
         # back-propagate from the ReLU's inputs directly
         out._ssq_relu_inputs = tuple(t for t in (y, res) if t is not None and t.requires_grad)
@@ -643,7 +645,7 @@ class BiasActQuantFn(torch.autograd.Function):
         yq = torch.empty_like(y)
         call("ssq_bias_act_fq", yp, bp, rp, _vp(out), _vp(yq), y.numel(), hw, C_, int(relu), dp,
              zpp, lo, hi, stream_of(y))
-        ctx.relu, ctx.q = bool(relu), (lo, hi)
+        ctx.relu, ctx.q = int(relu), (lo, hi)
         if keep:
             ctx.save_for_backward(out, delta, zp)
         return yq
@@ -661,7 +663,7 @@ class BiasActQuantFn(torch.autograd.Function):
         n = g.numel()
         ws, wsn = workspace(query("ssq_fq_bwd_workspace_size", n, n, 1), g.device)
         if ctx.relu:
-            call("ssq_fq_relu_bwd", _vp(out), gp, _vp(d), _vp(z), n, lo, hi, _vp(gin), _vp(gd),
+            call("ssq_fq_relu6_bwd" if ctx.relu == 2 else "ssq_fq_relu_bwd", _vp(out), gp, _vp(d), _vp(z), n, lo, hi, _vp(gin), _vp(gd),
                  _vp(gz), ws, wsn, stream_of(g))
         else:
             call("ssq_fq_bwd", _vp(out), gp, _vp(d), _vp(z), n, n, 1, lo, hi, _vp(gin), _vp(gd),
@@ -676,7 +678,7 @@ def bias_act_quant(y, bias, res, relu, delta, zp, n_bits, sym=False):
     """bias_act followed by fake_quant(delta, zp) in one pass (per-tensor quantizer)."""
     keep = torch.is_grad_enabled() and any(
         t is not None and t.requires_grad for t in (y, res, delta, zp))
-    return BiasActQuantFn.apply(y, bias, res, delta, zp, bool(relu), n_bits, sym, keep)
+    return BiasActQuantFn.apply(y, bias, res, delta, zp, int(relu), n_bits, sym, keep)
 
 
 class EpilogueFn(torch.autograd.Function):
@@ -707,7 +709,7 @@ class EpilogueFn(torch.autograd.Function):
         call("ssq_epilogue_fwd", yp, bp, gmp, php, rp, None if quant else _vp(out),
              _vp(out) if quant else None, y.numel(), hw, C_, int(relu), dp, zpp, lo, hi,
              stream_of(y))
-        ctx.cfg = (bool(relu), lo, hi, quant, C_, hw)
+        ctx.cfg = (int(relu), lo, hi, quant, C_, hw)
         ctx.save_for_backward(y, bias, gamma, phi, res, delta, zp)
         return out
 
@@ -743,8 +745,8 @@ class EpilogueFn(torch.autograd.Function):
 def epilogue(y, bias, gamma, phi, res, relu, q=None):
     """EpilogueFn with q an (initialised, per-tensor) act quantizer or None."""
     if q is None:
-        return EpilogueFn.apply(y, bias, gamma, phi, res, None, None, bool(relu), 8, False)
-    return EpilogueFn.apply(y, bias, gamma, phi, res, q.delta, q.zero_point, bool(relu), q.n_bits,
+        return EpilogueFn.apply(y, bias, gamma, phi, res, None, None, int(relu), 8, False)
+    return EpilogueFn.apply(y, bias, gamma, phi, res, q.delta, q.zero_point, int(relu), q.n_bits,
                             q.sym)
 
 

@@ -228,13 +228,19 @@ class QuantModule(nn.Module):
             bias = self.org_bias
         return weight, bias
 
+    def act_code(self):
+        """The fused epilogues' activation code: 0 identity, 1 ReLU, 2 ReLU6."""
+        if isinstance(self.activation_function, nn.ReLU6):
+            return 2
+        return 1 if isinstance(self.activation_function, nn.ReLU) else 0
+
     def epilogue_fusable(self, input):
-        """The conv bias add, the gamma^z/phi^z affine and a ReLU / identity activation can
-        run as the fused K13 epilogue (bit-identical to the eager ops): a conv on the
-        device, a constant bias, no SE module, no feature caching."""
+        """The conv bias add, the gamma^z/phi^z affine and a ReLU / ReLU6 / identity
+        activation can run as the fused K13 epilogue (bit-identical to the eager ops): a conv
+        on the device, a constant bias, no SE module, no feature caching."""
         if not (input.is_cuda and self.fwd_func is F.conv2d and self.se_module is None
                 and self.cache_features == 'none'
-                and isinstance(self.activation_function, (nn.ReLU, StraightThrough))):
+                and isinstance(self.activation_function, (nn.ReLU, nn.ReLU6, StraightThrough))):
             return False
         return not (self.bias is not None and self.bias.requires_grad and self.train_bias)
 
@@ -265,7 +271,7 @@ class QuantModule(nn.Module):
         act_q = self.use_act_quant and not self.disable_act_quant
         if self.epilogue_fusable(input):
             out, bias = self.forward_raw(input)
-            relu = isinstance(self.activation_function, nn.ReLU)
+            relu = self.act_code()
             q = fusable_act_quantizer(self.act_quantizer, act_q)
             gamma, phi = self.affine()
             if gamma is not None:

@@ -410,22 +410,35 @@ def test_fused_bwd_with_reg_matches_separate(K, golden):
     close(host(a3.grad), host(a1.grad) + host(a2.grad), rtol=1e-5, atol=1e-7)
 
 
+def _act_ref(t, relu):
+    """The eager activation of an activation code (0 identity, 1 ReLU, 2 ReLU6)."""
+    return torch.nn.functional.relu6(t) if relu == 2 else torch.relu(t) if relu else t
+
+
+# activation edge values: signed zeros, NaN, the ReLU6 clamp edge and its neighbours, inf
+EDGE = [-0.0, float("nan"), 0.0, 6.0, 6.0000005, 5.9999995, float("inf"), -float("inf")]
+
+
 @pytest.mark.parametrize("shape,res,relu", [((4, 8, 7, 7), True, True), ((3, 5, 6, 6), False, True),
                                             ((2, 16, 14, 14), True, False), ((2, 3, 5, 3), False, False),
-                                            ((32, 64, 56, 56), True, True)])
+                                            ((32, 64, 56, 56), True, True), ((4, 8, 7, 7), True, 2),
+                                            ((2, 3, 5, 3), False, 2), ((32, 64, 56, 56), False, 2)])
 def test_bias_act_matches_eager_ops(K, shape, res, relu):
-    """K13 epilogue == (y + bias) (+ residual) -> ReLU as separate fp32 torch ops on the
-    device, bit for bit (including -0.0 / NaN through the ReLU), and its backward."""
+    """K13 epilogue == (y + bias) (+ residual) -> ReLU / ReLU6 as separate fp32 torch ops
+    on the device, bit for bit (-0.0 / NaN / the clamp edges through the activation), and
+    its backward."""
     gen = torch.Generator().manual_seed(sum(shape))
     y = torch.randn(shape, generator=gen).cuda()
-    y.view(-1)[:3] = torch.tensor([-0.0, float("nan"), 0.0])
+    y.view(-1)[:8] = torch.tensor(EDGE)
     b = torch.randn(shape[1], generator=gen).cuda()
+    b[0] = 0.0
     r = torch.randn(shape, generator=gen).cuda() if res else None
+    if res:
+        r.view(-1)[:8] = 0.0
     ref = y + b.view(1, -1, 1, 1)
     if res:
         ref = ref + r
-    if relu:
-        ref = torch.relu(ref)
+    ref = _act_ref(ref, relu)
     out = K.bias_act(y, b, r, relu)
     np.testing.assert_array_equal(host(out).view(np.int32), host(ref).view(np.int32))
     # backward against autograd of the eager ops
@@ -439,8 +452,7 @@ def test_bias_act_matches_eager_ops(K, shape, res, relu):
     e = ye + b.view(1, -1, 1, 1)
     if res:
         e = e + re_
-    if relu:
-        e = torch.relu(e)
+    e = _act_ref(e, relu)
     e.backward(g)
     np.testing.assert_array_equal(host(yr.grad), host(ye.grad))
     if res:
@@ -547,21 +559,28 @@ def test_other_blocks_fused_epilogue_matches_unfused(K, kind, act, affine):
     x = torch.randn(4, cin, 14, 14).cuda()
     with torch.no_grad():
         qnn(x)
+    if kind == "inverted":   # the ReLU6 layers take the fused epilogue (activation code 2)
+        assert [m.act_code() for m in qb.conv] == [2, 2, 0]
+        assert all(m.epilogue_fusable(x) for m in qb.conv)
     _compare_fused_unfused(qb, x, act, _set_affine(qb) if affine else ())
 
 
 @pytest.mark.parametrize("shape", [(4, 8, 7, 7), (2, 3, 5, 3), (32, 64, 56, 56)])
 @pytest.mark.parametrize("res", [False, True])
-@pytest.mark.parametrize("relu", [False, True])
+@pytest.mark.parametrize("relu", [0, 1, 2])
 def test_bias_act_quant_matches_composed(K, shape, res, relu):
     """K13 + act q/dq in one pass == bias_act then fake_quant, bit for bit: the output,
-    and the gradients of y, the residual, delta and zero_point (ReLU backward folded into
-    the STE pass)."""
+    and the gradients of y, the residual, delta and zero_point (ReLU / ReLU6 backward
+    folded into the STE pass)."""
     gen = torch.Generator().manual_seed(sum(shape) + 7 * res + relu)
-    y = torch.randn(shape, generator=gen).cuda()
+    y = torch.randn(shape, generator=gen).cuda() * 4
     y.view(-1)[:3] = torch.tensor([-0.0, float("nan"), 0.0])
+    y.view(-1)[3:6] = torch.tensor([6.0, 6.0000005, 5.9999995])
     b = torch.randn(shape[1], generator=gen).cuda()
+    b[0] = 0.0
     r = torch.randn(shape, generator=gen).cuda() if res else None
+    if res:
+        r.view(-1)[:6] = 0.0
     d = torch.tensor(0.21).cuda()
     z = torch.tensor(3.0).cuda()
     g = torch.randn(shape, generator=gen).cuda()
