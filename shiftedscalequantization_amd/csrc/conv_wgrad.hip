@@ -9,15 +9,12 @@
 //                           * x[n, g*Cig + ci, oh*st + r - pad, ow*st + s - pad]
 // as an implicit GEMM (M = Cog, N = Cig*R*S, K = N*OH*OW) on v_mfma_f32_32x32x2_f32 (exact
 // fp32 products, k-ordered fp32 accumulation), deterministically:
-//   stage 1: workgroup (n-tile, g*m-tiles, split) owns a 64 x 128 output tile and a fixed
-//            range of K chunks (one chunk = TH output rows of one sample); per chunk it
-//            stages dy[64 co][TH*OW px] and the x rows the chunk touches in LDS, then each
-//            wave runs 64 x 32 of the tile (two 32x32 accumulators sharing one gathered
-//            x operand per lane, the expensive one);
-//            the tile is written to its split's slot of the workspace;
-//   stage 2: dW = the splits summed in split order.
+//   stage 1: workgroup (n-tile, g*m-tiles, split) owns a TM x TN output tile and a fixed
+//            range of K chunks; the tile is written to its split's slot of the workspace;
+//   stage 2: dW = the splits summed in a fixed order.
 // Same inputs -> same bits, run to run (no atomics).  Within tolerance of any other
 // summation order (the MIOpen / CPU results), like every fp32 convolution gradient.
+// Depthwise convs take a separate bandwidth-bound reduction (wgrad_dw_stage1).
 #include <algorithm>
 
 #include "ssq_common.h"
@@ -26,141 +23,157 @@ namespace ssq {
 
 typedef float f32x16 __attribute__((ext_vector_type(16)));
 
-constexpr int kTM = 64;    // co per workgroup tile
-constexpr int kTN = 128;   // (ci, r, s) columns per workgroup tile
-constexpr int kMaxPx = 128;  // output pixels per chunk (even)
-constexpr int kXSlots = 16;  // x values per thread per chunk (plan keeps the tile within)
+constexpr int kUnr = 2;  // k-steps per operand group (4 LDS reads + 4 MFMAs each)
 
 struct WgradGeo {
   int Nb, C, H, W, Co, OH, OW, R, S, st, pad, G, Cig, Cog;
-  int Ncol;         // Cig*R*S
-  int TH;           // output rows per chunk
-  int P;            // TH*OW (pixels per chunk, <= kMaxPx)
-  int Pp;           // P rounded up to even
-  int chunks_per_n; // ceil(OH / TH)
-  int nchunks;      // Nb * chunks_per_n
-  int cps;          // chunks per split
+  int Ncol;          // Cig*R*S
+  int WM;            // waves along M (TM = 64*WM, TN = 256/WM)
+  int Pq;            // output pixels per chunk (64 or 128; a sample's last chunk may be short)
+  int lda;           // A row pitch in LDS: Pq + 1 (odd: conflict-free A reads)
+  int chunks_per_n;  // ceil(OH*OW / Pq)
+  int nchunks;       // Nb * chunks_per_n
+  int cps;           // chunks per split
   int nsplit;
-  int in_rows;      // (TH-1)*st + R  (x rows staged per chunk)
-  int ci_span;      // channels staged per chunk (max over tiles)
-  int m_tiles;      // ceil(Cog / kTM)
-  FastDiv div_wp, div_rows;  // by W + 2*pad, by in_rows
+  int in_rows;       // x rows staged per chunk: (output rows a chunk can span - 1)*st + R
+  int ci_span;       // channels staged per chunk (max over tiles)
+  int xtile;         // ci_span * in_rows * (W + 2 pad)
+  int m_tiles, n_tiles;
 };
 
-__global__ __launch_bounds__(256, 2) void wgrad_stage1(const float* __restrict__ x,
+// Stage 1.  Workgroup (n-tile, g*m-tiles, split) owns a TM x TN tile of dW (4 waves as
+// WM x (4/WM), each wave 64 x 64 = 2 x 2 v_mfma_f32_32x32x2_f32 accumulators) and the
+// chunks [split*cps, ...) of K = (n, pixel): a chunk is Pq consecutive output pixels of
+// one sample (row-crossing), so dy[co][chunk] is one contiguous row segment per co.
+// Staging is LDS-DMA (global_load_lds, 4 B per lane, no registers): per chunk, each dy
+// row segment -> A[co][0..P) and each x row the chunk touches -> X[ci][row][pad..pad+W)
+// (padding columns stay zero; rows outside the image / channel range are zeroed with
+// ds_write).  Two LDS buffers: chunk c+1's DMA is issued before chunk c's MFMAs and
+// retired (vmcnt(0) + barrier) before they are read.  A k-step gives each lane two A
+// values (rows lane&31, +32) and two gathered B values (columns lane&31, +32) for four
+// MFMAs; the lane halves walk disjoint halves of the chunk (the MFMA's k = 0 / 1), so a
+// lane's pixel advances by one per step and its x offset incrementally.  Operand groups of
+// kUnr steps are read one group ahead of the MFMAs that use them.
+template <int WM>
+__global__ __launch_bounds__(256, 1) void wgrad_stage1(const float* __restrict__ x,
                                                     const float* __restrict__ dy, WgradGeo g,
                                                     float* __restrict__ part) {
+  constexpr int WN = 4 / WM, TM = 64 * WM, TN = 64 * WN;
   extern __shared__ float lds[];
-  const int lda = g.Pp + 1;                      // odd: A reads conflict-free
-  const int Wp = g.W + 2 * g.pad;                // x rows staged with zero padding columns
-  float* As = lds;                               // [kTM][lda]
-  float* Xs = lds + kTM * lda;                   // [ci_span][in_rows][Wp]
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const int nt = blockIdx.x;
+  const int Pq = g.Pq, lda = g.lda;
+  const int Wp = g.W + 2 * g.pad;
+  const int xbuf = g.xtile + 1;                    // + zero slot
+  float* Abuf = lds;                               // [2][TM][lda]
+  float* Xbuf = lds + 2 * TM * lda;                // [2][xtile + 1]
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wm = wave / WN, wn = wave - wm * WN;
   const int grp = blockIdx.y / g.m_tiles, mt = blockIdx.y - grp * g.m_tiles;
   const int split = blockIdx.z;
-  const int co0 = mt * kTM;                      // within the group
-  const int col0 = nt * kTN;
+  const int co0 = mt * TM;                         // within the group
+  const int col0 = blockIdx.x * TN;
   const int RS = g.R * g.S;
-  const int ci_lo = col0 / RS;                   // first channel the tile touches
-  // wave w owns columns col0 + 32w .. +31 (one per lane & 31) and all 64 rows of the
-  // tile (two 32-row accumulators sharing this lane's gathered x value)
-  const int col = col0 + wave * 32 + (lane & 31);
-  const bool cval = col < g.Ncol;
-  int xbase;
-  {
-    const int c = cval ? col : 0;
+  const int ci_lo = col0 / RS;
+  const int wrow = co0 + wm * 64, wcol = col0 + wn * 64;
+  int xb[2];
+#pragma unroll
+  for (int j = 0; j < 2; ++j) {
+    // a column past Ncol gathers from the tile's first column (in range, result unused)
+    const int col = wcol + 32 * j + (lane & 31);
+    const int c = col < g.Ncol ? col : ci_lo * RS;
     const int ci = c / RS, rs = c - ci * RS;
     const int r = rs / g.S;
-    xbase = ((ci - ci_lo) * g.in_rows + r) * Wp + (rs - r * g.S);
+    xb[j] = ((ci - ci_lo) * g.in_rows + r) * Wp + (rs - r * g.S);
   }
-  // the K range of a chunk is split in two halves, one per lane half (the MFMA's k = 0 / 1)
-  const int half = lane >> 5, arow = lane & 31;
-  const int Ph = g.Pp >> 1;
-  const int px0 = half * Ph;
-  const int oh_start = px0 / g.OW, ow_start = px0 - oh_start * g.OW;
-  const int row_adj = g.st * Wp - g.OW * g.st;   // offset change when ow wraps
-  const int HW = g.H * g.W, OHW = g.OH * g.OW;
-  const int xtot = g.ci_span * g.in_rows * Wp;
-  const int zslot = xtot;                        // Xs[xtot] = 0: the B operand past a chunk
-  if (tid == 0) Xs[zslot] = 0.0f;
-  const FastDiv dWp = g.div_wp, dRows = g.div_rows;
+  const int half = lane >> 5;
+  const int arow = (wm * 64 + (lane & 31)) * lda;
+  const int OHW = g.OH * g.OW, HW = g.H * g.W;
+  const int row_adj = g.st * Wp - g.OW * g.st;     // x offset change when ow wraps
   const int c_begin = split * g.cps, c_end = min(c_begin + g.cps, g.nchunks);
+  const int nrows_x = g.ci_span * g.in_rows;
 
-  // x tile element i of the chunk starting at input row ih0 (0 outside the image)
-  auto x_elem = [&](const float* sx, int ih0, int i) {
-    float v = 0.0f;
-    if (i < xtot) {
-      const int q = (int)fdiv((uint32_t)i, dWp), w = i - q * Wp;
-      const int cl = (int)fdiv((uint32_t)q, dRows), rr = q - cl * g.in_rows;
-      const int ci = ci_lo + cl, ih = ih0 + rr, iw = w - g.pad;
-      if (ci < g.Cig && ih >= 0 && ih < g.H && iw >= 0 && iw < g.W)
-        v = sx[(int64_t)ci * HW + (int64_t)ih * g.W + iw];
-    }
-    return v;
+  // both buffers zeroed once: A rows past Cog, X padding columns and the zero slot are
+  // never written by the DMA (a short chunk's A tail and out-of-image X rows are zeroed
+  // per chunk below)
+  for (int i = tid; i < 2 * TM * lda + 2 * xbuf; i += 256) lds[i] = 0.0f;
+  __syncthreads();
+
+  // chunk c -> (sample, first pixel, pixel count, first output row)
+  auto chunk_geo = [&](int c, int& n, int& p0, int& P, int& oh_first) {
+    n = c / g.chunks_per_n;
+    p0 = (c - n * g.chunks_per_n) * Pq;
+    P = min(Pq, OHW - p0);
+    oh_first = p0 / g.OW;
   };
-  // ---- global -> register prefetch of one chunk (issued before the previous chunk's
-  // MFMAs); x tiles beyond kXSlots values per thread load the rest synchronously
-  float ra[2][16], rx[kXSlots];
-  auto load_chunk = [&](int c) {
-    const int n = c / g.chunks_per_n;
-    const int oh0 = (c - n * g.chunks_per_n) * g.TH;
-    const int P = min(g.TH, g.OH - oh0) * g.OW;
-    const int ih0 = oh0 * g.st - g.pad;
-    const float* sa = dy + ((int64_t)n * g.Co + (int64_t)grp * g.Cog + co0) * OHW +
-                      (int64_t)oh0 * g.OW;
-#pragma unroll
-    for (int jr = 0; jr < 16; ++jr) {
-      const int r = wave + 4 * jr;
-      const bool rv = co0 + r < g.Cog;
-#pragma unroll
-      for (int jp = 0; jp < 2; ++jp) {
-        const int p = lane + 64 * jp;
-        ra[jp][jr] = (rv && p < P) ? sa[(int64_t)r * OHW + p] : 0.0f;
+  auto stage = [&](int c, int b) {
+    int n, p0, P, oh_first;
+    chunk_geo(c, n, p0, P, oh_first);
+    float* A = Abuf + b * TM * lda;
+    float* X = Xbuf + b * xbuf;
+    // dy: row r (co0 + r < Cog) -> A[r][0..P); a short chunk's tail columns -> 0
+    const float* sa = dy + ((int64_t)n * g.Co + (int64_t)grp * g.Cog + co0) * OHW + p0;
+    const int rows = min(TM, g.Cog - co0);
+    for (int r = wave; r < rows; r += 4) {
+      for (int k0 = 0; k0 < Pq; k0 += 64) {
+        const int k = k0 + lane;
+        if (k < P)
+          __builtin_amdgcn_global_load_lds((const void*)(sa + (int64_t)r * OHW + k),
+                                           (void*)(A + r * lda + k0), 4, 0, 0);
+        else if (k < Pq)
+          A[r * lda + k] = 0.0f;
       }
     }
+    // x: staged row q = (cl, rr) -> channel ci_lo + cl, input row ih0 + rr
+    const int ih0 = oh_first * g.st - g.pad;
     const float* sx = x + ((int64_t)n * g.C + (int64_t)grp * g.Cig) * HW;
-#pragma unroll
-    for (int j = 0; j < kXSlots; ++j) rx[j] = x_elem(sx, ih0, tid + 256 * j);
-  };
-  auto store_chunk = [&](int c) {
-#pragma unroll
-    for (int jr = 0; jr < 16; ++jr)
-#pragma unroll
-      for (int jp = 0; jp < 2; ++jp) {
-        const int p = lane + 64 * jp;
-        if (p < g.Pp) As[(wave + 4 * jr) * lda + p] = ra[jp][jr];
+    for (int q = wave; q < nrows_x; q += 4) {
+      const int cl = q / g.in_rows, rr = q - cl * g.in_rows;
+      const int ci = ci_lo + cl, ih = ih0 + rr;
+      float* drow = X + q * Wp + g.pad;
+      const bool ok = ci < g.Cig && ih >= 0 && ih < g.H;
+      for (int k0 = 0; k0 < g.W; k0 += 64) {
+        const int k = k0 + lane;
+        if (k < g.W) {
+          if (ok)
+            __builtin_amdgcn_global_load_lds(
+                (const void*)(sx + (int64_t)ci * HW + (int64_t)ih * g.W + k),
+                (void*)(drow + k0), 4, 0, 0);
+          else
+            drow[k] = 0.0f;
+        }
       }
-#pragma unroll
-    for (int j = 0; j < kXSlots; ++j) {
-      const int i = tid + 256 * j;
-      if (i < xtot) Xs[i] = rx[j];
-    }
-    if (xtot > 256 * kXSlots) {
-      const int n = c / g.chunks_per_n;
-      const int ih0 = (c - n * g.chunks_per_n) * g.TH * g.st - g.pad;
-      const float* sx = x + ((int64_t)n * g.C + (int64_t)grp * g.Cig) * HW;
-      for (int i = tid + 256 * kXSlots; i < xtot; i += 256) Xs[i] = x_elem(sx, ih0, i);
     }
   };
 
-  f32x16 acc0 = {0}, acc1 = {0};
-  if (c_begin < c_end) load_chunk(c_begin);
+  f32x16 acc00 = {0}, acc01 = {0}, acc10 = {0}, acc11 = {0};
+  if (c_begin < c_end) stage(c_begin, 0);
   for (int c = c_begin; c < c_end; ++c) {
-    const int n = c / g.chunks_per_n;
-    const int oh0 = (c - n * g.chunks_per_n) * g.TH;
-    const int P = min(g.TH, g.OH - oh0) * g.OW;
-    __syncthreads();                  // the previous chunk's MFMAs are done with the LDS
-    store_chunk(c);
-    __syncthreads();
-    if (c + 1 < c_end) load_chunk(c + 1);
-    int ow = ow_start, px = px0;
-    int off = xbase + oh_start * g.st * Wp + ow_start * g.st;
-    // one step's operands; the next step's are read while this step's MFMAs run
-    auto fetch = [&](float& a0, float& a1, float& b) {
-      b = Xs[px < P ? off : zslot];           // past the chunk: A and B both 0
-      a0 = As[arow * lda + px];
-      a1 = As[(arow + 32) * lda + px];
+    const int b = (c - c_begin) & 1;
+    asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+    __syncthreads();                  // chunk c staged; chunk c-1's reads of buffer b^1 done
+    if (c + 1 < c_end) stage(c + 1, b ^ 1);
+    int n, p0, P, oh_first;
+    chunk_geo(c, n, p0, P, oh_first);
+    const float* As = Abuf + b * TM * lda;
+    const float* Xs = Xbuf + b * xbuf;
+    const int zslot = g.xtile;        // Xs[zslot] = 0: B past the chunk's pixels
+    // k-steps of this chunk: its P pixels in two lane halves, rounded up to kUnr
+    const int Ph = ((P + 1) / 2 + kUnr - 1) / kUnr * kUnr;
+    int px = half * Ph;
+    int ow, off;
+    {
+      const int pix = p0 + px;
+      const int oh = pix / g.OW;
+      ow = pix - oh * g.OW;
+      off = (oh - oh_first) * g.st * Wp + ow * g.st;
+    }
+    float A0[kUnr], A1[kUnr], B0[kUnr], B1[kUnr];
+    auto fetch = [&](int u) {
+      const bool in = px < P;
+      B0[u] = Xs[in ? xb[0] + off : zslot];
+      B1[u] = Xs[in ? xb[1] + off : zslot];
+      A0[u] = As[arow + px];
+      A1[u] = As[arow + 32 * lda + px];
       ++px;
       ++ow;
       off += g.st;
@@ -168,29 +181,42 @@ __global__ __launch_bounds__(256, 2) void wgrad_stage1(const float* __restrict__
       ow = wrap ? 0 : ow;
       off += wrap ? row_adj : 0;
     };
-    float a0, a1, b;
-    fetch(a0, a1, b);
-    for (int t = 0; t < Ph; ++t) {
-      // (the fetch after the last step reads A's pad column and the zero slot: unused)
-      float na0, na1, nb;
-      fetch(na0, na1, nb);
-      acc0 = __builtin_amdgcn_mfma_f32_32x32x2f32(a0, b, acc0, 0, 0, 0);
-      acc1 = __builtin_amdgcn_mfma_f32_32x32x2f32(a1, b, acc1, 0, 0, 0);
-      a0 = na0;
-      a1 = na1;
-      b = nb;
+#pragma unroll
+    for (int u = 0; u < kUnr; ++u) fetch(u);
+    for (int t = 0; t < Ph; t += kUnr) {
+      float a0[kUnr], a1[kUnr], b0[kUnr], b1[kUnr];
+#pragma unroll
+      for (int u = 0; u < kUnr; ++u) {
+        a0[u] = A0[u];
+        a1[u] = A1[u];
+        b0[u] = B0[u];
+        b1[u] = B1[u];
+      }
+      // next group's operands (none after the last group)
+      if (t + kUnr < Ph) {
+#pragma unroll
+        for (int u = 0; u < kUnr; ++u) fetch(u);
+      }
+#pragma unroll
+      for (int u = 0; u < kUnr; ++u) {
+        acc00 = __builtin_amdgcn_mfma_f32_32x32x2f32(a0[u], b0[u], acc00, 0, 0, 0);
+        acc01 = __builtin_amdgcn_mfma_f32_32x32x2f32(a0[u], b1[u], acc01, 0, 0, 0);
+        acc10 = __builtin_amdgcn_mfma_f32_32x32x2f32(a1[u], b0[u], acc10, 0, 0, 0);
+        acc11 = __builtin_amdgcn_mfma_f32_32x32x2f32(a1[u], b1[u], acc11, 0, 0, 0);
+      }
     }
   }
-  // write this split's tile: C[row][col], row = (r&3) + 8*(r>>2) + 4*(lane>>5), col = lane&31
-  if (!cval) return;
-  float* dst = part + ((int64_t)split * g.G + grp) * (int64_t)g.Cog * g.Ncol + col;
+  // this split's tile: C[row][col], row = (r&3) + 8*(r>>2) + 4*(lane>>5), col = lane&31
+  float* dst = part + ((int64_t)split * g.G + grp) * (int64_t)g.Cog * g.Ncol;
 #pragma unroll
-  for (int t = 0; t < 2; ++t) {
-    const f32x16 acc = t == 0 ? acc0 : acc1;
+  for (int t = 0; t < 4; ++t) {
+    const f32x16 acc = t == 0 ? acc00 : t == 1 ? acc01 : t == 2 ? acc10 : acc11;
+    const int col = wcol + 32 * (t & 1) + (lane & 31);
+    if (col >= g.Ncol) continue;
 #pragma unroll
     for (int r = 0; r < 16; ++r) {
-      const int row = co0 + t * 32 + (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5);
-      if (row < g.Cog) dst[(int64_t)row * g.Ncol] = acc[r];
+      const int row = wrow + 32 * (t >> 1) + (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5);
+      if (row < g.Cog) dst[(int64_t)row * g.Ncol + col] = acc[r];
     }
   }
 }
@@ -318,6 +344,10 @@ static int dw_splits(int64_t Nb, int64_t C, int* spl) {
   return (int)(Nb / *spl);
 }
 
+static size_t wgrad_lds(int wm, int pq, int64_t xtile) {
+  return sizeof(float) * (2 * (size_t)(64 * wm) * (pq + 1) + 2 * (size_t)(xtile + 1));
+}
+
 static int wgrad_plan(int64_t Nb, int64_t C, int64_t H, int64_t W, int64_t Co, int64_t R,
                       int64_t S, int64_t st, int64_t pad, int64_t G, WgradGeo& g,
                       size_t* lds_bytes) {
@@ -327,44 +357,52 @@ static int wgrad_plan(int64_t Nb, int64_t C, int64_t H, int64_t W, int64_t Co, i
   const int64_t OH = (H + 2 * pad - R) / st + 1, OW = (W + 2 * pad - S) / st + 1;
   SSQ_REQUIRE(OH >= 1 && OW >= 1 && Nb * C * H * W < (1ll << 31) && Nb * Co * OH * OW < (1ll << 31),
               SSQ_E_ARG, "ssq_conv_wgrad: sizes");
-  SSQ_REQUIRE(OW <= kMaxPx, SSQ_E_ARG, "ssq_conv_wgrad: output width %lld > %d",
-              (long long)OW, kMaxPx);
   g.Nb = (int)Nb; g.C = (int)C; g.H = (int)H; g.W = (int)W; g.Co = (int)Co;
   g.OH = (int)OH; g.OW = (int)OW; g.R = (int)R; g.S = (int)S; g.st = (int)st; g.pad = (int)pad;
   g.G = (int)G; g.Cig = (int)(C / G); g.Cog = (int)(Co / G);
   g.Ncol = g.Cig * g.R * g.S;
-  // channels a 128-column tile can touch: floor((kTN-1)/RS) + 2
   const int RS = g.R * g.S;
-  g.ci_span = std::min(g.Cig, (kTN - 1) / RS + 2);
-  // output rows per chunk: up to kMaxPx pixels, shrunk until the tile fits 64 KiB of LDS
-  // (two workgroups per CU)
-  g.TH = (int)std::max<int64_t>(1, std::min<int64_t>(OH, kMaxPx / OW));
-  auto lds_for = [&](int th) {
-    const int pp = (th * g.OW + 1) & ~1;
-    return sizeof(float) * ((size_t)kTM * (pp + 1) +
-                            (size_t)g.ci_span * ((th - 1) * g.st + g.R) * (g.W + 2 * g.pad) + 1);
-  };
-  auto xslots = [&](int th) {
-    return ((size_t)g.ci_span * ((th - 1) * g.st + g.R) * (g.W + 2 * g.pad) + 255) / 256;
-  };
-  while (g.TH > 1 && (lds_for(g.TH) > 64 * 1024 || xslots(g.TH) > (size_t)kXSlots)) --g.TH;
-  g.P = g.TH * g.OW;
-  g.Pp = (g.P + 1) & ~1;
-  g.chunks_per_n = (g.OH + g.TH - 1) / g.TH;
+  const int64_t Wp = W + 2 * pad;
+  // Candidate layouts WM = 1, 2, 4 (TM = 64 WM, TN = 256 / WM) x Pq = 128, 64, in MFMA
+  // slots (64 cycles): every tile runs 2 MFMAs per pixel per wave, plus per chunk a fixed
+  // ~40 and one slot per LDS-DMA instruction a wave issues (A rows + x rows, / 4 waves).
+  double best = 1e300;
+  for (int wm : {1, 2, 4}) {
+    for (int pq : {128, 64}) {
+      const int TM = 64 * wm, TN = 256 / wm;
+      const int64_t span = std::min<int64_t>(g.Cig, (TN - 1) / RS + 2);
+      const int64_t orows = (pq - 1 + OW - 1) / OW + 1;     // output rows a chunk can span
+      const int64_t in_rows = (orows - 1) * st + R;
+      const int64_t xtile = span * in_rows * Wp;
+      if (wgrad_lds(wm, pq, xtile) > 160 * 1024) continue;
+      const int64_t cpn = (OH * OW + pq - 1) / pq;
+      const int64_t tiles = ((g.Cog + TM - 1) / TM) * ((g.Ncol + TN - 1) / TN);
+      const double dma = (double)(std::min<int64_t>(TM, g.Cog) * ((pq + 63) / 64) +
+                                  span * in_rows * ((W + 63) / 64)) / 4.0;
+      const double cost = (double)tiles * Nb * (2.0 * OH * OW + cpn * (40.0 + dma));
+      if (cost < best) {
+        best = cost;
+        g.WM = wm;
+        g.Pq = pq;
+        g.ci_span = (int)span;
+        g.in_rows = (int)in_rows;
+        g.xtile = (int)xtile;
+      }
+    }
+  }
+  SSQ_REQUIRE(best < 1e300, SSQ_E_ARG, "ssq_conv_wgrad: input rows too wide for the LDS tile");
+  const int TM = 64 * g.WM, TN = 256 / g.WM;
+  g.lda = g.Pq + 1;
+  g.chunks_per_n = (int)((OH * OW + g.Pq - 1) / g.Pq);
   g.nchunks = g.Nb * g.chunks_per_n;
-  g.in_rows = (g.TH - 1) * g.st + g.R;
-  g.div_wp = make_fastdiv((uint32_t)(g.W + 2 * g.pad));
-  g.div_rows = make_fastdiv((uint32_t)g.in_rows);
-  g.m_tiles = (g.Cog + kTM - 1) / kTM;
-  const int n_tiles = (g.Ncol + kTN - 1) / kTN;
-  const int64_t tiles = (int64_t)n_tiles * g.m_tiles * g.G;
-  // enough workgroups to fill 256 CUs twice, at least 2 chunks each
+  g.m_tiles = (g.Cog + TM - 1) / TM;
+  g.n_tiles = (g.Ncol + TN - 1) / TN;
+  const int64_t tiles = (int64_t)g.n_tiles * g.m_tiles * g.G;
+  // about two workgroups per CU over the grid, at least 2 chunks each
   int nsplit = (int)std::max<int64_t>(1, std::min<int64_t>(g.nchunks / 2, (512 + tiles - 1) / tiles));
   g.cps = (g.nchunks + nsplit - 1) / nsplit;
   g.nsplit = (g.nchunks + g.cps - 1) / g.cps;
-  *lds_bytes = lds_for(g.TH);
-  SSQ_REQUIRE(*lds_bytes <= 160 * 1024, SSQ_E_ARG, "ssq_conv_wgrad: LDS tile %zu B too large",
-              *lds_bytes);
+  *lds_bytes = wgrad_lds(g.WM, g.Pq, g.xtile);
   return SSQ_OK;
 }
 
@@ -433,12 +471,21 @@ extern "C" int ssq_conv_wgrad(const float* x, const float* dy, int64_t Nb, int64
   SSQ_REQUIRE(ws && ws_bytes >= need, SSQ_E_WS, "ssq_conv_wgrad: workspace too small");
   static bool lds_attr = false;
   if (!lds_attr) {  // dynamic LDS beyond 64 KiB must be opted into
-    hipFuncSetAttribute((const void*)wgrad_stage1, hipFuncAttributeMaxDynamicSharedMemorySize,
+    hipFuncSetAttribute((const void*)wgrad_stage1<1>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                        160 * 1024);
+    hipFuncSetAttribute((const void*)wgrad_stage1<2>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                        160 * 1024);
+    hipFuncSetAttribute((const void*)wgrad_stage1<4>, hipFuncAttributeMaxDynamicSharedMemorySize,
                         160 * 1024);
     lds_attr = true;
   }
-  const dim3 grid((g.Ncol + kTN - 1) / kTN, g.m_tiles * g.G, g.nsplit);
-  hipLaunchKernelGGL(wgrad_stage1, grid, dim3(256), lds, s, x, dy, g, (float*)ws);
+  const dim3 grid(g.n_tiles, g.m_tiles * g.G, g.nsplit);
+  if (g.WM == 1)
+    hipLaunchKernelGGL(wgrad_stage1<1>, grid, dim3(256), lds, s, x, dy, g, (float*)ws);
+  else if (g.WM == 2)
+    hipLaunchKernelGGL(wgrad_stage1<2>, grid, dim3(256), lds, s, x, dy, g, (float*)ws);
+  else
+    hipLaunchKernelGGL(wgrad_stage1<4>, grid, dim3(256), lds, s, x, dy, g, (float*)ws);
   const int64_t n = (int64_t)Co * g.Ncol;
   hipLaunchKernelGGL(wgrad_stage2, dim3((unsigned)std::min<int64_t>((n + 63) / 64, 4096)),
                      dim3(256), 0, s, (const float*)ws, g.nsplit, n, dw);

@@ -827,7 +827,7 @@ def pack_decode(packed, shape, zp, d1, per_ci, d2, n_bits, qmin):
 # ------------------------------------------------------------------ K17 conv weight gradient
 def conv_wgrad_supported(x, weight, stride, padding, dilation, groups):
     """Shapes ssq_conv_wgrad handles: 4-D fp32 NCHW on the device, square stride /
-    padding, dilation 1, output width <= 128."""
+    padding, dilation 1, and a plan whose LDS tile fits (nonzero workspace size)."""
     if x.dim() != 4 or weight.dim() != 4 or not x.is_cuda or x.dtype != torch.float32:
         return False
     st = stride if isinstance(stride, int) else stride[0]
@@ -838,8 +838,10 @@ def conv_wgrad_supported(x, weight, stride, padding, dilation, groups):
         return False
     if (dilation if isinstance(dilation, int) else max(dilation)) != 1:
         return False
-    ow = (x.shape[3] + 2 * pad - weight.shape[3]) // st + 1
-    return 1 <= ow <= 128
+    Nb, C, H, W = (int(v) for v in x.shape)
+    Co, _, R, S = (int(v) for v in weight.shape)
+    return query("ssq_conv_wgrad_workspace_size", Nb, C, H, W, Co, R, S, int(st), int(pad),
+                 int(groups)) > 0
 
 
 def conv_wgrad(x, dy, w_shape, stride, padding, groups):

@@ -704,6 +704,10 @@ def test_lp_loss_rows_equals_gathered(K, row_shape, p):
     (4, 64, 56, 64, 3, 1, 1, 1), (3, 16, 15, 24, 3, 2, 1, 1), (2, 32, 14, 48, 1, 2, 0, 1),
     (2, 24, 9, 24, 3, 1, 1, 24), (2, 48, 12, 96, 3, 1, 1, 2), (5, 130, 7, 70, 3, 1, 1, 1),
     (1, 3, 32, 16, 7, 2, 3, 1),
+    # GEMM path layouts: few input channels (WM = 4 tiles), rows wider than a wave and than
+    # a chunk, 7x7 planes (short chunks), stride 2 at 28x28
+    (2, 16, 14, 256, 1, 1, 0, 1), (1, 8, 70, 16, 3, 1, 1, 1), (1, 4, 130, 8, 3, 1, 1, 1),
+    (2, 256, 7, 512, 3, 1, 1, 1), (2, 64, 28, 128, 3, 2, 1, 1),
     # depthwise path: stride 2, planes wider than a wave, 5x5, odd batch
     (3, 32, 57, 32, 3, 2, 1, 32), (2, 144, 28, 144, 3, 1, 1, 144), (5, 16, 11, 16, 5, 1, 2, 16),
     (32, 8, 7, 8, 3, 1, 1, 8)])
