@@ -70,6 +70,15 @@ int ssq_fq_bwd(const float* x, const float* gy, const float* delta, const float*
                int64_t n, int64_t inner, int64_t nch, int qmin, int qmax,
                float* gx, float* gdelta, float* gzp, void* ws, size_t ws_bytes,
                ssq_stream_t stream);
+/* Backward of q/dq with torch.round instead of round_ste: ChannelQuantAct 'none' mode
+ * (quant/channelQuantAct.py:56-67; x / (delta*shiftedScale) rounded with no gradient).
+ * Pass delta = the fp32 product delta*shiftedScale.  The gradient wrt x is zero (not
+ * written); gdelta = sum gy*(q - zp) is the gradient wrt that product (the caller scales
+ * it by shiftedScale, the product's backward); gzp as ssq_fq_bwd.  Workspace as
+ * ssq_fq_bwd.                                                                          */
+int ssq_fq_round_bwd(const float* x, const float* gy, const float* delta, const float* zp,
+                     int64_t n, int64_t inner, int64_t nch, int qmin, int qmax, float* gdelta,
+                     float* gzp, void* ws, size_t ws_bytes, ssq_stream_t stream);
 /* Per-tensor ssq_fq_bwd for an x that is a ReLU output, with the ReLU backward folded in:
  * gx is written at the ReLU's input (x <= 0 -> 0, torch threshold_backward on the output),
  * bit-identical to ssq_fq_bwd followed by ssq_relu_bwd.  Workspace as ssq_fq_bwd with
@@ -149,6 +158,35 @@ int ssq_adashift_bwd(const float* gWhat, const float* W, const float* alpha,
                      int is_fc, int hard_round, int qmin, int qmax, float reg_lambda,
                      float reg_b, const float* reg_dev, float* galpha, float* gbeta,
                      float* reg_vals, void* ws, size_t ws_bytes, ssq_stream_t stream);
+
+/* Prepared adaShift (conv weights, S <= 4).  In the fused loop W, delta, the shifts and
+ * beta are frozen (layer_recon_fused_shiftedScale.py:59-66) and the reference computes its
+ * floor candidates x_q once (channelQuant.py:284-286).  ssq_adashift_prepare does that
+ * once: fpack[e] = the S floors floor(W/(delta*s_i)) as int8 bytes (byte i) of one 32-bit
+ * word, hterm[e] = h(beta) (hard_round: [beta >= 0]).  *overflow (device int, zeroed by the
+ * caller) becomes nonzero if a floor does not fit int8 -- the caller then keeps
+ * ssq_adashift_fwd/bwd.  The prepared forward / backward give the same What and alpha
+ * gradients as ssq_adashift_fwd / ssq_adashift_bwd (beta frozen: no gbeta) while
+ * streaming 12 B per weight each.  The backward is one launch: `counters` (int64 count =
+ * ssq_adashift_bwd_prepared_counters(), zero-initialised ONCE by the caller, left zeroed
+ * by every launch) lets the last workgroup of each column block finish the reduction in
+ * a fixed order.  galpha OVERWRITTEN; regulariser as ssq_adashift_bwd.                 */
+int ssq_adashift_prepare(const float* W, const float* beta, const float* delta,
+                         const float* shifts, int S, int64_t Co, int64_t Ci, int64_t K,
+                         int hard_round, uint32_t* fpack, float* hterm, int* overflow,
+                         ssq_stream_t stream);
+int ssq_adashift_fwd_prepared(const uint32_t* fpack, const float* hterm, const float* alpha,
+                              const float* delta, const float* zp, int S, int64_t Co,
+                              int64_t Ci, int64_t K, int hard_targets, int qmin, int qmax,
+                              float* What, void* codes_or_null, ssq_stream_t stream);
+size_t ssq_adashift_bwd_prepared_workspace_size(int64_t Co, int64_t Ci, int64_t K, int S);
+int64_t ssq_adashift_bwd_prepared_counters(int64_t Co, int64_t Ci, int64_t K);
+int ssq_adashift_bwd_prepared(const float* gWhat, const uint32_t* fpack, const float* hterm,
+                              const float* alpha, const float* delta, const float* zp, int S,
+                              int64_t Co, int64_t Ci, int64_t K, int qmin, int qmax,
+                              float reg_lambda, float reg_b, const float* reg_dev,
+                              float* galpha, float* reg_vals, unsigned* counters, void* ws,
+                              size_t ws_bytes, ssq_stream_t stream);
 
 /* Shift-regulariser alone (value + gradient wrt alpha), for iterations where the
  * reconstruction gradient is not wanted.  mode 0: lambda*sum(1-|2p-1|^b)

@@ -46,9 +46,13 @@ def load_data(args, device):
 
 
 def val_loader(val, bs=256):
+    """This rank's shard of the validation set in batches (validate_model all-reduces the
+    per-rank sums)."""
     if val is None:
         return None
     images, labels = val
+    lo, hi = shard_rows(len(images))
+    images, labels = images[lo:hi], labels[lo:hi]
     return [(images[i:i + bs], labels[i:i + bs]) for i in range(0, len(images), bs)]
 
 
@@ -67,6 +71,21 @@ def main(argv=None):
     t0 = time.time()
     qnn = D.build_qnn(args.arch, args.n_bits_w, args.n_bits_a, args.channel_wise, args.w_scale_method,
                       args.a_scale_method, device, args.checkpoint, args.disable_8bit_head_stem)
+    if args.test:
+        # the shipped default (`ShiftedScaleQuant.py --test=True` -> channelShift_wMSE,
+        # :119-183): input-channel scales by the ChannelQuantMSE range test, no recon loop
+        shifts = [float(s) for s in args.shift_targets.split(',')]
+        fc = [n for n, m in qnn.named_modules() if isinstance(m, QuantModule)][-1]
+        D.channelShift_wMSE(qnn, cali, level=args.mse_level, threshold=args.mse_threshold,
+                            opt_mode=args.shift_quant_mode, shiftTarget=shifts,
+                            layerDisabled=['.' + fc])
+        torch.cuda.synchronize(device)
+        acc = validate_model(loader, qnn) if loader is not None else None
+        print(f'channelShift_wMSE (level {args.mse_level}, threshold {args.mse_threshold}) '
+              f'finished in {time.time() - t0:.1f}s; accuracy of qnn_hard: {acc}')
+        if world > 1:
+            dist.destroy_process_group()
+        return qnn
     qnn.set_quant_state(True, False)
     with torch.no_grad():
         qnn(cali[:64])
@@ -107,6 +126,10 @@ def main(argv=None):
         qnn.set_quant_state(True, True)
         with torch.no_grad():
             qnn(cali[:64])
+        if world > 1:
+            # each rank initialised its act deltas on its own shard: all-average them
+            # (Brecq/main_imagenet_dist.py:210-211) so the act phase starts replicated
+            qnn.synchorize_activation_statistics()
         qnn.disable_network_output_quantization()
         D.recon_model(qnn, qnn, cali_data=cali, iters=args.iters_a, act_quant=True, opt_mode='mse',
                       lr=args.lr, p=args.p, batch_size=bs)

@@ -28,6 +28,7 @@ SIGNATURES = {
     "ssq_fq_fwd_multi": (_i, [_i, _p, _p, _p, _p, _p, _p, _p, _p, _p, _p]),
     "ssq_fq_bwd_workspace_size": (_sz, [_i64, _i64, _i64]),
     "ssq_fq_bwd": (_i, [_p, _p, _p, _p, _i64, _i64, _i64, _i, _i, _p, _p, _p, _p, _sz, _p]),
+    "ssq_fq_round_bwd": (_i, [_p, _p, _p, _p, _i64, _i64, _i64, _i, _i, _p, _p, _p, _sz, _p]),
     "ssq_fq_relu_bwd": (_i, [_p, _p, _p, _p, _i64, _i, _i, _p, _p, _p, _p, _sz, _p]),
     "ssq_fq_relu6_bwd": (_i, [_p, _p, _p, _p, _i64, _i, _i, _p, _p, _p, _p, _sz, _p]),
     "ssq_scale_init_workspace_size": (_sz, [_i64, _i64, _i]),
@@ -40,6 +41,13 @@ SIGNATURES = {
     "ssq_adashift_fwd": (_i, [_p, _p, _p, _p, _p, _p, _i, _i64, _i64, _i64, _i, _i, _i, _i, _i,
                               _p, _p, _p]),
     "ssq_adashift_bwd_workspace_size": (_sz, [_i64, _i64, _i64, _i, _i]),
+    "ssq_adashift_prepare": (_i, [_p, _p, _p, _p, _i, _i64, _i64, _i64, _i, _p, _p, _p, _p]),
+    "ssq_adashift_fwd_prepared": (_i, [_p, _p, _p, _p, _p, _i, _i64, _i64, _i64, _i, _i, _i, _p,
+                                       _p, _p]),
+    "ssq_adashift_bwd_prepared_workspace_size": (_sz, [_i64, _i64, _i64, _i]),
+    "ssq_adashift_bwd_prepared_counters": (_i64, [_i64, _i64, _i64]),
+    "ssq_adashift_bwd_prepared": (_i, [_p, _p, _p, _p, _p, _p, _i, _i64, _i64, _i64, _i, _i, _f,
+                                       _f, _p, _p, _p, _p, _p, _sz, _p]),
     "ssq_adashift_bwd": (_i, [_p, _p, _p, _p, _p, _p, _p, _i, _i64, _i64, _i64, _i, _i, _i, _i,
                               _f, _f, _p, _p, _p, _p, _p, _sz, _p]),
     "ssq_shift_reg": (_i, [_p, _i, _i64, _i, _f, _f, _p, _p, _p]),

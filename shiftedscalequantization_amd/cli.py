@@ -115,14 +115,20 @@ def get_train_samples(train_loader, num_samples):
 
 @torch.no_grad()
 def validate_model(val_loader, model, device=None, print_result=False):
-    """common.py:152-221: top-1 over (images, target) batches."""
+    """common.py:152-221: top-1 over (images, target) batches.  With several ranks each
+    validates its own shard of the validation set and the (correct, total) sums are
+    all-reduced (Brecq/main_imagenet_dist.py:114-124), so every rank returns the
+    whole-set top-1."""
+    from .parallel_dp import all_sum_
     device = next(model.parameters()).device if device is None else device
     model.eval()
-    correct = total = 0
+    sums = torch.zeros(2, dtype=torch.float64, device=device)
     for images, target in val_loader:
         out = model(images.to(device))
-        correct += (out.argmax(1) == target.to(device)).sum().item()
-        total += target.numel()
+        sums[0] += (out.argmax(1) == target.to(device)).sum()
+        sums[1] += target.numel()
+    all_sum_(sums)
+    correct, total = sums.tolist()
     acc = 100.0 * correct / max(total, 1)
     if print_result:
         print(f' * Acc@1 {acc:.3f}')

@@ -980,3 +980,320 @@ extern "C" int ssq_round_reg(const float* v, int64_t n, float lambda, float b, f
                      (double)lambda, loss_out);
   return check_launch("ssq_round_reg");
 }
+
+// ------------------------------------------------------------------ prepared adaShift (K5p/K6p)
+// In the fused loop (layer_recon_fused_shiftedScale.py:59-66) W, delta, the shift
+// candidates and beta are frozen: only alpha learns.  The reference therefore computes its
+// floors x_q ONCE (channelQuant.py:284-286) and each iteration only re-mixes them.  The
+// prepared path does the same: ssq_adashift_prepare evaluates, once, every floor
+// F_i = floor(W / (delta*s_i)) with the very fp32 ops the recomputing kernels use, packed as
+// int8 bytes into one 32-bit word per weight (S <= 4), and the rounding term
+// h(beta) (or [beta >= 0]) as fp32.  The per-iteration kernels then stream
+// fpack + hterm (+ gWhat) with no divide and no exp per element -- 12 B/elem forward
+// (fpack, hterm in; What out) and 12 B/elem backward (gWhat, fpack, hterm in), the §8(d)
+// algorithmic bytes -- and produce bit-identical What / identical gradients.  The alpha
+// backward reduction is ONE launch: each workgroup writes its fixed-order partials, the
+// last workgroup of a column block (agent-scope counter) sums that block's partials over
+// the row chunks in chunk order (deterministic whichever workgroup is last) and applies the
+// softmax/clamp chain + shift regulariser, then re-arms the counter for the next launch.
+constexpr int kMaxPrepS = 4;
+constexpr int kRBP = 8;            // rows per load batch in the prepared kernels
+
+__global__ __launch_bounds__(kBlock) void adashift_prepare_kernel(
+    const float* __restrict__ W, const float* __restrict__ beta, const float* __restrict__ delta,
+    Shifts sh, Geo g, uint32_t n, int hard_r, uint32_t* __restrict__ fpack,
+    float* __restrict__ hterm, int* __restrict__ overflow) {
+  const uint32_t stride = gridDim.x * blockDim.x;
+  int bad = 0;
+  for (uint32_t e = blockIdx.x * blockDim.x + threadIdx.x; e < n; e += stride) {
+    const uint32_t co = e / g.CiK;
+    const float w = W[e], d = delta[co];
+    uint32_t word = 0;
+    for (int i = 0; i < sh.n; ++i) {
+      const float F = floorf(w / __fmul_rn(d, sh.s[i]));   // = soft_floor's candidate
+      bad |= !(F >= -128.0f && F <= 127.0f);
+      const int fi = F >= -128.0f && F <= 127.0f ? (int)F : 0;
+      word |= ((uint32_t)(fi & 0xff)) << (8 * i);
+    }
+    fpack[e] = word;
+    const float b = beta[e];
+    hterm[e] = hard_r ? (b >= 0.0f ? 1.0f : 0.0f) : rect_sigmoid(b);
+  }
+  if (bad) atomicOr(overflow, 1);
+}
+
+__device__ __forceinline__ float unpack_floor(uint32_t word, int i) {
+  return (float)(int8_t)(uint8_t)(word >> (8 * i));
+}
+
+// Column tiling of the prepared kernels: whole input channels per workgroup (as
+// col_tiling), row chunks of >= 8 rows so each thread keeps 2-3 x 8 loads in flight and the
+// partials stay small (nchunk x Ci x S doubles), ~1536 workgroups at most.
+static ColTiling col_tiling_prep(const Geo& g) {
+  ColTiling t;
+  t.ncb = g.K >= (uint32_t)kBlock ? 1u : (uint32_t)kBlock / g.K;
+  if (t.ncb > g.Ci) t.ncb = g.Ci;
+  t.ncolblk = (g.Ci + t.ncb - 1) / t.ncb;
+  t.threads = (t.ncb * g.K + kWave - 1) / kWave * kWave;
+  uint32_t want = 1536 / t.ncolblk;
+  const uint32_t by_rows = (g.Co + kRBP - 1) / kRBP;
+  if (want > by_rows) want = by_rows;
+  if (want > kMaxChunks) want = kMaxChunks;
+  if (want < 1) want = 1;
+  t.R = (g.Co + want - 1) / want;
+  t.nchunk = (g.Co + t.R - 1) / t.R;
+  return t;
+}
+
+template <int NS, int HARD_T>
+__global__ __launch_bounds__(1024) void shift_fwd_prep(
+    const uint32_t* __restrict__ fpack, const float* __restrict__ hterm,
+    const float* __restrict__ alpha, const float* __restrict__ delta, const float* __restrict__ zp,
+    Geo g, ColTiling tl, float lo, float hi, float* __restrict__ What,
+    uint8_t* __restrict__ codes) {
+  const uint32_t ci0 = blockIdx.x * tl.ncb;
+  const uint32_t nci = min(tl.ncb, g.Ci - ci0);
+  const uint32_t t = threadIdx.x;
+  if (t >= nci * g.K) return;
+  const uint32_t ci = ci0 + t / g.K, j = ci0 * g.K + t;
+  float a[kMaxS], p[kMaxS];
+  load_row(alpha, ci, NS, a);
+  soft_targets<kMaxS>(a, NS, nullptr, p);
+  const int sel = argmax_first(p, NS);
+  const uint32_t co0 = blockIdx.y * tl.R, co1 = min(co0 + tl.R, g.Co);
+  auto one = [&](uint32_t co, uint32_t fw, float h, float d, float z) {
+    float xf;
+    if (HARD_T) {
+      xf = unpack_floor(fw, sel);
+    } else {
+      xf = __fmul_rn(unpack_floor(fw, 0), p[0]);
+#pragma unroll
+      for (int i = 1; i < NS; ++i) xf = __fadd_rn(xf, __fmul_rn(unpack_floor(fw, i), p[i]));
+    }
+    const float q = clampf(__fadd_rn(__fadd_rn(xf, h), z), lo, hi);
+    const uint32_t e = co * g.CiK + j;
+    What[e] = __fmul_rn(__fsub_rn(q, z), __fmul_rn(d, 1.0f));
+    if (codes) codes[e] = (uint8_t)((int)q & 0xff);
+  };
+  uint32_t co = co0;
+  for (; co + kRBP <= co1; co += kRBP) {
+    uint32_t fw[kRBP];
+    float h[kRBP], d[kRBP], z[kRBP];
+#pragma unroll
+    for (int r = 0; r < kRBP; ++r) {
+      const uint32_t e = (co + r) * g.CiK + j;
+      fw[r] = fpack[e];
+      h[r] = hterm[e];
+      d[r] = delta[co + r];
+      z[r] = zp[co + r];
+    }
+#pragma unroll
+    for (int r = 0; r < kRBP; ++r) one(co + r, fw[r], h[r], d[r], z[r]);
+  }
+  for (; co < co1; ++co) {
+    const uint32_t e = co * g.CiK + j;
+    one(co, fpack[e], hterm[e], delta[co], zp[co]);
+  }
+}
+
+// Backward: stage-1 sums of g_int * F_i per (chunk, ci) into part[(ci*nchunk + chunk)*S + i],
+// then the last-arriving workgroup of the column block finishes its input channels.
+template <int NS>
+__global__ __launch_bounds__(1024) void alpha_bwd_prep(
+    const float* __restrict__ gWhat, const uint32_t* __restrict__ fpack,
+    const float* __restrict__ hterm, const float* __restrict__ alpha,
+    const float* __restrict__ delta, const float* __restrict__ zp, Geo g, ColTiling tl, float lo,
+    float hi, float reg_lambda, float reg_b, const float* __restrict__ reg_dev,
+    double* __restrict__ part, unsigned* __restrict__ counters, float* __restrict__ galpha,
+    float* __restrict__ reg_vals) {
+  extern __shared__ double red[];  // [threads][S]
+  __shared__ int is_last;
+  const uint32_t ci0 = blockIdx.x * tl.ncb;
+  const uint32_t nci = min(tl.ncb, g.Ci - ci0);
+  const uint32_t t = threadIdx.x;
+  double acc[NS];
+#pragma unroll
+  for (int i = 0; i < NS; ++i) acc[i] = 0.0;
+  if (t < nci * g.K) {
+    const uint32_t ci = ci0 + t / g.K, j = ci0 * g.K + t;
+    float a[kMaxS], p[kMaxS];
+    load_row(alpha, ci, NS, a);
+    soft_targets<kMaxS>(a, NS, nullptr, p);
+    auto one = [&](uint32_t fw, float h, float d, float z, float gy) {
+      float F[NS];
+#pragma unroll
+      for (int i = 0; i < NS; ++i) F[i] = unpack_floor(fw, i);
+      float xf = __fmul_rn(F[0], p[0]);
+#pragma unroll
+      for (int i = 1; i < NS; ++i) xf = __fadd_rn(xf, __fmul_rn(F[i], p[i]));
+      const float u = __fadd_rn(__fadd_rn(xf, h), z);
+      const float gi = (u >= lo && u <= hi) ? __fmul_rn(gy, __fmul_rn(d, 1.0f)) : 0.0f;
+#pragma unroll
+      for (int i = 0; i < NS; ++i) acc[i] += (double)gi * (double)F[i];
+    };
+    const uint32_t co0 = blockIdx.y * tl.R, co1 = min(co0 + tl.R, g.Co);
+    uint32_t co = co0;
+    for (; co + kRBP <= co1; co += kRBP) {
+      uint32_t fw[kRBP];
+      float h[kRBP], d[kRBP], z[kRBP], gy[kRBP];
+#pragma unroll
+      for (int r = 0; r < kRBP; ++r) {
+        const uint32_t e = (co + r) * g.CiK + j;
+        fw[r] = fpack[e];
+        h[r] = hterm[e];
+        gy[r] = gWhat[e];
+        d[r] = delta[co + r];
+        z[r] = zp[co + r];
+      }
+#pragma unroll
+      for (int r = 0; r < kRBP; ++r) one(fw[r], h[r], d[r], z[r], gy[r]);
+    }
+    for (; co < co1; ++co) {
+      const uint32_t e = co * g.CiK + j;
+      one(fpack[e], hterm[e], delta[co], zp[co], gWhat[e]);
+    }
+  }
+#pragma unroll
+  for (int i = 0; i < NS; ++i) red[t * NS + i] = acc[i];
+  __syncthreads();
+  if (t < nci) {
+#pragma unroll
+    for (int i = 0; i < NS; ++i) {
+      double sum = 0.0;
+      for (uint32_t k = 0; k < g.K; ++k) sum += red[(t * g.K + k) * NS + i];
+      part[((size_t)(ci0 + t) * tl.nchunk + blockIdx.y) * NS + i] = sum;
+    }
+  }
+  if (tl.nchunk > 1) {
+    // release this workgroup's partials, then count it in; the last one acquires them all
+    __threadfence();
+    __syncthreads();
+    if (t == 0) {
+      const unsigned prev = atomicAdd(&counters[blockIdx.x], 1u);
+      is_last = prev == tl.nchunk - 1;
+    }
+    __syncthreads();
+    if (!is_last) return;
+    __threadfence();
+  }
+  if (t < nci) {
+    const uint32_t ci = ci0 + t;
+    if (reg_dev) {
+      reg_lambda = reg_dev[0];
+      reg_b = reg_dev[1];
+    }
+    double tot[kMaxS];
+    const double* pp = part + (size_t)ci * tl.nchunk * NS;
+#pragma unroll
+    for (int i = 0; i < NS; ++i) tot[i] = 0.0;
+    for (uint32_t c = 0; c < tl.nchunk; ++c) {
+#pragma unroll
+      for (int i = 0; i < NS; ++i) tot[i] += __builtin_nontemporal_load(pp + (size_t)c * NS + i);
+    }
+    float a[kMaxS], ga[kMaxS];
+    load_row(alpha, ci, NS, a);
+    const float reg = alpha_chain(a, NS, tot, reg_lambda, reg_b, 0, ga);
+#pragma unroll
+    for (int i = 0; i < NS; ++i) galpha[(size_t)ci * NS + i] = ga[i];
+    if (reg_vals) reg_vals[ci] = reg;
+  }
+  if (t == 0 && tl.nchunk > 1) counters[blockIdx.x] = 0u;  // re-armed for the next launch
+}
+
+extern "C" int ssq_adashift_prepare(const float* W, const float* beta, const float* delta,
+                                    const float* shifts, int S, int64_t Co, int64_t Ci, int64_t K,
+                                    int hard_round, uint32_t* fpack, float* hterm, int* overflow,
+                                    ssq_stream_t stream) {
+  SSQ_GEO(Co, Ci, K, 0, g);
+  SSQ_SHIFTS(shifts, S, sh);
+  SSQ_REQUIRE(S <= kMaxPrepS, SSQ_E_ARG, "ssq_adashift_prepare: S <= %d", kMaxPrepS);
+  SSQ_REQUIRE(W && beta && delta && fpack && hterm && overflow, SSQ_E_ARG,
+              "ssq_adashift_prepare: null");
+  const uint32_t n = g.Co * g.CiK;
+  hipLaunchKernelGGL(adashift_prepare_kernel, dim3(grid_for(n, kBlock)), dim3(kBlock), 0,
+                     (hipStream_t)stream, W, beta, delta, sh, g, n, hard_round, fpack, hterm,
+                     overflow);
+  return check_launch("ssq_adashift_prepare");
+}
+
+extern "C" int ssq_adashift_fwd_prepared(const uint32_t* fpack, const float* hterm,
+                                         const float* alpha, const float* delta, const float* zp,
+                                         int S, int64_t Co, int64_t Ci, int64_t K, int hard_targets,
+                                         int qmin, int qmax, float* What, void* codes,
+                                         ssq_stream_t stream) {
+  SSQ_GEO(Co, Ci, K, 0, g);
+  SSQ_REQUIRE(S >= 1 && S <= kMaxPrepS, SSQ_E_ARG, "ssq_adashift_fwd_prepared: 1 <= S <= %d",
+              kMaxPrepS);
+  SSQ_REQUIRE(fpack && hterm && alpha && delta && zp && What, SSQ_E_ARG,
+              "ssq_adashift_fwd_prepared: null");
+  const ColTiling tl = col_tiling_prep(g);
+  SSQ_REQUIRE(tl.threads <= 1024, SSQ_E_ARG, "ssq_adashift_fwd_prepared: K > 1024");
+  hipStream_t s = (hipStream_t)stream;
+  const float lo = (float)qmin, hi = (float)qmax;
+#define SSQ_FWDP(NS)                                                                            \
+  do {                                                                                          \
+    if (hard_targets)                                                                           \
+      hipLaunchKernelGGL((shift_fwd_prep<NS, 1>), dim3(tl.ncolblk, tl.nchunk), dim3(tl.threads), \
+                         0, s, fpack, hterm, alpha, delta, zp, g, tl, lo, hi, What,             \
+                         (uint8_t*)codes);                                                      \
+    else                                                                                        \
+      hipLaunchKernelGGL((shift_fwd_prep<NS, 0>), dim3(tl.ncolblk, tl.nchunk), dim3(tl.threads), \
+                         0, s, fpack, hterm, alpha, delta, zp, g, tl, lo, hi, What,             \
+                         (uint8_t*)codes);                                                      \
+  } while (0)
+  switch (S) {
+    case 1: SSQ_FWDP(1); break;
+    case 2: SSQ_FWDP(2); break;
+    case 3: SSQ_FWDP(3); break;
+    default: SSQ_FWDP(4); break;
+  }
+#undef SSQ_FWDP
+  return check_launch("ssq_adashift_fwd_prepared");
+}
+
+extern "C" size_t ssq_adashift_bwd_prepared_workspace_size(int64_t Co, int64_t Ci, int64_t K,
+                                                           int S) {
+  Geo g;
+  if (S < 1 || S > kMaxPrepS || make_geo(Co, Ci, K, 0, g) != SSQ_OK) return 0;
+  const ColTiling t = col_tiling_prep(g);
+  return (size_t)t.nchunk * g.Ci * S * sizeof(double);
+}
+
+extern "C" int64_t ssq_adashift_bwd_prepared_counters(int64_t Co, int64_t Ci, int64_t K) {
+  Geo g;
+  if (make_geo(Co, Ci, K, 0, g) != SSQ_OK) return 0;
+  return col_tiling_prep(g).ncolblk;
+}
+
+extern "C" int ssq_adashift_bwd_prepared(const float* gWhat, const uint32_t* fpack,
+                                         const float* hterm, const float* alpha,
+                                         const float* delta, const float* zp, int S, int64_t Co,
+                                         int64_t Ci, int64_t K, int qmin, int qmax,
+                                         float reg_lambda, float reg_b, const float* reg_dev,
+                                         float* galpha, float* reg_vals, unsigned* counters,
+                                         void* ws, size_t ws_bytes, ssq_stream_t stream) {
+  SSQ_GEO(Co, Ci, K, 0, g);
+  SSQ_REQUIRE(S >= 1 && S <= kMaxPrepS, SSQ_E_ARG, "ssq_adashift_bwd_prepared: 1 <= S <= %d",
+              kMaxPrepS);
+  SSQ_REQUIRE(gWhat && fpack && hterm && alpha && delta && zp && galpha && counters, SSQ_E_ARG,
+              "ssq_adashift_bwd_prepared: null");
+  const ColTiling tl = col_tiling_prep(g);
+  SSQ_REQUIRE(tl.threads <= 1024, SSQ_E_ARG, "ssq_adashift_bwd_prepared: K > 1024");
+  SSQ_REQUIRE(ws && ws_bytes >= ssq_adashift_bwd_prepared_workspace_size(Co, Ci, K, S), SSQ_E_WS,
+              "ssq_adashift_bwd_prepared: workspace too small");
+  hipStream_t s = (hipStream_t)stream;
+  const size_t lds = (size_t)tl.threads * S * sizeof(double);
+  const float lo = (float)qmin, hi = (float)qmax;
+#define SSQ_BWDP(NS)                                                                            \
+  hipLaunchKernelGGL((alpha_bwd_prep<NS>), dim3(tl.ncolblk, tl.nchunk), dim3(tl.threads), lds, s, \
+                     gWhat, fpack, hterm, alpha, delta, zp, g, tl, lo, hi, reg_lambda, reg_b,   \
+                     reg_dev, (double*)ws, counters, galpha, reg_vals)
+  switch (S) {
+    case 1: SSQ_BWDP(1); break;
+    case 2: SSQ_BWDP(2); break;
+    case 3: SSQ_BWDP(3); break;
+    default: SSQ_BWDP(4); break;
+  }
+#undef SSQ_BWDP
+  return check_launch("ssq_adashift_bwd_prepared");
+}

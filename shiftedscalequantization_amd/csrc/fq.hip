@@ -371,7 +371,7 @@ __global__ __launch_bounds__(kBlock) void fq_bwd_rows(const float* __restrict__ 
                                                       const float* __restrict__ gy,
                                                       const float* __restrict__ delta,
                                                       const float* __restrict__ zp,
-                                                      int64_t inner, float lo, float hi,
+                                                      int64_t inner, float lo, float hi, int ste,
                                                       float* __restrict__ gx,
                                                       float* __restrict__ gdelta,
                                                       float* __restrict__ gzp) {
@@ -400,12 +400,12 @@ __global__ __launch_bounds__(kBlock) void fq_bwd_rows(const float* __restrict__ 
   a2 = block_sum(a2, red);
   a3 = block_sum(a3, red);
   if (threadIdx.x == 0) {
-    if (gdelta) gdelta[c] = (float)(a0 - a1);
+    if (gdelta) gdelta[c] = (float)(ste ? a0 - a1 : a0);
     if (gzp) gzp[c] = (float)(a2 - a3);
   }
 }
 
-__global__ void fq_bwd_finalize(const double* __restrict__ part, int nblk,
+__global__ void fq_bwd_finalize(const double* __restrict__ part, int nblk, int ste,
                                 float* __restrict__ gdelta, float* __restrict__ gzp) {
   __shared__ double red[16];
   double a[4] = {0, 0, 0, 0};
@@ -413,7 +413,7 @@ __global__ void fq_bwd_finalize(const double* __restrict__ part, int nblk,
     for (int k = 0; k < 4; ++k) a[k] += part[4 * (int64_t)b + k];
   for (int k = 0; k < 4; ++k) a[k] = block_sum(a[k], red);
   if (threadIdx.x == 0) {
-    if (gdelta) gdelta[0] = (float)(a[0] - a[1]);
+    if (gdelta) gdelta[0] = (float)(ste ? a[0] - a[1] : a[0]);
     if (gzp) gzp[0] = (float)(a[2] - a[3]);
   }
 }
@@ -669,10 +669,14 @@ extern "C" size_t ssq_fq_bwd_workspace_size(int64_t n, int64_t inner, int64_t nc
   return nch == 1 ? (size_t)kBwdBlocks * 4 * sizeof(double) : 0;
 }
 
-static int fq_bwd(const char* what, int relu, const float* x, const float* gy,
+// ste = 1: round_ste (UAQ, quant_layer.py:92-98): gx = STE, gdelta includes the x/delta
+// path.  ste = 0: torch.round (no gradient through the rounding; ChannelQuantAct 'none',
+// channelQuantAct.py:56-67): gx is not written (it is zero) and gdelta = sum g*(q - zp).
+static int fq_bwd(const char* what, int relu, int ste, const float* x, const float* gy,
                   const float* delta, const float* zp, int64_t n, int64_t inner, int64_t nch,
                   int qmin, int qmax, float* gx, float* gdelta, float* gzp, void* ws,
                   size_t ws_bytes, hipStream_t s) {
+  if (!ste) gx = nullptr;
   SSQ_REQUIRE(n >= 1 && inner >= 1 && nch >= 1 && qmin < qmax, SSQ_E_ARG, "%s: sizes", what);
   SSQ_REQUIRE(x && gy && delta && zp, SSQ_E_ARG, "%s: null pointer", what);
   const float lo = (float)qmin, hi = (float)qmax;
@@ -698,13 +702,13 @@ static int fq_bwd(const char* what, int relu, const float* x, const float* gy,
     }
     if (want_red)
       hipLaunchKernelGGL(fq_bwd_finalize, dim3(1), dim3(kBlock), 0, s, (const double*)ws, grid,
-                         gdelta, gzp);
+                         ste, gdelta, gzp);
   } else {
     SSQ_REQUIRE(!relu, SSQ_E_ARG, "%s: the ReLU-fused backward is per-tensor only", what);
     SSQ_REQUIRE(n == nch * inner, SSQ_E_ARG,
                 "%s: per-channel reduction needs contiguous rows (n == nch*inner)", what);
     hipLaunchKernelGGL(fq_bwd_rows, dim3((unsigned)nch), dim3(kBlock), 0, s, x, gy, delta, zp,
-                       inner, lo, hi, gx, gdelta, gzp);
+                       inner, lo, hi, ste, gx, gdelta, gzp);
   }
   return check_launch(what);
 }
@@ -713,7 +717,7 @@ extern "C" int ssq_fq_bwd(const float* x, const float* gy, const float* delta, c
                           int64_t n, int64_t inner, int64_t nch, int qmin, int qmax, float* gx,
                           float* gdelta, float* gzp, void* ws, size_t ws_bytes,
                           ssq_stream_t stream) {
-  return fq_bwd("ssq_fq_bwd", 0, x, gy, delta, zp, n, inner, nch, qmin, qmax, gx, gdelta,
+  return fq_bwd("ssq_fq_bwd", 0, 1, x, gy, delta, zp, n, inner, nch, qmin, qmax, gx, gdelta,
                 gzp, ws, ws_bytes, (hipStream_t)stream);
 }
 
@@ -721,7 +725,7 @@ extern "C" int ssq_fq_relu_bwd(const float* x, const float* gy, const float* del
                                const float* zp, int64_t n, int qmin, int qmax, float* gx,
                                float* gdelta, float* gzp, void* ws, size_t ws_bytes,
                                ssq_stream_t stream) {
-  return fq_bwd("ssq_fq_relu_bwd", 1, x, gy, delta, zp, n, n, 1, qmin, qmax, gx, gdelta,
+  return fq_bwd("ssq_fq_relu_bwd", 1, 1, x, gy, delta, zp, n, n, 1, qmin, qmax, gx, gdelta,
                 gzp, ws, ws_bytes, (hipStream_t)stream);
 }
 
@@ -729,8 +733,16 @@ extern "C" int ssq_fq_relu6_bwd(const float* x, const float* gy, const float* de
                                 const float* zp, int64_t n, int qmin, int qmax, float* gx,
                                 float* gdelta, float* gzp, void* ws, size_t ws_bytes,
                                 ssq_stream_t stream) {
-  return fq_bwd("ssq_fq_relu6_bwd", 2, x, gy, delta, zp, n, n, 1, qmin, qmax, gx, gdelta,
+  return fq_bwd("ssq_fq_relu6_bwd", 2, 1, x, gy, delta, zp, n, n, 1, qmin, qmax, gx, gdelta,
                 gzp, ws, ws_bytes, (hipStream_t)stream);
+}
+
+extern "C" int ssq_fq_round_bwd(const float* x, const float* gy, const float* delta,
+                                const float* zp, int64_t n, int64_t inner, int64_t nch, int qmin,
+                                int qmax, float* gdelta, float* gzp, void* ws, size_t ws_bytes,
+                                ssq_stream_t stream) {
+  return fq_bwd("ssq_fq_round_bwd", 0, 0, x, gy, delta, zp, n, inner, nch, qmin, qmax, nullptr,
+                gdelta, gzp, ws, ws_bytes, (hipStream_t)stream);
 }
 
 extern "C" int ssq_stream_copy(const float* src, float* dst, int64_t n, ssq_stream_t stream) {

@@ -27,6 +27,52 @@ def build_ShiftedChannelQuantMSELayer(model, curName, layer, delta=1.0, **kwargs
     layer.weight_quantizer.init_scale(layer.org_weight.data)
 
 
+def build_ShiftedChannelQuantMSEBlock(model, prv_name, block, delta=1.0, **kwargs):
+    """myScaledMethods.py:27-40: every direct QuantModule child still on a UAQ."""
+    for name, layer in block.named_children():
+        if isinstance(layer, QuantModule) and isinstance(layer.weight_quantizer, UniformAffineQuantizer):
+            build_ShiftedChannelQuantMSELayer(model, prv_name + '.' + name, layer, delta, **kwargs)
+
+
+def build_ShiftedChannelQuantMSE(model, layerDisabled, prv_name="", delta=1.0, **kwargs):
+    """The nested builder of channelShift_wMSE (ShiftedScaleQuant.py:155-173), walk as
+    written: a QuantModule gets a ChannelQuantMSE unless it is ignore_reconstruction or
+    listed in layerDisabled; a QuantBasicBlock listed in layerDisabled has ALL its layers
+    built (the reference's inverted test, kept), otherwise it is recursed into."""
+    from .quant.quant_block import QuantBasicBlock
+    for name, module in model.named_children():
+        curName = prv_name + '.' + name
+        if isinstance(module, QuantModule):
+            if module.ignore_reconstruction:
+                continue
+            if curName not in layerDisabled:
+                build_ShiftedChannelQuantMSELayer(model, curName, module, delta, **kwargs)
+        elif isinstance(module, QuantBasicBlock):
+            if module.ignore_reconstruction:
+                continue
+            if curName in layerDisabled:
+                build_ShiftedChannelQuantMSEBlock(model, curName, module, delta, **kwargs)
+            else:
+                build_ShiftedChannelQuantMSE(module, layerDisabled, curName, delta, **kwargs)
+        else:
+            build_ShiftedChannelQuantMSE(module, layerDisabled, curName, delta, **kwargs)
+
+
+def channelShift_wMSE(qnn, cali_data, level=1, threshold=1.0, opt_mode='max',
+                      shiftTarget=(31 / 32, 33 / 32, 1.0), layerDisabled=('.model.fc',),
+                      init_samples=64):
+    """ShiftedScaleQuant.py:119-183, the path the shipped entry point runs (`--test=True`,
+    :361): weight-quant init on cali[:64], then per-(Ci,kh,kw) input scales chosen by
+    ChannelQuantMSE.init_scale (K10) for every reconstructable layer but the fc.  No
+    reconstruction loop; returns the quantized model (weight quant on, act quant off)."""
+    qnn.set_quant_state(True, False)
+    with torch.no_grad():
+        qnn(cali_data[:init_samples])
+    build_ShiftedChannelQuantMSE(qnn, list(layerDisabled), '', delta=1.0, shiftTarget=list(shiftTarget),
+                                 level=level, threshold=threshold, opt_mode=opt_mode)
+    return qnn
+
+
 def build_ShiftedChannelQuantLayer(model, curName, layer, delta=1.0, **kwargs):
     skip = tuple(kwargs.get('skipShiftLayer', []))
     shiftTarget = kwargs['shiftTarget'] if not (skip and curName.startswith(skip)) else [2 / 2]

@@ -111,6 +111,47 @@ def fake_quant(x, delta, zp, n_bits, sym=False):
     return FakeQuantFn.apply(x, delta, zp, n_bits, sym)
 
 
+class RoundQuantFn(torch.autograd.Function):
+    """q/dq with torch.round (NO straight-through estimator) at delta*scale, clamp
+    [lo, hi]: ChannelQuantAct 'none' mode (channelQuantAct.py:56-67).  The reference's
+    autograd gives d/dx = 0 (round has a zero gradient), d/ddelta = scale * sum g*(q-zp)
+    (through the product delta*shiftedScale), d/dzp = -sum_{clamped} g*delta*scale."""
+
+    @staticmethod
+    def forward(ctx, x, delta, zp, n_bits, sym, scale):
+        y, _ = fake_quant_fwd(x, delta, zp, n_bits, sym, scale=scale)
+        ctx.save_for_backward(x, delta, zp)
+        ctx.q = (n_bits, sym, scale)
+        return y
+
+    @staticmethod
+    def backward(ctx, gy):
+        x, delta, zp = ctx.saved_tensors
+        n_bits, sym, scale = ctx.q
+        need_x, need_d, need_z = ctx.needs_input_grad[:3]
+        gx = torch.zeros_like(x) if need_x else None
+        if not (need_d or need_z):
+            return gx, None, None, None, None, None
+        x, gy = x.contiguous(), gy.contiguous()
+        # the product delta*shiftedScale as the reference forms it (tensor * python float)
+        t = (delta.detach() * scale).contiguous()
+        z = _zp_like(zp.detach(), t).contiguous()
+        inner, nch = _channel_layout(x, t)
+        lo, hi = qrange(n_bits, sym)
+        gt = torch.empty(t.numel(), dtype=torch.float32, device=x.device)
+        gz = torch.empty(z.numel(), dtype=torch.float32, device=x.device) if need_z else None
+        wsb = query("ssq_fq_bwd_workspace_size", x.numel(), inner, nch)
+        ws, wsn = workspace(wsb, x.device)
+        call("ssq_fq_round_bwd", _vp(x), _vp(gy), _vp(t), _vp(z), x.numel(), inner, nch, lo, hi,
+             _vp(gt), _vp(gz), ws, wsn, stream_of(x))
+        gd = (gt * scale).view(delta.shape) if need_d else None
+        return (gx, gd, None if gz is None else gz.view(zp.shape), None, None, None)
+
+
+def round_quant(x, delta, zp, n_bits, sym=False, scale=1.0):
+    return RoundQuantFn.apply(x, delta, zp, n_bits, sym, float(scale))
+
+
 def fake_quant_multi(xs, deltas, zps, n_bits, sym=False):
     """Every tensor of a list in one launch (per-channel params staged in LDS)."""
     n = len(xs)
@@ -266,6 +307,72 @@ class AdaShiftFn(torch.autograd.Function):
 def adashift(alpha, beta, w, delta, zp, shifts, n_bits, sym, hard_t, hard_r, reg=None):
     return AdaShiftFn.apply(alpha, beta, w, delta, zp, tuple(shifts), n_bits, sym, bool(hard_t),
                             bool(hard_r), reg)
+
+
+class AdaShiftPrep:
+    """Loop-invariant state of a conv ChannelQuant in 'adaShift' mode (W, delta, shifts,
+    beta frozen, as in the fused loop): the packed int8 floors and h(beta) of
+    ssq_adashift_prepare, plus the backward's zeroed reduction counters.  `ok` is False
+    when a floor does not fit int8 (the caller keeps the recomputing kernels)."""
+
+    def __init__(self, w, beta, delta, shifts, hard_r):
+        w, wp = fptr(w.detach(), "weight")
+        b, bp = fptr(beta.detach(), "beta")
+        d, dp = fptr(delta.detach(), "delta")
+        Co, Ci, K, is_fc = geometry(w)
+        if is_fc:
+            raise A.SSQError("AdaShiftPrep: conv weights only")
+        self.geo = (Co, Ci, K)
+        self.S = len(shifts)
+        self.fpack = torch.empty(w.shape, dtype=torch.int32, device=w.device)
+        self.hterm = torch.empty_like(w)
+        flag = torch.zeros(1, dtype=torch.int32, device=w.device)
+        call("ssq_adashift_prepare", wp, bp, dp, A.shifts_arg(shifts), self.S, Co, Ci, K,
+             int(hard_r), _vp(self.fpack), _vp(self.hterm), _vp(flag), stream_of(w))
+        self.ok = int(flag.item()) == 0      # one sync, at preparation time only
+        n = int(query("ssq_adashift_bwd_prepared_counters", Co, Ci, K))
+        self.counters = torch.zeros(max(n, 1), dtype=torch.int32, device=w.device)
+
+
+class AdaShiftPrepFn(torch.autograd.Function):
+    """ChannelQuant 'adaShift' forward from the prepared floors (K5p) and its alpha
+    backward (K6p, one launch, shift regulariser folded in as in AdaShiftFn)."""
+
+    @staticmethod
+    def forward(ctx, alpha, prep, delta, zp, n_bits, sym, hard_t, reg):
+        a, ap = fptr(alpha.detach(), "alpha")
+        d, dp = fptr(delta.detach(), "delta")
+        z, zpp = fptr(zp.detach(), "zero_point")
+        Co, Ci, K = prep.geo
+        lo, hi = qrange(n_bits, sym)
+        out = torch.empty_like(prep.hterm)
+        call("ssq_adashift_fwd_prepared", _vp(prep.fpack), _vp(prep.hterm), ap, dp, zpp, prep.S,
+             Co, Ci, K, int(hard_t), lo, hi, _vp(out), None, stream_of(out))
+        ctx.save_for_backward(a, d, z)
+        ctx.cfg = (prep, n_bits, sym, hard_t, reg)
+        return out
+
+    @staticmethod
+    def backward(ctx, g):
+        a, d, z = ctx.saved_tensors
+        prep, n_bits, sym, hard_t, reg = ctx.cfg
+        if not ctx.needs_input_grad[0] or hard_t:
+            return (None,) * 8
+        g = g.contiguous()
+        Co, Ci, K = prep.geo
+        lo, hi = qrange(n_bits, sym)
+        ga = torch.empty_like(a)
+        lam, bb, reg_vals, reg_dev = (0.0, 0.0, None, None) if reg is None else reg
+        wsb = query("ssq_adashift_bwd_prepared_workspace_size", Co, Ci, K, prep.S)
+        ws, wsn = workspace(wsb, g.device)
+        call("ssq_adashift_bwd_prepared", _vp(g), _vp(prep.fpack), _vp(prep.hterm), _vp(a),
+             _vp(d), _vp(z), prep.S, Co, Ci, K, lo, hi, float(lam), float(bb), _vp(reg_dev),
+             _vp(ga), _vp(reg_vals), _vp(prep.counters), ws, wsn, stream_of(g))
+        return (ga, None, None, None, None, None, None, None)
+
+
+def adashift_prepared(alpha, prep, delta, zp, n_bits, sym, hard_t, reg=None):
+    return AdaShiftPrepFn.apply(alpha, prep, delta, zp, n_bits, sym, bool(hard_t), reg)
 
 
 def adashift_codes(alpha, beta, w, delta, zp, shifts, n_bits, sym):

@@ -18,42 +18,70 @@ def rank():
     return dist.get_rank() if dist.is_available() and dist.is_initialized() else 0
 
 
+# Test hook: when set to a list, every GradBucket.allreduce_ appends (local, reduced) flat
+# copies -- the per-rank gradient before the collective and the summed one after it.
+RECORD = None
+
+
 class GradBucket:
-    """Flat all-reduce bucket over a fixed list of parameters.
+    """Flat all-reduce bucket over the optimised parameters.
 
     average=False reproduces the reference (sum of per-rank gradients); average=True
-    divides by the world size (keeps the single-GPU loss scale)."""
+    divides by the world size (keeps the single-GPU loss scale).
+
+    The parameters that actually receive a gradient are fixed at the first call (the
+    iteration's graph is the same on every rank and every iteration); a parameter that
+    gets none keeps grad=None, as in the reference, so Adam skips it there too.  From then
+    on each such parameter's .grad IS its slice of the flat buffer: attach_() (called after
+    zero_grad) zeroes the buffer and points the grads at the slices, backward accumulates
+    into them in place, and the collective runs on the buffer with no copy in or out."""
 
     def __init__(self, params, average=False):
         self.params = [p for p in params if p.requires_grad]
         self.average = average
-        n = sum(p.numel() for p in self.params)
-        dev = self.params[0].device if self.params else torch.device("cpu")
+        self.live = None
+        self.flat = None
+        self.views = []
+
+    def _build(self):
+        self.live = [p for p in self.params if p.grad is not None]
+        n = sum(p.numel() for p in self.live)
+        dev = self.live[0].device if self.live else torch.device("cpu")
         self.flat = torch.zeros(n, dtype=torch.float32, device=dev)
+        off = 0
+        for p in self.live:
+            self.views.append(self.flat[off:off + p.numel()].view_as(p))
+            off += p.numel()
+
+    def attach_(self):
+        """Zero the bucket and make it the storage of every live gradient."""
+        if self.live is None:
+            return
+        self.flat.zero_()
+        for p, v in zip(self.live, self.views):
+            p.grad = v
 
     def allreduce_(self):
         ws = world()
         if ws == 1 or not self.params:
             return
-        off = 0
-        views = []
-        for p in self.params:
-            n = p.numel()
-            v = self.flat[off:off + n]
+        if self.live is None:
+            self._build()
+        for p, v in zip(self.live, self.views):
             if p.grad is None:
-                v.zero_()
-            else:
-                v.copy_(p.grad.reshape(-1))
-            views.append((p, v))
-            off += n
-        dist.all_reduce(self.flat, op=dist.ReduceOp.SUM)
-        if self.average:
-            self.flat.div_(ws)
-        for p, v in views:
-            if p.grad is None:
-                p.grad = v.view_as(p).clone()
-            else:
-                p.grad.copy_(v.view_as(p))
+                v.zero_()          # (cannot happen after the first call; kept defensive)
+                p.grad = v
+            elif p.grad.data_ptr() != v.data_ptr():
+                v.copy_(p.grad)    # first iteration, or a loop that reset the grads
+                p.grad = v
+        if RECORD is not None:
+            RECORD.append(["local", self.flat.detach().clone()])
+        if self.flat.numel():
+            dist.all_reduce(self.flat, op=dist.ReduceOp.SUM)
+            if self.average:
+                self.flat.div_(ws)
+        if RECORD is not None:
+            RECORD[-1].append(self.flat.detach().clone())
 
 
 def all_average_(t):
@@ -61,6 +89,18 @@ def all_average_(t):
     if ws > 1:
         dist.all_reduce(t, op=dist.ReduceOp.SUM)
         t.div_(ws)
+    return t
+
+
+def broadcast_(t, src=0):
+    if world() > 1:
+        dist.broadcast(t, src)
+    return t
+
+
+def all_sum_(t):
+    if world() > 1:
+        dist.all_reduce(t, op=dist.ReduceOp.SUM)
     return t
 
 

@@ -101,6 +101,8 @@ def _eager_loop(opt_params, loss_func, feeder, bucket, cached_grads, block, iter
         cur_inp, cur_out = feeder.next(perm)
         cur_grad = cached_grads[perm.to(cached_grads.device)] if cached_grads is not None else None
         optimizer.zero_grad()
+        if bucket is not None:
+            bucket.attach_()
         out_quant = block(cur_inp)
         err = loss_func(out_quant, cur_out, cur_grad)
         err.backward()
@@ -178,6 +180,8 @@ def _fast_loop(block, qmodules, opt_params, loss_func, feeder, bucket, iters, ac
                 graph_obj.replay()
             else:
                 optimizer.zero_grad()
+                if bucket is not None:
+                    bucket.attach_()
                 body()
             rec = last['rec'][0]
             loss_func.record(rec, rnd, b)

@@ -53,6 +53,7 @@ class ChannelQuant(nn.Module):
         self._src_kind = None       # 'floor' (init_v_beta) | 'dequant' (init_v)
         self._xq_cache = None
         self._fused_reg = None      # (lambda, b, reg_vals) set by FusedScaleLossFunction
+        self._prep = None           # (key, kernels.AdaShiftPrep) of the prepared path
 
     # ------------------------------------------------------------------ candidates
     @property
@@ -78,8 +79,30 @@ class ChannelQuant(nn.Module):
         self._xq_cache = list(v) if v else None
 
     # ------------------------------------------------------------------ forward
+    def _prepared(self):
+        """The prepared adaShift state (packed floors + h(beta), computed once) when the
+        loop-invariant inputs allow it: conv weight, S <= 4, floor candidates, beta not
+        being learned.  Rebuilt whenever beta, the hard_round flag or the captured weight
+        change (key below); None -> the recomputing kernels."""
+        if (self.isFC or self._src_kind != 'floor' or self.beta is None
+                or len(self.shiftTarget) > 4 or not self._src.is_cuda
+                or (self.beta.requires_grad and torch.is_grad_enabled())):
+            return None
+        key = (self._src.data_ptr(), self._src_delta.data_ptr(), self.beta.data_ptr(),
+               self.beta._version, bool(self.hard_round), tuple(self.shiftTarget))
+        if self._prep is None or self._prep[0] != key:
+            prep = K.AdaShiftPrep(self._src, self.beta, self._src_delta, self.shiftTarget,
+                                  self.hard_round)
+            self._prep = (key, prep if prep.ok else None)
+        return self._prep[1]
+
     def forward(self, x):
         if self.opt_mode == 'adaShift':
+            prep = self._prepared()
+            if prep is not None:
+                return K.adashift_prepared(self.alpha, prep, self._src_delta, self.zero_point,
+                                           self.n_bits, self.sym, self.hard_targets,
+                                           reg=self._fused_reg)
             return K.adashift(self.alpha, self.beta, self._src, self._src_delta, self.zero_point,
                               self.shiftTarget, self.n_bits, self.sym, self.hard_targets,
                               self.hard_round, reg=self._fused_reg)
@@ -133,6 +156,7 @@ class ChannelQuant(nn.Module):
 
     # ------------------------------------------------------------------ inits
     def _capture(self, x, kind):
+        self._prep = None
         self._src = x.detach().contiguous()
         self._src_delta = self.delta.detach().contiguous()
         self._src_kind = kind

@@ -1,7 +1,8 @@
 """ChannelQuantAct (reference: quant/channelQuantAct.py).
 
 Only opt_mode 'none' runs in the reference: per-tensor q/dq at delta*shiftedScale with a
-[0, n-1] clamp (channelQuantAct.py:56-67) -> ssq_fq_fwd/bwd here.  Its init_v refers to an
+[0, n-1] clamp and torch.round -- not round_ste, so no gradient reaches x
+(channelQuantAct.py:56-67) -> ssq_fq_fwd / ssq_fq_round_bwd here.  Its init_v refers to an
 undefined `x` and a missing `isFC`/`x_q` (channelQuantAct.py:125-134, AttributeError /
 NameError [probed]), and the 'adaShift' / 'adaround' branches read attributes that are
 never created, so those modes raise here too, with an explicit message.
@@ -35,11 +36,9 @@ class ChannelQuantAct(nn.Module):
 
     def forward(self, x):
         if self.opt_mode == 'none':
-            if self.shiftedScale == 1.0:
-                return K.fake_quant(x, self.delta, self.zero_point, self.n_bits, False)
-            y, _ = K.fake_quant_fwd(x, self.delta, self.zero_point, self.n_bits, False,
-                                    scale=self.shiftedScale)
-            return y
+            # asymmetric [0, n-1] clamp whatever uaq.sym says (channelQuantAct.py:63)
+            return K.round_quant(x, self.delta, self.zero_point, self.n_bits, False,
+                                 scale=self.shiftedScale)
         raise NotImplementedError(
             f"ChannelQuantAct opt_mode={self.opt_mode!r} is broken in the reference "
             "(channelQuantAct.py:38-61,125-134 read attributes that are never set)")

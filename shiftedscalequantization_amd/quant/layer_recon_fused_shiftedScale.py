@@ -44,8 +44,16 @@ def _weight_quantizers(module):
 GRAPH_WARMUP = 3     # eager iterations before the iteration body is captured
 
 
+def _block_hard_flags(quantizers):
+    """layer_recon_fused_shiftedScale.py:125-129: hard rounding AND hard shift choice."""
+    for q in quantizers:
+        q.hard_round = True
+        q.hard_targets = True
+        q.shiftedDone = True
+
+
 def _fused_loop(block, modules, iters, lmda, model, p, lr, bias_cal, batch_size, dp_average,
-                verbose, iter_hook=None, graph=True):
+                verbose, iter_hook=None, graph=True, set_hard=_block_hard_flags):
     device = next(model.parameters()).device
     quantizers, opt_params, beta_rg = [], [], {}
     for m in modules:
@@ -125,6 +133,8 @@ def _fused_loop(block, modules, iters, lmda, model, p, lr, bias_cal, batch_size,
             graph_obj.replay()
         else:
             optimizer.zero_grad()
+            if bucket is not None:
+                bucket.attach_()
             body()
         loss_func.bookkeep(last['rec'])
         if i % 500 == 0 and verbose:
@@ -152,10 +162,7 @@ def _fused_loop(block, modules, iters, lmda, model, p, lr, bias_cal, batch_size,
         print(f"Soft Round : {start_loss:.6f} -> {as_float(loss_func.rec_loss):.6f} "
               f"{loss_func.round_loss_val}")
     rec_loss_out.append(as_float(loss_func.rec_loss))
-    for q in quantizers:
-        q.hard_round = True
-        q.hard_targets = True
-        q.shiftedDone = True
+    set_hard(quantizers)
     with torch.no_grad():
         quant_out = block(cur_inp)
         loss_func(quant_out, cur_out)
@@ -191,10 +198,22 @@ def layer_recon_fused_shiftedScale(layer: QuantModule, iters: int = 20000, lmda:
                                    dp_average=False, verbose=True, graph=True):
     """layer_recon_fused_shiftedScale.py:144-221.  The reference raises UnboundLocalError
     (`opt_params += ...` before assignment, :156); this implements its evident intent: the
-    block loop on one layer with p = 1.0 (:165) and Adam's default lr."""
+    block loop on one layer with p = 1.0 (:165) and Adam's default lr, finished with the
+    layer variant's own flags (:207-211): hard shift targets + shiftedDone; with adaround
+    the hard flag lands on the LAYER (not its quantizer), so the final 'Hard Round'
+    evaluation keeps the soft rounding h(beta) either way -- reproduced as written."""
     model.train()
+
+    def set_hard(quantizers):
+        if adaround:
+            layer.hard_round = True
+        else:
+            for q in quantizers:
+                q.hard_targets = True
+                q.shiftedDone = True
+
     return _fused_loop(layer, [layer], iters, lmda, model, 1.0, 0.001, bias_cal, batch_size,
-                       dp_average, verbose, None, graph)
+                       dp_average, verbose, None, graph, set_hard=set_hard)
 
 
 class FusedScaleLossFunction:

@@ -26,6 +26,8 @@ def _loop(block, opt_params, optimizer, scheduler, loss_func, iters, batch_size,
     for i in t:
         cur_inp, cur_out = feeder.next()
         optimizer.zero_grad()
+        if bucket is not None:
+            bucket.attach_()
         quant_out = block(cur_inp)
         err = loss_func(quant_out, cur_out)
         err.backward()

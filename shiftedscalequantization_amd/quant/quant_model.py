@@ -1,5 +1,6 @@
 """QuantModel (reference: quant/quant_model.py): fold BN, then recursively replace
 Conv2d/Linear by QuantModule and known residual blocks by quant blocks."""
+import torch
 import torch.nn as nn
 
 from .fold_bn import search_fold_and_remove_bn
@@ -87,9 +88,18 @@ class QuantModel(nn.Module):
             m.use_weight_quant = s
 
     def synchorize_activation_statistics(self):
-        """All-average of activation deltas across ranks (the reference's intent at
-        quant_model.py:78-83, whose linklink call is commented out)."""
-        from ..parallel_dp import all_average_
+        """All-average of the activation deltas across ranks after the act init forward --
+        the reference's intent (quant_model.py:78-83, linklink call commented out; called
+        by Brecq/main_imagenet_dist.py:210-211).  Two additions keep the act quantizers
+        replicated, which the loop's gradient all-reduce assumes: the blocks' own output
+        quantizers (BaseQuantBlock.act_quantizer) are averaged too, and the zero points --
+        integers from each rank's own shard, 0 after a ReLU -- are taken from rank 0."""
+        from ..parallel_dp import all_average_, broadcast_
+        from .quant_block import BaseQuantBlock
         for m in self.modules():
-            if isinstance(m, QuantModule) and m.act_quantizer.delta is not None:
-                all_average_(m.act_quantizer.delta.data)
+            if isinstance(m, (QuantModule, BaseQuantBlock)):
+                aq = m.act_quantizer
+                if getattr(aq, 'delta', None) is not None and getattr(aq, 'inited', True):
+                    all_average_(aq.delta.data)
+                    if getattr(aq, 'zero_point', None) is not None and torch.is_tensor(aq.zero_point):
+                        broadcast_(aq.zero_point.data, 0)

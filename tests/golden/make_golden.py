@@ -730,9 +730,320 @@ def gen_recon_blocks(iters=30, brecq_iters=10, n_cali=16, res=16):
         save(f"recon_block_{kind}", **out)
 
 
+# ------------------------------------------------------------------ round-2 goldens
+def gen_act_quant():
+    """ChannelQuantAct 'none' mode (channelQuantAct.py:36-67): per-tensor A4 q/dq at
+    delta*shiftedScale with a [0, n-1] clamp and torch.round (no STE: d/dx = 0).  The
+    delta/zero_point come from a UAQ 'mse' init on ReLU'd data; the evaluated tensor keeps
+    negatives and large values so both clamp edges are hit."""
+    from quant.channelQuantAct import ChannelQuantAct
+    g = torch.Generator().manual_seed(1005)
+    out = {}
+    base = edge_tensor(g, (4, 6, 7, 7), 1.0)
+    uaq = UniformAffineQuantizer(n_bits=4, channel_wise=False, scale_method="mse", leaf_param=True)
+    with torch.no_grad():
+        uaq(torch.relu(base))
+    x = base * 1.5
+    out["x"] = t2n(x)
+    out["delta"] = t2n(uaq.delta.reshape(-1))
+    out["zp"] = t2n(uaq.zero_point.reshape(-1))
+    scales = (1.0, 33 / 32, 31 / 32, 0.5)
+    out["scales"] = np.array(scales, np.float64)
+    for k, s in enumerate(scales):
+        q = ChannelQuantAct(uaq=uaq, shiftTarget=[1.0, 0.5])
+        q.shiftedScale = s
+        xr = x.clone().requires_grad_(True)
+        y = q(xr)
+        gy = torch.randn(x.shape, generator=g)
+        uaq.delta.grad = None
+        uaq.zero_point.grad = None
+        (y * gy).sum().backward()
+        out[f"s{k}_y"] = t2n(y)
+        out[f"s{k}_gy"] = t2n(gy)
+        out[f"s{k}_gx"] = t2n(xr.grad) if xr.grad is not None else np.zeros(x.shape, np.float32)
+        out[f"s{k}_gdelta"] = t2n(uaq.delta.grad.reshape(-1))
+        out[f"s{k}_gzp"] = t2n(uaq.zero_point.grad.reshape(-1))
+    save("act_quant", **out)
+
+
+def gen_recon_layer_fused(iters=30, n_cali=16, res=16):
+    """a19: layer_recon_fused_shiftedScale raises UnboundLocalError in the reference
+    (`opt_params += ...` before assignment, layer_recon_fused_shiftedScale.py:156).  Its
+    evident intent -- the fused loop on ONE QuantModule with p = 1 (:165) and Adam's
+    default lr (= the block loop's 1e-3) -- is run here by the reference's own block loop
+    (block_recon_fused_shiftedScale accepts a QuantModule: named_modules() yields it) with
+    the loss class pinned to p = 1.  The layer variant's post-loop flags (:207-211: hard
+    targets + shiftedDone, hard_round only on the LAYER when adaround) are then applied
+    and the 'Hard Round' loss evaluated the way :212-215 do."""
+    qnn = _build_tiny_qnn()
+    torch.manual_seed(1005)
+    cali = torch.randn(n_cali, 3, res, res)
+    qnn.set_quant_state(True, False)
+    with torch.no_grad():
+        qnn(cali[:8])
+    shift = [31 / 32, 33 / 32, 1.0]
+    MSM.build_ShiftedChannelQuant(qnn, [BLOCK], "", shiftTarget=shift, skipShiftLayer=[])
+    qnn.set_quant_state(False, False)
+    layer = BLOCK + ".conv1"
+    _cache(qnn, [layer], cali, 8)
+    m = qnn.model[3].conv1
+    m.use_weight_quant = True
+    q = m.weight_quantizer
+    out = {"w": t2n(m.org_weight), "b": t2n(m.org_bias), "delta": t2n(q.delta.reshape(-1)),
+           "zp": t2n(q.zero_point.reshape(-1)),
+           "cached_inp": t2n(torch.cat(m.cached_inp_features)),
+           "cached_out": t2n(torch.cat(m.cached_out_features))}
+    orig = LRF.FusedScaleLossFunction
+
+    class _P1(orig):
+        def __init__(self, *a, **k):
+            k["p"] = 1.0
+            super().__init__(*a, **k)
+
+    LRF.FusedScaleLossFunction = _P1
+    try:
+        torch.manual_seed(1005)
+        with _Spy(_P1) as spy:
+            res_loss = LRF.block_recon_fused_shiftedScale(m, iters, (0.01, 0.1), qnn, None)
+    finally:
+        LRF.FusedScaleLossFunction = orig
+    out["perms"] = np.stack([p.numpy() for p in spy.perms]).astype(np.int64)
+    out["rec_loss"] = np.array([r[0] for r in spy.rec], np.float64)
+    out["total_loss"] = np.array([r[1] for r in spy.rec], np.float64)
+    out["soft_loss"] = np.array([res_loss[0]], np.float64)
+    out["alpha"] = t2n(q.alpha)
+    out["beta0"] = t2n(q.beta)
+    # the layer variant's flags: hard targets, SOFT rounding (hard_round untouched, :207-211)
+    q.hard_round = False
+    q.hard_targets = True
+    q.shiftedDone = True
+    inp = torch.cat(m.cached_inp_features)[:32]
+    tgt = torch.cat(m.cached_out_features)[:32]
+    with torch.no_grad():
+        out["hard_loss"] = np.array([float(lp_loss(m(inp), tgt, p=1.0))], np.float64)
+        out["what_layer_hard"] = t2n(q(m.weight))
+        q.hard_round = True
+        out["what_hard"] = t2n(q(m.weight))
+    out["iters"] = np.array([iters])
+    save("recon_layer_fused", **out)
+
+
+def gen_recon_block_shift(iters=20, n_cali=16, res=16):
+    """a21: block_recon_shiftedScale (layer_recon_shiftedScale.py:12-124 +
+    ScaleLossBlockFunction :340-412), shift phase (init_v, learned_hard_sigmoid, entropy
+    regulariser) then adaround phase (update_delta, init_beta, beta) on the tiny net's
+    BasicBlock at W2."""
+    qnn = _build_tiny_qnn()
+    torch.manual_seed(1005)
+    cali = torch.randn(n_cali, 3, res, res)
+    qnn.set_quant_state(True, False)
+    with torch.no_grad():
+        qnn(cali[:8])
+    shift = [31 / 32, 33 / 32, 1.0]
+    MSM.build_ShiftedChannelQuant(qnn, [BLOCK], "", shiftTarget=shift, skipShiftLayer=[])
+    qnn.set_quant_state(False, False)
+    _cache(qnn, [BLOCK], cali, 8)
+    MSM.set_quant_state_block(qnn, [BLOCK], "", True)
+    block = qnn.model[3]
+    out = {}
+    _dump_block(out, block)
+    for n in CONVS:
+        q = getattr(block, n).weight_quantizer
+        out[n + "_delta"] = t2n(q.delta.reshape(-1))
+        out[n + "_zp"] = t2n(q.zero_point.reshape(-1))
+    out["cached_inp"] = t2n(torch.cat(block.cached_inp_features))
+    out["cached_out"] = t2n(torch.cat(block.cached_out_features))
+    torch.manual_seed(1005)
+    with _Spy(LRS.ScaleLossBlockFunction) as spy:
+        l1 = LRS.block_recon_shiftedScale(block, iters, 0.1, qnn, None)
+    out["s_perms"] = np.stack([p.numpy() for p in spy.perms]).astype(np.int64)
+    out["s_rec_loss"] = np.array([r[0] for r in spy.rec], np.float64)
+    out["s_total_loss"] = np.array([r[1] for r in spy.rec], np.float64)
+    out["s_final"] = np.array(l1, np.float64)
+    for n in CONVS:
+        m = getattr(block, n)
+        q = m.weight_quantizer
+        out[n + "_s_alpha"] = t2n(q.alpha)
+        with torch.no_grad():
+            out[n + "_s_what"] = t2n(q(m.weight))       # hard targets (lhs mode)
+    with _Spy(LRS.ScaleLossBlockFunction) as spy:
+        l2 = LRS.block_recon_shiftedScale(block, iters, 0.01, qnn, None, adaround=True)
+    out["a_perms"] = np.stack([p.numpy() for p in spy.perms]).astype(np.int64)
+    out["a_rec_loss"] = np.array([r[0] for r in spy.rec], np.float64)
+    out["a_total_loss"] = np.array([r[1] for r in spy.rec], np.float64)
+    out["a_final"] = np.array(l2, np.float64)
+    for n in CONVS:
+        m = getattr(block, n)
+        q = m.weight_quantizer
+        out[n + "_a_delta"] = t2n(q.delta)
+        out[n + "_a_beta"] = t2n(q.beta)
+        with torch.no_grad():
+            out[n + "_a_what"] = t2n(q(m.weight))       # hard rounding (adaround mode)
+    out["iters"] = np.array([iters])
+    save("recon_block_shift", **out)
+
+
+def _tiny_net2():
+    """stem -> BasicBlock(16->16) -> BasicBlock(16->32, stride 2, downsample) -> pool -> fc:
+    two reconstructable blocks, so the second block's cached input carries the first
+    block's finished (hard) quantization, as in the driver (ShiftedScaleQuant.py:236-256)."""
+    from models.resnet import BasicBlock
+    torch.manual_seed(1005)
+    ds = nn.Sequential(nn.Conv2d(16, 32, 1, stride=2, bias=False), nn.BatchNorm2d(32))
+    net = nn.Sequential(nn.Conv2d(3, 16, 3, padding=1, bias=False), nn.BatchNorm2d(16), nn.ReLU(),
+                        BasicBlock(16, 16, norm_layer=nn.BatchNorm2d),
+                        BasicBlock(16, 32, stride=2, downsample=ds, norm_layer=nn.BatchNorm2d),
+                        nn.AdaptiveAvgPool2d(1), nn.Flatten(), nn.Linear(32, 10))
+    g = torch.Generator().manual_seed(7)
+    for m in net.modules():
+        if isinstance(m, nn.Conv2d):
+            nn.init.kaiming_normal_(m.weight, mode="fan_out", nonlinearity="relu")
+        if isinstance(m, nn.BatchNorm2d):
+            m.running_mean.copy_(torch.randn(m.num_features, generator=g) * 0.1)
+            m.running_var.copy_(torch.rand(m.num_features, generator=g) + 0.5)
+            m.weight.data.copy_(torch.rand(m.num_features, generator=g) + 0.5)
+            m.bias.data.copy_(torch.randn(m.num_features, generator=g) * 0.1)
+    return net.eval()
+
+
+def _build_tiny_qnn2(bits_w=2, bits_a=4):
+    wq = {"n_bits": bits_w, "channel_wise": True, "scale_method": "max", "tune_delta_zero": False,
+          "symmetric": False}
+    aq = {"n_bits": bits_a, "channel_wise": False, "scale_method": "mse", "tune_delta_zero": False,
+          "leaf_param": True, "symmetric": False}
+    qnn = QuantModel(model=_tiny_net2(), weight_quant_params=wq, act_quant_params=aq)
+    qnn.eval()
+    qnn.set_first_last_layer_to_8bit()
+    return qnn
+
+
+def _dump_qms(out, qnn, prefix):
+    qms = [m for m in qnn.modules() if isinstance(m, QuantModule)]
+    for k, m in enumerate(qms):
+        out[f"{prefix}qm{k}_w"], out[f"{prefix}qm{k}_b"] = t2n(m.org_weight), t2n(m.org_bias)
+        out[f"{prefix}qm{k}_delta"] = t2n(m.weight_quantizer.delta.reshape(-1))
+        out[f"{prefix}qm{k}_zp"] = t2n(m.weight_quantizer.zero_point.reshape(-1))
+        out[f"{prefix}qm{k}_bits"] = np.array([m.weight_quantizer.n_bits])
+
+
+def gen_driver(iters=20, n_cali=16, res=16):
+    """a23 + (f1): the shipped fused driver flow (channelShift_wLoss,
+    ShiftedScaleQuant.py:185-286) over BOTH blocks of a two-block net, with the
+    reference's own helpers: build_ShiftedChannelQuant, per block the 'if' cache under the
+    current quant state (earlier blocks finished and weight-quantized) and the FP 'of'
+    cache, set_quant_state_block, QuantRecursiveShiftRecon -> run_ShiftReconFused ->
+    block_recon_fused_shiftedScale, clear_cached_features; then the weight-quantized
+    network's logits.  Every block's cached features are recorded (the feature-cache
+    parity of SURVEY §8(f) row 1)."""
+    ssq_mod = types.ModuleType("data.cifar10")
+    ssq_mod.build_cifar10_data = lambda *a, **k: (None, None)
+    img_mod = types.ModuleType("data.imagenet")
+    img_mod.build_imagenet_data = lambda *a, **k: (None, None)
+    sys.modules.setdefault("data", types.ModuleType("data"))
+    sys.modules["data.cifar10"], sys.modules["data.imagenet"] = ssq_mod, img_mod
+    import ShiftedScaleQuant as SSQD
+    qnn = _build_tiny_qnn2()
+    torch.manual_seed(1005)
+    cali = torch.randn(n_cali, 3, res, res)
+    qnn.set_quant_state(True, False)
+    with torch.no_grad():
+        qnn(cali[:8])
+    out = {"cali": t2n(cali)}
+    _dump_qms(out, qnn, "")
+    shift = [31 / 32, 33 / 32, 1.0]
+    layers = [".model.3", ".model.4"]
+    MSM.build_ShiftedChannelQuant(qnn, layers, "", shiftTarget=shift, skipShiftLayer=[])
+    qnn.set_quant_state(False, False)
+    loss_dic = {}
+    torch.manual_seed(1005)
+    for k, layer in enumerate(layers):
+        _cache(qnn, [layer], cali, 8)
+        block = qnn.model[3 + k]
+        out[f"b{k}_cached_inp"] = t2n(torch.cat(block.cached_inp_features))
+        out[f"b{k}_cached_out"] = t2n(torch.cat(block.cached_out_features))
+        MSM.set_quant_state_block(qnn, [layer], "", True)
+        SSQD.QuantRecursiveShiftRecon(qnn, [layer], qnn, None, "", loss_dic, iters=iters, lmda=0.1,
+                                      shiftTarget=shift)
+        qnn.clear_cached_features()
+        out[f"b{k}_losses"] = np.array(loss_dic[layer][0], np.float64)
+        names = ("conv1", "conv2") + (("downsample",) if k == 1 else ())
+        for n in names:
+            m = getattr(block, n)
+            q = m.weight_quantizer
+            out[f"b{k}_{n}_alpha"] = t2n(q.alpha)
+            out[f"b{k}_{n}_beta0"] = t2n(q.beta)
+            with torch.no_grad():
+                out[f"b{k}_{n}_what_hard"] = t2n(q(m.weight))
+    qnn.set_quant_state(True, False)
+    with torch.no_grad():
+        out["logits"] = t2n(qnn(cali))
+    out["iters"] = np.array([iters])
+    save("recon_driver", **out)
+
+
+def gen_wmse_driver(n_cali=16, res=16):
+    """a23: the shipped default path `ShiftedScaleQuant.py --test=True` ->
+    channelShift_wMSE (:119-183): UAQ weight init on cali[:64], then every QuantModule not
+    in layerDisabled (only the fc there) and not ignore_reconstruction gets a
+    ChannelQuantMSE(opt_mode='max', level, threshold) through the reference's own
+    build_ShiftedChannelQuantMSELayer, whose init_scale picks the input scales.  The walk
+    is channelShift_wMSE's nested build_ShiftedChannelQuantMSE, restated here (it is a
+    closure the reference does not export).  Recorded: each layer's inp_scale and the
+    weight-quantized network's logits (validate_with_loss's forward)."""
+    out = {}
+    for level, thr in ((1, 1.0), (8, 2.0), (64, 2.0)):
+        qnn = _build_tiny_qnn2()
+        torch.manual_seed(1005)
+        cali = torch.randn(n_cali, 3, res, res)
+        qnn.set_quant_state(True, False)
+        with torch.no_grad():
+            qnn(cali[:8])
+        tag = f"l{level}"
+        if level == 1:
+            out["cali"] = t2n(cali)
+            _dump_qms(out, qnn, "")
+        layer_disabled = [".model.7"]
+        kw = dict(shiftTarget=[31 / 32, 33 / 32, 1.0], level=level, threshold=thr, opt_mode="max")
+        built = []
+
+        def walk(model, prv_name=""):
+            from quant.quant_block import QuantBasicBlock
+            for name, module in model.named_children():
+                cur = prv_name + "." + name
+                if isinstance(module, QuantModule):
+                    if module.ignore_reconstruction is True:
+                        continue
+                    if cur not in layer_disabled:
+                        MSM.build_ShiftedChannelQuantMSELayer(model, cur, module, 1.0, **kw)
+                        built.append(cur)
+                elif isinstance(module, QuantBasicBlock):
+                    if module.ignore_reconstruction is True:
+                        continue
+                    if cur in layer_disabled:
+                        MSM.build_ShiftedChannelQuantMSEBlock(model, cur, module, 1.0, **kw)
+                    else:
+                        walk(module, cur)
+                else:
+                    walk(module, cur)
+
+        walk(qnn)
+        out[f"{tag}_names"] = np.array(built)
+        qms = [m for m in qnn.modules() if isinstance(m, QuantModule)]
+        for k, m in enumerate(qms):
+            if isinstance(m.weight_quantizer, ChannelQuantMSE):
+                out[f"{tag}_qm{k}_inp_scale"] = t2n(m.weight_quantizer.inp_scale)
+                with torch.no_grad():
+                    out[f"{tag}_qm{k}_what"] = t2n(m.weight_quantizer(m.org_weight))
+        with torch.no_grad():
+            out[f"{tag}_logits"] = t2n(qnn(cali))
+        out[f"{tag}_thr"] = np.array([thr])
+    save("driver_wmse", **out)
+
+
 if __name__ == "__main__":
     which = sys.argv[1:] or ["uaq", "channelquant", "adaround", "inpscale", "loss", "recon",
-                             "layershift", "brecq", "blocks"]
+                             "layershift", "brecq", "blocks", "act", "layerfused", "blockshift", "driver",
+                             "wmse"]
     torch.set_num_threads(4)
     if "uaq" in which:
         gen_uaq()
@@ -752,3 +1063,13 @@ if __name__ == "__main__":
         gen_recon_brecq()
     if "blocks" in which:
         gen_recon_blocks()
+    if "act" in which:
+        gen_act_quant()
+    if "layerfused" in which:
+        gen_recon_layer_fused()
+    if "blockshift" in which:
+        gen_recon_block_shift()
+    if "driver" in which:
+        gen_driver()
+    if "wmse" in which:
+        gen_wmse_driver()

@@ -796,3 +796,159 @@ def test_affine_stays_live_after_raw_device_updates(K):
         ref = torch.nn.functional.conv2d(x, w, qm.bias, 1, 1) * new + qm.beta_out
     assert not torch.equal(y0, y1)
     np.testing.assert_array_equal(host(y1).view(np.int32), host(ref).view(np.int32))
+
+
+# ------------------------------------------------------------------ round 2: a10 init_v
+@pytest.mark.parametrize("tag", CQ_TAGS)
+def test_init_v_golden(K, golden, tag):
+    """a10 ChannelQuant.init_v (channelQuant.py:201-213): alpha from the DEQUANTIZED
+    'none'-mode candidates at delta*s_i (ssq_shift_init mode 1) vs the reference's alpha,
+    through the ChannelQuant class (which also sets mode 'learned_hard_sigmoid')."""
+    from shiftedscalequantization_amd import quant as Q
+    g = golden("channelquant")
+    w, is_fc, d, z, bits = _cq(g, tag)
+    alpha, _, _ = K.shift_init(dev(w), dev(d), SHIFTS, zp=dev(z), n_bits=bits, mode=1)
+    if not is_fc and w.shape[1] == 1:
+        alpha = alpha.view(1, -1)
+    np.testing.assert_allclose(host(alpha), g[tag + "_lhs_alpha0"], rtol=1e-6, atol=1e-7)
+    uaq = Q.UniformAffineQuantizer(n_bits=bits, channel_wise=True, ch=w.shape).cuda()
+    shape = (-1, 1) if is_fc else (-1, 1, 1, 1)
+    uaq.delta = torch.nn.Parameter(dev(g[tag + "_delta"]).view(shape))
+    uaq.zero_point = torch.nn.Parameter(dev(g[tag + "_zp"]).view(shape))
+    uaq.inited = True
+    cq = Q.ChannelQuant(1.0, uaq=uaq, weight_tensor=dev(w), shiftTarget=SHIFTS, name=tag)
+    cq.init_v(dev(w))
+    assert cq.opt_mode == "learned_hard_sigmoid"
+    np.testing.assert_allclose(host(cq.alpha), g[tag + "_lhs_alpha0"], rtol=1e-6, atol=1e-7)
+    np.testing.assert_array_equal(np.stack([host(t) for t in cq.x_q]), g[tag + "_lhs_xq"])
+
+
+# ------------------------------------------------------------------ round 2: a15 ChannelQuantAct
+def test_channel_quant_act_golden(K, golden):
+    """a15 ChannelQuantAct 'none' (channelQuantAct.py:36-67) at shiftedScale 1, 33/32,
+    31/32, 1/2: bit-exact q/dq with the [0, n-1] clamp (negatives and large values in the
+    input hit both edges); torch.round has no gradient wrt x (d/dx == 0 exactly); the
+    delta / zero_point gradients of the reference's autograd within 1e-5 (reductions)."""
+    from shiftedscalequantization_amd import quant as Q
+    g = golden("act_quant")
+    x = dev(g["x"])
+    uaq = Q.UniformAffineQuantizer(n_bits=4, channel_wise=False, scale_method="mse", leaf_param=True)
+    uaq.delta = torch.nn.Parameter(dev(g["delta"]).view(()))
+    uaq.zero_point = torch.nn.Parameter(dev(g["zp"]).view(()))
+    uaq.inited = True
+    for k, s in enumerate(g["scales"]):
+        q = Q.ChannelQuantAct(uaq=uaq, shiftTarget=[1.0, 0.5])
+        q.shiftedScale = float(s)
+        xr = x.clone().requires_grad_(True)
+        uaq.delta.grad = uaq.zero_point.grad = None
+        y = q(xr)
+        np.testing.assert_array_equal(host(y), g[f"s{k}_y"], err_msg=f"scale {s}")
+        (y * dev(g[f"s{k}_gy"])).sum().backward()
+        np.testing.assert_array_equal(host(xr.grad), g[f"s{k}_gx"])
+        close(host(uaq.delta.grad).reshape(-1), g[f"s{k}_gdelta"], rtol=1e-5, atol=1e-5)
+        close(host(uaq.zero_point.grad).reshape(-1), g[f"s{k}_gzp"], rtol=1e-5, atol=1e-5)
+    hi = (2 ** 4 - 1 - float(g["zp"][0])) * float(g["delta"][0])
+    assert host(y).min() >= -float(g["zp"][0]) * float(g["delta"][0]) * 0.5 - 1e-6
+    assert host(q(x)).max() <= hi + 1e-6
+
+
+# ------------------------------------------------------------------ round 2: prepared adaShift
+PREP_SHAPES = [(8, 6, 3, 3), (64, 64, 3, 3), (96, 48, 3, 3), (128, 64, 1, 1), (33, 5, 5, 5),
+               (24, 1, 3, 3), (512, 512, 3, 3), (256, 128, 1, 1), (7, 300, 1, 1)]
+
+
+@pytest.mark.parametrize("shape", PREP_SHAPES)
+@pytest.mark.parametrize("S", [1, 2, 3, 4])
+def test_adashift_prepared_matches_recompute(K, shape, S):
+    """The prepared path (packed int8 floors + h(beta), one-launch alpha backward) gives
+    the recomputing kernels' What bit for bit (soft and hard targets, soft and hard
+    rounding) and their alpha gradients (+ fused regulariser from the device pair) to
+    1e-6; repeated backward launches are bit-identical (the reduction counters re-arm and
+    the last-workgroup sum is in chunk order whoever arrives last)."""
+    shifts = [31 / 32, 33 / 32, 1.0, 17 / 16][:S]
+    gen = torch.Generator().manual_seed(hash((shape, S)) & 0xffff)
+    w = torch.randn(shape, generator=gen) * 0.05
+    d, z, _ = R.init_scale(w.numpy(), 2, False, True, "max")
+    wd, dd, zd = w.cuda(), dev(d), dev(z)
+    alpha, beta, _ = K.shift_init(wd, dd, shifts)
+    alpha = alpha + torch.randn(alpha.shape, generator=gen).cuda() * 0.5
+    if shape[1] == 1:
+        alpha = alpha.view(1, -1)
+    gy = torch.randn(shape, generator=gen).cuda()
+    for hr in (0, 1):
+        prep = K.AdaShiftPrep(wd, beta, dd, shifts, hr)
+        assert prep.ok
+        for ht in (0, 1):
+            ref = K.adashift(alpha, beta, wd, dd, zd, shifts, 2, False, ht, hr)
+            got = K.adashift_prepared(alpha, prep, dd, zd, 2, False, ht)
+            np.testing.assert_array_equal(host(got), host(ref), err_msg=f"ht{ht} hr{hr}")
+        regp = dev([0.1, 7.5])
+        vals_ref = torch.zeros(alpha.numel() // S, device="cuda")
+        vals_got = torch.zeros_like(vals_ref)
+        a1 = alpha.clone().requires_grad_(True)
+        K.adashift(a1, beta, wd, dd, zd, shifts, 2, False, 0, hr,
+                   reg=(0.0, 0.0, vals_ref, regp)).backward(gy)
+        grads = []
+        for _ in range(3):
+            a2 = alpha.clone().requires_grad_(True)
+            K.adashift_prepared(a2, prep, dd, zd, 2, False, 0,
+                                reg=(0.0, 0.0, vals_got, regp)).backward(gy)
+            grads.append(host(a2.grad))
+        close(grads[0], host(a1.grad), rtol=1e-6, atol=1e-7)
+        close(host(vals_got), host(vals_ref), rtol=1e-6, atol=1e-7)
+        np.testing.assert_array_equal(grads[0], grads[1])
+        np.testing.assert_array_equal(grads[0], grads[2])
+        assert int(prep.counters.abs().sum().item()) == 0
+
+
+def test_adashift_prepared_overflow_falls_back(K):
+    """A floor outside int8 (an 8-bit weight with a tiny delta) marks the preparation
+    unusable; ChannelQuant then keeps the recomputing kernels with identical results."""
+    from shiftedscalequantization_amd import quant as Q
+    w = torch.randn(16, 8, 3, 3).cuda() * 0.05
+    d = torch.full((16, 1, 1, 1), 1e-4, device="cuda")
+    beta = torch.zeros_like(w)
+    prep = K.AdaShiftPrep(w, beta, d, SHIFTS, 0)
+    assert not prep.ok
+    uaq = Q.UniformAffineQuantizer(n_bits=8, channel_wise=True, ch=w.shape).cuda()
+    uaq.delta = torch.nn.Parameter(d.clone())
+    uaq.zero_point = torch.nn.Parameter(torch.full_like(d, 128.0))
+    uaq.inited = True
+    cq = Q.ChannelQuant(1.0, uaq=uaq, weight_tensor=w, shiftTarget=SHIFTS)
+    cq.init_v_beta(w)
+    cq.opt_mode = "adaShift"
+    cq.beta.requires_grad_(False)
+    y = cq(w)
+    assert cq._prep is not None and cq._prep[1] is None
+    ref = K.adashift(cq.alpha, cq.beta, w, cq.delta, cq.zero_point, SHIFTS, 8, False, 0, 0)
+    np.testing.assert_array_equal(host(y), host(ref))
+
+
+# ------------------------------------------------------------------ round 2: finalisation
+@pytest.mark.parametrize("fixture", ["recon_fused", "recon_driver"])
+def test_hard_weights_from_reference_alpha_bit_exact(K, golden, fixture):
+    """a25: given the reference's FINAL alpha and beta, the finished quantizer (hard
+    targets, hard rounding) reproduces the reference's hard What bit for bit, through the
+    prepared kernel, the recomputing kernel and the export path's integer codes
+    ((code - zp) * delta == What exactly)."""
+    g = golden(fixture)
+    if fixture == "recon_fused":
+        items = [(n, g[n + "_w"], g[n + "_delta"], g[n + "_zp"], g[n + "_alpha"], g[n + "_beta0"],
+                  g[n + "_what_hard"]) for n in ("conv1", "conv2", "downsample")]
+    else:
+        items = []
+        qm = {1: ("b0", "conv1"), 2: ("b0", "conv2"), 3: ("b1", "conv1"), 4: ("b1", "conv2"),
+              5: ("b1", "downsample")}
+        for k, (b, n) in qm.items():
+            items.append((f"{b}.{n}", g[f"qm{k}_w"], g[f"qm{k}_delta"], g[f"qm{k}_zp"],
+                          g[f"{b}_{n}_alpha"], g[f"{b}_{n}_beta0"], g[f"{b}_{n}_what_hard"]))
+    for name, w, d, z, alpha, beta, what in items:
+        d4, z4 = dev(d).view(-1, 1, 1, 1), dev(z).view(-1, 1, 1, 1)
+        y = K.adashift(dev(alpha), dev(beta), dev(w), d4, z4, SHIFTS, 2, False, 1, 1)
+        np.testing.assert_array_equal(host(y), what, err_msg=name)
+        prep = K.AdaShiftPrep(dev(w), dev(beta), d4, SHIFTS, 1)
+        yp = K.adashift_prepared(dev(alpha), prep, d4, z4, 2, False, 1)
+        np.testing.assert_array_equal(host(yp), what, err_msg=name)
+        y2, codes = K.adashift_codes(dev(alpha), dev(beta), dev(w), d4, z4, SHIFTS, 2, False)
+        c = codes.cpu().numpy().astype(np.float32)
+        np.testing.assert_array_equal((c - z.reshape(-1, 1, 1, 1)) * d.reshape(-1, 1, 1, 1), what)
