@@ -159,18 +159,18 @@ int ssq_adashift_bwd(const float* gWhat, const float* W, const float* alpha,
                      float reg_b, const float* reg_dev, float* galpha, float* gbeta,
                      float* reg_vals, void* ws, size_t ws_bytes, ssq_stream_t stream);
 
-/* Prepared adaShift (conv weights, S <= 4).  In the fused loop W, delta, the shifts and
- * beta are frozen (layer_recon_fused_shiftedScale.py:59-66) and the reference computes its
- * floor candidates x_q once (channelQuant.py:284-286).  ssq_adashift_prepare does that
+/* Prepared adaShift (conv weights, S <= 4, K <= 256).  In the fused loop W, delta, the shifts
+ * and beta are frozen (layer_recon_fused_shiftedScale.py:59-66) and the reference computes
+ * its floor candidates x_q once (channelQuant.py:284-286).  ssq_adashift_prepare does that
  * once: fpack[e] = the S floors floor(W/(delta*s_i)) as int8 bytes (byte i) of one 32-bit
  * word, hterm[e] = h(beta) (hard_round: [beta >= 0]).  *overflow (device int, zeroed by the
  * caller) becomes nonzero if a floor does not fit int8 -- the caller then keeps
  * ssq_adashift_fwd/bwd.  The prepared forward / backward give the same What and alpha
- * gradients as ssq_adashift_fwd / ssq_adashift_bwd (beta frozen: no gbeta) while
- * streaming 12 B per weight each.  The backward is one launch: `counters` (int64 count =
- * ssq_adashift_bwd_prepared_counters(), zero-initialised ONCE by the caller, left zeroed
- * by every launch) lets the last workgroup of each column block finish the reduction in
- * a fixed order.  galpha OVERWRITTEN; regulariser as ssq_adashift_bwd.                 */
+ * gradients as ssq_adashift_fwd / ssq_adashift_bwd (beta frozen: no gbeta) while streaming
+ * 12 B per weight each.  The _multi forms take nseg weights (e.g. every conv of a block,
+ * same S) in ONE forward launch and TWO backward launches; arrays are indexed by segment.
+ * The backward reduces over (Co, K) in two fixed-order stages through `ws`; galpha
+ * OVERWRITTEN; regulariser as ssq_adashift_bwd (reg_vals may be NULL, or entries NULL). */
 int ssq_adashift_prepare(const float* W, const float* beta, const float* delta,
                          const float* shifts, int S, int64_t Co, int64_t Ci, int64_t K,
                          int hard_round, uint32_t* fpack, float* hterm, int* overflow,
@@ -178,15 +178,30 @@ int ssq_adashift_prepare(const float* W, const float* beta, const float* delta,
 int ssq_adashift_fwd_prepared(const uint32_t* fpack, const float* hterm, const float* alpha,
                               const float* delta, const float* zp, int S, int64_t Co,
                               int64_t Ci, int64_t K, int hard_targets, int qmin, int qmax,
-                              float* What, void* codes_or_null, ssq_stream_t stream);
+                              float* What, ssq_stream_t stream);
+int ssq_adashift_fwd_prepared_multi(int nseg, const uint32_t* const* fpack,
+                                    const float* const* hterm, const float* const* alpha,
+                                    const float* const* delta, const float* const* zp,
+                                    const int64_t* Co, const int64_t* Ci, const int64_t* K,
+                                    const int* qmin, const int* qmax, int S, int hard_targets,
+                                    float* const* What, ssq_stream_t stream);
 size_t ssq_adashift_bwd_prepared_workspace_size(int64_t Co, int64_t Ci, int64_t K, int S);
-int64_t ssq_adashift_bwd_prepared_counters(int64_t Co, int64_t Ci, int64_t K);
 int ssq_adashift_bwd_prepared(const float* gWhat, const uint32_t* fpack, const float* hterm,
                               const float* alpha, const float* delta, const float* zp, int S,
                               int64_t Co, int64_t Ci, int64_t K, int qmin, int qmax,
                               float reg_lambda, float reg_b, const float* reg_dev,
-                              float* galpha, float* reg_vals, unsigned* counters, void* ws,
-                              size_t ws_bytes, ssq_stream_t stream);
+                              float* galpha, float* reg_vals, void* ws, size_t ws_bytes,
+                              ssq_stream_t stream);
+size_t ssq_adashift_bwd_prepared_multi_workspace_size(int nseg, const int64_t* Co,
+                                                      const int64_t* Ci, const int64_t* K, int S);
+int ssq_adashift_bwd_prepared_multi(int nseg, const float* const* gWhat,
+                                    const uint32_t* const* fpack, const float* const* hterm,
+                                    const float* const* alpha, const float* const* delta,
+                                    const float* const* zp, const int64_t* Co, const int64_t* Ci,
+                                    const int64_t* K, const int* qmin, const int* qmax, int S,
+                                    float reg_lambda, float reg_b, const float* reg_dev,
+                                    float* const* galpha, float* const* reg_vals, void* ws,
+                                    size_t ws_bytes, ssq_stream_t stream);
 
 /* Shift-regulariser alone (value + gradient wrt alpha), for iterations where the
  * reconstruction gradient is not wanted.  mode 0: lambda*sum(1-|2p-1|^b)

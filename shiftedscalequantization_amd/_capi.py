@@ -43,11 +43,14 @@ SIGNATURES = {
     "ssq_adashift_bwd_workspace_size": (_sz, [_i64, _i64, _i64, _i, _i]),
     "ssq_adashift_prepare": (_i, [_p, _p, _p, _p, _i, _i64, _i64, _i64, _i, _p, _p, _p, _p]),
     "ssq_adashift_fwd_prepared": (_i, [_p, _p, _p, _p, _p, _i, _i64, _i64, _i64, _i, _i, _i, _p,
-                                       _p, _p]),
+                                       _p]),
+    "ssq_adashift_fwd_prepared_multi": (_i, [_i] + [_p] * 10 + [_i, _i, _p, _p]),
     "ssq_adashift_bwd_prepared_workspace_size": (_sz, [_i64, _i64, _i64, _i]),
-    "ssq_adashift_bwd_prepared_counters": (_i64, [_i64, _i64, _i64]),
     "ssq_adashift_bwd_prepared": (_i, [_p, _p, _p, _p, _p, _p, _i, _i64, _i64, _i64, _i, _i, _f,
-                                       _f, _p, _p, _p, _p, _p, _sz, _p]),
+                                       _f, _p, _p, _p, _p, _sz, _p]),
+    "ssq_adashift_bwd_prepared_multi_workspace_size": (_sz, [_i, _p, _p, _p, _i]),
+    "ssq_adashift_bwd_prepared_multi": (_i, [_i] + [_p] * 11 + [_i, _f, _f, _p, _p, _p, _p, _sz,
+                                                                 _p]),
     "ssq_adashift_bwd": (_i, [_p, _p, _p, _p, _p, _p, _p, _i, _i64, _i64, _i64, _i, _i, _i, _i,
                               _f, _f, _p, _p, _p, _p, _p, _sz, _p]),
     "ssq_shift_reg": (_i, [_p, _i, _i64, _i, _f, _f, _p, _p, _p]),

@@ -8,47 +8,9 @@
 // Conv kernels are column-tiled (see "column-tiled conv kernels"): the softmax of an
 // input channel's alpha row is computed once per thread, rows are coalesced sweeps, and
 // the alpha-gradient reductions over (Co, K) are two fixed-order stages (deterministic).
-#include "ssq_common.h"
+#include "adashift_common.h"
 
 namespace ssq {
-
-constexpr int kMaxS = 8;
-
-struct Shifts {
-  float s[kMaxS];
-  int n;
-};
-
-struct Geo {
-  uint32_t Co, Ci, K, CiK;
-  int is_fc;
-};
-
-__device__ __forceinline__ void decompose(uint32_t e, const Geo& g, uint32_t& co, uint32_t& ci) {
-  co = e / g.CiK;
-  ci = (e - co * g.CiK) / g.K;
-}
-
-__device__ __forceinline__ uint32_t alpha_row(const Geo& g, uint32_t co, uint32_t ci) {
-  return g.is_fc ? co * g.Ci + ci : ci;
-}
-
-__device__ __forceinline__ void load_row(const float* __restrict__ a, uint32_t row, int S,
-                                         float* out) {
-  for (int i = 0; i < S; ++i) out[i] = a[(size_t)row * S + i];
-}
-
-// soft shifted floor  sum_i F_i * p_i  (x_out = x_q0*p0; x_out += x_q1*p1; ...)
-__device__ __forceinline__ float soft_floor(float w, float d, const Shifts& sh, int S,
-                                            const float* p, float* F) {
-  float acc = 0.0f;
-  for (int i = 0; i < S; ++i) {
-    F[i] = floorf(w / __fmul_rn(d, sh.s[i]));
-    const float t = __fmul_rn(F[i], p[i]);
-    acc = i == 0 ? t : __fadd_rn(acc, t);
-  }
-  return acc;
-}
 
 // ------------------------------------------------------------------ adaShift forward
 __global__ __launch_bounds__(kBlock) void adashift_fwd_kernel(
@@ -77,63 +39,6 @@ __global__ __launch_bounds__(kBlock) void adashift_fwd_kernel(
     What[e] = __fmul_rn(__fsub_rn(q, z), __fmul_rn(d, 1.0f));
     if (codes) codes[e] = (uint8_t)((int)q & 0xff);
   }
-}
-
-// ------------------------------------------------------------------ shared stage-2 helper
-// Backward through p = clamp(softmax(a)*c + gamma, 0, 1), plus the optional shift
-// regulariser lambda*sum(1-|2p-1|^b) (value returned, gradient folded into g_p).
-// One shift's regulariser term and its gradient wrt p_i, in fp32 like the reference's
-// tensor ops (pow / log and their autograd): mode 0 = lambda * (1 - |2p-1|^b) (without
-// lambda in the value), mode 1 = entropy -p log(p + 1e-10).
-__device__ __forceinline__ void reg_term(float p, float reg_lambda, float reg_b, int reg_mode,
-                                         double& val, double& grad) {
-  if (reg_mode == 0) {  // lambda * sum(1 - ((p - 0.5).abs() * 2).pow(b))
-    const float r = __fmul_rn(fabsf(__fsub_rn(p, 0.5f)), 2.0f);
-    val = (double)__fsub_rn(1.0f, powf(r, reg_b));
-    grad = 0.0;
-    if (reg_b != 0.0f) {
-      const float sg = p > 0.5f ? 1.0f : (p < 0.5f ? -1.0f : 0.0f);
-      const float gr = __fmul_rn(__fmul_rn(-reg_lambda, reg_b), powf(r, __fsub_rn(reg_b, 1.0f)));
-      grad = (double)__fmul_rn(__fmul_rn(gr, 2.0f), sg);
-    }
-  } else {
-    const float lg = logf(__fadd_rn(p, 1e-10f));
-    val = -(double)__fmul_rn(p, lg);
-    grad = (double)(-reg_lambda * __fadd_rn(lg, p / __fadd_rn(p, 1e-10f)));
-  }
-}
-
-// Backward through p = clamp(softmax(a)*c + gamma, 0, 1) given d/dp in g_p (double).
-__device__ __forceinline__ void softmax_clamp_bwd(const float* s, int S, const double* g_p,
-                                                  float* ga_out) {
-  double gs[kMaxS], dot = 0.0;
-  for (int i = 0; i < S; ++i) {
-    const float u = __fadd_rn(__fmul_rn(s[i], kZmG), kGamma);
-    gs[i] = (u >= 0.0f && u <= 1.0f) ? g_p[i] * (double)kZmG : 0.0;
-    dot += gs[i] * (double)s[i];
-  }
-  for (int i = 0; i < S; ++i) ga_out[i] = (float)((double)s[i] * (gs[i] - dot));
-}
-
-// g_p += regulariser gradient; returns the regulariser value (summed in double, fixed
-// order); then the softmax/clamp backward into ga_out.
-__device__ __forceinline__ float alpha_chain(const float* a, int S, double* g_p, float reg_lambda,
-                                             float reg_b, int reg_mode, float* ga_out) {
-  float s[kMaxS], p[kMaxS];
-  soft_targets<kMaxS>(a, S, s, p);
-  float reg = 0.0f;
-  if (reg_lambda != 0.0f) {
-    double acc = 0.0;
-    for (int i = 0; i < S; ++i) {
-      double v, gr;
-      reg_term(p[i], reg_lambda, reg_b, reg_mode, v, gr);
-      acc += v;
-      g_p[i] += gr;
-    }
-    reg = (float)((double)reg_lambda * acc);
-  }
-  softmax_clamp_bwd(s, S, g_p, ga_out);
-  return reg;
 }
 
 // ------------------------------------------------------------------ adaShift backward
@@ -425,79 +330,9 @@ __global__ void reduce_partials(const double* __restrict__ part, int nblk, doubl
   if (threadIdx.x == 0) out[0] = (float)(a * scale);
 }
 
-// ------------------------------------------------------------------ host helpers
-static int make_geo(int64_t Co, int64_t Ci, int64_t K, int is_fc, Geo& g) {
-  SSQ_REQUIRE(Co >= 1 && Ci >= 1 && K >= 1, SSQ_E_ARG, "bad geometry (%lld,%lld,%lld)",
-              (long long)Co, (long long)Ci, (long long)K);
-  SSQ_REQUIRE(Co * Ci * K < (1ll << 31), SSQ_E_ARG, "weight too large for 32-bit indexing");
-  SSQ_REQUIRE(!is_fc || K == 1, SSQ_E_ARG, "Linear weights must have K == 1");
-  g.Co = (uint32_t)Co;
-  g.Ci = (uint32_t)Ci;
-  g.K = (uint32_t)K;
-  g.CiK = (uint32_t)(Ci * K);
-  g.is_fc = is_fc;
-  return SSQ_OK;
-}
-
-static int make_shifts(const float* shifts, int S, Shifts& sh) {
-  SSQ_REQUIRE(S >= 1 && S <= kMaxS && shifts, SSQ_E_ARG, "1 <= S <= %d shifts required", kMaxS);
-  sh.n = S;
-  for (int i = 0; i < kMaxS; ++i) sh.s[i] = i < S ? shifts[i] : 1.0f;
-  return SSQ_OK;
-}
-
 }  // namespace ssq
 
 using namespace ssq;
-
-#define SSQ_GEO(Co, Ci, K, fc, g)                      \
-  Geo g;                                               \
-  {                                                    \
-    int _r = make_geo(Co, Ci, K, fc, g);               \
-    if (_r) return _r;                                 \
-  }
-#define SSQ_SHIFTS(p, S, sh)                           \
-  Shifts sh;                                           \
-  {                                                    \
-    int _r = make_shifts(p, S, sh);                    \
-    if (_r) return _r;                                 \
-  }
-
-// ------------------------------------------------------------------ column-tiled conv kernels
-// A conv weight (Co, Ci, K) is tiled as [chunk of R output channels] x [column block of
-// ncb whole input channels = ncb*K contiguous columns].  Thread t owns column
-// j = ci0*K + t of every row of the chunk, so its input channel ci = ci0 + t/K is fixed:
-// the softmax p(alpha[ci]) is computed once per thread (not once per element), and each
-// row is one coalesced sweep of ncb*K contiguous floats.  delta/zp are per row (wave
-// uniform).  The alpha reductions write one fixed-order partial per (chunk, ci) and a
-// second launch sums the chunks with one wave per input channel (fixed shuffle tree):
-// deterministic, no atomics.
-struct ColTiling {
-  uint32_t ncb, ncolblk, R, nchunk, threads;
-};
-constexpr uint32_t kMaxChunks = 256;  // stage 2: lane c sums chunks c, c+64, ... in order
-
-// max_chunks: kMaxChunks for the reductions (stage 2 has one lane per chunk); the
-// forward has no second stage and takes as many row chunks as keep ~8 workgroups per CU
-// (down to 4 rows = one load batch per thread: its time is load latency, not bandwidth).
-static ColTiling col_tiling(const Geo& g, uint32_t max_chunks = kMaxChunks) {
-  ColTiling t;
-  t.ncb = g.K >= (uint32_t)kBlock ? 1u : (uint32_t)kBlock / g.K;
-  if (t.ncb > g.Ci) t.ncb = g.Ci;
-  t.ncolblk = (g.Ci + t.ncb - 1) / t.ncb;
-  t.threads = (t.ncb * g.K + kWave - 1) / kWave * kWave;
-  uint32_t want = 2048 / t.ncolblk;  // ~8 workgroups per CU
-  if (want < 1) want = 1;
-  if (want > max_chunks) want = max_chunks;
-  if (want > g.Co) want = g.Co;
-  t.R = (g.Co + want - 1) / want;
-  t.nchunk = (g.Co + t.R - 1) / t.R;
-  return t;
-}
-static size_t col_ws_bytes(const Geo& g, int S) {
-  const ColTiling t = col_tiling(g);
-  return (size_t)t.nchunk * g.Ci * S * sizeof(double);
-}
 
 // Rows are processed RB at a time with every load of the batch issued before any math
 // (the row stride is Ci*K floats, so each load is its own cache line: latency, not
@@ -979,321 +814,4 @@ extern "C" int ssq_round_reg(const float* v, int64_t n, float lambda, float b, f
   hipLaunchKernelGGL(reduce_partials, dim3(1), dim3(kBlock), 0, s, (const double*)ws, grid,
                      (double)lambda, loss_out);
   return check_launch("ssq_round_reg");
-}
-
-// ------------------------------------------------------------------ prepared adaShift (K5p/K6p)
-// In the fused loop (layer_recon_fused_shiftedScale.py:59-66) W, delta, the shift
-// candidates and beta are frozen: only alpha learns.  The reference therefore computes its
-// floors x_q ONCE (channelQuant.py:284-286) and each iteration only re-mixes them.  The
-// prepared path does the same: ssq_adashift_prepare evaluates, once, every floor
-// F_i = floor(W / (delta*s_i)) with the very fp32 ops the recomputing kernels use, packed as
-// int8 bytes into one 32-bit word per weight (S <= 4), and the rounding term
-// h(beta) (or [beta >= 0]) as fp32.  The per-iteration kernels then stream
-// fpack + hterm (+ gWhat) with no divide and no exp per element -- 12 B/elem forward
-// (fpack, hterm in; What out) and 12 B/elem backward (gWhat, fpack, hterm in), the §8(d)
-// algorithmic bytes -- and produce bit-identical What / identical gradients.  The alpha
-// backward reduction is ONE launch: each workgroup writes its fixed-order partials, the
-// last workgroup of a column block (agent-scope counter) sums that block's partials over
-// the row chunks in chunk order (deterministic whichever workgroup is last) and applies the
-// softmax/clamp chain + shift regulariser, then re-arms the counter for the next launch.
-constexpr int kMaxPrepS = 4;
-constexpr int kRBP = 8;            // rows per load batch in the prepared kernels
-
-__global__ __launch_bounds__(kBlock) void adashift_prepare_kernel(
-    const float* __restrict__ W, const float* __restrict__ beta, const float* __restrict__ delta,
-    Shifts sh, Geo g, uint32_t n, int hard_r, uint32_t* __restrict__ fpack,
-    float* __restrict__ hterm, int* __restrict__ overflow) {
-  const uint32_t stride = gridDim.x * blockDim.x;
-  int bad = 0;
-  for (uint32_t e = blockIdx.x * blockDim.x + threadIdx.x; e < n; e += stride) {
-    const uint32_t co = e / g.CiK;
-    const float w = W[e], d = delta[co];
-    uint32_t word = 0;
-    for (int i = 0; i < sh.n; ++i) {
-      const float F = floorf(w / __fmul_rn(d, sh.s[i]));   // = soft_floor's candidate
-      bad |= !(F >= -128.0f && F <= 127.0f);
-      const int fi = F >= -128.0f && F <= 127.0f ? (int)F : 0;
-      word |= ((uint32_t)(fi & 0xff)) << (8 * i);
-    }
-    fpack[e] = word;
-    const float b = beta[e];
-    hterm[e] = hard_r ? (b >= 0.0f ? 1.0f : 0.0f) : rect_sigmoid(b);
-  }
-  if (bad) atomicOr(overflow, 1);
-}
-
-__device__ __forceinline__ float unpack_floor(uint32_t word, int i) {
-  return (float)(int8_t)(uint8_t)(word >> (8 * i));
-}
-
-// Column tiling of the prepared kernels: whole input channels per workgroup (as
-// col_tiling), row chunks of >= 8 rows so each thread keeps 2-3 x 8 loads in flight and the
-// partials stay small (nchunk x Ci x S doubles), ~1536 workgroups at most.
-static ColTiling col_tiling_prep(const Geo& g) {
-  ColTiling t;
-  t.ncb = g.K >= (uint32_t)kBlock ? 1u : (uint32_t)kBlock / g.K;
-  if (t.ncb > g.Ci) t.ncb = g.Ci;
-  t.ncolblk = (g.Ci + t.ncb - 1) / t.ncb;
-  t.threads = (t.ncb * g.K + kWave - 1) / kWave * kWave;
-  uint32_t want = 1536 / t.ncolblk;
-  const uint32_t by_rows = (g.Co + kRBP - 1) / kRBP;
-  if (want > by_rows) want = by_rows;
-  if (want > kMaxChunks) want = kMaxChunks;
-  if (want < 1) want = 1;
-  t.R = (g.Co + want - 1) / want;
-  t.nchunk = (g.Co + t.R - 1) / t.R;
-  return t;
-}
-
-template <int NS, int HARD_T>
-__global__ __launch_bounds__(1024) void shift_fwd_prep(
-    const uint32_t* __restrict__ fpack, const float* __restrict__ hterm,
-    const float* __restrict__ alpha, const float* __restrict__ delta, const float* __restrict__ zp,
-    Geo g, ColTiling tl, float lo, float hi, float* __restrict__ What,
-    uint8_t* __restrict__ codes) {
-  const uint32_t ci0 = blockIdx.x * tl.ncb;
-  const uint32_t nci = min(tl.ncb, g.Ci - ci0);
-  const uint32_t t = threadIdx.x;
-  if (t >= nci * g.K) return;
-  const uint32_t ci = ci0 + t / g.K, j = ci0 * g.K + t;
-  float a[kMaxS], p[kMaxS];
-  load_row(alpha, ci, NS, a);
-  soft_targets<kMaxS>(a, NS, nullptr, p);
-  const int sel = argmax_first(p, NS);
-  const uint32_t co0 = blockIdx.y * tl.R, co1 = min(co0 + tl.R, g.Co);
-  auto one = [&](uint32_t co, uint32_t fw, float h, float d, float z) {
-    float xf;
-    if (HARD_T) {
-      xf = unpack_floor(fw, sel);
-    } else {
-      xf = __fmul_rn(unpack_floor(fw, 0), p[0]);
-#pragma unroll
-      for (int i = 1; i < NS; ++i) xf = __fadd_rn(xf, __fmul_rn(unpack_floor(fw, i), p[i]));
-    }
-    const float q = clampf(__fadd_rn(__fadd_rn(xf, h), z), lo, hi);
-    const uint32_t e = co * g.CiK + j;
-    What[e] = __fmul_rn(__fsub_rn(q, z), __fmul_rn(d, 1.0f));
-    if (codes) codes[e] = (uint8_t)((int)q & 0xff);
-  };
-  uint32_t co = co0;
-  for (; co + kRBP <= co1; co += kRBP) {
-    uint32_t fw[kRBP];
-    float h[kRBP], d[kRBP], z[kRBP];
-#pragma unroll
-    for (int r = 0; r < kRBP; ++r) {
-      const uint32_t e = (co + r) * g.CiK + j;
-      fw[r] = fpack[e];
-      h[r] = hterm[e];
-      d[r] = delta[co + r];
-      z[r] = zp[co + r];
-    }
-#pragma unroll
-    for (int r = 0; r < kRBP; ++r) one(co + r, fw[r], h[r], d[r], z[r]);
-  }
-  for (; co < co1; ++co) {
-    const uint32_t e = co * g.CiK + j;
-    one(co, fpack[e], hterm[e], delta[co], zp[co]);
-  }
-}
-
-// Backward: stage-1 sums of g_int * F_i per (chunk, ci) into part[(ci*nchunk + chunk)*S + i],
-// then the last-arriving workgroup of the column block finishes its input channels.
-template <int NS>
-__global__ __launch_bounds__(1024) void alpha_bwd_prep(
-    const float* __restrict__ gWhat, const uint32_t* __restrict__ fpack,
-    const float* __restrict__ hterm, const float* __restrict__ alpha,
-    const float* __restrict__ delta, const float* __restrict__ zp, Geo g, ColTiling tl, float lo,
-    float hi, float reg_lambda, float reg_b, const float* __restrict__ reg_dev,
-    double* __restrict__ part, unsigned* __restrict__ counters, float* __restrict__ galpha,
-    float* __restrict__ reg_vals) {
-  extern __shared__ double red[];  // [threads][S]
-  __shared__ int is_last;
-  const uint32_t ci0 = blockIdx.x * tl.ncb;
-  const uint32_t nci = min(tl.ncb, g.Ci - ci0);
-  const uint32_t t = threadIdx.x;
-  double acc[NS];
-#pragma unroll
-  for (int i = 0; i < NS; ++i) acc[i] = 0.0;
-  if (t < nci * g.K) {
-    const uint32_t ci = ci0 + t / g.K, j = ci0 * g.K + t;
-    float a[kMaxS], p[kMaxS];
-    load_row(alpha, ci, NS, a);
-    soft_targets<kMaxS>(a, NS, nullptr, p);
-    auto one = [&](uint32_t fw, float h, float d, float z, float gy) {
-      float F[NS];
-#pragma unroll
-      for (int i = 0; i < NS; ++i) F[i] = unpack_floor(fw, i);
-      float xf = __fmul_rn(F[0], p[0]);
-#pragma unroll
-      for (int i = 1; i < NS; ++i) xf = __fadd_rn(xf, __fmul_rn(F[i], p[i]));
-      const float u = __fadd_rn(__fadd_rn(xf, h), z);
-      const float gi = (u >= lo && u <= hi) ? __fmul_rn(gy, __fmul_rn(d, 1.0f)) : 0.0f;
-#pragma unroll
-      for (int i = 0; i < NS; ++i) acc[i] += (double)gi * (double)F[i];
-    };
-    const uint32_t co0 = blockIdx.y * tl.R, co1 = min(co0 + tl.R, g.Co);
-    uint32_t co = co0;
-    for (; co + kRBP <= co1; co += kRBP) {
-      uint32_t fw[kRBP];
-      float h[kRBP], d[kRBP], z[kRBP], gy[kRBP];
-#pragma unroll
-      for (int r = 0; r < kRBP; ++r) {
-        const uint32_t e = (co + r) * g.CiK + j;
-        fw[r] = fpack[e];
-        h[r] = hterm[e];
-        gy[r] = gWhat[e];
-        d[r] = delta[co + r];
-        z[r] = zp[co + r];
-      }
-#pragma unroll
-      for (int r = 0; r < kRBP; ++r) one(fw[r], h[r], d[r], z[r], gy[r]);
-    }
-    for (; co < co1; ++co) {
-      const uint32_t e = co * g.CiK + j;
-      one(fpack[e], hterm[e], delta[co], zp[co], gWhat[e]);
-    }
-  }
-#pragma unroll
-  for (int i = 0; i < NS; ++i) red[t * NS + i] = acc[i];
-  __syncthreads();
-  if (t < nci) {
-#pragma unroll
-    for (int i = 0; i < NS; ++i) {
-      double sum = 0.0;
-      for (uint32_t k = 0; k < g.K; ++k) sum += red[(t * g.K + k) * NS + i];
-      part[((size_t)(ci0 + t) * tl.nchunk + blockIdx.y) * NS + i] = sum;
-    }
-  }
-  if (tl.nchunk > 1) {
-    // release this workgroup's partials, then count it in; the last one acquires them all
-    __threadfence();
-    __syncthreads();
-    if (t == 0) {
-      const unsigned prev = atomicAdd(&counters[blockIdx.x], 1u);
-      is_last = prev == tl.nchunk - 1;
-    }
-    __syncthreads();
-    if (!is_last) return;
-    __threadfence();
-  }
-  if (t < nci) {
-    const uint32_t ci = ci0 + t;
-    if (reg_dev) {
-      reg_lambda = reg_dev[0];
-      reg_b = reg_dev[1];
-    }
-    double tot[kMaxS];
-    const double* pp = part + (size_t)ci * tl.nchunk * NS;
-#pragma unroll
-    for (int i = 0; i < NS; ++i) tot[i] = 0.0;
-    for (uint32_t c = 0; c < tl.nchunk; ++c) {
-#pragma unroll
-      for (int i = 0; i < NS; ++i) tot[i] += __builtin_nontemporal_load(pp + (size_t)c * NS + i);
-    }
-    float a[kMaxS], ga[kMaxS];
-    load_row(alpha, ci, NS, a);
-    const float reg = alpha_chain(a, NS, tot, reg_lambda, reg_b, 0, ga);
-#pragma unroll
-    for (int i = 0; i < NS; ++i) galpha[(size_t)ci * NS + i] = ga[i];
-    if (reg_vals) reg_vals[ci] = reg;
-  }
-  if (t == 0 && tl.nchunk > 1) counters[blockIdx.x] = 0u;  // re-armed for the next launch
-}
-
-extern "C" int ssq_adashift_prepare(const float* W, const float* beta, const float* delta,
-                                    const float* shifts, int S, int64_t Co, int64_t Ci, int64_t K,
-                                    int hard_round, uint32_t* fpack, float* hterm, int* overflow,
-                                    ssq_stream_t stream) {
-  SSQ_GEO(Co, Ci, K, 0, g);
-  SSQ_SHIFTS(shifts, S, sh);
-  SSQ_REQUIRE(S <= kMaxPrepS, SSQ_E_ARG, "ssq_adashift_prepare: S <= %d", kMaxPrepS);
-  SSQ_REQUIRE(W && beta && delta && fpack && hterm && overflow, SSQ_E_ARG,
-              "ssq_adashift_prepare: null");
-  const uint32_t n = g.Co * g.CiK;
-  hipLaunchKernelGGL(adashift_prepare_kernel, dim3(grid_for(n, kBlock)), dim3(kBlock), 0,
-                     (hipStream_t)stream, W, beta, delta, sh, g, n, hard_round, fpack, hterm,
-                     overflow);
-  return check_launch("ssq_adashift_prepare");
-}
-
-extern "C" int ssq_adashift_fwd_prepared(const uint32_t* fpack, const float* hterm,
-                                         const float* alpha, const float* delta, const float* zp,
-                                         int S, int64_t Co, int64_t Ci, int64_t K, int hard_targets,
-                                         int qmin, int qmax, float* What, void* codes,
-                                         ssq_stream_t stream) {
-  SSQ_GEO(Co, Ci, K, 0, g);
-  SSQ_REQUIRE(S >= 1 && S <= kMaxPrepS, SSQ_E_ARG, "ssq_adashift_fwd_prepared: 1 <= S <= %d",
-              kMaxPrepS);
-  SSQ_REQUIRE(fpack && hterm && alpha && delta && zp && What, SSQ_E_ARG,
-              "ssq_adashift_fwd_prepared: null");
-  const ColTiling tl = col_tiling_prep(g);
-  SSQ_REQUIRE(tl.threads <= 1024, SSQ_E_ARG, "ssq_adashift_fwd_prepared: K > 1024");
-  hipStream_t s = (hipStream_t)stream;
-  const float lo = (float)qmin, hi = (float)qmax;
-#define SSQ_FWDP(NS)                                                                            \
-  do {                                                                                          \
-    if (hard_targets)                                                                           \
-      hipLaunchKernelGGL((shift_fwd_prep<NS, 1>), dim3(tl.ncolblk, tl.nchunk), dim3(tl.threads), \
-                         0, s, fpack, hterm, alpha, delta, zp, g, tl, lo, hi, What,             \
-                         (uint8_t*)codes);                                                      \
-    else                                                                                        \
-      hipLaunchKernelGGL((shift_fwd_prep<NS, 0>), dim3(tl.ncolblk, tl.nchunk), dim3(tl.threads), \
-                         0, s, fpack, hterm, alpha, delta, zp, g, tl, lo, hi, What,             \
-                         (uint8_t*)codes);                                                      \
-  } while (0)
-  switch (S) {
-    case 1: SSQ_FWDP(1); break;
-    case 2: SSQ_FWDP(2); break;
-    case 3: SSQ_FWDP(3); break;
-    default: SSQ_FWDP(4); break;
-  }
-#undef SSQ_FWDP
-  return check_launch("ssq_adashift_fwd_prepared");
-}
-
-extern "C" size_t ssq_adashift_bwd_prepared_workspace_size(int64_t Co, int64_t Ci, int64_t K,
-                                                           int S) {
-  Geo g;
-  if (S < 1 || S > kMaxPrepS || make_geo(Co, Ci, K, 0, g) != SSQ_OK) return 0;
-  const ColTiling t = col_tiling_prep(g);
-  return (size_t)t.nchunk * g.Ci * S * sizeof(double);
-}
-
-extern "C" int64_t ssq_adashift_bwd_prepared_counters(int64_t Co, int64_t Ci, int64_t K) {
-  Geo g;
-  if (make_geo(Co, Ci, K, 0, g) != SSQ_OK) return 0;
-  return col_tiling_prep(g).ncolblk;
-}
-
-extern "C" int ssq_adashift_bwd_prepared(const float* gWhat, const uint32_t* fpack,
-                                         const float* hterm, const float* alpha,
-                                         const float* delta, const float* zp, int S, int64_t Co,
-                                         int64_t Ci, int64_t K, int qmin, int qmax,
-                                         float reg_lambda, float reg_b, const float* reg_dev,
-                                         float* galpha, float* reg_vals, unsigned* counters,
-                                         void* ws, size_t ws_bytes, ssq_stream_t stream) {
-  SSQ_GEO(Co, Ci, K, 0, g);
-  SSQ_REQUIRE(S >= 1 && S <= kMaxPrepS, SSQ_E_ARG, "ssq_adashift_bwd_prepared: 1 <= S <= %d",
-              kMaxPrepS);
-  SSQ_REQUIRE(gWhat && fpack && hterm && alpha && delta && zp && galpha && counters, SSQ_E_ARG,
-              "ssq_adashift_bwd_prepared: null");
-  const ColTiling tl = col_tiling_prep(g);
-  SSQ_REQUIRE(tl.threads <= 1024, SSQ_E_ARG, "ssq_adashift_bwd_prepared: K > 1024");
-  SSQ_REQUIRE(ws && ws_bytes >= ssq_adashift_bwd_prepared_workspace_size(Co, Ci, K, S), SSQ_E_WS,
-              "ssq_adashift_bwd_prepared: workspace too small");
-  hipStream_t s = (hipStream_t)stream;
-  const size_t lds = (size_t)tl.threads * S * sizeof(double);
-  const float lo = (float)qmin, hi = (float)qmax;
-#define SSQ_BWDP(NS)                                                                            \
-  hipLaunchKernelGGL((alpha_bwd_prep<NS>), dim3(tl.ncolblk, tl.nchunk), dim3(tl.threads), lds, s, \
-                     gWhat, fpack, hterm, alpha, delta, zp, g, tl, lo, hi, reg_lambda, reg_b,   \
-                     reg_dev, (double*)ws, counters, galpha, reg_vals)
-  switch (S) {
-    case 1: SSQ_BWDP(1); break;
-    case 2: SSQ_BWDP(2); break;
-    case 3: SSQ_BWDP(3); break;
-    default: SSQ_BWDP(4); break;
-  }
-#undef SSQ_BWDP
-  return check_launch("ssq_adashift_bwd_prepared");
 }

@@ -1,0 +1,521 @@
+// K5p / K6p: the prepared adaShift path, multi-segment.
+//
+// In the fused loop (layer_recon_fused_shiftedScale.py:59-66) W, delta, the shift
+// candidates and beta are frozen: only alpha learns.  The reference therefore computes its
+// floors x_q ONCE (channelQuant.py:284-286) and each iteration only re-mixes them.  The
+// prepared path does the same: ssq_adashift_prepare evaluates, once, every floor
+// F_i = floor(W / (delta*s_i)) with the very fp32 ops the recomputing kernels use, packed as
+// int8 bytes into one 32-bit word per weight (S <= 4), and the rounding term
+// h(beta) (or [beta >= 0]) as fp32.  The per-iteration kernels then stream
+// fpack + hterm (+ gWhat) with no divide and no exp per element -- 12 B/elem forward
+// (fpack, hterm in; What out) and 12 B/elem backward (gWhat, fpack, hterm in), the §8(d)
+// algorithmic bytes -- and produce bit-identical What / identical gradients.  The alpha
+// backward reduction is two fixed-order launches (a last-workgroup single launch measured
+// 88 us on a 512x512x3x3 conv: the agent-scope release fence every workgroup needs writes
+// back its XCD's L2, so it is not used).
+//
+// Every kernel takes a table of up to kMaxPrepSeg weights ("segments"), so the adaShift
+// forward of ALL the convs of a block is one launch and their alpha backward two (stage 1
+// over every segment's tiles, stage 2 over every segment's input channels): the weights of
+// a block depend only on alpha, which is fixed for the iteration
+// (quant/_engine.py stash_block_weights).
+#include <stdlib.h>
+
+#include "adashift_common.h"
+
+namespace ssq {
+
+constexpr int kMaxPrepS = 4;
+constexpr int kRBP = 8;            // rows per load batch
+constexpr int kMaxPrepSeg = 8;     // weights per launch (a block has <= 4 convs)
+
+__global__ __launch_bounds__(kBlock) void adashift_prepare_kernel(
+    const float* __restrict__ W, const float* __restrict__ beta, const float* __restrict__ delta,
+    Shifts sh, Geo g, uint32_t n, int hard_r, uint32_t* __restrict__ fpack,
+    float* __restrict__ hterm, int* __restrict__ overflow) {
+  const uint32_t stride = gridDim.x * blockDim.x;
+  int bad = 0;
+  for (uint32_t e = blockIdx.x * blockDim.x + threadIdx.x; e < n; e += stride) {
+    const uint32_t co = e / g.CiK;
+    const float w = W[e], d = delta[co];
+    uint32_t word = 0;
+    for (int i = 0; i < sh.n; ++i) {
+      const float F = floorf(w / __fmul_rn(d, sh.s[i]));   // = soft_floor's candidate
+      bad |= !(F >= -128.0f && F <= 127.0f);
+      const int fi = F >= -128.0f && F <= 127.0f ? (int)F : 0;
+      word |= ((uint32_t)(fi & 0xff)) << (8 * i);
+    }
+    fpack[e] = word;
+    const float b = beta[e];
+    hterm[e] = hard_r ? (b >= 0.0f ? 1.0f : 0.0f) : rect_sigmoid(b);
+  }
+  if (bad) atomicOr(overflow, 1);
+}
+
+__device__ __forceinline__ float unpack_floor(uint32_t word, int i) {
+  return (float)(int8_t)(uint8_t)(word >> (8 * i));
+}
+
+
+// Column tiling (as col_tiling: whole input channels per workgroup, ncb*K <= 256 columns,
+// 256 threads) with row chunks of >= 8 rows so each thread keeps 2-3 x 8 loads in flight and
+// the partials stay small (nchunk x Ci x S doubles); ~1536 workgroups at most per weight.
+// A/B tuning (tools/adashift_bench.py --blocks): SSQ_PREP_WGS = target workgroups per
+// weight, SSQ_PREP_ROWS = minimum rows per chunk; read once.
+static uint32_t prep_env(const char* name, uint32_t dflt) {
+  const char* v = getenv(name);
+  return v && *v ? (uint32_t)atoi(v) : dflt;
+}
+static ColTiling col_tiling_prep(const Geo& g) {
+  static const uint32_t kWgs = prep_env("SSQ_PREP_WGS", 1536);
+  static const uint32_t kRows = prep_env("SSQ_PREP_ROWS", kRBP);
+  ColTiling t;
+  t.ncb = g.K >= (uint32_t)kBlock ? 1u : (uint32_t)kBlock / g.K;
+  if (t.ncb > g.Ci) t.ncb = g.Ci;
+  t.ncolblk = (g.Ci + t.ncb - 1) / t.ncb;
+  t.threads = kBlock;
+  uint32_t want = kWgs / t.ncolblk;
+  const uint32_t by_rows = (g.Co + kRows - 1) / kRows;
+  if (want > by_rows) want = by_rows;
+  if (want > kMaxChunks) want = kMaxChunks;
+  if (want < 1) want = 1;
+  t.R = (g.Co + want - 1) / want;
+  t.nchunk = (g.Co + t.R - 1) / t.R;
+  return t;
+}
+
+struct PrepSeg {
+  const uint32_t* fpack;
+  const float* hterm;
+  const float* alpha;
+  const float* delta;
+  const float* zp;
+  const float* gWhat;
+  float* What;
+  double* part;
+  float* galpha;
+  float* reg_vals;
+  Geo g;
+  ColTiling tl;
+  uint32_t blk0;     // first workgroup of this segment (forward / stage 1)
+  uint32_t wave0;    // first wave of this segment (stage 2: one wave per input channel)
+  float lo, hi;
+};
+struct PrepTable {
+  PrepSeg s[kMaxPrepSeg];
+  int nseg;
+};
+
+// the segment of workgroup (or wave) `id` (uniform: the table is read with scalar loads
+// from the kernel arguments, as ssq_adam's)
+template <bool BY_WAVE>
+__device__ __forceinline__ int find_seg(const PrepTable& tab, uint32_t id) {
+  int si = 0;
+  while (si + 1 < tab.nseg && id >= (BY_WAVE ? tab.s[si + 1].wave0 : tab.s[si + 1].blk0)) ++si;
+  return si;
+}
+
+template <int NS, int HARD_T>
+__global__ __launch_bounds__(kBlock) void shift_fwd_prep(PrepTable tab) {
+  const PrepSeg& sg = tab.s[find_seg<false>(tab, blockIdx.x)];
+  const Geo& g = sg.g;
+  const uint32_t local = blockIdx.x - sg.blk0;
+  const uint32_t bx = local % sg.tl.ncolblk, by = local / sg.tl.ncolblk;
+  const uint32_t ci0 = bx * sg.tl.ncb;
+  const uint32_t nci = min(sg.tl.ncb, g.Ci - ci0);
+  const uint32_t t = threadIdx.x;
+  if (t >= nci * g.K) return;
+  const uint32_t ci = ci0 + t / g.K, j = ci0 * g.K + t;
+  float a[kMaxS], p[kMaxS];
+  load_row(sg.alpha, ci, NS, a);
+  soft_targets<kMaxS>(a, NS, nullptr, p);
+  const int sel = argmax_first(p, NS);
+  const uint32_t co0 = by * sg.tl.R, co1 = min(co0 + sg.tl.R, g.Co);
+  const uint32_t* __restrict__ fpack = sg.fpack;
+  const float* __restrict__ hterm = sg.hterm;
+  const float* __restrict__ delta = sg.delta;
+  const float* __restrict__ zp = sg.zp;
+  float* __restrict__ What = sg.What;
+  const float lo = sg.lo, hi = sg.hi;
+  auto one = [&](uint32_t co, uint32_t fw, float h, float d, float z) {
+    float xf;
+    if (HARD_T) {
+      xf = unpack_floor(fw, sel);
+    } else {
+      xf = __fmul_rn(unpack_floor(fw, 0), p[0]);
+#pragma unroll
+      for (int i = 1; i < NS; ++i) xf = __fadd_rn(xf, __fmul_rn(unpack_floor(fw, i), p[i]));
+    }
+    const float q = clampf(__fadd_rn(__fadd_rn(xf, h), z), lo, hi);
+    What[co * g.CiK + j] = __fmul_rn(__fsub_rn(q, z), __fmul_rn(d, 1.0f));
+  };
+  uint32_t co = co0;
+  for (; co + kRBP <= co1; co += kRBP) {
+    uint32_t fw[kRBP];
+    float h[kRBP], d[kRBP], z[kRBP];
+#pragma unroll
+    for (int r = 0; r < kRBP; ++r) {
+      const uint32_t e = (co + r) * g.CiK + j;
+      fw[r] = fpack[e];
+      h[r] = hterm[e];
+      d[r] = delta[co + r];
+      z[r] = zp[co + r];
+    }
+#pragma unroll
+    for (int r = 0; r < kRBP; ++r) one(co + r, fw[r], h[r], d[r], z[r]);
+  }
+  for (; co < co1; ++co) {
+    const uint32_t e = co * g.CiK + j;
+    one(co, fpack[e], hterm[e], delta[co], zp[co]);
+  }
+}
+
+// Backward stage 1: sums of g_int * F_i per (chunk, ci) into
+// part[(ci*nchunk + chunk)*S + i] (input-channel-major: stage 2 reads one coalesced run).
+template <int NS>
+__global__ __launch_bounds__(kBlock) void alpha_bwd_prep(PrepTable tab) {
+  __shared__ double red[kBlock * NS];
+  const PrepSeg& sg = tab.s[find_seg<false>(tab, blockIdx.x)];
+  const Geo& g = sg.g;
+  const uint32_t local = blockIdx.x - sg.blk0;
+  const uint32_t bx = local % sg.tl.ncolblk, by = local / sg.tl.ncolblk;
+  const uint32_t ci0 = bx * sg.tl.ncb;
+  const uint32_t nci = min(sg.tl.ncb, g.Ci - ci0);
+  const uint32_t t = threadIdx.x;
+  double acc[NS];
+#pragma unroll
+  for (int i = 0; i < NS; ++i) acc[i] = 0.0;
+  if (t < nci * g.K) {
+    const uint32_t ci = ci0 + t / g.K, j = ci0 * g.K + t;
+    float a[kMaxS], p[kMaxS];
+    load_row(sg.alpha, ci, NS, a);
+    soft_targets<kMaxS>(a, NS, nullptr, p);
+    const uint32_t* __restrict__ fpack = sg.fpack;
+    const float* __restrict__ hterm = sg.hterm;
+    const float* __restrict__ gWhat = sg.gWhat;
+    const float* __restrict__ delta = sg.delta;
+    const float* __restrict__ zp = sg.zp;
+    const float lo = sg.lo, hi = sg.hi;
+    auto one = [&](uint32_t fw, float h, float d, float z, float gy) {
+      float F[NS];
+#pragma unroll
+      for (int i = 0; i < NS; ++i) F[i] = unpack_floor(fw, i);
+      float xf = __fmul_rn(F[0], p[0]);
+#pragma unroll
+      for (int i = 1; i < NS; ++i) xf = __fadd_rn(xf, __fmul_rn(F[i], p[i]));
+      const float u = __fadd_rn(__fadd_rn(xf, h), z);
+      const float gi = (u >= lo && u <= hi) ? __fmul_rn(gy, __fmul_rn(d, 1.0f)) : 0.0f;
+#pragma unroll
+      for (int i = 0; i < NS; ++i) acc[i] += (double)gi * (double)F[i];
+    };
+    const uint32_t co0 = by * sg.tl.R, co1 = min(co0 + sg.tl.R, g.Co);
+    uint32_t co = co0;
+    for (; co + kRBP <= co1; co += kRBP) {
+      uint32_t fw[kRBP];
+      float h[kRBP], d[kRBP], z[kRBP], gy[kRBP];
+#pragma unroll
+      for (int r = 0; r < kRBP; ++r) {
+        const uint32_t e = (co + r) * g.CiK + j;
+        fw[r] = fpack[e];
+        h[r] = hterm[e];
+        gy[r] = gWhat[e];
+        d[r] = delta[co + r];
+        z[r] = zp[co + r];
+      }
+#pragma unroll
+      for (int r = 0; r < kRBP; ++r) one(fw[r], h[r], d[r], z[r], gy[r]);
+    }
+    for (; co < co1; ++co) {
+      const uint32_t e = co * g.CiK + j;
+      one(fpack[e], hterm[e], delta[co], zp[co], gWhat[e]);
+    }
+  }
+#pragma unroll
+  for (int i = 0; i < NS; ++i) red[t * NS + i] = acc[i];
+  __syncthreads();
+  if (t < nci) {
+#pragma unroll
+    for (int i = 0; i < NS; ++i) {
+      double sum = 0.0;
+      for (uint32_t k = 0; k < g.K; ++k) sum += red[(t * g.K + k) * NS + i];
+      sg.part[((size_t)(ci0 + t) * sg.tl.nchunk + by) * NS + i] = sum;
+    }
+  }
+}
+
+// Stage 2: one wave per (segment, input channel).  Every load the wave needs (alpha row,
+// the device (lambda, b) pair, lane c's chunks c, c+64, ... -- one coalesced run per round)
+// is issued before any math; lanes i < S evaluate shift i's regulariser term meanwhile; a
+// fixed shuffle tree adds the lanes and lane 0 applies the softmax/clamp backward (same
+// values, same order as alpha_chain).  Deterministic, no atomics.
+constexpr uint32_t kMaxPrepChunkRounds = kMaxChunks / kWave;
+template <int NS>
+__global__ __launch_bounds__(kBlock) void alpha_bwd_prep_stage2(PrepTable tab, float reg_lambda,
+                                                                 float reg_b,
+                                                                 const float* __restrict__ reg_dev) {
+  const uint32_t wave = blockIdx.x * (kBlock / kWave) + threadIdx.x / kWave;
+  const uint32_t lane = threadIdx.x & (kWave - 1);
+  const PrepSeg& sg = tab.s[find_seg<true>(tab, __builtin_amdgcn_readfirstlane(wave))];
+  const uint32_t ci = wave - sg.wave0;
+  if (ci >= sg.g.Ci) return;
+  const uint32_t nchunk = sg.tl.nchunk;
+  float a[kMaxS];
+  load_row(sg.alpha, ci, NS, a);
+  if (reg_dev) {
+    reg_lambda = reg_dev[0];
+    reg_b = reg_dev[1];
+  }
+  const double* pp = sg.part + (size_t)ci * nchunk * NS;
+  double v[kMaxPrepChunkRounds][NS];
+#pragma unroll
+  for (uint32_t r = 0; r < kMaxPrepChunkRounds; ++r) {
+    const uint32_t c = lane + r * kWave;
+#pragma unroll
+    for (int i = 0; i < NS; ++i) v[r][i] = c < nchunk ? pp[(size_t)c * NS + i] : 0.0;
+  }
+  float sm[kMaxS], p[kMaxS];
+  soft_targets<kMaxS>(a, NS, sm, p);
+  double rv = 0.0, rg = 0.0;
+  if (reg_lambda != 0.0f && lane < (uint32_t)NS) {
+    float pl = p[0];
+#pragma unroll
+    for (int i = 1; i < NS; ++i)
+      if ((uint32_t)i == lane) pl = p[i];
+    reg_term(pl, reg_lambda, reg_b, 0, rv, rg);
+  }
+  double tot[kMaxS];
+#pragma unroll
+  for (int i = 0; i < NS; ++i) {
+    tot[i] = v[0][i];
+#pragma unroll
+    for (uint32_t r = 1; r < kMaxPrepChunkRounds; ++r) tot[i] += v[r][i];
+    tot[i] = wave_sum(tot[i]);
+  }
+  double rvs[kMaxS], rgs[kMaxS];
+#pragma unroll
+  for (int i = 0; i < NS; ++i) {
+    rvs[i] = __shfl(rv, i, kWave);
+    rgs[i] = __shfl(rg, i, kWave);
+  }
+  if (lane != 0) return;
+  float ga[kMaxS], reg = 0.0f;
+  if (reg_lambda != 0.0f) {
+    double acc = 0.0;
+#pragma unroll
+    for (int i = 0; i < NS; ++i) {
+      acc += rvs[i];
+      tot[i] += rgs[i];
+    }
+    reg = (float)((double)reg_lambda * acc);
+  }
+  softmax_clamp_bwd(sm, NS, tot, ga);
+#pragma unroll
+  for (int i = 0; i < NS; ++i) sg.galpha[(size_t)ci * NS + i] = ga[i];
+  if (sg.reg_vals) sg.reg_vals[ci] = reg;
+}
+
+// ------------------------------------------------------------------ host side
+struct SegArgs {
+  int nseg;
+  const uint32_t* const* fpack;
+  const float* const* hterm;
+  const float* const* alpha;
+  const float* const* delta;
+  const float* const* zp;
+  const int64_t* Co;
+  const int64_t* Ci;
+  const int64_t* K;
+  const int* qmin;
+  const int* qmax;
+};
+
+static int make_seg(const SegArgs& a, int i, PrepSeg& sg, const char* what) {
+  SSQ_REQUIRE(a.fpack[i] && a.hterm[i] && a.alpha[i] && a.delta[i] && a.zp[i], SSQ_E_ARG,
+              "%s: null pointer in segment %d", what, i);
+  const int rc = make_geo(a.Co[i], a.Ci[i], a.K[i], 0, sg.g);
+  if (rc) return rc;
+  SSQ_REQUIRE(sg.g.K <= (uint32_t)kBlock, SSQ_E_ARG, "%s: kernel window K > %d", what, kBlock);
+  SSQ_REQUIRE(a.qmin[i] < a.qmax[i], SSQ_E_ARG, "%s: qmin >= qmax", what);
+  sg.fpack = a.fpack[i];
+  sg.hterm = a.hterm[i];
+  sg.alpha = a.alpha[i];
+  sg.delta = a.delta[i];
+  sg.zp = a.zp[i];
+  sg.gWhat = nullptr;
+  sg.What = nullptr;
+  sg.part = nullptr;
+  sg.galpha = nullptr;
+  sg.reg_vals = nullptr;
+  sg.tl = col_tiling_prep(sg.g);
+  sg.lo = (float)a.qmin[i];
+  sg.hi = (float)a.qmax[i];
+  return SSQ_OK;
+}
+
+static size_t part_bytes(const PrepSeg& sg, int S) {
+  const size_t b = (size_t)sg.tl.nchunk * sg.g.Ci * S * sizeof(double);
+  return (b + 255) / 256 * 256;
+}
+
+}  // namespace ssq
+
+using namespace ssq;
+
+extern "C" int ssq_adashift_prepare(const float* W, const float* beta, const float* delta,
+                                    const float* shifts, int S, int64_t Co, int64_t Ci, int64_t K,
+                                    int hard_round, uint32_t* fpack, float* hterm, int* overflow,
+                                    ssq_stream_t stream) {
+  SSQ_GEO(Co, Ci, K, 0, g);
+  SSQ_SHIFTS(shifts, S, sh);
+  SSQ_REQUIRE(S <= kMaxPrepS, SSQ_E_ARG, "ssq_adashift_prepare: S <= %d", kMaxPrepS);
+  SSQ_REQUIRE(W && beta && delta && fpack && hterm && overflow, SSQ_E_ARG,
+              "ssq_adashift_prepare: null");
+  const uint32_t n = g.Co * g.CiK;
+  hipLaunchKernelGGL(adashift_prepare_kernel, dim3(grid_for(n, kBlock)), dim3(kBlock), 0,
+                     (hipStream_t)stream, W, beta, delta, sh, g, n, hard_round, fpack, hterm,
+                     overflow);
+  return check_launch("ssq_adashift_prepare");
+}
+
+extern "C" int ssq_adashift_fwd_prepared_multi(int nseg, const uint32_t* const* fpack,
+                                               const float* const* hterm,
+                                               const float* const* alpha,
+                                               const float* const* delta, const float* const* zp,
+                                               const int64_t* Co, const int64_t* Ci,
+                                               const int64_t* K, const int* qmin, const int* qmax,
+                                               int S, int hard_targets, float* const* What,
+                                               ssq_stream_t stream) {
+  const char* what = "ssq_adashift_fwd_prepared_multi";
+  SSQ_REQUIRE(nseg >= 1 && fpack && hterm && alpha && delta && zp && Co && Ci && K && qmin &&
+                  qmax && What, SSQ_E_ARG, "%s: bad arrays", what);
+  SSQ_REQUIRE(S >= 1 && S <= kMaxPrepS, SSQ_E_ARG, "%s: 1 <= S <= %d", what, kMaxPrepS);
+  const SegArgs a{nseg, fpack, hterm, alpha, delta, zp, Co, Ci, K, qmin, qmax};
+  hipStream_t s = (hipStream_t)stream;
+  for (int base = 0; base < nseg; base += kMaxPrepSeg) {
+    PrepTable tab;
+    tab.nseg = nseg - base < kMaxPrepSeg ? nseg - base : kMaxPrepSeg;
+    uint32_t blk = 0;
+    for (int k = 0; k < tab.nseg; ++k) {
+      PrepSeg& sg = tab.s[k];
+      const int rc = make_seg(a, base + k, sg, what);
+      if (rc) return rc;
+      SSQ_REQUIRE(What[base + k], SSQ_E_ARG, "%s: null What", what);
+      sg.What = What[base + k];
+      sg.blk0 = blk;
+      sg.wave0 = 0;
+      blk += sg.tl.ncolblk * sg.tl.nchunk;
+    }
+#define SSQ_FWDP(NS)                                                                         \
+  do {                                                                                       \
+    if (hard_targets)                                                                        \
+      hipLaunchKernelGGL((shift_fwd_prep<NS, 1>), dim3(blk), dim3(kBlock), 0, s, tab);       \
+    else                                                                                     \
+      hipLaunchKernelGGL((shift_fwd_prep<NS, 0>), dim3(blk), dim3(kBlock), 0, s, tab);       \
+  } while (0)
+    switch (S) {
+      case 1: SSQ_FWDP(1); break;
+      case 2: SSQ_FWDP(2); break;
+      case 3: SSQ_FWDP(3); break;
+      default: SSQ_FWDP(4); break;
+    }
+#undef SSQ_FWDP
+    const int rc = check_launch(what);
+    if (rc) return rc;
+  }
+  return SSQ_OK;
+}
+
+extern "C" size_t ssq_adashift_bwd_prepared_multi_workspace_size(int nseg, const int64_t* Co,
+                                                                 const int64_t* Ci,
+                                                                 const int64_t* K, int S) {
+  if (nseg < 1 || !Co || !Ci || !K || S < 1 || S > kMaxPrepS) return 0;
+  size_t total = 0;
+  for (int i = 0; i < nseg; ++i) {
+    PrepSeg sg;
+    if (make_geo(Co[i], Ci[i], K[i], 0, sg.g) != SSQ_OK) return 0;
+    sg.tl = col_tiling_prep(sg.g);
+    total += part_bytes(sg, S);
+  }
+  return total;
+}
+
+extern "C" int ssq_adashift_bwd_prepared_multi(
+    int nseg, const float* const* gWhat, const uint32_t* const* fpack, const float* const* hterm,
+    const float* const* alpha, const float* const* delta, const float* const* zp,
+    const int64_t* Co, const int64_t* Ci, const int64_t* K, const int* qmin, const int* qmax,
+    int S, float reg_lambda, float reg_b, const float* reg_dev, float* const* galpha,
+    float* const* reg_vals, void* ws, size_t ws_bytes, ssq_stream_t stream) {
+  const char* what = "ssq_adashift_bwd_prepared_multi";
+  SSQ_REQUIRE(nseg >= 1 && gWhat && fpack && hterm && alpha && delta && zp && Co && Ci && K &&
+                  qmin && qmax && galpha, SSQ_E_ARG, "%s: bad arrays", what);
+  SSQ_REQUIRE(S >= 1 && S <= kMaxPrepS, SSQ_E_ARG, "%s: 1 <= S <= %d", what, kMaxPrepS);
+  SSQ_REQUIRE(ws && ws_bytes >= ssq_adashift_bwd_prepared_multi_workspace_size(nseg, Co, Ci, K, S),
+              SSQ_E_WS, "%s: workspace too small", what);
+  const SegArgs a{nseg, fpack, hterm, alpha, delta, zp, Co, Ci, K, qmin, qmax};
+  hipStream_t s = (hipStream_t)stream;
+  char* wsp = (char*)ws;
+  for (int base = 0; base < nseg; base += kMaxPrepSeg) {
+    PrepTable tab;
+    tab.nseg = nseg - base < kMaxPrepSeg ? nseg - base : kMaxPrepSeg;
+    uint32_t blk = 0, waves = 0;
+    for (int k = 0; k < tab.nseg; ++k) {
+      PrepSeg& sg = tab.s[k];
+      const int i = base + k;
+      const int rc = make_seg(a, i, sg, what);
+      if (rc) return rc;
+      SSQ_REQUIRE(gWhat[i] && galpha[i], SSQ_E_ARG, "%s: null gWhat/galpha", what);
+      sg.gWhat = gWhat[i];
+      sg.galpha = galpha[i];
+      sg.reg_vals = reg_vals ? reg_vals[i] : nullptr;
+      sg.part = (double*)wsp;
+      wsp += part_bytes(sg, S);
+      sg.blk0 = blk;
+      sg.wave0 = waves;
+      blk += sg.tl.ncolblk * sg.tl.nchunk;
+      waves += sg.g.Ci;
+    }
+    const unsigned blocks2 = (waves + kBlock / kWave - 1) / (kBlock / kWave);
+#define SSQ_BWDP(NS)                                                                          \
+  do {                                                                                        \
+    hipLaunchKernelGGL((alpha_bwd_prep<NS>), dim3(blk), dim3(kBlock), 0, s, tab);             \
+    hipLaunchKernelGGL((alpha_bwd_prep_stage2<NS>), dim3(blocks2), dim3(kBlock), 0, s, tab,   \
+                       reg_lambda, reg_b, reg_dev);                                           \
+  } while (0)
+    switch (S) {
+      case 1: SSQ_BWDP(1); break;
+      case 2: SSQ_BWDP(2); break;
+      case 3: SSQ_BWDP(3); break;
+      default: SSQ_BWDP(4); break;
+    }
+#undef SSQ_BWDP
+    const int rc = check_launch(what);
+    if (rc) return rc;
+  }
+  return SSQ_OK;
+}
+
+// single-weight forms (nseg = 1)
+extern "C" int ssq_adashift_fwd_prepared(const uint32_t* fpack, const float* hterm,
+                                         const float* alpha, const float* delta, const float* zp,
+                                         int S, int64_t Co, int64_t Ci, int64_t K, int hard_targets,
+                                         int qmin, int qmax, float* What, ssq_stream_t stream) {
+  return ssq_adashift_fwd_prepared_multi(1, &fpack, &hterm, &alpha, &delta, &zp, &Co, &Ci, &K,
+                                         &qmin, &qmax, S, hard_targets, &What, stream);
+}
+
+extern "C" size_t ssq_adashift_bwd_prepared_workspace_size(int64_t Co, int64_t Ci, int64_t K,
+                                                           int S) {
+  return ssq_adashift_bwd_prepared_multi_workspace_size(1, &Co, &Ci, &K, S);
+}
+
+extern "C" int ssq_adashift_bwd_prepared(const float* gWhat, const uint32_t* fpack,
+                                         const float* hterm, const float* alpha,
+                                         const float* delta, const float* zp, int S, int64_t Co,
+                                         int64_t Ci, int64_t K, int qmin, int qmax,
+                                         float reg_lambda, float reg_b, const float* reg_dev,
+                                         float* galpha, float* reg_vals, void* ws,
+                                         size_t ws_bytes, ssq_stream_t stream) {
+  return ssq_adashift_bwd_prepared_multi(1, &gWhat, &fpack, &hterm, &alpha, &delta, &zp, &Co, &Ci,
+                                         &K, &qmin, &qmax, S, reg_lambda, reg_b, reg_dev, &galpha,
+                                         reg_vals ? &reg_vals : nullptr, ws, ws_bytes, stream);
+}

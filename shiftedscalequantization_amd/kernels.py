@@ -312,8 +312,8 @@ def adashift(alpha, beta, w, delta, zp, shifts, n_bits, sym, hard_t, hard_r, reg
 class AdaShiftPrep:
     """Loop-invariant state of a conv ChannelQuant in 'adaShift' mode (W, delta, shifts,
     beta frozen, as in the fused loop): the packed int8 floors and h(beta) of
-    ssq_adashift_prepare, plus the backward's zeroed reduction counters.  `ok` is False
-    when a floor does not fit int8 (the caller keeps the recomputing kernels)."""
+    ssq_adashift_prepare.  `ok` is False when a floor does not fit int8 or the kernel
+    window exceeds 256 taps (the caller keeps the recomputing kernels)."""
 
     def __init__(self, w, beta, delta, shifts, hard_r):
         w, wp = fptr(w.detach(), "weight")
@@ -329,50 +329,76 @@ class AdaShiftPrep:
         flag = torch.zeros(1, dtype=torch.int32, device=w.device)
         call("ssq_adashift_prepare", wp, bp, dp, A.shifts_arg(shifts), self.S, Co, Ci, K,
              int(hard_r), _vp(self.fpack), _vp(self.hterm), _vp(flag), stream_of(w))
-        self.ok = int(flag.item()) == 0      # one sync, at preparation time only
-        n = int(query("ssq_adashift_bwd_prepared_counters", Co, Ci, K))
-        self.counters = torch.zeros(max(n, 1), dtype=torch.int32, device=w.device)
+        self.ok = int(flag.item()) == 0 and K <= 256   # one sync, at preparation time only
+
+
+def _ptrs(ts):
+    return (C.c_void_p * len(ts))(*[None if t is None else t.data_ptr() for t in ts])
 
 
 class AdaShiftPrepFn(torch.autograd.Function):
-    """ChannelQuant 'adaShift' forward from the prepared floors (K5p) and its alpha
-    backward (K6p, one launch, shift regulariser folded in as in AdaShiftFn)."""
+    """ChannelQuant 'adaShift' forward of SEVERAL prepared weights (e.g. every conv of a
+    block, same S and regulariser) in one launch (K5p), and their alpha backward in two
+    (K6p, shift regulariser folded in as in AdaShiftFn).  cfg = (hard_t, reg, entries),
+    entries[i] = (prep, delta, zp, n_bits, sym); inputs = the alphas; outputs = the Whats."""
 
     @staticmethod
-    def forward(ctx, alpha, prep, delta, zp, n_bits, sym, hard_t, reg):
-        a, ap = fptr(alpha.detach(), "alpha")
-        d, dp = fptr(delta.detach(), "delta")
-        z, zpp = fptr(zp.detach(), "zero_point")
-        Co, Ci, K = prep.geo
-        lo, hi = qrange(n_bits, sym)
-        out = torch.empty_like(prep.hterm)
-        call("ssq_adashift_fwd_prepared", _vp(prep.fpack), _vp(prep.hterm), ap, dp, zpp, prep.S,
-             Co, Ci, K, int(hard_t), lo, hi, _vp(out), None, stream_of(out))
-        ctx.save_for_backward(a, d, z)
-        ctx.cfg = (prep, n_bits, sym, hard_t, reg)
-        return out
+    def forward(ctx, cfg, *alphas):
+        hard_t, reg, entries = cfg
+        keep, al, dl, zl = [], [], [], []
+        for a, (prep, d, z, n_bits, sym) in zip(alphas, entries):
+            a, _ = fptr(a.detach(), "alpha")
+            d, _ = fptr(d.detach(), "delta")
+            z, _ = fptr(z.detach(), "zero_point")
+            al.append(a)
+            dl.append(d)
+            zl.append(z)
+        n = len(entries)
+        preps = [e[0] for e in entries]
+        outs = [torch.empty_like(p.hterm) for p in preps]
+        Co = (C.c_int64 * n)(*[p.geo[0] for p in preps])
+        Ci = (C.c_int64 * n)(*[p.geo[1] for p in preps])
+        Kk = (C.c_int64 * n)(*[p.geo[2] for p in preps])
+        qr = [qrange(e[3], e[4]) for e in entries]
+        lo = (C.c_int * n)(*[q[0] for q in qr])
+        hi = (C.c_int * n)(*[q[1] for q in qr])
+        call("ssq_adashift_fwd_prepared_multi", n, _ptrs([p.fpack for p in preps]),
+             _ptrs([p.hterm for p in preps]), _ptrs(al), _ptrs(dl), _ptrs(zl), Co, Ci, Kk, lo, hi,
+             preps[0].S, int(hard_t), _ptrs(outs), stream_of(outs[0]))
+        ctx.save_for_backward(*al, *dl, *zl)
+        ctx.cfg = (hard_t, reg, preps, (Co, Ci, Kk, lo, hi))
+        return tuple(outs)
 
     @staticmethod
-    def backward(ctx, g):
-        a, d, z = ctx.saved_tensors
-        prep, n_bits, sym, hard_t, reg = ctx.cfg
-        if not ctx.needs_input_grad[0] or hard_t:
-            return (None,) * 8
-        g = g.contiguous()
-        Co, Ci, K = prep.geo
-        lo, hi = qrange(n_bits, sym)
-        ga = torch.empty_like(a)
+    def backward(ctx, *gs):
+        hard_t, reg, preps, (Co, Ci, Kk, lo, hi) = ctx.cfg
+        n = len(preps)
+        if hard_t or not any(ctx.needs_input_grad[1:]):
+            return (None,) * (n + 1)
+        saved = ctx.saved_tensors
+        al, dl, zl = saved[:n], saved[n:2 * n], saved[2 * n:]
+        gs = [torch.zeros_like(p.hterm) if g is None else g.contiguous() for g, p in zip(gs, preps)]
+        gas = [torch.empty_like(a) for a in al]
         lam, bb, reg_vals, reg_dev = (0.0, 0.0, None, None) if reg is None else reg
-        wsb = query("ssq_adashift_bwd_prepared_workspace_size", Co, Ci, K, prep.S)
-        ws, wsn = workspace(wsb, g.device)
-        call("ssq_adashift_bwd_prepared", _vp(g), _vp(prep.fpack), _vp(prep.hterm), _vp(a),
-             _vp(d), _vp(z), prep.S, Co, Ci, K, lo, hi, float(lam), float(bb), _vp(reg_dev),
-             _vp(ga), _vp(reg_vals), _vp(prep.counters), ws, wsn, stream_of(g))
-        return (ga, None, None, None, None, None, None, None)
+        rv = reg_vals if isinstance(reg_vals, (list, tuple)) else [reg_vals] * n
+        S = preps[0].S
+        wsb = query("ssq_adashift_bwd_prepared_multi_workspace_size", n, Co, Ci, Kk, S)
+        ws, wsn = workspace(wsb, gs[0].device)
+        call("ssq_adashift_bwd_prepared_multi", n, _ptrs(gs), _ptrs([p.fpack for p in preps]),
+             _ptrs([p.hterm for p in preps]), _ptrs(al), _ptrs(dl), _ptrs(zl), Co, Ci, Kk, lo, hi, S,
+             float(lam), float(bb), _vp(reg_dev), _ptrs(gas),
+             _ptrs(rv) if any(v is not None for v in rv) else None, ws, wsn, stream_of(gs[0]))
+        return (None,) + tuple(ga if need else None for ga, need in zip(gas, ctx.needs_input_grad[1:]))
 
 
 def adashift_prepared(alpha, prep, delta, zp, n_bits, sym, hard_t, reg=None):
-    return AdaShiftPrepFn.apply(alpha, prep, delta, zp, n_bits, sym, bool(hard_t), reg)
+    """One prepared weight (ChannelQuant.forward in 'adaShift' mode)."""
+    return AdaShiftPrepFn.apply((bool(hard_t), reg, ((prep, delta, zp, n_bits, sym),)), alpha)[0]
+
+
+def adashift_prepared_multi(alphas, entries, hard_t, reg=None):
+    """Several prepared weights (same S, same regulariser schedule) in one launch."""
+    return AdaShiftPrepFn.apply((bool(hard_t), reg, tuple(entries)), *alphas)
 
 
 def adashift_codes(alpha, beta, w, delta, zp, shifts, n_bits, sym):

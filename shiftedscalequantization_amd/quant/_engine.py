@@ -76,6 +76,38 @@ class BatchFeeder:
         return self.inp[:n], self.out[:n]
 
 
+def stash_block_weights(quantizers):
+    """The adaShift What of every prepared conv quantizer of a block in ONE launch (their
+    alpha backward then runs as one two-launch reduction): they depend only on alpha,
+    fixed for the iteration.  Each quantizer's next forward returns its stashed What.
+    Quantizers that cannot use the prepared path (Linear, S > 4, int8 overflow, beta being
+    learned) are left to compute their own.  Graph-capturable (device work only)."""
+    groups = {}
+    for q in quantizers:
+        if q.opt_mode != 'adaShift':
+            continue
+        prep = q._prepared()
+        if prep is None:
+            continue
+        key = (prep.S, bool(q.hard_targets), id(q._fused_reg[3]) if q._fused_reg else None)
+        groups.setdefault(key, []).append((q, prep))
+    for (S, hard_t, _), members in groups.items():
+        qs = [q for q, _ in members]
+        reg = qs[0]._fused_reg
+        if reg is not None:
+            reg = (reg[0], reg[1], [q._fused_reg[2] for q in qs], reg[3])
+        entries = [(p, q._src_delta, q.zero_point, q.n_bits, q.sym) for q, p in members]
+        outs = K.adashift_prepared_multi([q.alpha for q in qs], entries, hard_t, reg=reg)
+        for q, w in zip(qs, outs):
+            q._stash = w
+
+
+def clear_stash(quantizers):
+    for q in quantizers:
+        if getattr(q, '_stash', None) is not None:
+            q._stash = None
+
+
 class LazyValue:
     """A device scalar (or a thunk producing one) read on demand."""
 

@@ -54,6 +54,7 @@ class ChannelQuant(nn.Module):
         self._xq_cache = None
         self._fused_reg = None      # (lambda, b, reg_vals) set by FusedScaleLossFunction
         self._prep = None           # (key, kernels.AdaShiftPrep) of the prepared path
+        self._stash = None          # What computed ahead by the block's batched launch
 
     # ------------------------------------------------------------------ candidates
     @property
@@ -97,6 +98,11 @@ class ChannelQuant(nn.Module):
         return self._prep[1]
 
     def forward(self, x):
+        if self._stash is not None:
+            # this iteration's What, computed with the other convs of the block in one
+            # launch (_engine.stash_block_weights); consumed once
+            w, self._stash = self._stash, None
+            return w
         if self.opt_mode == 'adaShift':
             prep = self._prepared()
             if prep is not None:

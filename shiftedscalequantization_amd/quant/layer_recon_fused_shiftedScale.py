@@ -19,7 +19,7 @@ from tqdm import tqdm
 
 from .. import kernels as K
 from ..parallel_dp import GradBucket, world
-from ._engine import BatchFeeder, SsqAdam, LazyValue, as_float
+from ._engine import BatchFeeder, SsqAdam, LazyValue, as_float, clear_stash, stash_block_weights
 from .quant_block import BaseQuantBlock
 from .quant_layer import QuantModule
 
@@ -96,7 +96,10 @@ def _fused_loop(block, modules, iters, lmda, model, p, lr, bias_cal, batch_size,
         """One iteration on the device: gather -> forward -> fused loss+grad -> backward
         (+ RCCL bucket) -> Adam.  No host sync, no host-side state: graph-capturable."""
         cur_inp, cur_out = feeder.gather_lazy()
+        if on_gpu:
+            stash_block_weights(quantizers)     # every conv's What in one launch
         quant_out = block(cur_inp)
+        clear_stash(quantizers)
         relu_in = getattr(quant_out, '_ssq_relu_inputs', None)
         if relu_in:
             # the block ends in the fused epilogue's ReLU: the loss pass writes the gradient

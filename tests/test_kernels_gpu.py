@@ -810,7 +810,7 @@ def test_init_v_golden(K, golden, tag):
     alpha, _, _ = K.shift_init(dev(w), dev(d), SHIFTS, zp=dev(z), n_bits=bits, mode=1)
     if not is_fc and w.shape[1] == 1:
         alpha = alpha.view(1, -1)
-    np.testing.assert_allclose(host(alpha), g[tag + "_lhs_alpha0"], rtol=1e-6, atol=1e-7)
+    close(host(alpha), g[tag + "_lhs_alpha0"], rtol=1e-5, atol=1e-6)   # log/mean ulps
     uaq = Q.UniformAffineQuantizer(n_bits=bits, channel_wise=True, ch=w.shape).cuda()
     shape = (-1, 1) if is_fc else (-1, 1, 1, 1)
     uaq.delta = torch.nn.Parameter(dev(g[tag + "_delta"]).view(shape))
@@ -819,7 +819,7 @@ def test_init_v_golden(K, golden, tag):
     cq = Q.ChannelQuant(1.0, uaq=uaq, weight_tensor=dev(w), shiftTarget=SHIFTS, name=tag)
     cq.init_v(dev(w))
     assert cq.opt_mode == "learned_hard_sigmoid"
-    np.testing.assert_allclose(host(cq.alpha), g[tag + "_lhs_alpha0"], rtol=1e-6, atol=1e-7)
+    close(host(cq.alpha), g[tag + "_lhs_alpha0"], rtol=1e-5, atol=1e-6)
     np.testing.assert_array_equal(np.stack([host(t) for t in cq.x_q]), g[tag + "_lhs_xq"])
 
 
@@ -863,8 +863,7 @@ def test_adashift_prepared_matches_recompute(K, shape, S):
     """The prepared path (packed int8 floors + h(beta), one-launch alpha backward) gives
     the recomputing kernels' What bit for bit (soft and hard targets, soft and hard
     rounding) and their alpha gradients (+ fused regulariser from the device pair) to
-    1e-6; repeated backward launches are bit-identical (the reduction counters re-arm and
-    the last-workgroup sum is in chunk order whoever arrives last)."""
+    1e-6; repeated backward launches are bit-identical (fixed-order reduction)."""
     shifts = [31 / 32, 33 / 32, 1.0, 17 / 16][:S]
     gen = torch.Generator().manual_seed(hash((shape, S)) & 0xffff)
     w = torch.randn(shape, generator=gen) * 0.05
@@ -891,6 +890,7 @@ def test_adashift_prepared_matches_recompute(K, shape, S):
         grads = []
         for _ in range(3):
             a2 = alpha.clone().requires_grad_(True)
+            vals_got.zero_()
             K.adashift_prepared(a2, prep, dd, zd, 2, False, 0,
                                 reg=(0.0, 0.0, vals_got, regp)).backward(gy)
             grads.append(host(a2.grad))
@@ -898,7 +898,42 @@ def test_adashift_prepared_matches_recompute(K, shape, S):
         close(host(vals_got), host(vals_ref), rtol=1e-6, atol=1e-7)
         np.testing.assert_array_equal(grads[0], grads[1])
         np.testing.assert_array_equal(grads[0], grads[2])
-        assert int(prep.counters.abs().sum().item()) == 0
+
+
+def test_adashift_prepared_multi_equals_single(K):
+    """Several weights in ONE multi-segment launch (a block's convs, up to 8 per launch and
+    more in further launches) give each weight's single-launch What and alpha gradient
+    bit for bit, with per-weight regulariser values."""
+    shapes = [(64, 64, 3, 3), (128, 64, 3, 3), (128, 64, 1, 1), (7, 300, 1, 1), (24, 1, 3, 3),
+              (33, 5, 5, 5), (96, 48, 3, 3), (512, 256, 3, 3), (16, 16, 3, 3), (40, 24, 1, 1)]
+    gen = torch.Generator().manual_seed(11)
+    regp = dev([0.1, 7.5])
+    alphas, entries, gys, singles = [], [], [], []
+    for k, shape in enumerate(shapes):
+        w = torch.randn(shape, generator=gen) * 0.05
+        d, z, _ = R.init_scale(w.numpy(), 2 if k % 2 else 4, False, True, "max")
+        wd, dd, zd = w.cuda(), dev(d), dev(z)
+        alpha, beta, _ = K.shift_init(wd, dd, SHIFTS)
+        alpha = alpha + torch.randn(alpha.shape, generator=gen).cuda() * 0.5
+        prep = K.AdaShiftPrep(wd, beta, dd, SHIFTS, 0)
+        assert prep.ok
+        bits = 2 if k % 2 else 4
+        alphas.append(alpha)
+        entries.append((prep, dd, zd, bits, False))
+        gys.append(torch.randn(shape, generator=gen).cuda())
+        a1 = alpha.clone().requires_grad_(True)
+        v1 = torch.zeros(alpha.shape[0], device="cuda")
+        y1 = K.adashift_prepared(a1, prep, dd, zd, bits, False, 0, reg=(0.0, 0.0, v1, regp))
+        y1.backward(gys[-1])
+        singles.append((host(y1), host(a1.grad), host(v1)))
+    am = [a.clone().requires_grad_(True) for a in alphas]
+    vals = [torch.zeros(a.shape[0], device="cuda") for a in alphas]
+    ys = K.adashift_prepared_multi(am, entries, False, reg=(0.0, 0.0, vals, regp))
+    torch.autograd.backward(list(ys), gys)
+    for k, (y, a, v, (ys1, ga1, v1)) in enumerate(zip(ys, am, vals, singles)):
+        np.testing.assert_array_equal(host(y), ys1, err_msg=str(shapes[k]))
+        np.testing.assert_array_equal(host(a.grad), ga1, err_msg=str(shapes[k]))
+        np.testing.assert_array_equal(host(v), v1, err_msg=str(shapes[k]))
 
 
 def test_adashift_prepared_overflow_falls_back(K):

@@ -155,18 +155,21 @@ def test_layer_recon_fused_matches_reference(Q, golden):
     assert q.hard_targets and q.shiftedDone and not q.hard_round    # the layer variant's flags
     with torch.no_grad():
         what_layer = host(q(m.weight))
-    flips = int(np.sum(what_layer != g["what_layer_hard"]))
-    parity_report("a19_layer_recon_fused", rec_rel_err=rec_err, soft_rel_err=soft_err,
-                  hard_rel_err=hard_err, alpha_dev=a_dev, alpha_dev_all=a_max,
-                  degenerate_rows=n_deg, hard_flips=flips, n_weights=what_layer.size)
-    assert rec_err <= 2e-4
-    assert soft_err <= 1e-3 and hard_err <= 1e-3
-    assert a_dev <= 2e-4 and a_max <= walk
-    assert flips <= 0.01 * what_layer.size
-    # np.testing on the fixture's own hard What (hard rounding too) as a second check
+    # hard targets + soft rounding: What carries h(beta), whose ulps (exp/log of the beta
+    # init) differ from the reference's CPU ones -> a float comparison, in units of delta
+    soft_dev = np.abs(what_layer - g["what_layer_hard"]).max() / g["delta"].max()
     q.hard_round = True
     with torch.no_grad():
-        assert np.mean(host(q(m.weight)) != g["what_hard"]) <= 0.01
+        flips = int(np.sum(host(q(m.weight)) != g["what_hard"]))
+    parity_report("a19_layer_recon_fused", rec_rel_err=rec_err, soft_rel_err=soft_err,
+                  hard_rel_err=hard_err, alpha_dev=a_dev, alpha_dev_all=a_max,
+                  degenerate_rows=n_deg, what_softround_dev_in_delta=soft_dev,
+                  hardround_flips=flips, n_weights=what_layer.size)
+    assert rec_err <= 1e-5
+    assert soft_err <= 1e-5 and hard_err <= 1e-5
+    assert a_dev <= 1e-5 and a_max <= walk
+    assert soft_dev <= 1e-5
+    assert flips <= 0.002 * what_layer.size
 
 
 # ------------------------------------------------------------------ a21
@@ -193,7 +196,7 @@ def test_block_recon_shiftedScale_matches_reference(Q, golden):
 
     def call(self, pred, tgt, grad=None):
         r = orig_call(self, pred, tgt, grad)
-        seen.append((float(self.rec_loss), float(r)))
+        seen.append((float(self.rec_loss), float(r.detach())))
         return r
 
     LRS._ScaleLossBase.__call__ = call
@@ -225,13 +228,15 @@ def test_block_recon_shiftedScale_matches_reference(Q, golden):
         stats[n + "_hard_flips"] = int(np.sum(what != g[n + "_a_what"]))
         stats[n + "_n"] = what.size
     parity_report("a21_block_recon_shiftedScale", **stats)
-    assert s_err <= 2e-4 and a_err <= 2e-4
-    assert fin.max() <= 5e-3
+    # observed on MI355X (r2): rel errors <= 5e-7, alpha dev <= 1e-6, beta dev <= 1.2e-5,
+    # 0 delta / hard-weight flips; asserted with margin
+    assert s_err <= 1e-5 and a_err <= 1e-5
+    assert fin.max() <= 1e-5
     for n in ("conv1", "conv2", "downsample"):
-        assert stats[n + "_alpha_dev"] <= 2e-4, n
-        assert stats[n + "_delta_flips"] <= 0.02 * g[n + "_a_delta"].size, n
-        assert stats[n + "_beta_dev"] <= 5e-3, n
-        assert stats[n + "_hard_flips"] <= 0.01 * stats[n + "_n"], n
+        assert stats[n + "_alpha_dev"] <= 1e-5, n
+        assert stats[n + "_delta_flips"] <= 0.005 * g[n + "_a_delta"].size, n
+        assert stats[n + "_beta_dev"] <= 1e-4, n
+        assert stats[n + "_hard_flips"] <= 0.002 * stats[n + "_n"], n
 
 
 # ------------------------------------------------------------------ §8(f) row 1: feature cache
@@ -273,7 +278,7 @@ def test_feature_cache_matches_reference(Q, golden):
         stats[key] = np.abs(x - ref).max() / np.abs(ref).max()
     parity_report("f1_feature_cache", **stats)
     for k, v in stats.items():
-        assert v <= 1e-5, (k, v)
+        assert v <= 1e-5, (k, v)   # observed (r2) <= 5e-7
     assert all(t.is_cuda for t in b1.cached_inp_features)
 
 
@@ -315,15 +320,17 @@ def test_fused_driver_flow_matches_reference(Q, golden):
         logits = host(qnn(cali))
     stats["logits_rel_err"] = np.abs(logits - g["logits"]).max() / np.abs(g["logits"]).max()
     parity_report("a23_fused_driver", **stats)
+    # observed (r2): cache / loss / logits rel errors <= 3e-7, 0 hard flips; alpha rows
+    # off by up to 4e-3 are the zero-gradient ones (+-lr random walk, bounded by 2*iters*lr)
     for k in (0, 1):
-        assert stats[f"b{k}_cache_rel_err"] <= 1e-4
-        assert stats[f"b{k}_loss_rel_err"] <= 5e-3
+        assert stats[f"b{k}_cache_rel_err"] <= 1e-5
+        assert stats[f"b{k}_loss_rel_err"] <= 1e-5
     for key, v in stats.items():
         if key.endswith("alpha_dev"):
             assert v <= iters * 2e-3, key
         if key.endswith("hard_flips"):
-            assert v <= 0.01 * g[key.replace("hard_flips", "what_hard")].size, key
-    assert stats["logits_rel_err"] <= 1e-2
+            assert v <= 0.002 * g[key.replace("hard_flips", "what_hard")].size, key
+    assert stats["logits_rel_err"] <= 1e-5
 
 
 @pytest.mark.parametrize("level", [1, 8, 64])
@@ -353,4 +360,4 @@ def test_wmse_driver_matches_reference(Q, golden, level):
         logits = host(qnn(cali))
     err = np.abs(logits - g[f"l{level}_logits"]).max() / np.abs(g[f"l{level}_logits"]).max()
     parity_report(f"a23_wmse_l{level}", logits_rel_err=err)
-    assert err <= 1e-4
+    assert err <= 1e-5             # observed (r2) <= 2.1e-7

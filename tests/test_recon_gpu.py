@@ -28,6 +28,18 @@ def dev(a):
     return torch.as_tensor(np.asarray(a)).cuda()
 
 
+def parity_report(test, **stats):
+    """Print the reached parity and append it to $SSQ_PARITY_LOG (jsonl) when set."""
+    import json
+    import os
+    rec = {"test": test, **{k: float(v) for k, v in stats.items()}}
+    print("PARITY", json.dumps(rec))
+    path = os.environ.get("SSQ_PARITY_LOG")
+    if path:
+        with open(path, "a") as f:
+            f.write(json.dumps(rec) + "\n")
+
+
 @pytest.fixture(params=["never", "always"])
 def wgrad(request):
     """Conv weight gradients from MIOpen ('never') or from K17 ssq_conv_wgrad ('always')."""
@@ -118,6 +130,8 @@ def test_block_recon_fused_matches_reference(Q, golden, graph, wgrad):
     # identical batches (same CPU RNG stream as the reference)
     np.testing.assert_array_equal(np.stack([p.numpy() for p in seen_perms]), g["perms"])
     rec = np.array(seen_rec)
+    stats = {"rec_rel_err": np.max(np.abs(rec - g["rec_loss"][:iters]) / np.abs(g["rec_loss"][:iters])),
+             "final_rel_err": np.max(np.abs(np.array(res) - g["final_losses"]) / np.abs(g["final_losses"]))}
     np.testing.assert_allclose(rec, g["rec_loss"][:iters], rtol=2e-4)
     np.testing.assert_allclose(res, g["final_losses"], rtol=5e-3)
     for n in ("conv1", "conv2", "downsample"):
@@ -132,13 +146,17 @@ def test_block_recon_fused_matches_reference(Q, golden, graph, wgrad):
         fl = np.stack(R.shift_floors(w, g[n + "_delta"].reshape(-1, 1, 1, 1), SHIFTS))
         degenerate = np.all(fl == fl[:1], axis=(0, 1, 3, 4))          # per input channel
         da = np.abs(q.alpha.detach().cpu().numpy() - g[n + "_alpha"])
+        stats[n + "_alpha_dev"] = da[~degenerate].max()
+        stats[n + "_alpha_dev_degenerate"] = da[degenerate].max(initial=0.0)
         assert da[~degenerate].max() <= 2e-4, (n, da[~degenerate].max())
         assert da[degenerate].max(initial=0.0) <= 30 * 1e-3 * 2, n      # <= iters * 2 lr
         np.testing.assert_allclose(q.beta.detach().cpu().numpy(), g[n + "_beta0"], rtol=1e-5, atol=1e-5)
         with torch.no_grad():
             what = q(getattr(block, n).weight).cpu().numpy()
+        stats[n + "_hard_flips"] = np.sum(what != g[n + "_what_hard"])
         mism = np.mean(what != g[n + "_what_hard"])
         assert mism <= 0.01, f"{n}: {mism:.4f} of hard weights differ"
+    parity_report(f"a18_block_recon_fused[graph={graph},wgrad={wgrad}]", **stats)
 
 
 def test_layer_recon_shiftedScale_matches_reference(Q, golden):
@@ -160,12 +178,18 @@ def test_layer_recon_shiftedScale_matches_reference(Q, golden):
     iters = int(g["iters"][0])
     torch.manual_seed(1005)
     l1 = Q.layer_recon_shiftedScale(m, iters, 0.1, qnn, None, verbose=False)
+    stats = {"shift_final_rel_err": np.max(np.abs(np.array(l1) - g["shift_final"]) / np.abs(g["shift_final"])),
+             "shift_alpha_dev": np.abs(m.weight_quantizer.alpha.detach().cpu().numpy() - g["shift_alpha"]).max()}
     np.testing.assert_allclose(l1, g["shift_final"], rtol=5e-3)
     np.testing.assert_allclose(m.weight_quantizer.alpha.detach().cpu().numpy(), g["shift_alpha"], atol=2e-4)
     m.weight_quantizer.hard_targets = False
     l2 = Q.layer_recon_shiftedScale(m, iters, 0.01, qnn, None, adaround=True, verbose=False)
     np.testing.assert_allclose(l2, g["ar_final"], rtol=5e-3)
     d = m.weight_quantizer.delta.detach().cpu().numpy()
+    stats["ar_final_rel_err"] = np.max(np.abs(np.array(l2) - g["ar_final"]) / np.abs(g["ar_final"]))
+    stats["ar_delta_flips"] = np.sum(d != g["ar_delta"])
+    stats["ar_beta_dev"] = np.abs(m.weight_quantizer.beta.detach().cpu().numpy() - g["ar_beta"]).max()
+    parity_report("a20_layer_recon_shiftedScale", **stats)
     assert np.mean(d != g["ar_delta"]) <= 0.02
     np.testing.assert_allclose(m.weight_quantizer.beta.detach().cpu().numpy(), g["ar_beta"], atol=5e-3)
 
@@ -198,12 +222,16 @@ def test_brecq_block_reconstruction_matches_reference(Q, golden, graph, wgrad):
         Q.block_reconstruction(qnn, block, cali, batch_size=8, iters=len(g["w_total_loss"]),
                                weight=0.01, asym=True, b_range=(20, 2), warmup=0.2,
                                act_quant=False, opt_mode="mse")
+        stats = {"w_total_rel_err": np.max(np.abs(np.array(seen) - g["w_total_loss"]) /
+                                           np.abs(g["w_total_loss"]))}
         np.testing.assert_allclose(seen, g["w_total_loss"], rtol=2e-4)
         for n in ("conv1", "conv2", "downsample"):
             q = getattr(block, n).weight_quantizer
+            stats[n + "_V_dev"] = np.abs(q.alpha.detach().cpu().numpy() - g[n + "_alpha"]).max()
             np.testing.assert_allclose(q.alpha.detach().cpu().numpy(), g[n + "_alpha"], atol=1e-4)
             with torch.no_grad():
                 what = q(getattr(block, n).weight).cpu().numpy()
+            stats[n + "_hard_flips"] = np.sum(what != g[n + "_what_hard"])
             assert np.mean(what != g[n + "_what_hard"]) <= 0.002
         # act phase
         qnn.set_quant_state(True, True)
@@ -217,6 +245,10 @@ def test_brecq_block_reconstruction_matches_reference(Q, golden, graph, wgrad):
         torch.manual_seed(1005)
         Q.block_reconstruction(qnn, block, cali, batch_size=8, iters=len(g["a_total_loss"]),
                                act_quant=True, opt_mode="mse", lr=4e-4, p=2.4)
+        stats["a_total_rel_err"] = np.max(np.abs(np.array(seen) - g["a_total_loss"]) / np.abs(g["a_total_loss"]))
+        stats["a_delta_rel_err"] = np.max(np.abs(np.array([float(q.delta) for q in aqs]) - g["a_delta"]) /
+                                          np.abs(g["a_delta"]))
+        parity_report(f"a22_brecq_basic[graph={graph},wgrad={wgrad}]", **stats)
         np.testing.assert_allclose(seen, g["a_total_loss"], rtol=1e-4)
         np.testing.assert_allclose([float(q.delta) for q in aqs], g["a_delta"], rtol=1e-5)
     finally:
@@ -300,6 +332,9 @@ def test_fused_recon_other_blocks_match_reference(Q, golden, kind):
     finally:
         LRF.BatchFeeder.draw, LRF.FusedScaleLossFunction.bookkeep = orig_draw, orig_keep
     np.testing.assert_array_equal(np.stack([p.numpy() for p in seen_perms]), g["f_perms"])
+    stats = {"rec_rel_err": np.max(np.abs(np.array(seen_rec) - g["f_rec_loss"][:iters]) /
+                                   np.abs(g["f_rec_loss"][:iters])),
+             "final_rel_err": np.max(np.abs(np.array(res) - g["f_final_losses"]) / np.abs(g["f_final_losses"]))}
     np.testing.assert_allclose(seen_rec, g["f_rec_loss"][:iters], rtol=2e-4)
     np.testing.assert_allclose(res, g["f_final_losses"], rtol=5e-3)
     from oracle import ssq_ref as R
@@ -315,11 +350,17 @@ def test_fused_recon_other_blocks_match_reference(Q, golden, kind):
         # least one) may take such a walk, bounded by iters * 2 * lr; every other row
         # follows the reference trajectory to 2e-4.
         off = ~degenerate & (da.max(axis=-1) > 2e-4)
+        stats[n + "_walking_rows"] = off.sum()
+        stats[n + "_rows"] = off.size
+        stats[n + "_alpha_dev_other"] = da[~degenerate & ~off].max(initial=0.0)
         assert off.sum() <= max(1, round(0.1 * off.size)), (n, np.nonzero(off)[0], da.max())
         assert da.max(initial=0.0) <= iters * 1e-3 * 2, n
         with torch.no_grad():
             what = q(m.weight).cpu().numpy()
+        stats[n + "_hard_flips"] = np.sum(what != g[f"f_{n}_what_hard"])
+        stats[n + "_n"] = what.size
         assert np.mean(what != g[f"f_{n}_what_hard"]) <= 0.01, n
+    parity_report(f"a18_fused_{kind}", **stats)
 
 
 @pytest.mark.parametrize("kind", ["bottleneck", "inverted", "resbottleneck"])
@@ -356,10 +397,14 @@ def test_brecq_other_blocks_match_reference(Q, golden, kind):
                                asym=True, b_range=(20, 2), warmup=0.2, act_quant=False, opt_mode="mse")
     finally:
         BR.LossFunction.record, BR.LossFunction.__init__ = orig_rec, orig_init
+    stats = {"total_rel_err": np.max(np.abs(np.array(seen) - g["b_total_loss"]) / np.abs(g["b_total_loss"]))}
     np.testing.assert_allclose(seen, g["b_total_loss"], rtol=2e-4)
     for n, m in named_qms(block, Q):
         q = m.weight_quantizer
+        stats[n + "_V_dev"] = np.abs(q.alpha.detach().cpu().numpy() - g[f"b_{n}_alpha"]).max()
         np.testing.assert_allclose(q.alpha.detach().cpu().numpy(), g[f"b_{n}_alpha"], atol=1e-4, err_msg=n)
         with torch.no_grad():
             what = q(m.weight).cpu().numpy()
+        stats[n + "_hard_flips"] = np.sum(what != g[f"b_{n}_what_hard"])
         assert np.mean(what != g[f"b_{n}_what_hard"]) <= 0.002, n
+    parity_report(f"a22_brecq_{kind}", **stats)
