@@ -11,8 +11,9 @@ One step (configs[1], ResNet-18 W2A4, 1024 calibration samples, synthetic data) 
     stem/head) in ONE multi-tensor launch.
 value = elements processed by all ranks / max-over-ranks wall time (Gelem/s, weak
 scaling: every rank owns its own calibration shard; no data-path collective).
-The reconstruction iteration rate (block_recon_fused_shiftedScale, batch 32) is
-reported beside it as `recon`.
+The reconstruction iteration rate (block_recon_fused_shiftedScale, batch 32, bias_cal, every
+ResNet-18 block, reference-faithful deterministic conv solvers as the headline) is reported
+beside it as `recon`, with its SURVEY §8(d) roofline as `roofline_recon`.
 """
 import argparse
 import json
@@ -51,7 +52,7 @@ def parse():
     p.add_argument("--warmup", type=int, default=5)
     p.add_argument("--n-cali", type=int, default=1024)
     p.add_argument("--no-cpu-baseline", action="store_true")
-    p.add_argument("--cpu-seconds", type=float, default=10.0)
+    p.add_argument("--cpu-seconds", type=float, default=15.0)
     p.add_argument("--no-recon", action="store_true")
     p.add_argument("--recon-iters", type=int, default=200)
     p.add_argument("--variant", type=int, default=-1, help="streaming cache policy A/B")
@@ -138,26 +139,69 @@ def time_events(fn, reps, dev, rounds=5):
     return sorted(times)[len(times) // 2]
 
 
-def cpu_baseline(act_dev, d_a, z_a, seconds):
-    """The plain-C oracle (scalar port, 1 thread) on a bounded sample of the same
-    workload: the first 16 calibration samples of the activation cache, repeated for
-    about `seconds` of CPU time."""
-    from oracle import c_oracle
-    sample = act_dev[:16].cpu().numpy()
-    d, z = d_a.cpu().numpy(), z_a.cpu().numpy()
-    c_oracle.fake_quant(sample[:1], d, z, 4)  # load / warm
+def host_cores():
+    """The host CPU share this process may use: OMP_NUM_THREADS when the box sets it (its
+    per-GPU share), else the affinity mask."""
+    env = int(os.environ.get("OMP_NUM_THREADS", "0") or 0)
+    return env if env > 0 else len(os.sched_getaffinity(0))
+
+
+def _timed(fn, seconds, min_reps=2):
+    fn()  # warm
     n, t0 = 0, time.perf_counter()
     while True:
-        c_oracle.fake_quant(sample, d, z, 4)
+        fn()
         n += 1
         el = time.perf_counter() - t0
-        if el >= seconds:
-            break
-    return {"value": round(n * sample.size / el / 1e9, 4), "unit": "Gelem/s", "cores": 1,
-            "kind": "port",
-            "sample": f"oracle/c ssqo_fake_quant, A4 per-tensor q/dq of act[:16] "
-                      f"({sample.size} elems) x{n} reps, {el:.1f}s, 1 thread, "
-                      f"{os.cpu_count()} host CPUs visible"}
+        if el >= seconds and n >= min_reps:
+            return n, el
+
+
+def cpu_baseline(act_dev, d_a, z_a, seconds, recon_state=None):
+    """The CPU ports on the GPU box's host cores, on bounded samples of the same workload:
+    * q/dq: the plain-C oracle (oracle/c, scalar) on act[:64] (12.8 M elements), 1 thread
+      and all cores (the sample split into one contiguous slice per thread; ctypes releases
+      the GIL);
+    * recon: oracle/recon_cpu.FusedBlockReconCPU -- the reference's fused iteration in
+      PyTorch-CPU ops, pinned to the reference trajectory by tests/test_oracle.py -- on
+      ResNet-18 layer1.0 (batch 32 from 64 cached samples, bias_cal), all cores."""
+    import concurrent.futures as cf
+
+    import numpy as np
+    from oracle import c_oracle
+    cores = host_cores()
+    sample = act_dev[:64].cpu().numpy()
+    d, z = d_a.cpu().numpy(), z_a.cpu().numpy()
+    c_oracle.fake_quant(sample[:1], d, z, 4)  # load / warm
+    n1, el1 = _timed(lambda: c_oracle.fake_quant(sample, d, z, 4), seconds / 3)
+    flat = sample.reshape(-1)
+    slices = np.array_split(flat, cores)
+    pool = cf.ThreadPoolExecutor(max_workers=cores)
+
+    def all_cores():
+        list(pool.map(lambda x: c_oracle.fake_quant(x, d, z, 4), slices))
+
+    nN, elN = _timed(all_cores, seconds / 3)
+    pool.shutdown()
+    out = {"value": round(nN * sample.size / elN / 1e9, 4), "unit": "Gelem/s", "cores": cores,
+           "kind": "port",
+           "sample": f"q/dq: oracle/c ssqo_fake_quant (scalar C port of quant_layer.py:92-98), "
+                     f"A4 per-tensor q/dq of act[:64] ({sample.size} elems) x{nN} reps in "
+                     f"{elN:.1f}s on {cores} threads; {os.cpu_count()} host CPUs visible",
+           "qdq_1thread_gelem_s": round(n1 * sample.size / el1 / 1e9, 4)}
+    if recon_state is not None:
+        import torch
+        from oracle.recon_cpu import FusedBlockReconCPU
+        torch.set_num_threads(cores)
+        torch.manual_seed(1005)
+        rc = FusedBlockReconCPU(recon_state["convs"], [31 / 32, 33 / 32, 1.0], 2, recon_state["inp"],
+                                recon_state["out"], 625, bias_cal=True)
+        nr, elr = _timed(rc.step, seconds / 3, min_reps=3)
+        out["recon_iters_per_s"] = round(nr / elr, 3)
+        out["recon_sample"] = (f"oracle/recon_cpu.FusedBlockReconCPU, ResNet-18 layer1.0 W2 S=3 "
+                               f"bias_cal, batch 32 of 64 cached samples, {nr} iterations in "
+                               f"{elr:.1f}s on {cores} torch threads")
+    return out
 
 
 def main():
@@ -220,12 +264,13 @@ def main():
     del big, y_big
 
     recon = None
+    recon_state = None
     if not args.no_recon:
-        try:
-            from shiftedscalequantization_amd.recon_bench import run_recon_bench
-            recon = run_recon_bench(dev, world, rank, iters=args.recon_iters)
-        except ImportError:
-            recon = None
+        from shiftedscalequantization_amd.recon_bench import run_recon_bench
+        want_cpu = world == 1 and rank == 0 and not args.no_cpu_baseline
+        recon = run_recon_bench(dev, world, rank, iters=args.recon_iters,
+                                cpu_sample=64 if want_cpu else 0)
+        recon_state = recon.pop("_cpu_state", None)
 
     out = {
         "metric": "Gelem/s shifted-scale q/dq + recon iters/s, ResNet-18 W2A4; top-1 vs ref",
@@ -261,9 +306,10 @@ def main():
                                  "frac": round(pc_gbs / HBM_PEAK_GBS, 4), "kernel_ms": round(ms_pc, 4)},
     }
     if recon is not None:
+        out["roofline_recon"] = recon.pop("roofline_recon")
         out["recon"] = recon
     if world == 1 and rank == 0 and not args.no_cpu_baseline:
-        out["cpu_baseline"] = cpu_baseline(act, d_a, z_a, args.cpu_seconds)
+        out["cpu_baseline"] = cpu_baseline(act, d_a, z_a, args.cpu_seconds, recon_state)
     if rank == 0:
         print(json.dumps(out), flush=True)
     if world > 1:

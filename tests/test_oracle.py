@@ -202,3 +202,31 @@ def test_schedules(golden):
         assert R.linear_temp_decay(t, 75.0, guard_zero=True) == g["sched_fused_shift"][t]
         assert R.linear_temp_decay(t, 100) == g["sched_lin"][t]
         assert R.linear_temp_decay(t, 100) == g["sched_lsh"][t]
+
+
+def test_recon_cpu_restatement_matches_reference_trajectory(golden):
+    """oracle/recon_cpu.py (the CPU restatement bench.py times as the recon cpu_baseline)
+    reproduces the reference's own 30-iteration block_recon_fused_shiftedScale run: the
+    same batches, per-iteration reconstruction losses and final alphas."""
+    import torch
+    from oracle.recon_cpu import FusedBlockReconCPU
+    g = golden("recon_fused")
+    t = lambda a: torch.as_tensor(np.asarray(a))   # noqa: E731
+    convs = {"conv1": (t(g["conv1_w"]), t(g["conv1_b"]), t(g["conv1_delta"]), t(g["conv1_zp"]), 2, 1),
+             "conv2": (t(g["conv2_w"]), t(g["conv2_b"]), t(g["conv2_delta"]), t(g["conv2_zp"]), 1, 1),
+             "downsample": (t(g["downsample_w"]), t(g["downsample_b"]), t(g["downsample_delta"]),
+                            t(g["downsample_zp"]), 2, 0)}
+    iters = int(g["iters"][0])
+    torch.manual_seed(1005)
+    rc = FusedBlockReconCPU(convs, [31 / 32, 33 / 32, 1.0], 2, t(g["cached_inp"]), t(g["cached_out"]),
+                            iters)
+    rec = [rc.step() for _ in range(iters)]
+    np.testing.assert_allclose(rec, g["rec_loss"][:iters], rtol=1e-5)
+    for n in ("conv1", "conv2", "downsample"):
+        # rows whose shift candidates are all equal have a zero analytic gradient: Adam turns
+        # summation-order noise into +-lr steps there (in the reference too), bounded below
+        fl = torch.stack(rc.convs[n].floors).numpy()
+        degenerate = np.all(fl == fl[:1], axis=(0, 1, 3, 4))
+        da = np.abs(rc.convs[n].alpha.detach().numpy() - g[n + "_alpha"])
+        assert da[~degenerate].max() <= 1e-5, (n, da[~degenerate].max())
+        assert da.max() <= iters * 2e-3, n

@@ -132,8 +132,9 @@ def test_block_recon_fused_matches_reference(Q, golden, graph, wgrad):
     rec = np.array(seen_rec)
     stats = {"rec_rel_err": np.max(np.abs(rec - g["rec_loss"][:iters]) / np.abs(g["rec_loss"][:iters])),
              "final_rel_err": np.max(np.abs(np.array(res) - g["final_losses"]) / np.abs(g["final_losses"]))}
-    np.testing.assert_allclose(rec, g["rec_loss"][:iters], rtol=2e-4)
-    np.testing.assert_allclose(res, g["final_losses"], rtol=5e-3)
+    # observed (r2, MI355X): rec / final rel err <= 8e-7, alpha dev <= 5e-7, 0 hard flips
+    np.testing.assert_allclose(rec, g["rec_loss"][:iters], rtol=1e-5)
+    np.testing.assert_allclose(res, g["final_losses"], rtol=1e-5)
     for n in ("conv1", "conv2", "downsample"):
         q = getattr(block, n).weight_quantizer
         # Input channels whose shift candidates are all identical (floor(W/(d*s_i)) equal
@@ -148,14 +149,14 @@ def test_block_recon_fused_matches_reference(Q, golden, graph, wgrad):
         da = np.abs(q.alpha.detach().cpu().numpy() - g[n + "_alpha"])
         stats[n + "_alpha_dev"] = da[~degenerate].max()
         stats[n + "_alpha_dev_degenerate"] = da[degenerate].max(initial=0.0)
-        assert da[~degenerate].max() <= 2e-4, (n, da[~degenerate].max())
+        assert da[~degenerate].max() <= 1e-5, (n, da[~degenerate].max())
         assert da[degenerate].max(initial=0.0) <= 30 * 1e-3 * 2, n      # <= iters * 2 lr
         np.testing.assert_allclose(q.beta.detach().cpu().numpy(), g[n + "_beta0"], rtol=1e-5, atol=1e-5)
         with torch.no_grad():
             what = q(getattr(block, n).weight).cpu().numpy()
         stats[n + "_hard_flips"] = np.sum(what != g[n + "_what_hard"])
         mism = np.mean(what != g[n + "_what_hard"])
-        assert mism <= 0.01, f"{n}: {mism:.4f} of hard weights differ"
+        assert mism <= 0.002, f"{n}: {mism:.4f} of hard weights differ"
     parity_report(f"a18_block_recon_fused[graph={graph},wgrad={wgrad}]", **stats)
 
 
@@ -180,18 +181,19 @@ def test_layer_recon_shiftedScale_matches_reference(Q, golden):
     l1 = Q.layer_recon_shiftedScale(m, iters, 0.1, qnn, None, verbose=False)
     stats = {"shift_final_rel_err": np.max(np.abs(np.array(l1) - g["shift_final"]) / np.abs(g["shift_final"])),
              "shift_alpha_dev": np.abs(m.weight_quantizer.alpha.detach().cpu().numpy() - g["shift_alpha"]).max()}
-    np.testing.assert_allclose(l1, g["shift_final"], rtol=5e-3)
-    np.testing.assert_allclose(m.weight_quantizer.alpha.detach().cpu().numpy(), g["shift_alpha"], atol=2e-4)
+    # observed (r2): final rel err <= 5e-7, alpha dev 4.4e-7, 0 delta flips, beta dev 2.4e-4
+    np.testing.assert_allclose(l1, g["shift_final"], rtol=1e-5)
+    np.testing.assert_allclose(m.weight_quantizer.alpha.detach().cpu().numpy(), g["shift_alpha"], atol=1e-5)
     m.weight_quantizer.hard_targets = False
     l2 = Q.layer_recon_shiftedScale(m, iters, 0.01, qnn, None, adaround=True, verbose=False)
-    np.testing.assert_allclose(l2, g["ar_final"], rtol=5e-3)
+    np.testing.assert_allclose(l2, g["ar_final"], rtol=1e-5)
     d = m.weight_quantizer.delta.detach().cpu().numpy()
     stats["ar_final_rel_err"] = np.max(np.abs(np.array(l2) - g["ar_final"]) / np.abs(g["ar_final"]))
     stats["ar_delta_flips"] = np.sum(d != g["ar_delta"])
     stats["ar_beta_dev"] = np.abs(m.weight_quantizer.beta.detach().cpu().numpy() - g["ar_beta"]).max()
     parity_report("a20_layer_recon_shiftedScale", **stats)
-    assert np.mean(d != g["ar_delta"]) <= 0.02
-    np.testing.assert_allclose(m.weight_quantizer.beta.detach().cpu().numpy(), g["ar_beta"], atol=5e-3)
+    assert np.mean(d != g["ar_delta"]) <= 0.005
+    np.testing.assert_allclose(m.weight_quantizer.beta.detach().cpu().numpy(), g["ar_beta"], atol=1e-3)
 
 
 @pytest.mark.parametrize("graph", [False, True])
@@ -224,11 +226,12 @@ def test_brecq_block_reconstruction_matches_reference(Q, golden, graph, wgrad):
                                act_quant=False, opt_mode="mse")
         stats = {"w_total_rel_err": np.max(np.abs(np.array(seen) - g["w_total_loss"]) /
                                            np.abs(g["w_total_loss"]))}
-        np.testing.assert_allclose(seen, g["w_total_loss"], rtol=2e-4)
+        # observed (r2): total rel err <= 6.2e-7, V dev <= 4.7e-7, 0 flips, act delta 2e-7
+        np.testing.assert_allclose(seen, g["w_total_loss"], rtol=1e-5)
         for n in ("conv1", "conv2", "downsample"):
             q = getattr(block, n).weight_quantizer
             stats[n + "_V_dev"] = np.abs(q.alpha.detach().cpu().numpy() - g[n + "_alpha"]).max()
-            np.testing.assert_allclose(q.alpha.detach().cpu().numpy(), g[n + "_alpha"], atol=1e-4)
+            np.testing.assert_allclose(q.alpha.detach().cpu().numpy(), g[n + "_alpha"], atol=1e-5)
             with torch.no_grad():
                 what = q(getattr(block, n).weight).cpu().numpy()
             stats[n + "_hard_flips"] = np.sum(what != g[n + "_what_hard"])
@@ -249,8 +252,8 @@ def test_brecq_block_reconstruction_matches_reference(Q, golden, graph, wgrad):
         stats["a_delta_rel_err"] = np.max(np.abs(np.array([float(q.delta) for q in aqs]) - g["a_delta"]) /
                                           np.abs(g["a_delta"]))
         parity_report(f"a22_brecq_basic[graph={graph},wgrad={wgrad}]", **stats)
-        np.testing.assert_allclose(seen, g["a_total_loss"], rtol=1e-4)
-        np.testing.assert_allclose([float(q.delta) for q in aqs], g["a_delta"], rtol=1e-5)
+        np.testing.assert_allclose(seen, g["a_total_loss"], rtol=1e-5)
+        np.testing.assert_allclose([float(q.delta) for q in aqs], g["a_delta"], rtol=5e-6)
     finally:
         BR.LossFunction.record, BR.LossFunction.__init__ = orig_rec, orig_init
         BR._fast_loop = orig_fast
@@ -335,8 +338,9 @@ def test_fused_recon_other_blocks_match_reference(Q, golden, kind):
     stats = {"rec_rel_err": np.max(np.abs(np.array(seen_rec) - g["f_rec_loss"][:iters]) /
                                    np.abs(g["f_rec_loss"][:iters])),
              "final_rel_err": np.max(np.abs(np.array(res) - g["f_final_losses"]) / np.abs(g["f_final_losses"]))}
-    np.testing.assert_allclose(seen_rec, g["f_rec_loss"][:iters], rtol=2e-4)
-    np.testing.assert_allclose(res, g["f_final_losses"], rtol=5e-3)
+    # observed (r2): rel errs <= 6.4e-7, non-walking alpha rows <= 7.3e-6, 0 hard flips
+    np.testing.assert_allclose(seen_rec, g["f_rec_loss"][:iters], rtol=1e-5)
+    np.testing.assert_allclose(res, g["f_final_losses"], rtol=1e-5)
     from oracle import ssq_ref as R
     for n, m in named_qms(block, Q):
         q = m.weight_quantizer
@@ -359,7 +363,8 @@ def test_fused_recon_other_blocks_match_reference(Q, golden, kind):
             what = q(m.weight).cpu().numpy()
         stats[n + "_hard_flips"] = np.sum(what != g[f"f_{n}_what_hard"])
         stats[n + "_n"] = what.size
-        assert np.mean(what != g[f"f_{n}_what_hard"]) <= 0.01, n
+        assert stats[n + "_alpha_dev_other"] <= 5e-5, n
+        assert np.mean(what != g[f"f_{n}_what_hard"]) <= 0.002, n
     parity_report(f"a18_fused_{kind}", **stats)
 
 
@@ -398,11 +403,11 @@ def test_brecq_other_blocks_match_reference(Q, golden, kind):
     finally:
         BR.LossFunction.record, BR.LossFunction.__init__ = orig_rec, orig_init
     stats = {"total_rel_err": np.max(np.abs(np.array(seen) - g["b_total_loss"]) / np.abs(g["b_total_loss"]))}
-    np.testing.assert_allclose(seen, g["b_total_loss"], rtol=2e-4)
+    np.testing.assert_allclose(seen, g["b_total_loss"], rtol=1e-5)      # observed <= 1.6e-7
     for n, m in named_qms(block, Q):
         q = m.weight_quantizer
         stats[n + "_V_dev"] = np.abs(q.alpha.detach().cpu().numpy() - g[f"b_{n}_alpha"]).max()
-        np.testing.assert_allclose(q.alpha.detach().cpu().numpy(), g[f"b_{n}_alpha"], atol=1e-4, err_msg=n)
+        np.testing.assert_allclose(q.alpha.detach().cpu().numpy(), g[f"b_{n}_alpha"], atol=1e-5, err_msg=n)
         with torch.no_grad():
             what = q(m.weight).cpu().numpy()
         stats[n + "_hard_flips"] = np.sum(what != g[f"b_{n}_what_hard"])
