@@ -15,6 +15,8 @@
 // Same inputs -> same bits, run to run (no atomics).  Within tolerance of any other
 // summation order (the MIOpen / CPU results), like every fp32 convolution gradient.
 // Depthwise convs take a separate bandwidth-bound reduction (wgrad_dw_stage1).
+#include <stdlib.h>
+
 #include <algorithm>
 
 #include "ssq_common.h"
@@ -221,6 +223,137 @@ __global__ __launch_bounds__(256, 1) void wgrad_stage1(const float* __restrict__
   }
 }
 
+// ------------------------------------------------------------------ 1x1 convolutions
+// A 1x1 conv's weight gradient is a plain GEMM, dW[co, ci] = sum_(n, p) dy[n, co, p] *
+// x[n, ci, src(p)], src(p) = (p / OW) * st * W + (p % OW) * st: no window, so instead of the
+// R x S input-row tile both operands are staged the same way -- per chunk of Pq1 output
+// pixels of one sample, A[co][k] = dy rows (contiguous) and B[ci][k] = x at src(p) (a
+// strided gather for stride 2), LDS-DMA'd 4 B per lane into two buffers.  Waves tile the
+// workgroup's TM x TN block as 64 x 64 (2 x 2 v_mfma_f32_32x32x2_f32 accumulators, exact
+// fp32); lane half h walks pixels h*Pq1/2 + t of the chunk (the MFMA's k = h), so both
+// operands are read with the same conflict-free pitch.  Splits over chunks, summed in a
+// fixed order by wgrad_stage2: deterministic.  (The R x S kernel's x tile needs
+// ci_span * in_rows * W floats; at 56x56 stride 2 that overflows the LDS.)
+constexpr int kPq1 = 64;
+constexpr int kLd1 = kPq1 + 1;     // odd pitch: row r, column c -> bank (r + c) mod 32-ish
+
+struct W1Geo {
+  int Nb, C, HW, W, Co, OW, OHW, st, G, Cig, Cog;
+  int WM, m_tiles, n_tiles, chunks_per_n, nchunks, cps, nsplit;
+  FastDiv dOW;
+};
+
+template <int WM>
+__global__ __launch_bounds__(256) void wgrad_1x1_stage1(const float* __restrict__ x,
+                                                        const float* __restrict__ dy, W1Geo g,
+                                                        float* __restrict__ part) {
+  constexpr int WN = 4 / WM, TM = 64 * WM, TN = 64 * WN;
+  __shared__ float lds[2 * (TM + TN) * kLd1];
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wm = wave / WN, wn = wave - wm * WN;
+  const int grp = blockIdx.y / g.m_tiles, mt = blockIdx.y - grp * g.m_tiles;
+  const int co0 = mt * TM, ci0 = blockIdx.x * TN;
+  const int rows_a = min(TM, g.Cog - co0), rows_b = min(TN, g.Cig - ci0);
+  const int c_begin = blockIdx.z * g.cps, c_end = min(c_begin + g.cps, g.nchunks);
+  // buffer b: A = lds + b*(TM+TN)*kLd1 [TM][kLd1], B right after it [TN][kLd1]
+  auto Abuf = [&](int b) { return lds + b * (TM + TN) * kLd1; };
+  auto Bbuf = [&](int b) { return lds + b * (TM + TN) * kLd1 + TM * kLd1; };
+  // rows past the channel ranges stay zero (their products are discarded anyway)
+  for (int i = tid; i < 2 * (TM + TN) * kLd1; i += 256) lds[i] = 0.0f;
+  __syncthreads();
+
+  auto stage = [&](int c, int b) {
+    const int n = c / g.chunks_per_n;
+    const int p0 = (c - n * g.chunks_per_n) * kPq1;
+    const int P = min(kPq1, g.OHW - p0);
+    const int k = lane;
+    const float* sa = dy + ((int64_t)n * g.Co + (int64_t)grp * g.Cog + co0) * g.OHW + p0;
+    for (int r = wave; r < rows_a; r += 4) {
+      if (k < P)
+        __builtin_amdgcn_global_load_lds((const void*)(sa + (int64_t)r * g.OHW + k),
+                                         (void*)(Abuf(b) + r * kLd1), 4, 0, 0);
+      else
+        Abuf(b)[r * kLd1 + k] = 0.0f;
+    }
+    const int p = p0 + k;
+    const int oh = (int)fdiv((uint32_t)p, g.dOW), ow = p - oh * g.OW;
+    const int src = oh * g.st * g.W + ow * g.st;
+    const float* sb = x + ((int64_t)n * g.C + (int64_t)grp * g.Cig + ci0) * g.HW + src;
+    for (int r = wave; r < rows_b; r += 4) {
+      if (k < P)
+        __builtin_amdgcn_global_load_lds((const void*)(sb + (int64_t)r * g.HW),
+                                         (void*)(Bbuf(b) + r * kLd1), 4, 0, 0);
+      else
+        Bbuf(b)[r * kLd1 + k] = 0.0f;
+    }
+  };
+
+  f32x16 acc00 = {0}, acc01 = {0}, acc10 = {0}, acc11 = {0};
+  const int ar = (wm * 64 + (lane & 31)) * kLd1, br = (wn * 64 + (lane & 31)) * kLd1;
+  const int kh = (lane >> 5) * (kPq1 / 2);
+  if (c_begin < c_end) stage(c_begin, 0);
+  for (int c = c_begin; c < c_end; ++c) {
+    const int b = (c - c_begin) & 1;
+    asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+    __syncthreads();                  // chunk c staged; chunk c-1's reads of buffer b^1 done
+    if (c + 1 < c_end) stage(c + 1, b ^ 1);
+    const float* A = Abuf(b);
+    const float* B = Bbuf(b);
+#pragma unroll 4
+    for (int t = 0; t < kPq1 / 2; ++t) {
+      const float a0 = A[ar + kh + t], a1 = A[ar + 32 * kLd1 + kh + t];
+      const float b0 = B[br + kh + t], b1 = B[br + 32 * kLd1 + kh + t];
+      acc00 = __builtin_amdgcn_mfma_f32_32x32x2f32(a0, b0, acc00, 0, 0, 0);
+      acc01 = __builtin_amdgcn_mfma_f32_32x32x2f32(a0, b1, acc01, 0, 0, 0);
+      acc10 = __builtin_amdgcn_mfma_f32_32x32x2f32(a1, b0, acc10, 0, 0, 0);
+      acc11 = __builtin_amdgcn_mfma_f32_32x32x2f32(a1, b1, acc11, 0, 0, 0);
+    }
+  }
+  // C[row][col], row = (r&3) + 8*(r>>2) + 4*(lane>>5), col = lane&31 (as wgrad_stage1)
+  float* dst = part + ((int64_t)blockIdx.z * g.G + grp) * (int64_t)g.Cog * g.Cig;
+  const int wrow = co0 + wm * 64, wcol = ci0 + wn * 64;
+#pragma unroll
+  for (int t = 0; t < 4; ++t) {
+    const f32x16 acc = t == 0 ? acc00 : t == 1 ? acc01 : t == 2 ? acc10 : acc11;
+    const int col = wcol + 32 * (t & 1) + (lane & 31);
+    if (col >= g.Cig) continue;
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      const int row = wrow + 32 * (t >> 1) + (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5);
+      if (row < g.Cog) dst[(int64_t)row * g.Cig + col] = acc[r];
+    }
+  }
+}
+
+static int wgrad_1x1_plan(int64_t Nb, int64_t C, int64_t H, int64_t W, int64_t Co, int64_t st,
+                          int64_t G, W1Geo& g) {
+  SSQ_REQUIRE(Nb >= 1 && C >= 1 && H >= 1 && W >= 1 && Co >= 1 && st >= 1 && G >= 1 &&
+                  C % G == 0 && Co % G == 0,
+              SSQ_E_ARG, "ssq_conv_wgrad: bad geometry");
+  const int64_t OH = (H - 1) / st + 1, OW = (W - 1) / st + 1;
+  SSQ_REQUIRE(Nb * C * H * W < (1ll << 31) && Nb * Co * OH * OW < (1ll << 31), SSQ_E_ARG,
+              "ssq_conv_wgrad: sizes");
+  g.Nb = (int)Nb; g.C = (int)C; g.HW = (int)(H * W); g.W = (int)W; g.Co = (int)Co;
+  g.OW = (int)OW; g.OHW = (int)(OH * OW); g.st = (int)st; g.G = (int)G;
+  g.Cig = (int)(C / G); g.Cog = (int)(Co / G);
+  g.dOW = make_fastdiv((uint32_t)OW);
+  // 128 x 128 workgroup tile: its two (TM + TN) x kLd1 buffers (133 KB) fit the LDS,
+  // the 64 x 256 forms' do not
+  g.WM = 2;
+  const int TM = 64 * g.WM, TN = 256 / g.WM;
+  g.m_tiles = (g.Cog + TM - 1) / TM;
+  g.n_tiles = (g.Cig + TN - 1) / TN;
+  g.chunks_per_n = (g.OHW + kPq1 - 1) / kPq1;
+  g.nchunks = g.Nb * g.chunks_per_n;
+  const int64_t tiles = (int64_t)g.m_tiles * g.n_tiles * g.G;
+  // ~2 workgroups per CU over the grid, at least 4 chunks each
+  int nsplit = (int)std::max<int64_t>(1, std::min<int64_t>(g.nchunks / 4, (512 + tiles - 1) / tiles));
+  g.cps = (g.nchunks + nsplit - 1) / nsplit;
+  g.nsplit = (g.nchunks + g.cps - 1) / g.cps;
+  return SSQ_OK;
+}
+
 // dW = the splits summed in a fixed order: wave w of a workgroup sums its quarter of the
 // splits in split order (8 loads in flight per lane), then the four wave sums are added
 // in wave order.  Same bits run to run; 4x the parallelism of one thread per element.
@@ -366,6 +499,12 @@ static int wgrad_plan(int64_t Nb, int64_t C, int64_t H, int64_t W, int64_t Co, i
   // Candidate layouts WM = 1, 2, 4 (TM = 64 WM, TN = 256 / WM) x Pq = 128, 64, in MFMA
   // slots (64 cycles): every tile runs 2 MFMAs per pixel per wave, plus per chunk a fixed
   // ~40 and one slot per LDS-DMA instruction a wave issues (A rows + x rows, / 4 waves).
+  // A/B knob: SSQ_K17_MAXLDS caps the LDS tile (bytes) -- 80 KiB lets two workgroups share
+  // a CU (8 waves: twice the latency hiding of one)
+  static const int64_t max_lds = [] {
+    const char* v = getenv("SSQ_K17_MAXLDS");
+    return (int64_t)(v && *v ? atoll(v) : 160 * 1024);
+  }();
   double best = 1e300;
   for (int wm : {1, 2, 4}) {
     for (int pq : {128, 64}) {
@@ -374,7 +513,7 @@ static int wgrad_plan(int64_t Nb, int64_t C, int64_t H, int64_t W, int64_t Co, i
       const int64_t orows = (pq - 1 + OW - 1) / OW + 1;     // output rows a chunk can span
       const int64_t in_rows = (orows - 1) * st + R;
       const int64_t xtile = span * in_rows * Wp;
-      if (wgrad_lds(wm, pq, xtile) > 160 * 1024) continue;
+      if ((int64_t)wgrad_lds(wm, pq, xtile) > max_lds) continue;
       const int64_t cpn = (OH * OW + pq - 1) / pq;
       const int64_t tiles = ((g.Cog + TM - 1) / TM) * ((g.Ncol + TN - 1) / TN);
       const double dma = (double)(std::min<int64_t>(TM, g.Cog) * ((pq + 63) / 64) +
@@ -417,6 +556,11 @@ extern "C" size_t ssq_conv_wgrad_workspace_size(int64_t Nb, int64_t C, int64_t H
     int spl;
     const int ns = dw_splits(Nb, C, &spl);
     return (size_t)ns * (size_t)C * (size_t)(R * S) * sizeof(float);
+  }
+  if (R == 1 && S == 1 && pad == 0) {
+    W1Geo g1;
+    if (wgrad_1x1_plan(Nb, C, H, W, Co, stride, groups, g1)) return 0;
+    return (size_t)g1.nsplit * (size_t)Co * (size_t)g1.Cig * sizeof(float);
   }
   WgradGeo g;
   size_t lds;
@@ -461,6 +605,19 @@ extern "C" int ssq_conv_wgrad(const float* x, const float* dy, int64_t Nb, int64
     const int64_t n = C * R * S;
     hipLaunchKernelGGL(wgrad_stage2, dim3((unsigned)std::min<int64_t>((n + 63) / 64, 4096)),
                        dim3(256), 0, s, (const float*)ws, ns, n, dw);
+    return check_launch("ssq_conv_wgrad");
+  }
+  if (R == 1 && S == 1 && pad == 0) {
+    W1Geo g1;
+    const int rc1 = wgrad_1x1_plan(Nb, C, H, W, Co, stride, groups, g1);
+    if (rc1) return rc1;
+    const size_t need1 = (size_t)g1.nsplit * (size_t)Co * (size_t)g1.Cig * sizeof(float);
+    SSQ_REQUIRE(ws && ws_bytes >= need1, SSQ_E_WS, "ssq_conv_wgrad: workspace too small");
+    const dim3 grid1(g1.n_tiles, g1.m_tiles * g1.G, g1.nsplit);
+    hipLaunchKernelGGL(wgrad_1x1_stage1<2>, grid1, dim3(256), 0, s, x, dy, g1, (float*)ws);
+    const int64_t n1 = (int64_t)Co * g1.Cig;
+    hipLaunchKernelGGL(wgrad_stage2, dim3((unsigned)std::min<int64_t>((n1 + 63) / 64, 4096)),
+                       dim3(256), 0, s, (const float*)ws, g1.nsplit, n1, dw);
     return check_launch("ssq_conv_wgrad");
   }
   WgradGeo g;

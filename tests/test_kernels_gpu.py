@@ -708,6 +708,10 @@ def test_lp_loss_rows_equals_gathered(K, row_shape, p):
     # a chunk, 7x7 planes (short chunks), stride 2 at 28x28
     (2, 16, 14, 256, 1, 1, 0, 1), (1, 8, 70, 16, 3, 1, 1, 1), (1, 4, 130, 8, 3, 1, 1, 1),
     (2, 256, 7, 512, 3, 1, 1, 1), (2, 64, 28, 128, 3, 2, 1, 1),
+    # 1x1 GEMM path: ResNet downsamples (stride 2 at 56x56 / 14x14), ragged channel
+    # counts over the 128 x 128 tile, grouped, a plane shorter than one chunk
+    (2, 64, 56, 128, 1, 2, 0, 1), (2, 256, 14, 512, 1, 2, 0, 1), (3, 72, 9, 40, 1, 1, 0, 1),
+    (2, 300, 7, 130, 1, 1, 0, 1), (2, 48, 12, 96, 1, 1, 0, 2), (4, 16, 5, 24, 1, 2, 0, 1),
     # depthwise path: stride 2, planes wider than a wave, 5x5, odd batch
     (3, 32, 57, 32, 3, 2, 1, 32), (2, 144, 28, 144, 3, 1, 1, 144), (5, 16, 11, 16, 5, 1, 2, 16),
     (32, 8, 7, 8, 3, 1, 1, 8)])
