@@ -360,6 +360,11 @@ int ssq_conv_wgrad(const float* x, const float* dy, int64_t Nb, int64_t C, int64
  * and its input gradient dx (the same sum transposed).  The MobileNetV2 blocks' depthwise
  * F.conv2d of QuantModule.forward (quant_layer.py:250) and its autograd; one plane per
  * workgroup staged in LDS ((H+2pad)*(W+2pad)*4 <= 128 KiB).  Deterministic.           */
+/* 1 when both the forward and the input-gradient plan of this depthwise shape fit the
+ * 128 KiB LDS stage (weight rows + zero-padded / margined planes), else 0 -- the caller
+ * then keeps MIOpen.                                                                    */
+int ssq_dwconv_supported(int64_t Nb, int64_t C, int64_t H, int64_t W, int64_t R, int64_t S,
+                         int64_t stride, int64_t pad);
 int ssq_dwconv_fwd(const float* x, const float* w, float* y, int64_t Nb, int64_t C, int64_t H,
                    int64_t W, int64_t R, int64_t S, int64_t stride, int64_t pad,
                    ssq_stream_t stream);

@@ -80,6 +80,7 @@ SIGNATURES = {
     "ssq_adam": (_i, [_i, _p, _p, _p, _p, _p, _f, _f, _f, _f, _p, _f, _f, _p]),
     "ssq_conv_wgrad_workspace_size": (_sz, [_i64] * 10),
     "ssq_conv_wgrad": (_i, [_p, _p] + [_i64] * 10 + [_p, _p, _sz, _p]),
+    "ssq_dwconv_supported": (_i, [_i64] * 8),
     "ssq_dwconv_fwd": (_i, [_p, _p, _p] + [_i64] * 8 + [_p]),
     "ssq_dwconv_bwd_data": (_i, [_p, _p, _p] + [_i64] * 8 + [_p]),
     "ssq_pack_bits": (_i, [_i]),

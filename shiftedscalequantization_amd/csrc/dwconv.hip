@@ -172,6 +172,13 @@ static int dw_check(int64_t Nb, int64_t C, int64_t H, int64_t W, int64_t R, int6
   return SSQ_OK;
 }
 
+// dynamic LDS of a plan: the P weight rows (RSMAX wide) + the P staged planes
+static int64_t dw_lds_bytes(const DwGeo& g) {
+  const int64_t rsmax = g.R * g.S <= 9 ? 9 : 25;
+  return ((int64_t)g.P * rsmax + (int64_t)g.P * g.Hs * g.Ws) * (int64_t)sizeof(float);
+}
+constexpr int64_t kDwLdsMax = 128 * 1024;   // the opted-in dynamic LDS
+
 template <typename K>
 static void lds_optin(K kernel) {
   hipFuncSetAttribute((const void*)kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
@@ -220,6 +227,8 @@ extern "C" int ssq_dwconv_fwd(const float* x, const float* w, float* y, int64_t 
   }
   DwGeo g;
   dw_geo(Nb, C, H, W, R, S, stride, pad, OH, OW, 0, g);
+  SSQ_REQUIRE(dw_lds_bytes(g) <= kDwLdsMax, SSQ_E_ARG,
+              "ssq_dwconv_fwd: LDS stage %lld B exceeds 128 KiB", (long long)dw_lds_bytes(g));
   hipStream_t s = (hipStream_t)stream;
   if (stride == 1) dw_launch<0, 1>(g, x, w, y, s);
   else if (stride == 2) dw_launch<0, 2>(g, x, w, y, s);
@@ -241,11 +250,21 @@ extern "C" int ssq_dwconv_bwd_data(const float* dy, const float* w, float* dx, i
   }
   DwGeo g;
   dw_geo(Nb, C, H, W, R, S, stride, pad, OH, OW, 1, g);
-  SSQ_REQUIRE((int64_t)g.Hs * g.Ws * (int64_t)sizeof(float) <= 128 * 1024, SSQ_E_ARG,
-              "ssq_dwconv_bwd_data: dy stage exceeds 128 KiB");
+  SSQ_REQUIRE(dw_lds_bytes(g) <= kDwLdsMax, SSQ_E_ARG,
+              "ssq_dwconv_bwd_data: LDS stage %lld B exceeds 128 KiB", (long long)dw_lds_bytes(g));
   hipStream_t s = (hipStream_t)stream;
   if (stride == 1) dw_launch<1, 1>(g, dy, w, dx, s);
   else if (stride == 2) dw_launch<1, 2>(g, dy, w, dx, s);
   else dw_launch<1, 0>(g, dy, w, dx, s);
   return check_launch("ssq_dwconv_bwd_data");
+}
+
+extern "C" int ssq_dwconv_supported(int64_t Nb, int64_t C, int64_t H, int64_t W, int64_t R,
+                                    int64_t S, int64_t stride, int64_t pad) {
+  int64_t OH, OW;
+  if (dw_check(Nb, C, H, W, R, S, stride, pad, &OH, &OW, "ssq_dwconv_supported")) return 0;
+  DwGeo gf, gb;
+  dw_geo(Nb, C, H, W, R, S, stride, pad, OH, OW, 0, gf);
+  dw_geo(Nb, C, H, W, R, S, stride, pad, OH, OW, 1, gb);
+  return dw_lds_bytes(gf) <= kDwLdsMax && dw_lds_bytes(gb) <= kDwLdsMax;
 }

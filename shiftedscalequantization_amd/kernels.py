@@ -995,7 +995,8 @@ def conv_wgrad(x, dy, w_shape, stride, padding, groups):
 # ------------------------------------------------------------------ K18 depthwise conv
 def dwconv_supported(x, weight, stride, padding, dilation, groups):
     """Depthwise shapes K18 handles: fp32 NCHW on the device, groups == C == Co, square
-    stride / padding, dilation 1, R*S <= 25, the padded input plane within 128 KiB."""
+    stride / padding, dilation 1, R*S <= 25, and forward AND input-gradient LDS stages
+    (weight rows + padded planes) within the 128 KiB opt-in (ssq_dwconv_supported)."""
     if x.dim() != 4 or weight.dim() != 4 or not x.is_cuda or x.dtype != torch.float32:
         return False
     if groups <= 1 or groups != x.shape[1] or groups != weight.shape[0] or weight.shape[1] != 1:
@@ -1007,8 +1008,11 @@ def dwconv_supported(x, weight, stride, padding, dilation, groups):
     if (dilation if isinstance(dilation, int) else max(dilation)) != 1:
         return False
     pad = padding if isinstance(padding, int) else padding[0]
+    st = stride if isinstance(stride, int) else stride[0]
+    Nb, C, H, W = (int(v) for v in x.shape)
     R, S = int(weight.shape[2]), int(weight.shape[3])
-    return R * S <= 25 and (x.shape[2] + 2 * pad) * (x.shape[3] + 2 * pad) * 4 <= 128 * 1024
+    # both the forward and the input-gradient stage must fit (the planner's own sizes)
+    return R * S <= 25 and bool(query("ssq_dwconv_supported", Nb, C, H, W, R, S, int(st), int(pad)))
 
 
 def _dw_dims(x_shape, w_shape, stride, padding):

@@ -167,3 +167,14 @@ def test_grad_bucket_allreduce_gloo():
         assert torch.equal(b, torch.arange(5, dtype=torch.float32) * 3)
         assert torch.equal(c, torch.full((2,), 0.5))            # average of 0 and 1
     assert out[0][3] == (0, 512) and out[1][3] == (512, 1024)
+
+
+def test_dwconv_support_query_covers_both_stages():
+    """K18 accepts a depthwise shape only when the forward AND the input-gradient LDS
+    stages fit (weight rows + padded planes / margined dy planes): 178x178 3x3 fits the
+    forward plane alone but not the backward's, so it goes to MIOpen (host-only query)."""
+    from shiftedscalequantization_amd import _capi as A
+    assert A.query("ssq_dwconv_supported", 2, 32, 112, 112, 3, 3, 1, 1) == 1
+    assert A.query("ssq_dwconv_supported", 2, 32, 56, 56, 5, 5, 2, 2) == 1
+    assert A.query("ssq_dwconv_supported", 2, 32, 178, 178, 3, 3, 1, 1) == 0
+    assert A.query("ssq_dwconv_supported", 2, 32, 180, 180, 3, 3, 1, 1) == 0
