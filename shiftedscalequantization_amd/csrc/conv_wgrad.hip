@@ -354,6 +354,168 @@ static int wgrad_1x1_plan(int64_t Nb, int64_t C, int64_t H, int64_t W, int64_t C
   return SSQ_OK;
 }
 
+// ------------------------------------------------------------------ im2col-DMA form
+// Any R x S / stride / padding, as one implicit GEMM whose K = (n, output pixel) runs
+// across samples: a chunk is kPqI consecutive k.  Per chunk each lane owns one k (its
+// sample, output row/column computed once) and both operands are gathered by LDS-DMA with
+// per-lane global addresses straight into GEMM layout -- A[co][k] = dy[n, co, p] and
+// B[col][k] = x[n, ci, oh*st + r - pad, ow*st + s - pad] for col = (ci, r, s); taps that
+// fall in the padding (and k past the end) read a zero page, so no LDS row is written by
+// anything but the DMA.  Rows are padded to a pitch of kPqI + 2 floats: every lane's
+// ds_read_b64 of two consecutive k (two MFMA k-steps) is bank-conflict-free.  Two 66 KB
+// buffers per workgroup (a 32-pixel chunk with two workgroups per CU measured 1.5-2x
+// slower: the per-lane gather DMA issue, not the MFMA, set the pace).  Waves tile the workgroup block as
+// 64 x 64 (2 x 2 v_mfma_f32_32x32x2_f32, exact fp32); splits over chunks, summed in a
+// fixed order by wgrad_stage2: deterministic.
+constexpr int kPqI = 64;
+constexpr int kLdI = kPqI + 2;
+__device__ float g_wgrad_zero_page[64];   // zero-initialised, never written
+
+struct I2cGeo {
+  int C, H, W, Co, OW, OHW, S, RS, st, pad, G, Cig, Cog, Ncol;
+  int64_t K;
+  int m_tiles, n_tiles, cps, nsplit;
+  int64_t nchunks;
+  FastDiv dOHW, dOW, dRS, dS;
+};
+
+template <int WM>
+__global__ __launch_bounds__(256) void wgrad_i2c_stage1(const float* __restrict__ x,
+                                                           const float* __restrict__ dy,
+                                                           I2cGeo g, float* __restrict__ part) {
+  constexpr int WN = 4 / WM, TM = 64 * WM, TN = 64 * WN, ROWS = TM + TN;
+  __shared__ float lds[2 * ROWS * kLdI];
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wm = wave / WN, wn = wave - wm * WN;
+  const int grp = blockIdx.y / g.m_tiles, mt = blockIdx.y - grp * g.m_tiles;
+  const int co0 = mt * TM, col0 = blockIdx.x * TN;
+  const int64_t c_begin = (int64_t)blockIdx.z * g.cps;
+  const int64_t c_end = min(c_begin + g.cps, g.nchunks);
+  const float* zero = g_wgrad_zero_page;
+  const float* xg = x + (int64_t)grp * g.Cig * g.H * g.W;
+  const float* dyg = dy + (int64_t)grp * g.Cog * g.OHW;
+  const int64_t xs_n = (int64_t)g.C * g.H * g.W, dys_n = (int64_t)g.Co * g.OHW;
+
+  auto stage = [&](int64_t c, int b) {
+    if (lane >= kPqI) return;
+    const int64_t k = c * kPqI + lane;
+    const bool kin = k < g.K;
+    const uint32_t kk = kin ? (uint32_t)k : 0u;
+    const int n = (int)fdiv(kk, g.dOHW), p = (int)kk - n * g.OHW;
+    const int oh = (int)fdiv((uint32_t)p, g.dOW), ow = p - oh * g.OW;
+    const int ih0 = oh * g.st - g.pad, iw0 = ow * g.st - g.pad;
+    const float* arow = dyg + n * dys_n + p;
+    const float* xrow = xg + n * xs_n;
+    float* dst = lds + (size_t)b * ROWS * kLdI;
+    for (int rr = wave; rr < ROWS; rr += 4) {
+      const float* src;
+      if (rr < TM) {
+        const int co = co0 + rr;
+        src = (kin && co < g.Cog) ? arow + (int64_t)co * g.OHW : zero;
+      } else {
+        const int col = col0 + rr - TM;
+        const int ci = (int)fdiv((uint32_t)col, g.dRS), rs = col - ci * g.RS;
+        const int r = (int)fdiv((uint32_t)rs, g.dS), sc = rs - r * g.S;
+        const int ih = ih0 + r, iw = iw0 + sc;
+        const bool ok = kin && col < g.Ncol && ih >= 0 && ih < g.H && iw >= 0 && iw < g.W;
+        src = ok ? xrow + ((int64_t)ci * g.H + ih) * g.W + iw : zero;
+      }
+      __builtin_amdgcn_global_load_lds((const void*)src, (void*)(dst + rr * kLdI), 4, 0, 0);
+    }
+  };
+
+  f32x16 acc00 = {0}, acc01 = {0}, acc10 = {0}, acc11 = {0};
+  const int h = lane >> 5;
+  const int ar = (wm * 64 + (lane & 31)) * kLdI + h * (kPqI / 2);
+  const int br = (TM + wn * 64 + (lane & 31)) * kLdI + h * (kPqI / 2);
+  if (c_begin < c_end) stage(c_begin, 0);
+  for (int64_t c = c_begin; c < c_end; ++c) {
+    const int b = (int)((c - c_begin) & 1);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();                  // chunk c staged; chunk c-1's reads of buffer b^1 done
+    if (c + 1 < c_end) stage(c + 1, b ^ 1);
+    const float* L = lds + (size_t)b * ROWS * kLdI;
+#pragma unroll
+    for (int u = 0; u < kPqI / 4; ++u) {
+      typedef float f32x2 __attribute__((ext_vector_type(2)));
+      const f32x2 a0 = *(const f32x2*)(L + ar + 2 * u);
+      const f32x2 a1 = *(const f32x2*)(L + ar + 32 * kLdI + 2 * u);
+      const f32x2 b0 = *(const f32x2*)(L + br + 2 * u);
+      const f32x2 b1 = *(const f32x2*)(L + br + 32 * kLdI + 2 * u);
+      acc00 = __builtin_amdgcn_mfma_f32_32x32x2f32(a0.x, b0.x, acc00, 0, 0, 0);
+      acc01 = __builtin_amdgcn_mfma_f32_32x32x2f32(a0.x, b1.x, acc01, 0, 0, 0);
+      acc10 = __builtin_amdgcn_mfma_f32_32x32x2f32(a1.x, b0.x, acc10, 0, 0, 0);
+      acc11 = __builtin_amdgcn_mfma_f32_32x32x2f32(a1.x, b1.x, acc11, 0, 0, 0);
+      acc00 = __builtin_amdgcn_mfma_f32_32x32x2f32(a0.y, b0.y, acc00, 0, 0, 0);
+      acc01 = __builtin_amdgcn_mfma_f32_32x32x2f32(a0.y, b1.y, acc01, 0, 0, 0);
+      acc10 = __builtin_amdgcn_mfma_f32_32x32x2f32(a1.y, b0.y, acc10, 0, 0, 0);
+      acc11 = __builtin_amdgcn_mfma_f32_32x32x2f32(a1.y, b1.y, acc11, 0, 0, 0);
+    }
+  }
+  float* dst = part + ((int64_t)blockIdx.z * g.G + grp) * (int64_t)g.Cog * g.Ncol;
+  const int wrow = co0 + wm * 64, wcol = col0 + wn * 64;
+#pragma unroll
+  for (int t = 0; t < 4; ++t) {
+    const f32x16 acc = t == 0 ? acc00 : t == 1 ? acc01 : t == 2 ? acc10 : acc11;
+    const int col = wcol + 32 * (t & 1) + (lane & 31);
+    if (col >= g.Ncol) continue;
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      const int row = wrow + 32 * (t >> 1) + (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5);
+      if (row < g.Cog) dst[(int64_t)row * g.Ncol + col] = acc[r];
+    }
+  }
+}
+
+static int wgrad_i2c_plan(int64_t Nb, int64_t C, int64_t H, int64_t W, int64_t Co, int64_t R,
+                          int64_t S, int64_t st, int64_t pad, int64_t G, I2cGeo& g) {
+  SSQ_REQUIRE(Nb >= 1 && C >= 1 && H >= 1 && W >= 1 && Co >= 1 && R >= 1 && S >= 1 && st >= 1 &&
+                  pad >= 0 && G >= 1 && C % G == 0 && Co % G == 0,
+              SSQ_E_ARG, "ssq_conv_wgrad: bad geometry");
+  const int64_t OH = (H + 2 * pad - R) / st + 1, OW = (W + 2 * pad - S) / st + 1;
+  SSQ_REQUIRE(OH >= 1 && OW >= 1 && Nb * C * H * W < (1ll << 31) &&
+                  Nb * Co * OH * OW < (1ll << 31),
+              SSQ_E_ARG, "ssq_conv_wgrad: sizes");
+  g.C = (int)C; g.H = (int)H; g.W = (int)W; g.Co = (int)Co; g.OW = (int)OW;
+  g.OHW = (int)(OH * OW); g.S = (int)S; g.RS = (int)(R * S); g.st = (int)st; g.pad = (int)pad;
+  g.G = (int)G; g.Cig = (int)(C / G); g.Cog = (int)(Co / G);
+  g.Ncol = g.Cig * g.RS;
+  g.K = Nb * OH * OW;
+  g.dOHW = make_fastdiv((uint32_t)g.OHW);
+  g.dOW = make_fastdiv((uint32_t)OW);
+  g.dRS = make_fastdiv((uint32_t)g.RS);
+  g.dS = make_fastdiv((uint32_t)S);
+  g.nchunks = (g.K + kPqI - 1) / kPqI;
+  return SSQ_OK;
+}
+
+// workgroup tile (64 WM x 256 / WM) wasting the fewest MFMA slots on padding, then the
+// split count: ~4 workgroups per CU over the grid, partials bounded to ~16 MB
+static void wgrad_i2c_tiles(I2cGeo& g, int* wm_out) {
+  int64_t best = INT64_MAX;
+  int wmb = 2;
+  for (int wm : {2}) {
+    const int64_t TM = 64 * wm, TN = 256 / wm;
+    const int64_t cost = ((g.Cog + TM - 1) / TM) * ((g.Ncol + TN - 1) / TN) * TM * TN;
+    if (cost < best) {
+      best = cost;
+      wmb = wm;
+    }
+  }
+  *wm_out = wmb;
+  const int TM = 64 * wmb, TN = 256 / wmb;
+  g.m_tiles = (g.Cog + TM - 1) / TM;
+  g.n_tiles = (g.Ncol + TN - 1) / TN;
+  const int64_t tiles = (int64_t)g.m_tiles * g.n_tiles * g.G;
+  const int64_t by_grid = (1024 + tiles - 1) / tiles;
+  const int64_t by_mem = std::max<int64_t>(1, (4ll << 20) / ((int64_t)g.Co * g.Ncol));
+  int64_t ns = std::min<int64_t>(by_grid, by_mem);
+  ns = std::max<int64_t>(1, std::min<int64_t>(ns, g.nchunks / 4));
+  g.cps = (int)((g.nchunks + ns - 1) / ns);
+  g.nsplit = (int)((g.nchunks + g.cps - 1) / g.cps);
+}
+
 // dW = the splits summed in a fixed order: wave w of a workgroup sums its quarter of the
 // splits in split order (8 loads in flight per lane), then the four wave sums are added
 // in wave order.  Same bits run to run; 4x the parallelism of one thread per element.
@@ -545,9 +707,26 @@ static int wgrad_plan(int64_t Nb, int64_t C, int64_t H, int64_t W, int64_t Co, i
   return SSQ_OK;
 }
 
+// Non-depthwise form: 0 auto, 1 the R x S input-row-tile kernel (1x1 on its GEMM), 2 the
+// im2col-DMA kernel for every shape (A/B knob: ssq_conv_wgrad_set_form).  Auto takes the
+// im2col-DMA kernel for ungrouped R x S > 1 convs with >= 128 output channels (its 128 x
+// 128 tile is half idle below that): ResNet-18 3x3 stride-2 convs 2-2.3x faster than the
+// row-tile kernel, 3x3 stride-1 1.1-1.4x (profiles/r2_wgrad_forms.log).
+static int g_wgrad_form = 0;
+static bool use_i2c(int64_t R, int64_t S, int64_t Co, int64_t G) {
+  if (g_wgrad_form != 0) return g_wgrad_form == 2;
+  return R * S > 1 && G == 1 && Co >= 128;
+}
+
 }  // namespace ssq
 
 using namespace ssq;
+
+extern "C" int ssq_conv_wgrad_set_form(int form) {
+  const int old = g_wgrad_form;
+  if (form >= 0 && form <= 2) g_wgrad_form = form;
+  return old;
+}
 
 extern "C" size_t ssq_conv_wgrad_workspace_size(int64_t Nb, int64_t C, int64_t H, int64_t W,
                                                 int64_t Co, int64_t R, int64_t S, int64_t stride,
@@ -556,6 +735,13 @@ extern "C" size_t ssq_conv_wgrad_workspace_size(int64_t Nb, int64_t C, int64_t H
     int spl;
     const int ns = dw_splits(Nb, C, &spl);
     return (size_t)ns * (size_t)C * (size_t)(R * S) * sizeof(float);
+  }
+  if (use_i2c(R, S, Co, groups)) {
+    I2cGeo gi;
+    int wm;
+    if (wgrad_i2c_plan(Nb, C, H, W, Co, R, S, stride, pad, groups, gi)) return 0;
+    wgrad_i2c_tiles(gi, &wm);
+    return (size_t)gi.nsplit * (size_t)Co * (size_t)gi.Ncol * sizeof(float);
   }
   if (R == 1 && S == 1 && pad == 0) {
     W1Geo g1;
@@ -605,6 +791,22 @@ extern "C" int ssq_conv_wgrad(const float* x, const float* dy, int64_t Nb, int64
     const int64_t n = C * R * S;
     hipLaunchKernelGGL(wgrad_stage2, dim3((unsigned)std::min<int64_t>((n + 63) / 64, 4096)),
                        dim3(256), 0, s, (const float*)ws, ns, n, dw);
+    return check_launch("ssq_conv_wgrad");
+  }
+  if (use_i2c(R, S, Co, groups)) {
+    I2cGeo gi;
+    int wm;
+    const int rci = wgrad_i2c_plan(Nb, C, H, W, Co, R, S, stride, pad, groups, gi);
+    if (rci) return rci;
+    wgrad_i2c_tiles(gi, &wm);
+    const size_t needi = (size_t)gi.nsplit * (size_t)Co * (size_t)gi.Ncol * sizeof(float);
+    SSQ_REQUIRE(ws && ws_bytes >= needi, SSQ_E_WS, "ssq_conv_wgrad: workspace too small");
+    const dim3 gridi(gi.n_tiles, gi.m_tiles * gi.G, gi.nsplit);
+    (void)wm;
+    hipLaunchKernelGGL(wgrad_i2c_stage1<2>, gridi, dim3(256), 0, s, x, dy, gi, (float*)ws);
+    const int64_t ni = (int64_t)Co * gi.Ncol;
+    hipLaunchKernelGGL(wgrad_stage2, dim3((unsigned)std::min<int64_t>((ni + 63) / 64, 4096)),
+                       dim3(256), 0, s, (const float*)ws, gi.nsplit, ni, dw);
     return check_launch("ssq_conv_wgrad");
   }
   if (R == 1 && S == 1 && pad == 0) {

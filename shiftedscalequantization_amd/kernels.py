@@ -977,6 +977,12 @@ def conv_wgrad_supported(x, weight, stride, padding, dilation, groups):
                  int(groups)) > 0
 
 
+def set_wgrad_form(form):
+    """K17 non-depthwise form: 0 auto, 1 input-row-tile (+1x1 GEMM), 2 im2col-DMA; returns
+    the previous value."""
+    return int(query("ssq_conv_wgrad_set_form", int(form)))
+
+
 def conv_wgrad(x, dy, w_shape, stride, padding, groups):
     """d loss / d weight of F.conv2d(x, w, stride, padding, groups) given dy (K17)."""
     st = stride if isinstance(stride, int) else stride[0]

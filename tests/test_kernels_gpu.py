@@ -699,6 +699,14 @@ def test_lp_loss_rows_equals_gathered(K, row_shape, p):
         np.testing.assert_array_equal(host(g1).view(np.int32), host(g2).view(np.int32))
 
 
+@pytest.fixture(params=[1, 2], ids=["tile", "i2c"])
+def wgrad_form(request):
+    from shiftedscalequantization_amd import kernels
+    old = kernels.set_wgrad_form(request.param)
+    yield request.param
+    kernels.set_wgrad_form(old)
+
+
 @pytest.mark.parametrize("cfg", [
     # (Nb, C, H, Co, k, stride, pad, groups)
     (4, 64, 56, 64, 3, 1, 1, 1), (3, 16, 15, 24, 3, 2, 1, 1), (2, 32, 14, 48, 1, 2, 0, 1),
@@ -715,9 +723,10 @@ def test_lp_loss_rows_equals_gathered(K, row_shape, p):
     # depthwise path: stride 2, planes wider than a wave, 5x5, odd batch
     (3, 32, 57, 32, 3, 2, 1, 32), (2, 144, 28, 144, 3, 1, 1, 144), (5, 16, 11, 16, 5, 1, 2, 16),
     (32, 8, 7, 8, 3, 1, 1, 8)])
-def test_conv_wgrad_matches_fp64(K, cfg):
-    """K17 weight gradient vs the fp64 CPU gradient: error within the fp32 accumulation
-    bound, bit-identical run to run, and the autograd wrapper equals the direct call."""
+def test_conv_wgrad_matches_fp64(K, cfg, wgrad_form):
+    """K17 weight gradient (both non-depthwise forms) vs the fp64 CPU gradient: error
+    within the fp32 accumulation bound, bit-identical run to run, and the autograd wrapper
+    equals the direct call."""
     Nb, C, H, Co, k, st, pad, g = cfg
     gen = torch.Generator().manual_seed(sum(cfg))
     x = torch.randn(Nb, C, H, H, generator=gen)

@@ -43,14 +43,18 @@ for name, (C, H, Co, k, st, pad, g) in SHAPES.items():
         row[f"miopen_det{int(det)}_us"] = round(ev_time(
             lambda: torch.nn.grad.conv2d_weight(x, w.shape, dy, st, pad, 1, g)), 1)
     torch.backends.cudnn.deterministic = False
+    K.set_wgrad_form(1)
     if not K.conv_wgrad_supported(x, w, st, pad, 1, g):
         row["k17_us"] = None
         print(json.dumps({name: row}), flush=True)
         continue
-    t = ev_time(lambda: K.conv_wgrad(x, dy, w.shape, st, pad, g))
     oh = dy.shape[2]
     flops = 2.0 * 32 * Co * (C // g) * k * k * oh * oh
-    row["k17_us"] = round(t, 1)
-    row["k17_tflops"] = round(flops / t / 1e6, 1)
+    for form, tag in ((1, "k17"), (2, "i2c")):
+        K.set_wgrad_form(form)
+        t = ev_time(lambda: K.conv_wgrad(x, dy, w.shape, st, pad, g))
+        row[tag + "_us"] = round(t, 1)
+        row[tag + "_tflops"] = round(flops / t / 1e6, 1)
+    K.set_wgrad_form(0)
     res[name] = row
     print(json.dumps({name: row}), flush=True)
