@@ -191,14 +191,23 @@ def test_layer_recon_shiftedScale_matches_reference(Q, golden):
     stats["ar_final_rel_err"] = np.max(np.abs(np.array(l2) - g["ar_final"]) / np.abs(g["ar_final"]))
     stats["ar_delta_flips"] = np.sum(d != g["ar_delta"])
     stats["ar_beta_dev"] = np.abs(m.weight_quantizer.beta.detach().cpu().numpy() - g["ar_beta"]).max()
+    stats["ar_beta_walkers"] = np.mean(np.abs(m.weight_quantizer.beta.detach().cpu().numpy() - g["ar_beta"]) > 2e-4)
     parity_report("a20_layer_recon_shiftedScale", **stats)
     assert np.mean(d != g["ar_delta"]) <= 0.005
     # beta entries whose rounding-loss gradient nearly cancels are walked by Adam in +-lr
-    # steps (observed r2: 11 of 4608 off by up to 1.6e-3 on one box, none above 2.4e-4 on
-    # another): bound the walkers' count and their step budget, the rest tightly
-    db = np.abs(m.weight_quantizer.beta.detach().cpu().numpy() - g["ar_beta"])
-    assert np.mean(db > 2e-4) <= 0.01, np.mean(db > 2e-4)
-    assert db.max() <= iters * 2 * 1e-3
+    # steps, and which entries do depends on the fp32 summation order of the box's conv
+    # weight-gradient solver (observed r2: 11 of 4608 off by up to 1.6e-3 on one box, 154
+    # on another, none above 2.4e-4 on a third).  Bounded by what Adam can do: no entry
+    # moves more than its step budget, most stay tight, and the hard rounding decision
+    # (h(beta) >= 0.5 <=> beta >= 0) agrees wherever the reference's beta is further from 0
+    # than that budget.
+    budget = iters * 2 * 1e-3
+    bq = m.weight_quantizer.beta.detach().cpu().numpy()
+    db = np.abs(bq - g["ar_beta"])
+    assert np.mean(db > 2e-4) <= 0.05, np.mean(db > 2e-4)
+    assert db.max() <= budget
+    decided = np.abs(g["ar_beta"]) > budget
+    assert np.all((bq >= 0)[decided] == (g["ar_beta"] >= 0)[decided])
 
 
 @pytest.mark.parametrize("graph", [False, True])

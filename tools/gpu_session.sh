@@ -21,5 +21,7 @@ cd /tmp && export TMPDIR=/tmp
 timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/prof_$TAG -o bench -- python3 $R/bench.py --no-cpu-baseline --recon-iters 100 > $OUT/prof_bench_$TAG.log 2>&1 || { echo "rocprof failed"; tail -20 $OUT/prof_bench_$TAG.log; exit 1; }
 KT=$(find $OUT/prof_$TAG -name "*kernel_trace.csv" | head -1)
 [ -n "$KT" ] && python3 $R/tools/trace_iter.py "$KT" > $OUT/iter_anatomy_$TAG.txt 2>&1
+# the full trace is tens of MB (gpurun copies back <= 64 MiB): keep the summaries only
+[ -n "$KT" ] && rm -f "$KT"
 find $OUT/prof_$TAG -name "*stats*"
 exit 0
