@@ -520,7 +520,8 @@ static void wgrad_i2c_tiles(I2cGeo& g, int* wm_out) {
 // splits in split order (8 loads in flight per lane), then the four wave sums are added
 // in wave order.  Same bits run to run; 4x the parallelism of one thread per element.
 __global__ __launch_bounds__(256) void wgrad_stage2(const float* __restrict__ part, int nsplit,
-                                                    int64_t n, float* __restrict__ dw) {
+                                                    int64_t n, float* __restrict__ dw,
+                                                    int64_t perm_inner = 0, int perm_rs = 0) {
   __shared__ float red[4][64];
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   const int q = (nsplit + 3) >> 2;
@@ -540,8 +541,15 @@ __global__ __launch_bounds__(256) void wgrad_stage2(const float* __restrict__ pa
     for (; s < s1; ++s) a = __fadd_rn(a, part[(int64_t)s * n + ic]);
     red[w][lane] = a;
     __syncthreads();
-    if (w == 0 && i < n)
-      dw[i] = __fadd_rn(__fadd_rn(__fadd_rn(red[0][lane], red[1][lane]), red[2][lane]), red[3][lane]);
+    if (w == 0 && i < n) {
+      // perm_rs > 0: part is [split][tap][co*ci] (band form), dW is [co*ci][tap]
+      int64_t o = i;
+      if (perm_rs > 0) {
+        const int64_t t = i / perm_inner;
+        o = (i - t * perm_inner) * perm_rs + t;
+      }
+      dw[o] = __fadd_rn(__fadd_rn(__fadd_rn(red[0][lane], red[1][lane]), red[2][lane]), red[3][lane]);
+    }
     __syncthreads();
   }
 }
@@ -707,12 +715,243 @@ static int wgrad_plan(int64_t Nb, int64_t C, int64_t H, int64_t W, int64_t Co, i
   return SSQ_OK;
 }
 
+// ------------------------------------------------------------------ band form (3x3, pad 1)
+// Ungrouped 3x3 / pad 1 convs at stride 1 or 2 whose output rows are whole float4s
+// (OW % 4 == 0: ResNet layer1 / layer2 shapes).  The GEMM columns are regrouped as
+// (tap, ci): a wave owns 32 co x 32 ci x all 9 taps (9 v_mfma_f32_32x32x2_f32
+// accumulators), so one dy fragment feeds 9 MFMAs and the 9 taps of an input channel are
+// 3 row windows of the same staged x rows.  K = (n, output pixel) is walked in bands of
+// RB whole output rows of one sample: per band the workgroup stages
+//   A[co][q]          = dy[n, co, oh0 + q / OW, q % OW]              (q < RB * OW)
+//   X[ci][ir][4 + iw] = x[n, ci, oh0*st - 1 + ir, iw]                (ir < (RB-1)*st + 3)
+// with 16-byte LDS-DMA (global_load_lds_dwordx4); every 16-byte LDS piece of a buffer is
+// written by the DMA -- from dy / x or, for padding columns, out-of-image rows and pitch
+// pads, from a zero page -- and the per-lane source offsets are band-independent, so they
+// are computed once per kernel (no division in the staging).  A lane walks 4 consecutive
+// pixels of its lane half per step: A by one ds_read_b128, each tap row's 4 x 3 window by
+// b32 + b128 + b32 (stride 1) or b32 + 2 x b128 (stride 2), 36 MFMAs per 10 LDS reads.
+// Pitches are odd multiples of 4 floats (conflict-free b128 reads).  Partials go to
+// part[split][tap][co][ci] (coalesced) and wgrad_stage2 sums the splits in a fixed order
+// into dW[co][ci][tap]: deterministic.
+constexpr int kBandMaxNI = 20;     // DMA instructions per wave per band (80 KB buffers)
+__device__ float g_band_zero_page[4 * 64];   // zero-initialised, never written
+
+struct BandGeo {
+  int C, H, W, Co, OW, OHW, Cig, Cog;
+  int RB, Q, PA, IR, PXrow, PXci;
+  int TMc, CBc;          // workgroup tile: co rows, input channels
+  int bufsz;             // floats per LDS buffer (a multiple of 1024)
+  int ni_w;              // DMA instructions per wave per band
+  int bands_per_n, nchunks, cps, nsplit, m_tiles, n_tiles, remap;
+};
+
+template <int WMX, int ST>
+__global__ __launch_bounds__(256, 1) void wgrad_band_stage1(const float* __restrict__ x,
+                                                            const float* __restrict__ dy,
+                                                            BandGeo g, float* __restrict__ part) {
+  constexpr int WNX = 4 / WMX;
+  extern __shared__ float lds[];
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wm = wave / WNX, wn = wave - wm * WNX;
+  // XCD-aware order (remap): the tiles of one split run on one XCD and share its L2
+  int wg = blockIdx.x;
+  const int tiles = g.m_tiles * g.n_tiles;
+  if (g.remap) {
+    const int per = (int)gridDim.x >> 3;
+    wg = (wg & 7) * per + (wg >> 3);
+  }
+  const int split = wg / tiles, tile = wg - split * tiles;
+  const int mt = tile / g.n_tiles, nt = tile - mt * g.n_tiles;
+  const int co0 = mt * g.TMc, ci0 = nt * g.CBc;
+  const int c_begin = split * g.cps, c_end = min(c_begin + g.cps, g.nchunks);
+
+  // per-lane DMA sources, band-independent: kind 0 zero page, 1 dy (+ soff), 2 x row ir
+  int soff[kBandMaxNI], meta[kBandMaxNI];
+  const int abytes = g.TMc * g.PA;
+#pragma unroll
+  for (int i = 0; i < kBandMaxNI; ++i) {
+    soff[i] = 0;
+    meta[i] = 0;
+    if (i < g.ni_w) {
+      const int o = (wave + 4 * i) * 256 + lane * 4;
+      if (o < abytes) {
+        const int row = o / g.PA, col = o - row * g.PA;
+        if (col < g.Q && co0 + row < g.Cog) {
+          soff[i] = (co0 + row) * g.OHW + col;   // + n*Co*OHW + oh0*OW per band
+          meta[i] = 1;
+        }
+      } else {
+        const int o2 = o - abytes;
+        const int cl = o2 / g.PXci, rem = o2 - cl * g.PXci;
+        const int ir = rem / g.PXrow, iw = rem - ir * g.PXrow - 4;
+        if (cl < g.CBc && ci0 + cl < g.Cig && ir < g.IR && iw >= 0 && iw < g.W) {
+          soff[i] = ((ci0 + cl) * g.H + ir) * g.W + iw;   // + n*C*H*W + ih0*W per band
+          meta[i] = 2 | (ir << 2);
+        }
+      }
+    }
+  }
+  const float* zero = g_band_zero_page + lane * 4;
+  auto stage = [&](int c, int b) {
+    const int n = c / g.bands_per_n;
+    const int oh0 = (c - n * g.bands_per_n) * g.RB;
+    const int ih0 = oh0 * ST - 1;
+    // branch-free source selection: dy row piece, x row piece, or the zero page
+    const float* ab = dy + (int64_t)n * g.Co * g.OHW + oh0 * g.OW;
+    const float* xb = x + (int64_t)n * g.C * g.H * g.W + (int64_t)ih0 * g.W;
+    float* dst = lds + b * g.bufsz + wave * 256;
+#pragma unroll
+    for (int i = 0; i < kBandMaxNI; ++i) {
+      if (i < g.ni_w) {
+        const int kind = meta[i] & 3;
+        const unsigned ih = (unsigned)(ih0 + (meta[i] >> 2));
+        const bool ok = kind == 1 || (kind == 2 && ih < (unsigned)g.H);
+        const float* base = kind == 1 ? ab : xb;
+        const float* src = ok ? base + soff[i] : zero;
+        __builtin_amdgcn_global_load_lds((const void*)src, (void*)(dst + i * 1024), 16, 0, 0);
+      }
+    }
+  };
+
+  typedef float f32x4v __attribute__((ext_vector_type(4)));
+  f32x16 acc[9];
+#pragma unroll
+  for (int t = 0; t < 9; ++t) acc[t] = f32x16{0};
+  const int h = lane >> 5, l32 = lane & 31;
+  const int arow = (wm * 32 + l32) * g.PA;
+  const int xrow = abytes + (wn * 32 + l32) * g.PXci;
+  const int q0 = h * (g.Q >> 1);
+  const int orow0 = q0 / g.OW, ow0 = q0 - orow0 * g.OW;
+  const int ngroups = g.Q >> 3;
+  constexpr int NW = ST == 1 ? 6 : 9;    // window floats per tap row: 4 pixels x 3 taps
+  // one step's operands: A (4 pixels) and the 3 tap-row windows, read one step ahead
+  auto fetch = [&](const float* L, int q, int orow, int ow, float (&a)[4], float (&w)[3][NW]) {
+    const f32x4v av = *(const f32x4v*)(L + arow + q);
+    a[0] = av.x; a[1] = av.y; a[2] = av.z; a[3] = av.w;
+    const float* xr0 = L + xrow + orow * ST * g.PXrow + ow * ST + 3;
+#pragma unroll
+    for (int r = 0; r < 3; ++r) {
+      const float* xr = xr0 + r * g.PXrow;
+      w[r][0] = xr[0];
+      const f32x4v t1 = *(const f32x4v*)(xr + 1);
+      w[r][1] = t1.x; w[r][2] = t1.y; w[r][3] = t1.z; w[r][4] = t1.w;
+      if (ST == 1) {
+        w[r][5] = xr[5];
+      } else {
+        const f32x4v t2 = *(const f32x4v*)(xr + 5);
+        w[r][5] = t2.x; w[r][6] = t2.y; w[r][7] = t2.z; w[r][8] = t2.w;
+      }
+    }
+  };
+
+  if (c_begin < c_end) stage(c_begin, 0);
+  for (int c = c_begin; c < c_end; ++c) {
+    const int b = (c - c_begin) & 1;
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();             // band c staged; band c-1's reads of buffer b^1 done
+    if (c + 1 < c_end) stage(c + 1, b ^ 1);
+    const float* L = lds + b * g.bufsz;
+    int q = q0, orow = orow0, ow = ow0;
+    float na[4], nw[3][NW];
+    fetch(L, q, orow, ow, na, nw);
+    for (int gi = 0; gi < ngroups; ++gi) {
+      float a[4], w[3][NW];
+#pragma unroll
+      for (int v = 0; v < 4; ++v) a[v] = na[v];
+#pragma unroll
+      for (int r = 0; r < 3; ++r)
+#pragma unroll
+        for (int j = 0; j < NW; ++j) w[r][j] = nw[r][j];
+      q += 4;
+      ow += 4;
+      if (ow == g.OW) {
+        ow = 0;
+        ++orow;
+      }
+      if (gi + 1 < ngroups) fetch(L, q, orow, ow, na, nw);
+#pragma unroll
+      for (int r = 0; r < 3; ++r)
+#pragma unroll
+        for (int v = 0; v < 4; ++v)
+#pragma unroll
+          for (int s = 0; s < 3; ++s)
+            acc[r * 3 + s] =
+                __builtin_amdgcn_mfma_f32_32x32x2f32(a[v], w[r][v * ST + s], acc[r * 3 + s], 0, 0, 0);
+    }
+  }
+  // part[split][tap][co][ci]: C[row][col], row = (i&3) + 8*(i>>2) + 4*h, col = lane&31
+  const int co_w = co0 + wm * 32, ci = ci0 + wn * 32 + l32;
+  if (ci < g.Cig) {
+#pragma unroll
+    for (int t = 0; t < 9; ++t) {
+      float* dst = part + ((int64_t)split * 9 + t) * g.Cog * g.Cig;
+#pragma unroll
+      for (int i = 0; i < 16; ++i) {
+        const int co = co_w + (i & 3) + 8 * (i >> 2) + 4 * h;
+        if (co < g.Cog) dst[(int64_t)co * g.Cig + ci] = acc[t][i];
+      }
+    }
+  }
+}
+
+// band plan: 0 if the shape is not a band shape or no tile fits two buffers in the LDS
+static int band_plan(int64_t Nb, int64_t C, int64_t H, int64_t W, int64_t Co, int64_t R,
+                     int64_t S, int64_t st, int64_t pad, int64_t G, BandGeo& g, int* wmx) {
+  if (G != 1 || R != 3 || S != 3 || pad != 1 || (st != 1 && st != 2)) return 0;
+  const int64_t OH = (H + 2 - 3) / st + 1, OW = (W + 2 - 3) / st + 1;
+  if (OH < 1 || OW < 4 || OW % 4 || W % 4 || Co % 32 || C % 32) return 0;
+  if (Nb * C * H * W >= (1ll << 31) || Nb * Co * OH * OW >= (1ll << 31)) return 0;
+  g.C = (int)C; g.H = (int)H; g.W = (int)W; g.Co = (int)Co; g.OW = (int)OW;
+  g.OHW = (int)(OH * OW); g.Cig = (int)C; g.Cog = (int)Co;
+  auto odd4 = [](int v) { v = (v + 3) / 4 * 4; return (v / 4) % 2 ? v : v + 4; };
+  const int64_t budget = 160 * 1024 / 2 / 4;   // floats per buffer
+  bool found = false;
+  // prefer the 64 x 64 tile; 128 co x 32 ci when 64 input channels do not fit
+  for (int wm : {2, 4}) {
+    if (found) break;
+    const int TMc = 32 * wm, CBc = 32 * (4 / wm);
+    if (wm == 4 && Co < 128) continue;
+    // the largest band of whole rows with RB * OW % 8 == 0 that fits
+    for (int rb = (int)std::min<int64_t>(OH, 8); rb >= 1; --rb) {
+      if (OH % rb || (rb * OW) % 8) continue;
+      const int Q = rb * (int)OW, PA = odd4(Q + 1);
+      const int IR = (rb - 1) * (int)st + 3, PXrow = (int)W + 8, PXci = odd4(IR * PXrow);
+      const int64_t buf = ((int64_t)TMc * PA + (int64_t)CBc * PXci + 1023) / 1024 * 1024;
+      if (buf > budget) continue;
+      g.RB = rb; g.Q = Q; g.PA = PA; g.IR = IR; g.PXrow = PXrow; g.PXci = PXci;
+      g.TMc = TMc; g.CBc = CBc; g.bufsz = (int)buf; g.ni_w = (int)(buf / 1024);
+      *wmx = wm;
+      found = true;
+      break;
+    }
+  }
+  if (!found || g.ni_w > kBandMaxNI) return 0;
+  g.m_tiles = (g.Cog + g.TMc - 1) / g.TMc;
+  g.n_tiles = (g.Cig + g.CBc - 1) / g.CBc;
+  g.bands_per_n = (int)(OH / g.RB);
+  g.nchunks = (int)Nb * g.bands_per_n;
+  const int tiles = g.m_tiles * g.n_tiles;
+  // one workgroup per CU (the two buffers take most of the LDS): ~256 workgroups
+  int ns = std::max(1, std::min(g.nchunks, (256 + tiles - 1) / tiles));
+  g.cps = (g.nchunks + ns - 1) / ns;
+  g.nsplit = (g.nchunks + g.cps - 1) / g.cps;
+  g.remap = ((int64_t)g.nsplit * tiles) % 8 == 0;
+  return 1;
+}
+
 // Non-depthwise form: 0 auto, 1 the R x S input-row-tile kernel (1x1 on its GEMM), 2 the
-// im2col-DMA kernel for every shape (A/B knob: ssq_conv_wgrad_set_form).  Auto takes the
-// im2col-DMA kernel for ungrouped R x S > 1 convs with >= 128 output channels (its 128 x
-// 128 tile is half idle below that): ResNet-18 3x3 stride-2 convs 2-2.3x faster than the
-// row-tile kernel, 3x3 stride-1 1.1-1.4x (profiles/r2_wgrad_forms.log).
+// im2col-DMA kernel for every shape, 3 the band kernel where it applies (A/B knob:
+// ssq_conv_wgrad_set_form).  Auto takes the band kernel for the shapes band_plan accepts,
+// then the im2col-DMA kernel for ungrouped R x S > 1 convs with >= 128 output channels
+// (its 128 x 128 tile is half idle below that): ResNet-18 3x3 stride-2 convs 2-2.3x faster
+// than the row-tile kernel, 3x3 stride-1 1.1-1.4x (profiles/r2_wgrad_forms.log).
 static int g_wgrad_form = 0;
+static bool use_band(int64_t Nb, int64_t C, int64_t H, int64_t W, int64_t Co, int64_t R,
+                     int64_t S, int64_t st, int64_t pad, int64_t G, BandGeo& g, int* wmx) {
+  if (g_wgrad_form != 0 && g_wgrad_form != 3) return false;
+  return band_plan(Nb, C, H, W, Co, R, S, st, pad, G, g, wmx) != 0;
+}
 static bool use_i2c(int64_t R, int64_t S, int64_t Co, int64_t G) {
   if (g_wgrad_form != 0) return g_wgrad_form == 2;
   return R * S > 1 && G == 1 && Co >= 128;
@@ -724,7 +963,7 @@ using namespace ssq;
 
 extern "C" int ssq_conv_wgrad_set_form(int form) {
   const int old = g_wgrad_form;
-  if (form >= 0 && form <= 2) g_wgrad_form = form;
+  if (form >= 0 && form <= 3) g_wgrad_form = form;
   return old;
 }
 
@@ -735,6 +974,12 @@ extern "C" size_t ssq_conv_wgrad_workspace_size(int64_t Nb, int64_t C, int64_t H
     int spl;
     const int ns = dw_splits(Nb, C, &spl);
     return (size_t)ns * (size_t)C * (size_t)(R * S) * sizeof(float);
+  }
+  {
+    BandGeo gb;
+    int wmx;
+    if (use_band(Nb, C, H, W, Co, R, S, stride, pad, groups, gb, &wmx))
+      return (size_t)gb.nsplit * 9 * (size_t)Co * (size_t)C * sizeof(float);
   }
   if (use_i2c(R, S, Co, groups)) {
     I2cGeo gi;
@@ -792,6 +1037,35 @@ extern "C" int ssq_conv_wgrad(const float* x, const float* dy, int64_t Nb, int64
     hipLaunchKernelGGL(wgrad_stage2, dim3((unsigned)std::min<int64_t>((n + 63) / 64, 4096)),
                        dim3(256), 0, s, (const float*)ws, ns, n, dw);
     return check_launch("ssq_conv_wgrad");
+  }
+  {
+    BandGeo gb;
+    int wmx;
+    if (use_band(Nb, C, H, W, Co, R, S, stride, pad, groups, gb, &wmx)) {
+      const size_t needb = (size_t)gb.nsplit * 9 * (size_t)Co * (size_t)C * sizeof(float);
+      SSQ_REQUIRE(ws && ws_bytes >= needb, SSQ_E_WS, "ssq_conv_wgrad: workspace too small");
+      static bool band_attr = false;
+      if (!band_attr) {  // two 80 KB buffers: the whole LDS
+        hipFuncSetAttribute((const void*)wgrad_band_stage1<2, 1>,
+                            hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+        hipFuncSetAttribute((const void*)wgrad_band_stage1<2, 2>,
+                            hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+        hipFuncSetAttribute((const void*)wgrad_band_stage1<4, 1>,
+                            hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+        hipFuncSetAttribute((const void*)wgrad_band_stage1<4, 2>,
+                            hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+        band_attr = true;
+      }
+      const dim3 gridb((unsigned)(gb.nsplit * gb.m_tiles * gb.n_tiles));
+      const size_t ldsb = 2 * (size_t)gb.bufsz * sizeof(float);
+      auto kb = wmx == 2 ? (stride == 1 ? wgrad_band_stage1<2, 1> : wgrad_band_stage1<2, 2>)
+                         : (stride == 1 ? wgrad_band_stage1<4, 1> : wgrad_band_stage1<4, 2>);
+      hipLaunchKernelGGL(kb, gridb, dim3(256), ldsb, s, x, dy, gb, (float*)ws);
+      const int64_t inner = Co * C, nb = 9 * inner;
+      hipLaunchKernelGGL(wgrad_stage2, dim3((unsigned)std::min<int64_t>((nb + 63) / 64, 4096)),
+                         dim3(256), 0, s, (const float*)ws, gb.nsplit, nb, dw, inner, 9);
+      return check_launch("ssq_conv_wgrad");
+    }
   }
   if (use_i2c(R, S, Co, groups)) {
     I2cGeo gi;

@@ -978,8 +978,8 @@ def conv_wgrad_supported(x, weight, stride, padding, dilation, groups):
 
 
 def set_wgrad_form(form):
-    """K17 non-depthwise form: 0 auto, 1 input-row-tile (+1x1 GEMM), 2 im2col-DMA; returns
-    the previous value."""
+    """K17 non-depthwise form: 0 auto, 1 input-row-tile (+1x1 GEMM), 2 im2col-DMA, 3 band
+    (3x3 pad 1 shapes it plans, else the row tile); returns the previous value."""
     return int(query("ssq_conv_wgrad_set_form", int(form)))
 
 

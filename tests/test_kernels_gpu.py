@@ -699,7 +699,7 @@ def test_lp_loss_rows_equals_gathered(K, row_shape, p):
         np.testing.assert_array_equal(host(g1).view(np.int32), host(g2).view(np.int32))
 
 
-@pytest.fixture(params=[1, 2], ids=["tile", "i2c"])
+@pytest.fixture(params=[1, 2, 3], ids=["tile", "i2c", "band"])
 def wgrad_form(request):
     from shiftedscalequantization_amd import kernels
     old = kernels.set_wgrad_form(request.param)
@@ -716,6 +716,10 @@ def wgrad_form(request):
     # a chunk, 7x7 planes (short chunks), stride 2 at 28x28
     (2, 16, 14, 256, 1, 1, 0, 1), (1, 8, 70, 16, 3, 1, 1, 1), (1, 4, 130, 8, 3, 1, 1, 1),
     (2, 256, 7, 512, 3, 1, 1, 1), (2, 64, 28, 128, 3, 2, 1, 1),
+    # band path (3x3 pad 1, OW % 4 == 0): ResNet layer1 / layer2 / layer2.0 stride 2,
+    # ragged output-channel tiles, fewer input channels than the tile, one-row bands
+    (3, 128, 28, 128, 3, 1, 1, 1), (2, 64, 56, 128, 3, 2, 1, 1), (2, 32, 16, 96, 3, 2, 1, 1),
+    (3, 32, 8, 160, 3, 1, 1, 1), (2, 96, 12, 64, 3, 1, 1, 1),
     # 1x1 GEMM path: ResNet downsamples (stride 2 at 56x56 / 14x14), ragged channel
     # counts over the 128 x 128 tile, grouped, a plane shorter than one chunk
     (2, 64, 56, 128, 1, 2, 0, 1), (2, 256, 14, 512, 1, 2, 0, 1), (3, 72, 9, 40, 1, 1, 0, 1),

@@ -50,7 +50,7 @@ for name, (C, H, Co, k, st, pad, g) in SHAPES.items():
         continue
     oh = dy.shape[2]
     flops = 2.0 * 32 * Co * (C // g) * k * k * oh * oh
-    for form, tag in ((1, "k17"), (2, "i2c")):
+    for form, tag in ((1, "k17"), (2, "i2c"), (3, "band"), (0, "auto")):
         K.set_wgrad_form(form)
         t = ev_time(lambda: K.conv_wgrad(x, dy, w.shape, st, pad, g))
         row[tag + "_us"] = round(t, 1)
