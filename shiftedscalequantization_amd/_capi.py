@@ -79,6 +79,7 @@ SIGNATURES = {
                               _p, _p, _p, _p, _p, _p, _sz, _p]),
     "ssq_adam": (_i, [_i, _p, _p, _p, _p, _p, _f, _f, _f, _f, _p, _f, _f, _p]),
     "ssq_conv_wgrad_set_form": (_i, [_i]),
+    "ssq_conv_wgrad_kind": (_i, [_i64] * 10),
     "ssq_conv_wgrad_workspace_size": (_sz, [_i64] * 10),
     "ssq_conv_wgrad": (_i, [_p, _p] + [_i64] * 10 + [_p, _p, _sz, _p]),
     "ssq_dwconv_supported": (_i, [_i64] * 8),

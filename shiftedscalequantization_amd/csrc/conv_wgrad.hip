@@ -967,6 +967,26 @@ extern "C" int ssq_conv_wgrad_set_form(int form) {
   return old;
 }
 
+extern "C" int ssq_conv_wgrad_kind(int64_t Nb, int64_t C, int64_t H, int64_t W, int64_t Co,
+                                   int64_t R, int64_t S, int64_t stride, int64_t pad,
+                                   int64_t groups) {
+  if (is_depthwise(C, Co, groups) && R * S <= 25 && Nb >= 1 && dw_lds_ok(H, W, pad)) return 5;
+  BandGeo gb;
+  int wmx;
+  if (use_band(Nb, C, H, W, Co, R, S, stride, pad, groups, gb, &wmx)) return 3;
+  if (use_i2c(R, S, Co, groups)) {
+    I2cGeo gi;
+    return wgrad_i2c_plan(Nb, C, H, W, Co, R, S, stride, pad, groups, gi) ? 0 : 2;
+  }
+  if (R == 1 && S == 1 && pad == 0) {
+    W1Geo g1;
+    return wgrad_1x1_plan(Nb, C, H, W, Co, stride, groups, g1) ? 0 : 4;
+  }
+  WgradGeo g;
+  size_t lds;
+  return wgrad_plan(Nb, C, H, W, Co, R, S, stride, pad, groups, g, &lds) ? 0 : 1;
+}
+
 extern "C" size_t ssq_conv_wgrad_workspace_size(int64_t Nb, int64_t C, int64_t H, int64_t W,
                                                 int64_t Co, int64_t R, int64_t S, int64_t stride,
                                                 int64_t pad, int64_t groups) {

@@ -977,6 +977,17 @@ def conv_wgrad_supported(x, weight, stride, padding, dilation, groups):
                  int(groups)) > 0
 
 
+def wgrad_kind(x_shape, w_shape, stride, padding, groups):
+    """The K17 kernel ssq_conv_wgrad runs for this shape (0 unsupported, 1 row tile,
+    2 im2col-DMA, 3 band, 4 1x1 GEMM, 5 depthwise)."""
+    st = stride if isinstance(stride, int) else stride[0]
+    pad = padding if isinstance(padding, int) else padding[0]
+    Nb, C, H, W = (int(v) for v in x_shape)
+    Co, _, R, S = (int(v) for v in w_shape)
+    return int(query("ssq_conv_wgrad_kind", Nb, C, H, W, Co, R, S, int(st), int(pad),
+                     int(groups)))
+
+
 def set_wgrad_form(form):
     """K17 non-depthwise form: 0 auto, 1 input-row-tile (+1x1 GEMM), 2 im2col-DMA, 3 band
     (3x3 pad 1 shapes it plans, else the row tile); returns the previous value."""
@@ -1094,9 +1105,12 @@ class Conv2dFn(torch.autograd.Function):
 
 
 # When the conv weight gradient runs on K17 (tools/wgrad_bench.py, batch 32, MI355X):
-#   'auto'   every grouped conv: depthwise ones on K17's LDS-staged reduction (MobileNetV2
-#            144x56x56 3x3: 74 vs 866 us on MIOpen, either mode), other grouped ones on
-#            its MFMA GEMM (RegNetX g=2: 217 vs 955 us); under the reference's
+#   'auto'   every shape the band kernel takes (3x3 pad 1, OW % 4 == 0: ResNet layer1 /
+#            layer2), in either mode -- it beats MIOpen's fastest non-deterministic solver
+#            there (layer1 3x3: 95 vs 110 us, layer2.0 stride 2: 63 vs 72 us,
+#            profiles/r2_wgrad_band.log); every grouped conv: depthwise ones on K17's
+#            LDS-staged reduction (MobileNetV2 144x56x56 3x3: 74 vs 866 us on MIOpen, either
+#            mode), other grouped ones on its MFMA GEMM (RegNetX g=2: 217 vs 955 us); under the reference's
 #            torch.backends.cudnn.deterministic also every stride-2 conv and every output
 #            plane >= 400 pixels, where MIOpen's deterministic solvers are 3-8x slower than
 #            K17 (stride-1 14x14 / 7x7 planes are as fast on MIOpen).
@@ -1110,6 +1124,8 @@ def _use_k17(x, weight, stride, padding, groups=1):
     if WGRAD_POLICY != "auto":
         return False
     if groups > 1:
+        return True
+    if wgrad_kind(x.shape, weight.shape, stride, padding, groups) == 3:
         return True
     if torch.backends.cudnn.deterministic:
         st = stride if isinstance(stride, int) else stride[0]
