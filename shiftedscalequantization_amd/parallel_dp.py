@@ -61,6 +61,11 @@ class GradBucket:
         for p, v in zip(self.live, self.views):
             p.grad = v
 
+    @property
+    def active(self):
+        """True once the bucket is built at world > 1 (what a graph capture needs)."""
+        return world() > 1 and self.live is not None
+
     def allreduce_(self):
         ws = world()
         if ws == 1 or not self.params:
@@ -74,6 +79,11 @@ class GradBucket:
             elif p.grad.data_ptr() != v.data_ptr():
                 v.copy_(p.grad)    # first iteration, or a loop that reset the grads
                 p.grad = v
+        self.reduce_()
+
+    def reduce_(self):
+        """The collective alone, on the attached bucket (between two graph replays)."""
+        ws = world()
         if RECORD is not None:
             RECORD.append(["local", self.flat.detach().clone()])
         if self.flat.numel():

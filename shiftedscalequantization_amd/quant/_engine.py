@@ -204,3 +204,50 @@ class frozen_except:
     def __exit__(self, *exc):
         for p in self.frozen:
             p.requires_grad_(True)
+
+
+# replays per form ("single" graph, "split" around the collective): test / report hook
+GRAPH_REPLAYS = {"single": 0, "split": 0}
+
+
+class IterationGraph:
+    """HIP-graph replay of a reconstruction iteration split at its one exchange step.
+
+    world == 1 (or no bucket): pre() + post() captured as one graph.  world > 1: the
+    gradient all-reduce cannot run inside the graph (gloo goes through the host; RCCL's
+    collective is issued by torch on its own stream), so the body is captured as two graphs
+    around it -- pre = zero the flat bucket the live gradients are views of, gather,
+    forward, fused loss + gradient, backward (accumulating in place into the bucket);
+    post = the fused Adam step -- and each iteration replays pre, runs the bucket's
+    collective eagerly, and replays post.  Same kernels, same order, same bits as the eager
+    iteration; the per-iteration launch work is two graph launches and one collective."""
+
+    def __init__(self, pre, post, bucket, ws_cache):
+        self.bucket = bucket if (bucket is not None and bucket.active) else None
+        self.graphs = []
+        with K.A.workspace_scope(ws_cache):
+            if self.bucket is None:
+                g = torch.cuda.CUDAGraph()
+                with torch.cuda.graph(g):
+                    pre()
+                    post()
+                self.graphs = [g]
+            else:
+                self.bucket.attach_()            # grads = views of the bucket (host side)
+                g1, g2 = torch.cuda.CUDAGraph(), torch.cuda.CUDAGraph()
+                with torch.cuda.graph(g1):
+                    self.bucket.flat.zero_()
+                    pre()
+                with torch.cuda.graph(g2, pool=g1.pool()):
+                    post()
+                self.graphs = [g1, g2]
+
+    def replay(self):
+        self.graphs[0].replay()
+        if self.bucket is not None:
+            self.bucket.reduce_()
+            self.graphs[1].replay()
+        GRAPH_REPLAYS["split" if self.bucket is not None else "single"] += 1
+
+    def release(self):
+        self.graphs = []

@@ -12,7 +12,7 @@ import torch
 
 from .. import kernels as K
 from ..parallel_dp import GradBucket, world
-from ._engine import BatchFeeder, LazyValue, SsqAdam, as_float, frozen_except
+from ._engine import BatchFeeder, IterationGraph, LazyValue, SsqAdam, as_float, frozen_except
 from .adaptive_rounding import AdaRoundQuantizer
 from .data_utils import save_grad_data, save_inp_oup_data
 from .quant_block import BaseQuantBlock
@@ -76,7 +76,7 @@ def _reconstruct(model, block, qmodules, cali_data, batch_size, iters, weight, o
         if opt_mode == 'mse' and opt_params[0].is_cuda:
             with frozen_except(block, opt_params):
                 _fast_loop(block, qmodules, opt_params, loss_func, feeder, bucket, iters, act_quant,
-                           lr, p, graph and world() == 1 and not multi_gpu)
+                           lr, p, graph)
         else:
             _eager_loop(opt_params, loss_func, feeder, bucket, cached_grads, block, iters, act_quant,
                         lr)
@@ -119,7 +119,8 @@ def _fast_loop(block, qmodules, opt_params, loss_func, feeder, bucket, iters, ac
     (lambda, b)), gather, forward, one fused lp_loss value+gradient pass (at the input of a
     final fused-epilogue ReLU), backward with the round loss's gradient folded into the
     AdaRound backward, fused Adam.  After GRAPH_WARMUP eager iterations the body is
-    replayed from a HIP graph (single GPU).  The cosine LR schedule is stepped by the
+    replayed from a HIP graph (at world > 1 as two graphs around the bucket all-reduce,
+    _engine.IterationGraph).  The cosine LR schedule is stepped by the
     reference's own torch scheduler on a shadow optimizer and copied into Adam's device lr."""
     if ITER_HOOK is not None:
         ITER_HOOK(-1, iters)
@@ -139,7 +140,7 @@ def _fast_loop(block, qmodules, opt_params, loss_func, feeder, bucket, iters, ac
             q._fused_reg = (0.0, 0.0, regp)
     last = {}
 
-    def body():
+    def body_pre():
         cur_inp, cur_out = feeder.gather_lazy()
         out = block(cur_inp)
         relu_in = getattr(out, '_ssq_relu_inputs', None)
@@ -148,6 +149,7 @@ def _fast_loop(block, qmodules, opt_params, loss_func, feeder, bucket, iters, ac
             # act quantizer is disabled): the reference's backward yields no gradient for it
             # and its Adam step skips it -- only the loss value remains
             last['rec'], _ = K.lp_loss_and_grad(out, cur_out, p, want_grad=False)
+            last['step'] = False
             return
         if relu_in:
             rec, g = K.lp_loss_and_grad(out, cur_out, p, relu_mask=True)
@@ -155,10 +157,12 @@ def _fast_loop(block, qmodules, opt_params, loss_func, feeder, bucket, iters, ac
         else:
             rec, g = K.lp_loss_and_grad(out, cur_out, p)
             out.backward(g)
-        if bucket is not None:
-            bucket.allreduce_()
-        optimizer.step(hyper=hyper)
         last['rec'] = rec
+        last['step'] = True
+
+    def body_post():
+        if last['step']:
+            optimizer.step(hyper=hyper)
 
     graph_obj, ws_cache = None, {}
     try:
@@ -171,18 +175,20 @@ def _fast_loop(block, qmodules, opt_params, loss_func, feeder, bucket, iters, ac
             # reference's forward computes it
             rnd = loss_func.round_value(b) if (active and loss_func.wants_value()) else 0.0
             if use_graph and i == GRAPH_WARMUP:
-                optimizer.zero_grad(set_to_none=True)
-                graph_obj = torch.cuda.CUDAGraph()
-                with K.A.workspace_scope(ws_cache):
-                    with torch.cuda.graph(graph_obj):
-                        body()
+                if bucket is None or not bucket.active:
+                    optimizer.zero_grad(set_to_none=True)
+                # world > 1: two graphs around the eager bucket all-reduce (IterationGraph)
+                graph_obj = IterationGraph(body_pre, body_post, bucket, ws_cache)
             if graph_obj is not None:
                 graph_obj.replay()
             else:
                 optimizer.zero_grad()
                 if bucket is not None:
                     bucket.attach_()
-                body()
+                body_pre()
+                if bucket is not None and last['step']:
+                    bucket.allreduce_()
+                body_post()
             rec = last['rec'][0]
             loss_func.record(rec, rnd, b)
             if scheduler is not None:
@@ -198,6 +204,7 @@ def _fast_loop(block, qmodules, opt_params, loss_func, feeder, bucket, iters, ac
             torch.cuda.current_stream().synchronize()
             for p_ in opt_params:       # detach the grads from the graph's private pool
                 p_.grad = None if p_.grad is None else p_.grad.clone()
+            graph_obj.release()
             del graph_obj
 
 

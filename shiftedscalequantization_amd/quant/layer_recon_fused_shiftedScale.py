@@ -19,7 +19,8 @@ from tqdm import tqdm
 
 from .. import kernels as K
 from ..parallel_dp import GradBucket, world
-from ._engine import BatchFeeder, SsqAdam, LazyValue, as_float, clear_stash, stash_block_weights
+from ._engine import (BatchFeeder, IterationGraph, LazyValue, SsqAdam, as_float, clear_stash,
+                      stash_block_weights)
 from .quant_block import BaseQuantBlock
 from .quant_layer import QuantModule
 
@@ -74,7 +75,7 @@ def _fused_loop(block, modules, iters, lmda, model, p, lr, bias_cal, batch_size,
         if bias_cal:
             opt_params += [m.alpha_out, m.beta_out]
     on_gpu = opt_params[0].is_cuda
-    use_graph = bool(graph and on_gpu and world() == 1 and iters > GRAPH_WARMUP + 1)
+    use_graph = bool(graph and on_gpu and iters > GRAPH_WARMUP + 1)
     # one ssq_adam launch for all parameters; its per-step scalars ride on the index copy,
     # so the whole iteration can be replayed from a HIP graph
     optimizer = SsqAdam(opt_params, lr=lr) if on_gpu else torch.optim.Adam(opt_params, lr=lr)
@@ -92,9 +93,9 @@ def _fused_loop(block, modules, iters, lmda, model, p, lr, bias_cal, batch_size,
     hyper = feeder.extra[2:4]
     last = {}
 
-    def body():
-        """One iteration on the device: gather -> forward -> fused loss+grad -> backward
-        (+ RCCL bucket) -> Adam.  No host sync, no host-side state: graph-capturable."""
+    def body_pre():
+        """One iteration on the device up to its exchange step: gather -> forward -> fused
+        loss+grad -> backward.  No host sync, no host-side state: graph-capturable."""
         cur_inp, cur_out = feeder.gather_lazy()
         if on_gpu:
             stash_block_weights(quantizers)     # every conv's What in one launch
@@ -109,13 +110,14 @@ def _fused_loop(block, modules, iters, lmda, model, p, lr, bias_cal, batch_size,
         else:
             rec, g_out = loss_func.loss_and_grad(quant_out, cur_out)
             quant_out.backward(g_out)
-        if bucket is not None:
-            bucket.allreduce_()
+        last['rec'] = rec
+
+    def body_post():
+        """After the (RCCL) bucket all-reduce: the fused Adam step."""
         if on_gpu:
             optimizer.step(hyper=hyper)
         else:
             optimizer.step()
-        last['rec'] = rec
 
     graph_obj, ws_cache = None, {}
     start_loss = 0.0
@@ -127,18 +129,20 @@ def _fused_loop(block, modules, iters, lmda, model, p, lr, bias_cal, batch_size,
         feeder.stage(feeder.draw(), extra=loss_func.schedule_pair() +
                      (optimizer.next_hyper() if on_gpu else (0.0, 0.0)))
         if use_graph and i == GRAPH_WARMUP:
-            optimizer.zero_grad(set_to_none=True)
-            graph_obj = torch.cuda.CUDAGraph()
-            with K.A.workspace_scope(ws_cache):
-                with torch.cuda.graph(graph_obj):
-                    body()
+            if bucket is None or not bucket.active:
+                optimizer.zero_grad(set_to_none=True)
+            # world > 1: two graphs around the eager bucket all-reduce (IterationGraph)
+            graph_obj = IterationGraph(body_pre, body_post, bucket, ws_cache)
         if graph_obj is not None:
             graph_obj.replay()
         else:
             optimizer.zero_grad()
             if bucket is not None:
                 bucket.attach_()
-            body()
+            body_pre()
+            if bucket is not None:
+                bucket.allreduce_()
+            body_post()
         loss_func.bookkeep(last['rec'])
         if i % 500 == 0 and verbose:
             start_loss = max(start_loss, as_float(loss_func.rec_loss))
@@ -148,6 +152,7 @@ def _fused_loop(block, modules, iters, lmda, model, p, lr, bias_cal, batch_size,
         torch.cuda.current_stream().synchronize()
         for p_ in opt_params:       # detach the grads from the graph's private pool
             p_.grad = None if p_.grad is None else p_.grad.clone()
+        graph_obj.release()
         del graph_obj
     loss_func.disarm()
     for q, rg in beta_rg.items():
@@ -185,7 +190,8 @@ def block_recon_fused_shiftedScale(block: BaseQuantBlock, iters: int = 20000, lm
                                    dp_average=False, verbose=True, iter_hook=None, graph=True):
     """layer_recon_fused_shiftedScale.py:23-141 -> [soft rec loss, hard rec loss].
     graph=True replays the iteration body from a HIP graph after GRAPH_WARMUP eager
-    iterations (single GPU); the arithmetic and the batch draws are unchanged."""
+    iterations (at world > 1 as two graphs around the bucket all-reduce); the arithmetic
+    and the batch draws are unchanged."""
     if act:
         # the reference's act branch builds ChannelQuantAct and calls its init_v, which
         # crashes (channelQuantAct.py:126-134): no working semantics exist to reproduce

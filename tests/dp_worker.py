@@ -108,6 +108,8 @@ def main():
         out[f"rec{k}_local"] = local.cpu().numpy()
         out[f"rec{k}_reduced"] = reduced.cpu().numpy()
     out["n_rec"] = np.array([len(P.RECORD)])
+    from shiftedscalequantization_amd.quant._engine import GRAPH_REPLAYS
+    out["split_replays"] = np.array([GRAPH_REPLAYS["split"]])
     np.savez(path, **out)
     dist.barrier()
     dist.destroy_process_group()

@@ -10,7 +10,9 @@ calibration data.  Checked, bit for bit:
   * they equal a single-process replay that feeds Adam the summed gradients from the
     same starting point (the "1-rank run fed the summed gradient of both shards");
   * the act deltas initialised on different shards differ before, and are identical
-    after, synchorize_activation_statistics (their mean).
+    after, synchorize_activation_statistics (their mean);
+  * after the eager warm-up the iterations replay HIP graphs split around the collective
+    (quant._engine.IterationGraph), so all of the above holds for the graph path.
 """
 import os
 import socket
@@ -59,6 +61,8 @@ def _run_world2(mode, tmp_path):
 
 
 def _check_buckets(r0, r1):
+    # the iterations after the eager warm-up replay the two graphs around the collective
+    assert int(r0["split_replays"][0]) > 0 and int(r1["split_replays"][0]) > 0
     n = int(r0["n_rec"][0])
     assert n == int(r1["n_rec"][0]) and n > 0
     for k in range(n):
