@@ -10,14 +10,14 @@
 // fpack + hterm (+ gWhat) with no divide and no exp per element -- 12 B/elem forward
 // (fpack, hterm in; What out) and 12 B/elem backward (gWhat, fpack, hterm in), the §8(d)
 // algorithmic bytes -- and produce bit-identical What / identical gradients.  The alpha
-// backward reduction is two fixed-order launches (a last-workgroup single launch measured
-// 88 us on a 512x512x3x3 conv: the agent-scope release fence every workgroup needs writes
-// back its XCD's L2, so it is not used).
+// backward is two fixed-order launches (chunk partials, then one wave per input channel).
+// Its one-launch form (SSQ_ALPHA_ONE_LAUNCH=1: partials handed off write-through, reduced
+// by the last workgroup of each column block, arrive_last) is bit-identical but slower on
+// every ResNet-18 shape (profiles/r2_alpha_one_launch_ab.log).
 //
 // Every kernel takes a table of up to kMaxPrepSeg weights ("segments"), so the adaShift
-// forward of ALL the convs of a block is one launch and their alpha backward two (stage 1
-// over every segment's tiles, stage 2 over every segment's input channels): the weights of
-// a block depend only on alpha, which is fixed for the iteration
+// forward of ALL the convs of a block is one launch and their alpha backward two: the
+// weights of a block depend only on alpha, which is fixed for the iteration
 // (quant/_engine.py stash_block_weights).
 #include <stdlib.h>
 
@@ -28,6 +28,9 @@ namespace ssq {
 constexpr int kMaxPrepS = 4;
 constexpr int kRBP = 8;            // rows per load batch
 constexpr int kMaxPrepSeg = 8;     // weights per launch (a block has <= 4 convs)
+// last-arriver counters of the one-launch alpha backward: one per (segment, column block)
+constexpr uint32_t kAlphaTickets = 8192;
+__device__ unsigned g_alpha_tickets[kAlphaTickets];
 
 __global__ __launch_bounds__(kBlock) void adashift_prepare_kernel(
     const float* __restrict__ W, const float* __restrict__ beta, const float* __restrict__ delta,
@@ -84,6 +87,11 @@ static ColTiling col_tiling_prep(const Geo& g) {
   return t;
 }
 
+static bool alpha_one_launch() {
+  static const bool on = prep_env("SSQ_ALPHA_ONE_LAUNCH", 0) != 0;
+  return on;
+}
+
 struct PrepSeg {
   const uint32_t* fpack;
   const float* hterm;
@@ -99,6 +107,7 @@ struct PrepSeg {
   ColTiling tl;
   uint32_t blk0;     // first workgroup of this segment (forward / stage 1)
   uint32_t wave0;    // first wave of this segment (stage 2: one wave per input channel)
+  uint32_t tick0;    // first last-arriver counter of this segment (one-launch form)
   float lo, hi;
 };
 struct PrepTable {
@@ -172,8 +181,10 @@ __global__ __launch_bounds__(kBlock) void shift_fwd_prep(PrepTable tab) {
 
 // Backward stage 1: sums of g_int * F_i per (chunk, ci) into
 // part[(ci*nchunk + chunk)*S + i] (input-channel-major: stage 2 reads one coalesced run).
-template <int NS>
-__global__ __launch_bounds__(kBlock) void alpha_bwd_prep(PrepTable tab) {
+template <int NS, bool FUSED>
+__global__ __launch_bounds__(kBlock) void alpha_bwd_prep(PrepTable tab, float reg_lambda,
+                                                          float reg_b,
+                                                          const float* __restrict__ reg_dev) {
   __shared__ double red[kBlock * NS];
   const PrepSeg& sg = tab.s[find_seg<false>(tab, blockIdx.x)];
   const Geo& g = sg.g;
@@ -238,9 +249,17 @@ __global__ __launch_bounds__(kBlock) void alpha_bwd_prep(PrepTable tab) {
     for (int i = 0; i < NS; ++i) {
       double sum = 0.0;
       for (uint32_t k = 0; k < g.K; ++k) sum += red[(t * g.K + k) * NS + i];
-      sg.part[((size_t)(ci0 + t) * sg.tl.nchunk + by) * NS + i] = sum;
+      double* dst = sg.part + ((size_t)(ci0 + t) * sg.tl.nchunk + by) * NS + i;
+      if (FUSED) st_sc1(dst, sum);
+      else *dst = sum;
     }
   }
+  if (!FUSED) return;
+  // the last of the column block's nchunk workgroups to finish reduces its input channels
+  if (!arrive_last(&g_alpha_tickets[sg.tick0 + bx], sg.tl.nchunk, (int*)red)) return;
+  const uint32_t w = threadIdx.x / kWave, lane = threadIdx.x & (kWave - 1);
+  for (uint32_t c = w; c < nci; c += kBlock / kWave)
+    alpha_reduce_ci<NS, true>(sg, ci0 + c, lane, reg_lambda, reg_b, reg_dev);
 }
 
 // Stage 2: one wave per (segment, input channel).  Every load the wave needs (alpha row,
@@ -249,15 +268,17 @@ __global__ __launch_bounds__(kBlock) void alpha_bwd_prep(PrepTable tab) {
 // fixed shuffle tree adds the lanes and lane 0 applies the softmax/clamp backward (same
 // values, same order as alpha_chain).  Deterministic, no atomics.
 constexpr uint32_t kMaxPrepChunkRounds = kMaxChunks / kWave;
-template <int NS>
-__global__ __launch_bounds__(kBlock) void alpha_bwd_prep_stage2(PrepTable tab, float reg_lambda,
-                                                                 float reg_b,
-                                                                 const float* __restrict__ reg_dev) {
-  const uint32_t wave = blockIdx.x * (kBlock / kWave) + threadIdx.x / kWave;
-  const uint32_t lane = threadIdx.x & (kWave - 1);
-  const PrepSeg& sg = tab.s[find_seg<true>(tab, __builtin_amdgcn_readfirstlane(wave))];
-  const uint32_t ci = wave - sg.wave0;
-  if (ci >= sg.g.Ci) return;
+
+// Input channel ci's alpha gradient from its chunk partials, by one wave: every load the
+// wave needs (alpha row, the device (lambda, b) pair, lane c's chunks c, c+64, ... -- one
+// coalesced run per round) is issued before any math; lanes i < S evaluate shift i's
+// regulariser term meanwhile; a fixed shuffle tree adds the lanes and lane 0 applies the
+// softmax/clamp backward (same values, same order as alpha_chain).  SC1: the partials were
+// handed off inside this launch (write-through loads, see arrive_last).
+template <int NS, bool SC1>
+__device__ __forceinline__ void alpha_reduce_ci(const PrepSeg& sg, uint32_t ci, uint32_t lane,
+                                                float reg_lambda, float reg_b,
+                                                const float* __restrict__ reg_dev) {
   const uint32_t nchunk = sg.tl.nchunk;
   float a[kMaxS];
   load_row(sg.alpha, ci, NS, a);
@@ -271,7 +292,10 @@ __global__ __launch_bounds__(kBlock) void alpha_bwd_prep_stage2(PrepTable tab, f
   for (uint32_t r = 0; r < kMaxPrepChunkRounds; ++r) {
     const uint32_t c = lane + r * kWave;
 #pragma unroll
-    for (int i = 0; i < NS; ++i) v[r][i] = c < nchunk ? pp[(size_t)c * NS + i] : 0.0;
+    for (int i = 0; i < NS; ++i) {
+      const double* q = pp + (size_t)c * NS + i;
+      v[r][i] = c < nchunk ? (SC1 ? ld_sc1(q) : *q) : 0.0;
+    }
   }
   float sm[kMaxS], p[kMaxS];
   soft_targets<kMaxS>(a, NS, sm, p);
@@ -312,6 +336,19 @@ __global__ __launch_bounds__(kBlock) void alpha_bwd_prep_stage2(PrepTable tab, f
 #pragma unroll
   for (int i = 0; i < NS; ++i) sg.galpha[(size_t)ci * NS + i] = ga[i];
   if (sg.reg_vals) sg.reg_vals[ci] = reg;
+}
+
+// Stage 2 (two-launch form): one wave per (segment, input channel).
+template <int NS>
+__global__ __launch_bounds__(kBlock) void alpha_bwd_prep_stage2(PrepTable tab, float reg_lambda,
+                                                                 float reg_b,
+                                                                 const float* __restrict__ reg_dev) {
+  const uint32_t wave = blockIdx.x * (kBlock / kWave) + threadIdx.x / kWave;
+  const uint32_t lane = threadIdx.x & (kWave - 1);
+  const PrepSeg& sg = tab.s[find_seg<true>(tab, __builtin_amdgcn_readfirstlane(wave))];
+  const uint32_t ci = wave - sg.wave0;
+  if (ci >= sg.g.Ci) return;
+  alpha_reduce_ci<NS, false>(sg, ci, lane, reg_lambda, reg_b, reg_dev);
 }
 
 // ------------------------------------------------------------------ host side
@@ -403,6 +440,7 @@ extern "C" int ssq_adashift_fwd_prepared_multi(int nseg, const uint32_t* const* 
       sg.What = What[base + k];
       sg.blk0 = blk;
       sg.wave0 = 0;
+      sg.tick0 = 0;
       blk += sg.tl.ncolblk * sg.tl.nchunk;
     }
 #define SSQ_FWDP(NS)                                                                         \
@@ -457,7 +495,7 @@ extern "C" int ssq_adashift_bwd_prepared_multi(
   for (int base = 0; base < nseg; base += kMaxPrepSeg) {
     PrepTable tab;
     tab.nseg = nseg - base < kMaxPrepSeg ? nseg - base : kMaxPrepSeg;
-    uint32_t blk = 0, waves = 0;
+    uint32_t blk = 0, waves = 0, ticks = 0;
     for (int k = 0; k < tab.nseg; ++k) {
       PrepSeg& sg = tab.s[k];
       const int i = base + k;
@@ -471,15 +509,29 @@ extern "C" int ssq_adashift_bwd_prepared_multi(
       wsp += part_bytes(sg, S);
       sg.blk0 = blk;
       sg.wave0 = waves;
+      sg.tick0 = ticks;
       blk += sg.tl.ncolblk * sg.tl.nchunk;
       waves += sg.g.Ci;
+      ticks += sg.tl.ncolblk;
     }
     const unsigned blocks2 = (waves + kBlock / kWave - 1) / (kBlock / kWave);
+    // two launches by default; SSQ_ALPHA_ONE_LAUNCH=1 (A/B knob) reduces in the same
+    // launch (last arriver per column block) while the counters last -- measured slower
+    // (64x64x3x3 9.6 -> 26 us, 512x256x1x1 9.8 -> 135 us): its reducer walks the column
+    // block's input channels with one wave each, serially, where stage 2 spreads them
+    // over the chip
+    const bool fused = alpha_one_launch() && ticks <= kAlphaTickets;
 #define SSQ_BWDP(NS)                                                                          \
   do {                                                                                        \
-    hipLaunchKernelGGL((alpha_bwd_prep<NS>), dim3(blk), dim3(kBlock), 0, s, tab);             \
-    hipLaunchKernelGGL((alpha_bwd_prep_stage2<NS>), dim3(blocks2), dim3(kBlock), 0, s, tab,   \
-                       reg_lambda, reg_b, reg_dev);                                           \
+    if (fused) {                                                                              \
+      hipLaunchKernelGGL((alpha_bwd_prep<NS, true>), dim3(blk), dim3(kBlock), 0, s, tab,      \
+                         reg_lambda, reg_b, reg_dev);                                         \
+    } else {                                                                                  \
+      hipLaunchKernelGGL((alpha_bwd_prep<NS, false>), dim3(blk), dim3(kBlock), 0, s, tab,     \
+                         reg_lambda, reg_b, reg_dev);                                         \
+      hipLaunchKernelGGL((alpha_bwd_prep_stage2<NS>), dim3(blocks2), dim3(kBlock), 0, s, tab, \
+                         reg_lambda, reg_b, reg_dev);                                         \
+    }                                                                                         \
   } while (0)
     switch (S) {
       case 1: SSQ_BWDP(1); break;

@@ -3,8 +3,11 @@
 //
 // lp_loss (quant_layer.py:25-32) is five eager launches plus five more in autograd; here
 // one pass reads pred and tgt and writes d loss/d pred (12 B/elem), with a deterministic
-// two-stage reduction of the loss value.  For p == 2 the gradient is bit-identical to
-// PyTorch's: (1/M) * (2*|d|) * sgn(d).
+// reduction of the loss value (workgroup partials summed in index order by a 1-workgroup
+// finalize launch, or by the last workgroup to finish: SSQ_LOSS_ONE_LAUNCH).  For p == 2
+// the gradient is bit-identical to PyTorch's: (1/M) * (2*|d|) * sgn(d).
+#include <stdlib.h>
+
 #include <type_traits>
 
 #include "ssq_common.h"
@@ -12,6 +15,7 @@
 namespace ssq {
 
 constexpr int kLossBlocks = 1024;
+__device__ unsigned g_loss_ticket;   // lp_loss_kernel's last-arriver counter (zero at rest)
 
 // |d|^p and its derivative p*|d|^(p-1) for one element.
 template <int PMODE>  // 0: p == 2, 1: p == 1, 2: general p
@@ -72,7 +76,8 @@ __global__ __launch_bounds__(kBlock) void lp_loss_kernel(const float* __restrict
                                                          const float* __restrict__ gscale,
                                                          int relu_mask, int vec, TgtRows tr4,
                                                          TgtRows tr1,
-                                                         double* __restrict__ part) {
+                                                         double* __restrict__ part, double m,
+                                                         float* __restrict__ loss_out) {
   __shared__ double red[16];
   double acc = 0.0;
   const float gs = gscale ? gscale[0] : 1.0f;
@@ -99,14 +104,39 @@ __global__ __launch_bounds__(kBlock) void lp_loss_kernel(const float* __restrict
   }
   if (!part) return;
   acc = block_sum(acc, red);
-  if (threadIdx.x == 0) part[blockIdx.x] = acc;
+  if (!loss_out) {                     // two-launch form: lp_loss_finalize sums the partials
+    if (threadIdx.x == 0) part[blockIdx.x] = acc;
+    return;
+  }
+  if (threadIdx.x == 0) st_sc1(part + blockIdx.x, acc);
+  // one-launch form: the last workgroup to finish sums the partials in index order
+  if (!arrive_last(&g_loss_ticket, gridDim.x, (int*)red)) return;
+  double v[kLossBlocks / kBlock];
+#pragma unroll
+  for (int k = 0; k < kLossBlocks / kBlock; ++k) {
+    const int i = threadIdx.x + k * kBlock;
+    v[k] = i < (int)gridDim.x ? ld_sc1(part + i) : 0.0;
+  }
+  double a = 0.0;
+#pragma unroll
+  for (int k = 0; k < kLossBlocks / kBlock; ++k) a += v[k];
+  a = block_sum(a, red);
+  if (threadIdx.x == 0) loss_out[0] = (float)(a / m);
 }
 
+// two-launch form: the block partials summed in index order (every load issued first)
 __global__ void lp_loss_finalize(const double* __restrict__ part, int nblk, double m,
                                  float* __restrict__ out) {
   __shared__ double red[16];
+  double v[kLossBlocks / kBlock];
+#pragma unroll
+  for (int k = 0; k < kLossBlocks / kBlock; ++k) {
+    const int i = threadIdx.x + k * kBlock;
+    v[k] = i < nblk ? part[i] : 0.0;
+  }
   double a = 0.0;
-  for (int i = threadIdx.x; i < nblk; i += blockDim.x) a += part[i];
+#pragma unroll
+  for (int k = 0; k < kLossBlocks / kBlock; ++k) a += v[k];
   a = block_sum(a, red);
   if (threadIdx.x == 0) out[0] = (float)(a / m);
 }
@@ -371,17 +401,19 @@ __global__ __launch_bounds__(kBlock) void epilogue_bwd_rows(
   }
 }
 
-// blocks [0, nb): per-channel gamma / phi gradients (sum over n in order); block nb: the
-// act quantizer's delta / zp gradients (rows in a fixed order, as fq_bwd_finalize).
+// blocks [0, nb): per-channel gamma / phi gradients (sum over n in order); block nb (when
+// launched): the act quantizer's delta / zp gradients (rows in a fixed order, as
+// fq_bwd_finalize).
 __global__ __launch_bounds__(kBlock) void epilogue_bwd_finalize(
-    const double* __restrict__ part, uint32_t N, uint32_t C, float* __restrict__ ggamma,
-    float* __restrict__ gphi, float* __restrict__ gdelta, float* __restrict__ gzp) {
+    const double* __restrict__ part, uint32_t N, uint32_t C, uint32_t nb,
+    float* __restrict__ ggamma, float* __restrict__ gphi, float* __restrict__ gdelta,
+    float* __restrict__ gzp) {
   __shared__ double red[16];
-  const uint32_t nb = (C + kBlock - 1) / kBlock;
   if (blockIdx.x < nb) {
     const uint32_t c = blockIdx.x * kBlock + threadIdx.x;
     if (c >= C) return;
     double sg = 0, sp = 0;
+#pragma unroll 8
     for (uint32_t n = 0; n < N; ++n) {
       sg += part[((int64_t)n * C + c) * kEpiParts + 0];
       sp += part[((int64_t)n * C + c) * kEpiParts + 1];
@@ -433,9 +465,16 @@ static int lp_loss(const char* what, const float* pred, const float* tgt, const 
                                : (p == 1.0f ? lp_loss_kernel<1, true> : lp_loss_kernel<2, true>))
                   : (p == 2.0f ? lp_loss_kernel<0, false>
                                : (p == 1.0f ? lp_loss_kernel<1, false> : lp_loss_kernel<2, false>));
+  // A/B knob SSQ_LOSS_ONE_LAUNCH: 1 finalises the loss value in the same launch (last
+  // workgroup to arrive), 0 in a 1-workgroup finalize launch
+  static const bool one = [] {
+    const char* e = getenv("SSQ_LOSS_ONE_LAUNCH");
+    return e && *e ? atoi(e) != 0 : false;
+  }();
+  const bool fuse = one && loss_out;
   hipLaunchKernelGGL(k, dim3(grid), dim3(kBlock), 0, s, pred, tgt, n, p, inv_m, grad, gscale,
-                     relu_mask, vec, tr4, tr1, part);
-  if (loss_out)
+                     relu_mask, vec, tr4, tr1, part, (double)M, fuse ? loss_out : nullptr);
+  if (loss_out && !fuse)
     hipLaunchKernelGGL(lp_loss_finalize, dim3(1), dim3(kBlock), 0, s, (const double*)part, grid,
                        (double)M, loss_out);
   return check_launch(what);
@@ -589,9 +628,13 @@ extern "C" int ssq_epilogue_bwd(const float* g, const float* y, const float* bia
 #undef SSQ_EB1
 #undef SSQ_EB
   if (ggamma || gphi || gdelta || gzp) {
-    const unsigned nb = (unsigned)((C + kBlock - 1) / kBlock);
-    hipLaunchKernelGGL(epilogue_bwd_finalize, dim3(nb + 1), dim3(kBlock), 0, s,
-                       (const double*)part, (uint32_t)N, (uint32_t)C, ggamma, gphi, gdelta, gzp);
+    // blocks [0, nb) only when gamma / phi are wanted; block nb (the act quantizer's four
+    // sums over every row, one workgroup) only when delta / zp are
+    const unsigned nb = (ggamma || gphi) ? (unsigned)((C + kBlock - 1) / kBlock) : 0u;
+    const unsigned nq = (gdelta || gzp) ? 1u : 0u;
+    hipLaunchKernelGGL(epilogue_bwd_finalize, dim3(nb + nq), dim3(kBlock), 0, s,
+                       (const double*)part, (uint32_t)N, (uint32_t)C, nb, ggamma, gphi, gdelta,
+                       gzp);
   }
   return check_launch("ssq_epilogue_bwd");
 }

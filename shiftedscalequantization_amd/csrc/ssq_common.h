@@ -199,6 +199,46 @@ __device__ __forceinline__ double block_sum(double v, double* lds /* >= 16 */) {
   return lds[0];
 }
 
+// ---------------------------------------------------------------- last-arriver hand-off
+// One launch instead of a partials kernel + a 1-workgroup finalize kernel
+// (cdna_hip_programming.md Guideline 16, counter form with write-through partials): every
+// workgroup stores its partials write-through (sc1, agent scope: no release fence), drains
+// them (every wave s_waitcnt vmcnt(0), then the barrier), and one lane takes a ticket
+// (relaxed agent-scope fetch_add on a per-reduction counter); the workgroup that draws
+// the last ticket reads every partial with sc1 loads (each of them: no acquire fence
+// needed) in a fixed order -- deterministic -- and resets the counter for the next
+// launch.  Counters are zero-initialised device globals (tickets below), so each
+// reduction owns its counters and two launches that share one must not run concurrently
+// (every caller here issues them on one stream, in order).
+typedef __attribute__((address_space(1))) unsigned long long gu64_t;
+typedef __attribute__((address_space(1))) unsigned int gu32_t;
+
+__device__ __forceinline__ void st_sc1(double* p, double v) {
+  __hip_atomic_store((gu64_t*)p, (unsigned long long)__double_as_longlong(v), __ATOMIC_RELAXED,
+                     __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ double ld_sc1(const double* p) {
+  return __longlong_as_double(
+      (long long)__hip_atomic_load((gu64_t*)p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+}
+// Every thread of the workgroup calls it after its partial stores; true in every thread of
+// the last-arriving workgroup of `nblocks` sharing `ticket`.  `flag`: one LDS word.
+__device__ __forceinline__ bool arrive_last(unsigned* ticket, unsigned nblocks, int* flag) {
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    const unsigned t = __hip_atomic_fetch_add((gu32_t*)ticket, 1u, __ATOMIC_RELAXED,
+                                              __HIP_MEMORY_SCOPE_AGENT);
+    *flag = t == nblocks - 1;
+  }
+  __syncthreads();
+  const bool last = *flag != 0;
+  if (last && threadIdx.x == 0)
+    __hip_atomic_store((gu32_t*)ticket, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");   // keep the sc1 loads below
+  return last;
+}
+
 // one element of the uniform affine fake-quant (quant_layer.py:92-98)
 struct QParams {
   float d, z, lo, hi;
