@@ -7,6 +7,7 @@
 // +1 B/elem when int codes are emitted.
 #include <stdarg.h>
 #include <stdio.h>
+#include <stdlib.h>
 
 #include "ssq_common.h"
 
@@ -188,23 +189,34 @@ struct Seg {
   uint32_t vec;    // x, y 16-B (codes 4-B) aligned: float4 path
 };
 constexpr int kMaxSeg = 48;      // keeps the by-value table under 4 KiB of kernel arguments
-constexpr int kTile = 4096;      // elements per workgroup: 4 float4 per thread
+constexpr int kTile = 4096;      // elements per workgroup: 4 float4 per thread (8 measured no faster)
 struct SegTable {
   Seg s[kMaxSeg];
   int nseg;
 };
 
 // One workgroup = one tile of one segment.  The (delta, zp) of every channel the tile
-// touches are staged in LDS once; each thread then issues its 4 float4 loads before any
-// math (16 B/lane, 4 KiB per wave in flight) and finds channels with a magic-number
+// touches are staged in LDS once; each thread then issues its U float4 loads before any
+// math (16 B/lane, U KiB per wave in flight) and finds channels with a magic-number
 // division (no 64-bit divides).  A float4 may straddle a channel boundary (inner % 4).
-__global__ __launch_bounds__(kBlock) void fq_fwd_multi_kernel(SegTable tab) {
-  __shared__ float sd[kTile + 2], sz[kTile + 2];
+// The LDS stage is dynamic, sized by the table's shortest rows (tile_channels): two
+// floats per channel a tile can touch, not per element, so long rows leave the CU's
+// LDS free for more resident workgroups.
+inline uint32_t tile_channels(uint32_t tile, uint32_t min_inner) {
+  const uint32_t c = tile / min_inner + 2;
+  return c < tile ? c : tile;
+}
+template <int U>
+__global__ __launch_bounds__(kBlock) void fq_fwd_multi_kernel(SegTable tab, uint32_t cap) {
+  constexpr uint32_t TILE = U * 4 * kBlock;
+  extern __shared__ float stage[];
+  float* sd = stage;
+  float* sz = stage + cap;
   int si = 0;
   while (si + 1 < tab.nseg && blockIdx.x >= tab.s[si + 1].blk0) ++si;
   const Seg& sg = tab.s[si];
-  const uint32_t t0 = (blockIdx.x - sg.blk0) * (uint32_t)kTile;
-  const uint32_t t1 = min(t0 + (uint32_t)kTile, sg.n);
+  const uint32_t t0 = (blockIdx.x - sg.blk0) * TILE;
+  const uint32_t t1 = min(t0 + TILE, sg.n);
   const uint32_t c0 = fdiv(t0, sg.div_inner), c1 = fdiv(t1 - 1, sg.div_inner);
   for (uint32_t c = c0 + threadIdx.x; c <= c1; c += blockDim.x) {
     sd[c - c0] = __fmul_rn(sg.delta[c % sg.nch], sg.scale);
@@ -214,7 +226,6 @@ __global__ __launch_bounds__(kBlock) void fq_fwd_multi_kernel(SegTable tab) {
   const float lo = sg.lo, hi = sg.hi;
   uint32_t e_tail = t0;
   if (sg.vec) {
-    constexpr int U = kTile / 4 / kBlock;
     const uint32_t v0 = t0 / 4, v1 = t1 / 4;  // whole float4s of the tile
     const f32x4* xv = (const f32x4*)sg.x;
     f32x4* yv = (f32x4*)sg.y;
@@ -597,14 +608,16 @@ extern "C" int ssq_fq_fwd(const float* x, float* y, void* codes, const float* de
       else
         launch_stream<FqPt>(v, grid, block, s, xv, yv, cv, delta, zp, n4, scale, lo, hi, chunk,
                             v.rcp ? 1 : 0);
-    } else if (n < (1ll << 31) && (n + kTile - 1) / kTile < (1ll << 31)) {
+    } else if (n < (1ll << 31)) {
       // per-channel: the LDS-staged tile kernel with one segment (no 64-bit divides)
       SegTable tab;
       tab.nseg = 1;
       tab.s[0] = Seg{x, y, delta, zp, (uint8_t*)codes, (uint32_t)n, 0u, (uint32_t)inner,
                      (uint32_t)nch, lo, hi, scale, make_fastdiv((uint32_t)inner), 1u};
-      hipLaunchKernelGGL(fq_fwd_multi_kernel, dim3((unsigned)((n + kTile - 1) / kTile)),
-                         dim3(kBlock), 0, s, tab);
+      const uint32_t cap = tile_channels(kTile, (uint32_t)inner);
+      hipLaunchKernelGGL(fq_fwd_multi_kernel<kTile / 4 / kBlock>,
+                         dim3((unsigned)((n + kTile - 1) / kTile)), dim3(kBlock),
+                         2 * cap * sizeof(float), s, tab, cap);
       return check_launch("ssq_fq_fwd");
     } else {
       SSQ_REQUIRE(inner < (1ll << 31) && nch < (1ll << 31), SSQ_E_ARG, "ssq_fq_fwd: dims");
@@ -646,6 +659,7 @@ extern "C" int ssq_fq_fwd_multi(int nseg, const float* const* x, float* const* y
     SegTable tab;
     tab.nseg = nseg - base < kMaxSeg ? nseg - base : kMaxSeg;
     int64_t blk = 0;
+    uint32_t min_inner = UINT32_MAX;
     for (int k = 0; k < tab.nseg; ++k) {
       const int i = base + k;
       const bool vec = aligned16(x[i]) && aligned16(y[i]);
@@ -653,10 +667,12 @@ extern "C" int ssq_fq_fwd_multi(int nseg, const float* const* x, float* const* y
                      (uint32_t)inner[i], (uint32_t)nch[i], (float)qmin[i], (float)qmax[i], 1.0f,
                      make_fastdiv((uint32_t)inner[i]), vec ? 1u : 0u};
       blk += (n[i] + kTile - 1) / kTile;
+      if ((uint32_t)inner[i] < min_inner) min_inner = (uint32_t)inner[i];
     }
     SSQ_REQUIRE(blk < (1ll << 31), SSQ_E_ARG, "ssq_fq_fwd_multi: too many tiles");
-    hipLaunchKernelGGL(fq_fwd_multi_kernel, dim3((unsigned)blk), dim3(kBlock), 0,
-                       (hipStream_t)stream, tab);
+    const uint32_t cap = tile_channels(kTile, min_inner);
+    hipLaunchKernelGGL(fq_fwd_multi_kernel<kTile / 4 / kBlock>, dim3((unsigned)blk), dim3(kBlock),
+                       2 * cap * sizeof(float), (hipStream_t)stream, tab, cap);
     const int rc = check_launch("ssq_fq_fwd_multi");
     if (rc) return rc;
   }

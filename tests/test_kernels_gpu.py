@@ -182,6 +182,20 @@ def test_fq_per_channel_unaligned(K):
     np.testing.assert_array_equal(host(y2), R.fake_quant(host(view), d, z, 8)[0])
 
 
+@pytest.mark.parametrize("shape", [(96, 2048, 3, 3), (1024, 512, 3, 3), (50, 65, 2, 2),
+                                   (1000, 512)])
+def test_fq_per_channel_long_rows(K, shape):
+    """Per-channel q/dq with rows of >= 256 elements (fq_fwd_rows: wave-uniform channel
+    parameters, waves spanning two rows), with codes: bit-exact against the oracle."""
+    gen = torch.Generator().manual_seed(sum(shape))
+    x = torch.randn(shape, generator=gen) * 0.05
+    d, z, _ = R.init_scale(x.numpy(), 2, False, True, "max")
+    y, c = K.fake_quant_fwd(x.cuda(), dev(d), dev(z), 2, codes=True)
+    ry, rq = R.fake_quant(x.numpy(), d, z, 2)
+    np.testing.assert_array_equal(host(y).view(np.int32), ry.view(np.int32))
+    np.testing.assert_array_equal(c.cpu().numpy().ravel(), rq.astype(np.uint8).ravel())
+
+
 def test_fq_multi_segment(K):
     gen = torch.Generator().manual_seed(11)
     shapes = [(64, 3, 7, 7), (64, 64, 3, 3), (128, 64, 1, 1), (1000, 512), (8, 1, 3, 3)]
