@@ -14,6 +14,8 @@ import pytest
 import torch
 import torch.nn as nn
 
+from conftest import assert_walk_bounded
+
 pytestmark = pytest.mark.gpu
 SHIFTS = [31 / 32, 33 / 32, 1.0]
 
@@ -216,13 +218,15 @@ def test_block_recon_shiftedScale_matches_reference(Q, golden):
     fin = np.abs(np.array(l1 + l2) - np.concatenate([g["s_final"], g["a_final"]])) / \
         np.abs(np.concatenate([g["s_final"], g["a_final"]]))
     stats = {"shift_total_rel_err": s_err, "ada_total_rel_err": a_err, "final_rel_err": fin.max()}
+    devs = {}
     for n in ("conv1", "conv2", "downsample"):
         m = getattr(block, n)
         q = m.weight_quantizer
-        stats[n + "_alpha_dev"] = np.abs(host(q.alpha) - g[n + "_s_alpha"]).max()
+        devs[n] = (np.abs(host(q.alpha) - g[n + "_s_alpha"]), np.abs(host(q.beta) - g[n + "_a_beta"]))
+        stats[n + "_alpha_dev"] = devs[n][0].max()
         dsel = host(q.delta)
         stats[n + "_delta_flips"] = int(np.sum(dsel != g[n + "_a_delta"]))
-        stats[n + "_beta_dev"] = np.abs(host(q.beta) - g[n + "_a_beta"]).max()
+        stats[n + "_beta_dev"] = devs[n][1].max()
         with torch.no_grad():
             what = host(q(m.weight))
         stats[n + "_hard_flips"] = int(np.sum(what != g[n + "_a_what"]))
@@ -233,9 +237,9 @@ def test_block_recon_shiftedScale_matches_reference(Q, golden):
     assert s_err <= 1e-5 and a_err <= 1e-5
     assert fin.max() <= 1e-5
     for n in ("conv1", "conv2", "downsample"):
-        assert stats[n + "_alpha_dev"] <= 1e-5, n
+        assert_walk_bounded(devs[n][0], 1e-5, iters * 2e-3, what=n + " alpha")
         assert stats[n + "_delta_flips"] <= 0.005 * g[n + "_a_delta"].size, n
-        assert stats[n + "_beta_dev"] <= 1e-4, n
+        assert_walk_bounded(devs[n][1], 1e-4, iters * 2e-3, frac=0.01, what=n + " beta")
         assert stats[n + "_hard_flips"] <= 0.002 * stats[n + "_n"], n
 
 
