@@ -349,10 +349,11 @@ int ssq_adam(int nseg, float* const* p, const float* const* g, float* const* m,
  * summed in a fixed order: bit-identical run to run.  OW <= 128, tensors < 2^31 elements. */
 /* A/B knob (returns the previous value; out-of-range values only query): non-depthwise
  * weight-gradient form, 0 auto, 1 input-row-tile kernel (+ 1x1 GEMM), 2 im2col-DMA kernel,
- * 3 band kernel (3x3 / pad 1 / stride 1-2 / OW % 4 == 0 shapes; others as 1). */
+ * 3 band kernel (3x3 / pad 1 / stride 1-2 / Cin, Cout multiples of 32; others as 1). */
 int ssq_conv_wgrad_set_form(int form);
 /* The kernel ssq_conv_wgrad runs for a shape under the current form: 0 unsupported,
- * 1 input-row tile, 2 im2col-DMA, 3 band, 4 1x1 GEMM, 5 depthwise reduction. */
+ * 1 input-row tile, 2 im2col-DMA, 3 band (16-byte staging), 4 1x1 GEMM, 5 depthwise
+ * reduction, 6 band (4-byte staging: planes whose rows are not 16-B aligned). */
 int ssq_conv_wgrad_kind(int64_t Nb, int64_t C, int64_t H, int64_t W, int64_t Co, int64_t R,
                         int64_t S, int64_t stride, int64_t pad, int64_t groups);
 size_t ssq_conv_wgrad_workspace_size(int64_t Nb, int64_t C, int64_t H, int64_t W, int64_t Co,

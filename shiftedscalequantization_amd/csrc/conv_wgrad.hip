@@ -716,36 +716,42 @@ static int wgrad_plan(int64_t Nb, int64_t C, int64_t H, int64_t W, int64_t Co, i
 }
 
 // ------------------------------------------------------------------ band form (3x3, pad 1)
-// Ungrouped 3x3 / pad 1 convs at stride 1 or 2 whose output rows are whole float4s
-// (OW % 4 == 0: ResNet layer1 / layer2 shapes).  The GEMM columns are regrouped as
-// (tap, ci): a wave owns 32 co x 32 ci x all 9 taps (9 v_mfma_f32_32x32x2_f32
-// accumulators), so one dy fragment feeds 9 MFMAs and the 9 taps of an input channel are
-// 3 row windows of the same staged x rows.  K = (n, output pixel) is walked in bands of
-// RB whole output rows of one sample: per band the workgroup stages
+// Ungrouped 3x3 / pad 1 convs at stride 1 or 2 with Cin, Cout multiples of 32 (every
+// ResNet-18 3x3 conv).  The GEMM columns are regrouped as (tap, ci): a wave owns 32 co x
+// 32 ci x all 9 taps (9 v_mfma_f32_32x32x2_f32 accumulators), so one dy fragment feeds 9
+// MFMAs and the 9 taps of an input channel are 3 row windows of the same staged x rows.
+// K = (n, output pixel) is walked in bands of RB whole output rows of one sample: per band
+// the workgroup stages
 //   A[co][q]          = dy[n, co, oh0 + q / OW, q % OW]              (q < RB * OW)
 //   X[ci][ir][4 + iw] = x[n, ci, oh0*st - 1 + ir, iw]                (ir < (RB-1)*st + 3)
-// with 16-byte LDS-DMA (global_load_lds_dwordx4); every 16-byte LDS piece of a buffer is
-// written by the DMA -- from dy / x or, for padding columns, out-of-image rows and pitch
-// pads, from a zero page -- and the per-lane source offsets are band-independent, so they
-// are computed once per kernel (no division in the staging).  A lane walks 4 consecutive
-// pixels of its lane half per step: A by one ds_read_b128, each tap row's 4 x 3 window by
-// b32 + b128 + b32 (stride 1) or b32 + 2 x b128 (stride 2), 36 MFMAs per 10 LDS reads.
-// Pitches are odd multiples of 4 floats (conflict-free b128 reads).  Partials go to
-// part[split][tap][co][ci] (coalesced) and wgrad_stage2 sums the splits in a fixed order
-// into dW[co][ci][tap]: deterministic.
-constexpr int kBandMaxNI = 20;     // DMA instructions per wave per band (80 KB buffers)
+// by LDS-DMA into a double buffer, every LDS piece of which is DMA-written -- from dy / x
+// or, for padding columns, out-of-image rows and pitch pads, from a zero page:
+//   * 16-byte pieces (global_load_lds_dwordx4) when rows are 16-B aligned (W, OW, the
+//     band's dy span multiples of 4 floats): the per-lane sources are band-independent,
+//     computed once per kernel (no division in the staging);
+//   * 4-byte pieces otherwise (14x14 and 7x7 planes), sources by magic-number division.
+// A lane walks V consecutive pixels of its lane half per step (V = 4, 2 or 1 by OW): A by
+// one ds_read of V floats, each tap row's window of (V-1)*st + 3 floats, 9*V MFMAs per
+// step, the next step's operands read during this step's MFMAs.  A band whose pixel count
+// does not split into the two lane halves is padded with pixels whose A is zero (their x
+// reads are clamped to the last real pixel).  Pitches are odd multiples of 4 floats
+// (conflict-free 16-B reads).  Partials go to part[split][tap][co][ci] (coalesced) and
+// wgrad_stage2 sums the splits in a fixed order into dW[co][ci][tap]: deterministic.
+constexpr int kBandMaxNI = 20;     // 16-B DMA instructions per wave per band (80 KB buffers)
 __device__ float g_band_zero_page[4 * 64];   // zero-initialised, never written
 
 struct BandGeo {
   int C, H, W, Co, OW, OHW, Cig, Cog;
-  int RB, Q, PA, IR, PXrow, PXci;
+  int RB, Q, Qp, PA, IR, PXrow, PXci;
   int TMc, CBc;          // workgroup tile: co rows, input channels
   int bufsz;             // floats per LDS buffer (a multiple of 1024)
+  int d16;               // 16-byte DMA with precomputed sources (else 4-byte pieces)
   int ni_w;              // DMA instructions per wave per band
   int bands_per_n, nchunks, cps, nsplit, m_tiles, n_tiles, remap;
+  FastDiv dPA, dPXci, dPXrow;
 };
 
-template <int WMX, int ST>
+template <int WMX, int ST, int V>
 __global__ __launch_bounds__(256, 1) void wgrad_band_stage1(const float* __restrict__ x,
                                                             const float* __restrict__ dy,
                                                             BandGeo g, float* __restrict__ part) {
@@ -765,15 +771,15 @@ __global__ __launch_bounds__(256, 1) void wgrad_band_stage1(const float* __restr
   const int mt = tile / g.n_tiles, nt = tile - mt * g.n_tiles;
   const int co0 = mt * g.TMc, ci0 = nt * g.CBc;
   const int c_begin = split * g.cps, c_end = min(c_begin + g.cps, g.nchunks);
-
-  // per-lane DMA sources, band-independent: kind 0 zero page, 1 dy (+ soff), 2 x row ir
-  int soff[kBandMaxNI], meta[kBandMaxNI];
   const int abytes = g.TMc * g.PA;
+
+  // 16-B form: per-lane DMA sources, band-independent: kind 0 zero page, 1 dy, 2 x row ir
+  int soff[kBandMaxNI], meta[kBandMaxNI];
 #pragma unroll
   for (int i = 0; i < kBandMaxNI; ++i) {
     soff[i] = 0;
     meta[i] = 0;
-    if (i < g.ni_w) {
+    if (g.d16 && i < g.ni_w) {
       const int o = (wave + 4 * i) * 256 + lane * 4;
       if (o < abytes) {
         const int row = o / g.PA, col = o - row * g.PA;
@@ -792,79 +798,145 @@ __global__ __launch_bounds__(256, 1) void wgrad_band_stage1(const float* __restr
       }
     }
   }
-  const float* zero = g_band_zero_page + lane * 4;
-  auto stage = [&](int c, int b) {
+  // band c's sources: its sample's dy rows from oh0 and x rows from ih0 = oh0*st - 1
+  struct Band {
+    const float* ab;
+    const float* xb;
+    int ih0;
+  };
+  auto band_of = [&](int c) {
     const int n = c / g.bands_per_n;
     const int oh0 = (c - n * g.bands_per_n) * g.RB;
     const int ih0 = oh0 * ST - 1;
-    // branch-free source selection: dy row piece, x row piece, or the zero page
-    const float* ab = dy + (int64_t)n * g.Co * g.OHW + oh0 * g.OW;
-    const float* xb = x + (int64_t)n * g.C * g.H * g.W + (int64_t)ih0 * g.W;
+    return Band{dy + (int64_t)n * g.Co * g.OHW + oh0 * g.OW,
+                x + (int64_t)n * g.C * g.H * g.W + (int64_t)ih0 * g.W, ih0};
+  };
+  // 16-B form: the whole band in one go (<= kBandMaxNI instructions per wave);
+  // branch-free source selection: dy row piece, x row piece, or the zero page
+  auto stage16 = [&](const Band& bd, int b) {
+    const float* zero = g_band_zero_page + lane * 4;
     float* dst = lds + b * g.bufsz + wave * 256;
 #pragma unroll
     for (int i = 0; i < kBandMaxNI; ++i) {
       if (i < g.ni_w) {
         const int kind = meta[i] & 3;
-        const unsigned ih = (unsigned)(ih0 + (meta[i] >> 2));
+        const unsigned ih = (unsigned)(bd.ih0 + (meta[i] >> 2));
         const bool ok = kind == 1 || (kind == 2 && ih < (unsigned)g.H);
-        const float* base = kind == 1 ? ab : xb;
+        const float* base = kind == 1 ? bd.ab : bd.xb;
         const float* src = ok ? base + soff[i] : zero;
         __builtin_amdgcn_global_load_lds((const void*)src, (void*)(dst + i * 1024), 16, 0, 0);
       }
     }
   };
+  // 4-B form: instructions [i0, i1) of this wave; instruction k = wave + 4i of the buffer
+  // covers floats [64k, 64k + 64), all in the A region or all in the X region (the A
+  // region is a multiple of 64 floats)
+  const int HW = g.H * g.W;
+  auto stage4 = [&](const Band& bd, int b, int i0, int i1) {
+    const float* zero = g_band_zero_page + lane;
+    float* dst = lds + b * g.bufsz + wave * 64;
+    for (int i = i0; i < i1; ++i) {
+      const int o = (wave + 4 * i) * 64 + lane;
+      const float* src = zero;
+      if ((wave + 4 * i) * 64 < abytes) {
+        const int row = (int)fdiv((uint32_t)o, g.dPA), col = o - row * g.PA;
+        if (col < g.Q && co0 + row < g.Cog) src = bd.ab + (co0 + row) * g.OHW + col;
+      } else {
+        const int o2 = o - abytes;
+        const int cl = (int)fdiv((uint32_t)o2, g.dPXci), rem = o2 - cl * g.PXci;
+        const int ir = (int)fdiv((uint32_t)rem, g.dPXrow), iw = rem - ir * g.PXrow - 4;
+        const unsigned ih = (unsigned)(bd.ih0 + ir);
+        if (cl < g.CBc && ci0 + cl < g.Cig && ir < g.IR && iw >= 0 && iw < g.W &&
+            ih < (unsigned)g.H)
+          src = bd.xb + (ci0 + cl) * HW + ir * g.W + iw;
+      }
+      __builtin_amdgcn_global_load_lds((const void*)src, (void*)(dst + i * 256), 4, 0, 0);
+    }
+  };
 
   typedef float f32x4v __attribute__((ext_vector_type(4)));
+  typedef float f32x2v __attribute__((ext_vector_type(2)));
   f32x16 acc[9];
 #pragma unroll
   for (int t = 0; t < 9; ++t) acc[t] = f32x16{0};
   const int h = lane >> 5, l32 = lane & 31;
   const int arow = (wm * 32 + l32) * g.PA;
   const int xrow = abytes + (wn * 32 + l32) * g.PXci;
-  const int q0 = h * (g.Q >> 1);
-  const int orow0 = q0 / g.OW, ow0 = q0 - orow0 * g.OW;
-  const int ngroups = g.Q >> 3;
-  constexpr int NW = ST == 1 ? 6 : 9;    // window floats per tap row: 4 pixels x 3 taps
-  // one step's operands: A (4 pixels) and the 3 tap-row windows, read one step ahead
-  auto fetch = [&](const float* L, int q, int orow, int ow, float (&a)[4], float (&w)[3][NW]) {
-    const f32x4v av = *(const f32x4v*)(L + arow + q);
-    a[0] = av.x; a[1] = av.y; a[2] = av.z; a[3] = av.w;
-    const float* xr0 = L + xrow + orow * ST * g.PXrow + ow * ST + 3;
+  const int q0 = h * (g.Qp >> 1);
+  const int ngroups = g.Qp / (2 * V);
+  // the last real pixel: x reads of padding pixels (A = 0) are clamped to it
+  const int last_row = (g.Q - 1) / g.OW, last_col = (g.Q - 1) - last_row * g.OW;
+  constexpr int NW = (V - 1) * ST + 3;   // window floats per tap row: V pixels x 3 taps
+  // one step's operands: A (V pixels) and the 3 tap-row windows, read one step ahead
+  auto fetch = [&](const float* L, int q, int orow, int ow, float (&a)[V], float (&w)[3][NW]) {
+    if constexpr (V == 4) {
+      const f32x4v av = *(const f32x4v*)(L + arow + q);
+      a[0] = av.x; a[1] = av.y; a[2] = av.z; a[3] = av.w;
+    } else if constexpr (V == 2) {
+      const f32x2v av = *(const f32x2v*)(L + arow + q);
+      a[0] = av.x; a[1] = av.y;
+    } else {
+      a[0] = L[arow + q];
+    }
+    int xr_row = orow, xr_col = ow;
+    if (q >= g.Q) {
+      xr_row = last_row;
+      xr_col = last_col - (V - 1);
+    }
+    const float* xr0 = L + xrow + xr_row * ST * g.PXrow + xr_col * ST + 3;
 #pragma unroll
     for (int r = 0; r < 3; ++r) {
       const float* xr = xr0 + r * g.PXrow;
-      w[r][0] = xr[0];
-      const f32x4v t1 = *(const f32x4v*)(xr + 1);
-      w[r][1] = t1.x; w[r][2] = t1.y; w[r][3] = t1.z; w[r][4] = t1.w;
-      if (ST == 1) {
-        w[r][5] = xr[5];
+      if constexpr (V == 4) {
+        w[r][0] = xr[0];
+        const f32x4v t1 = *(const f32x4v*)(xr + 1);
+        w[r][1] = t1.x; w[r][2] = t1.y; w[r][3] = t1.z; w[r][4] = t1.w;
+        if constexpr (ST == 1) {
+          w[r][5] = xr[5];
+        } else {
+          const f32x4v t2 = *(const f32x4v*)(xr + 5);
+          w[r][5] = t2.x; w[r][6] = t2.y; w[r][7] = t2.z; w[r][8] = t2.w;
+        }
       } else {
-        const f32x4v t2 = *(const f32x4v*)(xr + 5);
-        w[r][5] = t2.x; w[r][6] = t2.y; w[r][7] = t2.z; w[r][8] = t2.w;
+#pragma unroll
+        for (int j = 0; j < NW; ++j) w[r][j] = xr[j];
       }
     }
   };
 
-  if (c_begin < c_end) stage(c_begin, 0);
+  // 4-B form: the next band's instructions are spread over the first half of this band's
+  // steps, issued between the MFMAs (their address math runs in the MFMA shadow)
+  const int per_step = (g.ni_w + max(1, ngroups / 2) - 1) / max(1, ngroups / 2);
+  if (c_begin < c_end) {
+    const Band bd = band_of(c_begin);
+    if (g.d16) stage16(bd, 0);
+    else stage4(bd, 0, 0, g.ni_w);
+  }
   for (int c = c_begin; c < c_end; ++c) {
     const int b = (c - c_begin) & 1;
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();             // band c staged; band c-1's reads of buffer b^1 done
-    if (c + 1 < c_end) stage(c + 1, b ^ 1);
+    const bool more = c + 1 < c_end;
+    const Band nb = band_of(more ? c + 1 : c);
+    if (more && g.d16) stage16(nb, b ^ 1);
     const float* L = lds + b * g.bufsz;
-    int q = q0, orow = orow0, ow = ow0;
-    float na[4], nw[3][NW];
+    int q = q0, orow = q0 / g.OW, ow = q0 - orow * g.OW;
+    float na[V], nw[3][NW];
     fetch(L, q, orow, ow, na, nw);
     for (int gi = 0; gi < ngroups; ++gi) {
-      float a[4], w[3][NW];
+      if (more && !g.d16) {
+        const int i0 = gi * per_step;
+        if (i0 < g.ni_w) stage4(nb, b ^ 1, i0, min(i0 + per_step, g.ni_w));
+      }
+      float a[V], w[3][NW];
 #pragma unroll
-      for (int v = 0; v < 4; ++v) a[v] = na[v];
+      for (int v = 0; v < V; ++v) a[v] = na[v];
 #pragma unroll
       for (int r = 0; r < 3; ++r)
 #pragma unroll
         for (int j = 0; j < NW; ++j) w[r][j] = nw[r][j];
-      q += 4;
-      ow += 4;
+      q += V;
+      ow += V;
       if (ow == g.OW) {
         ow = 0;
         ++orow;
@@ -873,7 +945,7 @@ __global__ __launch_bounds__(256, 1) void wgrad_band_stage1(const float* __restr
 #pragma unroll
       for (int r = 0; r < 3; ++r)
 #pragma unroll
-        for (int v = 0; v < 4; ++v)
+        for (int v = 0; v < V; ++v)
 #pragma unroll
           for (int s = 0; s < 3; ++s)
             acc[r * 3 + s] =
@@ -897,36 +969,54 @@ __global__ __launch_bounds__(256, 1) void wgrad_band_stage1(const float* __restr
 
 // band plan: 0 if the shape is not a band shape or no tile fits two buffers in the LDS
 static int band_plan(int64_t Nb, int64_t C, int64_t H, int64_t W, int64_t Co, int64_t R,
-                     int64_t S, int64_t st, int64_t pad, int64_t G, BandGeo& g, int* wmx) {
+                     int64_t S, int64_t st, int64_t pad, int64_t G, BandGeo& g, int* wmx,
+                     int* vpx) {
   if (G != 1 || R != 3 || S != 3 || pad != 1 || (st != 1 && st != 2)) return 0;
   const int64_t OH = (H + 2 - 3) / st + 1, OW = (W + 2 - 3) / st + 1;
-  if (OH < 1 || OW < 4 || OW % 4 || W % 4 || Co % 32 || C % 32) return 0;
+  if (OH < 1 || OW < 1 || Co % 32 || C % 32) return 0;
   if (Nb * C * H * W >= (1ll << 31) || Nb * Co * OH * OW >= (1ll << 31)) return 0;
   g.C = (int)C; g.H = (int)H; g.W = (int)W; g.Co = (int)Co; g.OW = (int)OW;
   g.OHW = (int)(OH * OW); g.Cig = (int)C; g.Cog = (int)Co;
+  const int V = OW % 4 == 0 ? 4 : (OW % 2 == 0 ? 2 : 1);
   auto odd4 = [](int v) { v = (v + 3) / 4 * 4; return (v / 4) % 2 ? v : v + 4; };
   const int64_t budget = 160 * 1024 / 2 / 4;   // floats per buffer
   bool found = false;
-  // prefer the 64 x 64 tile; 128 co x 32 ci when 64 input channels do not fit
+  double best = 1e300;
+  // every (tile, band height) whose double buffer fits; the cheapest per output pixel by
+  // a per-wave cycle model: 9 MFMAs (64 cycles) per padded pixel pair, ~1500 cycles of
+  // wait + barrier per band, 16-B DMA issue ~40 cycles per instruction (before the MFMAs),
+  // 4-B DMA ~10 (interleaved with them)
   for (int wm : {2, 4}) {
-    if (found) break;
     const int TMc = 32 * wm, CBc = 32 * (4 / wm);
     if (wm == 4 && Co < 128) continue;
-    // the largest band of whole rows with RB * OW % 8 == 0 that fits
     for (int rb = (int)std::min<int64_t>(OH, 8); rb >= 1; --rb) {
-      if (OH % rb || (rb * OW) % 8) continue;
-      const int Q = rb * (int)OW, PA = odd4(Q + 1);
-      const int IR = (rb - 1) * (int)st + 3, PXrow = (int)W + 8, PXci = odd4(IR * PXrow);
+      if (OH % rb) continue;
+      const int Q = rb * (int)OW, Qp = (Q + 2 * V - 1) / (2 * V) * (2 * V);
+      const int IR = (rb - 1) * (int)st + 3;
+      // 16-B pieces need 16-B aligned x rows and dy spans
+      const bool d16 = W % 4 == 0 && g.OHW % 4 == 0 && Q % 4 == 0 && Qp == Q;
+      // LDS columns read: up to (OW - 1)*st + 3 + 2 (+ the 16-B form's whole row)
+      const int need = (int)((OW - 1) * st) + 6;
+      const int PXrow = d16 ? (int)W + 8 : (std::max<int>(need, (int)W + 4) + 3) / 4 * 4;
+      const int PA = odd4(Qp + 1), PXci = odd4(IR * PXrow);
       const int64_t buf = ((int64_t)TMc * PA + (int64_t)CBc * PXci + 1023) / 1024 * 1024;
       if (buf > budget) continue;
-      g.RB = rb; g.Q = Q; g.PA = PA; g.IR = IR; g.PXrow = PXrow; g.PXci = PXci;
-      g.TMc = TMc; g.CBc = CBc; g.bufsz = (int)buf; g.ni_w = (int)(buf / 1024);
+      const int ni = d16 ? (int)(buf / 1024) : (int)(buf / 256);
+      if (d16 && ni > kBandMaxNI) continue;
+      const double cost = (288.0 * Qp + 1500.0 + (d16 ? 40.0 : 10.0) * ni) / Q;
+      if (cost >= best) continue;
+      best = cost;
+      g.RB = rb; g.Q = Q; g.Qp = Qp; g.PA = PA; g.IR = IR; g.PXrow = PXrow; g.PXci = PXci;
+      g.TMc = TMc; g.CBc = CBc; g.bufsz = (int)buf; g.d16 = d16 ? 1 : 0; g.ni_w = ni;
       *wmx = wm;
+      *vpx = V;
       found = true;
-      break;
     }
   }
-  if (!found || g.ni_w > kBandMaxNI) return 0;
+  if (!found) return 0;
+  g.dPA = make_fastdiv((uint32_t)g.PA);
+  g.dPXci = make_fastdiv((uint32_t)g.PXci);
+  g.dPXrow = make_fastdiv((uint32_t)g.PXrow);
   g.m_tiles = (g.Cog + g.TMc - 1) / g.TMc;
   g.n_tiles = (g.Cig + g.CBc - 1) / g.CBc;
   g.bands_per_n = (int)(OH / g.RB);
@@ -948,9 +1038,10 @@ static int band_plan(int64_t Nb, int64_t C, int64_t H, int64_t W, int64_t Co, in
 // than the row-tile kernel, 3x3 stride-1 1.1-1.4x (profiles/r2_wgrad_forms.log).
 static int g_wgrad_form = 0;
 static bool use_band(int64_t Nb, int64_t C, int64_t H, int64_t W, int64_t Co, int64_t R,
-                     int64_t S, int64_t st, int64_t pad, int64_t G, BandGeo& g, int* wmx) {
+                     int64_t S, int64_t st, int64_t pad, int64_t G, BandGeo& g, int* wmx,
+                     int* vpx) {
   if (g_wgrad_form != 0 && g_wgrad_form != 3) return false;
-  return band_plan(Nb, C, H, W, Co, R, S, st, pad, G, g, wmx) != 0;
+  return band_plan(Nb, C, H, W, Co, R, S, st, pad, G, g, wmx, vpx) != 0;
 }
 static bool use_i2c(int64_t R, int64_t S, int64_t Co, int64_t G) {
   if (g_wgrad_form != 0) return g_wgrad_form == 2;
@@ -972,8 +1063,8 @@ extern "C" int ssq_conv_wgrad_kind(int64_t Nb, int64_t C, int64_t H, int64_t W, 
                                    int64_t groups) {
   if (is_depthwise(C, Co, groups) && R * S <= 25 && Nb >= 1 && dw_lds_ok(H, W, pad)) return 5;
   BandGeo gb;
-  int wmx;
-  if (use_band(Nb, C, H, W, Co, R, S, stride, pad, groups, gb, &wmx)) return 3;
+  int wmx, vpx;
+  if (use_band(Nb, C, H, W, Co, R, S, stride, pad, groups, gb, &wmx, &vpx)) return gb.d16 ? 3 : 6;
   if (use_i2c(R, S, Co, groups)) {
     I2cGeo gi;
     return wgrad_i2c_plan(Nb, C, H, W, Co, R, S, stride, pad, groups, gi) ? 0 : 2;
@@ -997,8 +1088,8 @@ extern "C" size_t ssq_conv_wgrad_workspace_size(int64_t Nb, int64_t C, int64_t H
   }
   {
     BandGeo gb;
-    int wmx;
-    if (use_band(Nb, C, H, W, Co, R, S, stride, pad, groups, gb, &wmx))
+    int wmx, vpx;
+    if (use_band(Nb, C, H, W, Co, R, S, stride, pad, groups, gb, &wmx, &vpx))
       return (size_t)gb.nsplit * 9 * (size_t)Co * (size_t)C * sizeof(float);
   }
   if (use_i2c(R, S, Co, groups)) {
@@ -1060,26 +1151,29 @@ extern "C" int ssq_conv_wgrad(const float* x, const float* dy, int64_t Nb, int64
   }
   {
     BandGeo gb;
-    int wmx;
-    if (use_band(Nb, C, H, W, Co, R, S, stride, pad, groups, gb, &wmx)) {
+    int wmx, vpx;
+    if (use_band(Nb, C, H, W, Co, R, S, stride, pad, groups, gb, &wmx, &vpx)) {
       const size_t needb = (size_t)gb.nsplit * 9 * (size_t)Co * (size_t)C * sizeof(float);
       SSQ_REQUIRE(ws && ws_bytes >= needb, SSQ_E_WS, "ssq_conv_wgrad: workspace too small");
+      typedef void (*BandK)(const float*, const float*, BandGeo, float*);
+      // [wm == 4][stride == 2][V = 4, 2, 1]
+      static const BandK kernels[2][2][3] = {
+          {{wgrad_band_stage1<2, 1, 4>, wgrad_band_stage1<2, 1, 2>, wgrad_band_stage1<2, 1, 1>},
+           {wgrad_band_stage1<2, 2, 4>, wgrad_band_stage1<2, 2, 2>, wgrad_band_stage1<2, 2, 1>}},
+          {{wgrad_band_stage1<4, 1, 4>, wgrad_band_stage1<4, 1, 2>, wgrad_band_stage1<4, 1, 1>},
+           {wgrad_band_stage1<4, 2, 4>, wgrad_band_stage1<4, 2, 2>, wgrad_band_stage1<4, 2, 1>}}};
       static bool band_attr = false;
       if (!band_attr) {  // two 80 KB buffers: the whole LDS
-        hipFuncSetAttribute((const void*)wgrad_band_stage1<2, 1>,
-                            hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
-        hipFuncSetAttribute((const void*)wgrad_band_stage1<2, 2>,
-                            hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
-        hipFuncSetAttribute((const void*)wgrad_band_stage1<4, 1>,
-                            hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
-        hipFuncSetAttribute((const void*)wgrad_band_stage1<4, 2>,
-                            hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+        for (auto& a : kernels)
+          for (auto& b : a)
+            for (BandK k : b)
+              hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                  160 * 1024);
         band_attr = true;
       }
+      const BandK kb = kernels[wmx == 4][stride == 2][vpx == 4 ? 0 : (vpx == 2 ? 1 : 2)];
       const dim3 gridb((unsigned)(gb.nsplit * gb.m_tiles * gb.n_tiles));
       const size_t ldsb = 2 * (size_t)gb.bufsz * sizeof(float);
-      auto kb = wmx == 2 ? (stride == 1 ? wgrad_band_stage1<2, 1> : wgrad_band_stage1<2, 2>)
-                         : (stride == 1 ? wgrad_band_stage1<4, 1> : wgrad_band_stage1<4, 2>);
       hipLaunchKernelGGL(kb, gridb, dim3(256), ldsb, s, x, dy, gb, (float*)ws);
       const int64_t inner = Co * C, nb = 9 * inner;
       hipLaunchKernelGGL(wgrad_stage2, dim3((unsigned)std::min<int64_t>((nb + 63) / 64, 4096)),

@@ -979,7 +979,8 @@ def conv_wgrad_supported(x, weight, stride, padding, dilation, groups):
 
 def wgrad_kind(x_shape, w_shape, stride, padding, groups):
     """The K17 kernel ssq_conv_wgrad runs for this shape (0 unsupported, 1 row tile,
-    2 im2col-DMA, 3 band, 4 1x1 GEMM, 5 depthwise)."""
+    2 im2col-DMA, 3 band with 16-B staging, 4 1x1 GEMM, 5 depthwise, 6 band with 4-B
+    staging)."""
     st = stride if isinstance(stride, int) else stride[0]
     pad = padding if isinstance(padding, int) else padding[0]
     Nb, C, H, W = (int(v) for v in x_shape)
@@ -990,7 +991,8 @@ def wgrad_kind(x_shape, w_shape, stride, padding, groups):
 
 def set_wgrad_form(form):
     """K17 non-depthwise form: 0 auto, 1 input-row-tile (+1x1 GEMM), 2 im2col-DMA, 3 band
-    (3x3 pad 1 shapes it plans, else the row tile); returns the previous value."""
+    (3x3 pad 1 shapes, Cin / Cout multiples of 32, else the row tile); returns the previous
+    value."""
     return int(query("ssq_conv_wgrad_set_form", int(form)))
 
 
@@ -1104,16 +1106,18 @@ class Conv2dFn(torch.autograd.Function):
         return gx, gw, None, None, None, None
 
 
-# When the conv weight gradient runs on K17 (tools/wgrad_bench.py, batch 32, MI355X):
-#   'auto'   every shape the band kernel takes (3x3 pad 1, OW % 4 == 0: ResNet layer1 /
-#            layer2), in either mode -- it beats MIOpen's fastest non-deterministic solver
-#            there (layer1 3x3: 95 vs 110 us, layer2.0 stride 2: 63 vs 72 us,
-#            profiles/r2_wgrad_band.log); every grouped conv: depthwise ones on K17's
-#            LDS-staged reduction (MobileNetV2 144x56x56 3x3: 74 vs 866 us on MIOpen, either
-#            mode), other grouped ones on its MFMA GEMM (RegNetX g=2: 217 vs 955 us); under the reference's
-#            torch.backends.cudnn.deterministic also every stride-2 conv and every output
-#            plane >= 400 pixels, where MIOpen's deterministic solvers are 3-8x slower than
-#            K17 (stride-1 14x14 / 7x7 planes are as fast on MIOpen).
+# When the conv weight gradient runs on K17 (tools/wgrad_bench.py, batch 32, MI355X,
+# profiles/r2_wgrad_band.log):
+#   'auto'   every shape the band kernel stages with 16-B pieces (3x3 pad 1: ResNet layer1,
+#            layer2, layer3.0's stride-2 conv), in either mode -- it beats MIOpen's fastest
+#            non-deterministic solver there (layer1 3x3: 97 vs 110 us, layer2.0 s2: 66 vs
+#            81, layer3.0 s2: 66 vs 85); every grouped conv: depthwise ones on K17's
+#            LDS-staged reduction (MobileNetV2 144x56x56 3x3: 60 vs 866 us on MIOpen, either
+#            mode), other grouped ones on its MFMA GEMM (RegNetX g=2: 326 vs 960 us); under
+#            the reference's torch.backends.cudnn.deterministic also every stride-2 conv and
+#            every output plane >= 100 pixels, where MIOpen's deterministic solvers are
+#            slower (layer3 3x3 14x14: band 132 vs 172 us, layer4.0 s2: 106 vs 372; the
+#            7x7 planes of layer4 stay on MIOpen: 98 vs 166).
 #   'always' / 'never' (MIOpen's choice) for A/B runs.
 WGRAD_POLICY = "auto"
 
@@ -1132,7 +1136,7 @@ def _use_k17(x, weight, stride, padding, groups=1):
         pad = padding if isinstance(padding, int) else padding[0]
         oh = (x.shape[2] + 2 * pad - weight.shape[2]) // st + 1
         ow = (x.shape[3] + 2 * pad - weight.shape[3]) // st + 1
-        return st > 1 or oh * ow >= 400
+        return st > 1 or oh * ow >= 100
     return False
 
 

@@ -734,6 +734,12 @@ def wgrad_form(request):
     # ragged output-channel tiles, fewer input channels than the tile, one-row bands
     (3, 128, 28, 128, 3, 1, 1, 1), (2, 64, 56, 128, 3, 2, 1, 1), (2, 32, 16, 96, 3, 2, 1, 1),
     (3, 32, 8, 160, 3, 1, 1, 1), (2, 96, 12, 64, 3, 1, 1, 1),
+    # band path on small planes: 2 / 1 pixels per step, 4-byte DMA (rows not 16-B aligned),
+    # bands padded to the two lane halves: ResNet layer3 / layer3.0 s2 / layer4 / layer4.0 s2,
+    # odd planes
+    (2, 256, 14, 256, 3, 1, 1, 1), (2, 128, 28, 256, 3, 2, 1, 1), (3, 512, 7, 512, 3, 1, 1, 1),
+    (2, 256, 14, 512, 3, 2, 1, 1), (2, 32, 9, 64, 3, 1, 1, 1), (2, 64, 10, 96, 3, 2, 1, 1),
+    (1, 32, 6, 32, 3, 1, 1, 1),
     # 1x1 GEMM path: ResNet downsamples (stride 2 at 56x56 / 14x14), ragged channel
     # counts over the 128 x 128 tile, grouped, a plane shorter than one chunk
     (2, 64, 56, 128, 1, 2, 0, 1), (2, 256, 14, 512, 1, 2, 0, 1), (3, 72, 9, 40, 1, 1, 0, 1),
