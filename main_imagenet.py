@@ -28,7 +28,7 @@ sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
 
 from shiftedscalequantization_amd import drivers as D  # noqa: E402
 from shiftedscalequantization_amd.cli import parse_args, seed_all, validate_model  # noqa: E402
-from shiftedscalequantization_amd.parallel_dp import shard_rows  # noqa: E402
+from shiftedscalequantization_amd.parallel_dp import replicated, shard_rows  # noqa: E402
 from shiftedscalequantization_amd.quant import QuantModule  # noqa: E402
 
 
@@ -60,9 +60,14 @@ def main(argv=None):
     args = parse_args(argv)
     world = int(os.environ.get('WORLD_SIZE', '1'))
     if world > 1:
-        dist.init_process_group('nccl')
-        torch.cuda.set_device(int(os.environ.get('LOCAL_RANK', '0')))
-        device = torch.device('cuda', torch.cuda.current_device())
+        # one process per GPU; ranks beyond the visible GPUs share them (gloo rehearsals)
+        local = int(os.environ.get('LOCAL_RANK', '0'))
+        device = torch.device('cuda', local % max(torch.cuda.device_count(), 1))
+        torch.cuda.set_device(device)
+        if args.dist_backend == 'nccl':
+            dist.init_process_group('nccl', device_id=device)
+        else:
+            dist.init_process_group(args.dist_backend)
     else:
         device = torch.device(args.device_gpu)
     seed_all(args.seed, deterministic=bool(args.deterministic))
@@ -143,6 +148,10 @@ def main(argv=None):
           f'({", ".join(f"{k} {v:.1f}s" for k, v in phases.items())}); block rec losses: '
           f'{ {k: v for k, v in report.items()} }')
     if world > 1:
+        # the calibrated model (learned shift logits, AdaRound V, gamma^z/phi^z, act deltas)
+        # must be bit-identical on every rank
+        print(f'rank {dist.get_rank()}/{world}: calibrated model replicated across ranks: '
+              f'{replicated(qnn)}')
         dist.destroy_process_group()
     return qnn
 

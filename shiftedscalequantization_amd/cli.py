@@ -68,6 +68,10 @@ def build_parser():
     p.add_argument('--keep_features_on_host', default=False, type=bool)
     p.add_argument('--deterministic', default=1, type=int,
                    help='1 (reference): deterministic MIOpen conv solvers; 0: fastest solvers')
+    # data parallel (one process per GPU under torch.distributed.run)
+    p.add_argument('--dist_backend', default='nccl', type=str,
+                   help="torch.distributed backend for world > 1: 'nccl' (= RCCL over xGMI); "
+                        "'gloo' rehearses several ranks on one GPU")
     return p
 
 

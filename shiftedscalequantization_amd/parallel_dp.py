@@ -121,3 +121,24 @@ def shard_rows(n, r=None, ws=None):
     per = (n + ws - 1) // ws
     lo = min(n, r * per)
     return lo, min(n, lo + per)
+
+
+def replicated(module):
+    """True when every floating-point parameter and buffer of `module` is bit-identical on
+    all ranks: per tensor an exact integer checksum of its fp32 bit patterns (and its
+    element count), compared between the all-reduced MIN and MAX.  The data-parallel
+    recon keeps the learned parameters replicated by construction; this checks it."""
+    ws = world()
+    tensors = [t for t in list(module.parameters()) + list(module.buffers())
+               if t.is_floating_point() and t.numel() > 0]
+    if ws == 1 or not tensors:
+        return True
+    dev = tensors[0].device
+    sig = torch.stack([torch.stack([t.detach().float().contiguous().view(torch.int32)
+                                    .to(torch.int64).sum(),
+                                    torch.tensor(t.numel(), device=dev)])
+                       for t in tensors]).to(dev)
+    lo, hi = sig.clone(), sig.clone()
+    dist.all_reduce(lo, op=dist.ReduceOp.MIN)
+    dist.all_reduce(hi, op=dist.ReduceOp.MAX)
+    return bool(torch.equal(lo, hi))

@@ -169,6 +169,32 @@ def test_grad_bucket_allreduce_gloo():
     assert out[0][3] == (0, 512) and out[1][3] == (512, 1024)
 
 
+def _replicated_worker(rank, world, port, out):
+    import torch.distributed as dist
+    from shiftedscalequantization_amd.parallel_dp import replicated
+    dist.init_process_group("gloo", init_method=f"tcp://127.0.0.1:{port}", rank=rank, world_size=world)
+    torch.manual_seed(3)
+    m = torch.nn.Sequential(torch.nn.Conv2d(3, 4, 3), torch.nn.BatchNorm2d(4))
+    same = replicated(m)
+    with torch.no_grad():                    # one ulp on one rank, one element
+        if rank == 1:
+            w = m[0].weight.view(-1)
+            w[5] = torch.nextafter(w[5], torch.tensor(1e9))
+    out[rank] = (same, replicated(m))
+    dist.destroy_process_group()
+
+
+def test_replicated_check_gloo():
+    """parallel_dp.replicated: identical modules on both ranks -> True; a one-ulp
+    difference in one element on one rank -> False on every rank."""
+    world = 2
+    port = _free_port()
+    mgr = mp.Manager()
+    out = mgr.dict()
+    mp.spawn(_replicated_worker, args=(world, port, out), nprocs=world, join=True)
+    assert out[0] == (True, False) and out[1] == (True, False)
+
+
 def test_dwconv_support_query_covers_both_stages():
     """K18 accepts a depthwise shape only when the forward AND the input-gradient LDS
     stages fit (weight rows + padded planes / margined dy planes): 178x178 3x3 fits the
