@@ -732,9 +732,9 @@ static int wgrad_plan(int64_t Nb, int64_t C, int64_t H, int64_t W, int64_t Co, i
 //   * 4-byte pieces otherwise (14x14 and 7x7 planes), sources by magic-number division.
 // A lane walks V consecutive pixels of its lane half per step (V = 4, 2 or 1 by OW): A by
 // one ds_read of V floats, each tap row's window of (V-1)*st + 3 floats, 9*V MFMAs per
-// step, the next step's operands read during this step's MFMAs.  A band whose pixel count
-// does not split into the two lane halves is padded with pixels whose A is zero (their x
-// reads are clamped to the last real pixel).  Pitches are odd multiples of 4 floats
+// step, the next step's operands read during this step's MFMAs (two register sets used
+// alternately).  A band whose pixel count does not split into the two lane halves is
+// padded with pixels whose A is zero (their x reads are clamped to the last real pixel).  Pitches are odd multiples of 4 floats
 // (conflict-free 16-B reads).  Partials go to part[split][tap][co][ci] (coalesced) and
 // wgrad_stage2 sums the splits in a fixed order into dW[co][ci][tap]: deterministic.
 constexpr int kBandMaxNI = 20;     // 16-B DMA instructions per wave per band (80 KB buffers)
@@ -921,27 +921,15 @@ __global__ __launch_bounds__(256, 1) void wgrad_band_stage1(const float* __restr
     if (more && g.d16) stage16(nb, b ^ 1);
     const float* L = lds + b * g.bufsz;
     int q = q0, orow = q0 / g.OW, ow = q0 - orow * g.OW;
-    float na[V], nw[3][NW];
-    fetch(L, q, orow, ow, na, nw);
-    for (int gi = 0; gi < ngroups; ++gi) {
-      if (more && !g.d16) {
-        const int i0 = gi * per_step;
-        if (i0 < g.ni_w) stage4(nb, b ^ 1, i0, min(i0 + per_step, g.ni_w));
-      }
-      float a[V], w[3][NW];
-#pragma unroll
-      for (int v = 0; v < V; ++v) a[v] = na[v];
-#pragma unroll
-      for (int r = 0; r < 3; ++r)
-#pragma unroll
-        for (int j = 0; j < NW; ++j) w[r][j] = nw[r][j];
+    auto advance = [&]() {
       q += V;
       ow += V;
       if (ow == g.OW) {
         ow = 0;
         ++orow;
       }
-      if (gi + 1 < ngroups) fetch(L, q, orow, ow, na, nw);
+    };
+    auto mfmas = [&](const float (&a)[V], const float (&w)[3][NW]) {
 #pragma unroll
       for (int r = 0; r < 3; ++r)
 #pragma unroll
@@ -950,6 +938,33 @@ __global__ __launch_bounds__(256, 1) void wgrad_band_stage1(const float* __restr
           for (int s = 0; s < 3; ++s)
             acc[r * 3 + s] =
                 __builtin_amdgcn_mfma_f32_32x32x2f32(a[v], w[r][v * ST + s], acc[r * 3 + s], 0, 0, 0);
+    };
+    auto stage_slice = [&](int gi) {
+      if (more && !g.d16) {
+        const int i0 = gi * per_step;
+        if (i0 < g.ni_w) stage4(nb, b ^ 1, i0, min(i0 + per_step, g.ni_w));
+      }
+    };
+    // two operand sets used alternately, each read one step ahead of its MFMAs: no
+    // register copies between steps (8 % faster than copying a prefetch set on layer1)
+    float a0[V], w0[3][NW], a1[V], w1[3][NW];
+    fetch(L, q, orow, ow, a0, w0);
+    for (int gi = 0; gi < ngroups; gi += 2) {
+      stage_slice(gi);
+      const bool two = gi + 1 < ngroups;
+      if (two) {
+        advance();
+        fetch(L, q, orow, ow, a1, w1);
+      }
+      mfmas(a0, w0);
+      if (two) {
+        stage_slice(gi + 1);
+        if (gi + 2 < ngroups) {
+          advance();
+          fetch(L, q, orow, ow, a0, w0);
+        }
+        mfmas(a1, w1);
+      }
     }
   }
   // part[split][tap][co][ci]: C[row][col], row = (i&3) + 8*(i>>2) + 4*h, col = lane&31
