@@ -55,6 +55,7 @@ def parse():
     p.add_argument("--cpu-seconds", type=float, default=15.0)
     p.add_argument("--no-recon", action="store_true")
     p.add_argument("--recon-iters", type=int, default=200)
+    p.add_argument("--no-validate", action="store_true")
     p.add_argument("--variant", type=int, default=-1, help="streaming cache policy A/B")
     p.add_argument("--dist-backend", default="nccl",
                    help="nccl (= RCCL over xGMI, the default) or gloo (rehearsing N > 1 ranks "
@@ -272,6 +273,14 @@ def main():
                                 cpu_sample=64 if want_cpu else 0)
         recon_state = recon.pop("_cpu_state", None)
 
+    validation = None
+    if not args.no_validate:
+        from shiftedscalequantization_amd.validate_bench import run_validate_bench
+        validation = run_validate_bench(dev, world, rank)
+        el = max_over_ranks(validation.pop("_elapsed_s"), world, dev)
+        validation["images_per_s"] = round(world * validation["_images"] / el, 1)
+        validation.pop("_images")
+
     out = {
         "metric": "Gelem/s shifted-scale q/dq + recon iters/s, ResNet-18 W2A4; top-1 vs ref",
         "value": round(value, 3),
@@ -308,6 +317,8 @@ def main():
     if recon is not None:
         out["roofline_recon"] = recon.pop("roofline_recon")
         out["recon"] = recon
+    if validation is not None:
+        out["validation"] = validation
     if world == 1 and rank == 0 and not args.no_cpu_baseline:
         out["cpu_baseline"] = cpu_baseline(act, d_a, z_a, args.cpu_seconds, recon_state)
     if rank == 0:

@@ -1083,6 +1083,10 @@ class DwConv2dFn(torch.autograd.Function):
         return gx, gw, None, None
 
 
+def _pair(v):
+    return [int(v), int(v)] if isinstance(v, int) else [int(t) for t in v]
+
+
 class Conv2dFn(torch.autograd.Function):
     """F.conv2d whose weight gradient runs on K17 (deterministic, MFMA); the forward and
     the input gradient stay on MIOpen."""
@@ -1100,7 +1104,12 @@ class Conv2dFn(torch.autograd.Function):
         g = g.contiguous()
         gx = gw = None
         if ctx.needs_input_grad[0]:
-            gx = torch.nn.grad.conv2d_input(x.shape, weight, g, stride, padding, dilation, groups)
+            # the saved input itself, not torch.nn.grad.conv2d_input's expanded dummy: the
+            # MIOpen backend makes an expanded input contiguous first (one activation-sized
+            # copy per call, 8.4 us on a ResNet-18 layer1 batch)
+            gx = torch.ops.aten.convolution_backward(
+                g, x, weight, None, _pair(stride), _pair(padding), _pair(dilation), False,
+                [0, 0], groups, (True, False, False))[0]
         if ctx.needs_input_grad[1]:
             gw = conv_wgrad(x, g, weight.shape, stride, padding, groups)
         return gx, gw, None, None, None, None

@@ -7,7 +7,7 @@ half of the fixture's calibration data (parallel_dp.shard_rows), runs the loop, 
 writes what the test compares: the learned parameters, their values before the loop, and
 every iteration's (local, all-reduced) gradient bucket (parallel_dp.RECORD).
 
-    python tests/dp_worker.py {fused|brecq} OUT.npz
+    python tests/dp_worker.py {fused|brecq|validate} OUT.npz
 """
 import os
 import sys
@@ -93,6 +93,24 @@ def run_brecq(out):
     out["a_delta"] = np.array([float(q.delta) for q in aqs], np.float32)
 
 
+def run_validate(out):
+    """(f3) + (e): each rank validates its contiguous share of the fixture's val batches;
+    cli.validate_model all-reduces (correct, total) (Brecq/main_imagenet_dist.py:114-124)."""
+    import test_recon2_gpu as T2
+    from shiftedscalequantization_amd import cli, quant as Q
+    from shiftedscalequantization_amd.parallel_dp import shard_rows
+    g = np.load(os.path.join(HERE, "golden", "validate_w2a4.npz"))
+    qnn = T2.tiny_net2(Q, g)
+    qnn.set_quant_state(True, True)
+    with torch.no_grad():
+        qnn(dev(g["cali"])[:8])
+    qnn.disable_network_output_quantization()
+    loader = T2._val_loader(g)
+    lo, hi = shard_rows(len(loader))
+    out["n_local"] = np.array([sum(int(t.numel()) for _, t in loader[lo:hi])])
+    out["top1"] = np.array([cli.validate_model(loader[lo:hi], qnn)], np.float64)
+
+
 def main():
     mode, path = sys.argv[1], sys.argv[2]
     torch.cuda.set_device(0)
@@ -102,7 +120,7 @@ def main():
     from shiftedscalequantization_amd import parallel_dp as P
     P.RECORD = []
     out = {"rank": np.array([dist.get_rank()])}
-    {"fused": run_fused, "brecq": run_brecq}[mode](out)
+    {"fused": run_fused, "brecq": run_brecq, "validate": run_validate}[mode](out)
     torch.cuda.synchronize()
     for k, (kind, local, reduced) in enumerate(P.RECORD):
         out[f"rec{k}_local"] = local.cpu().numpy()

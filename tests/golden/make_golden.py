@@ -1040,10 +1040,53 @@ def gen_wmse_driver(n_cali=16, res=16):
     save("driver_wmse", **out)
 
 
+def gen_validate(n_cali=16, n_val=40, res=16, bs=8):
+    """(f3) W2A4 fake-quant validation inference: weights UAQ 'max' (8-bit stem/head), acts
+    UAQ 'mse' initialised by one forward over cali[:8] under set_quant_state(True, True),
+    network output left unquantized (disable_network_output_quantization), then the
+    reference's own common.validate_model over a labelled synthetic set.  Half of the labels
+    are the FP network's predictions so top-1 is not chance.  Recorded: every act
+    quantizer's delta / zero_point, the quantized logits and the reference's top-1."""
+    import common as C
+    qnn = _build_tiny_qnn2()
+    torch.manual_seed(1005)
+    cali = torch.randn(n_cali, 3, res, res)
+    val = torch.randn(n_val, 3, res, res)
+    out = {"cali": t2n(cali), "val": t2n(val)}
+    with torch.no_grad():
+        fp = qnn(val)
+    g = torch.Generator().manual_seed(11)
+    labels = torch.randint(0, 10, (n_val,), generator=g)
+    labels[: n_val // 2] = fp[: n_val // 2].argmax(1)
+    qnn.set_quant_state(True, True)
+    with torch.no_grad():
+        qnn(cali[:8])
+    qnn.disable_network_output_quantization()
+    _dump_qms(out, qnn, "")
+    # every act quantizer (QuantModules and the blocks' output quantizers), in module order
+    owners = [m for m in qnn.modules() if hasattr(m, "act_quantizer")]
+    for k, m in enumerate(owners):
+        aq = m.act_quantizer
+        out[f"aq{k}_kind"] = np.array([type(m).__name__])
+        out[f"aq{k}_bits"] = np.array([aq.n_bits])
+        out[f"aq{k}_on"] = np.array([int(m.use_act_quant and not getattr(m, "disable_act_quant", False))])
+        if aq.delta is not None and aq.inited:
+            out[f"aq{k}_delta"] = t2n(torch.as_tensor(aq.delta).reshape(-1))
+            out[f"aq{k}_zp"] = t2n(torch.as_tensor(aq.zero_point).reshape(-1))
+    loader = [(val[i:i + bs], labels[i:i + bs]) for i in range(0, n_val, bs)]
+    top1 = C.validate_model(loader, qnn)
+    with torch.no_grad():
+        out["logits"] = t2n(qnn(val))
+    out["labels"] = labels.numpy().astype(np.int64)
+    out["top1"] = np.array([float(top1)], np.float64)
+    out["bs"] = np.array([bs])
+    save("validate_w2a4", **out)
+
+
 if __name__ == "__main__":
     which = sys.argv[1:] or ["uaq", "channelquant", "adaround", "inpscale", "loss", "recon",
                              "layershift", "brecq", "blocks", "act", "layerfused", "blockshift", "driver",
-                             "wmse"]
+                             "wmse", "validate"]
     torch.set_num_threads(4)
     if "uaq" in which:
         gen_uaq()
@@ -1073,3 +1116,5 @@ if __name__ == "__main__":
         gen_driver()
     if "wmse" in which:
         gen_wmse_driver()
+    if "validate" in which:
+        gen_validate()

@@ -105,3 +105,14 @@ def test_brecq_world2_replicated(tmp_path):
     np.testing.assert_allclose(r0["a_delta0"], (r0["a_delta_local"] + r1["a_delta_local"]) / 2,
                                rtol=1e-6)
     np.testing.assert_array_equal(r0["a_delta"], r1["a_delta"])
+
+
+def test_validation_world2_whole_set_top1(tmp_path):
+    """(f3) sharded validation: each rank sees only its half of the val batches, and both
+    return the reference's whole-set top-1 (the (correct, total) all-reduce)."""
+    r0, r1 = _run_world2("validate", tmp_path)
+    g = np.load(os.path.join(HERE, "golden", "validate_w2a4.npz"))
+    assert int(r0["n_local"][0]) + int(r1["n_local"][0]) == len(g["labels"])
+    assert int(r0["n_local"][0]) != len(g["labels"])
+    assert float(r0["top1"][0]) == float(g["top1"][0])
+    assert float(r1["top1"][0]) == float(g["top1"][0])

@@ -365,3 +365,50 @@ def test_wmse_driver_matches_reference(Q, golden, level):
     err = np.abs(logits - g[f"l{level}_logits"]).max() / np.abs(g[f"l{level}_logits"]).max()
     parity_report(f"a23_wmse_l{level}", logits_rel_err=err)
     assert err <= 1e-5             # observed (r2) <= 2.1e-7
+
+
+# ------------------------------------------------------------------ (f3) fake-quant validation
+def _val_loader(g):
+    val, labels, bs = dev(g["val"]), torch.as_tensor(g["labels"]), int(g["bs"][0])
+    return [(val[i:i + bs], labels[i:i + bs]) for i in range(0, val.shape[0], bs)]
+
+
+def test_w2a4_validation_matches_reference(Q):
+    """(f3) W2A4 fake-quant validation (common.py:152-221): weights UAQ 'max' with the 8-bit
+    stem/head, act deltas initialised by one forward under set_quant_state(True, True), the
+    network output unquantized, then cli.validate_model over a labelled set.  Every act
+    quantizer (QuantModules and the blocks' own output quantizers) equals the reference's
+    in bits / on-off / delta / zero point, the quantized logits agree to conv rounding and
+    top-1 equals the reference's."""
+    from shiftedscalequantization_amd import cli
+    g = np.load(os.path.join(os.path.dirname(__file__), "golden", "validate_w2a4.npz"))
+    qnn = tiny_net2(Q, g)
+    qnn.set_quant_state(True, True)
+    with torch.no_grad():
+        qnn(dev(g["cali"])[:8])
+    qnn.disable_network_output_quantization()
+    owners = [m for m in qnn.modules() if hasattr(m, "act_quantizer")]
+    assert len(owners) == len([k for k in g.files if k.endswith("_kind")])
+    stats = {}
+    for k, m in enumerate(owners):
+        aq = m.act_quantizer
+        assert type(m).__name__ == str(g[f"aq{k}_kind"][0]), k
+        assert aq.n_bits == int(g[f"aq{k}_bits"][0]), k
+        on = int(m.use_act_quant and not getattr(m, "disable_act_quant", False))
+        assert on == int(g[f"aq{k}_on"][0]), k
+        if f"aq{k}_delta" in g:
+            d = host(torch.as_tensor(aq.delta)).reshape(-1)
+            stats[f"aq{k}_delta_rel_err"] = float(np.abs(d - g[f"aq{k}_delta"]).max() / g[f"aq{k}_delta"].max())
+            np.testing.assert_array_equal(host(torch.as_tensor(aq.zero_point)).reshape(-1), g[f"aq{k}_zp"])
+    top1 = cli.validate_model(_val_loader(g), qnn)
+    with torch.no_grad():
+        logits = host(qnn(dev(g["val"])))
+    stats["logits_rel_err"] = np.abs(logits - g["logits"]).max() / np.abs(g["logits"]).max()
+    stats["argmax_mismatch"] = int(np.sum(logits.argmax(1) != g["logits"].argmax(1)))
+    stats["top1"], stats["top1_ref"] = top1, float(g["top1"][0])
+    parity_report("f3_w2a4_validation", **stats)
+    for k, v in stats.items():
+        if k.endswith("delta_rel_err"):
+            assert v <= 1e-6, (k, v)
+    assert stats["logits_rel_err"] <= 1e-5
+    assert top1 == pytest.approx(float(g["top1"][0]), abs=1e-9)

@@ -19,5 +19,5 @@ torch.backends.cudnn.benchmark = not det
 import time
 t0 = time.time()
 ips = run_block(torch.device("cuda"), name, iters=iters, warmup=10, arch=arch, n_cali=n_cali)
-print(json.dumps({"arch": arch, "block": name, "deterministic": det, "iters_per_s": round(ips, 1),
+print(json.dumps({"arch": arch, "block": name, "deterministic": det, "iters_per_s": round(ips["ips"] if isinstance(ips, dict) else ips, 1),
                   "wall_s": round(time.time() - t0, 1)}), flush=True)

@@ -18,7 +18,12 @@ for a, b in zip(gi, gi[1:]):
 segments.append(cur)
 
 
+FULL = len(sys.argv) > 2 and sys.argv[2] == "full"
+
+
 def fam(n):
+    if FULL:
+        return n[:200]
     n = n.split("(")[0]
     for k in ("ssq::", "igemm", "miopen", "batched_transpose", "at::native", "__amd", "Sub", "Op"):
         if k in n:
