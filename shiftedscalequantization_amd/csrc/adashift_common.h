@@ -133,6 +133,7 @@ static inline int make_shifts(const float* shifts, int S, Shifts& sh) {
 // deterministic, no atomics.
 struct ColTiling {
   uint32_t ncb, ncolblk, R, nchunk, threads;
+  uint32_t whole;   // prepared alpha backward: whole-column workgroups, no second stage
 };
 constexpr uint32_t kMaxChunks = 256;  // stage 2: lane c sums chunks c, c+64, ... in order
 
@@ -151,6 +152,7 @@ static inline ColTiling col_tiling(const Geo& g, uint32_t max_chunks = kMaxChunk
   if (want > g.Co) want = g.Co;
   t.R = (g.Co + want - 1) / want;
   t.nchunk = (g.Co + t.R - 1) / t.R;
+  t.whole = 0;
   return t;
 }
 static inline size_t col_ws_bytes(const Geo& g, int S) {

@@ -84,7 +84,35 @@ static ColTiling col_tiling_prep(const Geo& g) {
   if (want < 1) want = 1;
   t.R = (g.Co + want - 1) / want;
   t.nchunk = (g.Co + t.R - 1) / t.R;
+  t.whole = 0;
   return t;
+}
+
+// Alpha-backward tiling.  Small weights (Co <= SSQ_PREP_WHOLE_CO, default 64, and
+// K <= 64) take the whole-column form: a workgroup owns floor(64/K) whole input channels
+// (one wave-width of columns) over ALL Co rows, its 4 waves taking rows co = w (mod 4), so
+// each input channel's sum is complete inside the workgroup and is finalised there (a
+// fixed-order LDS sum, then the softmax/clamp backward): one launch, no partials.
+// Measured (tools/adashift_bench.py --blocks, profiles/r2_alpha_whole_ab.log): ResNet-18
+// layer1 (Co 64) 9.4 -> 8.2 us; at Co 128 it is slower (9.3 -> 10.1, 32 rows per thread
+// in series) and at Co 256 much slower, so larger weights keep the chunked two-launch
+// form, whose stage 1 spreads rows over the chip.  Both forms are dependent-latency
+// chains (alpha row, row batches, LDS sum, regulariser, store), not bandwidth.  Depends only on the weight's own shape, so a multi-segment launch gives each
+// weight its single-launch bits.
+static ColTiling bwd_tiling_prep(const Geo& g) {
+  static const uint32_t kWholeCo = prep_env("SSQ_PREP_WHOLE_CO", 64);
+  if (g.Co <= kWholeCo && g.K <= (uint32_t)kWave) {
+    ColTiling t;
+    t.ncb = (uint32_t)kWave / g.K;
+    if (t.ncb > g.Ci) t.ncb = g.Ci;
+    t.ncolblk = (g.Ci + t.ncb - 1) / t.ncb;
+    t.threads = kBlock;
+    t.R = g.Co;
+    t.nchunk = 1;
+    t.whole = 1;
+    return t;
+  }
+  return col_tiling_prep(g);
 }
 
 static bool alpha_one_launch() {
@@ -179,6 +207,142 @@ __global__ __launch_bounds__(kBlock) void shift_fwd_prep(PrepTable tab) {
   }
 }
 
+// Whole-column alpha backward (bwd_tiling_prep): workgroup `local` of the segment owns
+// input channels [ci0, ci0 + nci); lane l of wave w sums column ci0*K + l over rows
+// co = w, w + 4, ...; the 4 x K partials of an input channel are added in fixed order
+// (waves per column, then taps) and lane t < nci of wave 0 finalises channel ci0 + t as
+// alpha_reduce_ci's lane 0 does (regulariser terms in shift order, softmax/clamp backward).
+template <int NS>
+__device__ __forceinline__ void alpha_bwd_whole(const PrepSeg& sg, uint32_t local, double* red,
+                                                float reg_lambda, float reg_b,
+                                                const float* __restrict__ reg_dev) {
+  const Geo& g = sg.g;
+  const uint32_t ci0 = local * sg.tl.ncb;
+  const uint32_t nci = min(sg.tl.ncb, g.Ci - ci0);
+  const uint32_t w = threadIdx.x / kWave, lane = threadIdx.x & (kWave - 1);
+  constexpr uint32_t kW = kBlock / kWave;
+  double acc[NS];
+#pragma unroll
+  for (int i = 0; i < NS; ++i) acc[i] = 0.0;
+  if (lane < nci * g.K) {
+    const uint32_t ci = ci0 + lane / g.K, j = ci0 * g.K + lane;
+    float a[kMaxS], p[kMaxS];
+    load_row(sg.alpha, ci, NS, a);
+    soft_targets<kMaxS>(a, NS, nullptr, p);
+    const uint32_t* __restrict__ fpack = sg.fpack;
+    const float* __restrict__ hterm = sg.hterm;
+    const float* __restrict__ gWhat = sg.gWhat;
+    const float* __restrict__ delta = sg.delta;
+    const float* __restrict__ zp = sg.zp;
+    const float lo = sg.lo, hi = sg.hi;
+    auto one = [&](uint32_t fw, float h, float d, float z, float gy) {
+      float F[NS];
+#pragma unroll
+      for (int i = 0; i < NS; ++i) F[i] = unpack_floor(fw, i);
+      float xf = __fmul_rn(F[0], p[0]);
+#pragma unroll
+      for (int i = 1; i < NS; ++i) xf = __fadd_rn(xf, __fmul_rn(F[i], p[i]));
+      const float u = __fadd_rn(__fadd_rn(xf, h), z);
+      const float gi = (u >= lo && u <= hi) ? __fmul_rn(gy, __fmul_rn(d, 1.0f)) : 0.0f;
+#pragma unroll
+      for (int i = 0; i < NS; ++i) acc[i] += (double)gi * (double)F[i];
+    };
+    uint32_t co = w;
+    for (; co + kW * (kRBP - 1) < g.Co; co += kW * kRBP) {
+      uint32_t fw[kRBP];
+      float h[kRBP], d[kRBP], z[kRBP], gy[kRBP];
+#pragma unroll
+      for (int r = 0; r < kRBP; ++r) {
+        const uint32_t c = co + kW * r;
+        const uint32_t e = c * g.CiK + j;
+        fw[r] = fpack[e];
+        h[r] = hterm[e];
+        gy[r] = gWhat[e];
+        d[r] = delta[c];
+        z[r] = zp[c];
+      }
+#pragma unroll
+      for (int r = 0; r < kRBP; ++r) one(fw[r], h[r], d[r], z[r], gy[r]);
+    }
+    for (; co < g.Co; co += kW) {
+      const uint32_t e = co * g.CiK + j;
+      one(fpack[e], hterm[e], delta[co], zp[co], gWhat[e]);
+    }
+  }
+#pragma unroll
+  for (int i = 0; i < NS; ++i) red[threadIdx.x * NS + i] = acc[i];
+  __syncthreads();
+  if (w != 0) return;
+  // wave 0: lane l adds column l's 4 wave partials (all loads in flight at once), then
+  // lane t < nci adds its input channel's K columns; both in fixed order
+  {
+    double v[kW][NS];
+#pragma unroll
+    for (uint32_t ww = 0; ww < kW; ++ww)
+#pragma unroll
+      for (int i = 0; i < NS; ++i) v[ww][i] = red[(ww * kWave + lane) * NS + i];
+#pragma unroll
+    for (int i = 0; i < NS; ++i) {
+      double c = v[0][i];
+#pragma unroll
+      for (uint32_t ww = 1; ww < kW; ++ww) c += v[ww][i];
+      red[lane * NS + i] = c;
+    }
+  }
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+  if (lane >= nci) return;
+  const uint32_t t = lane, ci = ci0 + t;
+  double tot[kMaxS];
+  constexpr uint32_t kUnK = 9;   // 3x3 taps unrolled (loads issued together); others loop
+  if (g.K <= kUnK) {
+    double v[kUnK][NS];
+#pragma unroll
+    for (uint32_t k = 0; k < kUnK; ++k)
+#pragma unroll
+      for (int i = 0; i < NS; ++i) v[k][i] = k < g.K ? red[(t * g.K + k) * NS + i] : 0.0;
+#pragma unroll
+    for (int i = 0; i < NS; ++i) {
+      double sum = v[0][i];
+#pragma unroll
+      for (uint32_t k = 1; k < kUnK; ++k)
+        if (k < g.K) sum += v[k][i];
+      tot[i] = sum;
+    }
+  } else {
+#pragma unroll
+    for (int i = 0; i < NS; ++i) {
+      double sum = 0.0;
+      for (uint32_t k = 0; k < g.K; ++k) sum += red[(t * g.K + k) * NS + i];
+      tot[i] = sum;
+    }
+  }
+  float a[kMaxS];
+  load_row(sg.alpha, ci, NS, a);
+  if (reg_dev) {
+    reg_lambda = reg_dev[0];
+    reg_b = reg_dev[1];
+  }
+  float sm[kMaxS], p[kMaxS], ga[kMaxS];
+  soft_targets<kMaxS>(a, NS, sm, p);
+  float reg = 0.0f;
+  if (reg_lambda != 0.0f) {
+    double racc = 0.0;
+#pragma unroll
+    for (int i = 0; i < NS; ++i) {
+      double rv, rg;
+      reg_term(p[i], reg_lambda, reg_b, 0, rv, rg);
+      racc += rv;
+      tot[i] += rg;
+    }
+    reg = (float)((double)reg_lambda * racc);
+  }
+  softmax_clamp_bwd(sm, NS, tot, ga);
+#pragma unroll
+  for (int i = 0; i < NS; ++i) sg.galpha[(size_t)ci * NS + i] = ga[i];
+  if (sg.reg_vals) sg.reg_vals[ci] = reg;
+}
+
 // Backward stage 1: sums of g_int * F_i per (chunk, ci) into
 // part[(ci*nchunk + chunk)*S + i] (input-channel-major: stage 2 reads one coalesced run).
 template <int NS, bool FUSED>
@@ -189,6 +353,10 @@ __global__ __launch_bounds__(kBlock) void alpha_bwd_prep(PrepTable tab, float re
   const PrepSeg& sg = tab.s[find_seg<false>(tab, blockIdx.x)];
   const Geo& g = sg.g;
   const uint32_t local = blockIdx.x - sg.blk0;
+  if (sg.tl.whole) {             // uniform per workgroup
+    alpha_bwd_whole<NS>(sg, local, red, reg_lambda, reg_b, reg_dev);
+    return;
+  }
   const uint32_t bx = local % sg.tl.ncolblk, by = local / sg.tl.ncolblk;
   const uint32_t ci0 = bx * sg.tl.ncb;
   const uint32_t nci = min(sg.tl.ncb, g.Ci - ci0);
@@ -347,7 +515,7 @@ __global__ __launch_bounds__(kBlock) void alpha_bwd_prep_stage2(PrepTable tab, f
   const uint32_t lane = threadIdx.x & (kWave - 1);
   const PrepSeg& sg = tab.s[find_seg<true>(tab, __builtin_amdgcn_readfirstlane(wave))];
   const uint32_t ci = wave - sg.wave0;
-  if (ci >= sg.g.Ci) return;
+  if (sg.tl.whole || ci >= sg.g.Ci) return;    // whole-column segments finished in stage 1
   alpha_reduce_ci<NS, false>(sg, ci, lane, reg_lambda, reg_b, reg_dev);
 }
 
@@ -471,7 +639,7 @@ extern "C" size_t ssq_adashift_bwd_prepared_multi_workspace_size(int nseg, const
   for (int i = 0; i < nseg; ++i) {
     PrepSeg sg;
     if (make_geo(Co[i], Ci[i], K[i], 0, sg.g) != SSQ_OK) return 0;
-    sg.tl = col_tiling_prep(sg.g);
+    sg.tl = bwd_tiling_prep(sg.g);
     total += part_bytes(sg, S);
   }
   return total;
@@ -502,6 +670,7 @@ extern "C" int ssq_adashift_bwd_prepared_multi(
       const int rc = make_seg(a, i, sg, what);
       if (rc) return rc;
       SSQ_REQUIRE(gWhat[i] && galpha[i], SSQ_E_ARG, "%s: null gWhat/galpha", what);
+      sg.tl = bwd_tiling_prep(sg.g);
       sg.gWhat = gWhat[i];
       sg.galpha = galpha[i];
       sg.reg_vals = reg_vals ? reg_vals[i] : nullptr;
@@ -511,8 +680,10 @@ extern "C" int ssq_adashift_bwd_prepared_multi(
       sg.wave0 = waves;
       sg.tick0 = ticks;
       blk += sg.tl.ncolblk * sg.tl.nchunk;
-      waves += sg.g.Ci;
-      ticks += sg.tl.ncolblk;
+      if (!sg.tl.whole) {
+        waves += sg.g.Ci;
+        ticks += sg.tl.ncolblk;
+      }
     }
     const unsigned blocks2 = (waves + kBlock / kWave - 1) / (kBlock / kWave);
     // two launches by default; SSQ_ALPHA_ONE_LAUNCH=1 (A/B knob) reduces in the same
@@ -529,8 +700,9 @@ extern "C" int ssq_adashift_bwd_prepared_multi(
     } else {                                                                                  \
       hipLaunchKernelGGL((alpha_bwd_prep<NS, false>), dim3(blk), dim3(kBlock), 0, s, tab,     \
                          reg_lambda, reg_b, reg_dev);                                         \
-      hipLaunchKernelGGL((alpha_bwd_prep_stage2<NS>), dim3(blocks2), dim3(kBlock), 0, s, tab, \
-                         reg_lambda, reg_b, reg_dev);                                         \
+      if (blocks2)                                                                            \
+        hipLaunchKernelGGL((alpha_bwd_prep_stage2<NS>), dim3(blocks2), dim3(kBlock), 0, s,    \
+                           tab, reg_lambda, reg_b, reg_dev);                                  \
     }                                                                                         \
   } while (0)
     switch (S) {
