@@ -340,6 +340,19 @@ int ssq_adam(int nseg, float* const* p, const float* const* g, float* const* m,
              float one_minus_beta2, float eps, const float* hyper, float neg_step_size,
              float bias_correction2_sqrt, ssq_stream_t stream);
 
+/* ---------------------------------------------------------------- deferred finalizes
+ * With deferral on, ssq_lp_loss[_rows] (loss value) and ssq_epilogue_bwd (gamma/phi and act
+ * delta/zp gradients) queue their small finalize reduction on the stream instead of
+ * launching it; the next ssq_epilogue_bwd or prepared alpha backward on that stream runs
+ * the queue in extra workgroups of its own launch (same code and order: bit-identical).
+ * ssq_adam, the lp_loss entry points and ssq_flush_finalize launch what is still queued.
+ * The caller must give each producer's workspace a slot no other launch writes before the
+ * flush, and must flush before reading a queued output on the host or with other kernels
+ * (the reconstruction loop: deferral on for its body, flush at its end).  Host state,
+ * not thread-safe.  ssq_set_deferred_finalize returns the previous setting. */
+int ssq_set_deferred_finalize(int on);
+int ssq_flush_finalize(ssq_stream_t stream);
+
 /* ---------------------------------------------------------------- K17 conv weight gradient
  * Deterministic fp32 conv weight gradient (NCHW, dilation 1) on the fp32 matrix cores:
  *   dw[co, ci, r, s] = sum_{n,oh,ow} dy[n, co, oh, ow] * x[n, g*Cig + ci, oh*st + r - pad,

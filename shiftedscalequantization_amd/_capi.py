@@ -78,6 +78,8 @@ SIGNATURES = {
     "ssq_epilogue_bwd": (_i, [_p, _p, _p, _p, _p, _p, _i64, _i64, _i64, _i, _p, _p, _i, _i, _p,
                               _p, _p, _p, _p, _p, _p, _sz, _p]),
     "ssq_adam": (_i, [_i, _p, _p, _p, _p, _p, _f, _f, _f, _f, _p, _f, _f, _p]),
+    "ssq_set_deferred_finalize": (_i, [_i]),
+    "ssq_flush_finalize": (_i, [_p]),
     "ssq_conv_wgrad_set_form": (_i, [_i]),
     "ssq_conv_wgrad_kind": (_i, [_i64] * 10),
     "ssq_conv_wgrad_workspace_size": (_sz, [_i64] * 10),
@@ -181,12 +183,14 @@ class workspace_scope:
         _ws_scope = self.prev
 
 
-def workspace(nbytes, device):
-    """Per-(device, stream) scratch buffer for kernel partials (grown, never shrunk)."""
+def workspace(nbytes, device, slot=None):
+    """Per-(device, stream, slot) scratch buffer for kernel partials (grown, never shrunk).
+    `slot` names a buffer that only its producer writes (the deferred finalizes read their
+    partials after other launches have run: include/ssq.h)."""
     if nbytes == 0:
         return None, 0
     cache = _ws_cache if _ws_scope is None else _ws_scope
-    key = (device.index, torch.cuda.current_stream(device).cuda_stream)
+    key = (device.index, torch.cuda.current_stream(device).cuda_stream, slot)
     buf = cache.get(key)
     if buf is None or buf.numel() < nbytes:
         buf = torch.empty(max(int(nbytes), 1 << 16), dtype=torch.uint8, device=device)

@@ -22,6 +22,7 @@
 #include <stdlib.h>
 
 #include "adashift_common.h"
+#include "fin_tasks.h"
 
 namespace ssq {
 
@@ -348,7 +349,12 @@ __device__ __forceinline__ void alpha_bwd_whole(const PrepSeg& sg, uint32_t loca
 template <int NS, bool FUSED>
 __global__ __launch_bounds__(kBlock) void alpha_bwd_prep(PrepTable tab, float reg_lambda,
                                                           float reg_b,
-                                                          const float* __restrict__ reg_dev) {
+                                                          const float* __restrict__ reg_dev,
+                                                          FinTable fin, uint32_t nmain) {
+  if (blockIdx.x >= nmain) {          // queued finalize tasks (fin_tasks.h) ride on this launch
+    run_fin(fin, blockIdx.x - nmain);
+    return;
+  }
   __shared__ double red[kBlock * NS];
   const PrepSeg& sg = tab.s[find_seg<false>(tab, blockIdx.x)];
   const Geo& g = sg.g;
@@ -692,14 +698,20 @@ extern "C" int ssq_adashift_bwd_prepared_multi(
     // block's input channels with one wave each, serially, where stage 2 spreads them
     // over the chip
     const bool fused = alpha_one_launch() && ticks <= kAlphaTickets;
+    // queued finalize tasks of this stream ride on the first launch (their inputs live in
+    // their producers' own workspace slots, not in this one)
+    FinTable fin;
+    fin.n = 0;
+    fin.nwg = 0;
+    if (base == 0) fin = fin_take(s);
 #define SSQ_BWDP(NS)                                                                          \
   do {                                                                                        \
     if (fused) {                                                                              \
-      hipLaunchKernelGGL((alpha_bwd_prep<NS, true>), dim3(blk), dim3(kBlock), 0, s, tab,      \
-                         reg_lambda, reg_b, reg_dev);                                         \
+      hipLaunchKernelGGL((alpha_bwd_prep<NS, true>), dim3(blk + fin.nwg), dim3(kBlock), 0, s, \
+                         tab, reg_lambda, reg_b, reg_dev, fin, blk);                          \
     } else {                                                                                  \
-      hipLaunchKernelGGL((alpha_bwd_prep<NS, false>), dim3(blk), dim3(kBlock), 0, s, tab,     \
-                         reg_lambda, reg_b, reg_dev);                                         \
+      hipLaunchKernelGGL((alpha_bwd_prep<NS, false>), dim3(blk + fin.nwg), dim3(kBlock), 0,   \
+                         s, tab, reg_lambda, reg_b, reg_dev, fin, blk);                       \
       if (blocks2)                                                                            \
         hipLaunchKernelGGL((alpha_bwd_prep_stage2<NS>), dim3(blocks2), dim3(kBlock), 0, s,    \
                            tab, reg_lambda, reg_b, reg_dev);                                  \

@@ -1,0 +1,114 @@
+// Deferred finalize tasks of the reconstruction iteration.
+//
+// Two per-iteration reductions end in a small finalize launch of their own: the lp_loss
+// value (K11: 1024 workgroup partials -> 1 float) and the K13 epilogue backward's
+// per-channel gamma^z / phi^z sums (+ the act quantizer's delta / zp sums).  Each such
+// launch is a few microseconds of launch and load latency for a few KB of data.  With
+// deferral on (ssq_set_deferred_finalize, turned on by the fused recon loop's body) the
+// producing entry point does not launch its finalize: it queues it as a task on its
+// stream, and the next "host" launch on that stream (epilogue_bwd_rows, the prepared alpha
+// backward's first kernel) runs the queued tasks in extra workgroups appended to its grid.
+// Same device code, same summation order: bit-identical results, fewer launches.
+//
+// Rules that keep it correct whatever runs in between:
+//   * a task's inputs live in a workspace slot only its producer writes (the Python side
+//     gives lp_loss its own slot and alternates the epilogue backward between two), and
+//     every producer entry first hands pending tasks to its own launch, so at most one
+//     task per producer is pending;
+//   * ssq_adam (which reads gamma^z / phi^z / delta gradients), the lp_loss entry points,
+//     ssq_flush_finalize and ssq_set_deferred_finalize(0) launch whatever is still pending
+//     as one standalone kernel first; the recon loop flushes at the end of its body.
+#pragma once
+
+#include "ssq_common.h"
+
+namespace ssq {
+
+constexpr int kLossBlocks = 1024;   // lp_loss workgroup partials
+constexpr int kEpiParts = 6;        // doubles per (n, c) row of the epilogue backward
+
+struct FinTask {
+  int kind;                  // 0: lp_loss value, 1: epilogue backward sums
+  uint32_t nwg;              // workgroups the task takes
+  const double* part;
+  uint32_t a, b, c;          // loss: nblk; epilogue: N, C, nb
+  double m;                  // loss: M
+  float* o[4];               // loss: o[0]; epilogue: ggamma, gphi, gdelta, gzp
+};
+constexpr int kMaxFin = 4;
+struct FinTable {
+  FinTask t[kMaxFin];
+  int n;
+  uint32_t nwg;
+};
+
+// lp_loss value: the workgroup partials summed in index order (every load issued first)
+__device__ __forceinline__ void fin_loss(const double* __restrict__ part, int nblk, double m,
+                                         float* __restrict__ out) {
+  __shared__ double red[16];
+  double v[kLossBlocks / kBlock];
+#pragma unroll
+  for (int k = 0; k < kLossBlocks / kBlock; ++k) {
+    const int i = threadIdx.x + k * kBlock;
+    v[k] = i < nblk ? part[i] : 0.0;
+  }
+  double a = 0.0;
+#pragma unroll
+  for (int k = 0; k < kLossBlocks / kBlock; ++k) a += v[k];
+  a = block_sum(a, red);
+  if (threadIdx.x == 0) out[0] = (float)(a / m);
+}
+
+// epilogue backward: workgroups [0, nb) the per-channel gamma / phi gradients (sum over n
+// in order); workgroup nb (when launched) the act quantizer's delta / zp gradients (rows
+// in a fixed order, as fq_bwd_finalize)
+__device__ __forceinline__ void fin_epi(uint32_t bid, const double* __restrict__ part, uint32_t N,
+                                        uint32_t C, uint32_t nb, float* __restrict__ ggamma,
+                                        float* __restrict__ gphi, float* __restrict__ gdelta,
+                                        float* __restrict__ gzp) {
+  __shared__ double red[16];
+  if (bid < nb) {
+    const uint32_t c = bid * kBlock + threadIdx.x;
+    if (c >= C) return;
+    double sg = 0, sp = 0;
+#pragma unroll 8
+    for (uint32_t n = 0; n < N; ++n) {
+      sg += part[((int64_t)n * C + c) * kEpiParts + 0];
+      sp += part[((int64_t)n * C + c) * kEpiParts + 1];
+    }
+    if (ggamma) ggamma[c] = (float)sg;
+    if (gphi) gphi[c] = (float)sp;
+    return;
+  }
+  double a[4] = {0, 0, 0, 0};
+  for (uint32_t r = threadIdx.x; r < N * C; r += blockDim.x)
+    for (int k = 0; k < 4; ++k) a[k] += part[(int64_t)r * kEpiParts + 2 + k];
+  for (int k = 0; k < 4; ++k) a[k] = block_sum(a[k], red);
+  if (threadIdx.x == 0) {
+    if (gdelta) gdelta[0] = (float)(a[0] - a[1]);
+    if (gzp) gzp[0] = (float)(a[2] - a[3]);
+  }
+}
+
+// Workgroup k of the table's tasks (k < ft.nwg).
+__device__ __forceinline__ void run_fin(const FinTable& ft, uint32_t k) {
+  for (int i = 0; i < ft.n; ++i) {
+    const FinTask& t = ft.t[i];
+    if (k < t.nwg) {
+      if (t.kind == 0)
+        fin_loss(t.part, (int)t.a, t.m, t.o[0]);
+      else
+        fin_epi(k, t.part, t.a, t.b, t.c, t.o[0], t.o[1], t.o[2], t.o[3]);
+      return;
+    }
+    k -= t.nwg;
+  }
+}
+
+// host side (recon.hip)
+bool fin_defer_on();
+int fin_push(hipStream_t s, const FinTask& t);   // queue (flushes first when full)
+FinTable fin_take(hipStream_t s);                // remove and return the stream's pending tasks
+int fin_flush(hipStream_t s);                    // launch the pending tasks standalone
+
+}  // namespace ssq

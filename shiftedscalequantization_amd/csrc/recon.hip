@@ -10,11 +10,11 @@
 
 #include <type_traits>
 
+#include "fin_tasks.h"
 #include "ssq_common.h"
 
 namespace ssq {
 
-constexpr int kLossBlocks = 1024;
 __device__ unsigned g_loss_ticket;   // lp_loss_kernel's last-arriver counter (zero at rest)
 
 // |d|^p and its derivative p*|d|^(p-1) for one element.
@@ -127,18 +127,7 @@ __global__ __launch_bounds__(kBlock) void lp_loss_kernel(const float* __restrict
 // two-launch form: the block partials summed in index order (every load issued first)
 __global__ void lp_loss_finalize(const double* __restrict__ part, int nblk, double m,
                                  float* __restrict__ out) {
-  __shared__ double red[16];
-  double v[kLossBlocks / kBlock];
-#pragma unroll
-  for (int k = 0; k < kLossBlocks / kBlock; ++k) {
-    const int i = threadIdx.x + k * kBlock;
-    v[k] = i < nblk ? part[i] : 0.0;
-  }
-  double a = 0.0;
-#pragma unroll
-  for (int k = 0; k < kLossBlocks / kBlock; ++k) a += v[k];
-  a = block_sum(a, red);
-  if (threadIdx.x == 0) out[0] = (float)(a / m);
+  fin_loss(part, nblk, m, out);
 }
 
 // dst_k[r, :] = src_k[idx[r], :], 16-B vectors when rows allow it.  blockIdx.y is the
@@ -313,15 +302,17 @@ __global__ __launch_bounds__(kBlock) void adam_kernel(AdamTable tab, float w1, f
 //   and the act quantizer's four sums -> dL/ddelta, dL/dzp.
 // One wave per (n, c) row; the pre-activation values are recomputed from y with the
 // forward's fp32 operations (bit-identical masks), nothing of the forward is stored.
-constexpr int kEpiParts = 6;
-
 template <bool RES, int ACT, bool QUANT, bool AFFINE, bool VEC>
 __global__ __launch_bounds__(kBlock) void epilogue_bwd_rows(
     const float* __restrict__ g, const float* __restrict__ y, const float* __restrict__ bias,
     const float* __restrict__ gamma, const float* __restrict__ phi, const float* __restrict__ res,
     uint32_t rows, uint32_t C, uint32_t hw, const float* __restrict__ qdelta,
     const float* __restrict__ qzp, float lo, float hi, float* __restrict__ gy,
-    float* __restrict__ gres, double* __restrict__ part) {
+    float* __restrict__ gres, double* __restrict__ part, FinTable fin, uint32_t nmain) {
+  if (blockIdx.x >= nmain) {          // queued finalize tasks ride on this launch
+    run_fin(fin, blockIdx.x - nmain);
+    return;
+  }
   const uint32_t lane = threadIdx.x & (kWave - 1);
   const uint32_t r = blockIdx.x * (kBlock / kWave) + threadIdx.x / kWave;
   if (r >= rows) return;
@@ -408,28 +399,87 @@ __global__ __launch_bounds__(kBlock) void epilogue_bwd_finalize(
     const double* __restrict__ part, uint32_t N, uint32_t C, uint32_t nb,
     float* __restrict__ ggamma, float* __restrict__ gphi, float* __restrict__ gdelta,
     float* __restrict__ gzp) {
-  __shared__ double red[16];
-  if (blockIdx.x < nb) {
-    const uint32_t c = blockIdx.x * kBlock + threadIdx.x;
-    if (c >= C) return;
-    double sg = 0, sp = 0;
-#pragma unroll 8
-    for (uint32_t n = 0; n < N; ++n) {
-      sg += part[((int64_t)n * C + c) * kEpiParts + 0];
-      sp += part[((int64_t)n * C + c) * kEpiParts + 1];
+  fin_epi(blockIdx.x, part, N, C, nb, ggamma, gphi, gdelta, gzp);
+}
+
+// the queued finalize tasks of a stream as one standalone launch
+__global__ __launch_bounds__(kBlock) void fin_tasks_kernel(FinTable fin) {
+  run_fin(fin, blockIdx.x);
+}
+
+// ------------------------------------------------------------------ finalize queue (host)
+static bool g_fin_defer = false;
+struct PendingFin {
+  hipStream_t s;
+  FinTask t;
+};
+constexpr int kMaxPendingFin = 16;
+static PendingFin g_fin_pending[kMaxPendingFin];
+static int g_fin_npending = 0;
+
+bool fin_defer_on() { return g_fin_defer; }
+
+FinTable fin_take(hipStream_t s) {
+  FinTable ft;
+  ft.n = 0;
+  ft.nwg = 0;
+  int keep = 0;
+  for (int i = 0; i < g_fin_npending; ++i) {
+    if (g_fin_pending[i].s == s && ft.n < kMaxFin) {
+      ft.t[ft.n++] = g_fin_pending[i].t;
+      ft.nwg += g_fin_pending[i].t.nwg;
+    } else {
+      g_fin_pending[keep++] = g_fin_pending[i];
     }
-    if (ggamma) ggamma[c] = (float)sg;
-    if (gphi) gphi[c] = (float)sp;
-    return;
   }
-  double a[4] = {0, 0, 0, 0};
-  for (uint32_t r = threadIdx.x; r < N * C; r += blockDim.x)
-    for (int k = 0; k < 4; ++k) a[k] += part[(int64_t)r * kEpiParts + 2 + k];
-  for (int k = 0; k < 4; ++k) a[k] = block_sum(a[k], red);
-  if (threadIdx.x == 0) {
-    if (gdelta) gdelta[0] = (float)(a[0] - a[1]);
-    if (gzp) gzp[0] = (float)(a[2] - a[3]);
+  g_fin_npending = keep;
+  return ft;
+}
+
+int fin_flush(hipStream_t s) {
+  for (;;) {
+    const FinTable ft = fin_take(s);
+    if (ft.n == 0) return SSQ_OK;
+    hipLaunchKernelGGL(fin_tasks_kernel, dim3(ft.nwg), dim3(kBlock), 0, s, ft);
+    const int rc = check_launch("ssq finalize tasks");
+    if (rc) return rc;
   }
+}
+
+int fin_push(hipStream_t s, const FinTask& t) {
+  int mine = 0;
+  for (int i = 0; i < g_fin_npending; ++i) mine += g_fin_pending[i].s == s;
+  if (mine >= kMaxFin || g_fin_npending >= kMaxPendingFin) {
+    const int rc = fin_flush(s);
+    if (rc) return rc;
+    if (g_fin_npending >= kMaxPendingFin) {   // other streams' tasks: launch them too
+      while (g_fin_npending) {
+        const int r2 = fin_flush(g_fin_pending[0].s);
+        if (r2) return r2;
+      }
+    }
+  }
+  g_fin_pending[g_fin_npending++] = PendingFin{s, t};
+  return SSQ_OK;
+}
+
+// A host launch about to write [w0, w0 + wn): tasks that read it are launched standalone
+// first; the rest are handed to the host.
+static FinTable fin_take_for_host(hipStream_t s, const void* w0, size_t wn, int* rc) {
+  *rc = SSQ_OK;
+  for (int i = 0; i < g_fin_npending; ++i) {
+    const PendingFin& pf = g_fin_pending[i];
+    if (pf.s != s || !w0) continue;
+    const char* a = (const char*)pf.t.part;
+    if (a >= (const char*)w0 && a < (const char*)w0 + wn) {
+      *rc = fin_flush(s);
+      FinTable none;
+      none.n = 0;
+      none.nwg = 0;
+      return none;
+    }
+  }
+  return fin_take(s);
 }
 
 }  // namespace ssq
@@ -451,6 +501,10 @@ static int lp_loss(const char* what, const float* pred, const float* tgt, const 
   const bool gather = idx != nullptr;
   SSQ_REQUIRE(!gather || (row >= 1 && n % row == 0 && n < (1ll << 31)), SSQ_E_ARG,
               "%s: n must be a whole number of target rows (< 2^31 elements)", what);
+  {  // a queued loss task reads the workspace this launch is about to overwrite
+    const int rc = fin_flush(s);
+    if (rc) return rc;
+  }
   const int grid = grid_for(n, kBlock * 4, kLossBlocks);
   const float inv_m = 1.0f / (float)M;  // mean backward: 1.0 / numel in fp32
   double* part = loss_out ? (double*)ws : nullptr;
@@ -474,9 +528,21 @@ static int lp_loss(const char* what, const float* pred, const float* tgt, const 
   const bool fuse = one && loss_out;
   hipLaunchKernelGGL(k, dim3(grid), dim3(kBlock), 0, s, pred, tgt, n, p, inv_m, grad, gscale,
                      relu_mask, vec, tr4, tr1, part, (double)M, fuse ? loss_out : nullptr);
-  if (loss_out && !fuse)
+  if (loss_out && !fuse) {
+    if (fin_defer_on()) {
+      FinTask t{};
+      t.kind = 0;
+      t.nwg = 1;
+      t.part = part;
+      t.a = (uint32_t)grid;
+      t.m = (double)M;
+      t.o[0] = loss_out;
+      const int rc = check_launch(what);
+      return rc ? rc : fin_push(s, t);
+    }
     hipLaunchKernelGGL(lp_loss_finalize, dim3(1), dim3(kBlock), 0, s, (const double*)part, grid,
                        (double)M, loss_out);
+  }
   return check_launch(what);
 }
 
@@ -604,13 +670,17 @@ extern "C" int ssq_epilogue_bwd(const float* g, const float* y, const float* bia
   auto al = [](const void* q) { return ((uintptr_t)q & 15u) == 0; };
   const bool vec = hw % 4 == 0 && al(g) && al(y) && al(gy) && (!res || al(res)) &&
                    (!gres || al(gres));
-  const dim3 grid((unsigned)((rows + kBlock / kWave - 1) / (kBlock / kWave)));
+  const uint32_t nmain = (uint32_t)((rows + kBlock / kWave - 1) / (kBlock / kWave));
+  int frc = SSQ_OK;
+  const FinTable fin = fin_take_for_host(s, ws, ws_bytes, &frc);
+  if (frc) return frc;
+  const dim3 grid(nmain + fin.nwg);
   const float lo = (float)qmin, hi = (float)qmax;
   double* part = (double*)ws;
 #define SSQ_EB(R, A, Q, F, V)                                                                  \
   hipLaunchKernelGGL((epilogue_bwd_rows<R, A, Q, F, V>), grid, dim3(kBlock), 0, s, g, y, bias, \
                      gamma, phi, res, (uint32_t)rows, (uint32_t)C, (uint32_t)hw, delta, zp, lo, \
-                     hi, gy, gres, part)
+                     hi, gy, gres, part, fin, nmain)
 #define SSQ_EB1(R, A, Q, F) \
   if (vec) SSQ_EB(R, A, Q, F, true); else SSQ_EB(R, A, Q, F, false);
 #define SSQ_EB2(R, A, Q) \
@@ -632,6 +702,21 @@ extern "C" int ssq_epilogue_bwd(const float* g, const float* y, const float* bia
     // sums over every row, one workgroup) only when delta / zp are
     const unsigned nb = (ggamma || gphi) ? (unsigned)((C + kBlock - 1) / kBlock) : 0u;
     const unsigned nq = (gdelta || gzp) ? 1u : 0u;
+    if (fin_defer_on()) {
+      FinTask t{};
+      t.kind = 1;
+      t.nwg = nb + nq;
+      t.part = part;
+      t.a = (uint32_t)N;
+      t.b = (uint32_t)C;
+      t.c = nb;
+      t.o[0] = ggamma;
+      t.o[1] = gphi;
+      t.o[2] = gdelta;
+      t.o[3] = gzp;
+      const int rc = check_launch("ssq_epilogue_bwd");
+      return rc ? rc : fin_push(s, t);
+    }
     hipLaunchKernelGGL(epilogue_bwd_finalize, dim3(nb + nq), dim3(kBlock), 0, s,
                        (const double*)part, (uint32_t)N, (uint32_t)C, nb, ggamma, gphi, gdelta,
                        gzp);
@@ -672,6 +757,10 @@ extern "C" int ssq_adam(int nseg, float* const* p, const float* const* g, float*
                         float one_minus_beta2, float eps, const float* hyper, float neg_step_size,
                         float bias_correction2_sqrt, ssq_stream_t stream) {
   SSQ_REQUIRE(nseg >= 1 && p && g && m && v && n, SSQ_E_ARG, "ssq_adam: bad arrays");
+  {  // queued gamma / phi / delta gradient finalizes must land before the update reads them
+    const int rc = fin_flush((hipStream_t)stream);
+    if (rc) return rc;
+  }
   for (int base = 0; base < nseg; base += kMaxAdamSeg) {
     AdamTable tab;
     tab.nseg = nseg - base < kMaxAdamSeg ? nseg - base : kMaxAdamSeg;
@@ -691,4 +780,14 @@ extern "C" int ssq_adam(int nseg, float* const* p, const float* const* g, float*
     if (rc) return rc;
   }
   return SSQ_OK;
+}
+
+extern "C" int ssq_set_deferred_finalize(int on) {
+  const int prev = g_fin_defer ? 1 : 0;
+  g_fin_defer = on != 0;
+  return prev;
+}
+
+extern "C" int ssq_flush_finalize(ssq_stream_t stream) {
+  return fin_flush((hipStream_t)stream);
 }

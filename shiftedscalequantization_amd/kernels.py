@@ -628,7 +628,7 @@ def lp_loss_and_grad(pred, tgt, p=2.0, reduction="none", want_grad=True, loss_ou
     pred, pp = fptr(pred.detach(), "pred")
     loss = torch.empty(1, dtype=torch.float32, device=pred.device) if loss_out is None else loss_out
     grad = torch.empty_like(pred) if want_grad else None
-    ws, wsn = workspace(query("ssq_lp_loss_workspace_size", pred.numel()), pred.device)
+    ws, wsn = workspace(query("ssq_lp_loss_workspace_size", pred.numel()), pred.device, "loss")
     M = _lp_M(pred, reduction)
     if isinstance(tgt, Rows):
         cache, cp = fptr(tgt.cache.detach(), "tgt cache")
@@ -865,7 +865,8 @@ class EpilogueFn(torch.autograd.Function):
         gd = torch.empty(1, device=dev_) if (quant and need[5]) else None
         gz = torch.empty(1, device=dev_) if (quant and need[6]) else None
         N = g.numel() // (C_ * hw)
-        ws, wsn = workspace(query("ssq_epilogue_bwd_workspace_size", N * C_), dev_)
+        # two alternating slots: a queued finalize of the previous call still reads its own
+        ws, wsn = workspace(query("ssq_epilogue_bwd_workspace_size", N * C_), dev_, _epi_slot())
         call("ssq_epilogue_bwd", gp, _vp(y), _vp(b), _vp(gm), _vp(ph),
              _vp(r.contiguous() if r is not None else None), N, C_, hw, int(relu), _vp(d), _vp(z),
              lo, hi, _vp(gy), _vp(gres), _vp(ggm), _vp(gph), _vp(gd), _vp(gz), ws, wsn,
@@ -873,6 +874,44 @@ class EpilogueFn(torch.autograd.Function):
         shape = (lambda t, o: None if o is None else o.view(t.shape))
         return (gy if need[0] else None, None, shape(gamma, ggm), shape(phi, gph), gres,
                 shape(delta, gd), shape(zp, gz), None, None, None)
+
+
+_EPI_SLOT = [0]
+
+
+def _epi_slot():
+    _EPI_SLOT[0] ^= 1
+    return "epi%d" % _EPI_SLOT[0]
+
+
+def set_deferred_finalize(on):
+    """Queue the loss / epilogue-backward finalizes onto the next host launch (include/ssq.h,
+    csrc/fin_tasks.h); returns the previous setting."""
+    return bool(query("ssq_set_deferred_finalize", int(bool(on))))
+
+
+def flush_finalize(device=None):
+    """Launch the finalizes still queued on the current stream."""
+    dev_ = torch.device("cuda", torch.cuda.current_device()) if device is None else device
+    call("ssq_flush_finalize", C.c_void_p(torch.cuda.current_stream(dev_).cuda_stream))
+
+
+class deferred_finalize:
+    """Context: deferral on inside, flushed and restored on exit (the recon loop body)."""
+
+    def __init__(self, on=True, device=None):
+        self.on, self.device = on, device
+
+    def __enter__(self):
+        self.prev = set_deferred_finalize(self.on) if self.on else None
+        return self
+
+    def __exit__(self, *exc):
+        if self.on:
+            try:
+                flush_finalize(self.device)
+            finally:
+                set_deferred_finalize(self.prev)
 
 
 def epilogue(y, bias, gamma, phi, res, relu, q=None):

@@ -24,6 +24,9 @@ from ._engine import (BatchFeeder, IterationGraph, LazyValue, SsqAdam, as_float,
 from .quant_block import BaseQuantBlock
 from .quant_layer import QuantModule
 
+# A/B knob: deferred loss / epilogue finalizes inside the loop body (bit-identical either way)
+DEFER_FINALIZE = True
+
 
 def print_ratio(quantizers):
     """layer_recon_fused_shiftedScale.py:13-21: histogram of the selected shift index."""
@@ -93,9 +96,18 @@ def _fused_loop(block, modules, iters, lmda, model, p, lr, bias_cal, batch_size,
     hyper = feeder.extra[2:4]
     last = {}
 
+    # one GPU: the loss value and gamma^z/phi^z finalizes ride on the next backward launch
+    # (csrc/fin_tasks.h); with a bucket the grads are accumulated in place by autograd, so
+    # they must be final when backward returns them
+    defer = DEFER_FINALIZE and on_gpu and bucket is None
+
     def body_pre():
         """One iteration on the device up to its exchange step: gather -> forward -> fused
         loss+grad -> backward.  No host sync, no host-side state: graph-capturable."""
+        with K.deferred_finalize(defer):
+            _body_pre()
+
+    def _body_pre():
         cur_inp, cur_out = feeder.gather_lazy()
         if on_gpu:
             stash_block_weights(quantizers)     # every conv's What in one launch

@@ -438,3 +438,46 @@ def test_brecq_other_blocks_match_reference(Q, golden, kind):
         stats[n + "_hard_flips"] = np.sum(what != g[f"b_{n}_what_hard"])
         assert np.mean(what != g[f"b_{n}_what_hard"]) <= 0.002, n
     parity_report(f"a22_brecq_{kind}", **stats)
+
+
+@pytest.mark.parametrize("graph", [False, True])
+def test_deferred_finalize_bit_identical(Q, golden, graph):
+    """The fused loop with bias_cal queues its loss and gamma^z/phi^z finalizes onto the next
+    backward launch (csrc/fin_tasks.h): alpha, gamma^z, phi^z and every iteration's loss
+    are bit-identical to the loop that launches each finalize on its own."""
+    import importlib
+    LRF = importlib.import_module("shiftedscalequantization_amd.quant.layer_recon_fused_shiftedScale")
+    g = golden("recon_fused")
+    runs = []
+    for defer in (False, True):
+        qnn = build_qnn(Q, {})
+        block = qnn.model[3]
+        load_block(Q, g, block)
+        block.cached_inp_features = [dev(g["cached_inp"])]
+        block.cached_out_features = [dev(g["cached_out"])]
+        seen = []
+        orig_keep = LRF.FusedScaleLossFunction.bookkeep
+
+        def bookkeep(self, rec):
+            seen.append(float(rec.item()))
+            return orig_keep(self, rec)
+
+        LRF.FusedScaleLossFunction.bookkeep, prev = bookkeep, LRF.DEFER_FINALIZE
+        LRF.DEFER_FINALIZE = defer
+        try:
+            torch.manual_seed(1005)
+            res = LRF.block_recon_fused_shiftedScale(block, 12, (0.01, 0.1), qnn, None, verbose=False,
+                                                     graph=graph, bias_cal=True)
+        finally:
+            LRF.FusedScaleLossFunction.bookkeep, LRF.DEFER_FINALIZE = orig_keep, prev
+        out = {"rec": np.array(seen), "final": np.array(res)}
+        for n in ("conv1", "conv2", "downsample"):
+            m = getattr(block, n)
+            out[n + "_alpha"] = m.weight_quantizer.alpha.detach().cpu().numpy()
+            out[n + "_gamma"] = m.alpha_out.detach().cpu().numpy()
+            out[n + "_phi"] = m.beta_out.detach().cpu().numpy()
+        runs.append(out)
+    for k in runs[0]:
+        np.testing.assert_array_equal(runs[1][k], runs[0][k], err_msg=k)
+    # gamma^z / phi^z really were learned (their finalizes ran)
+    assert any(np.any(runs[1][n + "_gamma"] != 1.0) for n in ("conv1", "conv2", "downsample"))
