@@ -3,8 +3,9 @@
  * PTQ calibration path.  Plain pointers and sizes only: every pointer is DEVICE
  * memory owned by the caller (PyTorch's caching allocator in the Python host layer),
  * borrowed for the duration of the call.  Launches are asynchronous on `stream`
- * (a hipStream_t passed as void*); no entry point allocates, synchronizes or keeps
- * state, so every call is graph-capturable.
+ * (a hipStream_t passed as void*); no entry point allocates or synchronizes, and none
+ * keeps state except the opt-in deferred-finalize queue (ssq_set_deferred_finalize), so
+ * every call is graph-capturable.
  *
  * Return value: 0 on success; a negative SSQ_E* code for an argument error; otherwise
  * the hipError_t of a failed launch.  ssq_last_error() returns a thread-local message.
@@ -375,6 +376,15 @@ size_t ssq_conv_wgrad_workspace_size(int64_t Nb, int64_t C, int64_t H, int64_t W
 int ssq_conv_wgrad(const float* x, const float* dy, int64_t Nb, int64_t C, int64_t H, int64_t W,
                    int64_t Co, int64_t R, int64_t S, int64_t stride, int64_t pad, int64_t groups,
                    float* dw, void* ws, size_t ws_bytes, ssq_stream_t stream);
+/* The same weight gradient as one fp32 library GEMM (small output planes, where it beats
+ * the band kernel): the two operands, written in one launch,
+ *   dy2[co][n*P + p] = dy[n][co][p]                                  (Co x N*P)
+ *   col[n*P + p][(ci*R + r)*S + s] = x[n][ci][oh*st+r-pad][ow*st+s-pad] (N*P x C*R*S, 0 outside)
+ * with P = OH*OW; then dw = dy2 @ col (Co x C*R*S = dw's layout) by the caller's GEMM.
+ * Ungrouped convs; every operand < 2^31 elements. */
+int ssq_wgrad_gemm_operands(const float* x, const float* dy, int64_t Nb, int64_t C, int64_t H,
+                            int64_t W, int64_t Co, int64_t R, int64_t S, int64_t stride,
+                            int64_t pad, float* col, float* dy2, ssq_stream_t stream);
 
 /* ---------------------------------------------------------------- K18 depthwise conv
  * Depthwise (groups == C == Co) fp32 NCHW conv, dilation 1, R*S <= 25, zero padding:

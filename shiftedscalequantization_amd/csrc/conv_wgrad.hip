@@ -1253,3 +1253,65 @@ extern "C" int ssq_conv_wgrad(const float* x, const float* dy, int64_t Nb, int64
                      dim3(256), 0, s, (const float*)ws, g.nsplit, n, dw);
   return check_launch("ssq_conv_wgrad");
 }
+
+// ------------------------------------------------------------------ GEMM operands
+// The conv weight gradient as ONE library GEMM, for the small output planes where it beats
+// the band kernel (ResNet-18 layer3/4: 14x14 and 7x7 planes, K = N*OH*OW of 1.5-6 K):
+//   dW[Co, C*R*S] = dy2[Co, N*P] @ col[N*P, C*R*S],  P = OH*OW,
+//   dy2[co][n*P + p] = dy[n][co][p],
+//   col[n*P + p][(ci*R + r)*S + s] = x[n][ci][oh*st + r - pad][ow*st + s - pad] (0 outside).
+// One launch writes both operands (workgroups [0, nb1) col, the rest dy2); writes are
+// coalesced along the rows, the x / dy reads hit L2 (the tensors are a few MB).  The GEMM
+// (torch.matmul: hipBLASLt, fp32, one deterministic kernel per shape) is the caller's.
+__global__ __launch_bounds__(kBlock) void wgrad_gemm_operands(
+    const float* __restrict__ x, const float* __restrict__ dy, uint32_t C, uint32_t H,
+    uint32_t W, uint32_t Co, uint32_t R, uint32_t S, uint32_t st, int pad, uint32_t OW,
+    uint32_t NP, FastDiv dCRS, FastDiv dRS, FastDiv dS, FastDiv dP, FastDiv dOW, uint32_t CRS,
+    uint32_t P, uint32_t nb1, float* __restrict__ col, float* __restrict__ dy2) {
+  if (blockIdx.x < nb1) {
+    const uint32_t n1 = NP * CRS;
+    for (uint32_t e = blockIdx.x * kBlock + threadIdx.x; e < n1; e += nb1 * kBlock) {
+      const uint32_t row = fdiv(e, dCRS), k = e - row * CRS;
+      const uint32_t n = fdiv(row, dP), p = row - n * P;
+      const uint32_t oh = fdiv(p, dOW), ow = p - oh * OW;
+      const uint32_t ci = fdiv(k, dRS), rs = k - ci * R * S;
+      const uint32_t r = fdiv(rs, dS), s = rs - r * S;
+      const int ih = (int)(oh * st + r) - pad, iw = (int)(ow * st + s) - pad;
+      float v = 0.0f;
+      if (ih >= 0 && ih < (int)H && iw >= 0 && iw < (int)W)
+        v = x[(((size_t)n * C + ci) * H + ih) * W + iw];
+      col[e] = v;
+    }
+    return;
+  }
+  const uint32_t nb2 = gridDim.x - nb1;
+  const uint32_t n2 = Co * NP;
+  for (uint32_t e = (blockIdx.x - nb1) * kBlock + threadIdx.x; e < n2; e += nb2 * kBlock) {
+    const uint32_t co = e / NP, q = e - co * NP;
+    const uint32_t n = fdiv(q, dP), p = q - n * P;
+    dy2[e] = dy[((size_t)n * Co + co) * P + p];
+  }
+}
+
+extern "C" int ssq_wgrad_gemm_operands(const float* x, const float* dy, int64_t Nb, int64_t C,
+                                       int64_t H, int64_t W, int64_t Co, int64_t R, int64_t S,
+                                       int64_t stride, int64_t pad, float* col, float* dy2,
+                                       ssq_stream_t stream) {
+  SSQ_REQUIRE(x && dy && col && dy2, SSQ_E_ARG, "ssq_wgrad_gemm_operands: null pointer");
+  SSQ_REQUIRE(Nb >= 1 && C >= 1 && H >= 1 && W >= 1 && Co >= 1 && R >= 1 && S >= 1 &&
+                  stride >= 1 && pad >= 0, SSQ_E_ARG, "ssq_wgrad_gemm_operands: bad geometry");
+  const int64_t OH = (H + 2 * pad - R) / stride + 1, OW = (W + 2 * pad - S) / stride + 1;
+  SSQ_REQUIRE(OH >= 1 && OW >= 1, SSQ_E_ARG, "ssq_wgrad_gemm_operands: empty output plane");
+  const int64_t P = OH * OW, NP = Nb * P, CRS = C * R * S;
+  SSQ_REQUIRE(NP * CRS < (1ll << 31) && Co * NP < (1ll << 31) && Nb * C * H * W < (1ll << 31),
+              SSQ_E_ARG, "ssq_wgrad_gemm_operands: operands exceed 2^31 elements");
+  const uint32_t nb1 = (uint32_t)std::min<int64_t>((NP * CRS + kBlock - 1) / kBlock, 8192);
+  const uint32_t nb2 = (uint32_t)std::min<int64_t>((Co * NP + kBlock - 1) / kBlock, 2048);
+  hipLaunchKernelGGL(wgrad_gemm_operands, dim3(nb1 + nb2), dim3(kBlock), 0, (hipStream_t)stream,
+                     x, dy, (uint32_t)C, (uint32_t)H, (uint32_t)W, (uint32_t)Co, (uint32_t)R,
+                     (uint32_t)S, (uint32_t)stride, (int)pad, (uint32_t)OW, (uint32_t)NP,
+                     make_fastdiv((uint32_t)CRS), make_fastdiv((uint32_t)(R * S)),
+                     make_fastdiv((uint32_t)S), make_fastdiv((uint32_t)P),
+                     make_fastdiv((uint32_t)OW), (uint32_t)CRS, (uint32_t)P, nb1, col, dy2);
+  return check_launch("ssq_wgrad_gemm_operands");
+}

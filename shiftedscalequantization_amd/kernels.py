@@ -1050,6 +1050,26 @@ def conv_wgrad(x, dy, w_shape, stride, padding, groups):
     return dw
 
 
+def conv_wgrad_gemm(x, dy, w_shape, stride, padding):
+    """The same weight gradient as ONE fp32 library GEMM: ssq_wgrad_gemm_operands writes
+    dy2 (Co x N*P) and the im2col matrix (N*P x C*R*S) in one launch, then
+    dw = dy2 @ col (torch.matmul -> hipBLASLt; one kernel per shape, bit-identical run to
+    run).  Ungrouped convs.  Faster than the band kernel on small output planes."""
+    st = stride if isinstance(stride, int) else stride[0]
+    pad = padding if isinstance(padding, int) else padding[0]
+    x, xp = fptr(x.detach(), "x")
+    dy, dp = fptr(dy.detach(), "dy")
+    Nb, C_, H, W = (int(v) for v in x.shape)
+    Co, _, R, S = (int(v) for v in w_shape)
+    OH, OW = (H + 2 * pad - R) // st + 1, (W + 2 * pad - S) // st + 1
+    NP = Nb * OH * OW
+    col = torch.empty(NP, C_ * R * S, dtype=torch.float32, device=x.device)
+    dy2 = torch.empty(Co, NP, dtype=torch.float32, device=x.device)
+    call("ssq_wgrad_gemm_operands", xp, dp, Nb, C_, H, W, Co, R, S, int(st), int(pad), _vp(col),
+         _vp(dy2), stream_of(x))
+    return torch.matmul(dy2, col).view(tuple(w_shape))
+
+
 # ------------------------------------------------------------------ K18 depthwise conv
 def dwconv_supported(x, weight, stride, padding, dilation, groups):
     """Depthwise shapes K18 handles: fp32 NCHW on the device, groups == C == Co, square
@@ -1150,7 +1170,10 @@ class Conv2dFn(torch.autograd.Function):
                 g, x, weight, None, _pair(stride), _pair(padding), _pair(dilation), False,
                 [0, 0], groups, (True, False, False))[0]
         if ctx.needs_input_grad[1]:
-            gw = conv_wgrad(x, g, weight.shape, stride, padding, groups)
+            if _use_wgrad_gemm(x, weight, stride, padding, groups):
+                gw = conv_wgrad_gemm(x, g, weight.shape, stride, padding)
+            else:
+                gw = conv_wgrad(x, g, weight.shape, stride, padding, groups)
         return gx, gw, None, None, None, None
 
 
@@ -1170,12 +1193,44 @@ class Conv2dFn(torch.autograd.Function):
 WGRAD_POLICY = "auto"
 
 
+# Conv weight gradients as ONE library GEMM over an im2col matrix (conv_wgrad_gemm) where
+# the output plane is small: 3x3 (or larger) ungrouped convs with OH*OW <= 196,
+# Co >= 128 and C*R*S >= 1152 -- ResNet-18 layer3 / layer4 (tools/gemm_probe.py,
+# profiles/r2_wgrad_gemm.log: the GEMM runs at 94-115 TF there, the band kernel at 57 TF
+# on 14x14 planes).  'never' keeps K17 / MIOpen (A/B).
+WGRAD_GEMM = "auto"
+
+
+def _out_plane(x, weight, stride, padding):
+    st = stride if isinstance(stride, int) else stride[0]
+    pad = padding if isinstance(padding, int) else padding[0]
+    oh = (x.shape[2] + 2 * pad - weight.shape[2]) // st + 1
+    ow = (x.shape[3] + 2 * pad - weight.shape[3]) // st + 1
+    return oh, ow
+
+
+def _use_wgrad_gemm(x, weight, stride, padding, groups=1):
+    if WGRAD_GEMM != "auto" or groups != 1 or weight.shape[2] * weight.shape[3] == 1:
+        return False
+    if isinstance(stride, (tuple, list)) and len(set(stride)) != 1:
+        return False
+    if isinstance(padding, str) or (isinstance(padding, (tuple, list)) and len(set(padding)) != 1):
+        return False
+    oh, ow = _out_plane(x, weight, stride, padding)
+    Co, C_, R, S = (int(v) for v in weight.shape)
+    NP = x.shape[0] * oh * ow
+    return (oh * ow <= 196 and Co >= 128 and C_ * R * S >= 1152 and NP * C_ * R * S < (1 << 31)
+            and Co * NP < (1 << 31))
+
+
 def _use_k17(x, weight, stride, padding, groups=1):
     if WGRAD_POLICY == "always":
         return True
     if WGRAD_POLICY != "auto":
         return False
     if groups > 1:
+        return True
+    if _use_wgrad_gemm(x, weight, stride, padding, groups):
         return True
     if wgrad_kind(x.shape, weight.shape, stride, padding, groups) == 3:
         return True
@@ -1202,7 +1257,9 @@ def conv2d(x, weight, stride=1, padding=0, dilation=1, groups=1):
             return DwConv2dFn.apply(x, weight, stride, padding)
         return dwconv_fwd(x, weight, stride, padding)
     if weight.requires_grad and torch.is_grad_enabled() and \
-            conv_wgrad_supported(x, weight, stride, padding, dilation, groups) and \
-            _use_k17(x, weight, stride, padding, groups):
+            (dilation if isinstance(dilation, int) else max(dilation)) == 1 and \
+            (_use_wgrad_gemm(x, weight, stride, padding, groups) or
+             (conv_wgrad_supported(x, weight, stride, padding, dilation, groups) and
+              _use_k17(x, weight, stride, padding, groups))):
         return Conv2dFn.apply(x, weight, stride, padding, dilation, groups)
     return torch.nn.functional.conv2d(x, weight, None, stride, padding, dilation, groups)

@@ -767,11 +767,54 @@ def test_conv_wgrad_matches_fp64(K, cfg, wgrad_form):
     assert bool((err <= 1e-5 * mag + 1e-30).all()), float((err / mag.clamp_min(1e-30)).max())
     wd = w.cuda().requires_grad_(True)
     old, K.WGRAD_POLICY = K.WGRAD_POLICY, "always"
+    old_gemm, K.WGRAD_GEMM = K.WGRAD_GEMM, "never"
     try:
         out = K.conv2d(xd, wd, st, pad, 1, g)
         out.backward(dyd)
     finally:
-        K.WGRAD_POLICY = old
+        K.WGRAD_POLICY, K.WGRAD_GEMM = old, old_gemm
+    np.testing.assert_array_equal(host(wd.grad).view(np.int32), host(dw1).view(np.int32))
+
+
+@pytest.mark.parametrize("cfg", [
+    # (Nb, C, H, Co, k, stride, pad): ResNet-18 layer3 / layer3.0 s2 / layer4 / layer4.0 s2
+    # at batch 32 (the shapes the GEMM policy takes), a 5x5 and ragged sizes
+    (32, 256, 14, 256, 3, 1, 1), (32, 128, 28, 256, 3, 2, 1), (32, 512, 7, 512, 3, 1, 1),
+    (32, 256, 14, 512, 3, 2, 1), (3, 130, 9, 140, 3, 1, 1), (2, 64, 11, 128, 5, 2, 2)])
+def test_conv_wgrad_gemm_matches_fp64(K, cfg):
+    """The im2col + library-GEMM weight gradient (ssq_wgrad_gemm_operands + hipBLASLt) vs
+    the fp64 CPU gradient within the fp32 accumulation bound; its operands equal a host
+    im2col / permute exactly; bit-identical run to run; and K.conv2d routes the policy's
+    shapes to it."""
+    Nb, C, H, Co, k, st, pad = cfg
+    gen = torch.Generator().manual_seed(sum(cfg))
+    x = torch.randn(Nb, C, H, H, generator=gen)
+    w = torch.randn(Co, C, k, k, generator=gen)
+    y = torch.nn.functional.conv2d(x, w, None, st, pad)
+    dy = torch.randn(y.shape, generator=gen)
+    ref = torch.nn.grad.conv2d_weight(x.double(), w.shape, dy.double(), st, pad)
+    mag = torch.nn.grad.conv2d_weight(x.double().abs(), w.shape, dy.double().abs(), st, pad)
+    xd, dyd = x.cuda(), dy.cuda()
+    # the operands themselves, exactly
+    OH = y.shape[2]
+    NP = Nb * OH * OH
+    col = torch.empty(NP, C * k * k, device="cuda")
+    dy2 = torch.empty(Co, NP, device="cuda")
+    K.call("ssq_wgrad_gemm_operands", K.C.c_void_p(xd.data_ptr()), K.C.c_void_p(dyd.data_ptr()),
+           Nb, C, H, H, Co, k, k, st, pad, K.C.c_void_p(col.data_ptr()),
+           K.C.c_void_p(dy2.data_ptr()), K.stream_of(xd))
+    cref = torch.nn.functional.unfold(x, k, padding=pad, stride=st)        # (N, C*k*k, P)
+    np.testing.assert_array_equal(host(col), cref.permute(0, 2, 1).reshape(NP, -1).numpy())
+    np.testing.assert_array_equal(host(dy2), dy.permute(1, 0, 2, 3).reshape(Co, -1).numpy())
+    dw1 = K.conv_wgrad_gemm(xd, dyd, w.shape, st, pad)
+    dw2 = K.conv_wgrad_gemm(xd, dyd, w.shape, st, pad)
+    np.testing.assert_array_equal(host(dw1).view(np.int32), host(dw2).view(np.int32))
+    err = (dw1.double().cpu() - ref).abs()
+    assert bool((err <= 1e-5 * mag + 1e-30).all()), float((err / mag.clamp_min(1e-30)).max())
+    wd = w.cuda().requires_grad_(True)
+    assert K._use_wgrad_gemm(xd, wd, st, pad)
+    out = K.conv2d(xd, wd, st, pad)
+    out.backward(dyd)
     np.testing.assert_array_equal(host(wd.grad).view(np.int32), host(dw1).view(np.int32))
 
 
