@@ -381,7 +381,9 @@ int ssq_conv_wgrad(const float* x, const float* dy, int64_t Nb, int64_t C, int64
  *   dy2[co][n*P + p] = dy[n][co][p]                                  (Co x N*P)
  *   col[n*P + p][(ci*R + r)*S + s] = x[n][ci][oh*st+r-pad][ow*st+s-pad] (N*P x C*R*S, 0 outside)
  * with P = OH*OW; then dw = dy2 @ col (Co x C*R*S = dw's layout) by the caller's GEMM.
- * Ungrouped convs; every operand < 2^31 elements. */
+ * Either output may be NULL (with its input): the forward GEMM y2 = W @ col^T needs col
+ * only, a backward with a saved col needs dy2 only.  Ungrouped convs; every operand
+ * < 2^31 elements. */
 int ssq_wgrad_gemm_operands(const float* x, const float* dy, int64_t Nb, int64_t C, int64_t H,
                             int64_t W, int64_t Co, int64_t R, int64_t S, int64_t stride,
                             int64_t pad, float* col, float* dy2, ssq_stream_t stream);

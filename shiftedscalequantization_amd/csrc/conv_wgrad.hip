@@ -1297,7 +1297,9 @@ extern "C" int ssq_wgrad_gemm_operands(const float* x, const float* dy, int64_t 
                                        int64_t H, int64_t W, int64_t Co, int64_t R, int64_t S,
                                        int64_t stride, int64_t pad, float* col, float* dy2,
                                        ssq_stream_t stream) {
-  SSQ_REQUIRE(x && dy && col && dy2, SSQ_E_ARG, "ssq_wgrad_gemm_operands: null pointer");
+  SSQ_REQUIRE((x && col) || (dy && dy2), SSQ_E_ARG, "ssq_wgrad_gemm_operands: null pointer");
+  if (!(x && col)) col = nullptr;
+  if (!(dy && dy2)) dy2 = nullptr;
   SSQ_REQUIRE(Nb >= 1 && C >= 1 && H >= 1 && W >= 1 && Co >= 1 && R >= 1 && S >= 1 &&
                   stride >= 1 && pad >= 0, SSQ_E_ARG, "ssq_wgrad_gemm_operands: bad geometry");
   const int64_t OH = (H + 2 * pad - R) / stride + 1, OW = (W + 2 * pad - S) / stride + 1;
@@ -1305,8 +1307,8 @@ extern "C" int ssq_wgrad_gemm_operands(const float* x, const float* dy, int64_t 
   const int64_t P = OH * OW, NP = Nb * P, CRS = C * R * S;
   SSQ_REQUIRE(NP * CRS < (1ll << 31) && Co * NP < (1ll << 31) && Nb * C * H * W < (1ll << 31),
               SSQ_E_ARG, "ssq_wgrad_gemm_operands: operands exceed 2^31 elements");
-  const uint32_t nb1 = (uint32_t)std::min<int64_t>((NP * CRS + kBlock - 1) / kBlock, 8192);
-  const uint32_t nb2 = (uint32_t)std::min<int64_t>((Co * NP + kBlock - 1) / kBlock, 2048);
+  const uint32_t nb1 = col ? (uint32_t)std::min<int64_t>((NP * CRS + kBlock - 1) / kBlock, 8192) : 0u;
+  const uint32_t nb2 = dy2 ? (uint32_t)std::min<int64_t>((Co * NP + kBlock - 1) / kBlock, 2048) : 0u;
   hipLaunchKernelGGL(wgrad_gemm_operands, dim3(nb1 + nb2), dim3(kBlock), 0, (hipStream_t)stream,
                      x, dy, (uint32_t)C, (uint32_t)H, (uint32_t)W, (uint32_t)Co, (uint32_t)R,
                      (uint32_t)S, (uint32_t)stride, (int)pad, (uint32_t)OW, (uint32_t)NP,

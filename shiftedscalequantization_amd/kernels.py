@@ -1050,24 +1050,50 @@ def conv_wgrad(x, dy, w_shape, stride, padding, groups):
     return dw
 
 
-def conv_wgrad_gemm(x, dy, w_shape, stride, padding):
-    """The same weight gradient as ONE fp32 library GEMM: ssq_wgrad_gemm_operands writes
-    dy2 (Co x N*P) and the im2col matrix (N*P x C*R*S) in one launch, then
-    dw = dy2 @ col (torch.matmul -> hipBLASLt; one kernel per shape, bit-identical run to
-    run).  Ungrouped convs.  Faster than the band kernel on small output planes."""
+def _gemm_geo(x_shape, w_shape, stride, padding):
     st = stride if isinstance(stride, int) else stride[0]
     pad = padding if isinstance(padding, int) else padding[0]
-    x, xp = fptr(x.detach(), "x")
-    dy, dp = fptr(dy.detach(), "dy")
-    Nb, C_, H, W = (int(v) for v in x.shape)
+    Nb, C_, H, W = (int(v) for v in x_shape)
     Co, _, R, S = (int(v) for v in w_shape)
     OH, OW = (H + 2 * pad - R) // st + 1, (W + 2 * pad - S) // st + 1
+    return Nb, C_, H, W, Co, R, S, int(st), int(pad), OH, OW
+
+
+def gemm_operands(x, dy, w_shape, stride, padding, want_col=True, want_dy2=True):
+    """ssq_wgrad_gemm_operands: the im2col matrix col (N*P x C*R*S) of x and/or the
+    permuted gradient dy2 (Co x N*P), in one launch."""
+    shape = x.shape if x is not None else None
+    Nb, C_, H, W, Co, R, S, st, pad, OH, OW = _gemm_geo(shape, w_shape, stride, padding)
     NP = Nb * OH * OW
-    col = torch.empty(NP, C_ * R * S, dtype=torch.float32, device=x.device)
-    dy2 = torch.empty(Co, NP, dtype=torch.float32, device=x.device)
-    call("ssq_wgrad_gemm_operands", xp, dp, Nb, C_, H, W, Co, R, S, int(st), int(pad), _vp(col),
-         _vp(dy2), stream_of(x))
+    dev_ = (x if x is not None else dy).device
+    col = torch.empty(NP, C_ * R * S, dtype=torch.float32, device=dev_) if want_col else None
+    dy2 = torch.empty(Co, NP, dtype=torch.float32, device=dev_) if want_dy2 else None
+    xp = fptr(x.detach(), "x")[1] if want_col else None
+    dp = fptr(dy.detach(), "dy")[1] if want_dy2 else None
+    call("ssq_wgrad_gemm_operands", xp, dp, Nb, C_, H, W, Co, R, S, st, pad, _vp(col), _vp(dy2),
+         stream_of(col if want_col else dy2))
+    return col, dy2
+
+
+def conv_wgrad_gemm(x, dy, w_shape, stride, padding, col=None):
+    """The conv weight gradient as ONE fp32 library GEMM: dw = dy2 @ col
+    (torch.matmul -> hipBLASLt; one kernel per shape, bit-identical run to run), the
+    operands from ssq_wgrad_gemm_operands (col may be the forward's, saved).  Ungrouped
+    convs.  Faster than the band kernel on small output planes."""
+    c2, dy2 = gemm_operands(x if col is None else x, dy, w_shape, stride, padding,
+                            want_col=col is None, want_dy2=True)
+    col = c2 if col is None else col
     return torch.matmul(dy2, col).view(tuple(w_shape))
+
+
+def conv_fwd_gemm(x, weight, stride, padding):
+    """F.conv2d (no bias, ungrouped) as one fp32 library GEMM y2 = W[Co, C*R*S] @ col^T,
+    then y2 (Co x N*P) permuted to NCHW.  Returns (y, col); col serves the weight gradient."""
+    Nb, C_, H, W, Co, R, S, st, pad, OH, OW = _gemm_geo(x.shape, weight.shape, stride, padding)
+    col, _ = gemm_operands(x, None, weight.shape, stride, padding, want_col=True, want_dy2=False)
+    y2 = torch.matmul(weight.detach().reshape(Co, C_ * R * S), col.t())
+    y = y2.view(Co, Nb, OH * OW).permute(1, 0, 2).contiguous().view(Nb, Co, OH, OW)
+    return y, col
 
 
 # ------------------------------------------------------------------ K18 depthwise conv
@@ -1152,13 +1178,19 @@ class Conv2dFn(torch.autograd.Function):
 
     @staticmethod
     def forward(ctx, x, weight, stride, padding, dilation, groups):
-        ctx.save_for_backward(x, weight)
         ctx.cfg = (stride, padding, dilation, groups)
+        if _use_wgrad_gemm(x, weight, stride, padding, groups) and WGRAD_GEMM_FWD:
+            # small planes: the forward as one library GEMM over the im2col matrix, kept
+            # for the weight gradient's GEMM
+            y, col = conv_fwd_gemm(x, weight, stride, padding)
+            ctx.save_for_backward(x, weight, col)
+            return y
+        ctx.save_for_backward(x, weight, None)
         return torch.nn.functional.conv2d(x, weight, None, stride, padding, dilation, groups)
 
     @staticmethod
     def backward(ctx, g):
-        x, weight = ctx.saved_tensors
+        x, weight, col = ctx.saved_tensors
         stride, padding, dilation, groups = ctx.cfg
         g = g.contiguous()
         gx = gw = None
@@ -1170,8 +1202,8 @@ class Conv2dFn(torch.autograd.Function):
                 g, x, weight, None, _pair(stride), _pair(padding), _pair(dilation), False,
                 [0, 0], groups, (True, False, False))[0]
         if ctx.needs_input_grad[1]:
-            if _use_wgrad_gemm(x, weight, stride, padding, groups):
-                gw = conv_wgrad_gemm(x, g, weight.shape, stride, padding)
+            if col is not None or _use_wgrad_gemm(x, weight, stride, padding, groups):
+                gw = conv_wgrad_gemm(x, g, weight.shape, stride, padding, col=col)
             else:
                 gw = conv_wgrad(x, g, weight.shape, stride, padding, groups)
         return gx, gw, None, None, None, None
@@ -1199,6 +1231,10 @@ WGRAD_POLICY = "auto"
 # profiles/r2_wgrad_gemm.log: the GEMM runs at 94-115 TF there, the band kernel at 57 TF
 # on 14x14 planes).  'never' keeps K17 / MIOpen (A/B).
 WGRAD_GEMM = "auto"
+# ... and the forward of those convs too (MIOpen's deterministic forward takes 99 / 173 us
+# on layer3.0 / layer4.0's stride-2 convs where the GEMM takes 42 / 38,
+# profiles/r2_wgrad_gemm.log); the im2col matrix is then shared with the weight gradient
+WGRAD_GEMM_FWD = True
 
 
 def _out_plane(x, weight, stride, padding):

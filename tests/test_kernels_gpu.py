@@ -784,8 +784,9 @@ def test_conv_wgrad_matches_fp64(K, cfg, wgrad_form):
 def test_conv_wgrad_gemm_matches_fp64(K, cfg):
     """The im2col + library-GEMM weight gradient (ssq_wgrad_gemm_operands + hipBLASLt) vs
     the fp64 CPU gradient within the fp32 accumulation bound; its operands equal a host
-    im2col / permute exactly; bit-identical run to run; and K.conv2d routes the policy's
-    shapes to it."""
+    im2col / permute exactly; bit-identical run to run; K.conv2d routes the policy's
+    shapes to it, with the forward as the GEMM over the same im2col matrix (vs the fp64
+    conv) and the input gradient unchanged."""
     Nb, C, H, Co, k, st, pad = cfg
     gen = torch.Generator().manual_seed(sum(cfg))
     x = torch.randn(Nb, C, H, H, generator=gen)
@@ -814,8 +815,22 @@ def test_conv_wgrad_gemm_matches_fp64(K, cfg):
     wd = w.cuda().requires_grad_(True)
     assert K._use_wgrad_gemm(xd, wd, st, pad)
     out = K.conv2d(xd, wd, st, pad)
+    # the forward runs as the GEMM too (K.WGRAD_GEMM_FWD): vs the fp64 conv
+    yref = torch.nn.functional.conv2d(x.double(), w.double(), None, st, pad)
+    ymag = torch.nn.functional.conv2d(x.double().abs(), w.double().abs(), None, st, pad)
+    assert out.shape == yref.shape and out.is_contiguous()
+    yerr = (out.detach().double().cpu() - yref).abs()
+    assert bool((yerr <= 1e-5 * ymag + 1e-30).all()), float((yerr / ymag.clamp_min(1e-30)).max())
     out.backward(dyd)
     np.testing.assert_array_equal(host(wd.grad).view(np.int32), host(dw1).view(np.int32))
+    # input gradient (MIOpen, from the saved input) vs the fp64 one (MIOpen may pick another
+    # solver than for the plain conv's joint backward, so not bit-compared with it)
+    xg = xd.clone().requires_grad_(True)
+    K.conv2d(xg, w.cuda().requires_grad_(True), st, pad).backward(dyd)
+    gref = torch.nn.grad.conv2d_input(x.shape, w.double(), dy.double(), st, pad)
+    gmag = torch.nn.grad.conv2d_input(x.shape, w.double().abs(), dy.double().abs(), st, pad)
+    gerr = (xg.grad.double().cpu() - gref).abs()
+    assert bool((gerr <= 1e-5 * gmag + 1e-30).all()), float((gerr / gmag.clamp_min(1e-30)).max())
 
 
 @pytest.mark.parametrize("cfg", [
