@@ -1179,7 +1179,7 @@ class Conv2dFn(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, weight, stride, padding, dilation, groups):
         ctx.cfg = (stride, padding, dilation, groups)
-        if _use_wgrad_gemm(x, weight, stride, padding, groups) and WGRAD_GEMM_FWD:
+        if _use_fwd_gemm(x, weight, stride, padding, groups):
             # small planes: the forward as one library GEMM over the im2col matrix, kept
             # for the weight gradient's GEMM
             y, col = conv_fwd_gemm(x, weight, stride, padding)
@@ -1202,7 +1202,7 @@ class Conv2dFn(torch.autograd.Function):
                 g, x, weight, None, _pair(stride), _pair(padding), _pair(dilation), False,
                 [0, 0], groups, (True, False, False))[0]
         if ctx.needs_input_grad[1]:
-            if col is not None or _use_wgrad_gemm(x, weight, stride, padding, groups):
+            if _use_wgrad_gemm(x, weight, stride, padding, groups):
                 gw = conv_wgrad_gemm(x, g, weight.shape, stride, padding, col=col)
             else:
                 gw = conv_wgrad(x, g, weight.shape, stride, padding, groups)
@@ -1257,6 +1257,14 @@ def _use_wgrad_gemm(x, weight, stride, padding, groups=1):
     NP = x.shape[0] * oh * ow
     return (oh * ow <= 196 and Co >= 128 and C_ * R * S >= 1152 and NP * C_ * R * S < (1 << 31)
             and Co * NP < (1 << 31))
+
+
+def _use_fwd_gemm(x, weight, stride, padding, groups=1):
+    """The forward as the im2col GEMM on the weight-gradient GEMM's shapes.  Extending it to
+    layer2.0's stride-2 conv (MIOpen's deterministic forward 99 us standalone, the GEMM 40
+    + the 58 MB im2col pass) measured no gain in the loop (1639 -> 1617 it/s,
+    profiles/r2_wgrad_gemm.log), so it is not."""
+    return WGRAD_GEMM_FWD and _use_wgrad_gemm(x, weight, stride, padding, groups)
 
 
 def _use_k17(x, weight, stride, padding, groups=1):

@@ -813,7 +813,7 @@ def test_conv_wgrad_gemm_matches_fp64(K, cfg):
     err = (dw1.double().cpu() - ref).abs()
     assert bool((err <= 1e-5 * mag + 1e-30).all()), float((err / mag.clamp_min(1e-30)).max())
     wd = w.cuda().requires_grad_(True)
-    assert K._use_wgrad_gemm(xd, wd, st, pad)
+    assert K._use_wgrad_gemm(xd, wd, st, pad) and K._use_fwd_gemm(xd, wd, st, pad)
     out = K.conv2d(xd, wd, st, pad)
     # the forward runs as the GEMM too (K.WGRAD_GEMM_FWD): vs the fp64 conv
     yref = torch.nn.functional.conv2d(x.double(), w.double(), None, st, pad)

@@ -17,6 +17,8 @@ torch.backends.cudnn.benchmark = False
 dev = torch.device("cuda:0")
 SHAPES = {"layer3": (256, 256, 14, 1), "layer3.0_s2": (128, 256, 28, 2), "layer4": (512, 512, 7, 1),
           "layer4.0_s2": (256, 512, 14, 2)}
+if "--l12" in sys.argv:    # ResNet-18 layer1 / layer2 / layer2.0's stride-2 conv
+    SHAPES = {"layer1": (64, 64, 56, 1), "layer2": (128, 128, 28, 1), "layer2.0_s2": (64, 128, 56, 2)}
 out = {}
 for name, (ci, co, hw, st) in SHAPES.items():
     x = torch.randn(32, ci, hw, hw, device=dev)
