@@ -25,13 +25,15 @@
 namespace ssq {
 
 constexpr int kLossBlocks = 1024;   // lp_loss workgroup partials
-constexpr int kEpiParts = 6;        // doubles per (n, c) row of the epilogue backward
+constexpr int kEpiParts = 7;        // doubles per (n, c) row of the epilogue backward
+                                    // (slot 6: the fused tail's loss partial)
 
 struct FinTask {
-  int kind;                  // 0: lp_loss value, 1: epilogue backward sums
+  int kind;                  // 0: lp_loss value, 1: epilogue backward sums,
+                             // 2: loss value from the epilogue rows (fused tail)
   uint32_t nwg;              // workgroups the task takes
   const double* part;
-  uint32_t a, b, c;          // loss: nblk; epilogue: N, C, nb
+  uint32_t a, b, c;          // loss: nblk; epilogue: N, C, nb; rows loss: rows
   double m;                  // loss: M
   float* o[4];               // loss: o[0]; epilogue: ggamma, gphi, gdelta, gzp
 };
@@ -90,6 +92,17 @@ __device__ __forceinline__ void fin_epi(uint32_t bid, const double* __restrict__
   }
 }
 
+// fused tail (ssq_epilogue_loss_bwd): the per-row loss partials (slot 6 of each row's
+// kEpiParts doubles) summed in row order, one workgroup
+__device__ __forceinline__ void fin_loss_rows(const double* __restrict__ part, uint32_t rows,
+                                              double m, float* __restrict__ out) {
+  __shared__ double red[16];
+  double a = 0.0;
+  for (uint32_t r = threadIdx.x; r < rows; r += kBlock) a += part[(int64_t)r * kEpiParts + 6];
+  a = block_sum(a, red);
+  if (threadIdx.x == 0) out[0] = (float)(a / m);
+}
+
 // Workgroup k of the table's tasks (k < ft.nwg).
 __device__ __forceinline__ void run_fin(const FinTable& ft, uint32_t k) {
   for (int i = 0; i < ft.n; ++i) {
@@ -97,8 +110,10 @@ __device__ __forceinline__ void run_fin(const FinTable& ft, uint32_t k) {
     if (k < t.nwg) {
       if (t.kind == 0)
         fin_loss(t.part, (int)t.a, t.m, t.o[0]);
-      else
+      else if (t.kind == 1)
         fin_epi(k, t.part, t.a, t.b, t.c, t.o[0], t.o[1], t.o[2], t.o[3]);
+      else
+        fin_loss_rows(t.part, t.a, t.m, t.o[0]);
       return;
     }
     k -= t.nwg;

@@ -302,13 +302,17 @@ __global__ __launch_bounds__(kBlock) void adam_kernel(AdamTable tab, float w1, f
 //   and the act quantizer's four sums -> dL/ddelta, dL/dzp.
 // One wave per (n, c) row; the pre-activation values are recomputed from y with the
 // forward's fp32 operations (bit-identical masks), nothing of the forward is stored.
-template <bool RES, int ACT, bool QUANT, bool AFFINE, bool VEC>
+// LOSS (the fused tail, ssq_epilogue_loss_bwd): g is the cache of target rows instead of
+// dL/d(output); the output is recomputed (the forward's ops) and dL/d(output) is the p = 2
+// lp_loss gradient of K11 (lp_elem, identical ops), the loss partial goes to slot 6.
+template <bool RES, int ACT, bool QUANT, bool AFFINE, bool VEC, bool LOSS>
 __global__ __launch_bounds__(kBlock) void epilogue_bwd_rows(
     const float* __restrict__ g, const float* __restrict__ y, const float* __restrict__ bias,
     const float* __restrict__ gamma, const float* __restrict__ phi, const float* __restrict__ res,
     uint32_t rows, uint32_t C, uint32_t hw, const float* __restrict__ qdelta,
     const float* __restrict__ qzp, float lo, float hi, float* __restrict__ gy,
-    float* __restrict__ gres, double* __restrict__ part, FinTable fin, uint32_t nmain) {
+    float* __restrict__ gres, double* __restrict__ part, FinTable fin, uint32_t nmain,
+    const int64_t* __restrict__ lidx, float inv_m) {
   if (blockIdx.x >= nmain) {          // queued finalize tasks ride on this launch
     run_fin(fin, blockIdx.x - nmain);
     return;
@@ -320,18 +324,27 @@ __global__ __launch_bounds__(kBlock) void epilogue_bwd_rows(
   const float b = bias ? bias[c] : 0.0f;
   const float ga = AFFINE ? gamma[c] : 1.0f, ph = AFFINE ? phi[c] : 0.0f;
   const float d = QUANT ? qdelta[0] : 1.0f, z = QUANT ? qzp[0] : 0.0f;
-  double sg = 0, sp = 0, a0 = 0, a1 = 0, a2 = 0, a3 = 0;
-  auto one = [&](float yv, float gv, float rv, float& oy, float& orr) {
+  double sg = 0, sp = 0, a0 = 0, a1 = 0, a2 = 0, a3 = 0, la = 0;
+  auto one = [&](float yv, float gv_or_tgt, float rv, float& oy, float& orr) {
     const float pre = bias ? __fadd_rn(yv, b) : yv;
     float t = AFFINE ? __fadd_rn(__fmul_rn(pre, ga), ph) : pre;
     if (RES) t = __fadd_rn(t, rv);
     t = act_fwd<ACT>(t);
+    float tq = 0.0f, q = 0.0f;
+    bool m = true;
+    if (QUANT) {
+      tq = t / d;
+      const float v = __fadd_rn(rintf(tq), z);
+      m = (v >= lo) && (v <= hi);
+      q = clampf(v, lo, hi);
+    }
+    float gv = gv_or_tgt;
+    if (LOSS) {   // the forward's output (fq1's dequant), then the loss gradient wrt it
+      const float o = QUANT ? __fmul_rn(__fsub_rn(q, z), d) : t;
+      gv = lp_elem<0>(o, gv_or_tgt, 2.0f, inv_m, 1.0f, 0, la);
+    }
     float gt = gv;
     if (QUANT) {
-      const float tq = t / d;
-      const float v = __fadd_rn(rintf(tq), z);
-      const bool m = (v >= lo) && (v <= hi);
-      const float q = clampf(v, lo, hi);
       const float gq = __fmul_rn(gv, d);
       const float gi = m ? gq : 0.0f;
       gt = gi / d;
@@ -347,9 +360,11 @@ __global__ __launch_bounds__(kBlock) void epilogue_bwd_rows(
     sp += (double)gt;
   };
   const int64_t base = (int64_t)r * hw;
+  // LOSS: row (n, c)'s target is row c of cached sample idx[n] ([*, C, hw] cache)
+  const int64_t gbase = LOSS ? (lidx[r / C] * (int64_t)C + c) * hw : base;
   if (VEC) {
     const f32x4* Y = (const f32x4*)(y + base);
-    const f32x4* G = (const f32x4*)(g + base);
+    const f32x4* G = (const f32x4*)(g + gbase);
     const f32x4* R = RES ? (const f32x4*)(res + base) : nullptr;
     f32x4* GY = (f32x4*)(gy + base);
     f32x4* GR = gres ? (f32x4*)(gres + base) : nullptr;
@@ -368,7 +383,7 @@ __global__ __launch_bounds__(kBlock) void epilogue_bwd_rows(
   } else {
     for (uint32_t j = lane; j < hw; j += kWave) {
       float oy, orr;
-      one(y[base + j], g[base + j], RES ? res[base + j] : 0.0f, oy, orr);
+      one(y[base + j], g[gbase + j], RES ? res[base + j] : 0.0f, oy, orr);
       gy[base + j] = oy;
       if (gres) gres[base + j] = orr;
     }
@@ -381,6 +396,7 @@ __global__ __launch_bounds__(kBlock) void epilogue_bwd_rows(
     a2 = wave_sum(a2);
     a3 = wave_sum(a3);
   }
+  if (LOSS) la = wave_sum(la);
   if (lane == 0) {
     double* o = part + (int64_t)r * kEpiParts;
     o[0] = sg;
@@ -389,6 +405,7 @@ __global__ __launch_bounds__(kBlock) void epilogue_bwd_rows(
     o[3] = a1;
     o[4] = a2;
     o[5] = a3;
+    o[6] = la;
   }
 }
 
@@ -649,45 +666,50 @@ extern "C" size_t ssq_epilogue_bwd_workspace_size(int64_t rows) {
   return (size_t)rows * kEpiParts * sizeof(double);
 }
 
-extern "C" int ssq_epilogue_bwd(const float* g, const float* y, const float* bias,
-                                const float* gamma, const float* phi, const float* res,
-                                int64_t N, int64_t C, int64_t hw, int relu, const float* delta,
-                                const float* zp, int qmin, int qmax, float* gy, float* gres,
-                                float* ggamma, float* gphi, float* gdelta, float* gzp, void* ws,
-                                size_t ws_bytes, ssq_stream_t stream) {
-  SSQ_REQUIRE(g && y && gy && N >= 1 && C >= 1 && hw >= 1, SSQ_E_ARG,
-              "ssq_epilogue_bwd: bad args");
+// ssq_epilogue_bwd (g = dL/d(output)) and its fused-tail form ssq_epilogue_loss_bwd
+// (tgt = the cache of target rows, idx = this batch's rows: dL/d(output) of the p = 2
+// lp_loss computed in the pass, its value finalised into loss_out).
+static int epilogue_bwd(const char* what, const float* g, const float* y, const float* bias,
+                        const float* gamma, const float* phi, const float* res, int64_t N,
+                        int64_t C, int64_t hw, int relu, const float* delta, const float* zp,
+                        int qmin, int qmax, const int64_t* lidx, int64_t M, float* loss_out,
+                        float* gy, float* gres, float* ggamma, float* gphi, float* gdelta,
+                        float* gzp, void* ws, size_t ws_bytes, hipStream_t s) {
+  const bool loss = lidx != nullptr;
+  SSQ_REQUIRE(g && y && gy && N >= 1 && C >= 1 && hw >= 1, SSQ_E_ARG, "%s: bad args", what);
+  SSQ_REQUIRE(!loss || (loss_out && M >= 1), SSQ_E_ARG, "%s: loss_out and M required", what);
   SSQ_REQUIRE(!gamma == !phi && (!(ggamma || gphi) || gamma), SSQ_E_ARG,
-              "ssq_epilogue_bwd: gamma/phi gradients need gamma and phi");
-  SSQ_REQUIRE(!delta || (zp && qmin < qmax), SSQ_E_ARG, "ssq_epilogue_bwd: act quantizer");
-  SSQ_REQUIRE(!(gdelta || gzp) || delta, SSQ_E_ARG, "ssq_epilogue_bwd: delta/zp grads need delta");
+              "%s: gamma/phi gradients need gamma and phi", what);
+  SSQ_REQUIRE(!delta || (zp && qmin < qmax), SSQ_E_ARG, "%s: act quantizer", what);
+  SSQ_REQUIRE(!(gdelta || gzp) || delta, SSQ_E_ARG, "%s: delta/zp grads need delta", what);
   SSQ_REQUIRE(N * C * hw < (1ll << 31) && N * C < (1ll << 31), SSQ_E_ARG,
-              "ssq_epilogue_bwd: tensor exceeds 2^31 elements");
+              "%s: tensor exceeds 2^31 elements", what);
   const int64_t rows = N * C;
   SSQ_REQUIRE(ws && ws_bytes >= ssq_epilogue_bwd_workspace_size(rows), SSQ_E_WS,
-              "ssq_epilogue_bwd: workspace too small");
-  hipStream_t s = (hipStream_t)stream;
+              "%s: workspace too small", what);
   auto al = [](const void* q) { return ((uintptr_t)q & 15u) == 0; };
   const bool vec = hw % 4 == 0 && al(g) && al(y) && al(gy) && (!res || al(res)) &&
                    (!gres || al(gres));
+  SSQ_REQUIRE(!loss || vec, SSQ_E_ARG, "%s: the fused tail needs 16-B aligned rows", what);
+  SSQ_REQUIRE(relu >= 0 && relu <= 2, SSQ_E_ARG, "%s: activation code %d", what, relu);
   const uint32_t nmain = (uint32_t)((rows + kBlock / kWave - 1) / (kBlock / kWave));
   int frc = SSQ_OK;
   const FinTable fin = fin_take_for_host(s, ws, ws_bytes, &frc);
   if (frc) return frc;
   const dim3 grid(nmain + fin.nwg);
   const float lo = (float)qmin, hi = (float)qmax;
+  const float inv_m = loss ? 1.0f / (float)M : 0.0f;   // mean backward, as lp_loss
   double* part = (double*)ws;
-#define SSQ_EB(R, A, Q, F, V)                                                                  \
-  hipLaunchKernelGGL((epilogue_bwd_rows<R, A, Q, F, V>), grid, dim3(kBlock), 0, s, g, y, bias, \
-                     gamma, phi, res, (uint32_t)rows, (uint32_t)C, (uint32_t)hw, delta, zp, lo, \
-                     hi, gy, gres, part, fin, nmain)
+#define SSQ_EB(R, A, Q, F, V, L)                                                                  \
+  hipLaunchKernelGGL((epilogue_bwd_rows<R, A, Q, F, V, L>), grid, dim3(kBlock), 0, s, g, y, bias, \
+                     gamma, phi, res, (uint32_t)rows, (uint32_t)C, (uint32_t)hw, delta, zp, lo,    \
+                     hi, gy, gres, part, fin, nmain, lidx, inv_m)
 #define SSQ_EB1(R, A, Q, F) \
-  if (vec) SSQ_EB(R, A, Q, F, true); else SSQ_EB(R, A, Q, F, false);
+  if (loss) SSQ_EB(R, A, Q, F, true, true); else if (vec) SSQ_EB(R, A, Q, F, true, false); else SSQ_EB(R, A, Q, F, false, false);
 #define SSQ_EB2(R, A, Q) \
   if (gamma) { SSQ_EB1(R, A, Q, true) } else { SSQ_EB1(R, A, Q, false) }
 #define SSQ_EB3(R, A) \
   if (delta) { SSQ_EB2(R, A, true) } else { SSQ_EB2(R, A, false) }
-  SSQ_REQUIRE(relu >= 0 && relu <= 2, SSQ_E_ARG, "ssq_epilogue_bwd: activation code %d", relu);
   if (res) {
     if (relu == 2) { SSQ_EB3(true, 2) } else if (relu) { SSQ_EB3(true, 1) } else { SSQ_EB3(true, 0) }
   } else {
@@ -697,6 +719,28 @@ extern "C" int ssq_epilogue_bwd(const float* g, const float* y, const float* bia
 #undef SSQ_EB2
 #undef SSQ_EB1
 #undef SSQ_EB
+  int rc = check_launch(what);
+  if (rc) return rc;
+  if (loss) {
+    FinTask t{};
+    t.kind = 2;
+    t.nwg = 1;
+    t.part = part;
+    t.a = (uint32_t)rows;
+    t.m = (double)M;
+    t.o[0] = loss_out;
+    if (fin_defer_on()) {
+      rc = fin_push(s, t);
+    } else {
+      FinTable one;
+      one.t[0] = t;
+      one.n = 1;
+      one.nwg = 1;
+      hipLaunchKernelGGL(fin_tasks_kernel, dim3(1), dim3(kBlock), 0, s, one);
+      rc = check_launch(what);
+    }
+    if (rc) return rc;
+  }
   if (ggamma || gphi || gdelta || gzp) {
     // blocks [0, nb) only when gamma / phi are wanted; block nb (the act quantizer's four
     // sums over every row, one workgroup) only when delta / zp are
@@ -714,14 +758,38 @@ extern "C" int ssq_epilogue_bwd(const float* g, const float* y, const float* bia
       t.o[1] = gphi;
       t.o[2] = gdelta;
       t.o[3] = gzp;
-      const int rc = check_launch("ssq_epilogue_bwd");
-      return rc ? rc : fin_push(s, t);
+      return fin_push(s, t);
     }
     hipLaunchKernelGGL(epilogue_bwd_finalize, dim3(nb + nq), dim3(kBlock), 0, s,
                        (const double*)part, (uint32_t)N, (uint32_t)C, nb, ggamma, gphi, gdelta,
                        gzp);
   }
-  return check_launch("ssq_epilogue_bwd");
+  return check_launch(what);
+}
+
+extern "C" int ssq_epilogue_bwd(const float* g, const float* y, const float* bias,
+                                const float* gamma, const float* phi, const float* res,
+                                int64_t N, int64_t C, int64_t hw, int relu, const float* delta,
+                                const float* zp, int qmin, int qmax, float* gy, float* gres,
+                                float* ggamma, float* gphi, float* gdelta, float* gzp, void* ws,
+                                size_t ws_bytes, ssq_stream_t stream) {
+  return epilogue_bwd("ssq_epilogue_bwd", g, y, bias, gamma, phi, res, N, C, hw, relu, delta, zp,
+                      qmin, qmax, nullptr, 0, nullptr, gy, gres, ggamma, gphi, gdelta, gzp, ws,
+                      ws_bytes, (hipStream_t)stream);
+}
+
+extern "C" int ssq_epilogue_loss_bwd(const float* tgt_cache, const int64_t* idx, int64_t M,
+                                     float* loss_out, const float* y, const float* bias,
+                                     const float* gamma, const float* phi, const float* res,
+                                     int64_t N, int64_t C, int64_t hw, int relu,
+                                     const float* delta, const float* zp, int qmin, int qmax,
+                                     float* gy, float* gres, float* ggamma, float* gphi,
+                                     float* gdelta, float* gzp, void* ws, size_t ws_bytes,
+                                     ssq_stream_t stream) {
+  SSQ_REQUIRE(idx, SSQ_E_ARG, "ssq_epilogue_loss_bwd: idx is required");
+  return epilogue_bwd("ssq_epilogue_loss_bwd", tgt_cache, y, bias, gamma, phi, res, N, C, hw,
+                      relu, delta, zp, qmin, qmax, idx, M, loss_out, gy, gres, ggamma, gphi,
+                      gdelta, gzp, ws, ws_bytes, (hipStream_t)stream);
 }
 
 template <int ACT>

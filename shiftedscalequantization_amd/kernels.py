@@ -914,12 +914,64 @@ class deferred_finalize:
                 set_deferred_finalize(self.prev)
 
 
-def epilogue(y, bias, gamma, phi, res, relu, q=None):
-    """EpilogueFn with q an (initialised, per-tensor) act quantizer or None."""
+# Set by the fused recon loop around its block forward: the block's final epilogue is not
+# run; its output is returned as a placeholder carrying the epilogue's inputs (_ssq_tail),
+# and the loop runs forward + loss + backward of that epilogue in one pass
+# (epilogue_loss_bwd).  Only consumed by BaseQuantBlock._tail.
+TAIL_LAZY = [False]
+
+
+def epilogue(y, bias, gamma, phi, res, relu, q=None, lazy=False):
+    """EpilogueFn with q an (initialised, per-tensor) act quantizer or None.  lazy: see
+    TAIL_LAZY (the placeholder must only reach epilogue_loss_bwd)."""
+    # the fused tail needs 16-B aligned rows (hw % 4 == 0): other shapes run eagerly
+    if lazy and y.dim() == 4 and (y.shape[2] * y.shape[3]) % 4 == 0 and y.is_contiguous() \
+            and y.data_ptr() % 16 == 0 and (res is None or (res.is_contiguous() and res.data_ptr() % 16 == 0)):
+        out = torch.empty_like(y)
+        out._ssq_tail = (y, bias, gamma, phi, res, int(relu), q)
+        return out
     if q is None:
         return EpilogueFn.apply(y, bias, gamma, phi, res, None, None, int(relu), 8, False)
     return EpilogueFn.apply(y, bias, gamma, phi, res, q.delta, q.zero_point, int(relu), q.n_bits,
                             q.sym)
+
+
+def epilogue_loss_bwd(tail, tgt, M):
+    """The fused tail (ssq_epilogue_loss_bwd): for a lazy epilogue placeholder's inputs and a
+    Rows target, the p = 2 lp_loss value (1-element device tensor, mean over M) and the
+    gradients the epilogue's backward returns -- (loss, gy, gres, ggamma, gphi, gdelta, gzp),
+    None where the input needs none -- bit-identical to epilogue -> lp_loss_and_grad ->
+    backward."""
+    y, bias, gamma, phi, res, relu, q = tail
+    if not isinstance(tgt, Rows):
+        raise A.SSQError("epilogue_loss_bwd: the target must be a Rows view of the cache")
+    y, yp, bp, rp, C_, hw, _ = _epilogue_layout(y, bias, res)
+    dev_ = y.device
+    cache, cp = fptr(tgt.cache.detach(), "tgt cache")
+    idx = tgt.idx
+    N = y.shape[0]
+    if idx.dtype != torch.int64 or idx.numel() != N or tuple(cache.shape[1:]) != tuple(y.shape[1:]):
+        raise A.SSQError("epilogue_loss_bwd: Rows target does not match the output")
+    flat = (lambda t: None if t is None else t.detach().reshape(-1).contiguous())
+    gm, ph = flat(gamma), flat(phi)
+    if q is not None:
+        d, z = flat(q.delta), flat(q.zero_point)
+        lo, hi = qrange(q.n_bits, q.sym)
+    else:
+        d = z = None
+        lo, hi = 0, 1
+    loss = torch.empty(1, dtype=torch.float32, device=dev_)
+    gy = torch.empty_like(y)
+    gres = torch.empty_like(y) if (res is not None and res.requires_grad) else None
+    ggm = torch.empty(C_, device=dev_) if (gamma is not None and gamma.requires_grad) else None
+    gph = torch.empty(C_, device=dev_) if (phi is not None and phi.requires_grad) else None
+    gd = torch.empty(1, device=dev_) if (q is not None and q.delta.requires_grad) else None
+    gz = torch.empty(1, device=dev_) if (q is not None and q.zero_point.requires_grad) else None
+    ws, wsn = workspace(query("ssq_epilogue_bwd_workspace_size", N * C_), dev_, _epi_slot())
+    call("ssq_epilogue_loss_bwd", cp, _vp(idx), int(M), _vp(loss), yp, bp, _vp(gm), _vp(ph), rp,
+         N, C_, hw, int(relu), _vp(d), _vp(z), lo, hi, _vp(gy), _vp(gres), _vp(ggm), _vp(gph),
+         _vp(gd), _vp(gz), ws, wsn, stream_of(y))
+    return loss, gy, gres, ggm, gph, gd, gz
 
 
 def adam_step(params, grads, exp_avgs, exp_avg_sqs, beta1, beta2, eps, hyper=None,

@@ -26,6 +26,36 @@ from .quant_layer import QuantModule
 
 # A/B knob: deferred loss / epilogue finalizes inside the loop body (bit-identical either way)
 DEFER_FINALIZE = True
+# A/B knob: the block's final epilogue + loss + its backward as one pass (bit-identical)
+FUSE_TAIL = True
+
+
+def backward_tail(tail, grads):
+    """Resume autograd at a fused tail's inputs: the conv output y and the residual through
+    their graphs; gamma^z / phi^z / the act quantizer's delta and zero point are leaves here
+    (or views of leaves), accumulated as autograd would."""
+    y, bias, gamma, phi, res, relu, q = tail
+    _, gy, gres, ggm, gph, gd, gz = grads
+    roots, grs = [y], [gy]
+    if gres is not None:
+        roots.append(res)
+        grs.append(gres)
+    leaves = [(gamma, ggm), (phi, gph)]
+    if q is not None:
+        leaves += [(q.delta, gd), (q.zero_point, gz)]
+    for t, g in leaves:
+        if g is None:
+            continue
+        g = g.view(t.shape)
+        if t.is_leaf:
+            if t.grad is None:
+                t.grad = g
+            else:
+                t.grad.add_(g)
+        else:
+            roots.append(t)
+            grs.append(g)
+    torch.autograd.backward(roots, grs)
 
 
 def print_ratio(quantizers):
@@ -101,6 +131,9 @@ def _fused_loop(block, modules, iters, lmda, model, p, lr, bias_cal, batch_size,
     # they must be final when backward returns them
     defer = DEFER_FINALIZE and on_gpu and bucket is None
 
+    # the fused tail (K.epilogue_loss_bwd) needs the p = 2 loss (the reference's default)
+    fuse_tail = FUSE_TAIL and on_gpu and float(p) == 2.0
+
     def body_pre():
         """One iteration on the device up to its exchange step: gather -> forward -> fused
         loss+grad -> backward.  No host sync, no host-side state: graph-capturable."""
@@ -111,10 +144,20 @@ def _fused_loop(block, modules, iters, lmda, model, p, lr, bias_cal, batch_size,
         cur_inp, cur_out = feeder.gather_lazy()
         if on_gpu:
             stash_block_weights(quantizers)     # every conv's What in one launch
-        quant_out = block(cur_inp)
+        K.TAIL_LAZY[0] = fuse_tail
+        try:
+            quant_out = block(cur_inp)
+        finally:
+            K.TAIL_LAZY[0] = False
         clear_stash(quantizers)
+        tail = getattr(quant_out, '_ssq_tail', None)
         relu_in = getattr(quant_out, '_ssq_relu_inputs', None)
-        if relu_in:
+        if tail is not None:
+            # the block's final epilogue, the loss and the epilogue's backward in one pass;
+            # autograd resumes at the epilogue's inputs
+            rec, grads = loss_func.fused_tail(tail, quant_out, cur_out)
+            backward_tail(tail, grads)
+        elif relu_in:
             # the block ends in the fused epilogue's ReLU: the loss pass writes the gradient
             # at the ReLU's input and backward starts from the epilogue's inputs
             rec, g_pre = loss_func.loss_and_grad(quant_out, cur_out, relu_mask=True)
@@ -331,6 +374,12 @@ class FusedScaleLossFunction:
     def disarm(self):
         for qt in self.quantizer:
             qt._fused_reg = None
+
+    def fused_tail(self, tail, pred, tgt):
+        """loss_and_grad + the final epilogue's backward in one pass (K.epilogue_loss_bwd);
+        returns (rec_loss, the epilogue's input gradients)."""
+        grads = K.epilogue_loss_bwd(tail, tgt, K._lp_M(pred, "none"))
+        return grads[0][0], grads
 
     def loss_and_grad(self, pred, tgt, relu_mask=False):
         """One ssq_lp_loss pass: the loss value AND d loss / d pred (device only) -- or,

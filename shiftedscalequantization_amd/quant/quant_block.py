@@ -87,7 +87,8 @@ class BaseQuantBlock(nn.Module):
             q = fusable_act_quantizer(self.act_quantizer, self.use_act_quant)
             gamma, phi = last.affine()
             if gamma is not None:   # last's gamma^z/phi^z, residual, act (+ act quant)
-                out = K.epilogue(raw, bias, gamma, phi, residual, relu, q)
+                lazy = K.TAIL_LAZY[0] and (q is not None or not self.use_act_quant)
+                out = K.epilogue(raw, bias, gamma, phi, residual, relu, q, lazy=lazy)
                 if q is None and self.use_act_quant:
                     out = self.act_quantizer(out)
                 return out

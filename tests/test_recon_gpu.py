@@ -481,3 +481,49 @@ def test_deferred_finalize_bit_identical(Q, golden, graph):
         np.testing.assert_array_equal(runs[1][k], runs[0][k], err_msg=k)
     # gamma^z / phi^z really were learned (their finalizes ran)
     assert any(np.any(runs[1][n + "_gamma"] != 1.0) for n in ("conv1", "conv2", "downsample"))
+
+
+@pytest.mark.parametrize("graph", [False, True])
+def test_fused_tail_matches_unfused(Q, golden, graph):
+    """The block's final epilogue + the p = 2 loss + the epilogue backward as one pass
+    (K.epilogue_loss_bwd, the loop's FUSE_TAIL) against the three separate launches: every
+    learned parameter (alpha, gamma^z, phi^z) bit-identical after the loop, per-iteration
+    losses equal to the last float ulps (row-wise vs block-wise loss partials)."""
+    import importlib
+    LRF = importlib.import_module("shiftedscalequantization_amd.quant.layer_recon_fused_shiftedScale")
+    g = golden("recon_fused")
+    runs = []
+    for fuse in (False, True):
+        qnn = build_qnn(Q, {})
+        block = qnn.model[3]
+        load_block(Q, g, block)
+        block.cached_inp_features = [dev(g["cached_inp"])]
+        block.cached_out_features = [dev(g["cached_out"])]
+        seen = []
+        orig_keep = LRF.FusedScaleLossFunction.bookkeep
+
+        def bookkeep(self, rec):
+            seen.append(float(rec.item()))
+            return orig_keep(self, rec)
+
+        LRF.FusedScaleLossFunction.bookkeep, prev = bookkeep, LRF.FUSE_TAIL
+        LRF.FUSE_TAIL = fuse
+        try:
+            torch.manual_seed(1005)
+            res = LRF.block_recon_fused_shiftedScale(block, 12, (0.01, 0.1), qnn, None, verbose=False,
+                                                     graph=graph, bias_cal=True)
+        finally:
+            LRF.FusedScaleLossFunction.bookkeep, LRF.FUSE_TAIL = orig_keep, prev
+        out = {"rec": np.array(seen), "final": np.array(res)}
+        for n in ("conv1", "conv2", "downsample"):
+            m = getattr(block, n)
+            out[n + "_alpha"] = m.weight_quantizer.alpha.detach().cpu().numpy()
+            out[n + "_gamma"] = m.alpha_out.detach().cpu().numpy()
+            out[n + "_phi"] = m.beta_out.detach().cpu().numpy()
+        runs.append(out)
+    for k in runs[0]:
+        if k in ("rec", "final"):
+            np.testing.assert_allclose(runs[1][k], runs[0][k], rtol=1e-6, err_msg=k)
+        else:
+            np.testing.assert_array_equal(runs[1][k], runs[0][k], err_msg=k)
+    assert any(np.any(runs[1][n + "_gamma"] != 1.0) for n in ("conv1", "conv2", "downsample"))
