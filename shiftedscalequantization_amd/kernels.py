@@ -1298,7 +1298,7 @@ def _out_plane(x, weight, stride, padding):
 
 
 def _use_wgrad_gemm(x, weight, stride, padding, groups=1):
-    if WGRAD_GEMM != "auto" or groups != 1 or weight.shape[2] * weight.shape[3] == 1:
+    if WGRAD_GEMM != "auto" or groups != 1:
         return False
     if isinstance(stride, (tuple, list)) and len(set(stride)) != 1:
         return False
@@ -1307,8 +1307,13 @@ def _use_wgrad_gemm(x, weight, stride, padding, groups=1):
     oh, ow = _out_plane(x, weight, stride, padding)
     Co, C_, R, S = (int(v) for v in weight.shape)
     NP = x.shape[0] * oh * ow
-    return (oh * ow <= 196 and Co >= 128 and C_ * R * S >= 1152 and NP * C_ * R * S < (1 << 31)
-            and Co * NP < (1 << 31))
+    if NP * C_ * R * S >= (1 << 31) or Co * NP >= (1 << 31) or oh * ow > 196:
+        return False
+    if R * S == 1:
+        # 1x1 (the ResNet downsamples): layer3.0 / layer4.0 33 / 23 us vs K17's 1x1 kernel
+        # 44 / 44; layer2.0's (28x28 plane) stays on K17 (84 vs 42; tools/ds_gemm_probe.py)
+        return Co >= 256
+    return Co >= 128 and C_ * R * S >= 1152
 
 
 def _use_fwd_gemm(x, weight, stride, padding, groups=1):
@@ -1316,7 +1321,8 @@ def _use_fwd_gemm(x, weight, stride, padding, groups=1):
     layer2.0's stride-2 conv (MIOpen's deterministic forward 99 us standalone, the GEMM 40
     + the 58 MB im2col pass) measured no gain in the loop (1639 -> 1617 it/s,
     profiles/r2_wgrad_gemm.log), so it is not."""
-    return WGRAD_GEMM_FWD and _use_wgrad_gemm(x, weight, stride, padding, groups)
+    return (WGRAD_GEMM_FWD and weight.shape[2] * weight.shape[3] > 1
+            and _use_wgrad_gemm(x, weight, stride, padding, groups))
 
 
 def _use_k17(x, weight, stride, padding, groups=1):

@@ -780,7 +780,9 @@ def test_conv_wgrad_matches_fp64(K, cfg, wgrad_form):
     # (Nb, C, H, Co, k, stride, pad): ResNet-18 layer3 / layer3.0 s2 / layer4 / layer4.0 s2
     # at batch 32 (the shapes the GEMM policy takes), a 5x5 and ragged sizes
     (32, 256, 14, 256, 3, 1, 1), (32, 128, 28, 256, 3, 2, 1), (32, 512, 7, 512, 3, 1, 1),
-    (32, 256, 14, 512, 3, 2, 1), (3, 130, 9, 140, 3, 1, 1), (2, 64, 11, 128, 5, 2, 2)])
+    (32, 256, 14, 512, 3, 2, 1), (3, 130, 9, 140, 3, 1, 1), (2, 64, 11, 128, 5, 2, 2),
+    # 1x1 stride-2 downsamples of layer3.0 / layer4.0 (weight gradient only)
+    (32, 128, 28, 256, 1, 2, 0), (32, 256, 14, 512, 1, 2, 0)])
 def test_conv_wgrad_gemm_matches_fp64(K, cfg):
     """The im2col + library-GEMM weight gradient (ssq_wgrad_gemm_operands + hipBLASLt) vs
     the fp64 CPU gradient within the fp32 accumulation bound; its operands equal a host
@@ -813,7 +815,7 @@ def test_conv_wgrad_gemm_matches_fp64(K, cfg):
     err = (dw1.double().cpu() - ref).abs()
     assert bool((err <= 1e-5 * mag + 1e-30).all()), float((err / mag.clamp_min(1e-30)).max())
     wd = w.cuda().requires_grad_(True)
-    assert K._use_wgrad_gemm(xd, wd, st, pad) and K._use_fwd_gemm(xd, wd, st, pad)
+    assert K._use_wgrad_gemm(xd, wd, st, pad) and K._use_fwd_gemm(xd, wd, st, pad) == (k > 1)
     out = K.conv2d(xd, wd, st, pad)
     # the forward runs as the GEMM too (K.WGRAD_GEMM_FWD): vs the fp64 conv
     yref = torch.nn.functional.conv2d(x.double(), w.double(), None, st, pad)
