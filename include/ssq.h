@@ -334,8 +334,7 @@ int ssq_epilogue_bwd(const float* g, const float* y, const float* bias, const fl
  * output is recomputed from y with the forward's ops and never stored; dL/d(output) is
  * ssq_lp_loss_rows's gradient (mean over M) bit for bit; the loss value Sum|out - tgt|^2 / M
  * (row partials summed in row order) goes to loss_out.  tgt_cache is [*, C, hw], idx holds
- * the N cached rows of this batch.  Outputs and workspace as ssq_epilogue_bwd; 16-B
- * aligned rows (hw % 4 == 0) required. */
+ * the N cached rows of this batch.  Outputs and workspace as ssq_epilogue_bwd. */
 int ssq_epilogue_loss_bwd(const float* tgt_cache, const int64_t* idx, int64_t M, float* loss_out,
                           const float* y, const float* bias, const float* gamma, const float* phi,
                           const float* res, int64_t N, int64_t C, int64_t hw, int relu,

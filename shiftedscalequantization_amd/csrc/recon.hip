@@ -690,7 +690,6 @@ static int epilogue_bwd(const char* what, const float* g, const float* y, const 
   auto al = [](const void* q) { return ((uintptr_t)q & 15u) == 0; };
   const bool vec = hw % 4 == 0 && al(g) && al(y) && al(gy) && (!res || al(res)) &&
                    (!gres || al(gres));
-  SSQ_REQUIRE(!loss || vec, SSQ_E_ARG, "%s: the fused tail needs 16-B aligned rows", what);
   SSQ_REQUIRE(relu >= 0 && relu <= 2, SSQ_E_ARG, "%s: activation code %d", what, relu);
   const uint32_t nmain = (uint32_t)((rows + kBlock / kWave - 1) / (kBlock / kWave));
   int frc = SSQ_OK;
@@ -705,7 +704,8 @@ static int epilogue_bwd(const char* what, const float* g, const float* y, const 
                      gamma, phi, res, (uint32_t)rows, (uint32_t)C, (uint32_t)hw, delta, zp, lo,    \
                      hi, gy, gres, part, fin, nmain, lidx, inv_m)
 #define SSQ_EB1(R, A, Q, F) \
-  if (loss) SSQ_EB(R, A, Q, F, true, true); else if (vec) SSQ_EB(R, A, Q, F, true, false); else SSQ_EB(R, A, Q, F, false, false);
+  if (loss) { if (vec) SSQ_EB(R, A, Q, F, true, true); else SSQ_EB(R, A, Q, F, false, true); } \
+  else if (vec) SSQ_EB(R, A, Q, F, true, false); else SSQ_EB(R, A, Q, F, false, false);
 #define SSQ_EB2(R, A, Q) \
   if (gamma) { SSQ_EB1(R, A, Q, true) } else { SSQ_EB1(R, A, Q, false) }
 #define SSQ_EB3(R, A) \

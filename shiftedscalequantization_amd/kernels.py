@@ -924,7 +924,9 @@ TAIL_LAZY = [False]
 def epilogue(y, bias, gamma, phi, res, relu, q=None, lazy=False):
     """EpilogueFn with q an (initialised, per-tensor) act quantizer or None.  lazy: see
     TAIL_LAZY (the placeholder must only reach epilogue_loss_bwd)."""
-    # the fused tail needs 16-B aligned rows (hw % 4 == 0): other shapes run eagerly
+    # the fused tail on float4 rows (hw % 4 == 0); the kernel's scalar-row form is tested but
+    # measured no faster than the three passes on 7x7 planes (profiles/r2_wgrad_gemm.log),
+    # so those run eagerly
     if lazy and y.dim() == 4 and (y.shape[2] * y.shape[3]) % 4 == 0 and y.is_contiguous() \
             and y.data_ptr() % 16 == 0 and (res is None or (res.is_contiguous() and res.data_ptr() % 16 == 0)):
         out = torch.empty_like(y)

@@ -1084,3 +1084,45 @@ def test_hard_weights_from_reference_alpha_bit_exact(K, golden, fixture):
         y2, codes = K.adashift_codes(dev(alpha), dev(beta), dev(w), d4, z4, SHIFTS, 2, False)
         c = codes.cpu().numpy().astype(np.float32)
         np.testing.assert_array_equal((c - z.reshape(-1, 1, 1, 1)) * d.reshape(-1, 1, 1, 1), what)
+
+
+@pytest.mark.parametrize("hw", [7, 8])
+@pytest.mark.parametrize("quant", [False, True])
+def test_epilogue_loss_bwd_matches_separate_passes(K, hw, quant):
+    """ssq_epilogue_loss_bwd (the fused tail) vs the three passes it replaces -- epilogue
+    forward, lp_loss_rows (p = 2) against the cached target rows, epilogue backward -- on
+    float4 rows (8x8) and scalar rows (7x7), with gamma^z/phi^z, a residual, ReLU and
+    optionally the per-tensor act quantizer: every gradient bit-identical, the loss value to
+    the last ulps (row vs block partials)."""
+    from shiftedscalequantization_amd.quant.quant_layer import UniformAffineQuantizer
+    gen = torch.Generator().manual_seed(hw * 2 + int(quant))
+    N, C = 6, 20
+    y = torch.randn(N, C, hw, hw, generator=gen).cuda()
+    res = torch.randn(N, C, hw, hw, generator=gen).cuda().requires_grad_(True)
+    bias = torch.randn(C, generator=gen).cuda()
+    gamma = (1 + 0.1 * torch.randn(1, C, 1, 1, generator=gen)).cuda().requires_grad_(True)
+    phi = (0.1 * torch.randn(1, C, 1, 1, generator=gen)).cuda().requires_grad_(True)
+    cache = torch.randn(15, C, hw, hw, generator=gen).relu().cuda()
+    idx = torch.tensor([3, 14, 0, 7, 7, 9], dtype=torch.int64).cuda()
+    q = None
+    if quant:
+        q = UniformAffineQuantizer(n_bits=4, channel_wise=False, scale_method="max", leaf_param=True).cuda()
+        q.delta = torch.nn.Parameter(torch.tensor(0.21).cuda())
+        q.zero_point = torch.nn.Parameter(torch.tensor(0.0).cuda())
+        q.inited = True
+    # separate passes
+    yr = y.clone().requires_grad_(True)
+    out = K.epilogue(yr, bias, gamma, phi, res, 1, q)
+    loss1, g1 = K.lp_loss_and_grad(out, K.Rows(cache, idx), 2.0)
+    out.backward(g1)
+    sep = [yr.grad, res.grad, gamma.grad, phi.grad] + ([q.delta.grad, q.zero_point.grad] if quant else [])
+    sep = [host(t).copy() for t in sep]
+    for t in [res, gamma, phi] + ([q.delta, q.zero_point] if quant else []):
+        t.grad = None
+    # fused
+    tail = K.epilogue(y, bias, gamma, phi, res, 1, q, lazy=True)._ssq_tail
+    loss2, gy, gres, ggm, gph, gd, gz = K.epilogue_loss_bwd(tail, K.Rows(cache, idx), N * hw * hw)
+    fused = [gy, gres, ggm, gph] + ([gd, gz] if quant else [])
+    for a, b in zip(sep, fused):
+        np.testing.assert_array_equal(a.reshape(-1).view(np.int32), host(b).reshape(-1).view(np.int32))
+    close(host(loss2), host(loss1), rtol=1e-6, atol=0)
