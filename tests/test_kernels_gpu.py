@@ -1120,7 +1120,10 @@ def test_epilogue_loss_bwd_matches_separate_passes(K, hw, quant):
     for t in [res, gamma, phi] + ([q.delta, q.zero_point] if quant else []):
         t.grad = None
     # fused
-    tail = K.epilogue(y, bias, gamma, phi, res, 1, q, lazy=True)._ssq_tail
+    # the lazy placeholder carries exactly these inputs (taken on float4 rows only)
+    lazy = K.epilogue(y, bias, gamma, phi, res, 1, q, lazy=True)
+    assert hasattr(lazy, "_ssq_tail") == (hw * hw % 4 == 0)
+    tail = (y, bias, gamma, phi, res, 1, q)
     loss2, gy, gres, ggm, gph, gd, gz = K.epilogue_loss_bwd(tail, K.Rows(cache, idx), N * hw * hw)
     fused = [gy, gres, ggm, gph] + ([gd, gz] if quant else [])
     for a, b in zip(sep, fused):
