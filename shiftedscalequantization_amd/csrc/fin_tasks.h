@@ -61,25 +61,38 @@ __device__ __forceinline__ void fin_loss(const double* __restrict__ part, int nb
   if (threadIdx.x == 0) out[0] = (float)(a / m);
 }
 
-// epilogue backward: workgroups [0, nb) the per-channel gamma / phi gradients (sum over n
-// in order); workgroup nb (when launched) the act quantizer's delta / zp gradients (rows
-// in a fixed order, as fq_bwd_finalize)
+// epilogue backward: workgroups [0, nb) the per-channel gamma / phi gradients, kEpiChan
+// channels per workgroup, the samples n split over its 4 waves (wave w sums n = w, w + 4,
+// ... in order, then the 4 wave sums are added in wave order: every load of a channel in
+// flight at once); workgroup nb (when launched) the act quantizer's delta / zp gradients
+// (rows in a fixed order, as fq_bwd_finalize)
+constexpr uint32_t kEpiChan = kBlock / 4;
 __device__ __forceinline__ void fin_epi(uint32_t bid, const double* __restrict__ part, uint32_t N,
                                         uint32_t C, uint32_t nb, float* __restrict__ ggamma,
                                         float* __restrict__ gphi, float* __restrict__ gdelta,
                                         float* __restrict__ gzp) {
   __shared__ double red[16];
   if (bid < nb) {
-    const uint32_t c = bid * kBlock + threadIdx.x;
-    if (c >= C) return;
+    __shared__ double wsum[4][kEpiChan][2];
+    const uint32_t cl = threadIdx.x % kEpiChan, w = threadIdx.x / kEpiChan;
+    const uint32_t c = bid * kEpiChan + cl;
     double sg = 0, sp = 0;
+    if (c < C) {
 #pragma unroll 8
-    for (uint32_t n = 0; n < N; ++n) {
-      sg += part[((int64_t)n * C + c) * kEpiParts + 0];
-      sp += part[((int64_t)n * C + c) * kEpiParts + 1];
+      for (uint32_t n = w; n < N; n += 4) {
+        sg += part[((int64_t)n * C + c) * kEpiParts + 0];
+        sp += part[((int64_t)n * C + c) * kEpiParts + 1];
+      }
     }
-    if (ggamma) ggamma[c] = (float)sg;
-    if (gphi) gphi[c] = (float)sp;
+    wsum[w][cl][0] = sg;
+    wsum[w][cl][1] = sp;
+    __syncthreads();
+    if (w == 0 && c < C) {
+      sg = wsum[0][cl][0] + wsum[1][cl][0] + wsum[2][cl][0] + wsum[3][cl][0];
+      sp = wsum[0][cl][1] + wsum[1][cl][1] + wsum[2][cl][1] + wsum[3][cl][1];
+      if (ggamma) ggamma[c] = (float)sg;
+      if (gphi) gphi[c] = (float)sp;
+    }
     return;
   }
   double a[4] = {0, 0, 0, 0};

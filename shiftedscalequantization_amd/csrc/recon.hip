@@ -744,7 +744,7 @@ static int epilogue_bwd(const char* what, const float* g, const float* y, const 
   if (ggamma || gphi || gdelta || gzp) {
     // blocks [0, nb) only when gamma / phi are wanted; block nb (the act quantizer's four
     // sums over every row, one workgroup) only when delta / zp are
-    const unsigned nb = (ggamma || gphi) ? (unsigned)((C + kBlock - 1) / kBlock) : 0u;
+    const unsigned nb = (ggamma || gphi) ? (unsigned)((C + kEpiChan - 1) / kEpiChan) : 0u;
     const unsigned nq = (gdelta || gzp) ? 1u : 0u;
     if (fin_defer_on()) {
       FinTask t{};
