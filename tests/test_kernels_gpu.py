@@ -1088,14 +1088,15 @@ def test_hard_weights_from_reference_alpha_bit_exact(K, golden, fixture):
 
 @pytest.mark.parametrize("hw", [7, 8])
 @pytest.mark.parametrize("quant", [False, True])
-def test_epilogue_loss_bwd_matches_separate_passes(K, hw, quant):
+@pytest.mark.parametrize("relu", [0, 1])
+def test_epilogue_loss_bwd_matches_separate_passes(K, hw, quant, relu):
     """ssq_epilogue_loss_bwd (the fused tail) vs the three passes it replaces -- epilogue
     forward, lp_loss_rows (p = 2) against the cached target rows, epilogue backward -- on
-    float4 rows (8x8) and scalar rows (7x7), with gamma^z/phi^z, a residual, ReLU and
-    optionally the per-tensor act quantizer: every gradient bit-identical, the loss value to
-    the last ulps (row vs block partials)."""
+    float4 rows (8x8) and scalar rows (7x7), with gamma^z/phi^z, a residual, ReLU or
+    identity (InvertedResidual tails) and optionally the per-tensor act quantizer: every
+    gradient bit-identical, the loss value to the last ulps (row vs block partials)."""
     from shiftedscalequantization_amd.quant.quant_layer import UniformAffineQuantizer
-    gen = torch.Generator().manual_seed(hw * 2 + int(quant))
+    gen = torch.Generator().manual_seed(hw * 4 + int(quant) * 2 + relu)
     N, C = 6, 20
     y = torch.randn(N, C, hw, hw, generator=gen).cuda()
     res = torch.randn(N, C, hw, hw, generator=gen).cuda().requires_grad_(True)
@@ -1112,7 +1113,7 @@ def test_epilogue_loss_bwd_matches_separate_passes(K, hw, quant):
         q.inited = True
     # separate passes
     yr = y.clone().requires_grad_(True)
-    out = K.epilogue(yr, bias, gamma, phi, res, 1, q)
+    out = K.epilogue(yr, bias, gamma, phi, res, relu, q)
     loss1, g1 = K.lp_loss_and_grad(out, K.Rows(cache, idx), 2.0)
     out.backward(g1)
     sep = [yr.grad, res.grad, gamma.grad, phi.grad] + ([q.delta.grad, q.zero_point.grad] if quant else [])
@@ -1121,9 +1122,9 @@ def test_epilogue_loss_bwd_matches_separate_passes(K, hw, quant):
         t.grad = None
     # fused
     # the lazy placeholder carries exactly these inputs (taken on float4 rows only)
-    lazy = K.epilogue(y, bias, gamma, phi, res, 1, q, lazy=True)
+    lazy = K.epilogue(y, bias, gamma, phi, res, relu, q, lazy=True)
     assert hasattr(lazy, "_ssq_tail") == (hw * hw % 4 == 0)
-    tail = (y, bias, gamma, phi, res, 1, q)
+    tail = (y, bias, gamma, phi, res, relu, q)
     loss2, gy, gres, ggm, gph, gd, gz = K.epilogue_loss_bwd(tail, K.Rows(cache, idx), N * hw * hw)
     fused = [gy, gres, ggm, gph] + ([gd, gz] if quant else [])
     for a, b in zip(sep, fused):
