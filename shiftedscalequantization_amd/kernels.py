@@ -733,8 +733,22 @@ class BiasActFn(torch.autograd.Function):
         return gin, None, (gin if ctx.needs_input_grad[2] else None), None
 
 
-def bias_act(y, bias=None, res=None, relu=True):
-    """relu: activation code (False/0 identity, True/1 ReLU, 2 ReLU6)."""
+def _tail_ok(y, res):
+    """The fused tail (epilogue_loss_bwd) takes float4 rows: contiguous NCHW, hw % 4 == 0,
+    16-B aligned; the kernel's scalar-row form measured no faster on 7x7 planes
+    (profiles/r2_wgrad_gemm.log), so those run eagerly."""
+    return (y.dim() == 4 and (y.shape[2] * y.shape[3]) % 4 == 0 and y.is_contiguous()
+            and y.data_ptr() % 16 == 0
+            and (res is None or (res.is_contiguous() and res.data_ptr() % 16 == 0)))
+
+
+def bias_act(y, bias=None, res=None, relu=True, lazy=False):
+    """relu: activation code (False/0 identity, True/1 ReLU, 2 ReLU6).  lazy: see
+    TAIL_LAZY (the block's final epilogue, fused with the loss and its backward)."""
+    if lazy and int(relu) in (0, 1) and _tail_ok(y, res):
+        out = torch.empty_like(y)
+        out._ssq_tail = (y, bias, None, None, res, int(relu), None)
+        return out
     out = BiasActFn.apply(y, bias, res, int(relu))
     if int(relu) == 1:
         # lets a loss that folds the ReLU backward into its own pass (lp_loss relu_mask)
@@ -924,11 +938,7 @@ TAIL_LAZY = [False]
 def epilogue(y, bias, gamma, phi, res, relu, q=None, lazy=False):
     """EpilogueFn with q an (initialised, per-tensor) act quantizer or None.  lazy: see
     TAIL_LAZY (the placeholder must only reach epilogue_loss_bwd)."""
-    # the fused tail on float4 rows (hw % 4 == 0); the kernel's scalar-row form is tested but
-    # measured no faster than the three passes on 7x7 planes (profiles/r2_wgrad_gemm.log),
-    # so those run eagerly
-    if lazy and y.dim() == 4 and (y.shape[2] * y.shape[3]) % 4 == 0 and y.is_contiguous() \
-            and y.data_ptr() % 16 == 0 and (res is None or (res.is_contiguous() and res.data_ptr() % 16 == 0)):
+    if lazy and _tail_ok(y, res):
         out = torch.empty_like(y)
         out._ssq_tail = (y, bias, gamma, phi, res, int(relu), q)
         return out

@@ -95,7 +95,8 @@ class BaseQuantBlock(nn.Module):
             if q is not None:   # + the block's act quant in the same pass
                 return K.bias_act_quant(raw, bias, residual, relu, q.delta, q.zero_point,
                                         q.n_bits, q.sym)
-            out = K.bias_act(raw, bias, residual, relu)
+            lazy = K.TAIL_LAZY[0] and not self.use_act_quant
+            out = K.bias_act(raw, bias, residual, relu, lazy=lazy)
             if self.use_act_quant:
                 out = self.act_quantizer(out)
             return out
