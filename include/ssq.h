@@ -363,7 +363,9 @@ int ssq_adam(int nseg, float* const* p, const float* const* g, float* const* m,
  * The caller must give each producer's workspace a slot no other launch writes before the
  * flush, and must flush before reading a queued output on the host or with other kernels
  * (the reconstruction loop: deferral on for its body, flush at its end).  Host state,
- * not thread-safe.  ssq_set_deferred_finalize returns the previous setting. */
+ * not thread-safe.  ssq_set_deferred_finalize returns the previous setting; it launches
+ * nothing (it takes no stream), so flush every stream with queued tasks before turning
+ * deferral off. */
 int ssq_set_deferred_finalize(int on);
 int ssq_flush_finalize(ssq_stream_t stream);
 

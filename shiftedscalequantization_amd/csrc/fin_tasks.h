@@ -15,9 +15,11 @@
 //     gives lp_loss its own slot and alternates the epilogue backward between two), and
 //     every producer entry first hands pending tasks to its own launch, so at most one
 //     task per producer is pending;
-//   * ssq_adam (which reads gamma^z / phi^z / delta gradients), the lp_loss entry points,
-//     ssq_flush_finalize and ssq_set_deferred_finalize(0) launch whatever is still pending
-//     as one standalone kernel first; the recon loop flushes at the end of its body.
+//   * ssq_adam (which reads gamma^z / phi^z / delta gradients), the lp_loss entry points
+//     and ssq_flush_finalize launch whatever is still pending as one standalone kernel
+//     first; ssq_set_deferred_finalize(0) only flips the flag (it has no stream), so the
+//     caller flushes before turning deferral off -- the recon loop flushes at the end of
+//     its body (kernels.deferred_finalize).
 #pragma once
 
 #include "ssq_common.h"

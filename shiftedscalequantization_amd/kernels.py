@@ -928,11 +928,12 @@ class deferred_finalize:
                 set_deferred_finalize(self.prev)
 
 
-# Set by the fused recon loop around its block forward: the block's final epilogue is not
-# run; its output is returned as a placeholder carrying the epilogue's inputs (_ssq_tail),
-# and the loop runs forward + loss + backward of that epilogue in one pass
-# (epilogue_loss_bwd).  Only consumed by BaseQuantBlock._tail.
-TAIL_LAZY = [False]
+# Set by the fused recon loop around its block forward to the block it reconstructs: that
+# block's final epilogue is not run; its output is returned as a placeholder carrying the
+# epilogue's inputs (_ssq_tail), and the loop runs forward + loss + backward of that
+# epilogue in one pass (epilogue_loss_bwd).  Only consumed by BaseQuantBlock._tail, and
+# only by the block identical to TAIL_LAZY[0] (nested blocks and hooked blocks run eagerly).
+TAIL_LAZY = [None]
 
 
 def epilogue(y, bias, gamma, phi, res, relu, q=None, lazy=False):
@@ -1310,7 +1311,8 @@ def _out_plane(x, weight, stride, padding):
 
 
 def _use_wgrad_gemm(x, weight, stride, padding, groups=1):
-    if WGRAD_GEMM != "auto" or groups != 1:
+    # WGRAD_POLICY 'never' is the all-MIOpen A/B mode: no GEMM convs either
+    if WGRAD_GEMM != "auto" or WGRAD_POLICY == "never" or groups != 1:
         return False
     if isinstance(stride, (tuple, list)) and len(set(stride)) != 1:
         return False

@@ -84,10 +84,13 @@ class ChannelQuant(nn.Module):
         """The prepared adaShift state (packed floors + h(beta), computed once) when the
         loop-invariant inputs allow it: conv weight, S <= 4, floor candidates, beta not
         being learned.  Rebuilt whenever beta, the hard_round flag or the captured weight
-        change (key below); None -> the recomputing kernels."""
+        change (key below); None -> the recomputing kernels.  A trainable beta is never
+        prepared, also not under no_grad: an optimizer that writes it through raw pointers
+        (SsqAdam) leaves beta._version unchanged, so the key could not see the update."""
         if (self.isFC or self._src_kind != 'floor' or self.beta is None
                 or len(self.shiftTarget) > 4 or not self._src.is_cuda
-                or (self.beta.requires_grad and torch.is_grad_enabled())):
+                or self.beta.requires_grad):
+            self._prep = None
             return None
         key = (self._src.data_ptr(), self._src_delta.data_ptr(), self.beta.data_ptr(),
                self.beta._version, bool(self.hard_round), tuple(self.shiftTarget))

@@ -51,6 +51,9 @@ def backward_tail(tail, grads):
             if t.grad is None:
                 t.grad = g
             else:
+                # g may be a deferred-finalize output (fin_tasks.h): make it final before
+                # another kernel reads it
+                K.flush_finalize(g.device)
                 t.grad.add_(g)
         else:
             roots.append(t)
@@ -141,14 +144,18 @@ def _fused_loop(block, modules, iters, lmda, model, p, lr, bias_cal, batch_size,
             _body_pre()
 
     def _body_pre():
+        if defer and any(t.grad is not None for t in opt_params):
+            # a deferred gamma/phi gradient is only final after the next backward launch:
+            # AccumulateGrad must take it over, never add it into an existing .grad
+            raise RuntimeError("deferred finalizes need every parameter's .grad unset")
         cur_inp, cur_out = feeder.gather_lazy()
         if on_gpu:
             stash_block_weights(quantizers)     # every conv's What in one launch
-        K.TAIL_LAZY[0] = fuse_tail
+        K.TAIL_LAZY[0] = block if fuse_tail else None
         try:
             quant_out = block(cur_inp)
         finally:
-            K.TAIL_LAZY[0] = False
+            K.TAIL_LAZY[0] = None
         clear_stash(quantizers)
         tail = getattr(quant_out, '_ssq_tail', None)
         relu_in = getattr(quant_out, '_ssq_relu_inputs', None)

@@ -86,8 +86,11 @@ class BaseQuantBlock(nn.Module):
             relu = isinstance(self.activation_function, nn.ReLU)
             q = fusable_act_quantizer(self.act_quantizer, self.use_act_quant)
             gamma, phi = last.affine()
+            # lazy only for the block the loop targets, and only when no hook can see the
+            # placeholder output (K.TAIL_LAZY)
+            lazy_ok = K.TAIL_LAZY[0] is self and not self._forward_hooks
             if gamma is not None:   # last's gamma^z/phi^z, residual, act (+ act quant)
-                lazy = K.TAIL_LAZY[0] and (q is not None or not self.use_act_quant)
+                lazy = lazy_ok and (q is not None or not self.use_act_quant)
                 out = K.epilogue(raw, bias, gamma, phi, residual, relu, q, lazy=lazy)
                 if q is None and self.use_act_quant:
                     out = self.act_quantizer(out)
@@ -95,7 +98,7 @@ class BaseQuantBlock(nn.Module):
             if q is not None:   # + the block's act quant in the same pass
                 return K.bias_act_quant(raw, bias, residual, relu, q.delta, q.zero_point,
                                         q.n_bits, q.sym)
-            lazy = K.TAIL_LAZY[0] and not self.use_act_quant
+            lazy = lazy_ok and not self.use_act_quant
             out = K.bias_act(raw, bias, residual, relu, lazy=lazy)
             if self.use_act_quant:
                 out = self.act_quantizer(out)
