@@ -13,7 +13,8 @@ value = elements processed by all ranks / max-over-ranks wall time (Gelem/s, wea
 scaling: every rank owns its own calibration shard; no data-path collective).
 The reconstruction iteration rate (block_recon_fused_shiftedScale, batch 32, bias_cal, every
 ResNet-18 block, reference-faithful deterministic conv solvers as the headline) is reported
-beside it as `recon`, with its SURVEY §8(d) roofline as `roofline_recon`.
+beside it as `recon`, with its SURVEY §8(d) roofline as `roofline_recon` (priced on the
+loop's own kernel launches from a rocprofv3 trace of these loops: tools/recon_roofline.py).
 """
 import argparse
 import json
@@ -124,6 +125,25 @@ def pmc_traffic():
         return None
 
 
+RECON_ROOFLINE_FILE = "profiles/recon_roofline.json"
+
+
+def recon_roofline():
+    """SURVEY §8(d) recon roofline priced on the loop's own launches: the summary that
+    tools/recon_roofline.py wrote from a rocprofv3 kernel trace of this bench's recon loops
+    (per block, per kernel class: time and algorithmic bytes), or None."""
+    path = os.path.join(os.path.dirname(os.path.abspath(__file__)), RECON_ROOFLINE_FILE)
+    try:
+        with open(path) as f:
+            d = json.load(f)
+    except (OSError, ValueError):
+        return None
+    out = {k: v for k, v in d.items() if k != "blocks"}
+    out["source_file"] = RECON_ROOFLINE_FILE
+    out["per_block_gbs"] = {b: v["achieved_gbs"] for b, v in d.get("blocks", {}).items()}
+    return out
+
+
 def time_events(fn, reps, dev, rounds=5):
     """Average launch time (ms) of fn over `reps` back-to-back launches, measured with HIP
     events on the current stream; the median of `rounds` such groups (after one untimed
@@ -191,6 +211,23 @@ def cpu_baseline(act_dev, d_a, z_a, seconds, recon_state=None):
                      f"A4 per-tensor q/dq of act[:64] ({sample.size} elems) x{nN} reps in "
                      f"{elN:.1f}s on {cores} threads; {os.cpu_count()} host CPUs visible",
            "qdq_1thread_gelem_s": round(n1 * sample.size / el1 / 1e9, 4)}
+    # the reference's own CPU path: its eager torch op sequence (oracle/torch_eager.py) on
+    # the same sample, all cores and one thread
+    import torch
+    from oracle.torch_eager import uaq_fake_quant
+    xs, dt, zt = torch.from_numpy(sample), torch.from_numpy(d), torch.from_numpy(z)
+    prev = torch.get_num_threads()
+    eager = {}
+    for nt in (cores, 1):
+        torch.set_num_threads(nt)
+        ne, ele = _timed(lambda: uaq_fake_quant(xs, dt, zt, 4), seconds / 6)
+        eager[nt] = round(ne * sample.size / ele / 1e9, 4)
+    torch.set_num_threads(prev)
+    out["reference_eager_torch"] = {
+        "value": eager[cores], "unit": "Gelem/s", "cores": cores, "value_1thread": eager[1],
+        "kind": "reference op sequence",
+        "sample": "quant_layer.py:92-98 as torch-CPU eager ops (round(x/delta)+zp, clamp, "
+                  "(q-zp)*delta) on the same act[:64] sample"}
     if recon_state is not None:
         import torch
         from oracle.recon_cpu import FusedBlockReconCPU
@@ -255,7 +292,11 @@ def main():
     rd_gbs = 4.0 * n_act / (time_events(lambda: K.stream_read(act, sink), 20, dev) * 1e-3) / 1e9
     wr_gbs = 4.0 * n_act / (time_events(lambda: K.stream_write(y_act), 20, dev) * 1e-3) / 1e9
     mix_gbs = 2.0 / (1.0 / rd_gbs + 1.0 / wr_gbs)
-    ms_w = time_events(lambda: K.fake_quant_multi(weights, dws, zws, bits), 20, dev)
+    # all 21 weights in one launch: device time from a HIP-graph replay (no host launch
+    # cost), beside the eager host-launch rate of the same call
+    from shiftedscalequantization_amd.recon_bench import graph_time_ms
+    ms_w = graph_time_ms(lambda: K.fake_quant_multi(weights, dws, zws, bits))
+    ms_w_launch = time_events(lambda: K.fake_quant_multi(weights, dws, zws, bits), 20, dev)
     # W2 per-channel q/dq of the large synthetic weight of BASELINE.md §2 ([8192,2048,3,3],
     # per-output-channel delta/zp staged in LDS): the per-channel kernel's roofline line
     big = torch.empty(8192, 2048, 3, 3, device=dev).normal_(0.0, 0.02)
@@ -310,13 +351,18 @@ def main():
                      "mixed_rw_ceiling_gbs": round(mix_gbs, 1),
                      "frac_of_mixed_rw_ceiling": round(achieved / mix_gbs, 4)},
         "weights_multi_ms": round(ms_w, 4),
+        "weights_multi_ms_source": "HIP-graph replay of the one-launch W2/W8 q/dq of all 21 "
+                                   "weights (11.68 M elems): kernel time",
+        "weights_multi_launch_ms": round(ms_w_launch, 4),
         "roofline_per_channel": {"kernel": "fq_fwd_multi_kernel (ssq_fq_fwd per-channel, 1 segment)",
                                  "workload": "W2 per-channel q/dq of [8192,2048,3,3] (151 M elems)",
                                  "achieved": round(pc_gbs, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                                  "frac": round(pc_gbs / HBM_PEAK_GBS, 4), "kernel_ms": round(ms_pc, 4)},
     }
     if recon is not None:
-        out["roofline_recon"] = recon.pop("roofline_recon")
+        rr = recon_roofline()
+        if rr is not None:
+            out["roofline_recon"] = rr
         out["recon"] = recon
     if validation is not None:
         out["validation"] = validation

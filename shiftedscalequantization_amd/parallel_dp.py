@@ -21,6 +21,10 @@ def rank():
 # Test hook: when set to a list, every GradBucket.allreduce_ appends (local, reduced) flat
 # copies -- the per-rank gradient before the collective and the summed one after it.
 RECORD = None
+# Bench hook: when set to a list, every device bucket's collective appends (start, end,
+# elements) -- HIP events recorded on the current stream around it (the collective, the
+# current stream's wait on it, and the average's division), for its time per iteration.
+TIMING = None
 
 
 class GradBucket:
@@ -86,10 +90,18 @@ class GradBucket:
         ws = world()
         if RECORD is not None:
             RECORD.append(["local", self.flat.detach().clone()])
+        timed = TIMING is not None and self.flat.is_cuda
+        if timed:
+            e0 = torch.cuda.Event(enable_timing=True)
+            e0.record()
         if self.flat.numel():
             dist.all_reduce(self.flat, op=dist.ReduceOp.SUM)
             if self.average:
                 self.flat.div_(ws)
+        if timed:
+            e1 = torch.cuda.Event(enable_timing=True)
+            e1.record()
+            TIMING.append((e0, e1, self.flat.numel()))
         if RECORD is not None:
             RECORD[-1].append(self.flat.detach().clone())
 

@@ -209,6 +209,18 @@ class frozen_except:
 # replays per form ("single" graph, "split" around the collective): test / report hook
 GRAPH_REPLAYS = {"single": 0, "split": 0}
 
+# Test probe of the reconstruction loops: when set, called as ITER_PROBE[0](i, opt_params)
+# at the start of iteration i (before its batch is drawn) and once more with i = iters
+# after the last one.  At that point every p.grad still holds iteration i-1's gradient
+# (before its Adam step consumed it; a graph replay writes the same tensors), and an
+# in-place write to a parameter is what iteration i computes from (teacher forcing).
+ITER_PROBE = [None]
+
+
+def probe(i, opt_params):
+    if ITER_PROBE[0] is not None:
+        ITER_PROBE[0](i, opt_params)
+
 
 class IterationGraph:
     """HIP-graph replay of a reconstruction iteration split at its one exchange step.

@@ -12,7 +12,8 @@ import torch
 
 from .. import kernels as K
 from ..parallel_dp import GradBucket, world
-from ._engine import BatchFeeder, IterationGraph, LazyValue, SsqAdam, as_float, frozen_except
+from ._engine import (BatchFeeder, IterationGraph, LazyValue, SsqAdam, as_float, frozen_except,
+                      probe)
 from .adaptive_rounding import AdaRoundQuantizer
 from .data_utils import save_grad_data, save_inp_oup_data
 from .quant_block import BaseQuantBlock
@@ -97,6 +98,7 @@ def _eager_loop(opt_params, loss_func, feeder, bucket, cached_grads, block, iter
         scheduler = torch.optim.lr_scheduler.CosineAnnealingLR(optimizer, T_max=max(iters, 1),
                                                                eta_min=0.)
     for i in range(iters):
+        probe(i, opt_params)
         perm = feeder.draw()
         cur_inp, cur_out = feeder.next(perm)
         cur_grad = cached_grads[perm.to(cached_grads.device)] if cached_grads is not None else None
@@ -111,6 +113,7 @@ def _eager_loop(opt_params, loss_func, feeder, bucket, cached_grads, block, iter
         optimizer.step()
         if scheduler:
             scheduler.step()
+    probe(iters, opt_params)
 
 
 def _fast_loop(block, qmodules, opt_params, loss_func, feeder, bucket, iters, act_quant, lr, p,
@@ -169,6 +172,7 @@ def _fast_loop(block, qmodules, opt_params, loss_func, feeder, bucket, iters, ac
         for i in range(iters):
             if ITER_HOOK is not None:
                 ITER_HOOK(i, iters)
+            probe(i, opt_params)
             b, lam, active = loss_func.schedule()
             feeder.stage(feeder.draw(), extra=(lam, float(b)) + optimizer.next_hyper())
             # the round-loss value (reporting only) from alpha before this step, as the
@@ -197,6 +201,7 @@ def _fast_loop(block, qmodules, opt_params, loss_func, feeder, bucket, iters, ac
                 optimizer.param_groups[0]['lr'] = shadow.param_groups[0]['lr']
         if ITER_HOOK is not None:
             ITER_HOOK(iters, iters)
+        probe(iters, opt_params)
     finally:
         for q in ada:
             q._fused_reg = None

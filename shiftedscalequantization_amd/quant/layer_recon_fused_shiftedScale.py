@@ -20,7 +20,7 @@ from tqdm import tqdm
 from .. import kernels as K
 from ..parallel_dp import GradBucket, world
 from ._engine import (BatchFeeder, IterationGraph, LazyValue, SsqAdam, as_float, clear_stash,
-                      stash_block_weights)
+                      probe, stash_block_weights)
 from .quant_block import BaseQuantBlock
 from .quant_layer import QuantModule
 
@@ -185,6 +185,7 @@ def _fused_loop(block, modules, iters, lmda, model, p, lr, bias_cal, batch_size,
     start_loss = 0.0
     t = tqdm(range(iters), desc='', dynamic_ncols=True, disable=not verbose)
     for i in t:
+        probe(i, opt_params)
         if iter_hook is not None:
             iter_hook(i)
         # reference-identical CPU randperm draw + this iteration's (lambda_S, b2): one H2D copy
@@ -210,6 +211,7 @@ def _fused_loop(block, modules, iters, lmda, model, p, lr, bias_cal, batch_size,
             start_loss = max(start_loss, as_float(loss_func.rec_loss))
             t.set_description(f"{start_loss:.6f} -> {as_float(loss_func.rec_loss):.6f} "
                               f"{loss_func.round_loss_val} ")
+    probe(iters, opt_params)
     if graph_obj is not None:
         torch.cuda.current_stream().synchronize()
         for p_ in opt_params:       # detach the grads from the graph's private pool

@@ -11,7 +11,7 @@ from tqdm import tqdm
 
 from .. import kernels as K
 from ..parallel_dp import GradBucket, world
-from ._engine import BatchFeeder, LazyValue, as_float
+from ._engine import BatchFeeder, LazyValue, as_float, probe
 from .quant_block import BaseQuantBlock
 from .quant_layer import QuantModule, UniformAffineQuantizer
 
@@ -24,6 +24,7 @@ def _loop(block, opt_params, optimizer, scheduler, loss_func, iters, batch_size,
     start_loss = 0.0
     t = tqdm(range(iters), desc='', dynamic_ncols=True, disable=not verbose)
     for i in t:
+        probe(i, opt_params)
         cur_inp, cur_out = feeder.next()
         optimizer.zero_grad()
         if bucket is not None:
@@ -40,6 +41,7 @@ def _loop(block, opt_params, optimizer, scheduler, loss_func, iters, batch_size,
             start_loss = max(start_loss, as_float(loss_func.rec_loss))
             t.set_description(f"{start_loss:.6f} -> {as_float(loss_func.rec_loss):.6f} "
                               f"{as_float(loss_func.round_loss_val):.3f} ")
+    probe(iters, opt_params)
     return feeder, start_loss
 
 

@@ -24,6 +24,7 @@ import torch.nn as nn
 
 REF = "/root/reference"
 OUT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, OUT)       # realshape.py: the seeded real-shape cases shared with the tests
 
 
 # --------------------------------------------------------------------------- stubs
@@ -465,6 +466,81 @@ class _Spy:
         torch.randperm = self.orig_rp
 
 
+class _GradSpy:
+    """Records, at the chosen optimizer step counts (counted over every torch.optim.Adam
+    step taken inside the context), each optimised parameter's value before the step and
+    the gradient the reference's backward handed to it."""
+
+    def __init__(self, at, truth=None):
+        self.at, self.n, self.rec, self.truth, self.rec64 = set(at), 0, {}, truth, {}
+
+    def __enter__(self):
+        self.orig = torch.optim.Adam.step
+        spy = self
+
+        def step(opt, *a, **k):
+            if spy.n in spy.at:
+                ps = [p for grp in opt.param_groups for p in grp["params"]]
+                spy.rec[spy.n] = ([t2n(p) for p in ps], [t2n(p.grad) for p in ps])
+                if spy.truth is not None:
+                    spy.rec64[spy.n] = spy.truth(spy.n)
+            spy.n += 1
+            return spy.orig(opt, *a, **k)
+
+        torch.optim.Adam.step = step
+        return self
+
+    def __exit__(self, *exc):
+        torch.optim.Adam.step = self.orig
+
+    def dump(self, out, prefix=""):
+        """Full parameters and gradients (small tensors only)."""
+        for s, (ps, gs) in sorted(self.rec.items()):
+            for j, (p, g) in enumerate(zip(ps, gs)):
+                out[f"{prefix}gs{s}_p{j}"] = p
+                out[f"{prefix}gs{s}_g{j}"] = g
+            for j, t in enumerate(self.rec64.get(s, [])):
+                out[f"{prefix}gs{s}_t{j}"] = t
+        out[prefix + "grad_steps"] = np.array(sorted(self.rec), np.int64)
+
+
+def _to64(mod):
+    """`mod` in float64: parameters and buffers (.double()) and every float tensor held as
+    a plain attribute or in a list attribute (ChannelQuant's x_q, org_weight, caches)."""
+    mod.double()
+    for m in mod.modules():
+        for k, v in list(vars(m).items()):
+            if isinstance(v, nn.Parameter):
+                continue
+            if isinstance(v, torch.Tensor) and v.is_floating_point():
+                setattr(m, k, v.detach().double())
+            elif isinstance(v, list) and v and all(isinstance(t, torch.Tensor) for t in v):
+                setattr(m, k, [t.detach().double() if t.is_floating_point() else t for t in v])
+    return mod
+
+
+def _fused_truth(block, spy, lmda, iters, batch_size=32):
+    """The reference's own fused-loop gradient of iteration `step`, evaluated in float64 at
+    the parameters the fp32 run holds there (same batch, same loss schedule): the exact
+    gradient both fp32 implementations approximate."""
+    import copy
+
+    def truth(step):
+        b64 = _to64(copy.deepcopy(block))
+        qs = [m.weight_quantizer for m in b64.modules() if isinstance(m, QuantModule)]
+        for q in qs:
+            q.alpha.grad = None
+        lf = LRF.FusedScaleLossFunction(b64, qs, round_loss="relaxation", lmda=lmda, max_count=iters,
+                                        b_range=(20, 2), decay_start=0, warmup=0.2, p=2.0)
+        lf.count = step
+        perm = spy.perms[-1][:batch_size]
+        inp = torch.cat(b64.cached_inp_features)[perm]
+        tgt = torch.cat(b64.cached_out_features)[perm]
+        spy.orig_call(lf, b64(inp), tgt).backward()
+        return [np.asarray(q.alpha.grad.detach().numpy(), np.float64).copy() for q in qs]
+    return truth
+
+
 def _dump_block(out, block, prefix=""):
     for n in CONVS:
         m = getattr(block, n)
@@ -495,7 +571,9 @@ def gen_recon_fused(iters=30, n_cali=16, res=16):
     out["cached_out"] = t2n(torch.cat(block.cached_out_features))
     torch.manual_seed(1005)
     with _Spy(LRF.FusedScaleLossFunction) as spy:
-        res_loss = LRF.block_recon_fused_shiftedScale(block, iters, (0.01, 0.1), qnn, None)
+        with _GradSpy((0, 5, 20, iters - 1), _fused_truth(block, spy, (0.01, 0.1), iters)) as gspy:
+            res_loss = LRF.block_recon_fused_shiftedScale(block, iters, (0.01, 0.1), qnn, None)
+    gspy.dump(out)
     out["perms"] = np.stack([p.numpy() for p in spy.perms]).astype(np.int64)
     out["rec_loss"] = np.array([r[0] for r in spy.rec], np.float64)
     out["total_loss"] = np.array([r[1] for r in spy.rec], np.float64)
@@ -532,8 +610,9 @@ def gen_recon_layer_shift(iters=20, n_cali=16, res=16):
            "cached_inp": t2n(torch.cat(m.cached_inp_features)),
            "cached_out": t2n(torch.cat(m.cached_out_features))}
     torch.manual_seed(1005)
-    with _Spy(LRS.ScaleLossFunction) as spy:
+    with _Spy(LRS.ScaleLossFunction) as spy, _GradSpy((0, 5, iters - 1)) as gspy:
         l1 = LRS.layer_recon_shiftedScale(m, iters, 0.1, qnn, None)
+    gspy.dump(out, "shift_")
     out["shift_perms"] = np.stack([p.numpy() for p in spy.perms]).astype(np.int64)
     out["shift_total_loss"] = np.array([r[1] for r in spy.rec], np.float64)
     out["shift_rec_loss"] = np.array([r[0] for r in spy.rec], np.float64)
@@ -541,8 +620,9 @@ def gen_recon_layer_shift(iters=20, n_cali=16, res=16):
     out["shift_alpha"] = t2n(m.weight_quantizer.alpha)
     out["shift_xq"] = np.stack([t2n(t) for t in m.weight_quantizer.x_q])
     m.weight_quantizer.hard_targets = False
-    with _Spy(LRS.ScaleLossFunction) as spy:
+    with _Spy(LRS.ScaleLossFunction) as spy, _GradSpy((0, 5, iters - 1)) as gspy:
         l2 = LRS.layer_recon_shiftedScale(m, iters, 0.01, qnn, None, adaround=True)
+    gspy.dump(out, "ar_")
     out["ar_perms"] = np.stack([p.numpy() for p in spy.perms]).astype(np.int64)
     out["ar_total_loss"] = np.array([r[1] for r in spy.rec], np.float64)
     out["ar_rec_loss"] = np.array([r[0] for r in spy.rec], np.float64)
@@ -962,8 +1042,11 @@ def gen_driver(iters=20, n_cali=16, res=16):
         out[f"b{k}_cached_inp"] = t2n(torch.cat(block.cached_inp_features))
         out[f"b{k}_cached_out"] = t2n(torch.cat(block.cached_out_features))
         MSM.set_quant_state_block(qnn, [layer], "", True)
-        SSQD.QuantRecursiveShiftRecon(qnn, [layer], qnn, None, "", loss_dic, iters=iters, lmda=0.1,
-                                      shiftTarget=shift)
+        with _Spy(LRF.FusedScaleLossFunction) as spy, \
+                _GradSpy((0, 5, iters - 1), _fused_truth(block, spy, (0.01, 0.1), iters)) as gspy:
+            SSQD.QuantRecursiveShiftRecon(qnn, [layer], qnn, None, "", loss_dic, iters=iters,
+                                          lmda=0.1, shiftTarget=shift)
+        gspy.dump(out, f"b{k}_")
         qnn.clear_cached_features()
         out[f"b{k}_losses"] = np.array(loss_dic[layer][0], np.float64)
         names = ("conv1", "conv2") + (("downsample",) if k == 1 else ())
@@ -1083,10 +1166,141 @@ def gen_validate(n_cali=16, n_val=40, res=16, bs=8):
     save("validate_w2a4", **out)
 
 
+# ------------------------------------------------------------------ round-3: real shapes
+def _real_block(kind, cin, cout):
+    """The reference's own block classes at the real channel counts (realshape.CASES)."""
+    if kind == "basic":
+        from models.resnet import BasicBlock
+        ds = nn.Sequential(nn.Conv2d(cin, cout, 1, stride=2, bias=False), nn.BatchNorm2d(cout))
+        return BasicBlock(cin, cout, stride=2, downsample=ds, norm_layer=nn.BatchNorm2d)
+    if kind == "bottleneck":
+        from models.resnet import Bottleneck
+        ds = nn.Sequential(nn.Conv2d(cin, cout, 1, stride=1, bias=False), nn.BatchNorm2d(cout))
+        return Bottleneck(cin, cout // 4, stride=1, downsample=ds, norm_layer=nn.BatchNorm2d)
+    if kind == "inverted":
+        from models.mobilenetv2 import InvertedResidual
+        return InvertedResidual(cin, cout, 1, 6)
+    from models.regnet import ResBottleneckBlock
+    return ResBottleneckBlock(cin, cout, 2, 1.0, 48)
+
+
+def _real_qnn(case):
+    from quant.quant_block import BaseQuantBlock
+    import realshape as RS
+    if not hasattr(BaseQuantBlock, "setPathName"):
+        BaseQuantBlock.setPathName = lambda self, n: setattr(self, "pathName", n)
+    kind, cin, cout, _ = RS.CASES[case]
+    net = RS.seed_net(RS.wrap(_real_block(kind, cin, cout), cout))
+    lay = (RS.layout(net), RS.seed_sha(net))
+    wq = {"n_bits": 2, "channel_wise": True, "scale_method": "max", "tune_delta_zero": False,
+          "symmetric": False}
+    aq = {"n_bits": 4, "channel_wise": False, "scale_method": "mse", "tune_delta_zero": False,
+          "leaf_param": True, "symmetric": False}
+    qnn = QuantModel(model=net, weight_quant_params=wq, act_quant_params=aq)
+    qnn.eval()
+    return qnn, lay
+
+
+def _dump_sub(out, key, a, idx):
+    a = np.asarray(a, np.float32).reshape(-1)
+    out[key + "_sub"] = a[idx]
+    out[key + "_max"] = np.array([np.abs(a).max(initial=0.0)], np.float64)
+
+
+def gen_real_shapes(cases=None):
+    """Reference-pinned parity at the real block shapes of configs 2-5 (realshape.CASES):
+    the fused shifted-scale loop (block_recon_fused_shiftedScale, 20 iterations) and BRECQ's
+    AdaRound block reconstruction (10 iterations) on 8 calibration inputs.  Weights and
+    inputs are regenerated from integer seeds on both sides; recorded are the reference's
+    folded-weight hashes, weight quantizer deltas / zero points, FP block outputs,
+    per-iteration losses and batch draws, the shift logits alpha ([C_in, S]) with their value
+    and gradient at GRAD_STEPS, BRECQ's AdaRound V ([C_out, ...], full weight size:
+    sub-sampled at fixed entries with its max-abs, per-output-channel gradient L1 norms and
+    the packed sign bits that decide the hard rounding) and the hashes of the final hard
+    weights."""
+    import realshape as RS
+    from quant.channelQuant import ChannelQuant
+    shift = [31 / 32, 33 / 32, 1.0]
+    for case in (cases or RS.CASES):
+        kind, cin, cout, _ = RS.CASES[case]
+        x = RS.calib_input(case)
+        lay, ssha = _real_qnn(case)[1]
+        out = {"layout": np.array(lay), "seed_sha": np.array([ssha])}
+        # ---- fused shifted-scale loop
+        qnn, _ = _real_qnn(case)
+        block = qnn.model[0]
+        qnn.set_quant_state(True, False)
+        with torch.no_grad():
+            qnn(x)
+        qms = _named_qms(block)
+        out["qms"] = np.array([n for n, _ in qms])
+        for n, m in qms:
+            out[f"{n}_w_sha"] = np.array([RS.sha(t2n(m.org_weight))])
+            out[f"{n}_b_sha"] = np.array([RS.sha(t2n(m.org_bias))])
+            out[f"{n}_delta"] = t2n(m.weight_quantizer.delta.reshape(-1))
+            out[f"{n}_zp"] = t2n(m.weight_quantizer.zero_point.reshape(-1))
+            m.weight_quantizer = ChannelQuant(1.0, uaq=m.weight_quantizer, weight_tensor=m.org_weight.data,
+                                              shiftTarget=shift, name="." + n)
+            m.use_weight_quant = True
+            m.cache_features = "none"
+        qnn.set_quant_state(False, False)
+        with torch.no_grad():
+            fp = block(x)
+        out["cached_out"] = t2n(fp)
+        block.cached_inp_features, block.cached_out_features = [x.clone()], [fp.clone()]
+        MSM.set_quant_state_block(qnn, [".model.0"], "", True)
+        for n, m in qms:
+            out[f"{n}_beta0_sha"] = np.array([RS.sha(t2n(m.weight_quantizer.beta))]) \
+                if getattr(m.weight_quantizer, "beta", None) is not None else np.array([""])
+        torch.manual_seed(1005)
+        with _Spy(LRF.FusedScaleLossFunction) as spy:
+            with _GradSpy(RS.GRAD_STEPS, _fused_truth(block, spy, (0.01, 0.1), RS.ITERS)) as gspy:
+                res_loss = LRF.block_recon_fused_shiftedScale(block, RS.ITERS, (0.01, 0.1), qnn, None)
+        out["perms"] = np.stack([p.numpy() for p in spy.perms]).astype(np.int64)
+        out["rec_loss"] = np.array([r[0] for r in spy.rec], np.float64)
+        out["final_losses"] = np.array(res_loss, np.float64)
+        gspy.dump(out)      # alpha is [C_in, S] (per input channel): small, kept whole
+        for j, (n, m) in enumerate(qms):
+            q = m.weight_quantizer
+            out[f"{n}_alpha"] = t2n(q.alpha)
+            bt = t2n(q.beta)
+            out[f"{n}_beta_sha"] = np.array([RS.sha(bt)])
+            out[f"{n}_beta_sub"] = bt.reshape(-1)[RS.sub_idx(bt.size)]
+            with torch.no_grad():
+                out[f"{n}_what_hard_sha"] = np.array([RS.sha(t2n(q(m.weight)))])
+        # ---- BRECQ AdaRound block reconstruction
+        qnn, _ = _real_qnn(case)
+        block = qnn.model[0]
+        qnn.set_quant_state(True, False)
+        with torch.no_grad():
+            qnn(x)
+        qms = _named_qms(block)
+        torch.manual_seed(1005)
+        with _Spy(BR.LossFunction) as spy, _GradSpy(RS.BRECQ_GRAD_STEPS) as gspy:
+            BR.block_reconstruction(qnn, block, x, batch_size=8, iters=RS.BRECQ_ITERS, weight=0.01,
+                                    asym=True, b_range=(20, 2), warmup=0.2, act_quant=False,
+                                    opt_mode="mse")
+        out["b_perms"] = np.stack([p.numpy() for p in spy.perms]).astype(np.int64)
+        out["b_total_loss"] = np.array([r[1] for r in spy.rec], np.float64)
+        for j, (n, m) in enumerate(qms):
+            q = m.weight_quantizer
+            v = t2n(q.alpha)
+            idx = RS.sub_idx(v.size)          # fixed entries: the test re-derives them
+            _dump_sub(out, f"b_{n}_V", v, idx)
+            out[f"b_{n}_V_pos"] = np.packbits((v >= 0).reshape(-1))
+            for s_ in RS.BRECQ_GRAD_STEPS:
+                g = gspy.rec[s_][1][j]
+                _dump_sub(out, f"b_{n}_gs{s_}", g, idx)
+                out[f"b_{n}_gs{s_}_rowl1"] = RS.row_l1(g)
+            with torch.no_grad():
+                out[f"b_{n}_what_hard_sha"] = np.array([RS.sha(t2n(q(m.weight)))])
+        save(f"real_{case}", **out)
+
+
 if __name__ == "__main__":
     which = sys.argv[1:] or ["uaq", "channelquant", "adaround", "inpscale", "loss", "recon",
                              "layershift", "brecq", "blocks", "act", "layerfused", "blockshift", "driver",
-                             "wmse", "validate"]
+                             "wmse", "validate", "real"]
     torch.set_num_threads(4)
     if "uaq" in which:
         gen_uaq()
@@ -1118,3 +1332,5 @@ if __name__ == "__main__":
         gen_wmse_driver()
     if "validate" in which:
         gen_validate()
+    if "real" in which:
+        gen_real_shapes()

@@ -1,0 +1,157 @@
+"""SURVEY §8(d) reconstruction roofline from a rocprofv3 kernel trace of the REAL loop.
+
+    python tools/recon_roofline.py KERNEL_TRACE.csv [OUT.json]
+
+The trace is that of `bench.py` (recon_bench.run_recon_bench: for every ResNet-18 block
+one deterministic-solver loop, then one benchmark-solver loop; 20 warm-up + K timed
+iterations each, batch 32, bias_cal).  Loop segments are found from the gather launches
+(one per iteration; segments split at > 5 ms gaps); the deterministic loop of block b is
+the (2b)-th segment.  Over its timed iterations every launch is classified by kernel name
+and priced with the algorithmic bytes of that launch (A = batch * C_out * H' * W' output
+elements of the block's convs, N_W its weights, N_in its gathered input elements):
+
+  K5p  shift_fwd_prep                        12 B / weight   (packed floors + h(beta) in, W^ out)
+  K6p  alpha_bwd_prep (+ _stage2)            12 B / weight   (dL/dW^ + packed floors + h(beta) in)
+  K14  gather2_kernel                         8 B / input elem (batch rows in and out)
+  K13  bias_act_kernel<RES,...>              (8 + 4 RES) B / A (y [+ residual] in, activation out)
+  K13b epilogue_bwd_rows<RES,...,LOSS=false> (12 + 4 RES + 4 GRES) B / A (g, y [, res] in,
+                                              gy [, g_res] out)
+  K11t epilogue_bwd_rows<...,LOSS=true>      (12 + 4 RES + 4 GRES) B / A, the fused tail: y,
+                                              target rows [, res] in, gy [, g_res] out
+  K11  lp_loss_kernel                         12 B / A (prediction, target rows in, gradient out)
+  K12  adam_kernel                            28 B / parameter (p, g, m, v in; p, m, v out)
+
+GRES (a residual gradient is written) holds for blocks with a downsample branch.  Every
+other launch (MIOpen / hipBLASLt convs, the K17 / GEMM-operand conv kernels) is reported
+as conv time, outside the HBM set.  Writes the JSON that bench.py reports as
+`roofline_recon` (profiles/<round>_recon_roofline.json)."""
+import collections
+import csv
+import json
+import re
+import sys
+
+BATCH = 32
+S = 3
+# ResNet-18 blocks (models/resnet.py:260): input (C_in, H, W) at 224x224, C_out, stride
+BLOCKS = {"layer1.0": ((64, 56, 56), 64, 1), "layer1.1": ((64, 56, 56), 64, 1),
+          "layer2.0": ((64, 56, 56), 128, 2), "layer2.1": ((128, 28, 28), 128, 1),
+          "layer3.0": ((128, 28, 28), 256, 2), "layer3.1": ((256, 14, 14), 256, 1),
+          "layer4.0": ((256, 14, 14), 512, 2), "layer4.1": ((512, 7, 7), 512, 1)}
+HBM_PEAK_GBS = 8000.0
+
+
+def block_sizes(name):
+    (cin, h, w), cout, stride = BLOCKS[name]
+    ho, wo = (h + 2 - 3) // stride + 1, (w + 2 - 3) // stride + 1
+    ds = stride != 1 or cin != cout
+    n_w = cout * cin * 9 + cout * cout * 9 + (cout * cin if ds else 0)
+    # alpha rows = input channels per conv; bias_cal adds gamma^z / phi^z per output channel
+    n_par = (cin + cout + (cin if ds else 0)) * S + 2 * cout * (3 if ds else 2)
+    return {"A": BATCH * cout * ho * wo, "N_W": n_w, "N_in": BATCH * cin * h * w, "ds": ds,
+            "n_params": n_par}
+
+
+def targs(name):
+    m = re.search(r"<([^>]*)>", name)
+    if not m:
+        return []
+    return [a.strip() for a in m.group(1).split(",")]
+
+
+def classify(name, sz):
+    """(class, algorithmic bytes) of one launch, or (None, 0) outside the HBM set."""
+    a = targs(name)
+    A = sz["A"]
+    if "shift_fwd_prep" in name:
+        return "K5p_adashift_fwd", 12 * sz["N_W"]
+    if "alpha_bwd_prep_stage2" in name:
+        return "K6p_adashift_bwd", 0
+    if "alpha_bwd_prep" in name:
+        return "K6p_adashift_bwd", 12 * sz["N_W"]
+    if "gather2_kernel" in name:
+        return "K14_gather", 8 * sz["N_in"]
+    if "bias_act_kernel" in name:
+        res = a[0] == "true"
+        return "K13_epilogue_fwd", (8 + 4 * res) * A
+    if "epilogue_bwd_rows" in name:
+        res, loss = a[0] == "true", a[5] == "true"
+        gres = res and sz["ds"]
+        b = (12 + 4 * res + 4 * gres) * A
+        return ("K11t_fused_tail" if loss else "K13b_epilogue_bwd"), b
+    if "lp_loss_kernel" in name:
+        return "K11_lp_loss", 12 * A
+    if "adam_kernel" in name:
+        return "K12_adam", 28 * sz["n_params"]
+    return None, 0
+
+
+def segments(rows):
+    gi = [i for i, r in enumerate(rows) if "gather2_kernel" in r["Kernel_Name"]]
+    segs, cur = [], [gi[0]]
+    for a, b in zip(gi, gi[1:]):
+        if int(rows[b]["Start_Timestamp"]) - int(rows[a]["Start_Timestamp"]) > 5e6:
+            segs.append(cur)
+            cur = []
+        cur.append(b)
+    segs.append(cur)
+    return [s for s in segs if len(s) >= 50]          # the loops (not one-off gathers)
+
+
+def analyse(path, warmup=20):
+    rows = list(csv.DictReader(open(path)))
+    rows.sort(key=lambda r: int(r["Start_Timestamp"]))
+    segs = segments(rows)
+    names = list(BLOCKS)
+    if len(segs) != 2 * len(names):
+        raise SystemExit(f"expected {2 * len(names)} loop segments, found {len(segs)}")
+    out, tot_b, tot_us = {}, 0.0, 0.0
+    for b, name in enumerate(names):
+        seg = segs[2 * b][warmup:]          # the timed iterations of the deterministic loop
+        sz = block_sizes(name)
+        n_it = len(seg) - 1
+        us, by, cnt = collections.Counter(), collections.Counter(), collections.Counter()
+        other_us = 0.0
+        for r in rows[seg[0]:seg[-1]]:
+            d = (int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e3
+            cls, nb = classify(r["Kernel_Name"], sz)
+            if cls is None:
+                other_us += d
+                continue
+            us[cls] += d
+            by[cls] += nb
+            cnt[cls] += 1
+        t0, t1 = int(rows[seg[0]]["Start_Timestamp"]), int(rows[seg[-1]]["Start_Timestamp"])
+        cls_out = {c: {"us": round(us[c] / n_it, 2), "bytes": int(by[c] / n_it),
+                       "launches": round(cnt[c] / n_it, 2),
+                       "gbs": round(by[c] / (us[c] * 1e-6) / 1e9, 1) if us[c] else None}
+                   for c in sorted(us)}
+        b_it, us_it = sum(by.values()) / n_it, sum(us.values()) / n_it
+        out[name] = {"iterations": n_it, "wall_us": round((t1 - t0) / 1e3 / n_it, 2),
+                     "hbm_set_us": round(us_it, 2), "hbm_set_bytes": int(b_it),
+                     "achieved_gbs": round(b_it / (us_it * 1e-6) / 1e9, 1),
+                     "other_us": round(other_us / n_it, 2), "kernels": cls_out, "sizes": sz}
+        tot_b += b_it
+        tot_us += us_it
+    ach = tot_b / (tot_us * 1e-6) / 1e9
+    return {"bound": "hbm", "source": "rocprofv3 --kernel-trace of bench.py's recon loops "
+                                      "(deterministic solvers, timed iterations)",
+            "kernels": "K5p + K6p + K11t fused tail / K11 + K13 epilogues + K14 gather + "
+                       "K12 adam, every launch of the loop iteration, all 8 blocks",
+            "bytes_per_iteration": int(tot_b), "us_per_iteration": round(tot_us, 2),
+            "achieved": round(ach, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+            "frac": round(ach / HBM_PEAK_GBS, 4), "blocks": out}
+
+
+if __name__ == "__main__":
+    res = analyse(sys.argv[1])
+    txt = json.dumps(res, indent=1)
+    if len(sys.argv) > 2:
+        with open(sys.argv[2], "w") as f:
+            f.write(txt + "\n")
+    print(json.dumps({k: v for k, v in res.items() if k != "blocks"}))
+    for name, v in res["blocks"].items():
+        print(f"{name}: {v['hbm_set_us']:7.2f} us {v['hbm_set_bytes'] / 1e6:7.2f} MB "
+              f"{v['achieved_gbs']:7.1f} GB/s  (other {v['other_us']:.1f} us, wall {v['wall_us']:.1f})")
+        for c, k in v["kernels"].items():
+            print(f"    {c:20s} {k['us']:7.2f} us x{k['launches']:.0f} {k['bytes'] / 1e6:7.2f} MB {k['gbs']}")

@@ -18,6 +18,8 @@ KT=$(find $OUT/prof_$TAG -name "*kernel_trace.csv" | head -1)
 [ -n "$KT" ] && python3 $R/tools/trace_iter.py "$KT" > $OUT/iter_anatomy_$TAG.txt 2>&1
 # the headline kernel's full-size launches only (the stats average also holds small ones)
 [ -n "$KT" ] && python3 $R/tools/k1_trace_stats.py "$KT" > $OUT/k1_trace_$TAG.json 2>&1
+# the recon roofline priced on the loop's own launches (bench.py reports profiles/recon_roofline.json)
+[ -n "$KT" ] && python3 $R/tools/recon_roofline.py "$KT" $OUT/recon_roofline_$TAG.json > $OUT/recon_roofline_$TAG.txt 2>&1
 [ -n "$KT" ] && rm -f "$KT"
 cd $R
 bash tools/dist_bench2.sh > $OUT/dist2_$TAG.log 2>&1 || { echo "dist2 failed"; tail -30 $OUT/dist2_$TAG.log; exit 1; }
