@@ -519,6 +519,29 @@ def _to64(mod):
     return mod
 
 
+def _layer_truth(layer, spy, lmda, iters, adaround, batch_size=32):
+    """As _fused_truth, for layer_recon_shiftedScale's loop (ScaleLossFunction): the
+    gradient of the shift logits alpha (shift phase) or of AdaRound's beta (adaround
+    phase) in float64 at the fp32 run's parameters of iteration `step`."""
+    import copy
+
+    def truth(step):
+        l64 = _to64(copy.deepcopy(layer))
+        q = l64.weight_quantizer
+        p = q.beta if adaround else q.alpha
+        p.grad = None
+        lf = LRS.ScaleLossFunction(l64, round_loss="relaxation", lmda=lmda, max_count=iters,
+                                   b_range=(20, 2), decay_start=0, warmup=0.2, p=2.0,
+                                   adaround=adaround)
+        lf.count = step
+        perm = spy.perms[-1][:batch_size]
+        inp = torch.cat(l64.cached_inp_features)[perm]
+        tgt = torch.cat(l64.cached_out_features)[perm]
+        spy.orig_call(lf, l64(inp), tgt).backward()
+        return [np.asarray(p.grad.detach().numpy(), np.float64).copy()]
+    return truth
+
+
 def _fused_truth(block, spy, lmda, iters, batch_size=32):
     """The reference's own fused-loop gradient of iteration `step`, evaluated in float64 at
     the parameters the fp32 run holds there (same batch, same loss schedule): the exact
@@ -610,7 +633,8 @@ def gen_recon_layer_shift(iters=20, n_cali=16, res=16):
            "cached_inp": t2n(torch.cat(m.cached_inp_features)),
            "cached_out": t2n(torch.cat(m.cached_out_features))}
     torch.manual_seed(1005)
-    with _Spy(LRS.ScaleLossFunction) as spy, _GradSpy((0, 5, iters - 1)) as gspy:
+    with _Spy(LRS.ScaleLossFunction) as spy, \
+            _GradSpy((0, 5, iters - 1), _layer_truth(m, spy, 0.1, iters, False)) as gspy:
         l1 = LRS.layer_recon_shiftedScale(m, iters, 0.1, qnn, None)
     gspy.dump(out, "shift_")
     out["shift_perms"] = np.stack([p.numpy() for p in spy.perms]).astype(np.int64)
@@ -620,7 +644,8 @@ def gen_recon_layer_shift(iters=20, n_cali=16, res=16):
     out["shift_alpha"] = t2n(m.weight_quantizer.alpha)
     out["shift_xq"] = np.stack([t2n(t) for t in m.weight_quantizer.x_q])
     m.weight_quantizer.hard_targets = False
-    with _Spy(LRS.ScaleLossFunction) as spy, _GradSpy((0, 5, iters - 1)) as gspy:
+    with _Spy(LRS.ScaleLossFunction) as spy, \
+            _GradSpy((0, 5, iters - 1), _layer_truth(m, spy, 0.01, iters, True)) as gspy:
         l2 = LRS.layer_recon_shiftedScale(m, iters, 0.01, qnn, None, adaround=True)
     gspy.dump(out, "ar_")
     out["ar_perms"] = np.stack([p.numpy() for p in spy.perms]).astype(np.int64)
