@@ -124,13 +124,16 @@ def validate_model(val_loader, model, device=None, print_result=False):
     all-reduced (Brecq/main_imagenet_dist.py:114-124), so every rank returns the
     whole-set top-1."""
     from .parallel_dp import all_sum_
+    from .quant.quant_layer import frozen_weight_cache
     device = next(model.parameters()).device if device is None else device
     model.eval()
     sums = torch.zeros(2, dtype=torch.float64, device=device)
-    for images, target in val_loader:
-        out = model(images.to(device))
-        sums[0] += (out.argmax(1) == target.to(device)).sum()
-        sums[1] += target.numel()
+    # every layer's W_hat is quantized once per pass, not once per batch (bit-identical)
+    with frozen_weight_cache():
+        for images, target in val_loader:
+            out = model(images.to(device))
+            sums[0] += (out.argmax(1) == target.to(device)).sum()
+            sums[1] += target.numel()
     all_sum_(sums)
     correct, total = sums.tolist()
     acc = 100.0 * correct / max(total, 1)

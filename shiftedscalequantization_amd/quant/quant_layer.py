@@ -9,6 +9,7 @@ reference; the arithmetic runs in the HIP kernels of libssq.so:
 Feature caching keeps tensors on the device by default (the reference moves every batch
 to the host with .cpu(); quant_layer.py:247,278) -- identical values, no PCIe round trip.
 """
+import contextlib
 from typing import Union
 
 import torch
@@ -16,6 +17,25 @@ import torch.nn as nn
 import torch.nn.functional as F
 
 from .. import kernels as K
+
+# Frozen-weight cache of a validation pass (frozen_weight_cache): module -> (key, W_hat).
+_FROZEN_W = None
+
+
+@contextlib.contextmanager
+def frozen_weight_cache():
+    """Inside this context, under torch.no_grad, every QuantModule quantizes its weight once
+    and reuses that W_hat for the rest of the context.  validate_model (common.py:152-221)
+    runs the whole pass in it: no quantizer changes during inference, so each batch's
+    forward is bit-identical to recomputing W_hat, without the per-batch weight q/dq
+    launches.  The cache is keyed on the module, its weight quantizer object and the weight
+    tensor (identity and version), and is dropped when the context exits."""
+    global _FROZEN_W
+    prev, _FROZEN_W = _FROZEN_W, {}
+    try:
+        yield
+    finally:
+        _FROZEN_W = prev
 
 
 class StraightThrough(nn.Module):
@@ -219,7 +239,15 @@ class QuantModule(nn.Module):
 
     def _weight_bias(self):
         if self.use_weight_quant and self.cache_features == 'none':
-            weight = self.weight_quantizer(self.weight)
+            if _FROZEN_W is not None and not torch.is_grad_enabled():
+                key = (id(self.weight_quantizer), id(self.weight), self.weight._version)
+                hit = _FROZEN_W.get(self)
+                if hit is None or hit[0] != key:
+                    hit = (key, self.weight_quantizer(self.weight))
+                    _FROZEN_W[self] = hit
+                weight = hit[1]
+            else:
+                weight = self.weight_quantizer(self.weight)
             # no reconstruction ever optimises the conv bias: its gradient (a full
             # reduction over N,H,W per launch) is not requested
             bias = self.bias if (self.bias is None or self.train_bias) else self.bias.detach()

@@ -4,7 +4,8 @@ The reference validates its calibrated network with `common.validate_model`
 (common.py:152-221): a plain forward of the QuantModel with weights and activations
 fake-quantized.  Here that forward is MIOpen's conv + the fused K13 epilogue (bias,
 residual, ReLU and the A4 activation q/dq in one pass, `ssq_bias_act_fq`) + the W2/W8
-per-channel weight q/dq (K1) of every layer, under torch.no_grad.
+per-channel weight q/dq (K1) of every layer, under torch.no_grad; as in validate_model, each
+layer's W_hat is quantized once per validation pass (quant_layer.frozen_weight_cache).
 
 Workload: ResNet-18 (random init), weights UAQ 'mse' per channel W2 (8-bit stem/head), act
 UAQ 'mse' A4 initialised on 32 synthetic images, network output unquantized
@@ -18,6 +19,7 @@ import time
 import torch
 
 from .drivers import build_qnn
+from .quant.quant_layer import frozen_weight_cache
 
 
 def run_validate_bench(dev, world, rank, batch=128, iters=20, warmup=3):
@@ -33,8 +35,11 @@ def run_validate_bench(dev, world, rank, batch=128, iters=20, warmup=3):
             qnn(imgs)
         torch.cuda.synchronize(dev)
         t0 = time.perf_counter()
-        for _ in range(iters):
-            qnn(imgs)
+        # as validate_model: one pass = one frozen-weight cache, its first batch (inside the
+        # timed region) quantizes every weight
+        with frozen_weight_cache():
+            for _ in range(iters):
+                qnn(imgs)
         torch.cuda.synchronize(dev)
         el = time.perf_counter() - t0
     per_rank = batch * iters / el

@@ -412,3 +412,38 @@ def test_w2a4_validation_matches_reference(Q):
             assert v <= 1e-6, (k, v)
     assert stats["logits_rel_err"] <= 1e-5
     assert top1 == pytest.approx(float(g["top1"][0]), abs=1e-9)
+
+
+def test_frozen_weight_cache_bit_identical(Q):
+    """(f3) validate_model's frozen-weight cache: each layer's weight quantizer runs once per
+    pass (not once per batch) and every batch's logits equal the recomputing forward bit for
+    bit; leaving the context drops the cache, and a weight edit inside it re-quantizes."""
+    from shiftedscalequantization_amd.quant import quant_layer as QL
+    g = np.load(os.path.join(os.path.dirname(__file__), "golden", "validate_w2a4.npz"))
+    qnn = tiny_net2(Q, g)
+    qnn.set_quant_state(True, True)
+    with torch.no_grad():
+        qnn(dev(g["cali"])[:8])
+    qnn.disable_network_output_quantization()
+    batches = [x for x, _ in _val_loader(g)]
+    with torch.no_grad():
+        ref = [qnn(x).clone() for x in batches]
+    qms = [m for m in qnn.modules() if isinstance(m, Q.QuantModule) and m.use_weight_quant]
+    calls = {id(m): 0 for m in qms}
+    hooks = [m.weight_quantizer.register_forward_hook(
+        lambda mod, i, o, k=id(m): calls.__setitem__(k, calls[k] + 1)) for m in qms]
+    try:
+        with torch.no_grad(), QL.frozen_weight_cache():
+            got = [qnn(x).clone() for x in batches]
+            assert all(v == 1 for v in calls.values()), calls
+            with torch.no_grad():
+                qms[0].weight.mul_(1.0)          # version bump: that layer re-quantizes
+            qnn(batches[0])
+            assert calls[id(qms[0])] == 2 and all(calls[id(m)] == 1 for m in qms[1:])
+        assert QL._FROZEN_W is None
+    finally:
+        for h in hooks:
+            h.remove()
+    assert len(batches) >= 2
+    for a, b in zip(ref, got):
+        assert torch.equal(a, b)
