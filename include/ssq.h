@@ -4,7 +4,8 @@
  * memory owned by the caller (PyTorch's caching allocator in the Python host layer),
  * borrowed for the duration of the call.  Launches are asynchronous on `stream`
  * (a hipStream_t passed as void*); no entry point allocates or synchronizes, and none
- * keeps state except the opt-in deferred-finalize queue (ssq_set_deferred_finalize), so
+ * keeps state except the opt-in deferred-finalize queue (ssq_set_deferred_finalize) and
+ * the opt-in deferred prepared forward (ssq_set_deferred_prep_fwd), so
  * every call is graph-capturable.
  *
  * Return value: 0 on success; a negative SSQ_E* code for an argument error; otherwise
@@ -368,6 +369,19 @@ int ssq_adam(int nseg, float* const* p, const float* const* g, float* const* m,
  * deferral off. */
 int ssq_set_deferred_finalize(int on);
 int ssq_flush_finalize(ssq_stream_t stream);
+
+/* ---------------------------------------------------------------- deferred prepared forward
+ * The fused loop's iteration start in one launch (csrc/prep_ride.h).  With this deferral on,
+ * ssq_adashift_fwd_prepared_multi (<= 8 segments) does not launch: it queues its table on
+ * its stream, and the next ssq_gather_rows2 on that stream runs it in extra workgroups of
+ * the gather launch (same code: bit-identical What).  One table is queued at a time (a second
+ * call launches the first); ssq_flush_prep_fwd launches a table still queued on `stream`.
+ * The caller must not read the queued What before that gather or flush.  Host state, not
+ * thread-safe; ssq_set_deferred_prep_fwd returns the previous setting and launches nothing
+ * (flush before turning it off).  Replaces nothing in the reference: the iteration start of
+ * layer_recon_fused_shiftedScale.py:80-92 (batch draw, then the quantized forward). */
+int ssq_set_deferred_prep_fwd(int on);
+int ssq_flush_prep_fwd(ssq_stream_t stream);
 
 /* ---------------------------------------------------------------- K17 conv weight gradient
  * Deterministic fp32 conv weight gradient (NCHW, dilation 1) on the fp32 matrix cores:

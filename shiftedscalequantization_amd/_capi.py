@@ -82,6 +82,8 @@ SIGNATURES = {
     "ssq_adam": (_i, [_i, _p, _p, _p, _p, _p, _f, _f, _f, _f, _p, _f, _f, _p]),
     "ssq_set_deferred_finalize": (_i, [_i]),
     "ssq_flush_finalize": (_i, [_p]),
+    "ssq_set_deferred_prep_fwd": (_i, [_i]),
+    "ssq_flush_prep_fwd": (_i, [_p]),
     "ssq_conv_wgrad_set_form": (_i, [_i]),
     "ssq_conv_wgrad_kind": (_i, [_i64] * 10),
     "ssq_conv_wgrad_workspace_size": (_sz, [_i64] * 10),

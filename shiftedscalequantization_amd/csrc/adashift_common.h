@@ -133,7 +133,8 @@ static inline int make_shifts(const float* shifts, int S, Shifts& sh) {
 // deterministic, no atomics.
 struct ColTiling {
   uint32_t ncb, ncolblk, R, nchunk, threads;
-  uint32_t whole;   // prepared alpha backward: whole-column workgroups, no second stage
+  uint32_t whole;   // prepared alpha backward: one chunk, finalised in the workgroup
+  uint32_t form;    // prepared alpha backward: 0 thread-column (+ stage 2), 1 wave-column
 };
 constexpr uint32_t kMaxChunks = 256;  // stage 2: lane c sums chunks c, c+64, ... in order
 
@@ -153,6 +154,7 @@ static inline ColTiling col_tiling(const Geo& g, uint32_t max_chunks = kMaxChunk
   t.R = (g.Co + want - 1) / want;
   t.nchunk = (g.Co + t.R - 1) / t.R;
   t.whole = 0;
+  t.form = 0;
   return t;
 }
 static inline size_t col_ws_bytes(const Geo& g, int S) {

@@ -10,28 +10,26 @@
 // fpack + hterm (+ gWhat) with no divide and no exp per element -- 12 B/elem forward
 // (fpack, hterm in; What out) and 12 B/elem backward (gWhat, fpack, hterm in), the §8(d)
 // algorithmic bytes -- and produce bit-identical What / identical gradients.  The alpha
-// backward is two fixed-order launches (chunk partials, then one wave per input channel).
-// Its one-launch form (SSQ_ALPHA_ONE_LAUNCH=1: partials handed off write-through, reduced
-// by the last workgroup of each column block, arrive_last) is bit-identical but slower on
-// every ResNet-18 shape (profiles/r2_alpha_one_launch_ab.log).
+// backward is one launch for weights with Co <= 64 (bwd_tiling_prep: whole-column
+// workgroups that finalise their input channels) and two fixed-order launches otherwise
+// (chunk partials, then one wave per input channel).  Both kernels are latency-bound at
+// ResNet-18 sizes, so the loads a thread needs are issued before their first use.
 //
 // Every kernel takes a table of up to kMaxPrepSeg weights ("segments"), so the adaShift
-// forward of ALL the convs of a block is one launch and their alpha backward two: the
+// forward of ALL the convs of a block is one launch and their alpha backward one: the
 // weights of a block depend only on alpha, which is fixed for the iteration
 // (quant/_engine.py stash_block_weights).
 #include <stdlib.h>
 
 #include "adashift_common.h"
 #include "fin_tasks.h"
+#include "prep_ride.h"
 
 namespace ssq {
 
 constexpr int kMaxPrepS = 4;
 constexpr int kRBP = 8;            // rows per load batch
 constexpr int kMaxPrepSeg = 8;     // weights per launch (a block has <= 4 convs)
-// last-arriver counters of the one-launch alpha backward: one per (segment, column block)
-constexpr uint32_t kAlphaTickets = 8192;
-__device__ unsigned g_alpha_tickets[kAlphaTickets];
 
 __global__ __launch_bounds__(kBlock) void adashift_prepare_kernel(
     const float* __restrict__ W, const float* __restrict__ beta, const float* __restrict__ delta,
@@ -86,39 +84,38 @@ static ColTiling col_tiling_prep(const Geo& g) {
   t.R = (g.Co + want - 1) / want;
   t.nchunk = (g.Co + t.R - 1) / t.R;
   t.whole = 0;
+  t.form = 0;
   return t;
 }
 
-// Alpha-backward tiling.  Small weights (Co <= SSQ_PREP_WHOLE_CO, default 64, and
-// K <= 64) take the whole-column form: a workgroup owns floor(64/K) whole input channels
-// (one wave-width of columns) over ALL Co rows, its 4 waves taking rows co = w (mod 4), so
-// each input channel's sum is complete inside the workgroup and is finalised there (a
-// fixed-order LDS sum, then the softmax/clamp backward): one launch, no partials.
-// Measured (tools/adashift_bench.py --blocks, profiles/r2_alpha_whole_ab.log): ResNet-18
-// layer1 (Co 64) 9.4 -> 8.2 us; at Co 128 it is slower (9.3 -> 10.1, 32 rows per thread
-// in series) and at Co 256 much slower, so larger weights keep the chunked two-launch
-// form, whose stage 1 spreads rows over the chip.  Both forms are dependent-latency
-// chains (alpha row, row batches, LDS sum, regulariser, store), not bandwidth.  Depends only on the weight's own shape, so a multi-segment launch gives each
-// weight its single-launch bits.
+// Alpha-backward tiling.  Weights with K <= 64 and Co <= 64 (ResNet-18 layer1, the
+// ResNet-50 layer1 convs, ...) take the whole-column wave-column form (alpha_bwd_wavecol):
+// a workgroup owns one wave-width of columns -- cw = floor(64/K) whole input channels, i.e.
+// cw*K <= 64 contiguous columns of every row -- over ALL rows, its 4 waves taking rows
+// w, w + 4, ... (<= kWR each), and finalises its channels: one launch, no partials.
+// Larger weights keep the thread-column tiling of the forward (chunks of rows) and a
+// stage-2 launch that sums the chunk partials.  Measured and not kept
+// (tools/alpha_cold.py, profiles/r3_alpha_variants.txt): the wave-column form with row
+// chunks is ~1 us slower than the thread-column stage 1 on layer2-4, and handing its chunk
+// partials to the last-arriving chunk of each column group (one launch, no stage 2) costs
+// 6-13 us more than the stage-2 launch it saves: every chunk waits for its write-through
+// partials and a device-scope ticket atomic before its workgroup retires.  The tiling
+// depends only on the weight's own shape, so a multi-segment launch gives each weight its
+// single-launch bits.
+constexpr uint32_t kWR = 16;   // rows per wave (whole form: Co <= 4 * kWR = 64)
 static ColTiling bwd_tiling_prep(const Geo& g) {
-  static const uint32_t kWholeCo = prep_env("SSQ_PREP_WHOLE_CO", 64);
-  if (g.Co <= kWholeCo && g.K <= (uint32_t)kWave) {
-    ColTiling t;
-    t.ncb = (uint32_t)kWave / g.K;
-    if (t.ncb > g.Ci) t.ncb = g.Ci;
-    t.ncolblk = (g.Ci + t.ncb - 1) / t.ncb;
-    t.threads = kBlock;
-    t.R = g.Co;
-    t.nchunk = 1;
-    t.whole = 1;
-    return t;
-  }
-  return col_tiling_prep(g);
-}
-
-static bool alpha_one_launch() {
-  static const bool on = prep_env("SSQ_ALPHA_ONE_LAUNCH", 0) != 0;
-  return on;
+  constexpr uint32_t kMaxR = (kBlock / kWave) * kWR;
+  if (g.K > (uint32_t)kWave || g.Co > kMaxR) return col_tiling_prep(g);
+  ColTiling t;
+  t.form = 1;
+  t.threads = kBlock;
+  t.ncb = (uint32_t)kWave / g.K;
+  if (t.ncb > g.Ci) t.ncb = g.Ci;
+  t.ncolblk = (g.Ci + t.ncb - 1) / t.ncb;
+  t.R = g.Co;
+  t.nchunk = 1;
+  t.whole = 1;
+  return t;
 }
 
 struct PrepSeg {
@@ -136,7 +133,7 @@ struct PrepSeg {
   ColTiling tl;
   uint32_t blk0;     // first workgroup of this segment (forward / stage 1)
   uint32_t wave0;    // first wave of this segment (stage 2: one wave per input channel)
-  uint32_t tick0;    // first last-arriver counter of this segment (one-launch form)
+  uint32_t stage2;   // its chunks are reduced by the stage-2 launch
   float lo, hi;
 };
 struct PrepTable {
@@ -153,21 +150,21 @@ __device__ __forceinline__ int find_seg(const PrepTable& tab, uint32_t id) {
   return si;
 }
 
+// Forward: thread t of the workgroup owns column j = ci0*K + t of the chunk's rows.  Every
+// load is in flight before any math: the alpha row first (loads retire in order, so its
+// wait leaves the rows in flight), then the first row batch; each later batch is fetched
+// before the current one is stored.
 template <int NS, int HARD_T>
-__global__ __launch_bounds__(kBlock) void shift_fwd_prep(PrepTable tab) {
-  const PrepSeg& sg = tab.s[find_seg<false>(tab, blockIdx.x)];
+__device__ __forceinline__ void shift_fwd_body(const PrepTable& tab, uint32_t bid) {
+  const PrepSeg& sg = tab.s[find_seg<false>(tab, bid)];
   const Geo& g = sg.g;
-  const uint32_t local = blockIdx.x - sg.blk0;
+  const uint32_t local = bid - sg.blk0;
   const uint32_t bx = local % sg.tl.ncolblk, by = local / sg.tl.ncolblk;
   const uint32_t ci0 = bx * sg.tl.ncb;
   const uint32_t nci = min(sg.tl.ncb, g.Ci - ci0);
   const uint32_t t = threadIdx.x;
   if (t >= nci * g.K) return;
   const uint32_t ci = ci0 + t / g.K, j = ci0 * g.K + t;
-  float a[kMaxS], p[kMaxS];
-  load_row(sg.alpha, ci, NS, a);
-  soft_targets<kMaxS>(a, NS, nullptr, p);
-  const int sel = argmax_first(p, NS);
   const uint32_t co0 = by * sg.tl.R, co1 = min(co0 + sg.tl.R, g.Co);
   const uint32_t* __restrict__ fpack = sg.fpack;
   const float* __restrict__ hterm = sg.hterm;
@@ -175,155 +172,100 @@ __global__ __launch_bounds__(kBlock) void shift_fwd_prep(PrepTable tab) {
   const float* __restrict__ zp = sg.zp;
   float* __restrict__ What = sg.What;
   const float lo = sg.lo, hi = sg.hi;
-  auto one = [&](uint32_t co, uint32_t fw, float h, float d, float z) {
-    float xf;
-    if (HARD_T) {
-      xf = unpack_floor(fw, sel);
-    } else {
-      xf = __fmul_rn(unpack_floor(fw, 0), p[0]);
-#pragma unroll
-      for (int i = 1; i < NS; ++i) xf = __fadd_rn(xf, __fmul_rn(unpack_floor(fw, i), p[i]));
-    }
-    const float q = clampf(__fadd_rn(__fadd_rn(xf, h), z), lo, hi);
-    What[co * g.CiK + j] = __fmul_rn(__fsub_rn(q, z), __fmul_rn(d, 1.0f));
-  };
-  uint32_t co = co0;
-  for (; co + kRBP <= co1; co += kRBP) {
-    uint32_t fw[kRBP];
-    float h[kRBP], d[kRBP], z[kRBP];
+  float a[kMaxS];
+  load_row(sg.alpha, ci, NS, a);
+  uint32_t fw[kRBP];
+  float h[kRBP], d[kRBP], z[kRBP];
+  auto fetch = [&](uint32_t c) {
 #pragma unroll
     for (int r = 0; r < kRBP; ++r) {
-      const uint32_t e = (co + r) * g.CiK + j;
-      fw[r] = fpack[e];
-      h[r] = hterm[e];
-      d[r] = delta[co + r];
-      z[r] = zp[co + r];
+      fw[r] = 0u;
+      h[r] = d[r] = z[r] = 0.0f;
+      if (c + r < co1) {
+        const uint32_t e = (c + r) * g.CiK + j;
+        fw[r] = fpack[e];
+        h[r] = hterm[e];
+        d[r] = delta[c + r];
+        z[r] = zp[c + r];
+      }
     }
+  };
+  fetch(co0);
+  float p[kMaxS];
+  soft_targets<kMaxS>(a, NS, nullptr, p);
+  const int sel = argmax_first(p, NS);
+  for (uint32_t co = co0; co < co1; co += kRBP) {
+    float o[kRBP];
 #pragma unroll
-    for (int r = 0; r < kRBP; ++r) one(co + r, fw[r], h[r], d[r], z[r]);
-  }
-  for (; co < co1; ++co) {
-    const uint32_t e = co * g.CiK + j;
-    one(co, fpack[e], hterm[e], delta[co], zp[co]);
+    for (int r = 0; r < kRBP; ++r) {
+      float xf;
+      if (HARD_T) {
+        xf = unpack_floor(fw[r], sel);
+      } else {
+        xf = __fmul_rn(unpack_floor(fw[r], 0), p[0]);
+#pragma unroll
+        for (int i = 1; i < NS; ++i) xf = __fadd_rn(xf, __fmul_rn(unpack_floor(fw[r], i), p[i]));
+      }
+      const float q = clampf(__fadd_rn(__fadd_rn(xf, h[r]), z[r]), lo, hi);
+      o[r] = __fmul_rn(__fsub_rn(q, z[r]), __fmul_rn(d[r], 1.0f));
+    }
+    if (co + kRBP < co1) fetch(co + kRBP);
+#pragma unroll
+    for (int r = 0; r < kRBP; ++r)
+      if (co + r < co1) What[(co + r) * g.CiK + j] = o[r];
   }
 }
 
-// Whole-column alpha backward (bwd_tiling_prep): workgroup `local` of the segment owns
-// input channels [ci0, ci0 + nci); lane l of wave w sums column ci0*K + l over rows
-// co = w, w + 4, ...; the 4 x K partials of an input channel are added in fixed order
-// (waves per column, then taps) and lane t < nci of wave 0 finalises channel ci0 + t as
-// alpha_reduce_ci's lane 0 does (regulariser terms in shift order, softmax/clamp backward).
+template <int NS, int HARD_T>
+__global__ __launch_bounds__(kBlock) void shift_fwd_prep(PrepTable tab) {
+  shift_fwd_body<NS, HARD_T>(tab, blockIdx.x);
+}
+
+// The iteration start (prep_ride.h): workgroups [0, ngw) gather the batch rows, the rest
+// run the queued prepared forward.
+template <bool VEC, int NS, int HARD_T>
+__global__ __launch_bounds__(kBlock) void gather_shift_fwd(GatherArgs ga, uint32_t ngw,
+                                                           PrepTable tab) {
+  if (blockIdx.x < ngw) {
+    gather2_body<VEC>(ga, blockIdx.x % ga.gx, blockIdx.x / ga.gx);
+    return;
+  }
+  shift_fwd_body<NS, HARD_T>(tab, blockIdx.x - ngw);
+}
+
+template <bool VEC>
+__global__ __launch_bounds__(kBlock) void gather2_kernel(GatherArgs ga) {
+  gather2_body<VEC>(ga, blockIdx.x, blockIdx.y);
+}
+
+// d/dalpha of one weight element: the unclamped rounding u = sum_i F_i p_i + h + zp passes
+// the clamp's gradient (inclusive bounds) and contributes g_int * F_i to shift i's sum.
 template <int NS>
-__device__ __forceinline__ void alpha_bwd_whole(const PrepSeg& sg, uint32_t local, double* red,
-                                                float reg_lambda, float reg_b,
-                                                const float* __restrict__ reg_dev) {
-  const Geo& g = sg.g;
-  const uint32_t ci0 = local * sg.tl.ncb;
-  const uint32_t nci = min(sg.tl.ncb, g.Ci - ci0);
-  const uint32_t w = threadIdx.x / kWave, lane = threadIdx.x & (kWave - 1);
-  constexpr uint32_t kW = kBlock / kWave;
-  double acc[NS];
+__device__ __forceinline__ void alpha_accumulate(uint32_t fw, float h, float d, float z, float gy,
+                                                 const float* p, float lo, float hi,
+                                                 double* acc) {
+  float F[NS];
 #pragma unroll
-  for (int i = 0; i < NS; ++i) acc[i] = 0.0;
-  if (lane < nci * g.K) {
-    const uint32_t ci = ci0 + lane / g.K, j = ci0 * g.K + lane;
-    float a[kMaxS], p[kMaxS];
-    load_row(sg.alpha, ci, NS, a);
-    soft_targets<kMaxS>(a, NS, nullptr, p);
-    const uint32_t* __restrict__ fpack = sg.fpack;
-    const float* __restrict__ hterm = sg.hterm;
-    const float* __restrict__ gWhat = sg.gWhat;
-    const float* __restrict__ delta = sg.delta;
-    const float* __restrict__ zp = sg.zp;
-    const float lo = sg.lo, hi = sg.hi;
-    auto one = [&](uint32_t fw, float h, float d, float z, float gy) {
-      float F[NS];
+  for (int i = 0; i < NS; ++i) F[i] = unpack_floor(fw, i);
+  float xf = __fmul_rn(F[0], p[0]);
 #pragma unroll
-      for (int i = 0; i < NS; ++i) F[i] = unpack_floor(fw, i);
-      float xf = __fmul_rn(F[0], p[0]);
+  for (int i = 1; i < NS; ++i) xf = __fadd_rn(xf, __fmul_rn(F[i], p[i]));
+  const float u = __fadd_rn(__fadd_rn(xf, h), z);
+  const float gi = (u >= lo && u <= hi) ? __fmul_rn(gy, __fmul_rn(d, 1.0f)) : 0.0f;
 #pragma unroll
-      for (int i = 1; i < NS; ++i) xf = __fadd_rn(xf, __fmul_rn(F[i], p[i]));
-      const float u = __fadd_rn(__fadd_rn(xf, h), z);
-      const float gi = (u >= lo && u <= hi) ? __fmul_rn(gy, __fmul_rn(d, 1.0f)) : 0.0f;
-#pragma unroll
-      for (int i = 0; i < NS; ++i) acc[i] += (double)gi * (double)F[i];
-    };
-    uint32_t co = w;
-    for (; co + kW * (kRBP - 1) < g.Co; co += kW * kRBP) {
-      uint32_t fw[kRBP];
-      float h[kRBP], d[kRBP], z[kRBP], gy[kRBP];
-#pragma unroll
-      for (int r = 0; r < kRBP; ++r) {
-        const uint32_t c = co + kW * r;
-        const uint32_t e = c * g.CiK + j;
-        fw[r] = fpack[e];
-        h[r] = hterm[e];
-        gy[r] = gWhat[e];
-        d[r] = delta[c];
-        z[r] = zp[c];
-      }
-#pragma unroll
-      for (int r = 0; r < kRBP; ++r) one(fw[r], h[r], d[r], z[r], gy[r]);
-    }
-    for (; co < g.Co; co += kW) {
-      const uint32_t e = co * g.CiK + j;
-      one(fpack[e], hterm[e], delta[co], zp[co], gWhat[e]);
-    }
-  }
-#pragma unroll
-  for (int i = 0; i < NS; ++i) red[threadIdx.x * NS + i] = acc[i];
-  __syncthreads();
-  if (w != 0) return;
-  // wave 0: lane l adds column l's 4 wave partials (all loads in flight at once), then
-  // lane t < nci adds its input channel's K columns; both in fixed order
-  {
-    double v[kW][NS];
-#pragma unroll
-    for (uint32_t ww = 0; ww < kW; ++ww)
-#pragma unroll
-      for (int i = 0; i < NS; ++i) v[ww][i] = red[(ww * kWave + lane) * NS + i];
-#pragma unroll
-    for (int i = 0; i < NS; ++i) {
-      double c = v[0][i];
-#pragma unroll
-      for (uint32_t ww = 1; ww < kW; ++ww) c += v[ww][i];
-      red[lane * NS + i] = c;
-    }
-  }
-  __builtin_amdgcn_wave_barrier();
-  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
-  if (lane >= nci) return;
-  const uint32_t t = lane, ci = ci0 + t;
+  for (int i = 0; i < NS; ++i) acc[i] += (double)gi * (double)F[i];
+}
+
+// Input channel ci's alpha gradient from its summed d/dp (tot): the shift regulariser's
+// terms in shift order (value and gradient), then the softmax/clamp backward -- the same
+// values in the same order as alpha_chain.
+template <int NS>
+__device__ __forceinline__ void alpha_finalize(const PrepSeg& sg, uint32_t ci, const float* a,
+                                               const double* tot_in, float reg_lambda,
+                                               float reg_b) {
   double tot[kMaxS];
-  constexpr uint32_t kUnK = 9;   // 3x3 taps unrolled (loads issued together); others loop
-  if (g.K <= kUnK) {
-    double v[kUnK][NS];
 #pragma unroll
-    for (uint32_t k = 0; k < kUnK; ++k)
-#pragma unroll
-      for (int i = 0; i < NS; ++i) v[k][i] = k < g.K ? red[(t * g.K + k) * NS + i] : 0.0;
-#pragma unroll
-    for (int i = 0; i < NS; ++i) {
-      double sum = v[0][i];
-#pragma unroll
-      for (uint32_t k = 1; k < kUnK; ++k)
-        if (k < g.K) sum += v[k][i];
-      tot[i] = sum;
-    }
-  } else {
-#pragma unroll
-    for (int i = 0; i < NS; ++i) {
-      double sum = 0.0;
-      for (uint32_t k = 0; k < g.K; ++k) sum += red[(t * g.K + k) * NS + i];
-      tot[i] = sum;
-    }
-  }
-  float a[kMaxS];
-  load_row(sg.alpha, ci, NS, a);
-  if (reg_dev) {
-    reg_lambda = reg_dev[0];
-    reg_b = reg_dev[1];
-  }
+  for (int i = 0; i < NS; ++i) tot[i] = tot_in[i];
   float sm[kMaxS], p[kMaxS], ga[kMaxS];
   soft_targets<kMaxS>(a, NS, sm, p);
   float reg = 0.0f;
@@ -344,9 +286,127 @@ __device__ __forceinline__ void alpha_bwd_whole(const PrepSeg& sg, uint32_t loca
   if (sg.reg_vals) sg.reg_vals[ci] = reg;
 }
 
-// Backward stage 1: sums of g_int * F_i per (chunk, ci) into
+// Wave-column alpha backward (bwd_tiling_prep form 1, Co <= 64).  Lane l of wave w owns
+// column j = ci0*K + l of rows w + 4r; every load of the lane is issued before any math
+// (the alpha row, delta / zp -- one row per lane, broadcast with readlane -- and the wave's
+// <= kWR rows of gW^, packed floors and h(beta)).  The 4 x K partials of an input channel
+// are then added in fixed order (waves per column, then taps) and lane t < nci of wave 0
+// finalises channel ci0 + t.
+template <int NS>
+__device__ __forceinline__ void alpha_bwd_wavecol(const PrepSeg& sg, uint32_t local, double* red,
+                                                  float reg_lambda, float reg_b,
+                                                  const float* __restrict__ reg_dev) {
+  const Geo& g = sg.g;
+  constexpr uint32_t kW = kBlock / kWave;
+  const uint32_t ci0 = local * sg.tl.ncb, nci = min(sg.tl.ncb, g.Ci - ci0);
+  const uint32_t w = __builtin_amdgcn_readfirstlane(threadIdx.x / kWave);
+  const uint32_t lane = threadIdx.x & (kWave - 1);
+  const uint32_t co0 = 0, co1 = g.Co;
+  const bool col = lane < nci * g.K;
+  const uint32_t ci = ci0 + (col ? lane / g.K : 0u), j = ci0 * g.K + lane;
+  const uint32_t* __restrict__ fpack = sg.fpack;
+  const float* __restrict__ hterm = sg.hterm;
+  const float* __restrict__ gWhat = sg.gWhat;
+  const float lo = sg.lo, hi = sg.hi;
+  float a[kMaxS], af[kMaxS];
+  load_row(sg.alpha, ci, NS, a);
+  const bool fin_lane = w == 0 && lane < nci;
+  if (fin_lane) load_row(sg.alpha, ci0 + lane, NS, af);
+  if (reg_dev) {
+    reg_lambda = reg_dev[0];
+    reg_b = reg_dev[1];
+  }
+  float dl = 0.0f, zl = 0.0f;
+  if (co0 + lane < co1) {
+    dl = sg.delta[co0 + lane];
+    zl = sg.zp[co0 + lane];
+  }
+  uint32_t fw[kWR];
+  float h[kWR], gy[kWR];
+#pragma unroll
+  for (uint32_t r = 0; r < kWR; ++r) {
+    fw[r] = 0u;
+    h[r] = gy[r] = 0.0f;
+    const uint32_t c = co0 + w + kW * r;
+    if (col && c < co1) {
+      const uint32_t e = c * g.CiK + j;
+      fw[r] = fpack[e];
+      h[r] = hterm[e];
+      gy[r] = gWhat[e];
+    }
+  }
+  // no divergent branch around the rows: readlane must see every lane's delta / zp (lanes
+  // past the columns hold zero rows and add nothing; their slots are never read)
+  double acc[NS];
+#pragma unroll
+  for (int i = 0; i < NS; ++i) acc[i] = 0.0;
+  float p[kMaxS];
+  soft_targets<kMaxS>(a, NS, nullptr, p);
+#pragma unroll
+  for (uint32_t r = 0; r < kWR; ++r) {
+    const uint32_t rl = w + kW * r;      // row within the chunk (wave-uniform)
+    if (co0 + rl < co1) {
+      const float d = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(dl), rl));
+      const float z = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(zl), rl));
+      alpha_accumulate<NS>(fw[r], h[r], d, z, gy[r], p, lo, hi, acc);
+    }
+  }
+#pragma unroll
+  for (int i = 0; i < NS; ++i) red[threadIdx.x * NS + i] = acc[i];
+  __syncthreads();
+  double tot[kMaxS];
+#pragma unroll
+  for (int i = 0; i < NS; ++i) tot[i] = 0.0;
+  if (w == 0) {
+    // lane l adds column l's 4 wave partials (all loads first), then lane t < nci adds its
+    // input channel's K columns; both in fixed order
+    double v[kW][NS];
+#pragma unroll
+    for (uint32_t ww = 0; ww < kW; ++ww)
+#pragma unroll
+      for (int i = 0; i < NS; ++i) v[ww][i] = red[(ww * kWave + lane) * NS + i];
+#pragma unroll
+    for (int i = 0; i < NS; ++i) {
+      double c = v[0][i];
+#pragma unroll
+      for (uint32_t ww = 1; ww < kW; ++ww) c += v[ww][i];
+      red[lane * NS + i] = c;
+    }
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+    if (lane < nci) {
+      constexpr uint32_t kUnK = 9;   // 3x3 taps unrolled (loads issued together); others loop
+      if (g.K <= kUnK) {
+        double vk[kUnK][NS];
+#pragma unroll
+        for (uint32_t k = 0; k < kUnK; ++k)
+#pragma unroll
+          for (int i = 0; i < NS; ++i) vk[k][i] = k < g.K ? red[(lane * g.K + k) * NS + i] : 0.0;
+#pragma unroll
+        for (int i = 0; i < NS; ++i) {
+          double sum = vk[0][i];
+#pragma unroll
+          for (uint32_t k = 1; k < kUnK; ++k)
+            if (k < g.K) sum += vk[k][i];
+          tot[i] = sum;
+        }
+      } else {
+#pragma unroll
+        for (int i = 0; i < NS; ++i) {
+          double sum = 0.0;
+          for (uint32_t k = 0; k < g.K; ++k) sum += red[(lane * g.K + k) * NS + i];
+          tot[i] = sum;
+        }
+      }
+    }
+  }
+  if (fin_lane) alpha_finalize<NS>(sg, ci0 + lane, af, tot, reg_lambda, reg_b);
+}
+
+// Backward, one launch for every segment: wave-column segments finish here; the
+// thread-column stage 1 of the others writes sums of g_int * F_i per (chunk, ci) into
 // part[(ci*nchunk + chunk)*S + i] (input-channel-major: stage 2 reads one coalesced run).
-template <int NS, bool FUSED>
+template <int NS>
 __global__ __launch_bounds__(kBlock) void alpha_bwd_prep(PrepTable tab, float reg_lambda,
                                                           float reg_b,
                                                           const float* __restrict__ reg_dev,
@@ -359,8 +419,8 @@ __global__ __launch_bounds__(kBlock) void alpha_bwd_prep(PrepTable tab, float re
   const PrepSeg& sg = tab.s[find_seg<false>(tab, blockIdx.x)];
   const Geo& g = sg.g;
   const uint32_t local = blockIdx.x - sg.blk0;
-  if (sg.tl.whole) {             // uniform per workgroup
-    alpha_bwd_whole<NS>(sg, local, red, reg_lambda, reg_b, reg_dev);
+  if (sg.tl.form == 1) {             // uniform per workgroup
+    alpha_bwd_wavecol<NS>(sg, local, red, reg_lambda, reg_b, reg_dev);
     return;
   }
   const uint32_t bx = local % sg.tl.ncolblk, by = local / sg.tl.ncolblk;
@@ -380,19 +440,6 @@ __global__ __launch_bounds__(kBlock) void alpha_bwd_prep(PrepTable tab, float re
     const float* __restrict__ gWhat = sg.gWhat;
     const float* __restrict__ delta = sg.delta;
     const float* __restrict__ zp = sg.zp;
-    const float lo = sg.lo, hi = sg.hi;
-    auto one = [&](uint32_t fw, float h, float d, float z, float gy) {
-      float F[NS];
-#pragma unroll
-      for (int i = 0; i < NS; ++i) F[i] = unpack_floor(fw, i);
-      float xf = __fmul_rn(F[0], p[0]);
-#pragma unroll
-      for (int i = 1; i < NS; ++i) xf = __fadd_rn(xf, __fmul_rn(F[i], p[i]));
-      const float u = __fadd_rn(__fadd_rn(xf, h), z);
-      const float gi = (u >= lo && u <= hi) ? __fmul_rn(gy, __fmul_rn(d, 1.0f)) : 0.0f;
-#pragma unroll
-      for (int i = 0; i < NS; ++i) acc[i] += (double)gi * (double)F[i];
-    };
     const uint32_t co0 = by * sg.tl.R, co1 = min(co0 + sg.tl.R, g.Co);
     uint32_t co = co0;
     for (; co + kRBP <= co1; co += kRBP) {
@@ -408,11 +455,12 @@ __global__ __launch_bounds__(kBlock) void alpha_bwd_prep(PrepTable tab, float re
         z[r] = zp[co + r];
       }
 #pragma unroll
-      for (int r = 0; r < kRBP; ++r) one(fw[r], h[r], d[r], z[r], gy[r]);
+      for (int r = 0; r < kRBP; ++r)
+        alpha_accumulate<NS>(fw[r], h[r], d[r], z[r], gy[r], p, sg.lo, sg.hi, acc);
     }
     for (; co < co1; ++co) {
       const uint32_t e = co * g.CiK + j;
-      one(fpack[e], hterm[e], delta[co], zp[co], gWhat[e]);
+      alpha_accumulate<NS>(fpack[e], hterm[e], delta[co], zp[co], gWhat[e], p, sg.lo, sg.hi, acc);
     }
   }
 #pragma unroll
@@ -423,36 +471,27 @@ __global__ __launch_bounds__(kBlock) void alpha_bwd_prep(PrepTable tab, float re
     for (int i = 0; i < NS; ++i) {
       double sum = 0.0;
       for (uint32_t k = 0; k < g.K; ++k) sum += red[(t * g.K + k) * NS + i];
-      double* dst = sg.part + ((size_t)(ci0 + t) * sg.tl.nchunk + by) * NS + i;
-      if (FUSED) st_sc1(dst, sum);
-      else *dst = sum;
+      sg.part[((size_t)(ci0 + t) * sg.tl.nchunk + by) * NS + i] = sum;
     }
   }
-  if (!FUSED) return;
-  // the last of the column block's nchunk workgroups to finish reduces its input channels
-  if (!arrive_last(&g_alpha_tickets[sg.tick0 + bx], sg.tl.nchunk, (int*)red)) return;
-  const uint32_t w = threadIdx.x / kWave, lane = threadIdx.x & (kWave - 1);
-  for (uint32_t c = w; c < nci; c += kBlock / kWave)
-    alpha_reduce_ci<NS, true>(sg, ci0 + c, lane, reg_lambda, reg_b, reg_dev);
 }
 
-// Stage 2: one wave per (segment, input channel).  Every load the wave needs (alpha row,
-// the device (lambda, b) pair, lane c's chunks c, c+64, ... -- one coalesced run per round)
-// is issued before any math; lanes i < S evaluate shift i's regulariser term meanwhile; a
-// fixed shuffle tree adds the lanes and lane 0 applies the softmax/clamp backward (same
-// values, same order as alpha_chain).  Deterministic, no atomics.
+// Stage 2 (thread-column segments): one wave per (segment, input channel).  Every load the wave needs (alpha row, the device (lambda, b)
+// pair, lane c's chunks c, c+64, ... -- one coalesced run per round) is issued before any
+// math; lanes i < S evaluate shift i's regulariser term meanwhile; a fixed shuffle tree adds
+// the lanes and lane 0 applies the softmax/clamp backward (same values, same order as
+// alpha_chain).  Deterministic, no atomics.
 constexpr uint32_t kMaxPrepChunkRounds = kMaxChunks / kWave;
 
-// Input channel ci's alpha gradient from its chunk partials, by one wave: every load the
-// wave needs (alpha row, the device (lambda, b) pair, lane c's chunks c, c+64, ... -- one
-// coalesced run per round) is issued before any math; lanes i < S evaluate shift i's
-// regulariser term meanwhile; a fixed shuffle tree adds the lanes and lane 0 applies the
-// softmax/clamp backward (same values, same order as alpha_chain).  SC1: the partials were
-// handed off inside this launch (write-through loads, see arrive_last).
-template <int NS, bool SC1>
-__device__ __forceinline__ void alpha_reduce_ci(const PrepSeg& sg, uint32_t ci, uint32_t lane,
-                                                float reg_lambda, float reg_b,
-                                                const float* __restrict__ reg_dev) {
+template <int NS>
+__global__ __launch_bounds__(kBlock) void alpha_bwd_prep_stage2(PrepTable tab, float reg_lambda,
+                                                                 float reg_b,
+                                                                 const float* __restrict__ reg_dev) {
+  const uint32_t wave = blockIdx.x * (kBlock / kWave) + threadIdx.x / kWave;
+  const uint32_t lane = threadIdx.x & (kWave - 1);
+  const PrepSeg& sg = tab.s[find_seg<true>(tab, __builtin_amdgcn_readfirstlane(wave))];
+  const uint32_t ci = wave - sg.wave0;
+  if (!sg.stage2 || ci >= sg.g.Ci) return;
   const uint32_t nchunk = sg.tl.nchunk;
   float a[kMaxS];
   load_row(sg.alpha, ci, NS, a);
@@ -466,10 +505,7 @@ __device__ __forceinline__ void alpha_reduce_ci(const PrepSeg& sg, uint32_t ci, 
   for (uint32_t r = 0; r < kMaxPrepChunkRounds; ++r) {
     const uint32_t c = lane + r * kWave;
 #pragma unroll
-    for (int i = 0; i < NS; ++i) {
-      const double* q = pp + (size_t)c * NS + i;
-      v[r][i] = c < nchunk ? (SC1 ? ld_sc1(q) : *q) : 0.0;
-    }
+    for (int i = 0; i < NS; ++i) v[r][i] = c < nchunk ? pp[(size_t)c * NS + i] : 0.0;
   }
   float sm[kMaxS], p[kMaxS];
   soft_targets<kMaxS>(a, NS, sm, p);
@@ -510,19 +546,6 @@ __device__ __forceinline__ void alpha_reduce_ci(const PrepSeg& sg, uint32_t ci, 
 #pragma unroll
   for (int i = 0; i < NS; ++i) sg.galpha[(size_t)ci * NS + i] = ga[i];
   if (sg.reg_vals) sg.reg_vals[ci] = reg;
-}
-
-// Stage 2 (two-launch form): one wave per (segment, input channel).
-template <int NS>
-__global__ __launch_bounds__(kBlock) void alpha_bwd_prep_stage2(PrepTable tab, float reg_lambda,
-                                                                 float reg_b,
-                                                                 const float* __restrict__ reg_dev) {
-  const uint32_t wave = blockIdx.x * (kBlock / kWave) + threadIdx.x / kWave;
-  const uint32_t lane = threadIdx.x & (kWave - 1);
-  const PrepSeg& sg = tab.s[find_seg<true>(tab, __builtin_amdgcn_readfirstlane(wave))];
-  const uint32_t ci = wave - sg.wave0;
-  if (sg.tl.whole || ci >= sg.g.Ci) return;    // whole-column segments finished in stage 1
-  alpha_reduce_ci<NS, false>(sg, ci, lane, reg_lambda, reg_b, reg_dev);
 }
 
 // ------------------------------------------------------------------ host side
@@ -566,6 +589,78 @@ static int make_seg(const SegArgs& a, int i, PrepSeg& sg, const char* what) {
 static size_t part_bytes(const PrepSeg& sg, int S) {
   const size_t b = (size_t)sg.tl.nchunk * sg.g.Ci * S * sizeof(double);
   return (b + 255) / 256 * 256;
+}
+
+// ------------------------------------------------------------------ deferred forward
+struct PendingFwd {
+  bool on;
+  hipStream_t s;
+  PrepTable tab;
+  uint32_t blk;
+  int S, hard;
+};
+static bool g_fwd_defer = false;
+static PendingFwd g_fwd_pend{};
+
+static int launch_fwd(hipStream_t s, const PrepTable& tab, uint32_t blk, int S, int hard) {
+#define SSQ_FWDP(NS)                                                                         \
+  do {                                                                                       \
+    if (hard)                                                                                \
+      hipLaunchKernelGGL((shift_fwd_prep<NS, 1>), dim3(blk), dim3(kBlock), 0, s, tab);       \
+    else                                                                                     \
+      hipLaunchKernelGGL((shift_fwd_prep<NS, 0>), dim3(blk), dim3(kBlock), 0, s, tab);       \
+  } while (0)
+  switch (S) {
+    case 1: SSQ_FWDP(1); break;
+    case 2: SSQ_FWDP(2); break;
+    case 3: SSQ_FWDP(3); break;
+    default: SSQ_FWDP(4); break;
+  }
+#undef SSQ_FWDP
+  return check_launch("ssq_adashift_fwd_prepared_multi");
+}
+
+static int flush_fwd(hipStream_t s) {
+  if (!g_fwd_pend.on || g_fwd_pend.s != s) return SSQ_OK;
+  g_fwd_pend.on = false;
+  return launch_fwd(s, g_fwd_pend.tab, g_fwd_pend.blk, g_fwd_pend.S, g_fwd_pend.hard);
+}
+
+int launch_gather(hipStream_t s, const GatherArgs& a, bool vec) {
+  if (!(g_fwd_pend.on && g_fwd_pend.s == s)) {
+    const dim3 grid(a.gx, a.nrows);
+    if (vec)
+      hipLaunchKernelGGL(gather2_kernel<true>, grid, dim3(kBlock), 0, s, a);
+    else
+      hipLaunchKernelGGL(gather2_kernel<false>, grid, dim3(kBlock), 0, s, a);
+    return SSQ_OK;
+  }
+  const PendingFwd f = g_fwd_pend;
+  g_fwd_pend.on = false;
+  const uint32_t ngw = a.gx * a.nrows;
+  const dim3 grid(ngw + f.blk);
+#define SSQ_GF(V, NS)                                                                        \
+  do {                                                                                       \
+    if (f.hard)                                                                              \
+      hipLaunchKernelGGL((gather_shift_fwd<V, NS, 1>), grid, dim3(kBlock), 0, s, a, ngw, f.tab); \
+    else                                                                                     \
+      hipLaunchKernelGGL((gather_shift_fwd<V, NS, 0>), grid, dim3(kBlock), 0, s, a, ngw, f.tab); \
+  } while (0)
+#define SSQ_GFS(V)                    \
+  switch (f.S) {                      \
+    case 1: SSQ_GF(V, 1); break;      \
+    case 2: SSQ_GF(V, 2); break;      \
+    case 3: SSQ_GF(V, 3); break;      \
+    default: SSQ_GF(V, 4); break;     \
+  }
+  if (vec) {
+    SSQ_GFS(true)
+  } else {
+    SSQ_GFS(false)
+  }
+#undef SSQ_GFS
+#undef SSQ_GF
+  return SSQ_OK;
 }
 
 }  // namespace ssq
@@ -614,28 +709,35 @@ extern "C" int ssq_adashift_fwd_prepared_multi(int nseg, const uint32_t* const* 
       sg.What = What[base + k];
       sg.blk0 = blk;
       sg.wave0 = 0;
-      sg.tick0 = 0;
+      sg.stage2 = 0;
       blk += sg.tl.ncolblk * sg.tl.nchunk;
     }
-#define SSQ_FWDP(NS)                                                                         \
-  do {                                                                                       \
-    if (hard_targets)                                                                        \
-      hipLaunchKernelGGL((shift_fwd_prep<NS, 1>), dim3(blk), dim3(kBlock), 0, s, tab);       \
-    else                                                                                     \
-      hipLaunchKernelGGL((shift_fwd_prep<NS, 0>), dim3(blk), dim3(kBlock), 0, s, tab);       \
-  } while (0)
-    switch (S) {
-      case 1: SSQ_FWDP(1); break;
-      case 2: SSQ_FWDP(2); break;
-      case 3: SSQ_FWDP(3); break;
-      default: SSQ_FWDP(4); break;
+    // deferred: this table rides on the stream's next gather (prep_ride.h); a table still
+    // queued from an earlier call is launched first
+    int rc = g_fwd_pend.on ? flush_fwd(g_fwd_pend.s) : SSQ_OK;
+    if (rc) return rc;
+    if (g_fwd_defer && nseg <= kMaxPrepSeg) {
+      g_fwd_pend.on = true;
+      g_fwd_pend.s = s;
+      g_fwd_pend.tab = tab;
+      g_fwd_pend.blk = blk;
+      g_fwd_pend.S = S;
+      g_fwd_pend.hard = hard_targets;
+      return SSQ_OK;
     }
-#undef SSQ_FWDP
-    const int rc = check_launch(what);
+    rc = launch_fwd(s, tab, blk, S, hard_targets);
     if (rc) return rc;
   }
   return SSQ_OK;
 }
+
+extern "C" int ssq_set_deferred_prep_fwd(int on) {
+  const int prev = g_fwd_defer ? 1 : 0;
+  g_fwd_defer = on != 0;
+  return prev;
+}
+
+extern "C" int ssq_flush_prep_fwd(ssq_stream_t stream) { return flush_fwd((hipStream_t)stream); }
 
 extern "C" size_t ssq_adashift_bwd_prepared_multi_workspace_size(int nseg, const int64_t* Co,
                                                                  const int64_t* Ci,
@@ -669,7 +771,7 @@ extern "C" int ssq_adashift_bwd_prepared_multi(
   for (int base = 0; base < nseg; base += kMaxPrepSeg) {
     PrepTable tab;
     tab.nseg = nseg - base < kMaxPrepSeg ? nseg - base : kMaxPrepSeg;
-    uint32_t blk = 0, waves = 0, ticks = 0;
+    uint32_t blk = 0, waves = 0;
     for (int k = 0; k < tab.nseg; ++k) {
       PrepSeg& sg = tab.s[k];
       const int i = base + k;
@@ -683,21 +785,12 @@ extern "C" int ssq_adashift_bwd_prepared_multi(
       sg.part = (double*)wsp;
       wsp += part_bytes(sg, S);
       sg.blk0 = blk;
-      sg.wave0 = waves;
-      sg.tick0 = ticks;
       blk += sg.tl.ncolblk * sg.tl.nchunk;
-      if (!sg.tl.whole) {
-        waves += sg.g.Ci;
-        ticks += sg.tl.ncolblk;
-      }
+      sg.stage2 = sg.tl.form == 0;
+      sg.wave0 = waves;
+      if (sg.stage2) waves += sg.g.Ci;
     }
     const unsigned blocks2 = (waves + kBlock / kWave - 1) / (kBlock / kWave);
-    // two launches by default; SSQ_ALPHA_ONE_LAUNCH=1 (A/B knob) reduces in the same
-    // launch (last arriver per column block) while the counters last -- measured slower
-    // (64x64x3x3 9.6 -> 26 us, 512x256x1x1 9.8 -> 135 us): its reducer walks the column
-    // block's input channels with one wave each, serially, where stage 2 spreads them
-    // over the chip
-    const bool fused = alpha_one_launch() && ticks <= kAlphaTickets;
     // queued finalize tasks of this stream ride on the first launch (their inputs live in
     // their producers' own workspace slots, not in this one)
     FinTable fin;
@@ -706,16 +799,11 @@ extern "C" int ssq_adashift_bwd_prepared_multi(
     if (base == 0) fin = fin_take(s);
 #define SSQ_BWDP(NS)                                                                          \
   do {                                                                                        \
-    if (fused) {                                                                              \
-      hipLaunchKernelGGL((alpha_bwd_prep<NS, true>), dim3(blk + fin.nwg), dim3(kBlock), 0, s, \
-                         tab, reg_lambda, reg_b, reg_dev, fin, blk);                          \
-    } else {                                                                                  \
-      hipLaunchKernelGGL((alpha_bwd_prep<NS, false>), dim3(blk + fin.nwg), dim3(kBlock), 0,   \
-                         s, tab, reg_lambda, reg_b, reg_dev, fin, blk);                       \
-      if (blocks2)                                                                            \
-        hipLaunchKernelGGL((alpha_bwd_prep_stage2<NS>), dim3(blocks2), dim3(kBlock), 0, s,    \
-                           tab, reg_lambda, reg_b, reg_dev);                                  \
-    }                                                                                         \
+    hipLaunchKernelGGL((alpha_bwd_prep<NS>), dim3(blk + fin.nwg), dim3(kBlock), 0, s, tab,    \
+                       reg_lambda, reg_b, reg_dev, fin, blk);                                 \
+    if (blocks2)                                                                              \
+      hipLaunchKernelGGL((alpha_bwd_prep_stage2<NS>), dim3(blocks2), dim3(kBlock), 0, s, tab, \
+                         reg_lambda, reg_b, reg_dev);                                         \
   } while (0)
     switch (S) {
       case 1: SSQ_BWDP(1); break;

@@ -11,6 +11,7 @@
 #include <type_traits>
 
 #include "fin_tasks.h"
+#include "prep_ride.h"
 #include "ssq_common.h"
 
 namespace ssq {
@@ -128,32 +129,6 @@ __global__ __launch_bounds__(kBlock) void lp_loss_kernel(const float* __restrict
 __global__ void lp_loss_finalize(const double* __restrict__ part, int nblk, double m,
                                  float* __restrict__ out) {
   fin_loss(part, nblk, m, out);
-}
-
-// dst_k[r, :] = src_k[idx[r], :], 16-B vectors when rows allow it.  blockIdx.y is the
-// batch row (its source row index is one scalar load), blockIdx.x strides over the
-// concatenated row of both sources: no per-element integer division.
-template <bool VEC>
-__global__ __launch_bounds__(kBlock) void gather2_kernel(const float* __restrict__ s0,
-                                                         float* __restrict__ d0, int64_t row0,
-                                                         const float* __restrict__ s1,
-                                                         float* __restrict__ d1, int64_t row1,
-                                                         const int64_t* __restrict__ idx) {
-  typedef typename std::conditional<VEC, f32x4, float>::type T;
-  const int64_t w = VEC ? 4 : 1;
-  const int64_t r0 = row0 / w, r1 = s1 ? row1 / w : 0;
-  const int64_t r = blockIdx.y;
-  const int64_t src = idx[r];
-  const T* a0 = (const T*)s0 + src * r0;
-  T* b0 = (T*)d0 + r * r0;
-  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
-  for (int64_t k = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; k < r0; k += stride) b0[k] = a0[k];
-  if (s1) {
-    const T* a1 = (const T*)s1 + src * r1;
-    T* b1 = (T*)d1 + r * r1;
-    for (int64_t k = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; k < r1; k += stride)
-      b1[k] = a1[k];
-  }
 }
 
 // ------------------------------------------------------------------ K13 fused epilogue
@@ -594,13 +569,9 @@ extern "C" int ssq_gather_rows2(const float* src0, float* dst0, int64_t row0, co
   const int64_t need = (per + kBlock - 1) / kBlock;
   if (gx > need) gx = need;
   if (gx < 1) gx = 1;
-  const dim3 grid((unsigned)gx, (unsigned)nidx);
-  if (vec)
-    hipLaunchKernelGGL(gather2_kernel<true>, grid, dim3(kBlock), 0, (hipStream_t)stream, src0,
-                       dst0, row0, src1, dst1, row1, idx);
-  else
-    hipLaunchKernelGGL(gather2_kernel<false>, grid, dim3(kBlock), 0, (hipStream_t)stream, src0,
-                       dst0, row0, src1, dst1, row1, idx);
+  GatherArgs a{src0, dst0, row0, src1, dst1, row1, idx, (uint32_t)gx, (uint32_t)nidx};
+  const int rc = launch_gather((hipStream_t)stream, a, vec);
+  if (rc) return rc;
   return check_launch("ssq_gather_rows2");
 }
 

@@ -928,6 +928,28 @@ class deferred_finalize:
                 set_deferred_finalize(self.prev)
 
 
+class deferred_prep_fwd:
+    """Context (the fused loop's iteration start): the prepared adaShift forward launched
+    inside it rides on the next batch gather of its stream (include/ssq.h,
+    csrc/prep_ride.h); a forward still queued at exit is launched then."""
+
+    def __init__(self, on=True, device=None):
+        self.on, self.device = on, device
+
+    def __enter__(self):
+        self.prev = bool(query("ssq_set_deferred_prep_fwd", 1)) if self.on else None
+        return self
+
+    def __exit__(self, *exc):
+        if self.on:
+            dev_ = torch.device("cuda", torch.cuda.current_device()) if self.device is None \
+                else self.device
+            try:
+                call("ssq_flush_prep_fwd", C.c_void_p(torch.cuda.current_stream(dev_).cuda_stream))
+            finally:
+                query("ssq_set_deferred_prep_fwd", int(self.prev))
+
+
 # Set by the fused recon loop around its block forward to the block it reconstructs: that
 # block's final epilogue is not run; its output is returned as a placeholder carrying the
 # epilogue's inputs (_ssq_tail), and the loop runs forward + loss + backward of that

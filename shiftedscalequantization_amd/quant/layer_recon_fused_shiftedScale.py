@@ -26,6 +26,8 @@ from .quant_layer import QuantModule
 
 # A/B knob: deferred loss / epilogue finalizes inside the loop body (bit-identical either way)
 DEFER_FINALIZE = True
+# the iteration's prepared adaShift forward rides on its batch gather (K.deferred_prep_fwd)
+FUSE_START = True
 # A/B knob: the block's final epilogue + loss + its backward as one pass (bit-identical)
 FUSE_TAIL = True
 
@@ -148,9 +150,11 @@ def _fused_loop(block, modules, iters, lmda, model, p, lr, bias_cal, batch_size,
             # a deferred gamma/phi gradient is only final after the next backward launch:
             # AccumulateGrad must take it over, never add it into an existing .grad
             raise RuntimeError("deferred finalizes need every parameter's .grad unset")
-        cur_inp, cur_out = feeder.gather_lazy()
-        if on_gpu:
-            stash_block_weights(quantizers)     # every conv's What in one launch
+        # every conv's What (one table) and the batch gather in ONE launch
+        with K.deferred_prep_fwd(on_gpu and FUSE_START):
+            if on_gpu:
+                stash_block_weights(quantizers)
+            cur_inp, cur_out = feeder.gather_lazy()
         K.TAIL_LAZY[0] = block if fuse_tail else None
         try:
             quant_out = block(cur_inp)

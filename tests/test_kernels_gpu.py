@@ -1033,6 +1033,39 @@ def test_adashift_prepared_multi_equals_single(K):
         np.testing.assert_array_equal(host(v), v1, err_msg=str(shapes[k]))
 
 
+def test_prepared_forward_rides_on_gather(K):
+    """A deferred prepared forward (K.deferred_prep_fwd) runs inside the next batch gather's
+    launch: the What of every segment and the gathered rows are bit-identical to the two
+    separate launches; a forward with no gather after it is launched when the context ends."""
+    shapes = [(64, 64, 3, 3), (128, 64, 3, 3), (128, 64, 1, 1), (24, 5, 5, 5)]
+    gen = torch.Generator().manual_seed(5)
+    alphas, entries = [], []
+    for shape in shapes:
+        w = (torch.randn(shape, generator=gen) * 0.05).cuda()
+        d, z, _ = K.scale_init(w, 2, False, True, "max")
+        alpha, beta, _ = K.shift_init(w, d, SHIFTS)
+        alphas.append(alpha + torch.randn(alpha.shape, generator=gen).cuda() * 0.5)
+        entries.append((K.AdaShiftPrep(w, beta, d, SHIFTS, 0), d, z, 2, False))
+    src0 = torch.randn(40, 3, 8, 9, generator=gen).cuda()      # rows of 216 floats (vec)
+    src1 = torch.randn(40, 7, 5, generator=gen).cuda()         # rows of 35 floats (scalar)
+    idx = torch.randperm(40, generator=gen)[:13].cuda()
+    for s1 in (src0[:, :2], src1):
+        ref_w = K.adashift_prepared_multi(alphas, entries, False)
+        ref_g = K.gather_rows2(src0, idx, s1.contiguous())
+        with K.deferred_prep_fwd():
+            got_w = K.adashift_prepared_multi(alphas, entries, False)
+            got_g = K.gather_rows2(src0, idx, s1.contiguous())
+        torch.cuda.synchronize()
+        for a, b in zip(ref_w, got_w):
+            assert torch.equal(a, b)
+        for a, b in zip(ref_g, got_g):
+            assert torch.equal(a, b)
+    with K.deferred_prep_fwd():
+        late = K.adashift_prepared_multi(alphas, entries, False)
+    for a, b in zip(ref_w, late):
+        assert torch.equal(a, b)
+
+
 def test_adashift_prepared_overflow_falls_back(K):
     """A floor outside int8 (an 8-bit weight with a tiny delta) marks the preparation
     unusable; ChannelQuant then keeps the recomputing kernels with identical results."""

@@ -59,6 +59,45 @@ __global__ void k_flush(const float4* __restrict__ a, float4* __restrict__ b, si
     b[i] = a[i];
 }
 
+typedef float f4 __attribute__((ext_vector_type(4)));
+__global__ void k_flush_nt(const float4* __restrict__ a4, float4* __restrict__ b4, size_t n) {
+  const f4* a = (const f4*)a4;
+  f4* b = (f4*)b4;
+  for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < n;
+       i += (size_t)gridDim.x * blockDim.x)
+    __builtin_nontemporal_store(a[i], &b[i]);
+}
+
+__global__ void k_flush_rd(const float4* __restrict__ a, float* __restrict__ out, size_t n) {
+  float s = 0.0f;
+  for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < n;
+       i += (size_t)gridDim.x * blockDim.x)
+    s += a[i].x;
+  if (s == 12345.0f) out[0] = s;
+}
+
+// which part of the previous kernel's work does the next (empty) launch pay for?
+// after: a 512 MB copy with plain stores / with non-temporal stores / a 512 MB read-only
+// pass / a plain-store copy of 8 MB, 64 MB
+static int after_probe(float4* fa, float4* fb, float* out) {
+  const size_t n4 = ((size_t)512 << 20) / sizeof(float4);
+  for (int r = 0; r < 50; ++r) {
+    hipLaunchKernelGGL(k_flush, dim3(2048), dim3(256), 0, 0, fa, fb, n4);
+    hipLaunchKernelGGL(k_empty, dim3(1), dim3(256), 0, 0, out);
+    hipLaunchKernelGGL(k_flush_nt, dim3(2048), dim3(256), 0, 0, fa, fb, n4);
+    hipLaunchKernelGGL(k_empty, dim3(1), dim3(256), 0, 0, out);
+    hipLaunchKernelGGL(k_flush_rd, dim3(2048), dim3(256), 0, 0, fa, out, n4);
+    hipLaunchKernelGGL(k_empty, dim3(1), dim3(256), 0, 0, out);
+    hipLaunchKernelGGL(k_flush, dim3(2048), dim3(256), 0, 0, fa, fb, n4 / 64);
+    hipLaunchKernelGGL(k_empty, dim3(1), dim3(256), 0, 0, out);
+    hipLaunchKernelGGL(k_flush, dim3(2048), dim3(256), 0, 0, fa, fb, n4 / 8);
+    hipLaunchKernelGGL(k_empty, dim3(1), dim3(256), 0, 0, out);
+  }
+  CK(hipDeviceSynchronize());
+  printf("after-probe done\n");
+  return 0;
+}
+
 int main() {
   const size_t big = (size_t)512 << 20;   // 512 MB each way: well past L2 + MALL
   float4 *fa, *fb;
@@ -96,5 +135,5 @@ int main() {
     CK(hipDeviceSynchronize());
     printf("grid %d done\n", grid);
   }
-  return 0;
+  return after_probe(fa, fb, out);
 }

@@ -13,6 +13,8 @@ elements of the block's convs, N_W its weights, N_in its gathered input elements
   K5p  shift_fwd_prep                        12 B / weight   (packed floors + h(beta) in, W^ out)
   K6p  alpha_bwd_prep (+ _stage2)            12 B / weight   (dL/dW^ + packed floors + h(beta) in)
   K14  gather2_kernel                         8 B / input elem (batch rows in and out)
+  K14+K5p gather_shift_fwd                    8 B / input elem + 12 B / weight (the two above
+                                              in one launch: the iteration start)
   K13  bias_act_kernel<RES,...>              (8 + 4 RES) B / A (y [+ residual] in, activation out)
   K13b epilogue_bwd_rows<RES,...,LOSS=false> (12 + 4 RES + 4 GRES) B / A (g, y [, res] in,
                                               gy [, g_res] out)
@@ -63,6 +65,8 @@ def classify(name, sz):
     """(class, algorithmic bytes) of one launch, or (None, 0) outside the HBM set."""
     a = targs(name)
     A = sz["A"]
+    if "gather_shift_fwd" in name:
+        return "K14_K5p_gather_adashift_fwd", 8 * sz["N_in"] + 12 * sz["N_W"]
     if "shift_fwd_prep" in name:
         return "K5p_adashift_fwd", 12 * sz["N_W"]
     if "alpha_bwd_prep_stage2" in name:
@@ -87,7 +91,8 @@ def classify(name, sz):
 
 
 def segments(rows):
-    gi = [i for i, r in enumerate(rows) if "gather2_kernel" in r["Kernel_Name"]]
+    gi = [i for i, r in enumerate(rows) if "gather2_kernel" in r["Kernel_Name"] or
+          "gather_shift_fwd" in r["Kernel_Name"]]
     segs, cur = [], [gi[0]]
     for a, b in zip(gi, gi[1:]):
         if int(rows[b]["Start_Timestamp"]) - int(rows[a]["Start_Timestamp"]) > 5e6:
