@@ -411,14 +411,17 @@ __global__ __launch_bounds__(kBlock) void alpha_bwd_prep(PrepTable tab, float re
                                                           float reg_b,
                                                           const float* __restrict__ reg_dev,
                                                           FinTable fin, uint32_t nmain) {
-  if (blockIdx.x >= nmain) {          // queued finalize tasks (fin_tasks.h) ride on this launch
-    run_fin(fin, blockIdx.x - nmain);
+  // queued finalize tasks (fin_tasks.h) ride on this launch: its first workgroups
+  (void)nmain;
+  if (blockIdx.x < fin.nwg) {
+    run_fin(fin, blockIdx.x);
     return;
   }
+  const uint32_t bid = blockIdx.x - fin.nwg;
   __shared__ double red[kBlock * NS];
-  const PrepSeg& sg = tab.s[find_seg<false>(tab, blockIdx.x)];
+  const PrepSeg& sg = tab.s[find_seg<false>(tab, bid)];
   const Geo& g = sg.g;
-  const uint32_t local = blockIdx.x - sg.blk0;
+  const uint32_t local = bid - sg.blk0;
   if (sg.tl.form == 1) {             // uniform per workgroup
     alpha_bwd_wavecol<NS>(sg, local, red, reg_lambda, reg_b, reg_dev);
     return;

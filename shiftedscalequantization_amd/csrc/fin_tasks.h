@@ -7,7 +7,10 @@
 // deferral on (ssq_set_deferred_finalize, turned on by the fused recon loop's body) the
 // producing entry point does not launch its finalize: it queues it as a task on its
 // stream, and the next "host" launch on that stream (epilogue_bwd_rows, the prepared alpha
-// backward's first kernel) runs the queued tasks in extra workgroups appended to its grid.
+// backward's first kernel) runs the queued tasks in extra workgroups at the front of its
+// grid (dispatched first: they run beside the launch's own work).  The task code is kept
+// lean in registers: it is inlined into those kernels, whose occupancy it sets (a 16-deep
+// act-sum batch once took them from 8 to 3 waves per SIMD).
 // Same device code, same summation order: bit-identical results, fewer launches.
 //
 // Rules that keep it correct whatever runs in between:
@@ -27,6 +30,7 @@
 namespace ssq {
 
 constexpr int kLossBlocks = 1024;   // lp_loss workgroup partials
+constexpr uint32_t kFinBatch = 16;  // loads in flight per thread in the row-walking finalizes
 constexpr int kEpiParts = 7;        // doubles per (n, c) row of the epilogue backward
                                     // (slot 6: the fused tail's loss partial)
 
@@ -98,8 +102,22 @@ __device__ __forceinline__ void fin_epi(uint32_t bid, const double* __restrict__
     return;
   }
   double a[4] = {0, 0, 0, 0};
-  for (uint32_t r = threadIdx.x; r < N * C; r += blockDim.x)
-    for (int k = 0; k < 4; ++k) a[k] += part[(int64_t)r * kEpiParts + 2 + k];
+  constexpr uint32_t kB = kFinBatch / 4;   // 4 sums per row: keep the registers of the
+                                            // host kernels this rides on (occupancy) low
+  for (uint32_t r0 = threadIdx.x; r0 < N * C; r0 += kB * kBlock) {
+    double v[kB][4];
+#pragma unroll
+    for (uint32_t j = 0; j < kB; ++j) {
+      const uint32_t r = r0 + j * kBlock;
+#pragma unroll
+      for (int k = 0; k < 4; ++k) v[j][k] = r < N * C ? part[(int64_t)r * kEpiParts + 2 + k] : 0.0;
+    }
+#pragma unroll
+    for (uint32_t j = 0; j < kB; ++j)
+      if (r0 + j * kBlock < N * C)
+#pragma unroll
+        for (int k = 0; k < 4; ++k) a[k] += v[j][k];
+  }
   for (int k = 0; k < 4; ++k) a[k] = block_sum(a[k], red);
   if (threadIdx.x == 0) {
     if (gdelta) gdelta[0] = (float)(a[0] - a[1]);
@@ -108,12 +126,24 @@ __device__ __forceinline__ void fin_epi(uint32_t bid, const double* __restrict__
 }
 
 // fused tail (ssq_epilogue_loss_bwd): the per-row loss partials (slot 6 of each row's
-// kEpiParts doubles) summed in row order, one workgroup
+// kEpiParts doubles) summed in row order, one workgroup: thread t adds rows t, t + 256, ...
+// in order, kFinBatch loads in flight at a time (a 32 x 256 layer3 batch is 32 rows per
+// thread: serial loads took ~10 us), then the fixed block tree
 __device__ __forceinline__ void fin_loss_rows(const double* __restrict__ part, uint32_t rows,
                                               double m, float* __restrict__ out) {
   __shared__ double red[16];
   double a = 0.0;
-  for (uint32_t r = threadIdx.x; r < rows; r += kBlock) a += part[(int64_t)r * kEpiParts + 6];
+  for (uint32_t r0 = threadIdx.x; r0 < rows; r0 += kFinBatch * kBlock) {
+    double v[kFinBatch];
+#pragma unroll
+    for (uint32_t k = 0; k < kFinBatch; ++k) {
+      const uint32_t r = r0 + k * kBlock;
+      v[k] = r < rows ? part[(int64_t)r * kEpiParts + 6] : 0.0;
+    }
+#pragma unroll
+    for (uint32_t k = 0; k < kFinBatch; ++k)
+      if (r0 + k * kBlock < rows) a += v[k];
+  }
   a = block_sum(a, red);
   if (threadIdx.x == 0) out[0] = (float)(a / m);
 }

@@ -268,6 +268,73 @@ __global__ __launch_bounds__(kBlock) void adam_kernel(AdamTable tab, float w1, f
   }
 }
 
+// One element of the epilogue backward (the pass below): the forward recomputed from y with
+// the forward's fp32 operations, then dL/d(pre-activation) and the per-row sums.
+struct EpiRow {
+  float b, ga, ph;                                   // bias[c], gamma[c], phi[c]
+  double sg = 0, sp = 0, a0 = 0, a1 = 0, a2 = 0, a3 = 0, la = 0;
+};
+template <bool RES, int ACT, bool QUANT, bool AFFINE, bool LOSS, bool BIAS>
+__device__ __forceinline__ void epi_elem(EpiRow& w, float d, float z, float lo, float hi,
+                                         float inv_m, float yv, float gv_or_tgt, float rv,
+                                         float& oy, float& orr) {
+  const float pre = BIAS ? __fadd_rn(yv, w.b) : yv;
+  float t = AFFINE ? __fadd_rn(__fmul_rn(pre, w.ga), w.ph) : pre;
+  if (RES) t = __fadd_rn(t, rv);
+  t = act_fwd<ACT>(t);
+  float tq = 0.0f, q = 0.0f;
+  bool m = true;
+  if (QUANT) {
+    tq = t / d;
+    const float v = __fadd_rn(rintf(tq), z);
+    m = (v >= lo) && (v <= hi);
+    q = clampf(v, lo, hi);
+  }
+  float gv = gv_or_tgt;
+  if (LOSS) {   // the forward's output (fq1's dequant), then the loss gradient wrt it
+    const float o = QUANT ? __fmul_rn(__fsub_rn(q, z), d) : t;
+    gv = lp_elem<0>(o, gv_or_tgt, 2.0f, inv_m, 1.0f, 0, w.la);
+  }
+  float gt = gv;
+  if (QUANT) {
+    const float gq = __fmul_rn(gv, d);
+    const float gi = m ? gq : 0.0f;
+    gt = gi / d;
+    w.a0 += (double)gv * (double)__fsub_rn(q, z);
+    w.a1 += (double)gi * (double)(tq / d);
+    w.a2 += (double)gi;
+    w.a3 += (double)gq;
+  }
+  if (ACT) gt = act_pass<ACT>(t) ? gt : 0.0f;
+  oy = AFFINE ? __fmul_rn(gt, w.ga) : gt;
+  orr = gt;
+  w.sg += (double)gt * (double)pre;
+  w.sp += (double)gt;
+}
+
+// the row's sums over the wave (fixed shuffle tree), written by lane 0 to its kEpiParts slots
+template <bool QUANT, bool LOSS>
+__device__ __forceinline__ void epi_row_sums(EpiRow& w, uint32_t lane, double* __restrict__ o) {
+  w.sg = wave_sum(w.sg);
+  w.sp = wave_sum(w.sp);
+  if (QUANT) {
+    w.a0 = wave_sum(w.a0);
+    w.a1 = wave_sum(w.a1);
+    w.a2 = wave_sum(w.a2);
+    w.a3 = wave_sum(w.a3);
+  }
+  if (LOSS) w.la = wave_sum(w.la);
+  if (lane == 0) {
+    o[0] = w.sg;
+    o[1] = w.sp;
+    o[2] = w.a0;
+    o[3] = w.a1;
+    o[4] = w.a2;
+    o[5] = w.a3;
+    o[6] = w.la;
+  }
+}
+
 // Backward of the K13 epilogue (optionally with gamma^z/phi^z and the act quantizer):
 // t = (y + bias[c]) [*gamma[c] + phi[c]] [+ res] [-> ReLU] [-> fq]; given g = dL/d(output)
 //   g_t = dL/d(pre-ReLU t): the STE of the act quantizer (fq_bwd_pt's formulas), then the
@@ -275,12 +342,16 @@ __global__ __launch_bounds__(kBlock) void adam_kernel(AdamTable tab, float w1, f
 //   gy  = g_t * gamma[c] (mul backward) or g_t;   gres = g_t;
 //   per row (n, c): sum g_t*(y + bias[c]) -> dL/dgamma[c],  sum g_t -> dL/dphi[c],
 //   and the act quantizer's four sums -> dL/ddelta, dL/dzp.
-// One wave per (n, c) row; the pre-activation values are recomputed from y with the
-// forward's fp32 operations (bit-identical masks), nothing of the forward is stored.
+// A wave owns RPW (n, c) rows: RPW = 1 walks a row of any length in 64-lane strides; RPW = 4
+// (rows of <= 64 elements or float4s: ResNet-18 layer3 / layer4 planes) gives each lane one
+// element (float4) of each of 4 consecutive rows, every load of the 4 rows issued before any
+// math -- the same per-lane values and order as RPW = 1, so the same bits, with a quarter of
+// the waves.  The pre-activation values are recomputed from y with the forward's fp32
+// operations (bit-identical masks), nothing of the forward is stored.
 // LOSS (the fused tail, ssq_epilogue_loss_bwd): g is the cache of target rows instead of
 // dL/d(output); the output is recomputed (the forward's ops) and dL/d(output) is the p = 2
 // lp_loss gradient of K11 (lp_elem, identical ops), the loss partial goes to slot 6.
-template <bool RES, int ACT, bool QUANT, bool AFFINE, bool VEC, bool LOSS>
+template <bool RES, int ACT, bool QUANT, bool AFFINE, bool VEC, bool LOSS, int RPW>
 __global__ __launch_bounds__(kBlock) void epilogue_bwd_rows(
     const float* __restrict__ g, const float* __restrict__ y, const float* __restrict__ bias,
     const float* __restrict__ gamma, const float* __restrict__ phi, const float* __restrict__ res,
@@ -288,99 +359,119 @@ __global__ __launch_bounds__(kBlock) void epilogue_bwd_rows(
     const float* __restrict__ qzp, float lo, float hi, float* __restrict__ gy,
     float* __restrict__ gres, double* __restrict__ part, FinTable fin, uint32_t nmain,
     const int64_t* __restrict__ lidx, float inv_m) {
-  if (blockIdx.x >= nmain) {          // queued finalize tasks ride on this launch
-    run_fin(fin, blockIdx.x - nmain);
+  // queued finalize tasks ride on this launch: its first workgroups (dispatched first, so
+  // they run beside the main work instead of after it)
+  (void)nmain;
+  if (blockIdx.x < fin.nwg) {
+    run_fin(fin, blockIdx.x);
     return;
   }
+  const uint32_t bid = blockIdx.x - fin.nwg;
   const uint32_t lane = threadIdx.x & (kWave - 1);
-  const uint32_t r = blockIdx.x * (kBlock / kWave) + threadIdx.x / kWave;
-  if (r >= rows) return;
-  const uint32_t c = r % C;
-  const float b = bias ? bias[c] : 0.0f;
-  const float ga = AFFINE ? gamma[c] : 1.0f, ph = AFFINE ? phi[c] : 0.0f;
+  const uint32_t r0 = (bid * (kBlock / kWave) + threadIdx.x / kWave) * RPW;
+  if (r0 >= rows) return;
   const float d = QUANT ? qdelta[0] : 1.0f, z = QUANT ? qzp[0] : 0.0f;
-  double sg = 0, sp = 0, a0 = 0, a1 = 0, a2 = 0, a3 = 0, la = 0;
-  auto one = [&](float yv, float gv_or_tgt, float rv, float& oy, float& orr) {
-    const float pre = bias ? __fadd_rn(yv, b) : yv;
-    float t = AFFINE ? __fadd_rn(__fmul_rn(pre, ga), ph) : pre;
-    if (RES) t = __fadd_rn(t, rv);
-    t = act_fwd<ACT>(t);
-    float tq = 0.0f, q = 0.0f;
-    bool m = true;
-    if (QUANT) {
-      tq = t / d;
-      const float v = __fadd_rn(rintf(tq), z);
-      m = (v >= lo) && (v <= hi);
-      q = clampf(v, lo, hi);
-    }
-    float gv = gv_or_tgt;
-    if (LOSS) {   // the forward's output (fq1's dequant), then the loss gradient wrt it
-      const float o = QUANT ? __fmul_rn(__fsub_rn(q, z), d) : t;
-      gv = lp_elem<0>(o, gv_or_tgt, 2.0f, inv_m, 1.0f, 0, la);
-    }
-    float gt = gv;
-    if (QUANT) {
-      const float gq = __fmul_rn(gv, d);
-      const float gi = m ? gq : 0.0f;
-      gt = gi / d;
-      a0 += (double)gv * (double)__fsub_rn(q, z);
-      a1 += (double)gi * (double)(tq / d);
-      a2 += (double)gi;
-      a3 += (double)gq;
-    }
-    if (ACT) gt = act_pass<ACT>(t) ? gt : 0.0f;
-    oy = AFFINE ? __fmul_rn(gt, ga) : gt;
-    orr = gt;
-    sg += (double)gt * (double)pre;
-    sp += (double)gt;
+  EpiRow w[RPW];
+#pragma unroll
+  for (int k = 0; k < RPW; ++k) {
+    const uint32_t c = (r0 + k) % C;
+    const bool ok = r0 + k < rows;
+    w[k].b = (bias && ok) ? bias[c] : 0.0f;
+    w[k].ga = (AFFINE && ok) ? gamma[c] : 1.0f;
+    w[k].ph = (AFFINE && ok) ? phi[c] : 0.0f;
+  }
+  auto elem = [&](EpiRow& wr, float yv, float gv, float rv, float& oy, float& orr) {
+    if (bias) epi_elem<RES, ACT, QUANT, AFFINE, LOSS, true>(wr, d, z, lo, hi, inv_m, yv, gv, rv, oy, orr);
+    else epi_elem<RES, ACT, QUANT, AFFINE, LOSS, false>(wr, d, z, lo, hi, inv_m, yv, gv, rv, oy, orr);
   };
-  const int64_t base = (int64_t)r * hw;
   // LOSS: row (n, c)'s target is row c of cached sample idx[n] ([*, C, hw] cache)
-  const int64_t gbase = LOSS ? (lidx[r / C] * (int64_t)C + c) * hw : base;
+  auto gbase_of = [&](uint32_t r) -> int64_t {
+    return LOSS ? (lidx[r / C] * (int64_t)C + r % C) * hw : (int64_t)r * hw;
+  };
+  if (RPW == 1) {
+    EpiRow& wr = w[0];
+    const int64_t base = (int64_t)r0 * hw, gbase = gbase_of(r0);
+    if (VEC) {
+      const f32x4* Y = (const f32x4*)(y + base);
+      const f32x4* G = (const f32x4*)(g + gbase);
+      const f32x4* R = RES ? (const f32x4*)(res + base) : nullptr;
+      f32x4* GY = (f32x4*)(gy + base);
+      f32x4* GR = gres ? (f32x4*)(gres + base) : nullptr;
+      for (uint32_t v = lane; v < hw / 4; v += kWave) {
+        const f32x4 yv = Y[v], gv = G[v];
+        f32x4 rv = {0.0f, 0.0f, 0.0f, 0.0f};
+        if (RES) rv = R[v];
+        float oy[4], orr[4];
+        elem(wr, yv.x, gv.x, rv.x, oy[0], orr[0]);
+        elem(wr, yv.y, gv.y, rv.y, oy[1], orr[1]);
+        elem(wr, yv.z, gv.z, rv.z, oy[2], orr[2]);
+        elem(wr, yv.w, gv.w, rv.w, oy[3], orr[3]);
+        GY[v] = f32x4{oy[0], oy[1], oy[2], oy[3]};
+        if (GR) GR[v] = f32x4{orr[0], orr[1], orr[2], orr[3]};
+      }
+    } else {
+      for (uint32_t j = lane; j < hw; j += kWave) {
+        float oy, orr;
+        elem(wr, y[base + j], g[gbase + j], RES ? res[base + j] : 0.0f, oy, orr);
+        gy[base + j] = oy;
+        if (gres) gres[base + j] = orr;
+      }
+    }
+    epi_row_sums<QUANT, LOSS>(wr, lane, part + (int64_t)r0 * kEpiParts);
+    return;
+  }
+  // RPW rows, one element (float4) per lane and row, all loads first
+  const uint32_t nv = VEC ? hw / 4 : hw;     // <= 64 (host-checked)
+  const bool on = lane < nv;
   if (VEC) {
-    const f32x4* Y = (const f32x4*)(y + base);
-    const f32x4* G = (const f32x4*)(g + gbase);
-    const f32x4* R = RES ? (const f32x4*)(res + base) : nullptr;
-    f32x4* GY = (f32x4*)(gy + base);
-    f32x4* GR = gres ? (f32x4*)(gres + base) : nullptr;
-    for (uint32_t v = lane; v < hw / 4; v += kWave) {
-      const f32x4 yv = Y[v], gv = G[v];
-      f32x4 rv = {0.0f, 0.0f, 0.0f, 0.0f};
-      if (RES) rv = R[v];
-      float oy[4], orr[4];
-      one(yv.x, gv.x, rv.x, oy[0], orr[0]);
-      one(yv.y, gv.y, rv.y, oy[1], orr[1]);
-      one(yv.z, gv.z, rv.z, oy[2], orr[2]);
-      one(yv.w, gv.w, rv.w, oy[3], orr[3]);
-      GY[v] = f32x4{oy[0], oy[1], oy[2], oy[3]};
-      if (GR) GR[v] = f32x4{orr[0], orr[1], orr[2], orr[3]};
+    f32x4 yv[RPW], gv[RPW], rv[RPW];
+#pragma unroll
+    for (int k = 0; k < RPW; ++k) {
+      yv[k] = gv[k] = rv[k] = f32x4{0.0f, 0.0f, 0.0f, 0.0f};
+      if (on && r0 + k < rows) {
+        yv[k] = ((const f32x4*)(y + (int64_t)(r0 + k) * hw))[lane];
+        gv[k] = ((const f32x4*)(g + gbase_of(r0 + k)))[lane];
+        if (RES) rv[k] = ((const f32x4*)(res + (int64_t)(r0 + k) * hw))[lane];
+      }
+    }
+#pragma unroll
+    for (int k = 0; k < RPW; ++k) {
+      if (r0 + k >= rows) break;             // wave-uniform
+      if (on) {
+        float oy[4], orr[4];
+        elem(w[k], yv[k].x, gv[k].x, rv[k].x, oy[0], orr[0]);
+        elem(w[k], yv[k].y, gv[k].y, rv[k].y, oy[1], orr[1]);
+        elem(w[k], yv[k].z, gv[k].z, rv[k].z, oy[2], orr[2]);
+        elem(w[k], yv[k].w, gv[k].w, rv[k].w, oy[3], orr[3]);
+        const int64_t base = (int64_t)(r0 + k) * hw;
+        ((f32x4*)(gy + base))[lane] = f32x4{oy[0], oy[1], oy[2], oy[3]};
+        if (gres) ((f32x4*)(gres + base))[lane] = f32x4{orr[0], orr[1], orr[2], orr[3]};
+      }
+      epi_row_sums<QUANT, LOSS>(w[k], lane, part + (int64_t)(r0 + k) * kEpiParts);
     }
   } else {
-    for (uint32_t j = lane; j < hw; j += kWave) {
-      float oy, orr;
-      one(y[base + j], g[gbase + j], RES ? res[base + j] : 0.0f, oy, orr);
-      gy[base + j] = oy;
-      if (gres) gres[base + j] = orr;
+    float yv[RPW], gv[RPW], rv[RPW];
+#pragma unroll
+    for (int k = 0; k < RPW; ++k) {
+      yv[k] = gv[k] = rv[k] = 0.0f;
+      if (on && r0 + k < rows) {
+        yv[k] = y[(int64_t)(r0 + k) * hw + lane];
+        gv[k] = g[gbase_of(r0 + k) + lane];
+        if (RES) rv[k] = res[(int64_t)(r0 + k) * hw + lane];
+      }
     }
-  }
-  sg = wave_sum(sg);
-  sp = wave_sum(sp);
-  if (QUANT) {
-    a0 = wave_sum(a0);
-    a1 = wave_sum(a1);
-    a2 = wave_sum(a2);
-    a3 = wave_sum(a3);
-  }
-  if (LOSS) la = wave_sum(la);
-  if (lane == 0) {
-    double* o = part + (int64_t)r * kEpiParts;
-    o[0] = sg;
-    o[1] = sp;
-    o[2] = a0;
-    o[3] = a1;
-    o[4] = a2;
-    o[5] = a3;
-    o[6] = la;
+#pragma unroll
+    for (int k = 0; k < RPW; ++k) {
+      if (r0 + k >= rows) break;             // wave-uniform
+      if (on) {
+        float oy, orr;
+        elem(w[k], yv[k], gv[k], rv[k], oy, orr);
+        const int64_t base = (int64_t)(r0 + k) * hw;
+        gy[base + lane] = oy;
+        if (gres) gres[base + lane] = orr;
+      }
+      epi_row_sums<QUANT, LOSS>(w[k], lane, part + (int64_t)(r0 + k) * kEpiParts);
+    }
   }
 }
 
@@ -575,6 +666,16 @@ extern "C" int ssq_gather_rows2(const float* src0, float* dst0, int64_t row0, co
   return check_launch("ssq_gather_rows2");
 }
 
+// A/B knob SSQ_EPI_MULTI_ROW: 4 rows per wave on small planes for the epilogue backward
+// (1, the default), also for its fused-tail form (2), or never (0)
+static int epi_multi_row() {
+  static const int mode = [] {
+    const char* e = getenv("SSQ_EPI_MULTI_ROW");
+    return e && *e ? atoi(e) : 1;
+  }();
+  return mode;
+}
+
 static int bias_act(const char* what, const float* y, const float* bias, const float* res,
                     float* out, float* yq, int64_t n, int64_t hw, int64_t C, int relu,
                     const float* qdelta, const float* qzp, int qmin, int qmax, hipStream_t s,
@@ -662,7 +763,11 @@ static int epilogue_bwd(const char* what, const float* g, const float* y, const 
   const bool vec = hw % 4 == 0 && al(g) && al(y) && al(gy) && (!res || al(res)) &&
                    (!gres || al(gres));
   SSQ_REQUIRE(relu >= 0 && relu <= 2, SSQ_E_ARG, "%s: activation code %d", what, relu);
-  const uint32_t nmain = (uint32_t)((rows + kBlock / kWave - 1) / (kBlock / kWave));
+  // small planes (<= 64 elements or float4s per row): 4 rows per wave (same bits)
+  const bool multi = (vec ? hw / 4 : hw) <= kWave && epi_multi_row() >= (loss ? 2 : 1);
+  const int64_t rpw = multi ? 4 : 1;
+  const int64_t waves = (rows + rpw - 1) / rpw;
+  const uint32_t nmain = (uint32_t)((waves + kBlock / kWave - 1) / (kBlock / kWave));
   int frc = SSQ_OK;
   const FinTable fin = fin_take_for_host(s, ws, ws_bytes, &frc);
   if (frc) return frc;
@@ -670,13 +775,15 @@ static int epilogue_bwd(const char* what, const float* g, const float* y, const 
   const float lo = (float)qmin, hi = (float)qmax;
   const float inv_m = loss ? 1.0f / (float)M : 0.0f;   // mean backward, as lp_loss
   double* part = (double*)ws;
-#define SSQ_EB(R, A, Q, F, V, L)                                                                  \
-  hipLaunchKernelGGL((epilogue_bwd_rows<R, A, Q, F, V, L>), grid, dim3(kBlock), 0, s, g, y, bias, \
-                     gamma, phi, res, (uint32_t)rows, (uint32_t)C, (uint32_t)hw, delta, zp, lo,    \
-                     hi, gy, gres, part, fin, nmain, lidx, inv_m)
+#define SSQ_EB0(R, A, Q, F, V, L, P)                                                              \
+  hipLaunchKernelGGL((epilogue_bwd_rows<R, A, Q, F, V, L, P>), grid, dim3(kBlock), 0, s, g, y,    \
+                     bias, gamma, phi, res, (uint32_t)rows, (uint32_t)C, (uint32_t)hw, delta, zp, \
+                     lo, hi, gy, gres, part, fin, nmain, lidx, inv_m)
+#define SSQ_EB(R, A, Q, F, V, L) \
+  if (multi) SSQ_EB0(R, A, Q, F, V, L, 4); else SSQ_EB0(R, A, Q, F, V, L, 1);
 #define SSQ_EB1(R, A, Q, F) \
-  if (loss) { if (vec) SSQ_EB(R, A, Q, F, true, true); else SSQ_EB(R, A, Q, F, false, true); } \
-  else if (vec) SSQ_EB(R, A, Q, F, true, false); else SSQ_EB(R, A, Q, F, false, false);
+  if (loss) { if (vec) { SSQ_EB(R, A, Q, F, true, true) } else { SSQ_EB(R, A, Q, F, false, true) } } \
+  else if (vec) { SSQ_EB(R, A, Q, F, true, false) } else { SSQ_EB(R, A, Q, F, false, false) }
 #define SSQ_EB2(R, A, Q) \
   if (gamma) { SSQ_EB1(R, A, Q, true) } else { SSQ_EB1(R, A, Q, false) }
 #define SSQ_EB3(R, A) \
@@ -690,6 +797,7 @@ static int epilogue_bwd(const char* what, const float* g, const float* y, const 
 #undef SSQ_EB2
 #undef SSQ_EB1
 #undef SSQ_EB
+#undef SSQ_EB0
   int rc = check_launch(what);
   if (rc) return rc;
   if (loss) {

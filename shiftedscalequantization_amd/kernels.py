@@ -5,6 +5,7 @@ tensors on the HIP device; nothing here falls back to eager PyTorch arithmetic.
 Weight geometry: W is (Co, Ci, kh, kw) -> (Co, Ci, K=kh*kw), Linear (Co, Ci) -> K = 1.
 """
 import ctypes as C
+import os
 
 import torch
 
@@ -733,13 +734,21 @@ class BiasActFn(torch.autograd.Function):
         return gin, None, (gin if ctx.needs_input_grad[2] else None), None
 
 
+# The fused tail also on planes whose rows are not float4 rows (ResNet-18 layer4's 7x7), in
+# the kernel's scalar-row form: layer4.1 2114 it/s against 2085 with the three separate
+# passes, layer4.0 unchanged (profiles/r3_ab_knobs.txt).  A/B knob: SSQ_TAIL_SCALAR=0.
+TAIL_SCALAR = os.environ.get("SSQ_TAIL_SCALAR", "1") != "0"
+
+
 def _tail_ok(y, res):
-    """The fused tail (epilogue_loss_bwd) takes float4 rows: contiguous NCHW, hw % 4 == 0,
-    16-B aligned; the kernel's scalar-row form measured no faster on 7x7 planes
-    (profiles/r2_wgrad_gemm.log), so those run eagerly."""
-    return (y.dim() == 4 and (y.shape[2] * y.shape[3]) % 4 == 0 and y.is_contiguous()
-            and y.data_ptr() % 16 == 0
-            and (res is None or (res.is_contiguous() and res.data_ptr() % 16 == 0)))
+    """The fused tail (epilogue_loss_bwd) takes contiguous NCHW float4 rows (hw % 4 == 0,
+    16-B aligned), and scalar rows when TAIL_SCALAR is set."""
+    if not (y.dim() == 4 and y.is_contiguous() and (res is None or res.is_contiguous())):
+        return False
+    if TAIL_SCALAR:
+        return True
+    return ((y.shape[2] * y.shape[3]) % 4 == 0 and y.data_ptr() % 16 == 0
+            and (res is None or res.data_ptr() % 16 == 0))
 
 
 def bias_act(y, bias=None, res=None, relu=True, lazy=False):

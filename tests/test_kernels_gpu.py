@@ -1154,9 +1154,10 @@ def test_epilogue_loss_bwd_matches_separate_passes(K, hw, quant, relu):
     for t in [res, gamma, phi] + ([q.delta, q.zero_point] if quant else []):
         t.grad = None
     # fused
-    # the lazy placeholder carries exactly these inputs (taken on float4 rows only)
+    # the lazy placeholder carries exactly these inputs (taken on float4 rows, and on
+    # scalar rows while K.TAIL_SCALAR is set)
     lazy = K.epilogue(y, bias, gamma, phi, res, relu, q, lazy=True)
-    assert hasattr(lazy, "_ssq_tail") == (hw * hw % 4 == 0)
+    assert hasattr(lazy, "_ssq_tail") == (hw * hw % 4 == 0 or K.TAIL_SCALAR)
     tail = (y, bias, gamma, phi, res, relu, q)
     loss2, gy, gres, ggm, gph, gd, gz = K.epilogue_loss_bwd(tail, K.Rows(cache, idx), N * hw * hw)
     fused = [gy, gres, ggm, gph] + ([gd, gz] if quant else [])
