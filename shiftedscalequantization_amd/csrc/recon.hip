@@ -763,8 +763,9 @@ static int epilogue_bwd(const char* what, const float* g, const float* y, const 
   const bool vec = hw % 4 == 0 && al(g) && al(y) && al(gy) && (!res || al(res)) &&
                    (!gres || al(gres));
   SSQ_REQUIRE(relu >= 0 && relu <= 2, SSQ_E_ARG, "%s: activation code %d", what, relu);
-  // small planes (<= 64 elements or float4s per row): 4 rows per wave (same bits)
-  const bool multi = (vec ? hw / 4 : hw) <= kWave && epi_multi_row() >= (loss ? 2 : 1);
+  // small planes (<= 64 elements or float4s per row): 4 rows per wave (same bits); not with
+  // the act quantizer's four extra sums per row (3-4 waves per SIMD instead of 7-8)
+  const bool multi = (vec ? hw / 4 : hw) <= kWave && !delta && epi_multi_row() >= (loss ? 2 : 1);
   const int64_t rpw = multi ? 4 : 1;
   const int64_t waves = (rows + rpw - 1) / rpw;
   const uint32_t nmain = (uint32_t)((waves + kBlock / kWave - 1) / (kBlock / kWave));
@@ -780,7 +781,7 @@ static int epilogue_bwd(const char* what, const float* g, const float* y, const 
                      bias, gamma, phi, res, (uint32_t)rows, (uint32_t)C, (uint32_t)hw, delta, zp, \
                      lo, hi, gy, gres, part, fin, nmain, lidx, inv_m)
 #define SSQ_EB(R, A, Q, F, V, L) \
-  if (multi) SSQ_EB0(R, A, Q, F, V, L, 4); else SSQ_EB0(R, A, Q, F, V, L, 1);
+  if (multi) SSQ_EB0(R, A, Q, F, V, L, ((Q) ? 1 : 4)); else SSQ_EB0(R, A, Q, F, V, L, 1);
 #define SSQ_EB1(R, A, Q, F) \
   if (loss) { if (vec) { SSQ_EB(R, A, Q, F, true, true) } else { SSQ_EB(R, A, Q, F, false, true) } } \
   else if (vec) { SSQ_EB(R, A, Q, F, true, false) } else { SSQ_EB(R, A, Q, F, false, false) }
