@@ -1,13 +1,15 @@
-"""Per-iteration anatomy of the recon loop from a rocprofv3 kernel trace: finds the
-gather2 launches (one per iteration), and for each iteration window sums kernel busy
-time by kernel family; reports wall (gather-to-gather) vs GPU-busy time."""
+"""Per-iteration anatomy of the recon loop from a rocprofv3 kernel trace: finds the gather
+launches (gather2_kernel, or gather_shift_fwd -- the fused iteration start -- one per
+iteration), and for each iteration window sums kernel busy time by kernel family; reports
+wall (gather-to-gather) vs GPU-busy time."""
 import collections
 import csv
 import sys
 
 rows = list(csv.DictReader(open(sys.argv[1])))
 rows.sort(key=lambda r: int(r["Start_Timestamp"]))
-gi = [i for i, r in enumerate(rows) if "gather2_kernel" in r["Kernel_Name"]]
+gi = [i for i, r in enumerate(rows) if "gather2_kernel" in r["Kernel_Name"] or
+      "gather_shift_fwd" in r["Kernel_Name"]]
 # split into the two recon blocks by large gaps
 segments, cur = [], [gi[0]]
 for a, b in zip(gi, gi[1:]):
