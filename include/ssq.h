@@ -379,7 +379,7 @@ int ssq_flush_finalize(ssq_stream_t stream);
  * The caller must not read the queued What before that gather or flush.  Host state, not
  * thread-safe; ssq_set_deferred_prep_fwd returns the previous setting and launches nothing
  * (flush before turning it off).  Replaces nothing in the reference: the iteration start of
- * layer_recon_fused_shiftedScale.py:80-92 (batch draw, then the quantized forward). */
+ * layer_recon_fused_shiftedScale.py:94-100 (batch draw, then the quantized forward). */
 int ssq_set_deferred_prep_fwd(int on);
 int ssq_flush_prep_fwd(ssq_stream_t stream);
 
