@@ -4,8 +4,9 @@
  * memory owned by the caller (PyTorch's caching allocator in the Python host layer),
  * borrowed for the duration of the call.  Launches are asynchronous on `stream`
  * (a hipStream_t passed as void*); no entry point allocates or synchronizes, and none
- * keeps state except the opt-in deferred-finalize queue (ssq_set_deferred_finalize) and
- * the opt-in deferred prepared forward (ssq_set_deferred_prep_fwd), so
+ * keeps state except the opt-in deferred-finalize queue (ssq_set_deferred_finalize), the
+ * opt-in deferred prepared forward (ssq_set_deferred_prep_fwd) and the opt-in deferred
+ * multi-tensor q/dq (ssq_set_deferred_fq_multi), so
  * every call is graph-capturable.
  *
  * Return value: 0 on success; a negative SSQ_E* code for an argument error; otherwise
@@ -61,6 +62,17 @@ int ssq_fq_fwd_multi(int nseg, const float* const* x, float* const* y,
                      const float* const* delta, const float* const* zp,
                      const int64_t* n, const int64_t* inner, const int64_t* nch,
                      const int* qmin, const int* qmax, ssq_stream_t stream);
+/* With this deferral on, ssq_fq_fwd_multi (<= 48 segments) does not launch: it queues its
+ * table on its stream, and the next per-tensor ssq_fq_fwd on that stream (float4 path, no
+ * codes, the default streaming geometry) runs the table's tiles in extra workgroups of its
+ * own launch -- e.g. an activation cache and every weight of a network quantized in one
+ * launch (bench.py's step).  Same code: bit-identical outputs.  One table is queued at a
+ * time (a second call launches the first); ssq_flush_fq_multi launches a table still queued
+ * on `stream`.  The caller must not read the queued outputs before that launch or flush.
+ * Host state, not thread-safe; ssq_set_deferred_fq_multi returns the previous setting and
+ * launches nothing (flush before turning it off). */
+int ssq_set_deferred_fq_multi(int on);
+int ssq_flush_fq_multi(ssq_stream_t stream);
 
 /* STE backward of ssq_fq_fwd (autograd of quant_layer.py:92-98):
  *   gx = where(qmin <= rint(x/d)+zp <= qmax, gy*d, 0) / d

@@ -83,6 +83,8 @@ SIGNATURES = {
     "ssq_set_deferred_finalize": (_i, [_i]),
     "ssq_flush_finalize": (_i, [_p]),
     "ssq_set_deferred_prep_fwd": (_i, [_i]),
+    "ssq_set_deferred_fq_multi": (_i, [_i]),
+    "ssq_flush_fq_multi": (_i, [_p]),
     "ssq_flush_prep_fwd": (_i, [_p]),
     "ssq_conv_wgrad_set_form": (_i, [_i]),
     "ssq_conv_wgrad_kind": (_i, [_i64] * 10),

@@ -41,15 +41,15 @@ __device__ __forceinline__ uint32_t pack4(float a, float b, float c, float d) {
 // loads/stores.  chunk == 0: grid-stride; chunk > 0: workgroup b owns float4s
 // [b*chunk, (b+1)*chunk) and its threads stride through them.
 __device__ __forceinline__ void stream_range(int64_t n4, int64_t chunk, int64_t& i, int64_t& end,
-                                             int64_t& stride) {
+                                             int64_t& stride, uint32_t bid, uint32_t nblk) {
   if (chunk > 0) {
-    i = (int64_t)blockIdx.x * chunk + threadIdx.x;
-    end = min((int64_t)(blockIdx.x + 1) * chunk, n4);
+    i = (int64_t)bid * chunk + threadIdx.x;
+    end = min((int64_t)(bid + 1) * chunk, n4);
     stride = blockDim.x;
   } else {
-    i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    i = (int64_t)bid * blockDim.x + threadIdx.x;
     end = n4;
-    stride = (int64_t)gridDim.x * blockDim.x;
+    stride = (int64_t)nblk * blockDim.x;
   }
 }
 
@@ -74,13 +74,12 @@ __device__ __forceinline__ void fq_store4(f32x4 v, const QParams& p, f32x4* __re
 // of the wave's step is in its range -- one wave-uniform branch per step; otherwise (and
 // for an out-of-range delta) the IEEE divide.
 template <bool CODES, int UNROLL, bool NTL, bool NTS>
-__global__ __launch_bounds__(1024) void fq_fwd_pt(const f32x4* __restrict__ x,
-                                                  f32x4* __restrict__ y,
-                                                  uint32_t* __restrict__ codes,
-                                                  const float* __restrict__ delta,
-                                                  const float* __restrict__ zp, int64_t n4,
-                                                  float scale, float lo, float hi,
-                                                  int64_t chunk, int fastdiv) {
+__device__ __forceinline__ void fq_fwd_pt_body(const f32x4* __restrict__ x, f32x4* __restrict__ y,
+                                               uint32_t* __restrict__ codes,
+                                               const float* __restrict__ delta,
+                                               const float* __restrict__ zp, int64_t n4,
+                                               float scale, float lo, float hi, int64_t chunk,
+                                               int fastdiv, uint32_t bid, uint32_t nblk) {
   QParams p;
   p.d = __fmul_rn(delta[0], scale);
   p.z = zp[0];
@@ -88,7 +87,7 @@ __global__ __launch_bounds__(1024) void fq_fwd_pt(const f32x4* __restrict__ x,
   p.hi = hi;
   const float r = fastdiv ? recip_for_div(p.d) : 0.0f;
   int64_t i, end, stride;
-  stream_range(n4, chunk, i, end, stride);
+  stream_range(n4, chunk, i, end, stride, bid, nblk);
   for (; i + (UNROLL - 1) * stride < end; i += UNROLL * stride) {
     f32x4 v[UNROLL];
 #pragma unroll
@@ -109,6 +108,18 @@ __global__ __launch_bounds__(1024) void fq_fwd_pt(const f32x4* __restrict__ x,
     }
   }
   for (; i < end; i += stride) fq_store4<CODES, false>(x[i], p, y, codes, i);
+}
+
+template <bool CODES, int UNROLL, bool NTL, bool NTS>
+__global__ __launch_bounds__(1024) void fq_fwd_pt(const f32x4* __restrict__ x,
+                                                  f32x4* __restrict__ y,
+                                                  uint32_t* __restrict__ codes,
+                                                  const float* __restrict__ delta,
+                                                  const float* __restrict__ zp, int64_t n4,
+                                                  float scale, float lo, float hi,
+                                                  int64_t chunk, int fastdiv) {
+  fq_fwd_pt_body<CODES, UNROLL, NTL, NTS>(x, y, codes, delta, zp, n4, scale, lo, hi, chunk,
+                                          fastdiv, blockIdx.x, gridDim.x);
 }
 
 // General scalar path: any alignment, per-channel c = (i / inner) % nch.
@@ -207,15 +218,15 @@ inline uint32_t tile_channels(uint32_t tile, uint32_t min_inner) {
   return c < tile ? c : tile;
 }
 template <int U>
-__global__ __launch_bounds__(kBlock) void fq_fwd_multi_kernel(SegTable tab, uint32_t cap) {
+__device__ __forceinline__ void fq_fwd_multi_body(const SegTable& tab, uint32_t cap, uint32_t bid) {
   constexpr uint32_t TILE = U * 4 * kBlock;
   extern __shared__ float stage[];
   float* sd = stage;
   float* sz = stage + cap;
   int si = 0;
-  while (si + 1 < tab.nseg && blockIdx.x >= tab.s[si + 1].blk0) ++si;
+  while (si + 1 < tab.nseg && bid >= tab.s[si + 1].blk0) ++si;
   const Seg& sg = tab.s[si];
-  const uint32_t t0 = (blockIdx.x - sg.blk0) * TILE;
+  const uint32_t t0 = (bid - sg.blk0) * TILE;
   const uint32_t t1 = min(t0 + TILE, sg.n);
   const uint32_t c0 = fdiv(t0, sg.div_inner), c1 = fdiv(t1 - 1, sg.div_inner);
   for (uint32_t c = c0 + threadIdx.x; c <= c1; c += blockDim.x) {
@@ -269,6 +280,36 @@ __global__ __launch_bounds__(kBlock) void fq_fwd_multi_kernel(SegTable tab, uint
     sg.y[e] = fq1(sg.x[e], p, &q);
     if (sg.codes) sg.codes[e] = (uint8_t)((int)q & 0xff);
   }
+}
+
+template <int U>
+__global__ __launch_bounds__(kBlock) void fq_fwd_multi_kernel(SegTable tab, uint32_t cap) {
+  fq_fwd_multi_body<U>(tab, cap, blockIdx.x);
+}
+
+// A per-tensor q/dq (the activation cache) with a queued multi-tensor q/dq (the weights)
+// riding on the same launch (ssq_set_deferred_fq_multi): workgroups [0, npt) stream the
+// per-tensor part exactly as fq_fwd_pt with npt workgroups; the rest are the multi table's
+// tiles, which fill the CUs beside the streaming workgroups.  Same code, same bits.
+struct PtArgs {
+  const f32x4* x;
+  f32x4* y;
+  const float* delta;
+  const float* zp;
+  int64_t n4;
+  float scale, lo, hi;
+  int fastdiv;
+  uint32_t npt;
+};
+static_assert(sizeof(PtArgs) + sizeof(SegTable) + 16 <= 4096, "kernel arguments over 4 KiB");
+template <int UNROLL, bool NTL, bool NTS>
+__global__ __launch_bounds__(kBlock) void fq_fwd_pt_ride(PtArgs a, SegTable tab, uint32_t cap) {
+  if (blockIdx.x < a.npt) {
+    fq_fwd_pt_body<false, UNROLL, NTL, NTS>(a.x, a.y, nullptr, a.delta, a.zp, a.n4, a.scale,
+                                            a.lo, a.hi, 0, a.fastdiv, blockIdx.x, a.npt);
+    return;
+  }
+  fq_fwd_multi_body<kTile / 4 / kBlock>(tab, cap, blockIdx.x - a.npt);
 }
 
 // ------------------------------------------------------------------ backward
@@ -436,7 +477,7 @@ __global__ __launch_bounds__(1024) void copy_kernel(const f32x4* __restrict__ s,
                                                     f32x4* __restrict__ d, int64_t n4,
                                                     int64_t chunk) {
   int64_t i, end, stride;
-  stream_range(n4, chunk, i, end, stride);
+  stream_range(n4, chunk, i, end, stride, blockIdx.x, gridDim.x);
   for (; i + (UNROLL - 1) * stride < end; i += UNROLL * stride) {
     f32x4 v[UNROLL];
 #pragma unroll
@@ -560,6 +601,14 @@ struct FqPt {
   }
 };
 template <int U, bool NTL, bool NTS>
+struct FqPtRide {
+  static void go(dim3 g, dim3 b, hipStream_t s, const PtArgs& a, const SegTable& tab,
+                 uint32_t cap) {
+    hipLaunchKernelGGL((fq_fwd_pt_ride<U, NTL, NTS>), g, b, 2 * cap * sizeof(float), s, a, tab,
+                       cap);
+  }
+};
+template <int U, bool NTL, bool NTS>
 struct Copy {
   static void go(dim3 g, dim3 b, hipStream_t s, const f32x4* x, f32x4* y, int64_t n4,
                  int64_t chunk) {
@@ -568,6 +617,28 @@ struct Copy {
 };
 
 static bool aligned16(const void* p) { return ((uintptr_t)p & 15u) == 0; }
+
+// ------------------------------------------------------------------ deferred multi forward
+struct PendingFq {
+  bool on;
+  hipStream_t s;
+  SegTable tab;
+  uint32_t blk, cap;
+};
+static bool g_fq_defer = false;
+static PendingFq g_fq_pend{};
+
+static int launch_multi(hipStream_t s, const SegTable& tab, uint32_t blk, uint32_t cap) {
+  hipLaunchKernelGGL(fq_fwd_multi_kernel<kTile / 4 / kBlock>, dim3(blk), dim3(kBlock),
+                     2 * cap * sizeof(float), s, tab, cap);
+  return check_launch("ssq_fq_fwd_multi");
+}
+
+static int flush_fq(hipStream_t s) {
+  if (!g_fq_pend.on || g_fq_pend.s != s) return SSQ_OK;
+  g_fq_pend.on = false;
+  return launch_multi(s, g_fq_pend.tab, g_fq_pend.blk, g_fq_pend.cap);
+}
 
 }  // namespace ssq
 
@@ -602,7 +673,14 @@ extern "C" int ssq_fq_fwd(const float* x, float* y, void* codes, const float* de
       const f32x4* xv = (const f32x4*)x;
       f32x4* yv = (f32x4*)y;
       uint32_t* cv = (uint32_t*)codes;
-      if (codes)
+      if (!codes && chunk == 0 && block.x == (unsigned)kBlock && g_fq_pend.on &&
+          g_fq_pend.s == s) {
+        // a queued multi-tensor q/dq rides on this launch
+        const PendingFq f = g_fq_pend;
+        g_fq_pend.on = false;
+        const PtArgs a{xv, yv, delta, zp, n4, scale, lo, hi, v.rcp ? 1 : 0, grid.x};
+        launch_stream<FqPtRide>(v, dim3(grid.x + f.blk), block, s, a, f.tab, f.cap);
+      } else if (codes)
         launch_stream<FqPtCodes>(v, grid, block, s, xv, yv, cv, delta, zp, n4, scale, lo, hi,
                                  chunk, v.rcp ? 1 : 0);
       else
@@ -671,13 +749,31 @@ extern "C" int ssq_fq_fwd_multi(int nseg, const float* const* x, float* const* y
     }
     SSQ_REQUIRE(blk < (1ll << 31), SSQ_E_ARG, "ssq_fq_fwd_multi: too many tiles");
     const uint32_t cap = tile_channels(kTile, min_inner);
-    hipLaunchKernelGGL(fq_fwd_multi_kernel<kTile / 4 / kBlock>, dim3((unsigned)blk), dim3(kBlock),
-                       2 * cap * sizeof(float), (hipStream_t)stream, tab, cap);
-    const int rc = check_launch("ssq_fq_fwd_multi");
+    hipStream_t s = (hipStream_t)stream;
+    // a table still queued from an earlier call is launched first
+    int rc = g_fq_pend.on ? flush_fq(g_fq_pend.s) : SSQ_OK;
+    if (rc) return rc;
+    if (g_fq_defer && nseg <= kMaxSeg) {
+      g_fq_pend.on = true;
+      g_fq_pend.s = s;
+      g_fq_pend.tab = tab;
+      g_fq_pend.blk = (uint32_t)blk;
+      g_fq_pend.cap = cap;
+      return SSQ_OK;
+    }
+    rc = launch_multi(s, tab, (uint32_t)blk, cap);
     if (rc) return rc;
   }
   return SSQ_OK;
 }
+
+extern "C" int ssq_set_deferred_fq_multi(int on) {
+  const int prev = g_fq_defer ? 1 : 0;
+  g_fq_defer = on != 0;
+  return prev;
+}
+
+extern "C" int ssq_flush_fq_multi(ssq_stream_t stream) { return flush_fq((hipStream_t)stream); }
 
 extern "C" size_t ssq_fq_bwd_workspace_size(int64_t n, int64_t inner, int64_t nch) {
   (void)n;

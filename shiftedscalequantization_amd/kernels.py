@@ -176,6 +176,28 @@ def fake_quant_multi(xs, deltas, zps, n_bits, sym=False):
     return ys
 
 
+class deferred_fq_multi:
+    """Context: a fake_quant_multi inside it rides on the next per-tensor fake_quant_fwd of
+    its stream -- one launch for both (include/ssq.h ssq_set_deferred_fq_multi); a table
+    still queued at exit is launched then."""
+
+    def __init__(self, on=True, device=None):
+        self.on, self.device = on, device
+
+    def __enter__(self):
+        self.prev = bool(query("ssq_set_deferred_fq_multi", 1)) if self.on else None
+        return self
+
+    def __exit__(self, *exc):
+        if self.on:
+            dev_ = torch.device("cuda", torch.cuda.current_device()) if self.device is None \
+                else self.device
+            try:
+                call("ssq_flush_fq_multi", C.c_void_p(torch.cuda.current_stream(dev_).cuda_stream))
+            finally:
+                query("ssq_set_deferred_fq_multi", int(self.prev))
+
+
 # ------------------------------------------------------------------ K3/K4
 def scale_init(x, n_bits, sym=False, channel_wise=False, method="max", return_scores=False):
     """init_quantization_scale (quant_layer.py:100-166) on the device.

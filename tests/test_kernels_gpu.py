@@ -1033,6 +1033,36 @@ def test_adashift_prepared_multi_equals_single(K):
         np.testing.assert_array_equal(host(v), v1, err_msg=str(shapes[k]))
 
 
+def test_weights_qdq_ride_on_activation_qdq(K):
+    """A deferred multi-tensor q/dq (K.deferred_fq_multi: per-channel W2 / W8 weights of
+    several shapes, scalar-tail ones included) runs inside the next per-tensor q/dq launch:
+    both outputs bit-identical to the separate launches; a table with no per-tensor launch
+    after it is launched when the context ends."""
+    gen = torch.Generator().manual_seed(9)
+    act = torch.randn(7, 64, 56, 56, generator=gen).relu().cuda()
+    d_a, z_a, _ = K.scale_init(act[:2], 4, False, False, "max")
+    shapes = [(64, 3, 7, 7), (64, 64, 3, 3), (128, 64, 1, 1), (1000, 512), (33, 5, 3, 3)]
+    ws, ds, zs, bits = [], [], [], []
+    for k, shape in enumerate(shapes):
+        w = (torch.randn(shape, generator=gen) * 0.05).cuda()
+        b = 8 if k in (0, 3) else 2
+        d, z, _ = K.scale_init(w, b, False, True, "max")
+        ws.append(w), ds.append(d), zs.append(z), bits.append(b)
+    ref_w = K.fake_quant_multi(ws, ds, zs, bits)
+    ref_a, _ = K.fake_quant_fwd(act, d_a, z_a, 4)
+    with K.deferred_fq_multi():
+        got_w = K.fake_quant_multi(ws, ds, zs, bits)
+        got_a, _ = K.fake_quant_fwd(act, d_a, z_a, 4)
+    torch.cuda.synchronize()
+    assert torch.equal(ref_a, got_a)
+    for a, b in zip(ref_w, got_w):
+        assert torch.equal(a, b)
+    with K.deferred_fq_multi():
+        late = K.fake_quant_multi(ws, ds, zs, bits)
+    for a, b in zip(ref_w, late):
+        assert torch.equal(a, b)
+
+
 def test_prepared_forward_rides_on_gather(K):
     """A deferred prepared forward (K.deferred_prep_fwd) runs inside the next batch gather's
     launch: the What of every segment and the gathered rows are bit-identical to the two

@@ -10,8 +10,8 @@ import json
 import os
 import sys
 
-KERNELS = {"fq_fwd_pt": "ssq::fq_fwd_pt<", "fq_fwd_multi": "fq_fwd_multi_kernel",
-           "stream_copy": "ssq::copy_kernel<"}
+KERNELS = {"fq_fwd_pt": "ssq::fq_fwd_pt<", "fq_fwd_pt_ride": "ssq::fq_fwd_pt_ride<",
+           "fq_fwd_multi": "fq_fwd_multi_kernel", "stream_copy": "ssq::copy_kernel<"}
 
 
 def per_dispatch(d, counter):
