@@ -5,8 +5,9 @@
  * borrowed for the duration of the call.  Launches are asynchronous on `stream`
  * (a hipStream_t passed as void*); no entry point allocates or synchronizes, and none
  * keeps state except the opt-in deferred-finalize queue (ssq_set_deferred_finalize), the
- * opt-in deferred prepared forward (ssq_set_deferred_prep_fwd) and the opt-in deferred
- * multi-tensor q/dq (ssq_set_deferred_fq_multi), so
+ * opt-in deferred prepared forward (ssq_set_deferred_prep_fwd), the opt-in deferred
+ * multi-tensor q/dq (ssq_set_deferred_fq_multi) and the armed optimizer step
+ * (ssq_adam_arm), so
  * every call is graph-capturable.
  *
  * Return value: 0 on success; a negative SSQ_E* code for an argument error; otherwise
@@ -366,6 +367,19 @@ int ssq_adam(int nseg, float* const* p, const float* const* g, float* const* m,
              float* const* v, const int64_t* n, float one_minus_beta1, float beta2,
              float one_minus_beta2, float eps, const float* hyper, float neg_step_size,
              float bias_correction2_sqrt, ssq_stream_t stream);
+/* The same step, armed instead of launched: ssq_adam_arm records the nseg parameters
+ * (p, m, v, n; hyper is required) for `stream`; the next prepared alpha backward on that
+ * stream applies the step where each gradient is finalised -- the alpha segments of that
+ * launch in their finalisers, gamma^z / phi^z (parameters whose gradients the epilogue
+ * backward entry points of that stream produce) in their finalize tasks -- when it can
+ * cover EVERY armed parameter, and attaches nothing otherwise.  Same update, same fp32
+ * operations as ssq_adam: bit-identical.  ssq_adam_take returns 1 when the armed step ran
+ * inside a launch (nothing left to do) and 0 when it did not (the caller launches ssq_adam);
+ * either way it disarms.  The gradients are still written.  Host state, not thread-safe. */
+int ssq_adam_arm(int nseg, float* const* p, float* const* m, float* const* v, const int64_t* n,
+                 float one_minus_beta1, float beta2, float one_minus_beta2, float eps,
+                 const float* hyper, ssq_stream_t stream);
+int ssq_adam_take(ssq_stream_t stream);
 
 /* ---------------------------------------------------------------- deferred finalizes
  * With deferral on, ssq_lp_loss[_rows] (loss value) and ssq_epilogue_bwd (gamma/phi and act

@@ -80,6 +80,8 @@ SIGNATURES = {
     "ssq_epilogue_loss_bwd": (_i, [_p, _p, _i64, _p, _p, _p, _p, _p, _p, _i64, _i64, _i64, _i,
                                    _p, _p, _i, _i, _p, _p, _p, _p, _p, _p, _p, _sz, _p]),
     "ssq_adam": (_i, [_i, _p, _p, _p, _p, _p, _f, _f, _f, _f, _p, _f, _f, _p]),
+    "ssq_adam_arm": (_i, [_i, _p, _p, _p, _p, _f, _f, _f, _f, _p, _p]),
+    "ssq_adam_take": (_i, [_p]),
     "ssq_set_deferred_finalize": (_i, [_i]),
     "ssq_flush_finalize": (_i, [_p]),
     "ssq_set_deferred_prep_fwd": (_i, [_i]),

@@ -135,11 +135,17 @@ struct PrepSeg {
   uint32_t wave0;    // first wave of this segment (stage 2: one wave per input channel)
   uint32_t stage2;   // its chunks are reduced by the stage-2 launch
   float lo, hi;
+  float* alpha_w;    // fused optimizer step (ssq_adam_arm): alpha, its Adam m / v (or null)
+  float* am;
+  float* av;
 };
 struct PrepTable {
   PrepSeg s[kMaxPrepSeg];
   int nseg;
+  AdamConst ac;
 };
+static_assert(kMaxPrepSeg <= kMaxAdamSegs, "adam_attach covers one launch's segments");
+static_assert(sizeof(PrepTable) + sizeof(FinTable) + 64 <= 4096, "kernel arguments over 4 KiB");
 
 // the segment of workgroup (or wave) `id` (uniform: the table is read with scalar loads
 // from the kernel arguments, as ssq_adam's)
@@ -260,9 +266,9 @@ __device__ __forceinline__ void alpha_accumulate(uint32_t fw, float h, float d, 
 // terms in shift order (value and gradient), then the softmax/clamp backward -- the same
 // values in the same order as alpha_chain.
 template <int NS>
-__device__ __forceinline__ void alpha_finalize(const PrepSeg& sg, uint32_t ci, const float* a,
-                                               const double* tot_in, float reg_lambda,
-                                               float reg_b) {
+__device__ __forceinline__ void alpha_finalize(const PrepSeg& sg, const AdamConst& ac, uint32_t ci,
+                                               const float* a, const double* tot_in,
+                                               float reg_lambda, float reg_b) {
   double tot[kMaxS];
 #pragma unroll
   for (int i = 0; i < NS; ++i) tot[i] = tot_in[i];
@@ -284,6 +290,11 @@ __device__ __forceinline__ void alpha_finalize(const PrepSeg& sg, uint32_t ci, c
 #pragma unroll
   for (int i = 0; i < NS; ++i) sg.galpha[(size_t)ci * NS + i] = ga[i];
   if (sg.reg_vals) sg.reg_vals[ci] = reg;
+  if (sg.am) {                        // the fused optimizer step: this channel's S entries
+    const AdamRef r{sg.alpha_w, sg.am, sg.av};
+#pragma unroll
+    for (int i = 0; i < NS; ++i) adam_apply(ac, r, (uint32_t)(ci * NS + i), ga[i]);
+  }
 }
 
 // Wave-column alpha backward (bwd_tiling_prep form 1, Co <= 64).  Lane l of wave w owns
@@ -293,9 +304,9 @@ __device__ __forceinline__ void alpha_finalize(const PrepSeg& sg, uint32_t ci, c
 // are then added in fixed order (waves per column, then taps) and lane t < nci of wave 0
 // finalises channel ci0 + t.
 template <int NS>
-__device__ __forceinline__ void alpha_bwd_wavecol(const PrepSeg& sg, uint32_t local, double* red,
-                                                  float reg_lambda, float reg_b,
-                                                  const float* __restrict__ reg_dev) {
+__device__ __forceinline__ void alpha_bwd_wavecol(const PrepSeg& sg, const AdamConst& ac,
+                                                  uint32_t local, double* red, float reg_lambda,
+                                                  float reg_b, const float* __restrict__ reg_dev) {
   const Geo& g = sg.g;
   constexpr uint32_t kW = kBlock / kWave;
   const uint32_t ci0 = local * sg.tl.ncb, nci = min(sg.tl.ncb, g.Ci - ci0);
@@ -400,7 +411,7 @@ __device__ __forceinline__ void alpha_bwd_wavecol(const PrepSeg& sg, uint32_t lo
       }
     }
   }
-  if (fin_lane) alpha_finalize<NS>(sg, ci0 + lane, af, tot, reg_lambda, reg_b);
+  if (fin_lane) alpha_finalize<NS>(sg, ac, ci0 + lane, af, tot, reg_lambda, reg_b);
 }
 
 // Backward, one launch for every segment: wave-column segments finish here; the
@@ -423,7 +434,7 @@ __global__ __launch_bounds__(kBlock) void alpha_bwd_prep(PrepTable tab, float re
   const Geo& g = sg.g;
   const uint32_t local = bid - sg.blk0;
   if (sg.tl.form == 1) {             // uniform per workgroup
-    alpha_bwd_wavecol<NS>(sg, local, red, reg_lambda, reg_b, reg_dev);
+    alpha_bwd_wavecol<NS>(sg, tab.ac, local, red, reg_lambda, reg_b, reg_dev);
     return;
   }
   const uint32_t bx = local % sg.tl.ncolblk, by = local / sg.tl.ncolblk;
@@ -549,6 +560,11 @@ __global__ __launch_bounds__(kBlock) void alpha_bwd_prep_stage2(PrepTable tab, f
 #pragma unroll
   for (int i = 0; i < NS; ++i) sg.galpha[(size_t)ci * NS + i] = ga[i];
   if (sg.reg_vals) sg.reg_vals[ci] = reg;
+  if (sg.am) {                        // the fused optimizer step
+    const AdamRef r{sg.alpha_w, sg.am, sg.av};
+#pragma unroll
+    for (int i = 0; i < NS; ++i) adam_apply(tab.ac, r, (uint32_t)(ci * NS + i), ga[i]);
+  }
 }
 
 // ------------------------------------------------------------------ host side
@@ -583,6 +599,7 @@ static int make_seg(const SegArgs& a, int i, PrepSeg& sg, const char* what) {
   sg.part = nullptr;
   sg.galpha = nullptr;
   sg.reg_vals = nullptr;
+  sg.alpha_w = sg.am = sg.av = nullptr;
   sg.tl = col_tiling_prep(sg.g);
   sg.lo = (float)a.qmin[i];
   sg.hi = (float)a.qmax[i];
@@ -796,10 +813,21 @@ extern "C" int ssq_adashift_bwd_prepared_multi(
     const unsigned blocks2 = (waves + kBlock / kWave - 1) / (kBlock / kWave);
     // queued finalize tasks of this stream ride on the first launch (their inputs live in
     // their producers' own workspace slots, not in this one)
-    FinTable fin;
-    fin.n = 0;
-    fin.nwg = 0;
+    FinTable fin{};
     if (base == 0) fin = fin_take(s);
+    tab.ac = AdamConst{};
+    if (base == 0 && nseg <= kMaxPrepSeg) {
+      // the loop's armed optimizer step, when this launch can take all of it (fin_tasks.h)
+      int64_t len[kMaxPrepSeg];
+      AdamRef refs[kMaxPrepSeg];
+      for (int k = 0; k < tab.nseg; ++k) len[k] = Ci[k] * S;
+      if (adam_attach(s, tab.nseg, alpha, len, refs, fin, &tab.ac))
+        for (int k = 0; k < tab.nseg; ++k) {
+          tab.s[k].alpha_w = refs[k].p;
+          tab.s[k].am = refs[k].m;
+          tab.s[k].av = refs[k].v;
+        }
+    }
 #define SSQ_BWDP(NS)                                                                          \
   do {                                                                                        \
     hipLaunchKernelGGL((alpha_bwd_prep<NS>), dim3(blk + fin.nwg), dim3(kBlock), 0, s, tab,    \

@@ -34,20 +34,47 @@ constexpr uint32_t kFinBatch = 16;  // loads in flight per thread in the row-wal
 constexpr int kEpiParts = 7;        // doubles per (n, c) row of the epilogue backward
                                     // (slot 6: the fused tail's loss partial)
 
+// The recon loop's optimizer step applied where each gradient is finalised (ssq_adam_arm):
+// ssq_adam's update, torch.optim.Adam's single-tensor step, op for op.
+struct AdamConst {
+  float w1, b2, w2, eps;     // 1 - beta1, beta2, 1 - beta2, eps
+  const float* hyper;        // device (-lr/bc1, sqrt(bc2)) of this step
+};
+struct AdamRef {
+  float* p;                  // the parameter (nullptr: no fused step)
+  float* m;
+  float* v;
+};
+__device__ __forceinline__ void adam_apply(const AdamConst& c, const AdamRef& r, uint32_t e,
+                                           float g) {
+  const float nss = c.hyper[0], bc2s = c.hyper[1];
+  float m = r.m[e], v = r.v[e];
+  m = __fadd_rn(m, __fmul_rn(c.w1, __fsub_rn(g, m)));
+  v = __fadd_rn(__fmul_rn(v, c.b2), __fmul_rn(__fmul_rn(c.w2, g), g));
+  const float denom = __fadd_rn(__fdiv_rn(__fsqrt_rn(v), bc2s), c.eps);
+  r.p[e] = __fadd_rn(r.p[e], __fdiv_rn(__fmul_rn(nss, m), denom));
+  r.m[e] = m;
+  r.v[e] = v;
+}
+
 struct FinTask {
   int kind;                  // 0: lp_loss value, 1: epilogue backward sums,
-                             // 2: loss value from the epilogue rows (fused tail)
+                             // 2: loss value from the epilogue rows (fused tail),
+                             // 3: the fused Adam step of one final gradient (o[0], a elems)
   uint32_t nwg;              // workgroups the task takes
   const double* part;
-  uint32_t a, b, c;          // loss: nblk; epilogue: N, C, nb; rows loss: rows
+  uint32_t a, b, c;          // loss: nblk; epilogue: N, C, nb; rows loss: rows; adam: n
   double m;                  // loss: M
-  float* o[4];               // loss: o[0]; epilogue: ggamma, gphi, gdelta, gzp
+  float* o[4];               // loss: o[0]; epilogue: ggamma, gphi, gdelta, gzp; adam: grad
+  AdamRef ad[2];             // epilogue: the gamma / phi step fused in; adam: ad[0]
 };
-constexpr int kMaxFin = 4;
+constexpr int kMaxFin = 12;
+constexpr int kMaxAdamSegs = 8;      // alpha segments of one prepared alpha-backward launch
 struct FinTable {
   FinTask t[kMaxFin];
   int n;
   uint32_t nwg;
+  AdamConst ac;
 };
 
 // lp_loss value: the workgroup partials summed in index order (every load issued first)
@@ -76,7 +103,8 @@ constexpr uint32_t kEpiChan = kBlock / 4;
 __device__ __forceinline__ void fin_epi(uint32_t bid, const double* __restrict__ part, uint32_t N,
                                         uint32_t C, uint32_t nb, float* __restrict__ ggamma,
                                         float* __restrict__ gphi, float* __restrict__ gdelta,
-                                        float* __restrict__ gzp) {
+                                        float* __restrict__ gzp, const AdamConst& ac,
+                                        const AdamRef* ad) {
   __shared__ double red[16];
   if (bid < nb) {
     __shared__ double wsum[4][kEpiChan][2];
@@ -98,6 +126,8 @@ __device__ __forceinline__ void fin_epi(uint32_t bid, const double* __restrict__
       sp = wsum[0][cl][1] + wsum[1][cl][1] + wsum[2][cl][1] + wsum[3][cl][1];
       if (ggamma) ggamma[c] = (float)sg;
       if (gphi) gphi[c] = (float)sp;
+      if (ad[0].p) adam_apply(ac, ad[0], c, (float)sg);
+      if (ad[1].p) adam_apply(ac, ad[1], c, (float)sp);
     }
     return;
   }
@@ -148,6 +178,12 @@ __device__ __forceinline__ void fin_loss_rows(const double* __restrict__ part, u
   if (threadIdx.x == 0) out[0] = (float)(a / m);
 }
 
+// the fused Adam step of one final gradient (small tensors: gamma^z / phi^z), one workgroup
+__device__ __forceinline__ void fin_adam(const AdamConst& ac, const AdamRef& r,
+                                         const float* __restrict__ g, uint32_t n) {
+  for (uint32_t e = threadIdx.x; e < n; e += kBlock) adam_apply(ac, r, e, g[e]);
+}
+
 // Workgroup k of the table's tasks (k < ft.nwg).
 __device__ __forceinline__ void run_fin(const FinTable& ft, uint32_t k) {
   for (int i = 0; i < ft.n; ++i) {
@@ -156,9 +192,11 @@ __device__ __forceinline__ void run_fin(const FinTable& ft, uint32_t k) {
       if (t.kind == 0)
         fin_loss(t.part, (int)t.a, t.m, t.o[0]);
       else if (t.kind == 1)
-        fin_epi(k, t.part, t.a, t.b, t.c, t.o[0], t.o[1], t.o[2], t.o[3]);
-      else
+        fin_epi(k, t.part, t.a, t.b, t.c, t.o[0], t.o[1], t.o[2], t.o[3], ft.ac, t.ad);
+      else if (t.kind == 2)
         fin_loss_rows(t.part, t.a, t.m, t.o[0]);
+      else
+        fin_adam(ft.ac, t.ad[0], t.o[0], t.a);
       return;
     }
     k -= t.nwg;
@@ -166,6 +204,14 @@ __device__ __forceinline__ void run_fin(const FinTable& ft, uint32_t k) {
 }
 
 // host side (recon.hip)
+// The armed optimizer step (ssq_adam_arm) of stream s, attached to the alpha-backward launch
+// about to run (nseg segments of parameters alpha[i], len[i] elements; ft = the finalize
+// tasks riding on it): true when every armed parameter's update can run inside that launch
+// -- alpha in its finaliser (refs[i]), gamma^z / phi^z in their riding finalize task or as
+// extra kind-3 tasks appended to ft (gradients finished by earlier launches) -- and then
+// the attachments are made and *ac filled; false (nothing attached) otherwise.
+bool adam_attach(hipStream_t s, int nseg, const float* const* alpha, const int64_t* len,
+                 AdamRef* refs, FinTable& ft, AdamConst* ac);
 bool fin_defer_on();
 int fin_push(hipStream_t s, const FinTask& t);   // queue (flushes first when full)
 FinTable fin_take(hipStream_t s);                // remove and return the stream's pending tasks

@@ -482,7 +482,8 @@ __global__ __launch_bounds__(kBlock) void epilogue_bwd_finalize(
     const double* __restrict__ part, uint32_t N, uint32_t C, uint32_t nb,
     float* __restrict__ ggamma, float* __restrict__ gphi, float* __restrict__ gdelta,
     float* __restrict__ gzp) {
-  fin_epi(blockIdx.x, part, N, C, nb, ggamma, gphi, gdelta, gzp);
+  const AdamRef none[2] = {AdamRef{}, AdamRef{}};
+  fin_epi(blockIdx.x, part, N, C, nb, ggamma, gphi, gdelta, gzp, AdamConst{}, none);
 }
 
 // the queued finalize tasks of a stream as one standalone launch
@@ -503,7 +504,7 @@ static int g_fin_npending = 0;
 bool fin_defer_on() { return g_fin_defer; }
 
 FinTable fin_take(hipStream_t s) {
-  FinTable ft;
+  FinTable ft{};
   ft.n = 0;
   ft.nwg = 0;
   int keep = 0;
@@ -546,6 +547,100 @@ int fin_push(hipStream_t s, const FinTask& t) {
   return SSQ_OK;
 }
 
+// ------------------------------------------------------------------ armed optimizer step
+// ssq_adam_arm records the loop's Adam parameters; the epilogue backward entry points log
+// the gradient tensors they produce for armed gamma^z / phi^z (gradient pointer per
+// parameter pointer); the next alpha-backward launch of the stream attaches the whole step
+// (adam_attach) or nothing; ssq_adam_take reports which.
+constexpr int kMaxArmed = 32;
+constexpr uint32_t kMaxRideAdam = 4096;   // elements of a final gradient a kind-3 task takes
+struct ArmedAdam {
+  bool on, consumed;
+  hipStream_t s;
+  int n;
+  float* p[kMaxArmed];
+  float* m[kMaxArmed];
+  float* v[kMaxArmed];
+  int64_t len[kMaxArmed];
+  const float* g[kMaxArmed];    // logged final gradient (gamma^z / phi^z), or null
+  AdamConst c;
+};
+static ArmedAdam g_armed{};
+
+static int armed_index(const void* p) {
+  for (int k = 0; k < g_armed.n; ++k)
+    if (g_armed.p[k] == p) return k;
+  return -1;
+}
+
+// an epilogue backward on stream s produces the gradients of (gamma, phi)
+static void adam_log(hipStream_t s, const float* gamma, const float* phi, const float* ggamma,
+                     const float* gphi) {
+  if (!g_armed.on || g_armed.s != s) return;
+  const int kg = gamma && ggamma ? armed_index(gamma) : -1;
+  const int kp = phi && gphi ? armed_index(phi) : -1;
+  if (kg >= 0) g_armed.g[kg] = ggamma;
+  if (kp >= 0) g_armed.g[kp] = gphi;
+}
+
+bool adam_attach(hipStream_t s, int nseg, const float* const* alpha, const int64_t* len,
+                 AdamRef* refs, FinTable& ft, AdamConst* ac) {
+  if (!g_armed.on || g_armed.s != s || g_armed.consumed || nseg > kMaxAdamSegs) return false;
+  bool covered[kMaxArmed] = {};
+  int seg_k[kMaxAdamSegs];
+  for (int i = 0; i < nseg; ++i) {
+    const int k = armed_index(alpha[i]);
+    seg_k[i] = k;
+    if (k >= 0 && g_armed.len[k] == len[i]) covered[k] = true;
+    else seg_k[i] = -1;
+  }
+  int ride_k[kMaxFin][2];
+  for (int t = 0; t < ft.n; ++t) {
+    ride_k[t][0] = ride_k[t][1] = -1;
+    if (ft.t[t].kind != 1) continue;
+    for (int j = 0; j < 2; ++j) {
+      const float* gout = ft.t[t].o[j];
+      for (int k = 0; k < g_armed.n && gout; ++k)
+        if (g_armed.g[k] == gout) {
+          ride_k[t][j] = k;
+          covered[k] = true;
+        }
+    }
+  }
+  int extra[kMaxArmed], ne = 0;
+  for (int k = 0; k < g_armed.n; ++k) {
+    if (covered[k]) continue;
+    if (!g_armed.g[k] || g_armed.len[k] > (int64_t)kMaxRideAdam) return false;
+    extra[ne++] = k;
+  }
+  if (ft.n + ne > kMaxFin) return false;
+  // every armed parameter is covered: attach
+  for (int i = 0; i < nseg; ++i) {
+    const int k = seg_k[i];
+    refs[i] = k >= 0 ? AdamRef{g_armed.p[k], g_armed.m[k], g_armed.v[k]} : AdamRef{};
+  }
+  for (int t = 0; t < ft.n; ++t)
+    for (int j = 0; j < 2; ++j) {
+      const int k = ft.t[t].kind == 1 ? ride_k[t][j] : -1;
+      ft.t[t].ad[j] = k >= 0 ? AdamRef{g_armed.p[k], g_armed.m[k], g_armed.v[k]} : AdamRef{};
+    }
+  for (int e = 0; e < ne; ++e) {
+    const int k = extra[e];
+    FinTask t{};
+    t.kind = 3;
+    t.nwg = 1;
+    t.a = (uint32_t)g_armed.len[k];
+    t.o[0] = (float*)g_armed.g[k];
+    t.ad[0] = AdamRef{g_armed.p[k], g_armed.m[k], g_armed.v[k]};
+    ft.t[ft.n++] = t;
+    ft.nwg += 1;
+  }
+  ft.ac = g_armed.c;
+  *ac = g_armed.c;
+  g_armed.consumed = true;
+  return true;
+}
+
 // A host launch about to write [w0, w0 + wn): tasks that read it are launched standalone
 // first; the rest are handed to the host.
 static FinTable fin_take_for_host(hipStream_t s, const void* w0, size_t wn, int* rc) {
@@ -556,7 +651,7 @@ static FinTable fin_take_for_host(hipStream_t s, const void* w0, size_t wn, int*
     const char* a = (const char*)pf.t.part;
     if (a >= (const char*)w0 && a < (const char*)w0 + wn) {
       *rc = fin_flush(s);
-      FinTable none;
+      FinTable none{};
       none.n = 0;
       none.nwg = 0;
       return none;
@@ -812,7 +907,7 @@ static int epilogue_bwd(const char* what, const float* g, const float* y, const 
     if (fin_defer_on()) {
       rc = fin_push(s, t);
     } else {
-      FinTable one;
+      FinTable one{};
       one.t[0] = t;
       one.n = 1;
       one.nwg = 1;
@@ -821,6 +916,7 @@ static int epilogue_bwd(const char* what, const float* g, const float* y, const 
     }
     if (rc) return rc;
   }
+  adam_log(s, gamma, phi, ggamma, gphi);
   if (ggamma || gphi || gdelta || gzp) {
     // blocks [0, nb) only when gamma / phi are wanted; block nb (the act quantizer's four
     // sums over every row, one workgroup) only when delta / zp are
@@ -898,6 +994,36 @@ extern "C" int ssq_relu_bwd(const float* g, const float* out, float* gin, int64_
 extern "C" int ssq_relu6_bwd(const float* g, const float* out, float* gin, int64_t n,
                              ssq_stream_t stream) {
   return act_bwd<2>("ssq_relu6_bwd", g, out, gin, n, (hipStream_t)stream);
+}
+
+extern "C" int ssq_adam_arm(int nseg, float* const* p, float* const* m, float* const* v,
+                            const int64_t* n, float one_minus_beta1, float beta2,
+                            float one_minus_beta2, float eps, const float* hyper,
+                            ssq_stream_t stream) {
+  SSQ_REQUIRE(nseg >= 1 && nseg <= kMaxArmed && p && m && v && n && hyper, SSQ_E_ARG,
+              "ssq_adam_arm: 1 <= nseg <= %d, non-null arrays and device hyper required",
+              kMaxArmed);
+  ArmedAdam a{};
+  a.on = true;
+  a.s = (hipStream_t)stream;
+  a.n = nseg;
+  for (int k = 0; k < nseg; ++k) {
+    SSQ_REQUIRE(p[k] && m[k] && v[k] && n[k] >= 1, SSQ_E_ARG, "ssq_adam_arm: segment %d", k);
+    a.p[k] = p[k];
+    a.m[k] = m[k];
+    a.v[k] = v[k];
+    a.len[k] = n[k];
+  }
+  a.c = AdamConst{one_minus_beta1, beta2, one_minus_beta2, eps, hyper};
+  g_armed = a;
+  return SSQ_OK;
+}
+
+extern "C" int ssq_adam_take(ssq_stream_t stream) {
+  const bool mine = g_armed.on && g_armed.s == (hipStream_t)stream;
+  const int done = mine && g_armed.consumed ? 1 : 0;
+  if (mine) g_armed = ArmedAdam{};
+  return done;
 }
 
 extern "C" int ssq_adam(int nseg, float* const* p, const float* const* g, float* const* m,

@@ -1059,6 +1059,31 @@ def adam_step(params, grads, exp_avgs, exp_avg_sqs, beta1, beta2, eps, hyper=Non
          float(eps), _vp(hyper), float(neg_step_size), float(bc2_sqrt), stream_of(params[0]))
 
 
+def adam_arm(params, exp_avgs, exp_avg_sqs, beta1, beta2, eps, hyper):
+    """Arm one Adam step of `params` (include/ssq.h ssq_adam_arm): the next prepared alpha
+    backward on the current stream applies it where the gradients are finalised, when it
+    can take all of it.  adam_take() then says whether it did."""
+    n = len(params)
+    P = C.c_void_p * n
+    pa, ma, va = P(), P(), P()
+    na = (C.c_int64 * n)()
+    for k, (p_, m_, v_) in enumerate(zip(params, exp_avgs, exp_avg_sqs)):
+        for t, nm in ((p_, "param"), (m_, "exp_avg"), (v_, "exp_avg_sq")):
+            A.check(t, nm)
+            if not t.is_contiguous():
+                raise A.SSQError(f"adam_arm: {nm} must be contiguous")
+        pa[k], ma[k], va[k] = p_.data_ptr(), m_.data_ptr(), v_.data_ptr()
+        na[k] = p_.numel()
+    call("ssq_adam_arm", n, pa, ma, va, na, float(1 - beta1), float(beta2), float(1 - beta2),
+         float(eps), _vp(hyper), stream_of(params[0]))
+
+
+def adam_take(device=None):
+    """True when the armed Adam step ran inside a launch; disarms either way."""
+    dev_ = torch.device("cuda", torch.cuda.current_device()) if device is None else device
+    return bool(query("ssq_adam_take", C.c_void_p(torch.cuda.current_stream(dev_).cuda_stream)))
+
+
 def stream_copy(src, dst):
     call("ssq_stream_copy", _vp(src), _vp(dst), src.numel(), stream_of(src))
 

@@ -171,7 +171,22 @@ class SsqAdam:
         b1, b2 = g["betas"]
         return -(g["lr"] / (1 - b1 ** self.t)), (1 - b2 ** self.t) ** 0.5
 
+    def arm(self, hyper):
+        """Arm this step inside the next prepared alpha backward (K.adam_arm): the update
+        then runs where each gradient is finalised, no Adam launch of its own; step()
+        launches it only if that did not happen.  World 1 only (at world > 1 the gradients
+        are all-reduced between the backward and the step)."""
+        g = self.param_groups[0]
+        b1, b2 = g["betas"]
+        K.adam_arm(self.params, [self.state[p]["exp_avg"] for p in self.params],
+                   [self.state[p]["exp_avg_sq"] for p in self.params], b1, b2, g["eps"], hyper)
+        self._armed = True
+
     def step(self, hyper=None):
+        if getattr(self, "_armed", False):
+            self._armed = False
+            if K.adam_take(self.params[0].device):
+                return
         live = [p for p in self.params if p.grad is not None]
         if not live:
             return

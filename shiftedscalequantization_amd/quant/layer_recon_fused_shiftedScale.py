@@ -28,6 +28,8 @@ from .quant_layer import QuantModule
 DEFER_FINALIZE = True
 # the iteration's prepared adaShift forward rides on its batch gather (K.deferred_prep_fwd)
 FUSE_START = True
+# world 1: the Adam step rides on the alpha backward's launch (SsqAdam.arm, ssq_adam_arm)
+FUSE_ADAM = True
 # A/B knob: the block's final epilogue + loss + its backward as one pass (bit-identical)
 FUSE_TAIL = True
 
@@ -138,6 +140,8 @@ def _fused_loop(block, modules, iters, lmda, model, p, lr, bias_cal, batch_size,
 
     # the fused tail (K.epilogue_loss_bwd) needs the p = 2 loss (the reference's default)
     fuse_tail = FUSE_TAIL and on_gpu and float(p) == 2.0
+    # world 1: Adam runs where the gradients are finalised (no launch of its own)
+    fuse_adam = FUSE_ADAM and on_gpu and bucket is None
 
     def body_pre():
         """One iteration on the device up to its exchange step: gather -> forward -> fused
@@ -150,6 +154,9 @@ def _fused_loop(block, modules, iters, lmda, model, p, lr, bias_cal, batch_size,
             # a deferred gamma/phi gradient is only final after the next backward launch:
             # AccumulateGrad must take it over, never add it into an existing .grad
             raise RuntimeError("deferred finalizes need every parameter's .grad unset")
+        if fuse_adam:
+            # the optimizer step runs inside the alpha backward's launch (SsqAdam.arm)
+            optimizer.arm(hyper)
         # every conv's What (one table) and the batch gather in ONE launch
         with K.deferred_prep_fwd(on_gpu and FUSE_START):
             if on_gpu:

@@ -1194,3 +1194,39 @@ def test_epilogue_loss_bwd_matches_separate_passes(K, hw, quant, relu):
     for a, b in zip(sep, fused):
         np.testing.assert_array_equal(a.reshape(-1).view(np.int32), host(b).reshape(-1).view(np.int32))
     close(host(loss2), host(loss1), rtol=1e-6, atol=0)
+
+
+def test_armed_adam_falls_back_when_not_covered(K):
+    """An armed step the alpha backward cannot take entirely (a parameter whose gradient
+    no launch of the stream produced) is left alone: adam_take() is False and nothing was
+    updated by the launch."""
+    w = (torch.randn(64, 64, 3, 3) * 0.05).cuda()
+    d, z, _ = K.scale_init(w, 2, False, True, "max")
+    alpha, beta, _ = K.shift_init(w, d, [31 / 32, 33 / 32, 1.0])
+    prep = K.AdaShiftPrep(w, beta, d, [31 / 32, 33 / 32, 1.0], 0)
+    a = alpha.clone().requires_grad_(True)
+    other = torch.zeros(10, device="cuda")
+    ms = [torch.zeros_like(a), torch.zeros_like(other)]
+    vs = [torch.zeros_like(a), torch.zeros_like(other)]
+    hyper = torch.tensor([-1e-3, 0.5], device="cuda")
+    K.adam_arm([a, other], ms, vs, 0.9, 0.999, 1e-8, hyper)
+    y = K.adashift_prepared(a, prep, d, z, 2, False, 0)
+    y.backward(torch.randn_like(y))
+    torch.cuda.synchronize()
+    assert not K.adam_take()
+    assert torch.equal(a.detach(), alpha) and not torch.any(ms[0] != 0)
+    # armed on the launch's own alpha only: taken, and the update is ssq_adam's
+    b = alpha.clone().requires_grad_(True)
+    m1, v1 = torch.zeros_like(b), torch.zeros_like(b)
+    K.adam_arm([b], [m1], [v1], 0.9, 0.999, 1e-8, hyper)
+    gy = torch.randn_like(y)
+    K.adashift_prepared(b, prep, d, z, 2, False, 0).backward(gy)
+    torch.cuda.synchronize()
+    assert K.adam_take()
+    c = alpha.clone().requires_grad_(True)
+    m2, v2 = torch.zeros_like(c), torch.zeros_like(c)
+    K.adashift_prepared(c, prep, d, z, 2, False, 0).backward(gy)
+    with torch.no_grad():
+        K.adam_step([c], [c.grad], [m2], [v2], 0.9, 0.999, 1e-8, hyper=hyper)
+    assert torch.equal(b.grad, c.grad)
+    assert torch.equal(b.detach(), c.detach()) and torch.equal(m1, m2) and torch.equal(v1, v2)

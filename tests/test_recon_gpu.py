@@ -536,6 +536,71 @@ def test_fused_start_bit_identical(Q, golden, graph, det_convs):
 
 
 @pytest.mark.parametrize("graph", [False, True])
+@pytest.mark.parametrize("bias_cal", [False, True])
+def test_fused_adam_bit_identical(Q, golden, graph, bias_cal, det_convs):
+    """The optimizer step armed into the alpha backward's launch (SsqAdam.arm: alpha updated
+    in its finaliser, gamma^z / phi^z in their finalize tasks or extra workgroups) against
+    the separate ssq_adam launch: every iteration's loss, the learned parameters and Adam's
+    moments bit-identical; the armed step really ran inside the launch."""
+    import importlib
+    from shiftedscalequantization_amd.quant import _engine as E
+    LRF = importlib.import_module("shiftedscalequantization_amd.quant.layer_recon_fused_shiftedScale")
+    g = golden("recon_fused")
+    runs, taken = [], []
+    orig_step = E.SsqAdam.step
+
+    def step(self, hyper=None):
+        taken.append(bool(getattr(self, "_armed", False)))
+        return orig_step(self, hyper)
+
+    for fuse in (False, True):
+        qnn = build_qnn(Q, {})
+        block = qnn.model[3]
+        load_block(Q, g, block)
+        block.cached_inp_features = [dev(g["cached_inp"])]
+        block.cached_out_features = [dev(g["cached_out"])]
+        seen, opts = [], []
+        orig_keep = LRF.FusedScaleLossFunction.bookkeep
+        orig_init = E.SsqAdam.__init__
+
+        def bookkeep(self, rec):
+            seen.append(float(rec.item()))
+            return orig_keep(self, rec)
+
+        def init(self, *a, **k):
+            orig_init(self, *a, **k)
+            opts.append(self)
+
+        LRF.FusedScaleLossFunction.bookkeep, prev = bookkeep, LRF.FUSE_ADAM
+        E.SsqAdam.__init__, E.SsqAdam.step = init, step
+        LRF.FUSE_ADAM = fuse
+        taken.clear()
+        try:
+            torch.manual_seed(1005)
+            LRF.block_recon_fused_shiftedScale(block, 12, (0.01, 0.1), qnn, None, verbose=False,
+                                               graph=graph, bias_cal=bias_cal)
+        finally:
+            LRF.FusedScaleLossFunction.bookkeep, LRF.FUSE_ADAM = orig_keep, prev
+            E.SsqAdam.__init__, E.SsqAdam.step = orig_init, orig_step
+        assert any(taken) == fuse
+        out = {"rec": np.array(seen)}
+        for n in ("conv1", "conv2", "downsample"):
+            m = getattr(block, n)
+            out[n + "_alpha"] = m.weight_quantizer.alpha.detach().cpu().numpy()
+            out[n + "_gamma"] = m.alpha_out.detach().cpu().numpy()
+            out[n + "_phi"] = m.beta_out.detach().cpu().numpy()
+        for k, p_ in enumerate(opts[0].params):
+            out[f"m{k}"] = opts[0].state[p_]["exp_avg"].cpu().numpy()
+            out[f"v{k}"] = opts[0].state[p_]["exp_avg_sq"].cpu().numpy()
+        runs.append(out)
+    assert runs[0].keys() == runs[1].keys()
+    for k in runs[0]:
+        np.testing.assert_array_equal(runs[1][k], runs[0][k], err_msg=k)
+    if bias_cal:
+        assert any(np.any(runs[1][n + "_gamma"] != 1.0) for n in ("conv1", "conv2", "downsample"))
+
+
+@pytest.mark.parametrize("graph", [False, True])
 def test_fused_tail_matches_unfused(Q, golden, graph, det_convs):
     """The block's final epilogue + the p = 2 loss + the epilogue backward as one pass
     (K.epilogue_loss_bwd, the loop's FUSE_TAIL) against the three separate launches: every

@@ -21,7 +21,9 @@ elements of the block's convs, N_W its weights, N_in its gathered input elements
   K11t epilogue_bwd_rows<...,LOSS=true>      (12 + 4 RES + 4 GRES) B / A, the fused tail: y,
                                               target rows [, res] in, gy [, g_res] out
   K11  lp_loss_kernel                         12 B / A (prediction, target rows in, gradient out)
-  K12  adam_kernel                            28 B / parameter (p, g, m, v in; p, m, v out)
+  K12  adam_kernel                            28 B / parameter (p, g, m, v in; p, m, v out);
+                                              at world 1 the step rides on K6p's launch
+                                              (ssq_adam_arm) and its bytes are priced there
 
 GRES (a residual gradient is written) holds for blocks with a downsample branch.  Every
 other launch (MIOpen / hipBLASLt convs, the K17 / GEMM-operand conv kernels) is reported
@@ -126,6 +128,10 @@ def analyse(path, warmup=20):
             us[cls] += d
             by[cls] += nb
             cnt[cls] += 1
+        if not cnt["K12_adam"]:
+            # the optimizer step rides on the alpha backward's launch (ssq_adam_arm): its
+            # 28 B / parameter are that launch's too
+            by["K6p_adashift_bwd"] += 28 * sz["n_params"] * n_it
         t0, t1 = int(rows[seg[0]]["Start_Timestamp"]), int(rows[seg[-1]]["Start_Timestamp"])
         cls_out = {c: {"us": round(us[c] / n_it, 2), "bytes": int(by[c] / n_it),
                        "launches": round(cnt[c] / n_it, 2),
