@@ -32,7 +32,7 @@ namespace ssq {
 constexpr int kLossBlocks = 1024;   // lp_loss workgroup partials
 constexpr uint32_t kFinBatch = 16;  // loads in flight per thread in the row-walking finalizes
 constexpr int kEpiParts = 7;        // doubles per (n, c) row of the epilogue backward
-                                    // (slot 6: the fused tail's loss partial)
+                                    // (slot 6: the fused tail's row loss)
 
 // The recon loop's optimizer step applied where each gradient is finalised (ssq_adam_arm):
 // ssq_adam's update, torch.optim.Adam's single-tensor step, op for op.
@@ -155,10 +155,9 @@ __device__ __forceinline__ void fin_epi(uint32_t bid, const double* __restrict__
   }
 }
 
-// fused tail (ssq_epilogue_loss_bwd): the per-row loss partials (slot 6 of each row's
-// kEpiParts doubles) summed in row order, one workgroup: thread t adds rows t, t + 256, ...
-// in order, kFinBatch loads in flight at a time (a 32 x 256 layer3 batch is 32 rows per
-// thread: serial loads took ~10 us), then the fixed block tree
+// fused tail (ssq_epilogue_loss_bwd): the launch's per-workgroup loss partials (contiguous,
+// after the rows' records) summed in order, one workgroup: thread t adds partials t, t + 256,
+// ... in order, kFinBatch loads in flight at a time, then the fixed block tree
 __device__ __forceinline__ void fin_loss_rows(const double* __restrict__ part, uint32_t rows,
                                               double m, float* __restrict__ out) {
   __shared__ double red[16];
@@ -168,7 +167,7 @@ __device__ __forceinline__ void fin_loss_rows(const double* __restrict__ part, u
 #pragma unroll
     for (uint32_t k = 0; k < kFinBatch; ++k) {
       const uint32_t r = r0 + k * kBlock;
-      v[k] = r < rows ? part[(int64_t)r * kEpiParts + 6] : 0.0;
+      v[k] = r < rows ? part[r] : 0.0;
     }
 #pragma unroll
     for (uint32_t k = 0; k < kFinBatch; ++k)

@@ -351,25 +351,19 @@ __device__ __forceinline__ void epi_row_sums(EpiRow& w, uint32_t lane, double* _
 // LOSS (the fused tail, ssq_epilogue_loss_bwd): g is the cache of target rows instead of
 // dL/d(output); the output is recomputed (the forward's ops) and dL/d(output) is the p = 2
 // lp_loss gradient of K11 (lp_elem, identical ops), the loss partial goes to slot 6.
+// The wave's RPW rows (bid: the workgroup among the launch's main ones); returns the wave's
+// loss sum (LOSS: its rows' totals in row order), 0 for a wave past the last row.
 template <bool RES, int ACT, bool QUANT, bool AFFINE, bool VEC, bool LOSS, int RPW>
-__global__ __launch_bounds__(kBlock) void epilogue_bwd_rows(
+__device__ __forceinline__ double epilogue_rows_body(
     const float* __restrict__ g, const float* __restrict__ y, const float* __restrict__ bias,
     const float* __restrict__ gamma, const float* __restrict__ phi, const float* __restrict__ res,
     uint32_t rows, uint32_t C, uint32_t hw, const float* __restrict__ qdelta,
     const float* __restrict__ qzp, float lo, float hi, float* __restrict__ gy,
-    float* __restrict__ gres, double* __restrict__ part, FinTable fin, uint32_t nmain,
-    const int64_t* __restrict__ lidx, float inv_m) {
-  // queued finalize tasks ride on this launch: its first workgroups (dispatched first, so
-  // they run beside the main work instead of after it)
-  (void)nmain;
-  if (blockIdx.x < fin.nwg) {
-    run_fin(fin, blockIdx.x);
-    return;
-  }
-  const uint32_t bid = blockIdx.x - fin.nwg;
+    float* __restrict__ gres, double* __restrict__ part, const int64_t* __restrict__ lidx,
+    float inv_m, uint32_t bid) {
   const uint32_t lane = threadIdx.x & (kWave - 1);
   const uint32_t r0 = (bid * (kBlock / kWave) + threadIdx.x / kWave) * RPW;
-  if (r0 >= rows) return;
+  if (r0 >= rows) return 0.0;
   const float d = QUANT ? qdelta[0] : 1.0f, z = QUANT ? qzp[0] : 0.0f;
   EpiRow w[RPW];
 #pragma unroll
@@ -418,9 +412,10 @@ __global__ __launch_bounds__(kBlock) void epilogue_bwd_rows(
       }
     }
     epi_row_sums<QUANT, LOSS>(wr, lane, part + (int64_t)r0 * kEpiParts);
-    return;
+    return wr.la;
   }
   // RPW rows, one element (float4) per lane and row, all loads first
+  double wl = 0.0;
   const uint32_t nv = VEC ? hw / 4 : hw;     // <= 64 (host-checked)
   const bool on = lane < nv;
   if (VEC) {
@@ -448,6 +443,7 @@ __global__ __launch_bounds__(kBlock) void epilogue_bwd_rows(
         if (gres) ((f32x4*)(gres + base))[lane] = f32x4{orr[0], orr[1], orr[2], orr[3]};
       }
       epi_row_sums<QUANT, LOSS>(w[k], lane, part + (int64_t)(r0 + k) * kEpiParts);
+      wl += w[k].la;
     }
   } else {
     float yv[RPW], gv[RPW], rv[RPW];
@@ -471,7 +467,42 @@ __global__ __launch_bounds__(kBlock) void epilogue_bwd_rows(
         if (gres) gres[base + lane] = orr;
       }
       epi_row_sums<QUANT, LOSS>(w[k], lane, part + (int64_t)(r0 + k) * kEpiParts);
+      wl += w[k].la;
     }
+  }
+  return wl;
+}
+
+template <bool RES, int ACT, bool QUANT, bool AFFINE, bool VEC, bool LOSS, int RPW>
+__global__ __launch_bounds__(kBlock) void epilogue_bwd_rows(
+    const float* __restrict__ g, const float* __restrict__ y, const float* __restrict__ bias,
+    const float* __restrict__ gamma, const float* __restrict__ phi, const float* __restrict__ res,
+    uint32_t rows, uint32_t C, uint32_t hw, const float* __restrict__ qdelta,
+    const float* __restrict__ qzp, float lo, float hi, float* __restrict__ gy,
+    float* __restrict__ gres, double* __restrict__ part, FinTable fin, uint32_t nmain,
+    const int64_t* __restrict__ lidx, float inv_m) {
+  // queued finalize tasks ride on this launch: its first workgroups (dispatched first, so
+  // they run beside the main work instead of after it)
+  (void)nmain;
+  if (blockIdx.x < fin.nwg) {
+    run_fin(fin, blockIdx.x);
+    return;
+  }
+  const uint32_t bid = blockIdx.x - fin.nwg;
+  const double wl = epilogue_rows_body<RES, ACT, QUANT, AFFINE, VEC, LOSS, RPW>(
+      g, y, bias, gamma, phi, res, rows, C, hw, qdelta, qzp, lo, hi, gy, gres, part, lidx, inv_m,
+      bid);
+  if (!LOSS) return;
+  // the fused tail's loss: one partial per workgroup (its waves in order) after the rows'
+  // records, so the finalize sums rows / (4 RPW) values instead of every row's
+  __shared__ double sl[kBlock / kWave];
+  if ((threadIdx.x & (kWave - 1)) == 0) sl[threadIdx.x / kWave] = wl;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    double a = sl[0];
+#pragma unroll
+    for (int k = 1; k < kBlock / kWave; ++k) a += sl[k];
+    part[(int64_t)rows * kEpiParts + bid] = a;
   }
 }
 
@@ -830,7 +861,8 @@ extern "C" int ssq_epilogue_fwd(const float* y, const float* bias, const float* 
 }
 
 extern "C" size_t ssq_epilogue_bwd_workspace_size(int64_t rows) {
-  return (size_t)rows * kEpiParts * sizeof(double);
+  // the rows' records, then (fused tail) one loss partial per workgroup: <= ceil(rows / 4)
+  return ((size_t)rows * kEpiParts + (size_t)(rows + 3) / 4) * sizeof(double);
 }
 
 // ssq_epilogue_bwd (g = dL/d(output)) and its fused-tail form ssq_epilogue_loss_bwd
@@ -900,8 +932,8 @@ static int epilogue_bwd(const char* what, const float* g, const float* y, const 
     FinTask t{};
     t.kind = 2;
     t.nwg = 1;
-    t.part = part;
-    t.a = (uint32_t)rows;
+    t.part = part + (size_t)rows * kEpiParts;   // the launch's workgroup partials
+    t.a = nmain;
     t.m = (double)M;
     t.o[0] = loss_out;
     if (fin_defer_on()) {
