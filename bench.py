@@ -169,6 +169,18 @@ def host_cores():
     return env if env > 0 else len(os.sched_getaffinity(0))
 
 
+def cpu_model():
+    """The host CPU's model name (report it beside the CPU baseline)."""
+    try:
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if line.startswith("model name"):
+                    return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return None
+
+
 def _timed(fn, seconds, min_reps=2):
     fn()  # warm
     n, t0 = 0, time.perf_counter()
@@ -211,7 +223,8 @@ def cpu_baseline(act_dev, d_a, z_a, seconds, recon_state=None):
            "sample": f"q/dq: oracle/c ssqo_fake_quant (scalar C port of quant_layer.py:92-98), "
                      f"A4 per-tensor q/dq of act[:64] ({sample.size} elems) x{nN} reps in "
                      f"{elN:.1f}s on {cores} threads; {os.cpu_count()} host CPUs visible",
-           "qdq_1thread_gelem_s": round(n1 * sample.size / el1 / 1e9, 4)}
+           "qdq_1thread_gelem_s": round(n1 * sample.size / el1 / 1e9, 4),
+           "cpu_model": cpu_model()}
     # the reference's own CPU path: its eager torch op sequence (oracle/torch_eager.py) on
     # the same sample, all cores and one thread
     import torch
@@ -241,6 +254,10 @@ def cpu_baseline(act_dev, d_a, z_a, seconds, recon_state=None):
         out["recon_sample"] = (f"oracle/recon_cpu.FusedBlockReconCPU, ResNet-18 layer1.0 W2 S=3 "
                                f"bias_cal, batch 32 of 64 cached samples, {nr} iterations in "
                                f"{elr:.1f}s on {cores} torch threads")
+        torch.set_num_threads(1)
+        n1r, el1r = _timed(rc.step, seconds / 6, min_reps=2)
+        torch.set_num_threads(cores)
+        out["recon_iters_per_s_1thread"] = round(n1r / el1r, 3)
     return out
 
 

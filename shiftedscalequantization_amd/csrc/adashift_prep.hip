@@ -446,35 +446,52 @@ __global__ __launch_bounds__(kBlock) void alpha_bwd_prep(PrepTable tab, float re
   for (int i = 0; i < NS; ++i) acc[i] = 0.0;
   if (t < nci * g.K) {
     const uint32_t ci = ci0 + t / g.K, j = ci0 * g.K + t;
-    float a[kMaxS], p[kMaxS];
-    load_row(sg.alpha, ci, NS, a);
-    soft_targets<kMaxS>(a, NS, nullptr, p);
     const uint32_t* __restrict__ fpack = sg.fpack;
     const float* __restrict__ hterm = sg.hterm;
     const float* __restrict__ gWhat = sg.gWhat;
     const float* __restrict__ delta = sg.delta;
     const float* __restrict__ zp = sg.zp;
     const uint32_t co0 = by * sg.tl.R, co1 = min(co0 + sg.tl.R, g.Co);
-    uint32_t co = co0;
-    for (; co + kRBP <= co1; co += kRBP) {
-      uint32_t fw[kRBP];
-      float h[kRBP], d[kRBP], z[kRBP], gy[kRBP];
+    // the alpha row first, then the first row batch, both before the softmax (loads retire
+    // in order: the alpha wait leaves the rows in flight); each later batch is fetched
+    // before the current one is accumulated.  Rows are added in order, as before.
+    float a[kMaxS], p[kMaxS];
+    load_row(sg.alpha, ci, NS, a);
+    uint32_t fw[kRBP];
+    float h[kRBP], d[kRBP], z[kRBP], gy[kRBP];
+    auto fetch = [&](uint32_t c) {
 #pragma unroll
       for (int r = 0; r < kRBP; ++r) {
-        const uint32_t e = (co + r) * g.CiK + j;
-        fw[r] = fpack[e];
-        h[r] = hterm[e];
-        gy[r] = gWhat[e];
-        d[r] = delta[co + r];
-        z[r] = zp[co + r];
+        fw[r] = 0u;
+        h[r] = d[r] = z[r] = gy[r] = 0.0f;
+        if (c + r < co1) {
+          const uint32_t e = (c + r) * g.CiK + j;
+          fw[r] = fpack[e];
+          h[r] = hterm[e];
+          gy[r] = gWhat[e];
+          d[r] = delta[c + r];
+          z[r] = zp[c + r];
+        }
       }
+    };
+    fetch(co0);
+    soft_targets<kMaxS>(a, NS, nullptr, p);
+    for (uint32_t co = co0; co < co1; co += kRBP) {
+      uint32_t fw1[kRBP];
+      float h1[kRBP], d1[kRBP], z1[kRBP], gy1[kRBP];
+#pragma unroll
+      for (int r = 0; r < kRBP; ++r) {
+        fw1[r] = fw[r];
+        h1[r] = h[r];
+        d1[r] = d[r];
+        z1[r] = z[r];
+        gy1[r] = gy[r];
+      }
+      if (co + kRBP < co1) fetch(co + kRBP);
 #pragma unroll
       for (int r = 0; r < kRBP; ++r)
-        alpha_accumulate<NS>(fw[r], h[r], d[r], z[r], gy[r], p, sg.lo, sg.hi, acc);
-    }
-    for (; co < co1; ++co) {
-      const uint32_t e = co * g.CiK + j;
-      alpha_accumulate<NS>(fpack[e], hterm[e], delta[co], zp[co], gWhat[e], p, sg.lo, sg.hi, acc);
+        if (co + r < co1)
+          alpha_accumulate<NS>(fw1[r], h1[r], d1[r], z1[r], gy1[r], p, sg.lo, sg.hi, acc);
     }
   }
 #pragma unroll
