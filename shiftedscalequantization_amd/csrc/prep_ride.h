@@ -24,6 +24,23 @@ struct GatherArgs {
   uint32_t nrows;   // batch rows
 };
 
+// dst[k] = src[k] for k = k0, k0 + stride, ... < n: kGatherU loads in flight per lane
+// before their stores (src and dst never overlap)
+constexpr int kGatherU = 4;
+template <typename T>
+__device__ __forceinline__ void copy_strided(const T* __restrict__ src, T* __restrict__ dst,
+                                             int64_t k0, int64_t n, int64_t stride) {
+  for (int64_t k = k0; k < n; k += kGatherU * stride) {
+    T v[kGatherU];
+#pragma unroll
+    for (int u = 0; u < kGatherU; ++u)
+      if (k + u * stride < n) v[u] = src[k + u * stride];
+#pragma unroll
+    for (int u = 0; u < kGatherU; ++u)
+      if (k + u * stride < n) dst[k + u * stride] = v[u];
+  }
+}
+
 // dst_k[r, :] = src_k[idx[r], :] for batch row r, workgroup bx of the row's gx; 16-B
 // vectors when rows allow it.  Its source row index is one scalar load; the workgroups of
 // a row stride over the concatenated row of both sources: no per-element division.
@@ -36,11 +53,12 @@ __device__ __forceinline__ void gather2_body(const GatherArgs& a, uint32_t bx, u
   const T* a0 = (const T*)a.s0 + src * r0;
   T* b0 = (T*)a.d0 + (int64_t)r * r0;
   const int64_t stride = (int64_t)a.gx * blockDim.x;
-  for (int64_t k = (int64_t)bx * blockDim.x + threadIdx.x; k < r0; k += stride) b0[k] = a0[k];
+  const int64_t k0 = (int64_t)bx * blockDim.x + threadIdx.x;
+  copy_strided(a0, b0, k0, r0, stride);
   if (a.s1) {
     const T* a1 = (const T*)a.s1 + src * r1;
     T* b1 = (T*)a.d1 + (int64_t)r * r1;
-    for (int64_t k = (int64_t)bx * blockDim.x + threadIdx.x; k < r1; k += stride) b1[k] = a1[k];
+    copy_strided(a1, b1, k0, r1, stride);
   }
 }
 

@@ -436,7 +436,8 @@ EDGE = [-0.0, float("nan"), 0.0, 6.0, 6.0000005, 5.9999995, float("inf"), -float
 @pytest.mark.parametrize("shape,res,relu", [((4, 8, 7, 7), True, True), ((3, 5, 6, 6), False, True),
                                             ((2, 16, 14, 14), True, False), ((2, 3, 5, 3), False, False),
                                             ((32, 64, 56, 56), True, True), ((4, 8, 7, 7), True, 2),
-                                            ((2, 3, 5, 3), False, 2), ((32, 64, 56, 56), False, 2)])
+                                            ((2, 3, 5, 3), False, 2), ((32, 64, 56, 56), False, 2),
+                                            ((48, 64, 56, 56), True, True)])  # > 1 grid trip
 def test_bias_act_matches_eager_ops(K, shape, res, relu):
     """K13 epilogue == (y + bias) (+ residual) -> ReLU / ReLU6 as separate fp32 torch ops
     on the device, bit for bit (-0.0 / NaN / the clamp edges through the activation), and
