@@ -153,10 +153,21 @@ def round_quant(x, delta, zp, n_bits, sym=False, scale=1.0):
     return RoundQuantFn.apply(x, delta, zp, n_bits, sym, float(scale))
 
 
-def fake_quant_multi(xs, deltas, zps, n_bits, sym=False):
-    """Every tensor of a list in one launch (per-channel params staged in LDS)."""
+def fake_quant_multi(xs, deltas, zps, n_bits, sym=False, out=None):
+    """Every tensor of a list in one launch (per-channel params staged in LDS); out: a
+    list of contiguous fp32 outputs, one per input and of its shape (else allocated)."""
     n = len(xs)
-    ys = [torch.empty_like(x) for x in xs]
+    if out is None:
+        ys = [torch.empty_like(x) for x in xs]
+    else:
+        if len(out) != n:
+            raise ValueError(f"fake_quant_multi: {len(out)} outputs for {n} inputs")
+        for k, (x, y) in enumerate(zip(xs, out)):
+            A.check(y, f"out[{k}]")
+            if y.shape != x.shape or not y.is_contiguous():
+                raise ValueError(f"fake_quant_multi: out[{k}] must be contiguous, shape "
+                                 f"{tuple(x.shape)}")
+        ys = list(out)
     keep = []
     P = C.c_void_p * n
     xa, ya, da, za = P(), P(), P(), P()

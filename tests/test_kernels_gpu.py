@@ -205,6 +205,16 @@ def test_fq_multi_segment(K):
                             [dev(p[1]) for p in params], 2)
     for w, p, y in zip(ws, params, ys):
         np.testing.assert_array_equal(host(y), R.fake_quant(w.numpy(), p[0], p[1], 2)[0])
+    # caller-owned outputs (out=): written in place, same bits; wrong shapes refused
+    outs = [torch.full(s, float("nan"), device="cuda") for s in shapes]
+    ys2 = K.fake_quant_multi([w.cuda() for w in ws], [dev(p[0]) for p in params],
+                             [dev(p[1]) for p in params], 2, out=outs)
+    for y, y2, o in zip(ys, ys2, outs):
+        assert y2 is o
+        np.testing.assert_array_equal(host(y2), host(y))
+    with pytest.raises(ValueError):
+        K.fake_quant_multi([w.cuda() for w in ws], [dev(p[0]) for p in params],
+                           [dev(p[1]) for p in params], 2, out=outs[::-1])
 
 
 def test_fq_multi_many_ragged_segments(K):
