@@ -945,26 +945,42 @@ __global__ __launch_bounds__(256, 1) void wgrad_band_stage1(const float* __restr
         if (i0 < g.ni_w) stage4(nb, b ^ 1, i0, min(i0 + per_step, g.ni_w));
       }
     };
-    // two operand sets used alternately, each read one step ahead of its MFMAs: no
-    // register copies between steps (8 % faster than copying a prefetch set on layer1)
+    // two operand sets used alternately, each read one step ahead of its MFMAs.  The
+    // pair loop fetches unconditionally (its last fetch, one step past the band, reads
+    // in-buffer pitch pads / the clamped last pixel and is never used): with no
+    // conditional definitions the sets keep their registers, so the MFMAs wait only for
+    // their own set's reads, not for the set just issued (a conditional fetch made the
+    // compiler copy the new set into place behind an lgkmcnt(0) every step)
+    // Each half step: the other set's LDS reads interleaved one per MFMA at the front of
+    // the step's 9V MFMAs (scheduler directive), so they land long before that set's
+    // MFMAs wait for them
+    auto interleave = [&]() {
+      constexpr int NM = 9 * V, ND = NM < 12 ? NM : 12;
+#pragma unroll
+      for (int k = 0; k < ND; ++k) {
+        __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);   // 1 MFMA
+        __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);   // 1 DS read
+      }
+      __builtin_amdgcn_sched_group_barrier(0x008, NM - ND, 0);
+    };
     float a0[V], w0[3][NW], a1[V], w1[3][NW];
     fetch(L, q, orow, ow, a0, w0);
-    for (int gi = 0; gi < ngroups; gi += 2) {
-      stage_slice(gi);
-      const bool two = gi + 1 < ngroups;
-      if (two) {
-        advance();
-        fetch(L, q, orow, ow, a1, w1);
-      }
+    const int npairs = ngroups >> 1;
+    for (int gp = 0; gp < npairs; ++gp) {
+      stage_slice(2 * gp);
+      advance();
+      fetch(L, q, orow, ow, a1, w1);
       mfmas(a0, w0);
-      if (two) {
-        stage_slice(gi + 1);
-        if (gi + 2 < ngroups) {
-          advance();
-          fetch(L, q, orow, ow, a0, w0);
-        }
-        mfmas(a1, w1);
-      }
+      interleave();
+      stage_slice(2 * gp + 1);
+      advance();
+      fetch(L, q, orow, ow, a0, w0);
+      mfmas(a1, w1);
+      interleave();
+    }
+    if (ngroups & 1) {
+      stage_slice(ngroups - 1);
+      mfmas(a0, w0);
     }
   }
   // part[split][tap][co][ci]: C[row][col], row = (i&3) + 8*(i>>2) + 4*h, col = lane&31
