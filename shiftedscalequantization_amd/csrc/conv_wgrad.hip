@@ -782,15 +782,15 @@ __global__ __launch_bounds__(256, 1) void wgrad_band_stage1(const float* __restr
     if (g.d16 && i < g.ni_w) {
       const int o = (wave + 4 * i) * 256 + lane * 4;
       if (o < abytes) {
-        const int row = o / g.PA, col = o - row * g.PA;
+        const int row = (int)fdiv((uint32_t)o, g.dPA), col = o - row * g.PA;
         if (col < g.Q && co0 + row < g.Cog) {
           soff[i] = (co0 + row) * g.OHW + col;   // + n*Co*OHW + oh0*OW per band
           meta[i] = 1;
         }
       } else {
         const int o2 = o - abytes;
-        const int cl = o2 / g.PXci, rem = o2 - cl * g.PXci;
-        const int ir = rem / g.PXrow, iw = rem - ir * g.PXrow - 4;
+        const int cl = (int)fdiv((uint32_t)o2, g.dPXci), rem = o2 - cl * g.PXci;
+        const int ir = (int)fdiv((uint32_t)rem, g.dPXrow), iw = rem - ir * g.PXrow - 4;
         if (cl < g.CBc && ci0 + cl < g.Cig && ir < g.IR && iw >= 0 && iw < g.W) {
           soff[i] = ((ci0 + cl) * g.H + ir) * g.W + iw;   // + n*C*H*W + ih0*W per band
           meta[i] = 2 | (ir << 2);
@@ -819,12 +819,13 @@ __global__ __launch_bounds__(256, 1) void wgrad_band_stage1(const float* __restr
 #pragma unroll
     for (int i = 0; i < kBandMaxNI; ++i) {
       if (i < g.ni_w) {
+        // selects, not branches: bitwise conditions, 64-bit addresses picked by value
         const int kind = meta[i] & 3;
         const unsigned ih = (unsigned)(bd.ih0 + (meta[i] >> 2));
-        const bool ok = kind == 1 || (kind == 2 && ih < (unsigned)g.H);
-        const float* base = kind == 1 ? bd.ab : bd.xb;
-        const float* src = ok ? base + soff[i] : zero;
-        __builtin_amdgcn_global_load_lds((const void*)src, (void*)(dst + i * 1024), 16, 0, 0);
+        const bool ok = (kind == 1) | ((kind == 2) & (ih < (unsigned)g.H));
+        const uint64_t pa = (uint64_t)(bd.ab + soff[i]), px = (uint64_t)(bd.xb + soff[i]);
+        const uint64_t p = ok ? (kind == 1 ? pa : px) : (uint64_t)zero;
+        __builtin_amdgcn_global_load_lds((const void*)p, (void*)(dst + i * 1024), 16, 0, 0);
       }
     }
   };
