@@ -418,7 +418,8 @@ int ssq_flush_prep_fwd(ssq_stream_t stream);
  * summed in a fixed order: bit-identical run to run.  OW <= 128, tensors < 2^31 elements. */
 /* A/B knob (returns the previous value; out-of-range values only query): non-depthwise
  * weight-gradient form, 0 auto, 1 input-row-tile kernel (+ 1x1 GEMM), 2 im2col-DMA kernel,
- * 3 band kernel (3x3 / pad 1 / stride 1-2 / Cin, Cout multiples of 32; others as 1). */
+ * 3 band kernel (3x3 / pad 1 / stride 1-2 / Cin, Cout multiples of 32; others as 1), 4 the
+ * band kernel at 4 waves per workgroup instead of 8 (same bits). */
 int ssq_conv_wgrad_set_form(int form);
 /* The kernel ssq_conv_wgrad runs for a shape under the current form: 0 unsupported,
  * 1 input-row tile, 2 im2col-DMA, 3 band (16-byte staging), 4 1x1 GEMM, 5 depthwise

@@ -18,6 +18,7 @@
 #include <stdlib.h>
 
 #include <algorithm>
+#include <type_traits>
 
 #include "ssq_common.h"
 
@@ -751,15 +752,27 @@ struct BandGeo {
   FastDiv dPA, dPXci, dPXrow;
 };
 
-template <int WMX, int ST, int V>
-__global__ __launch_bounds__(256, 1) void wgrad_band_stage1(const float* __restrict__ x,
-                                                            const float* __restrict__ dy,
-                                                            BandGeo g, float* __restrict__ part) {
+template <int N>
+using IntC = std::integral_constant<int, N>;
+
+// NWV = 4: one wave per SIMD, each wave all 9 taps of its 32 co x 32 ci tile.  NWV = 8: two
+// waves per SIMD -- waves w and w + 4 own the same tile, w taps 0-4 (80 AGPRs), w + 4 taps
+// 5-8 (64): both walk every pixel of the band, each reading only its two tap rows, so while
+// one waits on LDS, the band barrier or its staging, the other keeps the SIMD's MFMA pipe
+// busy.  Every tap's accumulator sums the same pixels in the same order either way: the
+// two forms give the same bits.
+template <int WMX, int ST, int V, int NWV>
+__global__ __launch_bounds__(64 * NWV, 1) void wgrad_band_stage1(const float* __restrict__ x,
+                                                                 const float* __restrict__ dy,
+                                                                 BandGeo g, float* __restrict__ part) {
+  static_assert(NWV == 4 || NWV == 8, "4 or 8 waves");
   constexpr int WNX = 4 / WMX;
+  constexpr int kSlots = kBandMaxNI * 4 / NWV;   // 16-B pieces per wave per band, at most
   extern __shared__ float lds[];
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int wm = wave / WNX, wn = wave - wm * WNX;
+  const int wt = wave & 3, role = wave >> 2;
+  const int wm = wt / WNX, wn = wt - wm * WNX;
   // XCD-aware order (remap): the tiles of one split run on one XCD and share its L2
   int wg = blockIdx.x;
   const int tiles = g.m_tiles * g.n_tiles;
@@ -772,15 +785,19 @@ __global__ __launch_bounds__(256, 1) void wgrad_band_stage1(const float* __restr
   const int co0 = mt * g.TMc, ci0 = nt * g.CBc;
   const int c_begin = split * g.cps, c_end = min(c_begin + g.cps, g.nchunks);
   const int abytes = g.TMc * g.PA;
+  // this wave's DMA pieces: piece j = wave + NWV*i of the buffer (256 floats per 16-B
+  // piece, 64 per 4-B piece)
+  const int n16 = g.d16 ? min(kSlots, (g.bufsz / 256 - wave + NWV - 1) / NWV) : 0;
+  const int n4 = g.d16 ? 0 : (g.bufsz / 64 - wave + NWV - 1) / NWV;
 
   // 16-B form: per-lane DMA sources, band-independent: kind 0 zero page, 1 dy, 2 x row ir
-  int soff[kBandMaxNI], meta[kBandMaxNI];
+  int soff[kSlots], meta[kSlots];
 #pragma unroll
-  for (int i = 0; i < kBandMaxNI; ++i) {
+  for (int i = 0; i < kSlots; ++i) {
     soff[i] = 0;
     meta[i] = 0;
-    if (g.d16 && i < g.ni_w) {
-      const int o = (wave + 4 * i) * 256 + lane * 4;
+    if (i < n16) {
+      const int o = (wave + NWV * i) * 256 + lane * 4;
       if (o < abytes) {
         const int row = (int)fdiv((uint32_t)o, g.dPA), col = o - row * g.PA;
         if (col < g.Q && co0 + row < g.Cog) {
@@ -811,35 +828,35 @@ __global__ __launch_bounds__(256, 1) void wgrad_band_stage1(const float* __restr
     return Band{dy + (int64_t)n * g.Co * g.OHW + oh0 * g.OW,
                 x + (int64_t)n * g.C * g.H * g.W + (int64_t)ih0 * g.W, ih0};
   };
-  // 16-B form: the whole band in one go (<= kBandMaxNI instructions per wave);
-  // branch-free source selection: dy row piece, x row piece, or the zero page
+  // 16-B form: the whole band in one go; branch-free source selection: dy row piece,
+  // x row piece, or the zero page
   auto stage16 = [&](const Band& bd, int b) {
     const float* zero = g_band_zero_page + lane * 4;
     float* dst = lds + b * g.bufsz + wave * 256;
 #pragma unroll
-    for (int i = 0; i < kBandMaxNI; ++i) {
-      if (i < g.ni_w) {
+    for (int i = 0; i < kSlots; ++i) {
+      if (i < n16) {
         // selects, not branches: bitwise conditions, 64-bit addresses picked by value
         const int kind = meta[i] & 3;
         const unsigned ih = (unsigned)(bd.ih0 + (meta[i] >> 2));
         const bool ok = (kind == 1) | ((kind == 2) & (ih < (unsigned)g.H));
         const uint64_t pa = (uint64_t)(bd.ab + soff[i]), px = (uint64_t)(bd.xb + soff[i]);
         const uint64_t p = ok ? (kind == 1 ? pa : px) : (uint64_t)zero;
-        __builtin_amdgcn_global_load_lds((const void*)p, (void*)(dst + i * 1024), 16, 0, 0);
+        __builtin_amdgcn_global_load_lds((const void*)p, (void*)(dst + i * NWV * 256), 16, 0, 0);
       }
     }
   };
-  // 4-B form: instructions [i0, i1) of this wave; instruction k = wave + 4i of the buffer
-  // covers floats [64k, 64k + 64), all in the A region or all in the X region (the A
-  // region is a multiple of 64 floats)
+  // 4-B form: pieces [i0, i1) of this wave; piece j = wave + NWV*i covers floats
+  // [64j, 64j + 64), all in the A region or all in the X region (the A region is a
+  // multiple of 64 floats)
   const int HW = g.H * g.W;
   auto stage4 = [&](const Band& bd, int b, int i0, int i1) {
     const float* zero = g_band_zero_page + lane;
     float* dst = lds + b * g.bufsz + wave * 64;
     for (int i = i0; i < i1; ++i) {
-      const int o = (wave + 4 * i) * 64 + lane;
+      const int o = (wave + NWV * i) * 64 + lane;
       const float* src = zero;
-      if ((wave + 4 * i) * 64 < abytes) {
+      if ((wave + NWV * i) * 64 < abytes) {
         const int row = (int)fdiv((uint32_t)o, g.dPA), col = o - row * g.PA;
         if (col < g.Q && co0 + row < g.Cog) src = bd.ab + (co0 + row) * g.OHW + col;
       } else {
@@ -851,15 +868,12 @@ __global__ __launch_bounds__(256, 1) void wgrad_band_stage1(const float* __restr
             ih < (unsigned)g.H)
           src = bd.xb + (ci0 + cl) * HW + ir * g.W + iw;
       }
-      __builtin_amdgcn_global_load_lds((const void*)src, (void*)(dst + i * 256), 4, 0, 0);
+      __builtin_amdgcn_global_load_lds((const void*)src, (void*)(dst + i * NWV * 64), 4, 0, 0);
     }
   };
 
   typedef float f32x4v __attribute__((ext_vector_type(4)));
   typedef float f32x2v __attribute__((ext_vector_type(2)));
-  f32x16 acc[9];
-#pragma unroll
-  for (int t = 0; t < 9; ++t) acc[t] = f32x16{0};
   const int h = lane >> 5, l32 = lane & 31;
   const int arow = (wm * 32 + l32) * g.PA;
   const int xrow = abytes + (wn * 32 + l32) * g.PXci;
@@ -868,95 +882,77 @@ __global__ __launch_bounds__(256, 1) void wgrad_band_stage1(const float* __restr
   // the last real pixel: x reads of padding pixels (A = 0) are clamped to it
   const int last_row = (g.Q - 1) / g.OW, last_col = (g.Q - 1) - last_row * g.OW;
   constexpr int NW = (V - 1) * ST + 3;   // window floats per tap row: V pixels x 3 taps
-  // one step's operands: A (V pixels) and the 3 tap-row windows, read one step ahead
-  auto fetch = [&](const float* L, int q, int orow, int ow, float (&a)[V], float (&w)[3][NW]) {
-    if constexpr (V == 4) {
-      const f32x4v av = *(const f32x4v*)(L + arow + q);
-      a[0] = av.x; a[1] = av.y; a[2] = av.z; a[3] = av.w;
-    } else if constexpr (V == 2) {
-      const f32x2v av = *(const f32x2v*)(L + arow + q);
-      a[0] = av.x; a[1] = av.y;
-    } else {
-      a[0] = L[arow + q];
-    }
-    int xr_row = orow, xr_col = ow;
-    if (q >= g.Q) {
-      xr_row = last_row;
-      xr_col = last_col - (V - 1);
-    }
-    const float* xr0 = L + xrow + xr_row * ST * g.PXrow + xr_col * ST + 3;
-#pragma unroll
-    for (int r = 0; r < 3; ++r) {
-      const float* xr = xr0 + r * g.PXrow;
-      if constexpr (V == 4) {
-        w[r][0] = xr[0];
-        const f32x4v t1 = *(const f32x4v*)(xr + 1);
-        w[r][1] = t1.x; w[r][2] = t1.y; w[r][3] = t1.z; w[r][4] = t1.w;
-        if constexpr (ST == 1) {
-          w[r][5] = xr[5];
-        } else {
-          const f32x4v t2 = *(const f32x4v*)(xr + 5);
-          w[r][5] = t2.x; w[r][6] = t2.y; w[r][7] = t2.z; w[r][8] = t2.w;
-        }
-      } else {
-#pragma unroll
-        for (int j = 0; j < NW; ++j) w[r][j] = xr[j];
-      }
-    }
-  };
-
-  // 4-B form: the next band's instructions are spread over the first half of this band's
+  // 4-B form: the next band's pieces are spread over the first half of this band's
   // steps, issued between the MFMAs (their address math runs in the MFMA shadow)
-  const int per_step = (g.ni_w + max(1, ngroups / 2) - 1) / max(1, ngroups / 2);
+  const int per_step = (n4 + max(1, ngroups / 2) - 1) / max(1, ngroups / 2);
   if (c_begin < c_end) {
     const Band bd = band_of(c_begin);
     if (g.d16) stage16(bd, 0);
-    else stage4(bd, 0, 0, g.ni_w);
+    else stage4(bd, 0, 0, n4);
   }
-  for (int c = c_begin; c < c_end; ++c) {
-    const int b = (c - c_begin) & 1;
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __syncthreads();             // band c staged; band c-1's reads of buffer b^1 done
-    const bool more = c + 1 < c_end;
-    const Band nb = band_of(more ? c + 1 : c);
-    if (more && g.d16) stage16(nb, b ^ 1);
-    const float* L = lds + b * g.bufsz;
-    int q = q0, orow = q0 / g.OW, ow = q0 - orow * g.OW;
-    auto advance = [&]() {
-      q += V;
-      ow += V;
-      if (ow == g.OW) {
-        ow = 0;
-        ++orow;
+
+  // the band loop and the partial store for taps [T0, T1)
+  auto body = [&](auto t0c, auto t1c) {
+    constexpr int T0 = decltype(t0c)::value, T1 = decltype(t1c)::value, NT = T1 - T0;
+    constexpr int R0 = T0 / 3, NR = (T1 - 1) / 3 - R0 + 1;   // tap rows read
+    f32x16 acc[NT];
+#pragma unroll
+    for (int t = 0; t < NT; ++t) acc[t] = f32x16{0};
+    // one step's operands: A (V pixels) and the tap-row windows, read one step ahead
+    auto fetch = [&](const float* L, int q, int orow, int ow, float (&a)[V],
+                     float (&w)[NR][NW]) {
+      if constexpr (V == 4) {
+        const f32x4v av = *(const f32x4v*)(L + arow + q);
+        a[0] = av.x; a[1] = av.y; a[2] = av.z; a[3] = av.w;
+      } else if constexpr (V == 2) {
+        const f32x2v av = *(const f32x2v*)(L + arow + q);
+        a[0] = av.x; a[1] = av.y;
+      } else {
+        a[0] = L[arow + q];
+      }
+      int xr_row = orow, xr_col = ow;
+      if (q >= g.Q) {
+        xr_row = last_row;
+        xr_col = last_col - (V - 1);
+      }
+      const float* xr0 = L + xrow + (xr_row * ST + R0) * g.PXrow + xr_col * ST + 3;
+#pragma unroll
+      for (int r = 0; r < NR; ++r) {
+        const float* xr = xr0 + r * g.PXrow;
+        if constexpr (V == 4) {
+          w[r][0] = xr[0];
+          const f32x4v t1 = *(const f32x4v*)(xr + 1);
+          w[r][1] = t1.x; w[r][2] = t1.y; w[r][3] = t1.z; w[r][4] = t1.w;
+          if constexpr (ST == 1) {
+            w[r][5] = xr[5];
+          } else {
+            const f32x4v t2 = *(const f32x4v*)(xr + 5);
+            w[r][5] = t2.x; w[r][6] = t2.y; w[r][7] = t2.z; w[r][8] = t2.w;
+          }
+        } else {
+#pragma unroll
+          for (int j = 0; j < NW; ++j) w[r][j] = xr[j];
+        }
       }
     };
-    auto mfmas = [&](const float (&a)[V], const float (&w)[3][NW]) {
+    auto mfmas = [&](const float (&a)[V], const float (&w)[NR][NW]) {
 #pragma unroll
-      for (int r = 0; r < 3; ++r)
+      for (int r = 0; r < NR; ++r)
 #pragma unroll
         for (int v = 0; v < V; ++v)
 #pragma unroll
-          for (int s = 0; s < 3; ++s)
-            acc[r * 3 + s] =
-                __builtin_amdgcn_mfma_f32_32x32x2f32(a[v], w[r][v * ST + s], acc[r * 3 + s], 0, 0, 0);
+          for (int s = 0; s < 3; ++s) {
+            const int tap = (R0 + r) * 3 + s;
+            if (tap >= T0 && tap < T1)
+              acc[tap - T0] = __builtin_amdgcn_mfma_f32_32x32x2f32(a[v], w[r][v * ST + s],
+                                                                   acc[tap - T0], 0, 0, 0);
+          }
     };
-    auto stage_slice = [&](int gi) {
-      if (more && !g.d16) {
-        const int i0 = gi * per_step;
-        if (i0 < g.ni_w) stage4(nb, b ^ 1, i0, min(i0 + per_step, g.ni_w));
-      }
-    };
-    // two operand sets used alternately, each read one step ahead of its MFMAs.  The
-    // pair loop fetches unconditionally (its last fetch, one step past the band, reads
-    // in-buffer pitch pads / the clamped last pixel and is never used): with no
-    // conditional definitions the sets keep their registers, so the MFMAs wait only for
-    // their own set's reads, not for the set just issued (a conditional fetch made the
-    // compiler copy the new set into place behind an lgkmcnt(0) every step)
     // Each half step: the other set's LDS reads interleaved one per MFMA at the front of
-    // the step's 9V MFMAs (scheduler directive), so they land long before that set's
+    // the step's NT*V MFMAs (scheduler directive), so they land long before that set's
     // MFMAs wait for them
     auto interleave = [&]() {
-      constexpr int NM = 9 * V, ND = NM < 12 ? NM : 12;
+      constexpr int NM = NT * V, ND = NM < 12 ? NM : 12;
 #pragma unroll
       for (int k = 0; k < ND; ++k) {
         __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);   // 1 MFMA
@@ -964,39 +960,86 @@ __global__ __launch_bounds__(256, 1) void wgrad_band_stage1(const float* __restr
       }
       __builtin_amdgcn_sched_group_barrier(0x008, NM - ND, 0);
     };
-    float a0[V], w0[3][NW], a1[V], w1[3][NW];
-    fetch(L, q, orow, ow, a0, w0);
-    const int npairs = ngroups >> 1;
-    for (int gp = 0; gp < npairs; ++gp) {
-      stage_slice(2 * gp);
-      advance();
-      fetch(L, q, orow, ow, a1, w1);
-      mfmas(a0, w0);
-      interleave();
-      stage_slice(2 * gp + 1);
-      advance();
+    for (int c = c_begin; c < c_end; ++c) {
+      const int b = (c - c_begin) & 1;
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __syncthreads();             // band c staged; band c-1's reads of buffer b^1 done
+      const bool more = c + 1 < c_end;
+      const Band nb = band_of(more ? c + 1 : c);
+      if (more && g.d16) stage16(nb, b ^ 1);
+      const float* L = lds + b * g.bufsz;
+      int q = q0, orow = q0 / g.OW, ow = q0 - orow * g.OW;
+      auto advance = [&]() {
+        q += V;
+        ow += V;
+        if (ow == g.OW) {
+          ow = 0;
+          ++orow;
+        }
+      };
+      auto stage_slice = [&](int gi) {
+        if (more && !g.d16) {
+          const int i0 = gi * per_step;
+          if (i0 < n4) stage4(nb, b ^ 1, i0, min(i0 + per_step, n4));
+        }
+      };
+      // two operand sets used alternately, each read one step ahead of its MFMAs.  The
+      // pair loop fetches unconditionally (its last fetch, one step past the band, reads
+      // in-buffer pitch pads / the clamped last pixel and is never used): with no
+      // conditional definitions the sets keep their registers, so the MFMAs wait only for
+      // their own set's reads, not for the set just issued (a conditional fetch made the
+      // compiler copy the new set into place behind an lgkmcnt(0) every step)
+      float a0[V], w0[NR][NW], a1[V], w1[NR][NW];
       fetch(L, q, orow, ow, a0, w0);
-      mfmas(a1, w1);
-      interleave();
-    }
-    if (ngroups & 1) {
-      stage_slice(ngroups - 1);
-      mfmas(a0, w0);
-    }
-  }
-  // part[split][tap][co][ci]: C[row][col], row = (i&3) + 8*(i>>2) + 4*h, col = lane&31
-  const int co_w = co0 + wm * 32, ci = ci0 + wn * 32 + l32;
-  if (ci < g.Cig) {
-#pragma unroll
-    for (int t = 0; t < 9; ++t) {
-      float* dst = part + ((int64_t)split * 9 + t) * g.Cog * g.Cig;
-#pragma unroll
-      for (int i = 0; i < 16; ++i) {
-        const int co = co_w + (i & 3) + 8 * (i >> 2) + 4 * h;
-        if (co < g.Cog) dst[(int64_t)co * g.Cig + ci] = acc[t][i];
+      const int npairs = ngroups >> 1;
+      for (int gp = 0; gp < npairs; ++gp) {
+        stage_slice(2 * gp);
+        advance();
+        fetch(L, q, orow, ow, a1, w1);
+        mfmas(a0, w0);
+        interleave();
+        stage_slice(2 * gp + 1);
+        advance();
+        fetch(L, q, orow, ow, a0, w0);
+        mfmas(a1, w1);
+        interleave();
+      }
+      if (ngroups & 1) {
+        stage_slice(ngroups - 1);
+        mfmas(a0, w0);
       }
     }
+    // part[split][tap][co][ci]: C[row][col], row = (i&3) + 8*(i>>2) + 4*h, col = lane&31
+    const int co_w = co0 + wm * 32, ci = ci0 + wn * 32 + l32;
+    if (ci < g.Cig) {
+#pragma unroll
+      for (int t = 0; t < NT; ++t) {
+        float* dst = part + ((int64_t)split * 9 + T0 + t) * g.Cog * g.Cig;
+#pragma unroll
+        for (int i = 0; i < 16; ++i) {
+          const int co = co_w + (i & 3) + 8 * (i >> 2) + 4 * h;
+          if (co < g.Cog) dst[(int64_t)co * g.Cig + ci] = acc[t][i];
+        }
+      }
+    }
+  };
+  if constexpr (NWV == 4) {
+    body(IntC<0>{}, IntC<9>{});
+  } else {
+    if (role == 0) body(IntC<0>{}, IntC<5>{});
+    else body(IntC<5>{}, IntC<9>{});
   }
+}
+
+// The band kernel's waves per workgroup: 8 (two per SIMD, the default), or 4 (one per
+// SIMD) under ssq_conv_wgrad_set_form(4) or the A/B knob SSQ_BAND_WAVES=4
+static int g_wgrad_form = 0;
+static int band_waves() {
+  static const int w = [] {
+    const char* e = getenv("SSQ_BAND_WAVES");
+    return e && *e && atoi(e) == 4 ? 4 : 8;
+  }();
+  return g_wgrad_form == 4 ? 4 : w;
 }
 
 // band plan: 0 if the shape is not a band shape or no tile fits two buffers in the LDS
@@ -1063,16 +1106,16 @@ static int band_plan(int64_t Nb, int64_t C, int64_t H, int64_t W, int64_t Co, in
 }
 
 // Non-depthwise form: 0 auto, 1 the R x S input-row-tile kernel (1x1 on its GEMM), 2 the
-// im2col-DMA kernel for every shape, 3 the band kernel where it applies (A/B knob:
-// ssq_conv_wgrad_set_form).  Auto takes the band kernel for the shapes band_plan accepts,
-// then the im2col-DMA kernel for ungrouped R x S > 1 convs with >= 128 output channels
-// (its 128 x 128 tile is half idle below that): ResNet-18 3x3 stride-2 convs 2-2.3x faster
-// than the row-tile kernel, 3x3 stride-1 1.1-1.4x (profiles/r2_wgrad_forms.log).
-static int g_wgrad_form = 0;
+// im2col-DMA kernel for every shape, 3 the band kernel where it applies, 4 the same at 4
+// waves per workgroup (A/B knob: ssq_conv_wgrad_set_form; g_wgrad_form is above).  Auto
+// takes the band kernel for the shapes band_plan accepts, then the im2col-DMA kernel for
+// ungrouped R x S > 1 convs with >= 128 output channels (its 128 x 128 tile is half idle
+// below that): ResNet-18 3x3 stride-2 convs 2-2.3x faster than the row-tile kernel, 3x3
+// stride-1 1.1-1.4x (profiles/r2_wgrad_forms.log).
 static bool use_band(int64_t Nb, int64_t C, int64_t H, int64_t W, int64_t Co, int64_t R,
                      int64_t S, int64_t st, int64_t pad, int64_t G, BandGeo& g, int* wmx,
                      int* vpx) {
-  if (g_wgrad_form != 0 && g_wgrad_form != 3) return false;
+  if (g_wgrad_form != 0 && g_wgrad_form != 3 && g_wgrad_form != 4) return false;
   return band_plan(Nb, C, H, W, Co, R, S, st, pad, G, g, wmx, vpx) != 0;
 }
 static bool use_i2c(int64_t R, int64_t S, int64_t Co, int64_t G) {
@@ -1086,7 +1129,7 @@ using namespace ssq;
 
 extern "C" int ssq_conv_wgrad_set_form(int form) {
   const int old = g_wgrad_form;
-  if (form >= 0 && form <= 3) g_wgrad_form = form;
+  if (form >= 0 && form <= 4) g_wgrad_form = form;
   return old;
 }
 
@@ -1188,25 +1231,33 @@ extern "C" int ssq_conv_wgrad(const float* x, const float* dy, int64_t Nb, int64
       const size_t needb = (size_t)gb.nsplit * 9 * (size_t)Co * (size_t)C * sizeof(float);
       SSQ_REQUIRE(ws && ws_bytes >= needb, SSQ_E_WS, "ssq_conv_wgrad: workspace too small");
       typedef void (*BandK)(const float*, const float*, BandGeo, float*);
-      // [wm == 4][stride == 2][V = 4, 2, 1]
-      static const BandK kernels[2][2][3] = {
-          {{wgrad_band_stage1<2, 1, 4>, wgrad_band_stage1<2, 1, 2>, wgrad_band_stage1<2, 1, 1>},
-           {wgrad_band_stage1<2, 2, 4>, wgrad_band_stage1<2, 2, 2>, wgrad_band_stage1<2, 2, 1>}},
-          {{wgrad_band_stage1<4, 1, 4>, wgrad_band_stage1<4, 1, 2>, wgrad_band_stage1<4, 1, 1>},
-           {wgrad_band_stage1<4, 2, 4>, wgrad_band_stage1<4, 2, 2>, wgrad_band_stage1<4, 2, 1>}}};
+      // [8 waves][wm == 4][stride == 2][V = 4, 2, 1]
+#define SSQ_BK(NWV)                                                                          \
+  {{{wgrad_band_stage1<2, 1, 4, NWV>, wgrad_band_stage1<2, 1, 2, NWV>,                        \
+     wgrad_band_stage1<2, 1, 1, NWV>},                                                        \
+    {wgrad_band_stage1<2, 2, 4, NWV>, wgrad_band_stage1<2, 2, 2, NWV>,                        \
+     wgrad_band_stage1<2, 2, 1, NWV>}},                                                       \
+   {{wgrad_band_stage1<4, 1, 4, NWV>, wgrad_band_stage1<4, 1, 2, NWV>,                        \
+     wgrad_band_stage1<4, 1, 1, NWV>},                                                        \
+    {wgrad_band_stage1<4, 2, 4, NWV>, wgrad_band_stage1<4, 2, 2, NWV>,                        \
+     wgrad_band_stage1<4, 2, 1, NWV>}}}
+      static const BandK kernels[2][2][2][3] = {SSQ_BK(4), SSQ_BK(8)};
+#undef SSQ_BK
       static bool band_attr = false;
       if (!band_attr) {  // two 80 KB buffers: the whole LDS
-        for (auto& a : kernels)
-          for (auto& b : a)
-            for (BandK k : b)
-              hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                  160 * 1024);
+        for (auto& a0 : kernels)
+          for (auto& a : a0)
+            for (auto& b : a)
+              for (BandK k : b)
+                hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                    160 * 1024);
         band_attr = true;
       }
-      const BandK kb = kernels[wmx == 4][stride == 2][vpx == 4 ? 0 : (vpx == 2 ? 1 : 2)];
+      const int w8 = band_waves() == 8;
+      const BandK kb = kernels[w8][wmx == 4][stride == 2][vpx == 4 ? 0 : (vpx == 2 ? 1 : 2)];
       const dim3 gridb((unsigned)(gb.nsplit * gb.m_tiles * gb.n_tiles));
       const size_t ldsb = 2 * (size_t)gb.bufsz * sizeof(float);
-      hipLaunchKernelGGL(kb, gridb, dim3(256), ldsb, s, x, dy, gb, (float*)ws);
+      hipLaunchKernelGGL(kb, gridb, dim3(w8 ? 512 : 256), ldsb, s, x, dy, gb, (float*)ws);
       const int64_t inner = Co * C, nb = 9 * inner;
       hipLaunchKernelGGL(wgrad_stage2, dim3((unsigned)std::min<int64_t>((nb + 63) / 64, 4096)),
                          dim3(256), 0, s, (const float*)ws, gb.nsplit, nb, dw, inner, 9);

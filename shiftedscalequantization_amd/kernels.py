@@ -1184,8 +1184,8 @@ def wgrad_kind(x_shape, w_shape, stride, padding, groups):
 
 def set_wgrad_form(form):
     """K17 non-depthwise form: 0 auto, 1 input-row-tile (+1x1 GEMM), 2 im2col-DMA, 3 band
-    (3x3 pad 1 shapes, Cin / Cout multiples of 32, else the row tile); returns the previous
-    value."""
+    (3x3 pad 1 shapes, Cin / Cout multiples of 32, else the row tile), 4 band at 4 waves per
+    workgroup (one per SIMD; 3 runs 8); returns the previous value."""
     return int(query("ssq_conv_wgrad_set_form", int(form)))
 
 

@@ -724,7 +724,7 @@ def test_lp_loss_rows_equals_gathered(K, row_shape, p):
         np.testing.assert_array_equal(host(g1).view(np.int32), host(g2).view(np.int32))
 
 
-@pytest.fixture(params=[1, 2, 3], ids=["tile", "i2c", "band"])
+@pytest.fixture(params=[1, 2, 3, 4], ids=["tile", "i2c", "band", "band4w"])
 def wgrad_form(request):
     from shiftedscalequantization_amd import kernels
     old = kernels.set_wgrad_form(request.param)
@@ -785,6 +785,31 @@ def test_conv_wgrad_matches_fp64(K, cfg, wgrad_form):
     finally:
         K.WGRAD_POLICY, K.WGRAD_GEMM = old, old_gemm
     np.testing.assert_array_equal(host(wd.grad).view(np.int32), host(dw1).view(np.int32))
+
+
+@pytest.mark.parametrize("cfg", [
+    # (Nb, C, H, Co, stride): ResNet-18 layer1 / layer2.0 s2 / layer2 / layer3.0 s2 (16-B
+    # staging), layer3 / layer4 (4-B staging, 2 / 1 pixels per step), ragged tiles
+    (32, 64, 56, 64, 1), (8, 64, 56, 128, 2), (8, 128, 28, 128, 1), (8, 128, 28, 256, 2),
+    (4, 256, 14, 256, 1), (4, 512, 7, 512, 1), (3, 32, 8, 160, 1), (2, 96, 12, 64, 1)])
+def test_band_wgrad_two_waves_per_simd_bit_identical(K, cfg):
+    """The band kernel at 8 waves per workgroup (two per SIMD, the taps split 5 / 4 between
+    the waves of a tile) gives the 4-wave kernel's bits: every tap sums the same pixels in
+    the same order."""
+    Nb, C, H, Co, st = cfg
+    gen = torch.Generator().manual_seed(sum(cfg))
+    x = torch.randn(Nb, C, H, H, generator=gen).cuda()
+    oh = (H - 1) // st + 1
+    dy = torch.randn(Nb, Co, oh, oh, generator=gen).cuda()
+    old = K.set_wgrad_form(3)
+    try:
+        assert K.wgrad_kind(x.shape, (Co, C, 3, 3), st, 1, 1) in (3, 6)
+        dw8 = K.conv_wgrad(x, dy, (Co, C, 3, 3), st, 1, 1)
+        K.set_wgrad_form(4)
+        dw4 = K.conv_wgrad(x, dy, (Co, C, 3, 3), st, 1, 1)
+    finally:
+        K.set_wgrad_form(old)
+    np.testing.assert_array_equal(host(dw8).view(np.int32), host(dw4).view(np.int32))
 
 
 @pytest.mark.parametrize("cfg", [
