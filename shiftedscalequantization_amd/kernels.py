@@ -1340,6 +1340,8 @@ class Conv2dFn(torch.autograd.Function):
             ctx.save_for_backward(x, weight, col)
             return y
         ctx.save_for_backward(x, weight, None)
+        if _use_fwd_1x1(x, weight, stride, padding, dilation, groups):
+            return conv1x1_fwd_gemm(x, weight, stride)
         return torch.nn.functional.conv2d(x, weight, None, stride, padding, dilation, groups)
 
     @staticmethod
@@ -1428,6 +1430,41 @@ def _use_fwd_gemm(x, weight, stride, padding, groups=1):
             and _use_wgrad_gemm(x, weight, stride, padding, groups))
 
 
+# 1x1 stride-2 convs (the ResNet downsamples) forward as ONE strided-batched library GEMM
+# on the subsampled input, y[n] = W @ x[n, :, ::s, ::s]: NCHW in, NCHW out (MIOpen
+# transposes NCHW <-> CNHW around its own GEMM).  tools/ds_fwd_probe.py
+# (profiles/r3_ds_fwd_probe.json), deterministic solvers: layer2.0 35.9 -> 22.3 us and
+# layer4.0 30.9 -> 14.4 at batch 32 (recon), 112 -> 66 and 103 -> 34 at batch 128
+# (validation); layer3.0's 14x14 plane is slower at batch 32 (27.5 -> 56.6, hipBLASLt's
+# pick for that batched shape), so output planes of 100-400 pixels stay on MIOpen below
+# batch 128.  Bit-identical run to run.  Stride-1 1x1 convs stay on MIOpen (unmeasured).
+# A/B knob: SSQ_FWD_1X1_GEMM=0.
+FWD_1X1_GEMM = os.environ.get("SSQ_FWD_1X1_GEMM", "1") != "0"
+
+
+def _use_fwd_1x1(x, weight, stride, padding, dilation, groups):
+    if not FWD_1X1_GEMM or groups != 1 or weight.shape[2] != 1 or weight.shape[3] != 1:
+        return False
+    if x.dim() != 4 or not x.is_cuda or x.dtype != torch.float32:
+        return False
+    st, pad, dil = (_pair(v) for v in (stride, padding, dilation))
+    if st[0] != st[1] or st[0] < 2 or pad != [0, 0] or dil != [1, 1]:
+        return False
+    oh, ow = _out_plane(x, weight, st[0], 0)
+    return not (100 < oh * ow < 400 and x.shape[0] < 128)
+
+
+def conv1x1_fwd_gemm(x, weight, stride):
+    """F.conv2d of a 1x1 / pad 0 / stride s conv as one strided-batched GEMM on the
+    subsampled input (see FWD_1X1_GEMM)."""
+    st = stride if isinstance(stride, int) else stride[0]
+    xs = x[:, :, ::st, ::st]
+    n, c, oh, ow = xs.shape
+    co = int(weight.shape[0])
+    y = torch.matmul(weight.detach().reshape(co, c), xs.reshape(n, c, oh * ow))
+    return y.view(n, co, oh, ow)
+
+
 def _use_k17(x, weight, stride, padding, groups=1):
     if WGRAD_POLICY == "always":
         return True
@@ -1455,7 +1492,8 @@ DWCONV_POLICY = "auto"
 
 def conv2d(x, weight, stride=1, padding=0, dilation=1, groups=1):
     """F.conv2d without bias: depthwise convs on K18/K17 (DWCONV_POLICY), otherwise MIOpen
-    with the K17 weight gradient when the weight needs one (WGRAD_POLICY)."""
+    with the K17 weight gradient when the weight needs one (WGRAD_POLICY); 1x1 stride-2
+    forwards as one batched GEMM (FWD_1X1_GEMM)."""
     if DWCONV_POLICY == "auto" and dwconv_supported(x, weight, stride, padding, dilation, groups) \
             and x.is_contiguous():
         if torch.is_grad_enabled() and (x.requires_grad or weight.requires_grad):
@@ -1467,4 +1505,7 @@ def conv2d(x, weight, stride=1, padding=0, dilation=1, groups=1):
              (conv_wgrad_supported(x, weight, stride, padding, dilation, groups) and
               _use_k17(x, weight, stride, padding, groups))):
         return Conv2dFn.apply(x, weight, stride, padding, dilation, groups)
+    if _use_fwd_1x1(x, weight, stride, padding, dilation, groups) and \
+            not (torch.is_grad_enabled() and (x.requires_grad or weight.requires_grad)):
+        return conv1x1_fwd_gemm(x, weight, stride)
     return torch.nn.functional.conv2d(x, weight, None, stride, padding, dilation, groups)

@@ -813,6 +813,58 @@ def test_band_wgrad_two_waves_per_simd_bit_identical(K, cfg):
 
 
 @pytest.mark.parametrize("cfg", [
+    # (Nb, C, H, Co): ResNet-18 downsamples at batch 32 (layer2.0 / layer4.0: batched GEMM;
+    # layer3.0: MIOpen below batch 128), layer3.0 at batch 128, odd sizes
+    (32, 64, 56, 128), (32, 256, 14, 512), (32, 128, 28, 256), (128, 128, 28, 256),
+    (3, 40, 9, 24)])
+def test_conv1x1_stride2_forward_gemm(K, cfg):
+    """1x1 stride-2 forward as one strided-batched GEMM (FWD_1X1_GEMM) vs the fp64 conv within
+    the fp32 accumulation bound, bit-identical run to run, taken by K.conv2d with and without
+    grad exactly where the policy says, and the autograd path's gradients unchanged (MIOpen
+    input gradient, K17 / GEMM weight gradient)."""
+    Nb, C, H, Co = cfg
+    gen = torch.Generator().manual_seed(sum(cfg))
+    x = torch.randn(Nb, C, H, H, generator=gen)
+    w = torch.randn(Co, C, 1, 1, generator=gen) * 0.05
+    ref = torch.nn.functional.conv2d(x.double(), w.double(), None, 2)
+    mag = torch.nn.functional.conv2d(x.double().abs(), w.double().abs(), None, 2)
+    xd, wd = x.cuda(), w.cuda()
+    use = K._use_fwd_1x1(xd, wd, 2, 0, 1, 1)
+    assert use == (not (100 < ((H + 1) // 2) ** 2 < 400 and Nb < 128))
+    y1, y2 = K.conv1x1_fwd_gemm(xd, wd, 2), K.conv1x1_fwd_gemm(xd, wd, 2)
+    np.testing.assert_array_equal(host(y1).view(np.int32), host(y2).view(np.int32))
+    err = (y1.double().cpu() - ref).abs()
+    assert bool((err <= 1e-5 * mag + 1e-30).all())
+    with torch.no_grad():
+        y3 = K.conv2d(xd, wd, 2, 0)
+    if use:
+        np.testing.assert_array_equal(host(y3).view(np.int32), host(y1).view(np.int32))
+    assert bool(((y3.double().cpu() - ref).abs() <= 1e-5 * mag + 1e-30).all())
+    # training path under the reference's cudnn.deterministic (Conv2dFn): same forward, and
+    # the gradients of the MIOpen-forward path
+    old_det = torch.backends.cudnn.deterministic
+    old, K.FWD_1X1_GEMM = K.FWD_1X1_GEMM, True
+    torch.backends.cudnn.deterministic = True
+    try:
+        xg = xd.clone().requires_grad_(True)
+        wg = wd.clone().requires_grad_(True)
+        yg = K.conv2d(xg, wg, 2, 0)
+        if use:
+            np.testing.assert_array_equal(host(yg.detach()).view(np.int32), host(y1).view(np.int32))
+        dy = torch.randn(yg.shape, generator=gen).cuda()
+        yg.backward(dy)
+        K.FWD_1X1_GEMM = False
+        xm = xd.clone().requires_grad_(True)
+        wm = wd.clone().requires_grad_(True)
+        K.conv2d(xm, wm, 2, 0).backward(dy)
+    finally:
+        K.FWD_1X1_GEMM = old
+        torch.backends.cudnn.deterministic = old_det
+    np.testing.assert_array_equal(host(xg.grad).view(np.int32), host(xm.grad).view(np.int32))
+    np.testing.assert_array_equal(host(wg.grad).view(np.int32), host(wm.grad).view(np.int32))
+
+
+@pytest.mark.parametrize("cfg", [
     # (Nb, C, H, Co, k, stride, pad): ResNet-18 layer3 / layer3.0 s2 / layer4 / layer4.0 s2
     # at batch 32 (the shapes the GEMM policy takes), a 5x5 and ragged sizes
     (32, 256, 14, 256, 3, 1, 1), (32, 128, 28, 256, 3, 2, 1), (32, 512, 7, 512, 3, 1, 1),
