@@ -11,7 +11,7 @@ import torch
 import torch.nn.functional as F
 
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
-from tools.overlap_probe import graph_ms  # noqa: E402
+from shiftedscalequantization_amd.recon_bench import graph_time_ms as graph_ms  # noqa: E402
 
 dev = torch.device("cuda:0")
 
