@@ -1443,7 +1443,9 @@ FWD_1X1_GEMM = os.environ.get("SSQ_FWD_1X1_GEMM", "1") != "0"
 
 
 def _use_fwd_1x1(x, weight, stride, padding, dilation, groups):
-    if not FWD_1X1_GEMM or groups != 1 or weight.shape[2] != 1 or weight.shape[3] != 1:
+    # WGRAD_POLICY 'never' is the all-MIOpen A/B mode: no GEMM convs there either
+    if not FWD_1X1_GEMM or WGRAD_POLICY == "never" or groups != 1 or weight.shape[2] != 1 \
+            or weight.shape[3] != 1:
         return False
     if x.dim() != 4 or not x.is_cuda or x.dtype != torch.float32:
         return False
