@@ -1,6 +1,8 @@
 # r3: K17 band-kernel A/B in one session: the fp64 wgrad parity tests and the recon loop
 # tests on the new build, then tools/band_ab.py alternating the base build (ab/) and the
-# new one (in-tree), then the recon loop of layer1/2 under rocprofv3 on the new build.
+# new one (in-tree).  Make the base first, e.g.: git stash; python -c "import __graft_entry__
+# as g; g.build()"; mkdir -p ab; cp shiftedscalequantization_amd/libssq.so ab/libssq_base.so;
+# git stash pop; rebuild.
 R=${GRAFT_REPO_ROOT:-$(pwd)}
 OUT=$R/gpurun_out
 mkdir -p $OUT
