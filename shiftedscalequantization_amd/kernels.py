@@ -153,38 +153,61 @@ def round_quant(x, delta, zp, n_bits, sym=False, scale=1.0):
     return RoundQuantFn.apply(x, delta, zp, n_bits, sym, float(scale))
 
 
+class FqMultiPlan:
+    """fake_quant_multi's arguments checked and packed once: calling the plan launches the
+    same table again (one ctypes call), e.g. a fixed model's weights quantised every step.
+    The plan holds its tensors; it reads their current values at each launch, so in-place
+    updates are seen, but a tensor replaced by a new one needs a new plan."""
+
+    def __init__(self, xs, deltas, zps, n_bits, sym=False, out=None):
+        n = len(xs)
+        if out is None:
+            ys = [torch.empty_like(x) for x in xs]
+        else:
+            if len(out) != n:
+                raise ValueError(f"fake_quant_multi: {len(out)} outputs for {n} inputs")
+            for k, (x, y) in enumerate(zip(xs, out)):
+                A.check(y, f"out[{k}]")
+                if y.shape != x.shape or not y.is_contiguous():
+                    raise ValueError(f"fake_quant_multi: out[{k}] must be contiguous, shape "
+                                     f"{tuple(x.shape)}")
+            ys = list(out)
+        keep = []
+        P = C.c_void_p * n
+        xa, ya, da, za = P(), P(), P(), P()
+        na, ia, ca = (C.c_int64 * n)(), (C.c_int64 * n)(), (C.c_int64 * n)()
+        lo_a, hi_a = (C.c_int * n)(), (C.c_int * n)()
+        nb = n_bits if isinstance(n_bits, (list, tuple)) else [n_bits] * n
+        for k, (x, d, z, y) in enumerate(zip(xs, deltas, zps, ys)):
+            x, xp = fptr(x)
+            d, dp = fptr(d.detach())
+            z, zpp = fptr(z.detach())
+            keep += [x, d, z]
+            inner, nch = _channel_layout(x, d)
+            xa[k], ya[k], da[k], za[k] = xp.value, y.data_ptr(), dp.value, zpp.value
+            na[k], ia[k], ca[k] = x.numel(), inner, nch
+            lo_a[k], hi_a[k] = qrange(nb[k], sym)
+        self.ys, self.keep = ys, keep
+        self.args = (n, xa, ya, da, za, na, ia, ca, lo_a, hi_a)
+        self.device = xs[0].device
+
+    def __call__(self):
+        call("ssq_fq_fwd_multi", *self.args, stream_of(self.ys[0]))
+        if _DEFERRED_FQ_KEEP is not None:
+            # the table may launch later (riding on the next per-tensor launch): keep any
+            # contiguous copies made for it alive until then
+            _DEFERRED_FQ_KEEP.append(self)
+        return self.ys
+
+
 def fake_quant_multi(xs, deltas, zps, n_bits, sym=False, out=None):
     """Every tensor of a list in one launch (per-channel params staged in LDS); out: a
-    list of contiguous fp32 outputs, one per input and of its shape (else allocated)."""
-    n = len(xs)
-    if out is None:
-        ys = [torch.empty_like(x) for x in xs]
-    else:
-        if len(out) != n:
-            raise ValueError(f"fake_quant_multi: {len(out)} outputs for {n} inputs")
-        for k, (x, y) in enumerate(zip(xs, out)):
-            A.check(y, f"out[{k}]")
-            if y.shape != x.shape or not y.is_contiguous():
-                raise ValueError(f"fake_quant_multi: out[{k}] must be contiguous, shape "
-                                 f"{tuple(x.shape)}")
-        ys = list(out)
-    keep = []
-    P = C.c_void_p * n
-    xa, ya, da, za = P(), P(), P(), P()
-    na, ia, ca = (C.c_int64 * n)(), (C.c_int64 * n)(), (C.c_int64 * n)()
-    lo_a, hi_a = (C.c_int * n)(), (C.c_int * n)()
-    nb = n_bits if isinstance(n_bits, (list, tuple)) else [n_bits] * n
-    for k, (x, d, z, y) in enumerate(zip(xs, deltas, zps, ys)):
-        x, xp = fptr(x)
-        d, dp = fptr(d.detach())
-        z, zpp = fptr(z.detach())
-        keep += [x, d, z]
-        inner, nch = _channel_layout(x, d)
-        xa[k], ya[k], da[k], za[k] = xp.value, y.data_ptr(), dp.value, zpp.value
-        na[k], ia[k], ca[k] = x.numel(), inner, nch
-        lo_a[k], hi_a[k] = qrange(nb[k], sym)
-    call("ssq_fq_fwd_multi", n, xa, ya, da, za, na, ia, ca, lo_a, hi_a, stream_of(xs[0]))
-    return ys
+    list of contiguous fp32 outputs, one per input and of its shape (else allocated).
+    FqMultiPlan packs the same arguments once for repeated launches."""
+    return FqMultiPlan(xs, deltas, zps, n_bits, sym, out)()
+
+
+_DEFERRED_FQ_KEEP = None
 
 
 class deferred_fq_multi:
@@ -196,10 +219,14 @@ class deferred_fq_multi:
         self.on, self.device = on, device
 
     def __enter__(self):
+        global _DEFERRED_FQ_KEEP
         self.prev = bool(query("ssq_set_deferred_fq_multi", 1)) if self.on else None
+        if self.on:
+            self.prev_keep, _DEFERRED_FQ_KEEP = _DEFERRED_FQ_KEEP, []
         return self
 
     def __exit__(self, *exc):
+        global _DEFERRED_FQ_KEEP
         if self.on:
             dev_ = torch.device("cuda", torch.cuda.current_device()) if self.device is None \
                 else self.device
@@ -207,6 +234,8 @@ class deferred_fq_multi:
                 call("ssq_flush_fq_multi", C.c_void_p(torch.cuda.current_stream(dev_).cuda_stream))
             finally:
                 query("ssq_set_deferred_fq_multi", int(self.prev))
+                # every queued table has launched: its inputs may be freed (stream order)
+                _DEFERRED_FQ_KEEP = self.prev_keep
 
 
 # ------------------------------------------------------------------ K3/K4

@@ -215,6 +215,20 @@ def test_fq_multi_segment(K):
     with pytest.raises(ValueError):
         K.fake_quant_multi([w.cuda() for w in ws], [dev(p[0]) for p in params],
                            [dev(p[1]) for p in params], 2, out=outs[::-1])
+    # a launch plan: the same bits every launch, in-place input updates seen, riding on a
+    # per-tensor launch under deferred_fq_multi
+    xs = [w.cuda() for w in ws]
+    plan = K.FqMultiPlan(xs, [dev(p[0]) for p in params], [dev(p[1]) for p in params], 2)
+    for y, y3 in zip(ys, plan()):
+        np.testing.assert_array_equal(host(y3), host(y))
+    xs[1].mul_(-1.0)
+    act = torch.randn(4, 8, 7, 7, generator=gen).relu_().cuda()
+    with K.deferred_fq_multi():
+        ys4 = plan()
+        K.fake_quant_fwd(act, dev([0.1]), dev([0.0]), 4)
+    np.testing.assert_array_equal(host(ys4[1]), R.fake_quant(-ws[1].numpy(), params[1][0],
+                                                            params[1][1], 2)[0])
+    np.testing.assert_array_equal(host(ys4[0]), host(ys[0]))
 
 
 def test_fq_multi_many_ragged_segments(K):

@@ -19,15 +19,19 @@ def main():
     act, d_a, z_a, weights, dws, zws, bits = bench.make_workload(dev, 0, 1024)
     y_act = torch.empty_like(act)
     y_w = [torch.empty_like(w) for w in weights]
-    prealloc = [True]
+    plan = K.FqMultiPlan(weights, dws, zws, bits, out=y_w)
+    mode = ["alloc"]
 
     def step():
         with K.deferred_fq_multi():
-            K.fake_quant_multi(weights, dws, zws, bits, out=y_w if prealloc[0] else None)
+            if mode[0] == "plan":
+                plan()
+            else:
+                K.fake_quant_multi(weights, dws, zws, bits, out=y_w if mode[0] == "out" else None)
             K.fake_quant_fwd(act, d_a, z_a, 4, out=y_act)
 
-    for pre in (False, True):
-        prealloc[0] = pre
+    for m in ("alloc", "out", "plan"):
+        mode[0] = m
         for _ in range(20):
             step()
         torch.cuda.synchronize()
@@ -39,7 +43,7 @@ def main():
                 step()
             host.append((time.perf_counter() - t0) / 20 * 1e3)
             torch.cuda.synchronize()
-        print(f"outputs {'preallocated' if pre else 'allocated per call'}: host ms/step "
+        print(f"{m} (alloc: outputs per call, out: preallocated, plan: FqMultiPlan): host ms/step "
               f"(20 calls, no sync) median {statistics.median(host):.4f}  all "
               f"{[round(h, 4) for h in host]}")
     dev_ms = graph_time_ms(step, reps=20, rounds=5)
