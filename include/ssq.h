@@ -313,6 +313,12 @@ int ssq_bias_act(const float* y, const float* bias, const float* res, float* out
                  int64_t hw, int64_t C, int relu, ssq_stream_t stream);
 int ssq_relu_bwd(const float* g, const float* out, float* gin, int64_t n, ssq_stream_t stream);
 int ssq_relu6_bwd(const float* g, const float* out, float* gin, int64_t n, ssq_stream_t stream);
+/* F.max_pool2d forward, NCHW fp32, square K x K window (K <= 7), stride, pad <= K/2, no
+ * dilation, floor mode: torch's rule (a larger value or a NaN replaces the running max, ties
+ * keep the first, window walked row-major), bit-identical to torch.  The ResNet stem's pool
+ * (models/resnet.py's maxpool after the stem; validation common.py:153-221). */
+int ssq_maxpool2d_fwd(const float* x, float* y, int64_t N, int64_t C, int64_t H, int64_t W,
+                      int64_t K, int64_t stride, int64_t pad, ssq_stream_t stream);
 /* ssq_bias_act with the following per-tensor activation fake-quant (quant_layer.py:92-98,
  * applied at quant_layer.py:272 / quant_block.py:118) in the same pass:
  *   yq = (clamp(rint(out/delta[0]) + zp[0], qmin, qmax) - zp[0]) * delta[0]

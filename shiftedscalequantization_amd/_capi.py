@@ -93,6 +93,7 @@ SIGNATURES = {
     "ssq_conv_wgrad_workspace_size": (_sz, [_i64] * 10),
     "ssq_conv_wgrad": (_i, [_p, _p] + [_i64] * 10 + [_p, _p, _sz, _p]),
     "ssq_wgrad_gemm_operands": (_i, [_p, _p] + [_i64] * 9 + [_p, _p, _p]),
+    "ssq_maxpool2d_fwd": (_i, [_p, _p] + [_i64] * 7 + [_p]),
     "ssq_dwconv_supported": (_i, [_i64] * 8),
     "ssq_dwconv_fwd": (_i, [_p, _p, _p] + [_i64] * 8 + [_p]),
     "ssq_dwconv_bwd_data": (_i, [_p, _p, _p] + [_i64] * 8 + [_p]),

@@ -1097,3 +1097,82 @@ extern "C" int ssq_set_deferred_finalize(int on) {
 extern "C" int ssq_flush_finalize(ssq_stream_t stream) {
   return fin_flush((hipStream_t)stream);
 }
+
+// ------------------------------------------------------------------ stem max-pool
+// F.max_pool2d forward (NCHW fp32, kernel K x K <= 7 x 7, stride, zero-free padding, no
+// dilation, floor mode): the ResNet stem's 3x3 / s2 / p1 pool that follows the stem's K13
+// epilogue in validation (torch's kernel ran at 1.8 TB/s there).  One output per thread
+// (2x2 / 3x3 windows: every tap loaded at once), the window walked row-major with torch's
+// rule (a larger value or a NaN replaces the running max; ties keep the first), so the
+// result is bit-identical to torch's.
+template <int KT>   // KT > 0: the window size at compile time (every load issued at once)
+__global__ __launch_bounds__(kBlock) void maxpool2d_kernel(const float* __restrict__ x,
+                                                           float* __restrict__ y, uint32_t total,
+                                                           uint32_t H, uint32_t W, uint32_t OH,
+                                                           uint32_t OW, uint32_t Kr, uint32_t st,
+                                                           int pad, FastDiv dOW, FastDiv dOH) {
+  const uint32_t K = KT > 0 ? (uint32_t)KT : Kr;
+  const uint32_t stride = gridDim.x * blockDim.x;
+  for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < total; i += stride) {
+    const uint32_t q1 = fdiv(i, dOW), ow = i - q1 * OW;
+    const uint32_t nc = fdiv(q1, dOH), oh = q1 - nc * OH;
+    const float* __restrict__ xp = x + (size_t)nc * H * W;
+    const int h0 = (int)(oh * st) - pad, w0 = (int)(ow * st) - pad;
+    float m = -__builtin_inff();
+    if constexpr (KT > 0) {
+      // in-range taps loaded (out-of-range ones read a clamped in-plane address and are
+      // skipped), then the row-major max
+      float v[KT * KT];
+      bool ok[KT * KT];
+#pragma unroll
+      for (int r = 0; r < KT; ++r)
+#pragma unroll
+        for (int s2 = 0; s2 < KT; ++s2) {
+          const int h = h0 + r, w = w0 + s2;
+          ok[r * KT + s2] = h >= 0 && h < (int)H && w >= 0 && w < (int)W;
+          const int hc = min(max(h, 0), (int)H - 1), wc = min(max(w, 0), (int)W - 1);
+          v[r * KT + s2] = xp[(size_t)hc * W + wc];
+        }
+#pragma unroll
+      for (int t = 0; t < KT * KT; ++t)
+        if (ok[t] && (v[t] > m || __builtin_isnan(v[t]))) m = v[t];
+    } else {
+      for (uint32_t r = 0; r < K; ++r) {
+        const int h = h0 + (int)r;
+        if (h < 0 || h >= (int)H) continue;
+        for (uint32_t s2 = 0; s2 < K; ++s2) {
+          const int w = w0 + (int)s2;
+          if (w < 0 || w >= (int)W) continue;
+          const float v = xp[(size_t)h * W + w];
+          if (v > m || __builtin_isnan(v)) m = v;
+        }
+      }
+    }
+    y[i] = m;
+  }
+}
+
+extern "C" int ssq_maxpool2d_fwd(const float* x, float* y, int64_t N, int64_t C, int64_t H,
+                                 int64_t W, int64_t K, int64_t stride, int64_t pad,
+                                 ssq_stream_t s) {
+  SSQ_REQUIRE(x && y, SSQ_E_ARG, "ssq_maxpool2d_fwd: null pointer");
+  SSQ_REQUIRE(N >= 1 && C >= 1 && H >= 1 && W >= 1 && K >= 1 && K <= 7 && stride >= 1 &&
+                  pad >= 0 && 2 * pad <= K, SSQ_E_ARG,
+              "ssq_maxpool2d_fwd: bad geometry (K <= 7, pad <= K / 2)");
+  const int64_t OH = (H + 2 * pad - K) / stride + 1, OW = (W + 2 * pad - K) / stride + 1;
+  SSQ_REQUIRE(OH >= 1 && OW >= 1, SSQ_E_ARG, "ssq_maxpool2d_fwd: empty output");
+  const int64_t total = N * C * OH * OW;
+  SSQ_REQUIRE(total < (1ll << 31) && N * C * H * W < (1ll << 31), SSQ_E_ARG,
+              "ssq_maxpool2d_fwd: tensor exceeds 2^31 elements");
+  const dim3 grid(grid_for(total, kBlock, 8192));
+#define SSQ_MP(KT)                                                                         \
+  hipLaunchKernelGGL(maxpool2d_kernel<KT>, grid, dim3(kBlock), 0, (hipStream_t)s, x, y,      \
+                     (uint32_t)total, (uint32_t)H, (uint32_t)W, (uint32_t)OH, (uint32_t)OW, \
+                     (uint32_t)K, (uint32_t)stride, (int)pad, make_fastdiv((uint32_t)OW),    \
+                     make_fastdiv((uint32_t)OH))
+  if (K == 3) SSQ_MP(3);
+  else if (K == 2) SSQ_MP(2);
+  else SSQ_MP(0);
+#undef SSQ_MP
+  return check_launch("ssq_maxpool2d_fwd");
+}

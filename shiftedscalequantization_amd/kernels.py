@@ -210,6 +210,54 @@ def fake_quant_multi(xs, deltas, zps, n_bits, sym=False, out=None):
 _DEFERRED_FQ_KEEP = None
 
 
+def maxpool2d(x, k, stride, padding):
+    """F.max_pool2d forward (no dilation, floor mode) on ssq_maxpool2d_fwd: bit-identical to
+    torch's, NCHW fp32 on the device, K <= 7, padding <= K // 2."""
+    x, xp = fptr(x, "x")
+    N, C_, H, W = (int(v) for v in x.shape)
+    OH, OW = (H + 2 * padding - k) // stride + 1, (W + 2 * padding - k) // stride + 1
+    y = torch.empty((N, C_, OH, OW), dtype=torch.float32, device=x.device)
+    call("ssq_maxpool2d_fwd", xp, _vp(y), N, C_, H, W, int(k), int(stride), int(padding),
+         stream_of(x))
+    return y
+
+
+# QuantModel swaps nn.MaxPool2d for SsqMaxPool2d (A/B knob: SSQ_MAXPOOL=0 keeps torch's)
+MAXPOOL_HIP = os.environ.get("SSQ_MAXPOOL", "1") != "0"
+
+
+class SsqMaxPool2d(torch.nn.MaxPool2d):
+    """nn.MaxPool2d whose forward runs on ssq_maxpool2d_fwd where it applies (a square
+    window of <= 7, padding <= K // 2, no dilation / ceil mode / indices, a 4-D fp32 device
+    input that needs no gradient); torch's pooling otherwise.  Same results either way."""
+
+    @staticmethod
+    def wrap(m):
+        s = SsqMaxPool2d(m.kernel_size, m.stride, m.padding, m.dilation, m.return_indices,
+                         m.ceil_mode)
+        return s
+
+    def _plan(self):
+        def one(v):
+            if isinstance(v, int):
+                return v
+            return v[0] if len(set(v)) == 1 else None
+        k, st, pad, dil = (one(v) for v in (self.kernel_size, self.stride, self.padding,
+                                            self.dilation))
+        if None in (k, st, pad, dil) or dil != 1 or self.ceil_mode or self.return_indices:
+            return None
+        if k > 7 or 2 * pad > k:
+            return None
+        return k, st, pad
+
+    def forward(self, x):
+        plan = self._plan()
+        if (plan is not None and x.dim() == 4 and x.is_cuda and x.dtype == torch.float32
+                and not (torch.is_grad_enabled() and x.requires_grad)):
+            return maxpool2d(x, *plan)
+        return super().forward(x)
+
+
 class deferred_fq_multi:
     """Context: a fake_quant_multi inside it rides on the next per-tensor fake_quant_fwd of
     its stream -- one launch for both (include/ssq.h ssq_set_deferred_fq_multi); a table

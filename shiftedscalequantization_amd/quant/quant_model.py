@@ -3,6 +3,7 @@ Conv2d/Linear by QuantModule and known residual blocks by quant blocks."""
 import torch
 import torch.nn as nn
 
+from .. import kernels as K
 from .fold_bn import search_fold_and_remove_bn
 from .quant_block import BaseQuantBlock, specials
 from .quant_layer import QuantModule, StraightThrough
@@ -38,6 +39,9 @@ class QuantModel(nn.Module):
                     setattr(module, name, StraightThrough())
             elif isinstance(child_module, StraightThrough):
                 continue
+            elif type(child_module) is nn.MaxPool2d and K.MAXPOOL_HIP:
+                # the stem's pool on ssq_maxpool2d_fwd (same results as torch's)
+                setattr(module, name, K.SsqMaxPool2d.wrap(child_module))
             else:
                 self.quant_module_refactor(child_module, weight_quant_params, act_quant_params,
                                            depth + 1, moduleName=curName)

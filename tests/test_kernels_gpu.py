@@ -827,6 +827,36 @@ def test_band_wgrad_two_waves_per_simd_bit_identical(K, cfg):
 
 
 @pytest.mark.parametrize("cfg", [
+    # (N, C, H, W, k, stride, pad): the ResNet stem's pool at batch 8, odd planes, 2x2 / s2,
+    # 3x3 / s1, 5x5 / s2 / p2, a 7x7 window over a 7x7 plane
+    (8, 64, 112, 112, 3, 2, 1), (3, 5, 17, 13, 3, 2, 1), (2, 4, 8, 8, 2, 2, 0),
+    (2, 3, 9, 11, 3, 1, 1), (1, 6, 15, 15, 5, 2, 2), (2, 2, 7, 7, 7, 1, 3)])
+def test_maxpool2d_matches_torch(K, cfg):
+    """ssq_maxpool2d_fwd (SsqMaxPool2d, the stem's pool in QuantModel) == torch's
+    F.max_pool2d bit for bit, NaN / inf / signed zeros / ties included; the module takes
+    torch's path where a gradient is needed."""
+    N, C, H, W, k, st, pad = cfg
+    gen = torch.Generator().manual_seed(sum(cfg))
+    x = torch.randn(N, C, H, W, generator=gen)
+    x.view(-1)[:8] = torch.tensor([float("nan"), -0.0, 0.0, float("inf"), -float("inf"),
+                                   1.0, 1.0, -0.0])
+    x[0, 0, 1, :] = 0.0
+    x[0, 0, 2, ::2] = -0.0
+    xd = x.cuda()
+    ref = torch.nn.functional.max_pool2d(xd, k, st, pad)
+    y = K.maxpool2d(xd, k, st, pad)
+    np.testing.assert_array_equal(host(y).view(np.int32), host(ref).view(np.int32))
+    m = K.SsqMaxPool2d.wrap(torch.nn.MaxPool2d(k, st, pad))
+    with torch.no_grad():
+        np.testing.assert_array_equal(host(m(xd)).view(np.int32), host(ref).view(np.int32))
+    xg = xd.clone().requires_grad_(True)
+    out = m(xg)
+    assert out.grad_fn is not None
+    out.sum().backward()
+    assert xg.grad is not None
+
+
+@pytest.mark.parametrize("cfg", [
     # (Nb, C, H, Co): ResNet-18 downsamples at batch 32 (layer2.0 / layer4.0: batched GEMM;
     # layer3.0: MIOpen below batch 128), layer3.0 at batch 128, odd sizes
     (32, 64, 56, 128), (32, 256, 14, 512), (32, 128, 28, 256), (128, 128, 28, 256),
