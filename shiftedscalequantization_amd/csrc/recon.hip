@@ -1105,6 +1105,53 @@ extern "C" int ssq_flush_finalize(ssq_stream_t stream) {
 // (2x2 / 3x3 windows: every tap loaded at once), the window walked row-major with torch's
 // rule (a larger value or a NaN replaces the running max; ties keep the first), so the
 // result is bit-identical to torch's.
+// The stem's 3x3 / s2 / p1 pool with W and OW even: two adjacent outputs per thread, their
+// 5 input columns per row read as one scalar (column 2*ow0 - 1) and two float2s (columns
+// 2*ow0 .. 2*ow0 + 3): 9 loads for 2 outputs instead of 18; same taps, same order, same
+// rule as maxpool2d_kernel.
+__global__ __launch_bounds__(kBlock) void maxpool3s2_pair_kernel(
+    const float* __restrict__ x, float* __restrict__ y, uint32_t total2, uint32_t H, uint32_t W,
+    uint32_t OH, uint32_t OW, FastDiv dOW2, FastDiv dOH) {
+  typedef float f32x2v __attribute__((ext_vector_type(2)));
+  const uint32_t OW2 = OW / 2, stride = gridDim.x * blockDim.x;
+  for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < total2; i += stride) {
+    const uint32_t q1 = fdiv(i, dOW2), ow0 = 2 * (i - q1 * OW2);
+    const uint32_t nc = fdiv(q1, dOH), oh = q1 - nc * OH;
+    const float* __restrict__ xp = x + (size_t)nc * H * W;
+    const int h0 = 2 * (int)oh - 1, c0 = 2 * (int)ow0;   // window columns c0-1 .. c0+3
+    float v[3][5];
+    bool rok[3];
+#pragma unroll
+    for (int r = 0; r < 3; ++r) {
+      const int h = h0 + r;
+      rok[r] = h >= 0 && h < (int)H;
+      const float* row = xp + (size_t)min(max(h, 0), (int)H - 1) * W;
+      v[r][0] = row[max(c0 - 1, 0)];
+      const f32x2v a = *(const f32x2v*)(row + c0);
+      v[r][1] = a.x;
+      v[r][2] = a.y;
+      const int c2 = min(c0 + 2, (int)W - 2);          // W even: c0 + 2 <= W - 2 unless edge
+      const f32x2v b = *(const f32x2v*)(row + c2);
+      v[r][3] = b.x;
+      v[r][4] = b.y;
+    }
+    const bool left = c0 >= 1, right = c0 + 2 < (int)W;  // column c0-1 / c0+2 in the plane
+    float m0 = -__builtin_inff(), m1 = -__builtin_inff();
+#pragma unroll
+    for (int r = 0; r < 3; ++r) {
+      if (!rok[r]) continue;
+      // output ow0: columns c0-1, c0, c0+1 ; output ow0+1: columns c0+1, c0+2, c0+3
+      if (left && (v[r][0] > m0 || __builtin_isnan(v[r][0]))) m0 = v[r][0];
+      if (v[r][1] > m0 || __builtin_isnan(v[r][1])) m0 = v[r][1];
+      if (v[r][2] > m0 || __builtin_isnan(v[r][2])) m0 = v[r][2];
+      if (v[r][2] > m1 || __builtin_isnan(v[r][2])) m1 = v[r][2];
+      if (right && (v[r][3] > m1 || __builtin_isnan(v[r][3]))) m1 = v[r][3];
+      if (right && c0 + 3 < (int)W && (v[r][4] > m1 || __builtin_isnan(v[r][4]))) m1 = v[r][4];
+    }
+    *(f32x2v*)(y + (size_t)q1 * OW + ow0) = f32x2v{m0, m1};
+  }
+}
+
 template <int KT>   // KT > 0: the window size at compile time (every load issued at once)
 __global__ __launch_bounds__(kBlock) void maxpool2d_kernel(const float* __restrict__ x,
                                                            float* __restrict__ y, uint32_t total,
@@ -1152,6 +1199,15 @@ __global__ __launch_bounds__(kBlock) void maxpool2d_kernel(const float* __restri
   }
 }
 
+// A/B knob SSQ_POOL_PAIR=0: the one-output-per-thread pool for the stem's shape too
+static bool pair_pool() {
+  static const bool on = [] {
+    const char* e = getenv("SSQ_POOL_PAIR");
+    return !(e && *e && atoi(e) == 0);
+  }();
+  return on;
+}
+
 extern "C" int ssq_maxpool2d_fwd(const float* x, float* y, int64_t N, int64_t C, int64_t H,
                                  int64_t W, int64_t K, int64_t stride, int64_t pad,
                                  ssq_stream_t s) {
@@ -1164,6 +1220,15 @@ extern "C" int ssq_maxpool2d_fwd(const float* x, float* y, int64_t N, int64_t C,
   const int64_t total = N * C * OH * OW;
   SSQ_REQUIRE(total < (1ll << 31) && N * C * H * W < (1ll << 31), SSQ_E_ARG,
               "ssq_maxpool2d_fwd: tensor exceeds 2^31 elements");
+  const bool al8 = ((uintptr_t)x & 7u) == 0 && ((uintptr_t)y & 7u) == 0;
+  if (K == 3 && stride == 2 && pad == 1 && W % 2 == 0 && OW % 2 == 0 && al8 && pair_pool()) {
+    const int64_t total2 = total / 2;
+    hipLaunchKernelGGL(maxpool3s2_pair_kernel, dim3(grid_for(total2, kBlock, 8192)),
+                       dim3(kBlock), 0, (hipStream_t)s, x, y, (uint32_t)total2, (uint32_t)H,
+                       (uint32_t)W, (uint32_t)OH, (uint32_t)OW,
+                       make_fastdiv((uint32_t)(OW / 2)), make_fastdiv((uint32_t)OH));
+    return check_launch("ssq_maxpool2d_fwd");
+  }
   const dim3 grid(grid_for(total, kBlock, 8192));
 #define SSQ_MP(KT)                                                                         \
   hipLaunchKernelGGL(maxpool2d_kernel<KT>, grid, dim3(kBlock), 0, (hipStream_t)s, x, y,      \

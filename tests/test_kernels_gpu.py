@@ -830,7 +830,9 @@ def test_band_wgrad_two_waves_per_simd_bit_identical(K, cfg):
     # (N, C, H, W, k, stride, pad): the ResNet stem's pool at batch 8, odd planes, 2x2 / s2,
     # 3x3 / s1, 5x5 / s2 / p2, a 7x7 window over a 7x7 plane
     (8, 64, 112, 112, 3, 2, 1), (3, 5, 17, 13, 3, 2, 1), (2, 4, 8, 8, 2, 2, 0),
-    (2, 3, 9, 11, 3, 1, 1), (1, 6, 15, 15, 5, 2, 2), (2, 2, 7, 7, 7, 1, 3)])
+    (2, 3, 9, 11, 3, 1, 1), (1, 6, 15, 15, 5, 2, 2), (2, 2, 7, 7, 7, 1, 3),
+    # the two-outputs-per-thread 3x3 / s2 / p1 form (even W and OW): small and odd H
+    (2, 3, 6, 8, 3, 2, 1), (3, 2, 5, 4, 3, 2, 1)])
 def test_maxpool2d_matches_torch(K, cfg):
     """ssq_maxpool2d_fwd (SsqMaxPool2d, the stem's pool in QuantModel) == torch's
     F.max_pool2d bit for bit, NaN / inf / signed zeros / ties included; the module takes
