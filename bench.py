@@ -114,16 +114,27 @@ def make_workload(dev, rank, n_cali):
 PMC_FILE = "profiles/pmc_traffic.json"
 
 
+def _stamp(d):
+    """Provenance of a committed measurement summary against the tree this bench runs from:
+    the source hash it was measured at (shiftedscalequantization_amd.build.source_sha) and
+    stale = True when the kernels changed since, or when it carries no stamp."""
+    from shiftedscalequantization_amd.build import source_sha
+    prov = d.get("provenance") or {}
+    return {"measured_at_git": prov.get("git_sha"), "measured_at_csrc": prov.get("csrc_sha"),
+            "csrc_now": source_sha(), "stale": prov.get("csrc_sha") != source_sha()}
+
+
 def pmc_traffic(kernel="fq_fwd_pt"):
-    """HBM bytes per launch of `kernel` from the committed rocprofv3 PMC passes
-    (tools/pmc_session.sh: FETCH_SIZE and WRITE_SIZE in separate passes, read side
-    doubled per the gfx950 correction), or None if they were not collected."""
+    """(HBM bytes per launch of `kernel`, provenance) from the committed rocprofv3 PMC passes
+    (tools/pmc_session.sh: FETCH_SIZE and WRITE_SIZE in separate passes, read side doubled
+    per the gfx950 correction), or (None, None) if they were not collected."""
     path = os.path.join(os.path.dirname(os.path.abspath(__file__)), PMC_FILE)
     try:
         with open(path) as f:
-            return float(json.load(f)[kernel]["hbm_bytes_per_launch"])
+            d = json.load(f)
+        return float(d[kernel]["hbm_bytes_per_launch"]), _stamp(d)
     except (OSError, KeyError, ValueError):
-        return None
+        return None, None
 
 
 RECON_ROOFLINE_FILE = "profiles/recon_roofline.json"
@@ -139,8 +150,9 @@ def recon_roofline():
             d = json.load(f)
     except (OSError, ValueError):
         return None
-    out = {k: v for k, v in d.items() if k != "blocks"}
-    out["source_file"] = RECON_ROOFLINE_FILE
+    out = {k: v for k, v in d.items() if k not in ("blocks", "provenance")}
+    out["source_file"] = RECON_ROOFLINE_FILE + " (a committed trace, not this run)"
+    out.update(_stamp(d))
     out["per_block_gbs"] = {b: v["achieved_gbs"] for b, v in d.get("blocks", {}).items()}
     return out
 
@@ -218,30 +230,34 @@ def cpu_baseline(act_dev, d_a, z_a, seconds, recon_state=None):
 
     nN, elN = _timed(all_cores, seconds / 3)
     pool.shutdown()
-    out = {"value": round(nN * sample.size / elN / 1e9, 4), "unit": "Gelem/s", "cores": cores,
-           "kind": "port",
-           "sample": f"q/dq: oracle/c ssqo_fake_quant (scalar C port of quant_layer.py:92-98), "
-                     f"A4 per-tensor q/dq of act[:64] ({sample.size} elems) x{nN} reps in "
-                     f"{elN:.1f}s on {cores} threads; {os.cpu_count()} host CPUs visible",
-           "qdq_1thread_gelem_s": round(n1 * sample.size / el1 / 1e9, 4),
-           "cpu_model": cpu_model()}
-    # the reference's own CPU path: its eager torch op sequence (oracle/torch_eager.py) on
-    # the same sample, all cores and one thread
+    c_port = {"value": round(nN * sample.size / elN / 1e9, 4), "unit": "Gelem/s", "cores": cores,
+              "kind": "port", "value_1thread": round(n1 * sample.size / el1 / 1e9, 4),
+              "sample": f"oracle/c ssqo_fake_quant (scalar C port of quant_layer.py:92-98), "
+                        f"act[:64] ({sample.size} elems) x{nN} reps in {elN:.1f}s on {cores} "
+                        f"threads"}
+    # the reference's own CPU path -- the headline baseline: its eager torch op sequence
+    # (oracle/torch_eager.py, quant_layer.py:18-22,92-98) on the same sample, all cores and
+    # one thread
     import torch
     from oracle.torch_eager import uaq_fake_quant
     xs, dt, zt = torch.from_numpy(sample), torch.from_numpy(d), torch.from_numpy(z)
     prev = torch.get_num_threads()
-    eager = {}
+    eager, eager_n = {}, {}
     for nt in (cores, 1):
         torch.set_num_threads(nt)
         ne, ele = _timed(lambda: uaq_fake_quant(xs, dt, zt, 4), seconds / 6)
         eager[nt] = round(ne * sample.size / ele / 1e9, 4)
+        eager_n[nt] = (ne, ele)
     torch.set_num_threads(prev)
-    out["reference_eager_torch"] = {
-        "value": eager[cores], "unit": "Gelem/s", "cores": cores, "value_1thread": eager[1],
-        "kind": "reference op sequence",
-        "sample": "quant_layer.py:92-98 as torch-CPU eager ops (round(x/delta)+zp, clamp, "
-                  "(q-zp)*delta) on the same act[:64] sample"}
+    out = {"value": eager[cores], "unit": "Gelem/s", "cores": cores,
+           # a restatement (the reference's source cannot travel to the GPU box), op for op
+           "kind": "port",
+           "sample": f"the reference's UniformAffineQuantizer.forward op sequence "
+                     f"(quant_layer.py:18-22,92-98: x/delta, round_ste, +zp, clamp, -zp, *delta) "
+                     f"as torch-CPU eager ops on act[:64] ({sample.size} elems, A4 per-tensor), "
+                     f"x{eager_n[cores][0]} reps in {eager_n[cores][1]:.1f}s on {cores} torch "
+                     f"threads; {os.cpu_count()} host CPUs visible",
+           "value_1thread": eager[1], "cpu_model": cpu_model(), "c_port": c_port}
     if recon_state is not None:
         import torch
         from oracle.recon_cpu import FusedBlockReconCPU
@@ -296,8 +312,8 @@ def main():
     ms_step_k = graph_time_ms(step, reps=20, rounds=9)
     ms_fq = time_events(lambda: K.fake_quant_fwd(act, d_a, z_a, 4, out=y_act), 20, dev, rounds=9)
     # the committed PMC passes were collected on the default workload (1024 samples)
-    traffic = pmc_traffic("fq_fwd_pt_ride") if args.n_cali == 1024 else None
-    traffic_k1 = pmc_traffic("fq_fwd_pt") if args.n_cali == 1024 else None
+    traffic, traffic_prov = pmc_traffic("fq_fwd_pt_ride") if args.n_cali == 1024 else (None, None)
+    traffic_k1, _ = pmc_traffic("fq_fwd_pt") if args.n_cali == 1024 else (None, None)
     alg_bytes = 8.0 * (n_act + n_w)
     achieved = alg_bytes / (ms_step_k * 1e-3) / 1e9
     achieved_k1 = 8.0 * n_act / (ms_fq * 1e-3) / 1e9
@@ -380,7 +396,9 @@ def main():
                                "ssq_fq_fwd_multi tiles riding on the launch: the whole step)",
                      "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
-                     "traffic_source": PMC_FILE if traffic is not None else None,
+                     "traffic_source": (PMC_FILE + " (committed PMC passes, not this run)")
+                                       if traffic is not None else None,
+                     "traffic_provenance": traffic_prov,
                      "kernel_ms": round(ms_step_k, 4), "alg_bytes_per_launch": int(alg_bytes),
                      "k1_alone": {"kernel": "fq_fwd_pt (A4 activation only)",
                                   "kernel_ms": round(ms_fq, 4),

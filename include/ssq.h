@@ -47,13 +47,21 @@ int ssq_version(void);
 int ssq_set_variant(int variant);
 
 /* ---------------------------------------------------------------- K1/K2 uniform affine q/dq
- * UniformAffineQuantizer.forward (quant_layer.py:77-98), ChannelQuant opt_mode 'none'
- * (channelQuant.py:79-94) and ChannelQuantAct 'none' (channelQuantAct.py:56-67):
- *   d = delta[c]*scale; q = clamp(rint(x/d) + zp[c], qmin, qmax); y = (q - zp[c]) * d
- * Element i belongs to channel c = (i / inner) % nch   (nch == 1: per-tensor).     */
+ * UniformAffineQuantizer.forward (quant_layer.py:77-98), with round_ste (:18-22):
+ *   d = delta[c]*scale; t = x/d; q = clamp((rint(t) - t) + t + zp[c], qmin, qmax);
+ *   y = (q - zp[c]) * d
+ * (rint(t) - t) + t == rint(t) for finite t and NaN at t = +-inf, as the reference's
+ * round_ste; clamp keeps NaN (torch.clamp).  Element i belongs to channel
+ * c = (i / inner) % nch   (nch == 1: per-tensor).                                     */
 int ssq_fq_fwd(const float* x, float* y, void* codes_or_null, const float* delta,
                const float* zp, int64_t n, int64_t inner, int64_t nch, float scale,
                int qmin, int qmax, ssq_stream_t stream);
+/* The same q/dq with plain torch.round (t = +-inf clamps to an edge): ChannelQuant
+ * opt_mode 'none' (channelQuant.py:79-94), ChannelQuantAct 'none'
+ * (channelQuantAct.py:56-67), AdaRound 'nearest' (adaptive_rounding.py:40-41).       */
+int ssq_fq_round_fwd(const float* x, float* y, void* codes_or_null, const float* delta,
+                     const float* zp, int64_t n, int64_t inner, int64_t nch, float scale,
+                     int qmin, int qmax, ssq_stream_t stream);
 
 /* Several tensors in ONE launch (e.g. every conv weight of a network): segment s is
  * the tensor x[s] (n[s] elements, inner[s] per channel, nch[s] channels). Per-channel
@@ -70,8 +78,9 @@ int ssq_fq_fwd_multi(int nseg, const float* const* x, float* const* y,
  * launch (bench.py's step).  Same code: bit-identical outputs.  One table is queued at a
  * time (a second call launches the first); ssq_flush_fq_multi launches a table still queued
  * on `stream`.  The caller must not read the queued outputs before that launch or flush.
- * Host state, not thread-safe; ssq_set_deferred_fq_multi returns the previous setting and
- * launches nothing (flush before turning it off). */
+ * Host state, not thread-safe; ssq_set_deferred_fq_multi returns the previous setting;
+ * turning it off launches a table still queued (on its own stream), and only a table queued
+ * under deferral rides on a per-tensor launch. */
 int ssq_set_deferred_fq_multi(int on);
 int ssq_flush_fq_multi(ssq_stream_t stream);
 
@@ -409,8 +418,8 @@ int ssq_flush_finalize(ssq_stream_t stream);
  * the gather launch (same code: bit-identical What).  One table is queued at a time (a second
  * call launches the first); ssq_flush_prep_fwd launches a table still queued on `stream`.
  * The caller must not read the queued What before that gather or flush.  Host state, not
- * thread-safe; ssq_set_deferred_prep_fwd returns the previous setting and launches nothing
- * (flush before turning it off).  Replaces nothing in the reference: the iteration start of
+ * thread-safe; ssq_set_deferred_prep_fwd returns the previous setting; turning it off
+ * launches a forward still queued (on its own stream).  Replaces nothing in the reference: the iteration start of
  * layer_recon_fused_shiftedScale.py:94-100 (batch draw, then the quantized forward). */
 int ssq_set_deferred_prep_fwd(int on);
 int ssq_flush_prep_fwd(ssq_stream_t stream);

@@ -23,10 +23,11 @@ void ssqo_fake_quant(const float* x, float* y, uint8_t* codes, const float* delt
   for (int64_t i = 0; i < n; ++i) {
     const int64_t c = nch == 1 ? 0 : (i / inner) % nch;
     const float d = delta[c] * scale, z = zp[c];
-    float q = rintf(x[i] / d) + z;
-    q = q < lo ? lo : (q > hi ? hi : q);
+    const float t = x[i] / d;
+    float q = ((rintf(t) - t) + t) + z;  /* round_ste: round(t), NaN at t = +-inf */
+    q = q < lo ? lo : (q > hi ? hi : q); /* torch.clamp: NaN stays NaN */
     y[i] = (q - z) * d;
-    if (codes) codes[i] = (uint8_t)((int)q & 0xff);
+    if (codes) codes[i] = q == q ? (uint8_t)((int)q & 0xff) : 0;
   }
 }
 

@@ -38,14 +38,26 @@ def qrange(n_bits, sym):
 
 
 # ----------------------------------------------------------------- K1 / K2  (quant_layer.py:77-98)
-def fake_quant(x, delta, zp, n_bits, sym=False):
+def round_ste_fwd(t):
+    """round_ste's forward value (quant_layer.py:18-22): (round(t) - t) + t in fp32 --
+    round(t) for every finite t, NaN at t = +-inf."""
+    t = _f(t)
+    with np.errstate(invalid="ignore"):
+        return ((np.rint(t) - t) + t).astype(F32)
+
+
+def fake_quant(x, delta, zp, n_bits, sym=False, ste=True):
     """UniformAffineQuantizer.forward (quant_layer.py:92-98). delta/zp broadcast against x.
-    Returns (dequantized fp32, integer codes as int32)."""
+    ste=False: plain torch.round (ChannelQuant / ChannelQuantAct 'none').  np.clip keeps
+    NaN, as torch.clamp.  Returns (dequantized fp32, integer codes as int32)."""
     x, delta, zp = _f(x), _f(delta), _f(zp)
     lo, hi = qrange(n_bits, sym)
-    x_int = np.rint(x / delta) + zp                 # round_ste fwd == round (SURVEY §8 a1)
-    xq = np.clip(x_int, F32(lo), F32(hi))
-    return ((xq - zp) * delta).astype(F32), xq.astype(np.int32)
+    with np.errstate(invalid="ignore", over="ignore", divide="ignore"):
+        t = x / delta
+        x_int = (round_ste_fwd(t) if ste else np.rint(t)) + zp
+        xq = np.clip(x_int, F32(lo), F32(hi))
+        codes = np.where(np.isnan(xq), F32(0), xq).astype(np.int32)
+        return ((xq - zp) * delta).astype(F32), codes
 
 
 def fake_quant_bwd(x, delta, zp, n_bits, sym, gy):
@@ -54,7 +66,7 @@ def fake_quant_bwd(x, delta, zp, n_bits, sym, gy):
     x, delta, zp, gy = _f(x), _f(delta), _f(zp), _f(gy)
     lo, hi = qrange(n_bits, sym)
     t = x / delta
-    x_int = np.rint(t) + zp
+    x_int = round_ste_fwd(t) + zp
     m = (x_int >= lo) & (x_int <= hi)
     xq = np.clip(x_int, F32(lo), F32(hi))
     g_q = gy * delta                                  # mul backward (wrt x_quant - zp)

@@ -25,6 +25,7 @@ SIGNATURES = {
     "ssq_version": (_i, []),
     "ssq_set_variant": (_i, [_i]),
     "ssq_fq_fwd": (_i, [_p, _p, _p, _p, _p, _i64, _i64, _i64, _f, _i, _i, _p]),
+    "ssq_fq_round_fwd": (_i, [_p, _p, _p, _p, _p, _i64, _i64, _i64, _f, _i, _i, _p]),
     "ssq_fq_fwd_multi": (_i, [_i, _p, _p, _p, _p, _p, _p, _p, _p, _p, _p]),
     "ssq_fq_bwd_workspace_size": (_sz, [_i64, _i64, _i64]),
     "ssq_fq_bwd": (_i, [_p, _p, _p, _p, _i64, _i64, _i64, _i, _i, _p, _p, _p, _p, _sz, _p]),

@@ -25,6 +25,31 @@ CFLAGS = ["-O3", f"--offload-arch={ARCH}", "-fPIC", "-std=c++17", "-ffp-contract
           "-fhip-fp32-correctly-rounded-divide-sqrt", "-Wall", "-Wno-unused-function"]
 
 
+def source_sha():
+    """sha256 (16 hex) of every source the library is built from (SOURCES + HEADERS, in
+    that order): the provenance stamp of committed measurements (profiles/*.json), which
+    bench.py compares against the tree it runs from (the GPU box has no .git)."""
+    import hashlib
+    h = hashlib.sha256()
+    for name in SOURCES + HEADERS:
+        with open(os.path.join(CSRC, name), "rb") as f:
+            h.update(name.encode() + b"\0" + f.read())
+    return h.hexdigest()[:16]
+
+
+def provenance():
+    """{"csrc_sha": source_sha(), "git_sha": $SSQ_GIT_SHA or `git rev-parse HEAD` when a
+    repository is present, else None}: stamped into measurement summaries."""
+    sha = os.environ.get("SSQ_GIT_SHA")
+    if not sha:
+        try:
+            sha = subprocess.run(["git", "rev-parse", "--short=12", "HEAD"], cwd=HERE,
+                                 capture_output=True, text=True, timeout=10).stdout.strip() or None
+        except (OSError, subprocess.SubprocessError):
+            sha = None
+    return {"csrc_sha": source_sha(), "git_sha": sha}
+
+
 def _hipcc():
     for c in (os.environ.get("HIPCC"), shutil.which("hipcc"), "/opt/rocm/bin/hipcc"):
         if c and os.path.exists(c):

@@ -103,9 +103,42 @@ static ColTiling col_tiling_prep(const Geo& g) {
 // depends only on the weight's own shape, so a multi-segment launch gives each weight its
 // single-launch bits.
 constexpr uint32_t kWR = 16;   // rows per wave (whole form: Co <= 4 * kWR = 64)
+// Form 2 (r4): the thread-column stage 1 with the chunk reduction in the same launch -- the
+// last workgroup of each column block to finish (one ticket counter per column block, write-
+// through partials: arrive_last) reduces that block's chunks in the fixed order of the stage-2
+// launch (one wave per input channel: lane c takes chunk c, then the fixed shuffle tree) and
+// finalises the block's channels.  Row chunks are sized so a weight takes ~kK6pWgs
+// workgroups (one resident round: each workgroup pays the ticket round trip once, in
+// parallel) and at most one wave-width of chunks.  SSQ_K6P_FORM selects the form for A/B
+// (0: stage 1 + stage 2, 1: wave-column for Co <= 64 else form 0, 2: one launch).
+constexpr uint32_t kMaxTicketBlk = 256;          // column blocks per segment (form 2)
+constexpr uint32_t kOneStage = 4096;             // form 2: partial doubles staged in LDS (32 KiB)
+__device__ unsigned g_k6p_tickets[kMaxPrepSeg * kMaxTicketBlk];
+
+static ColTiling bwd_tiling_onelaunch(const Geo& g) {
+  static const uint32_t kWgs = prep_env("SSQ_K6P_WGS", 256);
+  static const uint32_t kRows = prep_env("SSQ_K6P_ROWS", 4);
+  ColTiling t = col_tiling_prep(g);
+  uint32_t want = (kWgs + t.ncolblk - 1) / t.ncolblk;
+  const uint32_t by_rows = (g.Co + kRows - 1) / kRows;
+  const uint32_t by_lds = kOneStage / (t.ncb * kMaxPrepS);   // a block's partials fit the stage
+  if (want > by_rows) want = by_rows;
+  if (want > by_lds) want = by_lds;
+  if (want < 1) want = 1;
+  t.R = (g.Co + want - 1) / want;
+  t.nchunk = (g.Co + t.R - 1) / t.R;
+  t.form = 2;
+  return t;
+}
+
 static ColTiling bwd_tiling_prep(const Geo& g) {
+  static const uint32_t kForm = prep_env("SSQ_K6P_FORM", 1);
   constexpr uint32_t kMaxR = (kBlock / kWave) * kWR;
-  if (g.K > (uint32_t)kWave || g.Co > kMaxR) return col_tiling_prep(g);
+  if (kForm == 2) {
+    const ColTiling t = bwd_tiling_onelaunch(g);
+    if (t.ncolblk <= kMaxTicketBlk) return t;
+  }
+  if (kForm == 0 || g.K > (uint32_t)kWave || g.Co > kMaxR) return col_tiling_prep(g);
   ColTiling t;
   t.form = 1;
   t.threads = kBlock;
@@ -134,6 +167,7 @@ struct PrepSeg {
   uint32_t blk0;     // first workgroup of this segment (forward / stage 1)
   uint32_t wave0;    // first wave of this segment (stage 2: one wave per input channel)
   uint32_t stage2;   // its chunks are reduced by the stage-2 launch
+  uint32_t ticket0;  // form 2: its column blocks' ticket counters start here
   float lo, hi;
   float* alpha_w;    // fused optimizer step (ssq_adam_arm): alpha, its Adam m / v (or null)
   float* am;
@@ -414,6 +448,53 @@ __device__ __forceinline__ void alpha_bwd_wavecol(const PrepSeg& sg, const AdamC
   if (fin_lane) alpha_finalize<NS>(sg, ac, ci0 + lane, af, tot, reg_lambda, reg_b);
 }
 
+// Form 2's in-launch stage 2 (run by the last arriving workgroup of a column block): the
+// block's chunk partials -- one contiguous run, part[(ci*nchunk + chunk)*S + i] -- are staged
+// in LDS by one coalesced pass (write-through loads), thread (ci, i) adds its nchunk values in
+// chunk order, and thread ci finalises the channel (regulariser, softmax / clamp backward,
+// the armed Adam step).  One global round trip, then LDS.
+template <int NS>
+__device__ __forceinline__ void alpha_reduce_chunks(const PrepSeg& sg, const AdamConst& ac,
+                                                    uint32_t ci0, uint32_t nci, double* stage,
+                                                    double* red, float reg_lambda, float reg_b,
+                                                    const float* __restrict__ reg_dev) {
+  const uint32_t nchunk = sg.tl.nchunk;
+  const uint32_t n = nci * nchunk * NS;
+  const double* src = sg.part + (size_t)ci0 * nchunk * NS;
+  constexpr uint32_t kPer = (kOneStage + kBlock - 1) / kBlock;
+  double v[kPer];
+#pragma unroll
+  for (uint32_t r = 0; r < kPer; ++r) {
+    const uint32_t k = threadIdx.x + r * kBlock;
+    v[r] = k < n ? ld_sc1(src + k) : 0.0;
+  }
+#pragma unroll
+  for (uint32_t r = 0; r < kPer; ++r) {
+    const uint32_t k = threadIdx.x + r * kBlock;
+    if (k < n) stage[k] = v[r];
+  }
+  __syncthreads();
+  for (uint32_t pr = threadIdx.x; pr < nci * NS; pr += kBlock) {
+    const uint32_t c = pr / NS, i = pr - c * NS;
+    double sum = 0.0;
+    for (uint32_t k = 0; k < nchunk; ++k) sum += stage[(c * nchunk + k) * NS + i];
+    red[pr] = sum;
+  }
+  __syncthreads();
+  if (reg_dev) {
+    reg_lambda = reg_dev[0];
+    reg_b = reg_dev[1];
+  }
+  for (uint32_t c = threadIdx.x; c < nci; c += kBlock) {
+    float a[kMaxS];
+    load_row(sg.alpha, ci0 + c, NS, a);
+    double tot[kMaxS];
+#pragma unroll
+    for (int i = 0; i < NS; ++i) tot[i] = red[c * NS + i];
+    alpha_finalize<NS>(sg, ac, ci0 + c, a, tot, reg_lambda, reg_b);
+  }
+}
+
 // Backward, one launch for every segment: wave-column segments finish here; the
 // thread-column stage 1 of the others writes sums of g_int * F_i per (chunk, ci) into
 // part[(ci*nchunk + chunk)*S + i] (input-channel-major: stage 2 reads one coalesced run).
@@ -497,14 +578,22 @@ __global__ __launch_bounds__(kBlock) void alpha_bwd_prep(PrepTable tab, float re
 #pragma unroll
   for (int i = 0; i < NS; ++i) red[t * NS + i] = acc[i];
   __syncthreads();
+  const bool onel = sg.tl.form == 2;
   if (t < nci) {
 #pragma unroll
     for (int i = 0; i < NS; ++i) {
       double sum = 0.0;
       for (uint32_t k = 0; k < g.K; ++k) sum += red[(t * g.K + k) * NS + i];
-      sg.part[((size_t)(ci0 + t) * sg.tl.nchunk + by) * NS + i] = sum;
+      double* dst = sg.part + ((size_t)(ci0 + t) * sg.tl.nchunk + by) * NS + i;
+      if (onel) st_sc1(dst, sum);      // write-through: read back by the last arriver
+      else *dst = sum;
     }
   }
+  if (!onel) return;
+  // form 2: the last workgroup of this column block reduces its chunks and finalises
+  if (!arrive_last(&g_k6p_tickets[sg.ticket0 + bx], sg.tl.nchunk, (int*)red)) return;
+  extern __shared__ double stage[];
+  alpha_reduce_chunks<NS>(sg, tab.ac, ci0, nci, stage, red, reg_lambda, reg_b, reg_dev);
 }
 
 // Stage 2 (thread-column segments): one wave per (segment, input channel).  Every load the wave needs (alpha row, the device (lambda, b)
@@ -617,6 +706,7 @@ static int make_seg(const SegArgs& a, int i, PrepSeg& sg, const char* what) {
   sg.galpha = nullptr;
   sg.reg_vals = nullptr;
   sg.alpha_w = sg.am = sg.av = nullptr;
+  sg.ticket0 = 0;
   sg.tl = col_tiling_prep(sg.g);
   sg.lo = (float)a.qmin[i];
   sg.hi = (float)a.qmax[i];
@@ -664,7 +754,7 @@ static int flush_fwd(hipStream_t s) {
 }
 
 int launch_gather(hipStream_t s, const GatherArgs& a, bool vec) {
-  if (!(g_fwd_pend.on && g_fwd_pend.s == s)) {
+  if (!(g_fwd_defer && g_fwd_pend.on && g_fwd_pend.s == s)) {
     const dim3 grid(a.gx, a.nrows);
     if (vec)
       hipLaunchKernelGGL(gather2_kernel<true>, grid, dim3(kBlock), 0, s, a);
@@ -771,6 +861,8 @@ extern "C" int ssq_adashift_fwd_prepared_multi(int nseg, const uint32_t* const* 
 extern "C" int ssq_set_deferred_prep_fwd(int on) {
   const int prev = g_fwd_defer ? 1 : 0;
   g_fwd_defer = on != 0;
+  // switching off: a forward still queued (on whichever stream) launches now, on its stream
+  if (!g_fwd_defer && g_fwd_pend.on) (void)flush_fwd(g_fwd_pend.s);
   return prev;
 }
 
@@ -824,10 +916,15 @@ extern "C" int ssq_adashift_bwd_prepared_multi(
       sg.blk0 = blk;
       blk += sg.tl.ncolblk * sg.tl.nchunk;
       sg.stage2 = sg.tl.form == 0;
+      sg.ticket0 = (uint32_t)k * kMaxTicketBlk;
       sg.wave0 = waves;
       if (sg.stage2) waves += sg.g.Ci;
     }
     const unsigned blocks2 = (waves + kBlock / kWave - 1) / (kBlock / kWave);
+    // form 2 segments stage a column block's partials in dynamic LDS
+    size_t shm = 0;
+    for (int k = 0; k < tab.nseg; ++k)
+      if (tab.s[k].tl.form == 2) shm = kOneStage * sizeof(double);
     // queued finalize tasks of this stream ride on the first launch (their inputs live in
     // their producers' own workspace slots, not in this one)
     FinTable fin{};
@@ -847,7 +944,7 @@ extern "C" int ssq_adashift_bwd_prepared_multi(
     }
 #define SSQ_BWDP(NS)                                                                          \
   do {                                                                                        \
-    hipLaunchKernelGGL((alpha_bwd_prep<NS>), dim3(blk + fin.nwg), dim3(kBlock), 0, s, tab,    \
+    hipLaunchKernelGGL((alpha_bwd_prep<NS>), dim3(blk + fin.nwg), dim3(kBlock), shm, s, tab,  \
                        reg_lambda, reg_b, reg_dev, fin, blk);                                 \
     if (blocks2)                                                                              \
       hipLaunchKernelGGL((alpha_bwd_prep_stage2<NS>), dim3(blocks2), dim3(kBlock), 0, s, tab, \

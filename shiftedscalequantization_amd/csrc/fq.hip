@@ -53,15 +53,15 @@ __device__ __forceinline__ void stream_range(int64_t n4, int64_t chunk, int64_t&
   }
 }
 
-template <bool CODES, bool NTS, bool FAST = false>
+template <bool CODES, bool NTS, bool STE, bool FAST = false>
 __device__ __forceinline__ void fq_store4(f32x4 v, const QParams& p, f32x4* __restrict__ y,
                                           uint32_t* __restrict__ codes, int64_t k, float r = 0.0f) {
   f32x4 o;
   float q0, q1, q2, q3;
-  o.x = fq1<FAST>(v.x, p, &q0, r);
-  o.y = fq1<FAST>(v.y, p, &q1, r);
-  o.z = fq1<FAST>(v.z, p, &q2, r);
-  o.w = fq1<FAST>(v.w, p, &q3, r);
+  o.x = fq1<FAST, STE>(v.x, p, &q0, r);
+  o.y = fq1<FAST, STE>(v.y, p, &q1, r);
+  o.z = fq1<FAST, STE>(v.z, p, &q2, r);
+  o.w = fq1<FAST, STE>(v.w, p, &q3, r);
   st4<NTS>(o, &y[k]);
   if (CODES) codes[k] = pack4(q0, q1, q2, q3);
 }
@@ -73,13 +73,13 @@ __device__ __forceinline__ void fq_store4(f32x4 v, const QParams& p, f32x4* __re
 // fastdiv: x/delta in the reciprocal form (div_fast, bit-identical) when every element
 // of the wave's step is in its range -- one wave-uniform branch per step; otherwise (and
 // for an out-of-range delta) the IEEE divide.
-template <bool CODES, int UNROLL, bool NTL, bool NTS>
-__device__ __forceinline__ void fq_fwd_pt_body(const f32x4* __restrict__ x, f32x4* __restrict__ y,
-                                               uint32_t* __restrict__ codes,
-                                               const float* __restrict__ delta,
-                                               const float* __restrict__ zp, int64_t n4,
-                                               float scale, float lo, float hi, int64_t chunk,
-                                               int fastdiv, uint32_t bid, uint32_t nblk) {
+template <bool CODES, int UNROLL, bool NTL, bool NTS, bool STE>
+__device__ __forceinline__ void fq_fwd_pt_steps(const f32x4* __restrict__ x, f32x4* __restrict__ y,
+                                                uint32_t* __restrict__ codes,
+                                                const float* __restrict__ delta,
+                                                const float* __restrict__ zp, int64_t n4,
+                                                float scale, float lo, float hi, int64_t chunk,
+                                                int fastdiv, uint32_t bid, uint32_t nblk) {
   QParams p;
   p.d = __fmul_rn(delta[0], scale);
   p.z = zp[0];
@@ -101,13 +101,29 @@ __device__ __forceinline__ void fq_fwd_pt_body(const f32x4* __restrict__ x, f32x
     if (__all(ok)) {
 #pragma unroll
       for (int u = 0; u < UNROLL; ++u)
-        fq_store4<CODES, NTS, true>(v[u], p, y, codes, i + u * stride, r);
+        fq_store4<CODES, NTS, STE, true>(v[u], p, y, codes, i + u * stride, r);
     } else {
 #pragma unroll
-      for (int u = 0; u < UNROLL; ++u) fq_store4<CODES, NTS>(v[u], p, y, codes, i + u * stride);
+      for (int u = 0; u < UNROLL; ++u) fq_store4<CODES, NTS, STE>(v[u], p, y, codes, i + u * stride);
     }
   }
-  for (; i < end; i += stride) fq_store4<CODES, false>(x[i], p, y, codes, i);
+  for (; i < end; i += stride) fq_store4<CODES, false, STE>(x[i], p, y, codes, i);
+}
+
+// round_ste (every UniformAffineQuantizer) or torch.round: one branch per launch
+template <bool CODES, int UNROLL, bool NTL, bool NTS>
+__device__ __forceinline__ void fq_fwd_pt_body(const f32x4* __restrict__ x, f32x4* __restrict__ y,
+                                               uint32_t* __restrict__ codes,
+                                               const float* __restrict__ delta,
+                                               const float* __restrict__ zp, int64_t n4,
+                                               float scale, float lo, float hi, int64_t chunk,
+                                               int fastdiv, int ste, uint32_t bid, uint32_t nblk) {
+  if (ste)
+    fq_fwd_pt_steps<CODES, UNROLL, NTL, NTS, true>(x, y, codes, delta, zp, n4, scale, lo, hi,
+                                                   chunk, fastdiv, bid, nblk);
+  else
+    fq_fwd_pt_steps<CODES, UNROLL, NTL, NTS, false>(x, y, codes, delta, zp, n4, scale, lo, hi,
+                                                    chunk, fastdiv, bid, nblk);
 }
 
 template <bool CODES, int UNROLL, bool NTL, bool NTS>
@@ -117,9 +133,9 @@ __global__ __launch_bounds__(1024) void fq_fwd_pt(const f32x4* __restrict__ x,
                                                   const float* __restrict__ delta,
                                                   const float* __restrict__ zp, int64_t n4,
                                                   float scale, float lo, float hi,
-                                                  int64_t chunk, int fastdiv) {
+                                                  int64_t chunk, int fastdiv, int ste) {
   fq_fwd_pt_body<CODES, UNROLL, NTL, NTS>(x, y, codes, delta, zp, n4, scale, lo, hi, chunk,
-                                          fastdiv, blockIdx.x, gridDim.x);
+                                          fastdiv, ste, blockIdx.x, gridDim.x);
 }
 
 // General scalar path: any alignment, per-channel c = (i / inner) % nch.
@@ -130,7 +146,7 @@ __global__ __launch_bounds__(kBlock) void fq_fwd_scalar(const float* __restrict_
                                                         const float* __restrict__ zp,
                                                         int64_t n, int64_t start, int64_t inner,
                                                         int64_t nch, float scale, float lo,
-                                                        float hi) {
+                                                        float hi, int ste) {
   const int64_t stride = (int64_t)gridDim.x * blockDim.x;
   for (int64_t i = start + (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
     int64_t c = nch == 1 ? 0 : (i / inner) % nch;
@@ -140,7 +156,7 @@ __global__ __launch_bounds__(kBlock) void fq_fwd_scalar(const float* __restrict_
     p.lo = lo;
     p.hi = hi;
     float q;
-    y[i] = fq1(x[i], p, &q);
+    y[i] = ste ? fq1<false, true>(x[i], p, &q) : fq1<false, false>(x[i], p, &q);
     if (codes) codes[i] = (uint8_t)((int)q & 0xff);
   }
 }
@@ -154,7 +170,7 @@ __global__ __launch_bounds__(kBlock) void fq_fwd_pc(const f32x4* __restrict__ x,
                                                     const float* __restrict__ delta,
                                                     const float* __restrict__ zp,
                                                     int64_t n4, uint32_t inner, uint32_t nch,
-                                                    float scale, float lo, float hi) {
+                                                    float scale, float lo, float hi, int ste) {
   const int64_t stride = (int64_t)gridDim.x * blockDim.x;
   for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n4; i += stride) {
     f32x4 v = x[i], o;
@@ -174,7 +190,7 @@ __global__ __launch_bounds__(kBlock) void fq_fwd_pc(const f32x4* __restrict__ x,
       p.z = zp[cc];
       p.lo = lo;
       p.hi = hi;
-      out[j] = fq1(in[j], p, &q[j]);
+      out[j] = ste ? fq1<false, true>(in[j], p, &q[j]) : fq1<false, false>(in[j], p, &q[j]);
     }
     o.x = out[0];
     o.y = out[1];
@@ -204,6 +220,7 @@ constexpr int kTile = 4096;      // elements per workgroup: 4 float4 per thread 
 struct SegTable {
   Seg s[kMaxSeg];
   int nseg;
+  int ste;         // round_ste (1, every UniformAffineQuantizer table) or torch.round (0)
 };
 
 // One workgroup = one tile of one segment.  The (delta, zp) of every channel the tile
@@ -217,8 +234,8 @@ inline uint32_t tile_channels(uint32_t tile, uint32_t min_inner) {
   const uint32_t c = tile / min_inner + 2;
   return c < tile ? c : tile;
 }
-template <int U>
-__device__ __forceinline__ void fq_fwd_multi_body(const SegTable& tab, uint32_t cap, uint32_t bid) {
+template <int U, bool STE>
+__device__ __forceinline__ void fq_fwd_multi_tile(const SegTable& tab, uint32_t cap, uint32_t bid) {
   constexpr uint32_t TILE = U * 4 * kBlock;
   extern __shared__ float stage[];
   float* sd = stage;
@@ -261,7 +278,7 @@ __device__ __forceinline__ void fq_fwd_multi_body(const SegTable& tab, uint32_t 
           next += sg.inner;
         }
         QParams p{sd[c - c0], sz[c - c0], lo, hi};
-        o[j] = fq1(a[j], p, &q[j]);
+        o[j] = fq1<false, STE>(a[j], p, &q[j]);
       }
       f32x4 r;
       r.x = o[0];
@@ -277,9 +294,17 @@ __device__ __forceinline__ void fq_fwd_multi_body(const SegTable& tab, uint32_t 
     const uint32_t cl = fdiv(e, sg.div_inner) - c0;
     QParams p{sd[cl], sz[cl], lo, hi};
     float q;
-    sg.y[e] = fq1(sg.x[e], p, &q);
+    sg.y[e] = fq1<false, STE>(sg.x[e], p, &q);
     if (sg.codes) sg.codes[e] = (uint8_t)((int)q & 0xff);
   }
+}
+
+template <int U>
+__device__ __forceinline__ void fq_fwd_multi_body(const SegTable& tab, uint32_t cap, uint32_t bid) {
+  if (tab.ste)
+    fq_fwd_multi_tile<U, true>(tab, cap, bid);
+  else
+    fq_fwd_multi_tile<U, false>(tab, cap, bid);
 }
 
 template <int U>
@@ -298,7 +323,7 @@ struct PtArgs {
   const float* zp;
   int64_t n4;
   float scale, lo, hi;
-  int fastdiv;
+  int fastdiv, ste;
   uint32_t npt;
 };
 static_assert(sizeof(PtArgs) + sizeof(SegTable) + 16 <= 4096, "kernel arguments over 4 KiB");
@@ -306,7 +331,7 @@ template <int UNROLL, bool NTL, bool NTS>
 __global__ __launch_bounds__(kBlock) void fq_fwd_pt_ride(PtArgs a, SegTable tab, uint32_t cap) {
   if (blockIdx.x < a.npt) {
     fq_fwd_pt_body<false, UNROLL, NTL, NTS>(a.x, a.y, nullptr, a.delta, a.zp, a.n4, a.scale,
-                                            a.lo, a.hi, 0, a.fastdiv, blockIdx.x, a.npt);
+                                            a.lo, a.hi, 0, a.fastdiv, a.ste, blockIdx.x, a.npt);
     return;
   }
   fq_fwd_multi_body<kTile / 4 / kBlock>(tab, cap, blockIdx.x - a.npt);
@@ -586,18 +611,18 @@ template <int U, bool NTL, bool NTS>
 struct FqPtCodes {
   static void go(dim3 g, dim3 b, hipStream_t s, const f32x4* x, f32x4* y, uint32_t* c,
                  const float* d, const float* z, int64_t n4, float sc, float lo, float hi,
-                 int64_t chunk, int fastdiv) {
+                 int64_t chunk, int fastdiv, int ste) {
     hipLaunchKernelGGL((fq_fwd_pt<true, U, NTL, NTS>), g, b, 0, s, x, y, c, d, z, n4, sc, lo, hi,
-                       chunk, fastdiv);
+                       chunk, fastdiv, ste);
   }
 };
 template <int U, bool NTL, bool NTS>
 struct FqPt {
   static void go(dim3 g, dim3 b, hipStream_t s, const f32x4* x, f32x4* y, uint32_t* c,
                  const float* d, const float* z, int64_t n4, float sc, float lo, float hi,
-                 int64_t chunk, int fastdiv) {
+                 int64_t chunk, int fastdiv, int ste) {
     hipLaunchKernelGGL((fq_fwd_pt<false, U, NTL, NTS>), g, b, 0, s, x, y, c, d, z, n4, sc, lo, hi,
-                       chunk, fastdiv);
+                       chunk, fastdiv, ste);
   }
 };
 template <int U, bool NTL, bool NTS>
@@ -652,13 +677,13 @@ extern "C" int ssq_set_variant(int v) {
   return old;
 }
 
-extern "C" int ssq_fq_fwd(const float* x, float* y, void* codes, const float* delta,
-                          const float* zp, int64_t n, int64_t inner, int64_t nch, float scale,
-                          int qmin, int qmax, ssq_stream_t stream) {
-  SSQ_REQUIRE(n >= 0 && inner >= 1 && nch >= 1, SSQ_E_ARG, "ssq_fq_fwd: bad sizes");
-  SSQ_REQUIRE(qmin < qmax, SSQ_E_ARG, "ssq_fq_fwd: qmin >= qmax");
+static int fq_fwd_impl(const char* what, int ste, const float* x, float* y, void* codes,
+                       const float* delta, const float* zp, int64_t n, int64_t inner,
+                       int64_t nch, float scale, int qmin, int qmax, ssq_stream_t stream) {
+  SSQ_REQUIRE(n >= 0 && inner >= 1 && nch >= 1, SSQ_E_ARG, "%s: bad sizes", what);
+  SSQ_REQUIRE(qmin < qmax, SSQ_E_ARG, "%s: qmin >= qmax", what);
   if (n == 0) return SSQ_OK;
-  SSQ_REQUIRE(x && y && delta && zp, SSQ_E_ARG, "ssq_fq_fwd: null pointer");
+  SSQ_REQUIRE(x && y && delta && zp, SSQ_E_ARG, "%s: null pointer", what);
   hipStream_t s = (hipStream_t)stream;
   const float lo = (float)qmin, hi = (float)qmax;
   const bool vec = aligned16(x) && aligned16(y) && (!codes || ((uintptr_t)codes & 3u) == 0);
@@ -673,49 +698,68 @@ extern "C" int ssq_fq_fwd(const float* x, float* y, void* codes, const float* de
       const f32x4* xv = (const f32x4*)x;
       f32x4* yv = (f32x4*)y;
       uint32_t* cv = (uint32_t*)codes;
-      if (!codes && chunk == 0 && block.x == (unsigned)kBlock && g_fq_pend.on &&
+      if (!codes && chunk == 0 && block.x == (unsigned)kBlock && g_fq_defer && g_fq_pend.on &&
           g_fq_pend.s == s) {
         // a queued multi-tensor q/dq rides on this launch
         const PendingFq f = g_fq_pend;
         g_fq_pend.on = false;
-        const PtArgs a{xv, yv, delta, zp, n4, scale, lo, hi, v.rcp ? 1 : 0, grid.x};
+        const PtArgs a{xv, yv, delta, zp, n4, scale, lo, hi, v.rcp ? 1 : 0, ste, grid.x};
         launch_stream<FqPtRide>(v, dim3(grid.x + f.blk), block, s, a, f.tab, f.cap);
       } else if (codes)
         launch_stream<FqPtCodes>(v, grid, block, s, xv, yv, cv, delta, zp, n4, scale, lo, hi,
-                                 chunk, v.rcp ? 1 : 0);
+                                 chunk, v.rcp ? 1 : 0, ste);
       else
         launch_stream<FqPt>(v, grid, block, s, xv, yv, cv, delta, zp, n4, scale, lo, hi, chunk,
-                            v.rcp ? 1 : 0);
+                            v.rcp ? 1 : 0, ste);
     } else if (n < (1ll << 31)) {
       // per-channel: the LDS-staged tile kernel with one segment (no 64-bit divides)
       SegTable tab;
       tab.nseg = 1;
+      tab.ste = ste;
       tab.s[0] = Seg{x, y, delta, zp, (uint8_t*)codes, (uint32_t)n, 0u, (uint32_t)inner,
                      (uint32_t)nch, lo, hi, scale, make_fastdiv((uint32_t)inner), 1u};
       const uint32_t cap = tile_channels(kTile, (uint32_t)inner);
       hipLaunchKernelGGL(fq_fwd_multi_kernel<kTile / 4 / kBlock>,
                          dim3((unsigned)((n + kTile - 1) / kTile)), dim3(kBlock),
                          2 * cap * sizeof(float), s, tab, cap);
-      return check_launch("ssq_fq_fwd");
+      return check_launch(what);
     } else {
-      SSQ_REQUIRE(inner < (1ll << 31) && nch < (1ll << 31), SSQ_E_ARG, "ssq_fq_fwd: dims");
+      SSQ_REQUIRE(inner < (1ll << 31) && nch < (1ll << 31), SSQ_E_ARG, "%s: dims", what);
       const int grid = grid_for(n4, kBlock, 4096);
       if (codes)
         hipLaunchKernelGGL((fq_fwd_pc<true>), dim3(grid), dim3(kBlock), 0, s, (const f32x4*)x,
                            (f32x4*)y, (uint32_t*)codes, delta, zp, n4, (uint32_t)inner,
-                           (uint32_t)nch, scale, lo, hi);
+                           (uint32_t)nch, scale, lo, hi, ste);
       else
         hipLaunchKernelGGL((fq_fwd_pc<false>), dim3(grid), dim3(kBlock), 0, s, (const f32x4*)x,
                            (f32x4*)y, nullptr, delta, zp, n4, (uint32_t)inner, (uint32_t)nch,
-                           scale, lo, hi);
+                           scale, lo, hi, ste);
     }
   }
   const int64_t start = n4 * 4;
   if (start < n) {
     hipLaunchKernelGGL(fq_fwd_scalar, dim3(grid_for(n - start, kBlock)), dim3(kBlock), 0, s, x,
-                       y, (uint8_t*)codes, delta, zp, n, start, inner, nch, scale, lo, hi);
+                       y, (uint8_t*)codes, delta, zp, n, start, inner, nch, scale, lo, hi, ste);
   }
-  return check_launch("ssq_fq_fwd");
+  return check_launch(what);
+}
+
+// UniformAffineQuantizer.forward: round_ste (quant_layer.py:18-22,92-98)
+extern "C" int ssq_fq_fwd(const float* x, float* y, void* codes, const float* delta,
+                          const float* zp, int64_t n, int64_t inner, int64_t nch, float scale,
+                          int qmin, int qmax, ssq_stream_t stream) {
+  return fq_fwd_impl("ssq_fq_fwd", 1, x, y, codes, delta, zp, n, inner, nch, scale, qmin, qmax,
+                     stream);
+}
+
+// the same q/dq with torch.round: ChannelQuant / ChannelQuantAct 'none'
+// (channelQuant.py:79-94, channelQuantAct.py:56-67), AdaRound 'nearest'
+// (adaptive_rounding.py:40-41)
+extern "C" int ssq_fq_round_fwd(const float* x, float* y, void* codes, const float* delta,
+                                const float* zp, int64_t n, int64_t inner, int64_t nch,
+                                float scale, int qmin, int qmax, ssq_stream_t stream) {
+  return fq_fwd_impl("ssq_fq_round_fwd", 0, x, y, codes, delta, zp, n, inner, nch, scale, qmin,
+                     qmax, stream);
 }
 
 extern "C" int ssq_fq_fwd_multi(int nseg, const float* const* x, float* const* y,
@@ -736,6 +780,7 @@ extern "C" int ssq_fq_fwd_multi(int nseg, const float* const* x, float* const* y
   for (int base = 0; base < nseg; base += kMaxSeg) {
     SegTable tab;
     tab.nseg = nseg - base < kMaxSeg ? nseg - base : kMaxSeg;
+    tab.ste = 1;
     int64_t blk = 0;
     uint32_t min_inner = UINT32_MAX;
     for (int k = 0; k < tab.nseg; ++k) {
@@ -770,6 +815,9 @@ extern "C" int ssq_fq_fwd_multi(int nseg, const float* const* x, float* const* y
 extern "C" int ssq_set_deferred_fq_multi(int on) {
   const int prev = g_fq_defer ? 1 : 0;
   g_fq_defer = on != 0;
+  // switching off: a table still queued (on whichever stream) launches now, on its stream
+  // (a launch error is left for the next check_launch to report)
+  if (!g_fq_defer && g_fq_pend.on) (void)flush_fq(g_fq_pend.s);
   return prev;
 }
 

@@ -286,7 +286,7 @@ __device__ __forceinline__ void epi_elem(EpiRow& w, float d, float z, float lo, 
   bool m = true;
   if (QUANT) {
     tq = t / d;
-    const float v = __fadd_rn(rintf(tq), z);
+    const float v = round_ste_zp(tq, z);                // the act quantizer's round_ste
     m = (v >= lo) && (v <= hi);
     q = clampf(v, lo, hi);
   }

@@ -113,8 +113,10 @@ __device__ __forceinline__ float div_fast(float x, float d, float r) {
 }
 
 __device__ __forceinline__ float clampf(float v, float lo, float hi) {
-  // torch.clamp semantics on finite values: min(max(v, lo), hi)
-  return fminf(fmaxf(v, lo), hi);
+  // torch.clamp: min(max(v, lo), hi) with a NaN input kept NaN (fminf / fmaxf would
+  // return the bound): IEEE 754-2019 maximum / minimum, v_maximum3_f32 / v_minimum3_f32
+  // on gfx950 -- two instructions, as many as the bound-returning form
+  return __builtin_elementwise_minimum(__builtin_elementwise_maximum(v, lo), hi);
 }
 
 // torch.sigmoid in fp32 (1 / (1 + exp(-x))).
@@ -127,11 +129,14 @@ __device__ __forceinline__ float rect_sigmoid(float v) {
 }
 
 // d h / d v  (clamp mask inclusive) * upstream
+// The reference's autograd order: clamp backward (0 outside, NaN u -> 0), * (zeta-gamma),
+// sigmoid backward g*(1-s)*s -- so a NaN v gives NaN even under a zero upstream, and an
+// outside-the-clamp finite v gives +0 as before.
 __device__ __forceinline__ float rect_sigmoid_grad(float v, float g) {
   float s = sigmoidf(v);
   float u = __fadd_rn(__fmul_rn(s, kZmG), kGamma);
-  if (!(u >= 0.0f && u <= 1.0f)) return 0.0f;
-  return __fmul_rn(__fmul_rn(__fmul_rn(g, kZmG), __fsub_rn(1.0f, s)), s);
+  const float gu = (u >= 0.0f && u <= 1.0f) ? g : 0.0f;
+  return __fmul_rn(__fmul_rn(__fmul_rn(gu, kZmG), __fsub_rn(1.0f, s)), s);
 }
 
 // p = clamp(softmax(a)*(zeta-gamma)+gamma, 0, 1) over S logits (channelQuant.py:120-121)
@@ -239,17 +244,32 @@ __device__ __forceinline__ bool arrive_last(unsigned* ticket, unsigned nblocks, 
   return last;
 }
 
-// one element of the uniform affine fake-quant (quant_layer.py:92-98)
+// round_ste's forward (quant_layer.py:18-22) plus the zero point: ((round(t) - t) + t) + zp.
+// (round(t) - t) + t is round(t) for every finite t (round(t) - t is a multiple of ulp(t)
+// no larger than 1/2: both operations are exact) and NaN at t = +-inf, where torch.round
+// alone returns +-inf.  Evaluated as v = round(t) + zp, then fma(v, 0, v): v for every
+// finite v (the product is a signed zero), NaN for an infinite one -- one instruction.
+// Only the sign of a zero v can differ from the reference's order, and (q - zp) * delta
+// maps both signs to the same dequantized value.
+__device__ __forceinline__ float round_ste_zp(float t, float z) {
+  const float v = __fadd_rn(rintf(t), z);
+  return __fmaf_rn(v, 0.0f, v);
+}
+
+// one element of the uniform affine fake-quant (quant_layer.py:92-98).  STE: the
+// UniformAffineQuantizer's round_ste; !STE: plain torch.round (ChannelQuant 'none',
+// ChannelQuantAct 'none', AdaRound 'nearest'): the two differ only where x / delta is
+// +-inf (NaN vs a clamped edge).
 struct QParams {
   float d, z, lo, hi;
 };
 
-template <bool FAST = false>
+template <bool FAST = false, bool STE = true>
 __device__ __forceinline__ float fq1(float x, const QParams& p, float* qout, float r = 0.0f) {
   // x / delta: IEEE fp32 divide, or its bit-identical reciprocal form (div_fast)
   float t = FAST ? div_fast(x, p.d, r) : x / p.d;
-  float v = __fadd_rn(rintf(t), p.z);      // round_ste fwd == round half-even, + zp
-  float q = clampf(v, p.lo, p.hi);         // clamp(x_int, lo, hi)
+  const float v = STE ? round_ste_zp(t, p.z) : __fadd_rn(rintf(t), p.z);  // + zp
+  float q = clampf(v, p.lo, p.hi);         // clamp(x_int, lo, hi): NaN stays NaN
   *qout = q;
   return __fmul_rn(__fsub_rn(q, p.z), p.d);  // (x_quant - zp) * delta
 }

@@ -56,9 +56,12 @@ def _zp_like(zp, delta):
         zp.reshape(zp.shape + (1,) * (delta.dim() - zp.dim())).expand(delta.shape).contiguous()
 
 
-def fake_quant_fwd(x, delta, zp, n_bits, sym=False, scale=1.0, codes=False, out=None):
+def fake_quant_fwd(x, delta, zp, n_bits, sym=False, scale=1.0, codes=False, out=None,
+                   ste=True):
     """UniformAffineQuantizer.forward (quant_layer.py:92-98). Returns (y, codes|None);
-    `out` (same shape, fp32, on the device) receives y when given."""
+    `out` (same shape, fp32, on the device) receives y when given.  ste=True rounds as the
+    reference's round_ste ((round(t) - t) + t: NaN at t = +-inf), ste=False as plain
+    torch.round (ChannelQuant / ChannelQuantAct 'none', AdaRound 'nearest')."""
     x, xp = fptr(x, "x")
     delta, dp = fptr(delta.detach(), "delta")
     zp, zpp = fptr(_zp_like(zp.detach(), delta), "zero_point")
@@ -71,8 +74,8 @@ def fake_quant_fwd(x, delta, zp, n_bits, sym=False, scale=1.0, codes=False, out=
     else:
         y = torch.empty_like(x)
     cb = _codes_buf(x, codes)
-    call("ssq_fq_fwd", xp, _vp(y), _vp(cb), dp, zpp, x.numel(), inner, nch, float(scale), lo, hi,
-         stream_of(x))
+    call("ssq_fq_fwd" if ste else "ssq_fq_round_fwd", xp, _vp(y), _vp(cb), dp, zpp, x.numel(),
+         inner, nch, float(scale), lo, hi, stream_of(x))
     return y, cb
 
 
@@ -120,7 +123,7 @@ class RoundQuantFn(torch.autograd.Function):
 
     @staticmethod
     def forward(ctx, x, delta, zp, n_bits, sym, scale):
-        y, _ = fake_quant_fwd(x, delta, zp, n_bits, sym, scale=scale)
+        y, _ = fake_quant_fwd(x, delta, zp, n_bits, sym, scale=scale, ste=False)
         ctx.save_for_backward(x, delta, zp)
         ctx.q = (n_bits, sym, scale)
         return y
@@ -156,11 +159,19 @@ def round_quant(x, delta, zp, n_bits, sym=False, scale=1.0):
 class FqMultiPlan:
     """fake_quant_multi's arguments checked and packed once: calling the plan launches the
     same table again (one ctypes call), e.g. a fixed model's weights quantised every step.
-    The plan holds its tensors; it reads their current values at each launch, so in-place
-    updates are seen, but a tensor replaced by a new one needs a new plan."""
+    The plan holds its tensors and reads their current values at each launch, so in-place
+    updates of x / delta / zero_point are seen; it therefore refuses non-contiguous inputs
+    (a contiguous copy would freeze their values at plan time).  A tensor replaced by a new
+    one needs a new plan.  fake_quant_multi (one launch) copies non-contiguous inputs."""
 
-    def __init__(self, xs, deltas, zps, n_bits, sym=False, out=None):
+    def __init__(self, xs, deltas, zps, n_bits, sym=False, out=None, _once=False):
         n = len(xs)
+        if not _once:
+            for k, (x, d, z) in enumerate(zip(xs, deltas, zps)):
+                for t, what in ((x, "x"), (d, "delta"), (z, "zero_point")):
+                    if not t.is_contiguous():
+                        raise ValueError(f"FqMultiPlan: {what}[{k}] is not contiguous (a copy "
+                                         "would not see later in-place updates)")
         if out is None:
             ys = [torch.empty_like(x) for x in xs]
         else:
@@ -204,7 +215,7 @@ def fake_quant_multi(xs, deltas, zps, n_bits, sym=False, out=None):
     """Every tensor of a list in one launch (per-channel params staged in LDS); out: a
     list of contiguous fp32 outputs, one per input and of its shape (else allocated).
     FqMultiPlan packs the same arguments once for repeated launches."""
-    return FqMultiPlan(xs, deltas, zps, n_bits, sym, out)()
+    return FqMultiPlan(xs, deltas, zps, n_bits, sym, out, _once=True)()
 
 
 _DEFERRED_FQ_KEEP = None
@@ -447,6 +458,49 @@ def _ptrs(ts):
     return (C.c_void_p * len(ts))(*[None if t is None else t.data_ptr() for t in ts])
 
 
+# Gradient destinations of leaf parameters (data_ptr -> contiguous tensor of the parameter's
+# size), set by the data-parallel loop to the slices of its all-reduce bucket (grads_into):
+# the backward kernels below then write a parameter's gradient straight into its slice and
+# hand autograd None for it -- no AccumulateGrad add, and a deferred finalize (fin_tasks.h)
+# may still be pending when backward returns: nothing reads the slice before the collective,
+# which runs after the iteration's queued finalizes are flushed.  Each such parameter must
+# get its gradient from exactly one kernel per iteration (alpha: its adaShift backward;
+# gamma^z / phi^z: their module's epilogue).
+GRAD_INTO = {}
+INTO_WRITES = [0]       # gradients written straight into a GRAD_INTO slice (test counter)
+
+
+class grads_into:
+    """Context: GRAD_INTO = mapping (param.data_ptr() -> destination) inside."""
+
+    def __init__(self, mapping):
+        self.mapping = mapping or {}
+
+    def __enter__(self):
+        self.prev = dict(GRAD_INTO)
+        GRAD_INTO.clear()
+        GRAD_INTO.update(self.mapping)
+        return self
+
+    def __exit__(self, *exc):
+        GRAD_INTO.clear()
+        GRAD_INTO.update(self.prev)
+
+
+def _grad_dest(param, numel, device, need=True):
+    """(destination tensor, written_into) for a parameter's gradient: its GRAD_INTO slice,
+    or a fresh buffer (None when the gradient is not needed)."""
+    if param is None or not need:
+        return None, False
+    d = GRAD_INTO.get(param.data_ptr()) if GRAD_INTO else None
+    if d is not None:
+        if d.numel() != numel or not d.is_contiguous():
+            raise A.SSQError("grads_into: destination does not match the parameter")
+        INTO_WRITES[0] += 1
+        return d.view(-1), True
+    return torch.empty(numel, device=device), False
+
+
 class AdaShiftPrepFn(torch.autograd.Function):
     """ChannelQuant 'adaShift' forward of SEVERAL prepared weights (e.g. every conv of a
     block, same S and regulariser) in one launch (K5p), and their alpha backward in two
@@ -489,7 +543,8 @@ class AdaShiftPrepFn(torch.autograd.Function):
         saved = ctx.saved_tensors
         al, dl, zl = saved[:n], saved[n:2 * n], saved[2 * n:]
         gs = [torch.zeros_like(p.hterm) if g is None else g.contiguous() for g, p in zip(gs, preps)]
-        gas = [torch.empty_like(a) for a in al]
+        dst = [_grad_dest(a, a.numel(), a.device) for a in al]
+        gas = [d.view(a.shape) for (d, _), a in zip(dst, al)]
         lam, bb, reg_vals, reg_dev = (0.0, 0.0, None, None) if reg is None else reg
         rv = reg_vals if isinstance(reg_vals, (list, tuple)) else [reg_vals] * n
         S = preps[0].S
@@ -499,7 +554,8 @@ class AdaShiftPrepFn(torch.autograd.Function):
              _ptrs([p.hterm for p in preps]), _ptrs(al), _ptrs(dl), _ptrs(zl), Co, Ci, Kk, lo, hi, S,
              float(lam), float(bb), _vp(reg_dev), _ptrs(gas),
              _ptrs(rv) if any(v is not None for v in rv) else None, ws, wsn, stream_of(gs[0]))
-        return (None,) + tuple(ga if need else None for ga, need in zip(gas, ctx.needs_input_grad[1:]))
+        return (None,) + tuple(ga if (need and not into) else None
+                               for ga, (_, into), need in zip(gas, dst, ctx.needs_input_grad[1:]))
 
 
 def adashift_prepared(alpha, prep, delta, zp, n_bits, sym, hard_t, reg=None):
@@ -993,8 +1049,8 @@ class EpilogueFn(torch.autograd.Function):
         d, z = flat(delta), flat(zp)
         gy = torch.empty_like(g)
         gres = torch.empty_like(g) if (res is not None and need[4]) else None
-        ggm = torch.empty(C_, device=dev_) if (gamma is not None and need[2]) else None
-        gph = torch.empty(C_, device=dev_) if (phi is not None and need[3]) else None
+        ggm, gm_into = _grad_dest(gamma, C_, dev_, need[2])
+        gph, ph_into = _grad_dest(phi, C_, dev_, need[3])
         gd = torch.empty(1, device=dev_) if (quant and need[5]) else None
         gz = torch.empty(1, device=dev_) if (quant and need[6]) else None
         N = g.numel() // (C_ * hw)
@@ -1005,8 +1061,9 @@ class EpilogueFn(torch.autograd.Function):
              lo, hi, _vp(gy), _vp(gres), _vp(ggm), _vp(gph), _vp(gd), _vp(gz), ws, wsn,
              stream_of(g))
         shape = (lambda t, o: None if o is None else o.view(t.shape))
-        return (gy if need[0] else None, None, shape(gamma, ggm), shape(phi, gph), gres,
-                shape(delta, gd), shape(zp, gz), None, None, None)
+        return (gy if need[0] else None, None, None if gm_into else shape(gamma, ggm),
+                None if ph_into else shape(phi, gph), gres, shape(delta, gd), shape(zp, gz), None,
+                None, None)
 
 
 _EPI_SLOT = [0]
@@ -1117,15 +1174,16 @@ def epilogue_loss_bwd(tail, tgt, M):
     loss = torch.empty(1, dtype=torch.float32, device=dev_)
     gy = torch.empty_like(y)
     gres = torch.empty_like(y) if (res is not None and res.requires_grad) else None
-    ggm = torch.empty(C_, device=dev_) if (gamma is not None and gamma.requires_grad) else None
-    gph = torch.empty(C_, device=dev_) if (phi is not None and phi.requires_grad) else None
+    ggm, gm_into = _grad_dest(gamma, C_, dev_, gamma is not None and gamma.requires_grad)
+    gph, ph_into = _grad_dest(phi, C_, dev_, phi is not None and phi.requires_grad)
     gd = torch.empty(1, device=dev_) if (q is not None and q.delta.requires_grad) else None
     gz = torch.empty(1, device=dev_) if (q is not None and q.zero_point.requires_grad) else None
     ws, wsn = workspace(query("ssq_epilogue_bwd_workspace_size", N * C_), dev_, _epi_slot())
     call("ssq_epilogue_loss_bwd", cp, _vp(idx), int(M), _vp(loss), yp, bp, _vp(gm), _vp(ph), rp,
          N, C_, hw, int(relu), _vp(d), _vp(z), lo, hi, _vp(gy), _vp(gres), _vp(ggm), _vp(gph),
          _vp(gd), _vp(gz), ws, wsn, stream_of(y))
-    return loss, gy, gres, ggm, gph, gd, gz
+    # a gradient written into its GRAD_INTO slice is not handed back (already in place)
+    return loss, gy, gres, None if gm_into else ggm, None if ph_into else gph, gd, gz
 
 
 def adam_step(params, grads, exp_avgs, exp_avg_sqs, beta1, beta2, eps, hyper=None,

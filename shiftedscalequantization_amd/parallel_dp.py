@@ -65,6 +65,14 @@ class GradBucket:
         for p, v in zip(self.live, self.views):
             p.grad = v
 
+    def into_map(self):
+        """{param.data_ptr(): its bucket slice} for the live parameters (K.grads_into): the
+        backward kernels write those gradients straight into the bucket.  Empty before the
+        bucket is built (the first iteration hands the gradients over through .grad)."""
+        if self.live is None:
+            return {}
+        return {p.data_ptr(): v for p, v in zip(self.live, self.views)}
+
     @property
     def active(self):
         """True once the bucket is built at world > 1 (what a graph capture needs)."""

@@ -29,7 +29,7 @@ class AdaRoundQuantizer(nn.Module):
 
     def forward(self, x):
         if self.round_mode == 'nearest':
-            y, _ = K.fake_quant_fwd(x, self.delta, self.zero_point, self.n_bits, False)
+            y, _ = K.fake_quant_fwd(x, self.delta, self.zero_point, self.n_bits, False, ste=False)
             return y
         elif self.round_mode == 'nearest_ste':
             return K.fake_quant(x, self.delta, self.zero_point, self.n_bits, False)

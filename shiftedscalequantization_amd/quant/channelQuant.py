@@ -70,7 +70,7 @@ class ChannelQuant(nn.Module):
                     out.append(torch.floor(self._src / (self._src_delta * st)))
                 else:
                     y, _ = K.fake_quant_fwd(self._src, self._src_delta, self.zero_point,
-                                            self.n_bits, self.sym, scale=st)
+                                            self.n_bits, self.sym, scale=st, ste=False)
                     out.append(y)
             self._xq_cache = out
         return self._xq_cache
@@ -120,7 +120,7 @@ class ChannelQuant(nn.Module):
                               self.hard_round, scale=self.shiftedScale)
         elif self.opt_mode == 'none':
             y, _ = K.fake_quant_fwd(x, self.delta, self.zero_point, self.n_bits, self.sym,
-                                    scale=self.shiftedScale)
+                                    scale=self.shiftedScale, ste=False)
             return y
         elif self.opt_mode in 'learned_hard_sigmoid':  # substring test, channelQuant.py:81
             return K.lhs(self.alpha, self._src, self._src_delta, self.zero_point, self.shiftTarget,

@@ -133,10 +133,12 @@ def _fused_loop(block, modules, iters, lmda, model, p, lr, bias_cal, batch_size,
     hyper = feeder.extra[2:4]
     last = {}
 
-    # one GPU: the loss value and gamma^z/phi^z finalizes ride on the next backward launch
-    # (csrc/fin_tasks.h); with a bucket the grads are accumulated in place by autograd, so
-    # they must be final when backward returns them
-    defer = DEFER_FINALIZE and on_gpu and bucket is None
+    # the loss value and gamma^z/phi^z finalizes ride on the next backward launch
+    # (csrc/fin_tasks.h).  With a bucket (world > 1) the backward kernels write alpha and
+    # gamma^z / phi^z straight into their bucket slices (K.grads_into) instead of handing
+    # them to autograd, whose in-place add would read a finalize still queued; the queued
+    # ones are flushed at the end of the body, before the collective
+    defer = DEFER_FINALIZE and on_gpu
 
     # the fused tail (K.epilogue_loss_bwd) needs the p = 2 loss (the reference's default)
     fuse_tail = FUSE_TAIL and on_gpu and float(p) == 2.0
@@ -146,11 +148,12 @@ def _fused_loop(block, modules, iters, lmda, model, p, lr, bias_cal, batch_size,
     def body_pre():
         """One iteration on the device up to its exchange step: gather -> forward -> fused
         loss+grad -> backward.  No host sync, no host-side state: graph-capturable."""
-        with K.deferred_finalize(defer):
-            _body_pre()
+        into = bucket.into_map() if (bucket is not None and defer) else {}
+        with K.grads_into(into), K.deferred_finalize(defer):
+            _body_pre(into)
 
-    def _body_pre():
-        if defer and any(t.grad is not None for t in opt_params):
+    def _body_pre(into):
+        if defer and any(t.grad is not None and t.data_ptr() not in into for t in opt_params):
             # a deferred gamma/phi gradient is only final after the next backward launch:
             # AccumulateGrad must take it over, never add it into an existing .grad
             raise RuntimeError("deferred finalizes need every parameter's .grad unset")

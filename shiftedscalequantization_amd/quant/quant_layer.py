@@ -28,14 +28,32 @@ def frozen_weight_cache():
     and reuses that W_hat for the rest of the context.  validate_model (common.py:152-221)
     runs the whole pass in it: no quantizer changes during inference, so each batch's
     forward is bit-identical to recomputing W_hat, without the per-batch weight q/dq
-    launches.  The cache is keyed on the module, its weight quantizer object and the weight
-    tensor (identity and version), and is dropped when the context exits."""
+    launches.  The cache is keyed on the module, its weight quantizer object, the weight
+    tensor (identity and version) and the quantizer's tensors and mode flags
+    (_quantizer_state), and is dropped when the context exits.  Writes through raw pointers
+    (SsqAdam, graph replays) bump no version: nothing may train inside the context."""
     global _FROZEN_W
     prev, _FROZEN_W = _FROZEN_W, {}
     try:
         yield
     finally:
         _FROZEN_W = prev
+
+
+_STATE_FLAGS = ('soft_targets', 'hard_round', 'hard_targets', 'opt_mode', 'shiftedScale',
+                'round_mode', 'n_bits')
+
+
+def _quantizer_state(q):
+    """What a weight quantizer's output depends on besides the weight: every tensor it holds
+    (identity, storage, version counter) and its mode flags.  SsqAdam and graph replays write
+    parameters through raw pointers without bumping _version, so the frozen-weight cache is
+    only sound while nothing trains -- validate_model's pass (no_grad, no optimizer)."""
+    ts = tuple((k, id(v), v.data_ptr(), v._version) for k, v in sorted(vars(q).items())
+               if isinstance(v, torch.Tensor))
+    ps = tuple((k, id(v), v.data_ptr(), v._version) for k, v in q.named_parameters(recurse=False))
+    flags = tuple((k, getattr(q, k)) for k in _STATE_FLAGS if hasattr(q, k))
+    return ts + ps + flags
 
 
 class StraightThrough(nn.Module):
@@ -240,7 +258,8 @@ class QuantModule(nn.Module):
     def _weight_bias(self):
         if self.use_weight_quant and self.cache_features == 'none':
             if _FROZEN_W is not None and not torch.is_grad_enabled():
-                key = (id(self.weight_quantizer), id(self.weight), self.weight._version)
+                key = (id(self.weight_quantizer), id(self.weight), self.weight._version,
+                       _quantizer_state(self.weight_quantizer))
                 hit = _FROZEN_W.get(self)
                 if hit is None or hit[0] != key:
                     hit = (key, self.weight_quantizer(self.weight))

@@ -7,7 +7,7 @@ half of the fixture's calibration data (parallel_dp.shard_rows), runs the loop, 
 writes what the test compares: the learned parameters, their values before the loop, and
 every iteration's (local, all-reduced) gradient bucket (parallel_dp.RECORD).
 
-    python tests/dp_worker.py {fused|brecq|validate} OUT.npz
+    python tests/dp_worker.py {fused|fused_bc|fused_bc_nodefer|brecq|validate} OUT.npz
 """
 import os
 import sys
@@ -32,7 +32,19 @@ def host(t):
     return t.detach().float().cpu().numpy().copy()
 
 
-def run_fused(out):
+def run_fused_bc(out):
+    run_fused(out, bias_cal=True)
+
+
+def run_fused_bc_nodefer(out):
+    import importlib
+    # the module (quant/__init__ re-exports a function of the same name)
+    LRF = importlib.import_module("shiftedscalequantization_amd.quant.layer_recon_fused_shiftedScale")
+    LRF.DEFER_FINALIZE = False
+    run_fused(out, bias_cal=True)
+
+
+def run_fused(out, bias_cal=False):
     from conftest import load_golden
     import test_recon_gpu as T
     from shiftedscalequantization_amd import quant as Q
@@ -51,14 +63,21 @@ def run_fused(out):
     def hook(i):
         if i == 0:
             for n in convs:
-                out[n + "_alpha0"] = host(getattr(block, n).weight_quantizer.alpha)
+                m = getattr(block, n)
+                out[n + "_alpha0"] = host(m.weight_quantizer.alpha)
+                out[n + "_gamma0"], out[n + "_phi0"] = host(m.alpha_out), host(m.beta_out)
 
+    from shiftedscalequantization_amd import kernels as K
+    K.INTO_WRITES[0] = 0
     torch.manual_seed(1005)
     res = block_recon_fused_shiftedScale(block, FUSED_ITERS, (0.01, 0.1), qnn, None, verbose=False,
-                                         iter_hook=hook, batch_size=FUSED_BS)
+                                         iter_hook=hook, batch_size=FUSED_BS, bias_cal=bias_cal)
     out["final_losses"] = np.array(res, np.float64)
+    out["into_writes"] = np.array([K.INTO_WRITES[0]])
     for n in convs:
-        out[n + "_alpha"] = host(getattr(block, n).weight_quantizer.alpha)
+        m = getattr(block, n)
+        out[n + "_alpha"] = host(m.weight_quantizer.alpha)
+        out[n + "_gamma"], out[n + "_phi"] = host(m.alpha_out), host(m.beta_out)
 
 
 def run_brecq(out):
@@ -120,7 +139,8 @@ def main():
     from shiftedscalequantization_amd import parallel_dp as P
     P.RECORD = []
     out = {"rank": np.array([dist.get_rank()])}
-    {"fused": run_fused, "brecq": run_brecq, "validate": run_validate}[mode](out)
+    {"fused": run_fused, "fused_bc": run_fused_bc, "fused_bc_nodefer": run_fused_bc_nodefer,
+     "brecq": run_brecq, "validate": run_validate}[mode](out)
     torch.cuda.synchronize()
     for k, (kind, local, reduced) in enumerate(P.RECORD):
         out[f"rec{k}_local"] = local.cpu().numpy()

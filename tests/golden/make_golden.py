@@ -143,6 +143,50 @@ def edge_tensor(g, shape, scale=1.0):
     return x
 
 
+# IEEE special values planted into the *_specials fixtures (after the quantizer's scale was
+# initialised on clean data: a NaN in the 'max' init makes the reference's Python round()
+# raise): NaN, +-inf, +-0 and the largest finite magnitudes
+SPECIALS = [float("nan"), float("inf"), -float("inf"), 0.0, -0.0, 3.0e38, -3.0e38,
+            float("nan")]
+
+
+def special_pos(shape):
+    """Fixed, distinct flat positions of SPECIALS: weights ([Co, Ci, ...]) get them in odd
+    output channels and in only two input channels (1 and Ci - 2), so that the per-input-
+    channel shift logits of the other channels keep finite gradients; other tensors
+    (activations) at a fixed stride."""
+    shape = tuple(shape)
+    n = int(np.prod(shape))
+    if len(shape) in (2, 4) and shape[0] >= 4:
+        co, ci = shape[0], shape[1]
+        cis = [min(1, ci - 1), max(ci - 2, 0)]
+        inner = int(np.prod(shape[2:])) if len(shape) == 4 else 1
+        pos = []
+        for k in range(len(SPECIALS)):
+            c, i, t = (2 * k + 1) % co, cis[k % 2], (k * 5) % inner
+            p = (c * ci + i) * inner + t
+            while p in pos:
+                p = (p + 1) % n
+            pos.append(p)
+        return pos
+    pos = []
+    k = 0
+    while len(pos) < len(SPECIALS):
+        p = (k * 37 + 5) % n
+        if p not in pos:
+            pos.append(p)
+        k += 1
+    return pos
+
+
+def with_specials(x):
+    y = x.clone()
+    flat = y.view(-1)
+    for p, v in zip(special_pos(x.shape), SPECIALS):
+        flat[p] = v
+    return y
+
+
 # --------------------------------------------------------------------------- K1-K4 UAQ
 def gen_uaq():
     g = torch.Generator().manual_seed(1005)
@@ -188,6 +232,58 @@ def gen_uaq():
     save("uaq", **out)
 
 
+def gen_uaq_specials():
+    """UAQ forward + STE backward (quant_layer.py:77-98) and ChannelQuantAct 'none'
+    (channelQuantAct.py:36-67) on inputs holding SPECIALS: the scales are initialised on
+    the clean tensor, then the quantizer runs on the tensor with the specials planted.
+    torch.clamp propagates NaN (the dequant is NaN there), +-inf clamp to the edges, and
+    the gradients are whatever the reference's autograd makes of them (NaN in the delta
+    sums where a NaN or an inf meets the x/delta path)."""
+    from quant.channelQuantAct import ChannelQuantAct
+    g = torch.Generator().manual_seed(2718)
+    out = {}
+    cases = [("b4_asym_pt_mse", 4, False, False, "mse", (4, 6, 7, 7)),
+             ("b2_asym_cw_max", 2, False, True, "max", (12, 5, 3, 3)),
+             ("b8_asym_cw_max", 8, False, True, "max", (12, 5, 3, 3)),
+             ("b4_sym_cw_max", 4, True, True, "max", (12, 5, 3, 3))]
+    for tag, bits, sym, cw, method, shape in cases:
+        x = edge_tensor(g, shape, 0.2 if cw else 1.0)
+        if not cw:
+            x = torch.relu(x)
+        q = UniformAffineQuantizer(n_bits=bits, symmetric=sym, channel_wise=cw, scale_method=method,
+                                   leaf_param=not cw, ch=shape)
+        with torch.no_grad():
+            q(x)                                   # scale init on the clean tensor
+        xs = with_specials(x * 1.5)
+        xr = xs.clone().requires_grad_(True)
+        y = q(xr)
+        gy = torch.randn(shape, generator=g)
+        (y * gy).sum().backward()
+        out[tag + "_x"] = t2n(xs)
+        out[tag + "_y"] = t2n(y)
+        out[tag + "_delta"] = t2n(q.delta.reshape(-1))
+        out[tag + "_zp"] = t2n(q.zero_point.reshape(-1))
+        out[tag + "_gy"] = t2n(gy)
+        out[tag + "_gx"] = t2n(xr.grad)
+        out[tag + "_gdelta"] = t2n(q.delta.grad.reshape(-1))
+        out[tag + "_gzp"] = t2n(q.zero_point.grad.reshape(-1))
+        if tag == "b4_asym_pt_mse":
+            # ChannelQuantAct 'none' on the same tensor (no STE: torch.round)
+            for k, sc in enumerate((1.0, 0.5)):
+                ca = ChannelQuantAct(uaq=q, shiftTarget=[1.0, 0.5])
+                ca.shiftedScale = sc
+                q.delta.grad = None
+                q.zero_point.grad = None
+                xr = xs.clone().requires_grad_(True)
+                ya = ca(xr)
+                (ya * gy).sum().backward()
+                out[f"act_s{k}_scale"] = np.array([sc], np.float64)
+                out[f"act_s{k}_y"] = t2n(ya)
+                out[f"act_s{k}_gdelta"] = t2n(q.delta.grad.reshape(-1))
+                out[f"act_s{k}_gzp"] = t2n(q.zero_point.grad.reshape(-1))
+    save("uaq_specials", **out)
+
+
 # --------------------------------------------------------------------------- K5-K9 ChannelQuant
 def _mk_uaq(w, bits=2, method="max"):
     q = UniformAffineQuantizer(n_bits=bits, channel_wise=True, scale_method=method, ch=w.shape)
@@ -195,7 +291,10 @@ def _mk_uaq(w, bits=2, method="max"):
     return q
 
 
-def gen_channelquant():
+def gen_channelquant(specials=False):
+    """specials=True: the same cases with SPECIALS planted into the weight AFTER the UAQ
+    scale init (init_v_beta, every mode and the AdaRound phase then see them), written to
+    channelquant_specials.npz with the same keys."""
     g = torch.Generator().manual_seed(1005)
     out = {}
     shapes = {"conv": (8, 6, 3, 3), "fc": (10, 12), "dw": (6, 1, 3, 3)}
@@ -205,6 +304,9 @@ def gen_channelquant():
             tag = f"{name}_b{bits}"
             w = torch.randn(shape, generator=g) * 0.05
             uaq = _mk_uaq(w, bits)
+            w_clean = w
+            if specials:
+                w = with_specials(w)
             cq = ChannelQuant(1.0, uaq=uaq, weight_tensor=w, shiftTarget=shift, name=tag)
             cq.init_v_beta(w.clone())
             cq.opt_mode = "adaShift"
@@ -237,7 +339,7 @@ def gen_channelquant():
             out[tag + "_delta_sel"] = t2n(cq.get_delta())
 
             # learned_hard_sigmoid path (init_v, channelQuant.py:201-213)
-            uaq2 = _mk_uaq(w, bits)
+            uaq2 = _mk_uaq(w_clean, bits)
             cq2 = ChannelQuant(1.0, uaq=uaq2, weight_tensor=w, shiftTarget=shift, name=tag)
             cq2.init_v(w.clone())
             out[tag + "_lhs_xq"] = np.stack([t2n(t) for t in cq2.x_q])
@@ -273,15 +375,19 @@ def gen_channelquant():
                     out[f"{tag}_ar_r{int(hard_r)}_gbeta"] = t2n(cq2.beta.grad)
             cq2.opt_mode = "none"
             out[tag + "_none_y"] = t2n(cq2(w))
-    save("channelquant", **out)
+    save("channelquant_specials" if specials else "channelquant", **out)
 
 
-def gen_adaround():
+def gen_adaround(specials=False):
+    """specials=True: SPECIALS planted into the weight after the UAQ scale init
+    (adaround_specials.npz, same keys)."""
     g = torch.Generator().manual_seed(1005)
     out = {}
     for name, shape in {"conv": (8, 6, 3, 3), "fc": (10, 12)}.items():
         w = torch.randn(shape, generator=g) * 0.05
         uaq = _mk_uaq(w, 2)
+        if specials:
+            w = with_specials(w)
         ar = AdaRoundQuantizer(uaq=uaq, round_mode="learned_hard_sigmoid", weight_tensor=w)
         out[name + "_w"] = t2n(w)
         out[name + "_delta"] = t2n(ar.delta.reshape(-1))
@@ -301,7 +407,7 @@ def gen_adaround():
                 (y * gy).sum().backward()
                 out[f"{name}_s{int(soft)}_galpha"] = t2n(ar.alpha.grad)
         out[name + "_h"] = t2n(ar.get_soft_targets())
-    save("adaround", **out)
+    save("adaround_specials" if specials else "adaround", **out)
 
 
 # --------------------------------------------------------------------------- K10
@@ -542,17 +648,20 @@ def _layer_truth(layer, spy, lmda, iters, adaround, batch_size=32):
     return truth
 
 
-def _fused_truth(block, spy, lmda, iters, batch_size=32):
+def _fused_truth(block, spy, lmda, iters, batch_size=32, bias_cal=False):
     """The reference's own fused-loop gradient of iteration `step`, evaluated in float64 at
     the parameters the fp32 run holds there (same batch, same loss schedule): the exact
-    gradient both fp32 implementations approximate."""
+    gradient both fp32 implementations approximate.  bias_cal: also gamma^z / phi^z, in the
+    optimizer's order (alpha, alpha_out, beta_out per QuantModule)."""
     import copy
 
     def truth(step):
         b64 = _to64(copy.deepcopy(block))
-        qs = [m.weight_quantizer for m in b64.modules() if isinstance(m, QuantModule)]
-        for q in qs:
-            q.alpha.grad = None
+        mods = [m for m in b64.modules() if isinstance(m, QuantModule)]
+        qs = [m.weight_quantizer for m in mods]
+        for m in mods:
+            m.weight_quantizer.alpha.grad = None
+            m.alpha_out.grad = m.beta_out.grad = None
         lf = LRF.FusedScaleLossFunction(b64, qs, round_loss="relaxation", lmda=lmda, max_count=iters,
                                         b_range=(20, 2), decay_start=0, warmup=0.2, p=2.0)
         lf.count = step
@@ -560,8 +669,45 @@ def _fused_truth(block, spy, lmda, iters, batch_size=32):
         inp = torch.cat(b64.cached_inp_features)[perm]
         tgt = torch.cat(b64.cached_out_features)[perm]
         spy.orig_call(lf, b64(inp), tgt).backward()
-        return [np.asarray(q.alpha.grad.detach().numpy(), np.float64).copy() for q in qs]
+        ts = []
+        for m in mods:
+            ts.append(m.weight_quantizer.alpha.grad)
+            if bias_cal:
+                ts += [m.alpha_out.grad, m.beta_out.grad]
+        return [np.asarray(t.detach().numpy(), np.float64).copy() for t in ts]
     return truth
+
+
+class _BiasCalAdam:
+    """Oracle-side shim for --bias_cal (README.md:20,33): the reference's own intent, the
+    commented-out `opt_params += [module.alpha_out]` / `[module.beta_out]` lines right after
+    each shift logit (layer_recon_fused_shiftedScale.py:65-68; the parameters:
+    quant_layer.py:231-238, applied at :258-259).  Inside the context the Adam the loop
+    builds (:73) also holds, after each QuantModule's alpha, that module's gamma^z and
+    phi^z -- nothing else of the reference changes."""
+
+    def __init__(self, block):
+        self.mods = [m for m in block.modules() if isinstance(m, QuantModule)]
+
+    def __enter__(self):
+        self.orig = torch.optim.Adam
+        mods, orig = self.mods, self.orig
+
+        class Adam(orig):
+            def __init__(self, params, *a, **k):
+                out = []
+                for p in list(params):
+                    out.append(p)
+                    for m in mods:
+                        if m.weight_quantizer.alpha is p:
+                            out += [m.alpha_out, m.beta_out]
+                super().__init__(out, *a, **k)
+
+        torch.optim.Adam = Adam
+        return self
+
+    def __exit__(self, *exc):
+        torch.optim.Adam = self.orig
 
 
 def _dump_block(out, block, prefix=""):
@@ -571,7 +717,10 @@ def _dump_block(out, block, prefix=""):
         out[prefix + n + "_b"] = t2n(m.org_bias)
 
 
-def gen_recon_fused(iters=30, n_cali=16, res=16):
+def gen_recon_fused(iters=30, n_cali=16, res=16, bias_cal=False):
+    """block_recon_fused_shiftedScale on the tiny net's BasicBlock.  bias_cal=True:
+    under _BiasCalAdam (gamma^z / phi^z learned too) -> recon_fused_biascal.npz, with their
+    values / gradients in the gs<step>_p/g/t records and their final values."""
     qnn = _build_tiny_qnn()
     torch.manual_seed(1005)
     cali = torch.randn(n_cali, 3, res, res)
@@ -593,8 +742,11 @@ def gen_recon_fused(iters=30, n_cali=16, res=16):
     out["cached_inp"] = t2n(torch.cat(block.cached_inp_features))
     out["cached_out"] = t2n(torch.cat(block.cached_out_features))
     torch.manual_seed(1005)
-    with _Spy(LRF.FusedScaleLossFunction) as spy:
-        with _GradSpy((0, 5, 20, iters - 1), _fused_truth(block, spy, (0.01, 0.1), iters)) as gspy:
+    import contextlib
+    with _Spy(LRF.FusedScaleLossFunction) as spy, \
+            (_BiasCalAdam(block) if bias_cal else contextlib.nullcontext()):
+        with _GradSpy((0, 5, 20, iters - 1),
+                      _fused_truth(block, spy, (0.01, 0.1), iters, bias_cal=bias_cal)) as gspy:
             res_loss = LRF.block_recon_fused_shiftedScale(block, iters, (0.01, 0.1), qnn, None)
     gspy.dump(out)
     out["perms"] = np.stack([p.numpy() for p in spy.perms]).astype(np.int64)
@@ -606,10 +758,12 @@ def gen_recon_fused(iters=30, n_cali=16, res=16):
         q = m.weight_quantizer
         out[n + "_alpha"] = t2n(q.alpha)
         out[n + "_beta0"] = t2n(q.beta)  # beta is never optimised in the fused loop
+        out[n + "_gamma"] = t2n(m.alpha_out)
+        out[n + "_phi"] = t2n(m.beta_out)
         with torch.no_grad():
             out[n + "_what_hard"] = t2n(q(m.weight))
     out["iters"] = np.array([iters])
-    save("recon_fused", **out)
+    save("recon_fused_biascal" if bias_cal else "recon_fused", **out)
 
 
 def gen_recon_layer_shift(iters=20, n_cali=16, res=16):
@@ -709,6 +863,58 @@ def gen_recon_brecq(iters=10, n_cali=16, res=16):
     out["a_total_loss"] = np.array([r[1] for r in spy.rec], np.float64)
     out["a_delta"] = np.array([float(q.delta) for q in aqs], np.float32)
     save("recon_brecq", **out)
+
+
+def gen_recon_layer_brecq(iters=10, n_cali=16, res=16):
+    """a22, BRECQ's per-layer path: layer_reconstruction (quant/layer_recon.py:10-104, its own
+    LossFunction :107-170) as Brecq/main_imagenet.py's recon_model calls it for a
+    QuantModule, on the tiny net's block conv1 (3x3 conv, 2-bit) and on its fc (Linear,
+    8-bit last layer), in that order (the fc's captured input then carries conv1's finished
+    hard rounding): the AdaRound weight phase, then after the act-delta init the act phase
+    (Adam lr 4e-4 on the act delta, cosine LR, p = 2.4).  The fc's act quantizer is the
+    network output's, disabled (disable_network_output_quantization), so its delta reaches
+    no output: no gradient, no Adam step -- only the loss values are recorded."""
+    from quant import layer_recon as LR
+    qnn = _build_tiny_qnn()
+    torch.manual_seed(1005)
+    cali = torch.randn(n_cali, 3, res, res)
+    qnn.set_quant_state(True, False)
+    with torch.no_grad():
+        qnn(cali[:8])
+    out = {"cali": t2n(cali)}
+    _dump_qms(out, qnn, "")
+    layers = [("conv", qnn.model[3].conv1), ("fc", qnn.model[6])]
+    assert isinstance(layers[1][1], QuantModule) and layers[1][1].weight.dim() == 2
+    for tag, layer in layers:
+        torch.manual_seed(1005)
+        with _Spy(LR.LossFunction) as spy:
+            LR.layer_reconstruction(qnn, layer, cali, batch_size=8, iters=iters, weight=0.01,
+                                    asym=True, b_range=(20, 2), warmup=0.2, act_quant=False,
+                                    opt_mode="mse")
+        out[f"{tag}_w_perms"] = np.stack([p.numpy() for p in spy.perms]).astype(np.int64)
+        out[f"{tag}_w_total_loss"] = np.array([r[1] for r in spy.rec], np.float64)
+        out[f"{tag}_alpha"] = t2n(layer.weight_quantizer.alpha)
+        with torch.no_grad():
+            out[f"{tag}_what_hard"] = t2n(layer.weight_quantizer(layer.weight))
+    qnn.set_quant_state(True, True)
+    with torch.no_grad():
+        qnn(cali[:8])
+    qnn.disable_network_output_quantization()
+    for tag, layer in layers:
+        aq = layer.act_quantizer
+        out[f"{tag}_a_delta0"] = np.array([float(aq.delta)], np.float32)
+        out[f"{tag}_a_on"] = np.array([int(not aq.disable_act_quant and not layer.disable_act_quant)])
+        torch.manual_seed(1005)
+        with _Spy(LR.LossFunction) as spy:
+            LR.layer_reconstruction(qnn, layer, cali, batch_size=8, iters=iters, act_quant=True,
+                                    opt_mode="mse", lr=4e-4, p=2.4)
+        out[f"{tag}_a_perms"] = np.stack([p.numpy() for p in spy.perms]).astype(np.int64)
+        out[f"{tag}_a_total_loss"] = np.array([r[1] for r in spy.rec], np.float64)
+        out[f"{tag}_a_delta"] = np.array([float(aq.delta)], np.float32)
+    with torch.no_grad():
+        out["logits"] = t2n(qnn(cali))
+    out["iters"] = np.array([iters])
+    save("recon_layer_brecq", **out)
 
 
 # ------------------------------------------------------------------ other block types
@@ -1194,6 +1400,9 @@ def gen_validate(n_cali=16, n_val=40, res=16, bs=8):
 # ------------------------------------------------------------------ round-3: real shapes
 def _real_block(kind, cin, cout):
     """The reference's own block classes at the real channel counts (realshape.CASES)."""
+    if kind == "basic1":
+        from models.resnet import BasicBlock
+        return BasicBlock(cin, cout, norm_layer=nn.BatchNorm2d)
     if kind == "basic":
         from models.resnet import BasicBlock
         ds = nn.Sequential(nn.Conv2d(cin, cout, 1, stride=2, bias=False), nn.BatchNorm2d(cout))
@@ -1232,6 +1441,89 @@ def _dump_sub(out, key, a, idx):
     out[key + "_max"] = np.array([np.abs(a).max(initial=0.0)], np.float64)
 
 
+def _real_fused(case, x, iters, grad_steps, bias_cal, out, keep_cached=True):
+    """The fused shifted-scale loop (block_recon_fused_shiftedScale) on the real-shape case:
+    the recorded inputs (weight hashes, deltas / zero points, the FP block output), the
+    batch draws, per-iteration losses, values / gradients (+ the float64 truth) at
+    grad_steps, final alpha (and gamma^z / phi^z with bias_cal) and hard-weight hashes."""
+    import contextlib
+    import realshape as RS
+    from quant.channelQuant import ChannelQuant
+    shift = [31 / 32, 33 / 32, 1.0]
+    qnn, _ = _real_qnn(case)
+    block = qnn.model[0]
+    qnn.set_quant_state(True, False)
+    with torch.no_grad():
+        qnn(x)
+    qms = _named_qms(block)
+    out["qms"] = np.array([n for n, _ in qms])
+    for n, m in qms:
+        out[f"{n}_w_sha"] = np.array([RS.sha(t2n(m.org_weight))])
+        out[f"{n}_b_sha"] = np.array([RS.sha(t2n(m.org_bias))])
+        out[f"{n}_delta"] = t2n(m.weight_quantizer.delta.reshape(-1))
+        out[f"{n}_zp"] = t2n(m.weight_quantizer.zero_point.reshape(-1))
+        m.weight_quantizer = ChannelQuant(1.0, uaq=m.weight_quantizer, weight_tensor=m.org_weight.data,
+                                          shiftTarget=shift, name="." + n)
+        m.use_weight_quant = True
+        m.cache_features = "none"
+    qnn.set_quant_state(False, False)
+    with torch.no_grad():
+        fp = block(x)
+    if keep_cached:
+        out["cached_out"] = t2n(fp)
+    out["cached_out_sha"] = np.array([RS.sha(t2n(fp))])
+    block.cached_inp_features, block.cached_out_features = [x.clone()], [fp.clone()]
+    MSM.set_quant_state_block(qnn, [".model.0"], "", True)
+    for n, m in qms:
+        out[f"{n}_beta0_sha"] = np.array([RS.sha(t2n(m.weight_quantizer.beta))]) \
+            if getattr(m.weight_quantizer, "beta", None) is not None else np.array([""])
+    torch.manual_seed(1005)
+    with _Spy(LRF.FusedScaleLossFunction) as spy, \
+            (_BiasCalAdam(block) if bias_cal else contextlib.nullcontext()):
+        with _GradSpy(grad_steps, _fused_truth(block, spy, (0.01, 0.1), iters, bias_cal=bias_cal)) as gspy:
+            res_loss = LRF.block_recon_fused_shiftedScale(block, iters, (0.01, 0.1), qnn, None)
+    out["perms"] = np.stack([p.numpy() for p in spy.perms]).astype(np.int64)
+    out["rec_loss"] = np.array([r[0] for r in spy.rec], np.float64)
+    out["final_losses"] = np.array(res_loss, np.float64)
+    out["iters"] = np.array([iters])
+    gspy.dump(out)      # alpha is [C_in, S], gamma / phi [1, C_out, 1, 1]: small, kept whole
+    for j, (n, m) in enumerate(qms):
+        q = m.weight_quantizer
+        out[f"{n}_alpha"] = t2n(q.alpha)
+        out[f"{n}_gamma"] = t2n(m.alpha_out)
+        out[f"{n}_phi"] = t2n(m.beta_out)
+        bt = t2n(q.beta)
+        out[f"{n}_beta_sha"] = np.array([RS.sha(bt)])
+        out[f"{n}_beta_sub"] = bt.reshape(-1)[RS.sub_idx(bt.size)]
+        with torch.no_grad():
+            out[f"{n}_what_hard_sha"] = np.array([RS.sha(t2n(q(m.weight)))])
+    return qms
+
+
+def gen_real_biascal(cases=("r18_layer4_0", "r18_layer1_0")):
+    """--bias_cal at the real shapes: the fused loop under _BiasCalAdam (alpha, gamma^z and
+    phi^z learned), 20 iterations, values / gradients / float64 truth at GRAD_STEPS."""
+    import realshape as RS
+    for case in cases:
+        out = {}
+        _real_fused(case, RS.calib_input(case), RS.ITERS, RS.GRAD_STEPS, True, out, keep_cached=False)
+        save(f"real_{case}_biascal", **out)
+
+
+def gen_long_horizon(case="r18_layer1_0"):
+    """The driver's horizon: 625 iterations of block_recon_fused_shiftedScale
+    (ShiftedScaleQuant.py:53-55; the b / b2 schedules end at iters and 3/4 iters,
+    layer_recon_fused_shiftedScale.py:246-250,382-399) on the ResNet-18 layer1.0 shape, as
+    shipped and with --bias_cal.  The FP block output is the one in real_<case>.npz
+    (checked by hash)."""
+    import realshape as RS
+    x = RS.calib_input(case)
+    for bias_cal in (False, True):
+        out = {}
+        _real_fused(case, x, RS.LONG_ITERS, RS.LONG_GRAD_STEPS, bias_cal, out, keep_cached=False)
+        save(f"long_{case}" + ("_biascal" if bias_cal else ""), **out)
+
+
 def gen_real_shapes(cases=None):
     """Reference-pinned parity at the real block shapes of configs 2-5 (realshape.CASES):
     the fused shifted-scale loop (block_recon_fused_shiftedScale, 20 iterations) and BRECQ's
@@ -1244,55 +1536,13 @@ def gen_real_shapes(cases=None):
     the packed sign bits that decide the hard rounding) and the hashes of the final hard
     weights."""
     import realshape as RS
-    from quant.channelQuant import ChannelQuant
-    shift = [31 / 32, 33 / 32, 1.0]
     for case in (cases or RS.CASES):
         kind, cin, cout, _ = RS.CASES[case]
         x = RS.calib_input(case)
         lay, ssha = _real_qnn(case)[1]
         out = {"layout": np.array(lay), "seed_sha": np.array([ssha])}
         # ---- fused shifted-scale loop
-        qnn, _ = _real_qnn(case)
-        block = qnn.model[0]
-        qnn.set_quant_state(True, False)
-        with torch.no_grad():
-            qnn(x)
-        qms = _named_qms(block)
-        out["qms"] = np.array([n for n, _ in qms])
-        for n, m in qms:
-            out[f"{n}_w_sha"] = np.array([RS.sha(t2n(m.org_weight))])
-            out[f"{n}_b_sha"] = np.array([RS.sha(t2n(m.org_bias))])
-            out[f"{n}_delta"] = t2n(m.weight_quantizer.delta.reshape(-1))
-            out[f"{n}_zp"] = t2n(m.weight_quantizer.zero_point.reshape(-1))
-            m.weight_quantizer = ChannelQuant(1.0, uaq=m.weight_quantizer, weight_tensor=m.org_weight.data,
-                                              shiftTarget=shift, name="." + n)
-            m.use_weight_quant = True
-            m.cache_features = "none"
-        qnn.set_quant_state(False, False)
-        with torch.no_grad():
-            fp = block(x)
-        out["cached_out"] = t2n(fp)
-        block.cached_inp_features, block.cached_out_features = [x.clone()], [fp.clone()]
-        MSM.set_quant_state_block(qnn, [".model.0"], "", True)
-        for n, m in qms:
-            out[f"{n}_beta0_sha"] = np.array([RS.sha(t2n(m.weight_quantizer.beta))]) \
-                if getattr(m.weight_quantizer, "beta", None) is not None else np.array([""])
-        torch.manual_seed(1005)
-        with _Spy(LRF.FusedScaleLossFunction) as spy:
-            with _GradSpy(RS.GRAD_STEPS, _fused_truth(block, spy, (0.01, 0.1), RS.ITERS)) as gspy:
-                res_loss = LRF.block_recon_fused_shiftedScale(block, RS.ITERS, (0.01, 0.1), qnn, None)
-        out["perms"] = np.stack([p.numpy() for p in spy.perms]).astype(np.int64)
-        out["rec_loss"] = np.array([r[0] for r in spy.rec], np.float64)
-        out["final_losses"] = np.array(res_loss, np.float64)
-        gspy.dump(out)      # alpha is [C_in, S] (per input channel): small, kept whole
-        for j, (n, m) in enumerate(qms):
-            q = m.weight_quantizer
-            out[f"{n}_alpha"] = t2n(q.alpha)
-            bt = t2n(q.beta)
-            out[f"{n}_beta_sha"] = np.array([RS.sha(bt)])
-            out[f"{n}_beta_sub"] = bt.reshape(-1)[RS.sub_idx(bt.size)]
-            with torch.no_grad():
-                out[f"{n}_what_hard_sha"] = np.array([RS.sha(t2n(q(m.weight)))])
+        _real_fused(case, x, RS.ITERS, RS.GRAD_STEPS, False, out)
         # ---- BRECQ AdaRound block reconstruction
         qnn, _ = _real_qnn(case)
         block = qnn.model[0]
@@ -1323,9 +1573,10 @@ def gen_real_shapes(cases=None):
 
 
 if __name__ == "__main__":
-    which = sys.argv[1:] or ["uaq", "channelquant", "adaround", "inpscale", "loss", "recon",
+    which = sys.argv[1:] or ["uaq", "channelquant", "adaround", "specials", "inpscale", "loss", "recon",
                              "layershift", "brecq", "blocks", "act", "layerfused", "blockshift", "driver",
-                             "wmse", "validate", "real"]
+                             "wmse", "validate", "real", "recon_biascal", "real_biascal", "long",
+                             "layerbrecq"]
     torch.set_num_threads(4)
     if "uaq" in which:
         gen_uaq()
@@ -1333,6 +1584,10 @@ if __name__ == "__main__":
         gen_channelquant()
     if "adaround" in which:
         gen_adaround()
+    if "specials" in which:
+        gen_uaq_specials()
+        gen_channelquant(specials=True)
+        gen_adaround(specials=True)
     if "inpscale" in which:
         gen_inpscale()
     if "loss" in which:
@@ -1359,3 +1614,11 @@ if __name__ == "__main__":
         gen_validate()
     if "real" in which:
         gen_real_shapes()
+    if "layerbrecq" in which:
+        gen_recon_layer_brecq()
+    if "recon_biascal" in which:
+        gen_recon_fused(bias_cal=True)
+    if "real_biascal" in which:
+        gen_real_biascal()
+    if "long" in which:
+        gen_long_horizon()

@@ -12,6 +12,9 @@ reference nor the package; the block classes are passed in by each side.
 Cases (reference file: the block's definition; the network position it is taken from):
   r18_layer4_0  ResNet-18 layer4.0  BasicBlock(256, 512, stride 2, 1x1 downsample)
                 models/resnet.py:22 / :260 (resnet18), input plane 8x8 (224-res: 14x14)
+  r18_layer1_0  ResNet-18 layer1.0  BasicBlock(64, 64, stride 1, no downsample): the
+                Co <= 64 wave-column alpha backward and the band weight-gradient shapes,
+                input plane 16x16 (224-res: 56x56)
   r50_layer1_0  ResNet-50 layer1.0  Bottleneck(64, 64, downsample 64 -> 256)
                 models/resnet.py:66, input plane 6x6 (224-res: 56x56)
   mbv2_960      MobileNetV2 features[16]  InvertedResidual(160, 160, 1, expand 6):
@@ -28,6 +31,7 @@ import torch.nn as nn
 
 CASES = {
     "r18_layer4_0": ("basic", 256, 512, 8),
+    "r18_layer1_0": ("basic1", 64, 64, 16),
     "r50_layer1_0": ("bottleneck", 64, 256, 6),
     "mbv2_960": ("inverted", 160, 160, 7),
     "rgx_g9": ("resbottleneck", 192, 432, 10),
@@ -36,6 +40,8 @@ N_CALI = 8
 ITERS = 20            # fused shifted-scale loop iterations
 BRECQ_ITERS = 10      # BRECQ AdaRound iterations
 GRAD_STEPS = (0, 5, ITERS - 1)
+LONG_ITERS = 625      # the driver's per-block horizon (ShiftedScaleQuant.py:53-55)
+LONG_GRAD_STEPS = (0, 125, 312, 469, 624)   # warm-up, both b schedules, the end
 BRECQ_GRAD_STEPS = (0, BRECQ_ITERS - 1)
 N_SUB = 8192          # sub-sampled entries of a full-size parameter / gradient
 WEIGHT_SEED, INPUT_SEED = 2024, 2025

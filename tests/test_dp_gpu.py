@@ -73,16 +73,23 @@ def _check_buckets(r0, r1):
     return [r0[f"rec{k}_reduced"] for k in range(n)]
 
 
-def test_fused_recon_world2_replicated(tmp_path):
+@pytest.mark.parametrize("bias_cal", [False, True])
+def test_fused_recon_world2_replicated(tmp_path, bias_cal):
+    """bias_cal: gamma^z / phi^z in the bucket too.  The deferred loss / gamma^z / phi^z
+    finalizes stay on at world 2: the backward kernels write alpha, gamma^z and phi^z straight
+    into their bucket slices (K.grads_into; counted by K.INTO_WRITES)."""
     from shiftedscalequantization_amd.quant._engine import SsqAdam
-    r0, r1 = _run_world2("fused", tmp_path)
+    r0, r1 = _run_world2("fused_bc" if bias_cal else "fused", tmp_path)
     reduced = _check_buckets(r0, r1)
     convs = ("conv1", "conv2", "downsample")
-    for n in convs:
-        np.testing.assert_array_equal(r0[n + "_alpha0"], r1[n + "_alpha0"])
-        np.testing.assert_array_equal(r0[n + "_alpha"], r1[n + "_alpha"])
+    keys = [(n, k) for n in convs for k in (("alpha", "gamma", "phi") if bias_cal else ("alpha",))]
+    for n, k in keys:
+        np.testing.assert_array_equal(r0[f"{n}_{k}0"], r1[f"{n}_{k}0"])
+        np.testing.assert_array_equal(r0[f"{n}_{k}"], r1[f"{n}_{k}"])
+    # every iteration after the bucket is built: one write per parameter, per rank
+    assert int(r0["into_writes"][0]) >= len(keys) * 2, int(r0["into_writes"][0])
     # single-process replay: Adam (lr 1e-3) fed the summed buckets from the same start
-    params = [torch.nn.Parameter(torch.as_tensor(r0[n + "_alpha0"]).cuda()) for n in convs]
+    params = [torch.nn.Parameter(torch.as_tensor(r0[f"{n}_{k}0"]).cuda()) for n, k in keys]
     opt = SsqAdam(params, lr=1e-3)
     sizes = [p.numel() for p in params]
     for flat in reduced:
@@ -90,9 +97,26 @@ def test_fused_recon_world2_replicated(tmp_path):
         for p, g in zip(params, parts):
             p.grad = torch.as_tensor(g).view_as(p).cuda()
         opt.step()
-    for n, p in zip(convs, params):
-        np.testing.assert_array_equal(p.detach().cpu().numpy(), r0[n + "_alpha"], err_msg=n)
+    for (n, k), p in zip(keys, params):
+        np.testing.assert_array_equal(p.detach().cpu().numpy(), r0[f"{n}_{k}"], err_msg=n + k)
     np.testing.assert_array_equal(r0["final_losses"] != r1["final_losses"], [True, True])
+    if bias_cal:
+        assert any(np.any(r0[f"{n}_gamma"] != 1.0) for n in convs)
+
+
+def test_fused_recon_world2_deferral_bit_identical(tmp_path):
+    """World 2 with bias_cal: the loop with the deferred finalizes writing into the bucket
+    and the loop finalizing each gradient by its own launch (DEFER_FINALIZE off) give
+    bit-identical buckets, parameters and losses."""
+    on = _run_world2("fused_bc", tmp_path)
+    off = _run_world2("fused_bc_nodefer", tmp_path)
+    assert int(on[0]["into_writes"][0]) > 0 and int(off[0]["into_writes"][0]) == 0
+    for a, b in zip(on, off):
+        assert int(a["n_rec"][0]) == int(b["n_rec"][0])
+        for k in a:
+            if k in ("into_writes",):
+                continue
+            np.testing.assert_array_equal(a[k], b[k], err_msg=k)
 
 
 def test_brecq_world2_replicated(tmp_path):

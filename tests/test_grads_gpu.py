@@ -54,31 +54,36 @@ def check(stats, got, g, prefix, steps, n_p):
     return worst
 
 
+@pytest.mark.parametrize("bias_cal", [False, True])
 @pytest.mark.parametrize("graph", [False, True])
-def test_a18_fused_block_gradients(Q, golden, graph):
+def test_a18_fused_block_gradients(Q, golden, graph, bias_cal):
+    """bias_cal=True: against recon_fused_biascal.npz, the reference run with its commented
+    gamma^z / phi^z opt_params lines realised (make_golden._BiasCalAdam): alpha, gamma^z and
+    phi^z of every conv forced and their gradients checked (9 tensors)."""
     from test_recon_gpu import build_qnn, load_block
     import importlib
     LRF = importlib.import_module("shiftedscalequantization_amd.quant.layer_recon_fused_shiftedScale")
     E = importlib.import_module("shiftedscalequantization_amd.quant._engine")
-    g = golden("recon_fused")
+    g = golden("recon_fused_biascal" if bias_cal else "recon_fused")
     qnn = build_qnn(Q, {})
     block = qnn.model[3]
     load_block(Q, g, block)
     block.cached_inp_features = [dev(g["cached_inp"])]
     block.cached_out_features = [dev(g["cached_out"])]
-    steps, force = forced(g, "", 3)
+    n_p = 9 if bias_cal else 3
+    steps, force = forced(g, "", n_p)
     probe, got, before = grad_recorder(steps, force)
     E.ITER_PROBE[0] = probe
     try:
         torch.manual_seed(1005)
         LRF.block_recon_fused_shiftedScale(block, int(g["iters"][0]), (0.01, 0.1), qnn, None,
-                                           verbose=False, graph=graph)
+                                           verbose=False, graph=graph, bias_cal=bias_cal)
     finally:
         E.ITER_PROBE[0] = None
-    stats = {"init_dev": max(np.abs(before[0][j] - force[0][j]).max() for j in range(3))}
-    worst = check(stats, got, g, "", steps, 3)
+    stats = {"init_dev": max(np.abs(before[0][j] - force[0][j]).max() for j in range(n_p))}
+    worst = check(stats, got, g, "", steps, n_p)
     stats["worst_grad_over_bound"] = worst
-    parity_report(f"a18_grad[graph={graph}]", **stats)
+    parity_report(f"a18_grad[graph={graph},bias_cal={bias_cal}]", **stats)
     # iteration 0 starts from our own init_v_beta: the reference's alpha to an ulp or two
     # (its log / softmax-inverse evaluated on the device)
     assert stats["init_dev"] <= INIT_TOL

@@ -64,6 +64,63 @@ def test_uaq_golden(K, golden):
         close(host(zz.grad).reshape(-1), g[t + "_gzp"], rtol=1e-4, atol=1e-4)
 
 
+def test_uaq_specials_golden(K, golden):
+    """NaN / +-inf / +-0 / +-3e38 inputs against the reference (uaq_specials.npz): torch.clamp
+    keeps NaN and round_ste turns an infinite x/delta into NaN, so the dequant is NaN there;
+    every other output and gx bit for bit, the reductions within the usual tolerance (NaN
+    where the reference's sum is NaN).  Per-tensor (float4 stream), per-channel (LDS tile
+    kernel), the multi-tensor table, and ChannelQuantAct's torch.round q/dq."""
+    g = golden("uaq_specials")
+    for t in [k for k in tags(g, "_gdelta") if not k.startswith("act_")]:
+        bits = int(t.split("_")[0][1:])
+        sym = "_sym_" in t
+        cw = "_cw_" in t
+        x = g[t + "_x"]
+        shape = (-1,) + (1,) * (x.ndim - 1) if cw else (1,)
+        d, z = dev(g[t + "_delta"].reshape(shape)), dev(g[t + "_zp"].reshape(shape))
+        y, _ = K.fake_quant_fwd(dev(x), d, z, bits, sym)
+        np.testing.assert_array_equal(host(y), g[t + "_y"], err_msg=t)
+        assert np.isnan(host(y)).sum() == np.isnan(g[t + "_y"]).sum() > np.isnan(x).sum(), t
+        if cw:
+            ym = K.fake_quant_multi([dev(x)], [d], [z], bits, sym)[0]
+            np.testing.assert_array_equal(host(ym), g[t + "_y"], err_msg=t)
+        xr, dd, zz = dev(x).requires_grad_(True), d.clone().requires_grad_(True), z.clone().requires_grad_(True)
+        K.fake_quant(xr, dd, zz, bits, sym).backward(dev(g[t + "_gy"]))
+        np.testing.assert_array_equal(host(xr.grad), g[t + "_gx"], err_msg=t)
+        close(host(dd.grad).reshape(-1), g[t + "_gdelta"], rtol=1e-4, atol=1e-4)
+        close(host(zz.grad).reshape(-1), g[t + "_gzp"], rtol=1e-4, atol=1e-4)
+        np.testing.assert_array_equal(np.isnan(host(dd.grad).reshape(-1)), np.isnan(g[t + "_gdelta"]))
+    x = g["b4_asym_pt_mse_x"]
+    d, z = dev(g["b4_asym_pt_mse_delta"]), dev(g["b4_asym_pt_mse_zp"])
+    for k in (0, 1):
+        dd, zz = d.clone().requires_grad_(True), z.clone().requires_grad_(True)
+        ya = K.round_quant(dev(x), dd, zz, 4, False, scale=float(g[f"act_s{k}_scale"][0]))
+        np.testing.assert_array_equal(host(ya), g[f"act_s{k}_y"], err_msg=f"act_s{k}")
+        ya.backward(dev(g["b4_asym_pt_mse_gy"]))
+        close(host(dd.grad).reshape(-1), g[f"act_s{k}_gdelta"], rtol=1e-4, atol=1e-4)
+        close(host(zz.grad).reshape(-1), g[f"act_s{k}_gzp"], rtol=1e-4, atol=1e-4)
+
+
+@pytest.mark.parametrize("relu", [0, 1, 2])
+def test_bias_act_quant_specials_vs_oracle(K, relu):
+    """The fused epilogue's act q/dq (K13 + K1 in one pass, forward and the fused tail's
+    recompute) on NaN / +-inf / huge pre-activations: the act quantizer's round_ste and
+    torch.clamp semantics, bit for bit against the oracle applied to bias_act's output."""
+    gen = torch.Generator().manual_seed(31 + relu)
+    shape = (4, 8, 7, 7)
+    y = torch.randn(shape, generator=gen).cuda() * 4
+    y.view(-1)[:8] = torch.tensor([float("nan"), float("inf"), -float("inf"), 3e38, -3e38,
+                                   -0.0, 0.0, 6.0])
+    b = torch.randn(shape[1], generator=gen).cuda()
+    d, z = torch.tensor([0.21]).cuda(), torch.tensor([3.0]).cuda()
+    with torch.no_grad():
+        a = K.bias_act_quant(y, b, None, relu, d, z, 4)
+        pre = K.bias_act(y, b, None, relu)
+    ref, _ = R.fake_quant(host(pre), np.float32(0.21), np.float32(3.0), 4)
+    np.testing.assert_array_equal(host(a).view(np.int32), ref.view(np.int32))
+    assert np.isnan(ref).any()
+
+
 def test_uaq_zero_range(K, golden):
     g = golden("uaq")
     x = dev(g["zero_x"])
@@ -258,11 +315,16 @@ def _cq(g, tag):
 
 
 CQ_TAGS = ["conv_b2", "conv_b4", "fc_b2", "fc_b4", "dw_b2", "dw_b4"]
+# channelquant_specials: the same cases with NaN / +-inf / +-0 / +-3e38 planted into W after
+# the scale init (make_golden.SPECIALS): NaN wherever the reference gives NaN, the rest as
+# before (assert_array_equal / assert_allclose compare NaN positions as equal)
+CQ_FILES = ["channelquant", "channelquant_specials"]
 
 
+@pytest.mark.parametrize("fname", CQ_FILES)
 @pytest.mark.parametrize("tag", CQ_TAGS)
-def test_shift_init_golden(K, golden, tag):
-    g = golden("channelquant")
+def test_shift_init_golden(K, golden, tag, fname):
+    g = golden(fname)
     w, is_fc, d, z, bits = _cq(g, tag)
     alpha, beta, _ = K.shift_init(dev(w), dev(d), SHIFTS)
     close(host(alpha), g[tag + "_alpha0"], rtol=1e-5, atol=1e-6)
@@ -270,9 +332,10 @@ def test_shift_init_golden(K, golden, tag):
     np.testing.assert_array_equal(host(beta) >= 0, g[tag + "_beta"] >= 0)
 
 
+@pytest.mark.parametrize("fname", CQ_FILES)
 @pytest.mark.parametrize("tag", CQ_TAGS)
-def test_adashift_golden(K, golden, tag):
-    g = golden("channelquant")
+def test_adashift_golden(K, golden, tag, fname):
+    g = golden(fname)
     w, is_fc, d, z, bits = _cq(g, tag)
     alpha, beta = g[tag + "_alpha"], g[tag + "_beta"]
     np.testing.assert_array_equal(host(K.get_delta(dev(d), dev(alpha), SHIFTS, w.shape)),
@@ -294,12 +357,15 @@ def test_adashift_golden(K, golden, tag):
     y, codes = K.adashift_codes(dev(alpha), dev(beta), dev(w), dev(d), dev(z), SHIFTS, bits, False)
     np.testing.assert_array_equal(host(y), g[tag + "_t1r1_y"])
     c = codes.cpu().numpy().astype(np.float32)
-    np.testing.assert_array_equal((c - z) * d, g[tag + "_t1r1_y"])   # What = (q - zp) * delta
+    ref = g[tag + "_t1r1_y"]
+    ok = ~np.isnan(ref)                 # a NaN weight has no integer code
+    np.testing.assert_array_equal(((c - z) * d)[ok], ref[ok])   # What = (q - zp) * delta
 
 
+@pytest.mark.parametrize("fname", CQ_FILES)
 @pytest.mark.parametrize("tag", CQ_TAGS)
-def test_lhs_adaround_golden(K, golden, tag):
-    g = golden("channelquant")
+def test_lhs_adaround_golden(K, golden, tag, fname):
+    g = golden(fname)
     w, is_fc, d, z, bits = _cq(g, tag)
     alpha = g[tag + "_lhs_alpha"]
     a = dev(alpha).requires_grad_(True)
@@ -322,9 +388,10 @@ def test_lhs_adaround_golden(K, golden, tag):
     close(host(b.grad), g[tag + "_ar_r0_gbeta"], rtol=1e-4, atol=1e-7)
 
 
+@pytest.mark.parametrize("fname", ["adaround", "adaround_specials"])
 @pytest.mark.parametrize("name", ["conv", "fc"])
-def test_adaround_quantizer_golden(K, golden, name):
-    g = golden("adaround")
+def test_adaround_quantizer_golden(K, golden, name, fname):
+    g = golden(fname)
     w = g[name + "_w"]
     shape = (-1, 1) if w.ndim == 2 else (-1, 1, 1, 1)
     d, z = g[name + "_delta"].reshape(shape), g[name + "_zp"].reshape(shape)

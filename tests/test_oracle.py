@@ -65,6 +65,35 @@ def test_uaq_backward(golden):
         close(np.reshape(gz, -1), g[t + "_gzp"], rtol=1e-4, atol=1e-4)
 
 
+def test_uaq_specials(golden):
+    """NaN / +-inf / +-0 / +-3e38 inputs (uaq_specials.npz): NaN where the reference gives
+    NaN (torch.clamp keeps NaN; round_ste turns an infinite x/delta into NaN), every other
+    value bit for bit; ChannelQuantAct 'none' (torch.round) clamps +-inf to an edge."""
+    g = golden("uaq_specials")
+    for t in tags(g, "_gdelta"):
+        if t.startswith("act_"):
+            continue
+        bits = int(t.split("_")[0][1:])
+        sym = "_sym_" in t
+        x = g[t + "_x"]
+        shape = (-1,) + (1,) * (x.ndim - 1) if "_cw_" in t else ()
+        d, z = g[t + "_delta"].reshape(shape), g[t + "_zp"].reshape(shape)
+        y, _ = R.fake_quant(x, d, z, bits, sym)
+        np.testing.assert_array_equal(y, g[t + "_y"], err_msg=t)
+        assert np.isnan(y).sum() > np.isnan(x).sum(), t          # the infinities too
+        gx, gd, gz = R.fake_quant_bwd(x, d, z, bits, sym, g[t + "_gy"])
+        np.testing.assert_array_equal(gx, g[t + "_gx"], err_msg=t)
+        close(np.reshape(gd, -1), g[t + "_gdelta"], rtol=1e-4, atol=1e-4)
+        close(np.reshape(gz, -1), g[t + "_gzp"], rtol=1e-4, atol=1e-4)
+    x = g["b4_asym_pt_mse_x"]
+    for k in (0, 1):
+        sc = float(g[f"act_s{k}_scale"][0])
+        d = np.float32(g["b4_asym_pt_mse_delta"][0]) * np.float32(sc)
+        y, _ = R.fake_quant(x, d, g["b4_asym_pt_mse_zp"][0], 4, False, ste=False)
+        np.testing.assert_array_equal(y, g[f"act_s{k}_y"])
+        assert np.isnan(y).sum() == np.isnan(x).sum()
+
+
 # ------------------------------------------------------------------ ChannelQuant (K5-K9)
 SHIFTS = [31 / 32, 33 / 32, 1.0]
 
@@ -79,9 +108,13 @@ def _cq_setup(g, tag):
     return w, is_fc, d, z, bits
 
 
+CQ_FILES = ["channelquant", "channelquant_specials"]   # _specials: NaN / +-inf / +-0 in W
+
+
+@pytest.mark.parametrize("fname", CQ_FILES)
 @pytest.mark.parametrize("tag", ["conv_b2", "conv_b4", "fc_b2", "fc_b4", "dw_b2", "dw_b4"])
-def test_channelquant_init_v_beta(golden, tag):
-    g = golden("channelquant")
+def test_channelquant_init_v_beta(golden, tag, fname):
+    g = golden(fname)
     w, is_fc, d, z, bits = _cq_setup(g, tag)
     xq, alpha, beta = R.init_v_beta(w, d, SHIFTS)
     np.testing.assert_array_equal(np.stack(xq), g[tag + "_xq"])
@@ -91,9 +124,10 @@ def test_channelquant_init_v_beta(golden, tag):
     np.testing.assert_array_equal(beta >= 0, g[tag + "_beta"] >= 0)
 
 
+@pytest.mark.parametrize("fname", CQ_FILES)
 @pytest.mark.parametrize("tag", ["conv_b2", "conv_b4", "fc_b2", "fc_b4", "dw_b2", "dw_b4"])
-def test_channelquant_adashift(golden, tag):
-    g = golden("channelquant")
+def test_channelquant_adashift(golden, tag, fname):
+    g = golden(fname)
     w, is_fc, d, z, bits = _cq_setup(g, tag)
     xq = list(g[tag + "_xq"])
     alpha, beta = g[tag + "_alpha"], g[tag + "_beta"]
@@ -114,9 +148,10 @@ def test_channelquant_adashift(golden, tag):
                 close(gb, g[k + "_gbeta"], rtol=1e-4, atol=1e-7)
 
 
+@pytest.mark.parametrize("fname", CQ_FILES)
 @pytest.mark.parametrize("tag", ["conv_b2", "conv_b4", "fc_b2", "fc_b4", "dw_b2", "dw_b4"])
-def test_channelquant_lhs_and_adaround(golden, tag):
-    g = golden("channelquant")
+def test_channelquant_lhs_and_adaround(golden, tag, fname):
+    g = golden(fname)
     w, is_fc, d, z, bits = _cq_setup(g, tag)
     xq, alpha0 = R.init_v(w, d, z, bits, False, SHIFTS)
     np.testing.assert_array_equal(np.stack(xq), g[tag + "_lhs_xq"])
@@ -137,9 +172,10 @@ def test_channelquant_lhs_and_adaround(golden, tag):
     np.testing.assert_array_equal(R.none_fwd(w, dsel, z, bits, False), g[tag + "_none_y"])
 
 
+@pytest.mark.parametrize("fname", ["adaround", "adaround_specials"])
 @pytest.mark.parametrize("name", ["conv", "fc"])
-def test_adaround_quantizer(golden, name):
-    g = golden("adaround")
+def test_adaround_quantizer(golden, name, fname):
+    g = golden(fname)
     w = g[name + "_w"]
     shape = (-1, 1) if w.ndim == 2 else (-1, 1, 1, 1)
     d, z = g[name + "_delta"].reshape(shape), g[name + "_zp"].reshape(shape)

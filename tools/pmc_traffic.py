@@ -44,5 +44,8 @@ for tag in KERNELS:
     res[tag] = {"launches": [len(fetch[tag]), len(write[tag])], "FETCH_SIZE_KiB_median": f,
                 "WRITE_SIZE_KiB_median": w, "hbm_bytes_per_launch": (2.0 * f + w) * 1024.0,
                 "correction": "read side doubled (gfx950 FETCH_SIZE = 1/2 of wide streaming reads)"}
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+from shiftedscalequantization_amd.build import provenance  # noqa: E402
+res["provenance"] = provenance()
 json.dump(res, open(sys.argv[3], "w"), indent=1)
 print(json.dumps(res, indent=1))

@@ -32,6 +32,7 @@ as conv time, outside the HBM set.  Writes the JSON that bench.py reports as
 import collections
 import csv
 import json
+import os
 import re
 import sys
 
@@ -156,6 +157,9 @@ def analyse(path, warmup=20):
 
 if __name__ == "__main__":
     res = analyse(sys.argv[1])
+    sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+    from shiftedscalequantization_amd.build import provenance
+    res["provenance"] = provenance()
     txt = json.dumps(res, indent=1)
     if len(sys.argv) > 2:
         with open(sys.argv[2], "w") as f:
