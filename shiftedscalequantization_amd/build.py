@@ -89,10 +89,13 @@ def build(force=False, verbose=True):
                 print(f"[ssq build] compiled {os.path.basename(s)}")
     objs = [os.path.join(OBJ, s.replace(".hip", ".o")) for s in SOURCES]
     if force or jobs or _stale(LIB, objs):
-        cmd = [hipcc, f"--offload-arch={ARCH}", "-shared", "-fPIC", "-o", LIB] + objs
+        # link beside, then rename: a reader (or a tree snapshot) never sees a partial file
+        tmp = LIB + ".tmp"
+        cmd = [hipcc, f"--offload-arch={ARCH}", "-shared", "-fPIC", "-o", tmp] + objs
         r = subprocess.run(cmd, capture_output=True, text=True)
         if r.returncode != 0:
             raise RuntimeError(f"link failed:\n{r.stderr}")
+        os.replace(tmp, LIB)
         if verbose:
             print(f"[ssq build] linked {LIB}")
     return LIB

@@ -112,7 +112,7 @@ constexpr uint32_t kWR = 16;   // rows per wave (whole form: Co <= 4 * kWR = 64)
 // parallel) and at most one wave-width of chunks.  SSQ_K6P_FORM selects the form for A/B
 // (0: stage 1 + stage 2, 1: wave-column for Co <= 64 else form 0, 2: one launch).
 constexpr uint32_t kMaxTicketBlk = 256;          // column blocks per segment (form 2)
-constexpr uint32_t kOneStage = 4096;             // form 2: partial doubles staged in LDS (32 KiB)
+constexpr uint32_t kMaxOneChunks = 16;           // form 2: row chunks per column block
 __device__ unsigned g_k6p_tickets[kMaxPrepSeg * kMaxTicketBlk];
 
 static ColTiling bwd_tiling_onelaunch(const Geo& g) {
@@ -121,9 +121,8 @@ static ColTiling bwd_tiling_onelaunch(const Geo& g) {
   ColTiling t = col_tiling_prep(g);
   uint32_t want = (kWgs + t.ncolblk - 1) / t.ncolblk;
   const uint32_t by_rows = (g.Co + kRows - 1) / kRows;
-  const uint32_t by_lds = kOneStage / (t.ncb * kMaxPrepS);   // a block's partials fit the stage
   if (want > by_rows) want = by_rows;
-  if (want > by_lds) want = by_lds;
+  if (want > kMaxOneChunks) want = kMaxOneChunks;
   if (want < 1) want = 1;
   t.R = (g.Co + want - 1) / want;
   t.nchunk = (g.Co + t.R - 1) / t.R;
@@ -131,9 +130,36 @@ static ColTiling bwd_tiling_onelaunch(const Geo& g) {
   return t;
 }
 
+// Form 3 (r4): one workgroup per input channel, for weights with Co*K <= kChanElems (every
+// ResNet-18 conv but layer4's 3x3: 4608).  Its 256 threads take the channel's Co*K
+// (row, tap) elements -- thread t: elements t, t + 256, ... (<= 9), every load issued before
+// any math -- and reduce them in the workgroup (fixed shuffle tree per wave, then the 4
+// waves in order): one launch, no partials, and as many workgroups as input channels.  The
+// wave-column form puts a whole column block on one CU (10 workgroups for a layer1 conv):
+// its time is the few CUs' load bandwidth, not latency.
+constexpr uint32_t kChanPer = 9;                      // elements per thread
+constexpr uint32_t kChanElems = kChanPer * kBlock;    // 2304
+
 static ColTiling bwd_tiling_prep(const Geo& g) {
-  static const uint32_t kForm = prep_env("SSQ_K6P_FORM", 1);
+  // SSQ_K6P_FORM (A/B): 3 = form 3 where it fits, else form 0 (default); 1 = the wave-column
+  // form where it fits, else form 0; 0 = stage 1 + stage 2 everywhere; 2 = one launch with
+  // the last-arriver reduction
+  static const uint32_t kForm = prep_env("SSQ_K6P_FORM", 3);
   constexpr uint32_t kMaxR = (kBlock / kWave) * kWR;
+  if (kForm == 3) {
+    if (g.Co * g.K <= kChanElems) {
+      ColTiling t;
+      t.form = 3;
+      t.threads = kBlock;
+      t.ncb = 1;
+      t.ncolblk = g.Ci;
+      t.R = g.Co;
+      t.nchunk = 1;
+      t.whole = 1;
+      return t;
+    }
+    return col_tiling_prep(g);
+  }
   if (kForm == 2) {
     const ColTiling t = bwd_tiling_onelaunch(g);
     if (t.ncolblk <= kMaxTicketBlk) return t;
@@ -168,6 +194,7 @@ struct PrepSeg {
   uint32_t wave0;    // first wave of this segment (stage 2: one wave per input channel)
   uint32_t stage2;   // its chunks are reduced by the stage-2 launch
   uint32_t ticket0;  // form 2: its column blocks' ticket counters start here
+  FastDiv divK;      // form 3: (row, tap) of a flat element index
   float lo, hi;
   float* alpha_w;    // fused optimizer step (ssq_adam_arm): alpha, its Adam m / v (or null)
   float* am;
@@ -448,50 +475,169 @@ __device__ __forceinline__ void alpha_bwd_wavecol(const PrepSeg& sg, const AdamC
   if (fin_lane) alpha_finalize<NS>(sg, ac, ci0 + lane, af, tot, reg_lambda, reg_b);
 }
 
-// Form 2's in-launch stage 2 (run by the last arriving workgroup of a column block): the
-// block's chunk partials -- one contiguous run, part[(ci*nchunk + chunk)*S + i] -- are staged
-// in LDS by one coalesced pass (write-through loads), thread (ci, i) adds its nchunk values in
-// chunk order, and thread ci finalises the channel (regulariser, softmax / clamp backward,
-// the armed Adam step).  One global round trip, then LDS.
+// Form 3: input channel ci of the segment in one workgroup (see bwd_tiling_prep).
+template <int NS>
+__device__ __forceinline__ void alpha_bwd_channel(const PrepSeg& sg, const AdamConst& ac,
+                                                  uint32_t ci, double* red, float reg_lambda,
+                                                  float reg_b, const float* __restrict__ reg_dev) {
+  const Geo& g = sg.g;
+  const uint32_t n = g.Co * g.K, t = threadIdx.x;
+  const uint32_t lane = t & (kWave - 1), w = t / kWave;
+  float a[kMaxS];
+  load_row(sg.alpha, ci, NS, a);
+  float pp[kMaxS], pm[kMaxS], pv[kMaxS];
+  const bool fin = t == 0;
+  if (fin && sg.am) {                 // the armed Adam state, loaded with everything else
+#pragma unroll
+    for (int i = 0; i < NS; ++i) {
+      pp[i] = sg.alpha_w[(size_t)ci * NS + i];
+      pm[i] = sg.am[(size_t)ci * NS + i];
+      pv[i] = sg.av[(size_t)ci * NS + i];
+    }
+  }
+  if (reg_dev) {
+    reg_lambda = reg_dev[0];
+    reg_b = reg_dev[1];
+  }
+  uint32_t fw[kChanPer];
+  float h[kChanPer], gy[kChanPer], d[kChanPer], z[kChanPer];
+#pragma unroll
+  for (uint32_t e = 0; e < kChanPer; ++e) {
+    const uint32_t f = t + e * kBlock;
+    fw[e] = 0u;
+    h[e] = gy[e] = d[e] = z[e] = 0.0f;
+    if (f < n) {
+      const uint32_t co = fdiv(f, sg.divK);
+      const uint32_t idx = co * g.CiK + ci * g.K + (f - co * g.K);
+      fw[e] = sg.fpack[idx];
+      h[e] = sg.hterm[idx];
+      gy[e] = sg.gWhat[idx];
+      d[e] = sg.delta[co];
+      z[e] = sg.zp[co];
+    }
+  }
+  float p[kMaxS];
+  soft_targets<kMaxS>(a, NS, nullptr, p);
+  double acc[NS];
+#pragma unroll
+  for (int i = 0; i < NS; ++i) acc[i] = 0.0;
+#pragma unroll
+  for (uint32_t e = 0; e < kChanPer; ++e)
+    if (t + e * kBlock < n) alpha_accumulate<NS>(fw[e], h[e], d[e], z[e], gy[e], p, sg.lo, sg.hi, acc);
+#pragma unroll
+  for (int i = 0; i < NS; ++i) acc[i] = wave_sum(acc[i]);
+  if (lane == 0) {
+#pragma unroll
+    for (int i = 0; i < NS; ++i) red[w * NS + i] = acc[i];
+  }
+  __syncthreads();
+  if (!fin) return;
+  double tot[kMaxS];
+#pragma unroll
+  for (int i = 0; i < NS; ++i) {
+    double s = red[i];
+#pragma unroll
+    for (int k = 1; k < kBlock / kWave; ++k) s += red[k * NS + i];
+    tot[i] = s;
+  }
+  float sm[kMaxS], ga[kMaxS];
+  soft_targets<kMaxS>(a, NS, sm, p);
+  float reg = 0.0f;
+  if (reg_lambda != 0.0f) {
+    double racc = 0.0;
+#pragma unroll
+    for (int i = 0; i < NS; ++i) {
+      double rv, rg;
+      reg_term(p[i], reg_lambda, reg_b, 0, rv, rg);
+      racc += rv;
+      tot[i] += rg;
+    }
+    reg = (float)((double)reg_lambda * racc);
+  }
+  softmax_clamp_bwd(sm, NS, tot, ga);
+#pragma unroll
+  for (int i = 0; i < NS; ++i) sg.galpha[(size_t)ci * NS + i] = ga[i];
+  if (sg.reg_vals) sg.reg_vals[ci] = reg;
+  if (sg.am) {
+    const AdamRef r{sg.alpha_w, sg.am, sg.av};
+#pragma unroll
+    for (int i = 0; i < NS; ++i)
+      adam_apply_loaded(ac, r, (uint32_t)(ci * NS + i), ga[i], pp[i], pm[i], pv[i]);
+  }
+}
+
+// Form 2's in-launch stage 2 (run by the last arriving workgroup of a column block): thread
+// c takes input channel ci0 + c; every load it needs -- the alpha row, the armed Adam state,
+// the channel's nchunk partials (one contiguous run, write-through loads) -- is issued before
+// any math; the partials are added in chunk order and the channel finalised (regulariser,
+// softmax / clamp backward, the Adam step): one global round trip.
 template <int NS>
 __device__ __forceinline__ void alpha_reduce_chunks(const PrepSeg& sg, const AdamConst& ac,
-                                                    uint32_t ci0, uint32_t nci, double* stage,
-                                                    double* red, float reg_lambda, float reg_b,
-                                                    const float* __restrict__ reg_dev) {
+                                                    uint32_t ci0, uint32_t nci, float reg_lambda,
+                                                    float reg_b, const float* __restrict__ reg_dev) {
   const uint32_t nchunk = sg.tl.nchunk;
-  const uint32_t n = nci * nchunk * NS;
-  const double* src = sg.part + (size_t)ci0 * nchunk * NS;
-  constexpr uint32_t kPer = (kOneStage + kBlock - 1) / kBlock;
-  double v[kPer];
-#pragma unroll
-  for (uint32_t r = 0; r < kPer; ++r) {
-    const uint32_t k = threadIdx.x + r * kBlock;
-    v[r] = k < n ? ld_sc1(src + k) : 0.0;
-  }
-#pragma unroll
-  for (uint32_t r = 0; r < kPer; ++r) {
-    const uint32_t k = threadIdx.x + r * kBlock;
-    if (k < n) stage[k] = v[r];
-  }
-  __syncthreads();
-  for (uint32_t pr = threadIdx.x; pr < nci * NS; pr += kBlock) {
-    const uint32_t c = pr / NS, i = pr - c * NS;
-    double sum = 0.0;
-    for (uint32_t k = 0; k < nchunk; ++k) sum += stage[(c * nchunk + k) * NS + i];
-    red[pr] = sum;
-  }
-  __syncthreads();
   if (reg_dev) {
     reg_lambda = reg_dev[0];
     reg_b = reg_dev[1];
   }
   for (uint32_t c = threadIdx.x; c < nci; c += kBlock) {
-    float a[kMaxS];
-    load_row(sg.alpha, ci0 + c, NS, a);
+    const uint32_t ci = ci0 + c;
+    float a[kMaxS], pp[kMaxS], pm[kMaxS], pv[kMaxS];
+    load_row(sg.alpha, ci, NS, a);
+    if (sg.am) {
+#pragma unroll
+      for (int i = 0; i < NS; ++i) {
+        pp[i] = sg.alpha_w[(size_t)ci * NS + i];
+        pm[i] = sg.am[(size_t)ci * NS + i];
+        pv[i] = sg.av[(size_t)ci * NS + i];
+      }
+    }
+    const double* src = sg.part + (size_t)ci * nchunk * NS;
+    constexpr uint32_t kB = 8;       // chunks per load batch (registers of the host kernel)
     double tot[kMaxS];
 #pragma unroll
-    for (int i = 0; i < NS; ++i) tot[i] = red[c * NS + i];
-    alpha_finalize<NS>(sg, ac, ci0 + c, a, tot, reg_lambda, reg_b);
+    for (int i = 0; i < NS; ++i) tot[i] = 0.0;
+    for (uint32_t k0 = 0; k0 < nchunk; k0 += kB) {
+      double v[kB][NS];
+#pragma unroll
+      for (uint32_t k = 0; k < kB; ++k)
+#pragma unroll
+        for (int i = 0; i < NS; ++i)
+          v[k][i] = k0 + k < nchunk ? ld_sc1(src + (k0 + k) * NS + i) : 0.0;
+#pragma unroll
+      for (int i = 0; i < NS; ++i) {
+        double t = k0 == 0 ? v[0][i] : tot[i] + v[0][i];
+#pragma unroll
+        for (uint32_t k = 1; k < kB; ++k)
+          if (k0 + k < nchunk) t += v[k][i];
+        tot[i] = t;
+      }
+    }
+    // alpha_finalize with the Adam state already loaded
+    float sm[kMaxS], p[kMaxS], ga[kMaxS];
+    soft_targets<kMaxS>(a, NS, sm, p);
+    float reg = 0.0f;
+    if (reg_lambda != 0.0f) {
+      double racc = 0.0;
+#pragma unroll
+      for (int i = 0; i < NS; ++i) {
+        double rv, rg;
+        reg_term(p[i], reg_lambda, reg_b, 0, rv, rg);
+        racc += rv;
+        tot[i] += rg;
+      }
+      reg = (float)((double)reg_lambda * racc);
+    }
+    softmax_clamp_bwd(sm, NS, tot, ga);
+#pragma unroll
+    for (int i = 0; i < NS; ++i) sg.galpha[(size_t)ci * NS + i] = ga[i];
+    if (sg.reg_vals) sg.reg_vals[ci] = reg;
+    if (sg.am) {
+      const AdamRef r{sg.alpha_w, sg.am, sg.av};
+#pragma unroll
+      for (int i = 0; i < NS; ++i)
+        adam_apply_loaded(ac, r, (uint32_t)(ci * NS + i), ga[i], pp[i], pm[i], pv[i]);
+    }
   }
 }
 
@@ -516,6 +662,10 @@ __global__ __launch_bounds__(kBlock) void alpha_bwd_prep(PrepTable tab, float re
   const uint32_t local = bid - sg.blk0;
   if (sg.tl.form == 1) {             // uniform per workgroup
     alpha_bwd_wavecol<NS>(sg, tab.ac, local, red, reg_lambda, reg_b, reg_dev);
+    return;
+  }
+  if (sg.tl.form == 3) {
+    alpha_bwd_channel<NS>(sg, tab.ac, local, red, reg_lambda, reg_b, reg_dev);
     return;
   }
   const uint32_t bx = local % sg.tl.ncolblk, by = local / sg.tl.ncolblk;
@@ -592,8 +742,7 @@ __global__ __launch_bounds__(kBlock) void alpha_bwd_prep(PrepTable tab, float re
   if (!onel) return;
   // form 2: the last workgroup of this column block reduces its chunks and finalises
   if (!arrive_last(&g_k6p_tickets[sg.ticket0 + bx], sg.tl.nchunk, (int*)red)) return;
-  extern __shared__ double stage[];
-  alpha_reduce_chunks<NS>(sg, tab.ac, ci0, nci, stage, red, reg_lambda, reg_b, reg_dev);
+  alpha_reduce_chunks<NS>(sg, tab.ac, ci0, nci, reg_lambda, reg_b, reg_dev);
 }
 
 // Stage 2 (thread-column segments): one wave per (segment, input channel).  Every load the wave needs (alpha row, the device (lambda, b)
@@ -707,6 +856,7 @@ static int make_seg(const SegArgs& a, int i, PrepSeg& sg, const char* what) {
   sg.reg_vals = nullptr;
   sg.alpha_w = sg.am = sg.av = nullptr;
   sg.ticket0 = 0;
+  sg.divK = make_fastdiv(sg.g.K);
   sg.tl = col_tiling_prep(sg.g);
   sg.lo = (float)a.qmin[i];
   sg.hi = (float)a.qmax[i];
@@ -921,10 +1071,7 @@ extern "C" int ssq_adashift_bwd_prepared_multi(
       if (sg.stage2) waves += sg.g.Ci;
     }
     const unsigned blocks2 = (waves + kBlock / kWave - 1) / (kBlock / kWave);
-    // form 2 segments stage a column block's partials in dynamic LDS
-    size_t shm = 0;
-    for (int k = 0; k < tab.nseg; ++k)
-      if (tab.s[k].tl.form == 2) shm = kOneStage * sizeof(double);
+    const size_t shm = 0;
     // queued finalize tasks of this stream ride on the first launch (their inputs live in
     // their producers' own workspace slots, not in this one)
     FinTable fin{};

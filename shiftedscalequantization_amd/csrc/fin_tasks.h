@@ -45,16 +45,20 @@ struct AdamRef {
   float* m;
   float* v;
 };
-__device__ __forceinline__ void adam_apply(const AdamConst& c, const AdamRef& r, uint32_t e,
-                                           float g) {
+// the update of one entry from its loaded (p, m, v)
+__device__ __forceinline__ void adam_apply_loaded(const AdamConst& c, const AdamRef& r, uint32_t e,
+                                                  float g, float p, float m, float v) {
   const float nss = c.hyper[0], bc2s = c.hyper[1];
-  float m = r.m[e], v = r.v[e];
   m = __fadd_rn(m, __fmul_rn(c.w1, __fsub_rn(g, m)));
   v = __fadd_rn(__fmul_rn(v, c.b2), __fmul_rn(__fmul_rn(c.w2, g), g));
   const float denom = __fadd_rn(__fdiv_rn(__fsqrt_rn(v), bc2s), c.eps);
-  r.p[e] = __fadd_rn(r.p[e], __fdiv_rn(__fmul_rn(nss, m), denom));
+  r.p[e] = __fadd_rn(p, __fdiv_rn(__fmul_rn(nss, m), denom));
   r.m[e] = m;
   r.v[e] = v;
+}
+__device__ __forceinline__ void adam_apply(const AdamConst& c, const AdamRef& r, uint32_t e,
+                                           float g) {
+  adam_apply_loaded(c, r, e, g, r.p[e], r.m[e], r.v[e]);
 }
 
 struct FinTask {

@@ -1418,7 +1418,7 @@ def _real_block(kind, cin, cout):
     return ResBottleneckBlock(cin, cout, 2, 1.0, 48)
 
 
-def _real_qnn(case):
+def _real_qnn(case, bits_w=2, bits_a=4):
     from quant.quant_block import BaseQuantBlock
     import realshape as RS
     if not hasattr(BaseQuantBlock, "setPathName"):
@@ -1426,9 +1426,9 @@ def _real_qnn(case):
     kind, cin, cout, _ = RS.CASES[case]
     net = RS.seed_net(RS.wrap(_real_block(kind, cin, cout), cout))
     lay = (RS.layout(net), RS.seed_sha(net))
-    wq = {"n_bits": 2, "channel_wise": True, "scale_method": "max", "tune_delta_zero": False,
+    wq = {"n_bits": bits_w, "channel_wise": True, "scale_method": "max", "tune_delta_zero": False,
           "symmetric": False}
-    aq = {"n_bits": 4, "channel_wise": False, "scale_method": "mse", "tune_delta_zero": False,
+    aq = {"n_bits": bits_a, "channel_wise": False, "scale_method": "mse", "tune_delta_zero": False,
           "leaf_param": True, "symmetric": False}
     qnn = QuantModel(model=net, weight_quant_params=wq, act_quant_params=aq)
     qnn.eval()
@@ -1498,6 +1498,61 @@ def _real_fused(case, x, iters, grad_steps, bias_cal, out, keep_cached=True):
         with torch.no_grad():
             out[f"{n}_what_hard_sha"] = np.array([RS.sha(t2n(q(m.weight)))])
     return qms
+
+
+def gen_real_layer_shift(case="r18_layer1_0", iters=20):
+    """Config 1 (W4A8, layer_recon_shiftedScale, layer_recon_shiftedScale.py:262-338 +
+    ScaleLossFunction :414-486) at the real ResNet-18 layer1.0.conv1 shape (64 -> 64, 3x3):
+    the shift phase (init_v, learned_hard_sigmoid, entropy regulariser, lambda 0.1) then the
+    AdaRound phase (update_delta, init_beta, beta, lambda 0.01), as gen_recon_layer_shift
+    does on the toy conv.  Recorded: the conv's cached FP output (the loop's target), batch
+    draws, per-iteration losses, the shift logits with their values / gradients (+ float64
+    truth) at the recorded steps, the selected per-(Co, Ci) delta, the final beta and the
+    hashes of the hard weights of both phases."""
+    import realshape as RS
+    x = RS.calib_input(case)
+    qnn, (lay, ssha) = _real_qnn(case, bits_w=4, bits_a=8)
+    out = {"layout": np.array(lay), "seed_sha": np.array([ssha])}
+    qnn.set_quant_state(True, False)
+    with torch.no_grad():
+        qnn(x)
+    block_name, layer_name = ".model.0", ".model.0.conv1"
+    MSM.build_ShiftedChannelQuant(qnn, [block_name], "", shiftTarget=[31 / 32, 33 / 32, 1.0],
+                                  skipShiftLayer=[])
+    qnn.set_quant_state(False, False)
+    _cache(qnn, [layer_name], x, RS.N_CALI)
+    m = qnn.model[0].conv1
+    m.use_weight_quant = True
+    q = m.weight_quantizer
+    out["w_sha"] = np.array([RS.sha(t2n(m.org_weight))])
+    out["b_sha"] = np.array([RS.sha(t2n(m.org_bias))])
+    out["delta"] = t2n(q.delta.reshape(-1))
+    out["zp"] = t2n(q.zero_point.reshape(-1))
+    out["cached_out"] = t2n(torch.cat(m.cached_out_features))
+    torch.manual_seed(1005)
+    with _Spy(LRS.ScaleLossFunction) as spy, \
+            _GradSpy((0, 5, iters - 1), _layer_truth(m, spy, 0.1, iters, False)) as gspy:
+        l1 = LRS.layer_recon_shiftedScale(m, iters, 0.1, qnn, None)
+    gspy.dump(out, "shift_")
+    out["shift_perms"] = np.stack([p.numpy() for p in spy.perms]).astype(np.int64)
+    out["shift_total_loss"] = np.array([r[1] for r in spy.rec], np.float64)
+    out["shift_final"] = np.array(l1, np.float64)
+    out["shift_alpha"] = t2n(q.alpha)
+    out["shift_xq_sha"] = np.array([RS.sha(np.stack([t2n(t) for t in q.x_q]))])
+    with torch.no_grad():
+        out["shift_what_sha"] = np.array([RS.sha(t2n(q(m.weight)))])
+    q.hard_targets = False
+    with _Spy(LRS.ScaleLossFunction) as spy:
+        l2 = LRS.layer_recon_shiftedScale(m, iters, 0.01, qnn, None, adaround=True)
+    out["ar_perms"] = np.stack([p.numpy() for p in spy.perms]).astype(np.int64)
+    out["ar_total_loss"] = np.array([r[1] for r in spy.rec], np.float64)
+    out["ar_final"] = np.array(l2, np.float64)
+    out["ar_delta"] = t2n(q.delta)
+    out["ar_beta"] = t2n(q.beta)
+    with torch.no_grad():
+        out["ar_what_sha"] = np.array([RS.sha(t2n(q(m.weight)))])
+    out["iters"] = np.array([iters])
+    save(f"real_{case}_layer_shift_w4a8", **out)
 
 
 def gen_real_biascal(cases=("r18_layer4_0", "r18_layer1_0")):
@@ -1576,7 +1631,7 @@ if __name__ == "__main__":
     which = sys.argv[1:] or ["uaq", "channelquant", "adaround", "specials", "inpscale", "loss", "recon",
                              "layershift", "brecq", "blocks", "act", "layerfused", "blockshift", "driver",
                              "wmse", "validate", "real", "recon_biascal", "real_biascal", "long",
-                             "layerbrecq"]
+                             "layerbrecq", "reallayer"]
     torch.set_num_threads(4)
     if "uaq" in which:
         gen_uaq()
@@ -1614,6 +1669,8 @@ if __name__ == "__main__":
         gen_validate()
     if "real" in which:
         gen_real_shapes()
+    if "reallayer" in which:
+        gen_real_layer_shift()
     if "layerbrecq" in which:
         gen_recon_layer_brecq()
     if "recon_biascal" in which:

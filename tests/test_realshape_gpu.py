@@ -83,14 +83,14 @@ def our_block(kind, cin, cout):
     return nets.ResBottleneckBlock(cin, cout, 2, 48)
 
 
-def real_qnn(Q, case, g, cuda=True):
+def real_qnn(Q, case, g, cuda=True, bits_w=2, bits_a=4):
     """The seeded FP net of `case`, wrapped (BN folded on the CPU as the reference does)."""
     kind, cin, cout, _ = RS.CASES[case]
     net = RS.seed_net(RS.wrap(our_block(kind, cin, cout), cout))
     assert RS.layout(net) == [str(s) for s in g["layout"]]
     assert RS.seed_sha(net) == str(g["seed_sha"][0]), "seeded FP parameters differ"
-    wq = {"n_bits": 2, "channel_wise": True, "scale_method": "max"}
-    aq = {"n_bits": 4, "channel_wise": False, "scale_method": "mse", "leaf_param": True}
+    wq = {"n_bits": bits_w, "channel_wise": True, "scale_method": "max"}
+    aq = {"n_bits": bits_a, "channel_wise": False, "scale_method": "mse", "leaf_param": True}
     qnn = Q.QuantModel(net, wq, aq).eval()
     return qnn.cuda() if cuda else qnn
 
@@ -125,7 +125,8 @@ def setup_fused(Q, case, g, stats, cached=None):
     from shiftedscalequantization_amd import drivers as D
     if cached is not None:
         assert str(cached["cached_out_sha"][0]) == str(g["cached_out_sha"][0])
-        g = dict(g, cached_out=cached["cached_out"])
+        g = dict(g, cached_out=cached["cached_out"], layout=cached["layout"],
+                 seed_sha=cached["seed_sha"])
     qnn, block, x, qms = init_weights(Q, case, g, stats)
     for n, m in qms:
         m.weight_quantizer = Q.ChannelQuant(1.0, uaq=m.weight_quantizer, weight_tensor=m.org_weight,
@@ -437,6 +438,90 @@ def test_long_horizon_trajectory(Q, golden, bias_cal):
         check_trajectory(g, qms, stats, rec, res, got, steps, RS.LONG_ITERS, bias_cal)
     finally:
         parity_report(f"long_traj[bias_cal={bias_cal}]", **stats)
+
+
+def test_real_layer_shift_w4a8_matches_reference(Q, golden):
+    """Config 1 at the real ResNet-18 layer1.0.conv1 shape (W4A8, layer_recon_shiftedScale:
+    layer_recon_shiftedScale.py:262-338): the shift phase's losses, alpha trajectory and
+    teacher-forced gradients (against the float64 truth), its hard weights; then the
+    AdaRound phase's losses, selected deltas, beta (walk-bounded, hard rounding decided
+    where the reference's beta is outside the walk budget) and hard weights."""
+    import importlib
+    from shiftedscalequantization_amd import drivers as D
+    E = importlib.import_module("shiftedscalequantization_amd.quant._engine")
+    case = "r18_layer1_0"
+    g = golden(f"real_{case}_layer_shift_w4a8")
+    stats = {}
+    qnn = real_qnn(Q, case, g, bits_w=4, bits_a=8)
+    x = RS.calib_input(case).cuda()
+    qnn.set_quant_state(True, False)
+    with torch.no_grad():
+        qnn(x)
+    m = qnn.model[0].conv1
+    assert RS.sha(host(m.org_weight)) == str(g["w_sha"][0])
+    assert RS.sha(host(m.org_bias)) == str(g["b_sha"][0])
+    np.testing.assert_array_equal(host(m.weight_quantizer.delta).reshape(-1), g["delta"])
+    np.testing.assert_array_equal(host(m.weight_quantizer.zero_point).reshape(-1), g["zp"])
+    D.build_ShiftedChannelQuant(qnn, [".model.0"], "", shiftTarget=SHIFTS, skipShiftLayer=[])
+    qnn.set_quant_state(False, False)
+    with torch.no_grad():
+        fp = host(m(x))
+    stats["fp_out_rel_err"] = np.abs(fp - g["cached_out"]).max() / np.abs(g["cached_out"]).max()
+    assert stats["fp_out_rel_err"] <= 1e-5
+    m.cached_inp_features, m.cached_out_features = [x.clone()], [dev(g["cached_out"])]
+    m.use_weight_quant = True
+    q = m.weight_quantizer
+    iters = int(g["iters"][0])
+    steps = [int(s_) for s_ in g["shift_grad_steps"]]
+    # teacher-forced at the recorded steps (alpha set to the reference's value there): the
+    # gradient is held to the float64 truth, and the trajectory stays the reference's
+    probe, got, before = grad_recorder(steps, {s_: [g[f"shift_gs{s_}_p0"]] for s_ in steps})
+    E.ITER_PROBE[0] = probe
+    try:
+        torch.manual_seed(1005)
+        l1 = Q.layer_recon_shiftedScale(m, iters, 0.1, qnn, None, verbose=False)
+    finally:
+        E.ITER_PROBE[0] = None
+    stats["shift_final_rel_err"] = np.max(np.abs(np.array(l1) - g["shift_final"]) / np.abs(g["shift_final"]))
+    np.testing.assert_allclose(l1, g["shift_final"], rtol=1e-5)
+    assert RS.sha(np.stack([host(t) for t in q.x_q])) == str(g["shift_xq_sha"][0])
+    da = np.abs(host(q.alpha) - g["shift_alpha"])
+    stats["shift_alpha_dev"] = da.max()
+    stats["shift_alpha_walkers"] = assert_walk_bounded(da, 1e-5, iters * 2e-3, frac=0.02,
+                                                      what="shift alpha")
+    worst = 0.0
+    for s_ in steps:
+        worst = max(worst, grad_stats(stats, f"shift_g{s_}", got[s_], [g[f"shift_gs{s_}_g0"]],
+                                      truths(g, "shift_", s_, 1)))
+    stats["shift_grad_worst_over_bound"] = worst
+    stats["shift_init_dev"] = np.abs(before[0][0] - g["shift_gs0_p0"]).max()
+    with torch.no_grad():
+        wh = RS.sha(host(q(m.weight)))
+    stats["shift_hard_identical"] = float(wh == str(g["shift_what_sha"][0]))
+    q.hard_targets = False
+    l2 = Q.layer_recon_shiftedScale(m, iters, 0.01, qnn, None, adaround=True, verbose=False)
+    stats["ar_final_rel_err"] = np.max(np.abs(np.array(l2) - g["ar_final"]) / np.abs(g["ar_final"]))
+    d = host(q.delta)
+    stats["ar_delta_flips"] = int(np.sum(d != g["ar_delta"]))
+    bq = host(q.beta)
+    db = np.abs(bq - g["ar_beta"])
+    budget = iters * 2e-3
+    stats["ar_beta_dev_max"] = db.max()
+    stats["ar_beta_walk_frac"] = float(np.mean(db > 2e-4))
+    decided = np.abs(g["ar_beta"]) > budget
+    stats["ar_undecided_frac"] = float(np.mean(~decided))
+    with torch.no_grad():
+        wh2 = RS.sha(host(q(m.weight)))
+    stats["ar_hard_identical"] = float(wh2 == str(g["ar_what_sha"][0]))
+    parity_report("real_layer_shift_w4a8[r18_layer1_0]", **stats)
+    np.testing.assert_allclose(l2, g["ar_final"], rtol=1e-5)
+    assert worst <= 1.0, stats
+    assert stats["shift_init_dev"] <= 5e-7
+    assert np.mean(d != g["ar_delta"]) <= 0.005
+    assert db.max() <= budget and np.mean(db > 2e-4) <= 0.05
+    assert np.all((bq >= 0)[decided] == (g["ar_beta"] >= 0)[decided])
+    if stats["shift_alpha_walkers"] == 0:
+        assert stats["shift_hard_identical"] == 1.0
 
 
 @pytest.mark.parametrize("case", CASES)

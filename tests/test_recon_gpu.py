@@ -363,7 +363,12 @@ def test_brecq_layer_reconstruction_matches_reference(Q, golden, graph):
             stats[tag + "_a_total_rel_err"] = np.max(np.abs(np.array(seen) - g[tag + "_a_total_loss"]) /
                                                      np.abs(g[tag + "_a_total_loss"]))
             stats[tag + "_a_delta_rel_err"] = abs(float(aq.delta) - g[tag + "_a_delta"][0]) / g[tag + "_a_delta"][0]
-            np.testing.assert_allclose(seen, g[tag + "_a_total_loss"], rtol=1e-5)
+            # the fc's act quantizer is the disabled network output: its "loss" is the fp32
+            # noise between two evaluations of the same quantized layer (~7e-7, a sum of
+            # squares of near-cancelling differences) -- agreeing to ~2e-5 relative is what
+            # fp32 convs / GEMMs in another summation order give there
+            rtol = 1e-5 if int(g[tag + "_a_on"][0]) else 1e-4
+            np.testing.assert_allclose(seen, g[tag + "_a_total_loss"], rtol=rtol)
             np.testing.assert_allclose([float(aq.delta)], g[tag + "_a_delta"], rtol=5e-6)
         with torch.no_grad():
             logits = qnn(cali).cpu().numpy()
