@@ -134,7 +134,7 @@ static inline int make_shifts(const float* shifts, int S, Shifts& sh) {
 struct ColTiling {
   uint32_t ncb, ncolblk, R, nchunk, threads;
   uint32_t whole;   // prepared alpha backward: one chunk, finalised in the workgroup
-  uint32_t form;    // prepared alpha backward: 0 thread-column (+ stage 2), 1 wave-column
+  uint32_t form;    // prepared alpha backward: 0 thread-column (+ stage 2), 3 one workgroup per ci
 };
 constexpr uint32_t kMaxChunks = 256;  // stage 2: lane c sums chunks c, c+64, ... in order
 

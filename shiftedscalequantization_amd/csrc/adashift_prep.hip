@@ -10,8 +10,8 @@
 // fpack + hterm (+ gWhat) with no divide and no exp per element -- 12 B/elem forward
 // (fpack, hterm in; What out) and 12 B/elem backward (gWhat, fpack, hterm in), the §8(d)
 // algorithmic bytes -- and produce bit-identical What / identical gradients.  The alpha
-// backward is one launch for weights with Co <= 64 (bwd_tiling_prep: whole-column
-// workgroups that finalise their input channels) and two fixed-order launches otherwise
+// backward is one launch for weights with Co*K <= 1280 (bwd_tiling_prep: one workgroup
+// per input channel, which it finalises) and two fixed-order launches otherwise
 // (chunk partials, then one wave per input channel).  Both kernels are latency-bound at
 // ResNet-18 sizes, so the loads a thread needs are issued before their first use.
 //
@@ -88,89 +88,41 @@ static ColTiling col_tiling_prep(const Geo& g) {
   return t;
 }
 
-// Alpha-backward tiling.  Weights with K <= 64 and Co <= 64 (ResNet-18 layer1, the
-// ResNet-50 layer1 convs, ...) take the whole-column wave-column form (alpha_bwd_wavecol):
-// a workgroup owns one wave-width of columns -- cw = floor(64/K) whole input channels, i.e.
-// cw*K <= 64 contiguous columns of every row -- over ALL rows, its 4 waves taking rows
-// w, w + 4, ... (<= kWR each), and finalises its channels: one launch, no partials.
-// Larger weights keep the thread-column tiling of the forward (chunks of rows) and a
-// stage-2 launch that sums the chunk partials.  Measured and not kept
-// (tools/alpha_cold.py, profiles/r3_alpha_variants.txt): the wave-column form with row
-// chunks is ~1 us slower than the thread-column stage 1 on layer2-4, and handing its chunk
-// partials to the last-arriving chunk of each column group (one launch, no stage 2) costs
-// 6-13 us more than the stage-2 launch it saves: every chunk waits for its write-through
-// partials and a device-scope ticket atomic before its workgroup retires.  The tiling
-// depends only on the weight's own shape, so a multi-segment launch gives each weight its
-// single-launch bits.
-constexpr uint32_t kWR = 16;   // rows per wave (whole form: Co <= 4 * kWR = 64)
-// Form 2 (r4): the thread-column stage 1 with the chunk reduction in the same launch -- the
-// last workgroup of each column block to finish (one ticket counter per column block, write-
-// through partials: arrive_last) reduces that block's chunks in the fixed order of the stage-2
-// launch (one wave per input channel: lane c takes chunk c, then the fixed shuffle tree) and
-// finalises the block's channels.  Row chunks are sized so a weight takes ~kK6pWgs
-// workgroups (one resident round: each workgroup pays the ticket round trip once, in
-// parallel) and at most one wave-width of chunks.  SSQ_K6P_FORM selects the form for A/B
-// (0: stage 1 + stage 2, 1: wave-column for Co <= 64 else form 0, 2: one launch).
-constexpr uint32_t kMaxTicketBlk = 256;          // column blocks per segment (form 2)
-constexpr uint32_t kMaxOneChunks = 16;           // form 2: row chunks per column block
-__device__ unsigned g_k6p_tickets[kMaxPrepSeg * kMaxTicketBlk];
-
-static ColTiling bwd_tiling_onelaunch(const Geo& g) {
-  static const uint32_t kWgs = prep_env("SSQ_K6P_WGS", 256);
-  static const uint32_t kRows = prep_env("SSQ_K6P_ROWS", 4);
-  ColTiling t = col_tiling_prep(g);
-  uint32_t want = (kWgs + t.ncolblk - 1) / t.ncolblk;
-  const uint32_t by_rows = (g.Co + kRows - 1) / kRows;
-  if (want > by_rows) want = by_rows;
-  if (want > kMaxOneChunks) want = kMaxOneChunks;
-  if (want < 1) want = 1;
-  t.R = (g.Co + want - 1) / want;
-  t.nchunk = (g.Co + t.R - 1) / t.R;
-  t.form = 2;
-  return t;
-}
-
-// Form 3 (r4): one workgroup per input channel, for weights with Co*K <= kChanElems (every
-// ResNet-18 conv but layer4's 3x3: 4608).  Its 256 threads take the channel's Co*K
-// (row, tap) elements -- thread t: elements t, t + 256, ... (<= 9), every load issued before
-// any math -- and reduce them in the workgroup (fixed shuffle tree per wave, then the 4
-// waves in order): one launch, no partials, and as many workgroups as input channels.  The
-// wave-column form puts a whole column block on one CU (10 workgroups for a layer1 conv):
-// its time is the few CUs' load bandwidth, not latency.
-constexpr uint32_t kChanPer = 9;                      // elements per thread
-constexpr uint32_t kChanElems = kChanPer * kBlock;    // 2304
+// Alpha-backward tiling.  Weights with Co*K <= kChanElems (ResNet-18 layer1 / layer2 3x3
+// convs and every 1x1 downsample, the ResNet-50 1x1 convs up to Co = 1280) take one
+// workgroup per input channel (alpha_bwd_channel): its 256 threads take the channel's Co*K
+// (row, tap) elements -- thread t: elements t, t + 256, ... (<= kChanPer), every load issued
+// before any math -- and reduce them in the workgroup (fixed shuffle tree per wave, then the
+// 4 waves in order): one launch, no partials, and as many workgroups as input channels.
+// Larger weights keep the thread-column tiling of the forward (chunks of rows) and a stage-2
+// launch that sums the chunk partials.  The tiling depends only on the weight's own shape, so
+// a multi-segment launch gives each weight its single-launch bits.
+//
+// Measured and not kept (tools/alpha_cold.py; profiles/r3_alpha_variants.txt,
+// profiles/r4_k6p_forms.txt): a wave-column form (one wave-width of columns over all rows,
+// Co <= 64: 10 workgroups for a layer1 conv, bound by those few CUs' loads) -- 10.4 us on
+// layer1 against 8.3 us here; one-launch forms that hand the chunk partials to the last
+// arriving workgroup of a column block (write-through partials, a device-scope ticket) --
+// 6-13 us slower than the stage-2 launch they save; and this form with 9 elements per thread
+// (up to Co*K = 2304, layer3 3x3) -- equal on layer3 (16.0 vs 15.8 us) but its registers
+// (97 VGPRs) cost the other forms' occupancy.
+constexpr uint32_t kChanPer = 5;                      // elements per thread
+constexpr uint32_t kChanElems = kChanPer * kBlock;    // 1280
 
 static ColTiling bwd_tiling_prep(const Geo& g) {
-  // SSQ_K6P_FORM (A/B): 3 = form 3 where it fits, else form 0 (default); 1 = the wave-column
-  // form where it fits, else form 0; 0 = stage 1 + stage 2 everywhere; 2 = one launch with
-  // the last-arriver reduction
+  // SSQ_K6P_FORM (A/B): 3 = the per-channel form where it fits, else thread-column (default);
+  // 0 = thread-column stage 1 + stage 2 everywhere
   static const uint32_t kForm = prep_env("SSQ_K6P_FORM", 3);
-  constexpr uint32_t kMaxR = (kBlock / kWave) * kWR;
-  if (kForm == 3) {
-    if (g.Co * g.K <= kChanElems) {
-      ColTiling t;
-      t.form = 3;
-      t.threads = kBlock;
-      t.ncb = 1;
-      t.ncolblk = g.Ci;
-      t.R = g.Co;
-      t.nchunk = 1;
-      t.whole = 1;
-      return t;
-    }
-    return col_tiling_prep(g);
-  }
-  if (kForm == 2) {
-    const ColTiling t = bwd_tiling_onelaunch(g);
-    if (t.ncolblk <= kMaxTicketBlk) return t;
-  }
-  if (kForm == 0 || g.K > (uint32_t)kWave || g.Co > kMaxR) return col_tiling_prep(g);
+  // rows per channel: a thread's elements sit one row (Ci*K floats) apart, so a 1x1 weight
+  // with many rows is read as Co scattered words per workgroup (r4, layer4.0's 512x256x1x1
+  // downsample: its launch 21.5 -> 26.5 us in this form); SSQ_K6P_CHAN_CO for A/B
+  static const uint32_t kMaxCo = prep_env("SSQ_K6P_CHAN_CO", 256);
+  if (kForm != 3 || g.Co * g.K > kChanElems || g.Co > kMaxCo) return col_tiling_prep(g);
   ColTiling t;
-  t.form = 1;
+  t.form = 3;
   t.threads = kBlock;
-  t.ncb = (uint32_t)kWave / g.K;
-  if (t.ncb > g.Ci) t.ncb = g.Ci;
-  t.ncolblk = (g.Ci + t.ncb - 1) / t.ncb;
+  t.ncb = 1;
+  t.ncolblk = g.Ci;
   t.R = g.Co;
   t.nchunk = 1;
   t.whole = 1;
@@ -193,8 +145,7 @@ struct PrepSeg {
   uint32_t blk0;     // first workgroup of this segment (forward / stage 1)
   uint32_t wave0;    // first wave of this segment (stage 2: one wave per input channel)
   uint32_t stage2;   // its chunks are reduced by the stage-2 launch
-  uint32_t ticket0;  // form 2: its column blocks' ticket counters start here
-  FastDiv divK;      // form 3: (row, tap) of a flat element index
+  FastDiv divK;      // per-channel form: (row, tap) of a flat element index
   float lo, hi;
   float* alpha_w;    // fused optimizer step (ssq_adam_arm): alpha, its Adam m / v (or null)
   float* am;
@@ -323,159 +274,7 @@ __device__ __forceinline__ void alpha_accumulate(uint32_t fw, float h, float d, 
   for (int i = 0; i < NS; ++i) acc[i] += (double)gi * (double)F[i];
 }
 
-// Input channel ci's alpha gradient from its summed d/dp (tot): the shift regulariser's
-// terms in shift order (value and gradient), then the softmax/clamp backward -- the same
-// values in the same order as alpha_chain.
-template <int NS>
-__device__ __forceinline__ void alpha_finalize(const PrepSeg& sg, const AdamConst& ac, uint32_t ci,
-                                               const float* a, const double* tot_in,
-                                               float reg_lambda, float reg_b) {
-  double tot[kMaxS];
-#pragma unroll
-  for (int i = 0; i < NS; ++i) tot[i] = tot_in[i];
-  float sm[kMaxS], p[kMaxS], ga[kMaxS];
-  soft_targets<kMaxS>(a, NS, sm, p);
-  float reg = 0.0f;
-  if (reg_lambda != 0.0f) {
-    double racc = 0.0;
-#pragma unroll
-    for (int i = 0; i < NS; ++i) {
-      double rv, rg;
-      reg_term(p[i], reg_lambda, reg_b, 0, rv, rg);
-      racc += rv;
-      tot[i] += rg;
-    }
-    reg = (float)((double)reg_lambda * racc);
-  }
-  softmax_clamp_bwd(sm, NS, tot, ga);
-#pragma unroll
-  for (int i = 0; i < NS; ++i) sg.galpha[(size_t)ci * NS + i] = ga[i];
-  if (sg.reg_vals) sg.reg_vals[ci] = reg;
-  if (sg.am) {                        // the fused optimizer step: this channel's S entries
-    const AdamRef r{sg.alpha_w, sg.am, sg.av};
-#pragma unroll
-    for (int i = 0; i < NS; ++i) adam_apply(ac, r, (uint32_t)(ci * NS + i), ga[i]);
-  }
-}
-
-// Wave-column alpha backward (bwd_tiling_prep form 1, Co <= 64).  Lane l of wave w owns
-// column j = ci0*K + l of rows w + 4r; every load of the lane is issued before any math
-// (the alpha row, delta / zp -- one row per lane, broadcast with readlane -- and the wave's
-// <= kWR rows of gW^, packed floors and h(beta)).  The 4 x K partials of an input channel
-// are then added in fixed order (waves per column, then taps) and lane t < nci of wave 0
-// finalises channel ci0 + t.
-template <int NS>
-__device__ __forceinline__ void alpha_bwd_wavecol(const PrepSeg& sg, const AdamConst& ac,
-                                                  uint32_t local, double* red, float reg_lambda,
-                                                  float reg_b, const float* __restrict__ reg_dev) {
-  const Geo& g = sg.g;
-  constexpr uint32_t kW = kBlock / kWave;
-  const uint32_t ci0 = local * sg.tl.ncb, nci = min(sg.tl.ncb, g.Ci - ci0);
-  const uint32_t w = __builtin_amdgcn_readfirstlane(threadIdx.x / kWave);
-  const uint32_t lane = threadIdx.x & (kWave - 1);
-  const uint32_t co0 = 0, co1 = g.Co;
-  const bool col = lane < nci * g.K;
-  const uint32_t ci = ci0 + (col ? lane / g.K : 0u), j = ci0 * g.K + lane;
-  const uint32_t* __restrict__ fpack = sg.fpack;
-  const float* __restrict__ hterm = sg.hterm;
-  const float* __restrict__ gWhat = sg.gWhat;
-  const float lo = sg.lo, hi = sg.hi;
-  float a[kMaxS], af[kMaxS];
-  load_row(sg.alpha, ci, NS, a);
-  const bool fin_lane = w == 0 && lane < nci;
-  if (fin_lane) load_row(sg.alpha, ci0 + lane, NS, af);
-  if (reg_dev) {
-    reg_lambda = reg_dev[0];
-    reg_b = reg_dev[1];
-  }
-  float dl = 0.0f, zl = 0.0f;
-  if (co0 + lane < co1) {
-    dl = sg.delta[co0 + lane];
-    zl = sg.zp[co0 + lane];
-  }
-  uint32_t fw[kWR];
-  float h[kWR], gy[kWR];
-#pragma unroll
-  for (uint32_t r = 0; r < kWR; ++r) {
-    fw[r] = 0u;
-    h[r] = gy[r] = 0.0f;
-    const uint32_t c = co0 + w + kW * r;
-    if (col && c < co1) {
-      const uint32_t e = c * g.CiK + j;
-      fw[r] = fpack[e];
-      h[r] = hterm[e];
-      gy[r] = gWhat[e];
-    }
-  }
-  // no divergent branch around the rows: readlane must see every lane's delta / zp (lanes
-  // past the columns hold zero rows and add nothing; their slots are never read)
-  double acc[NS];
-#pragma unroll
-  for (int i = 0; i < NS; ++i) acc[i] = 0.0;
-  float p[kMaxS];
-  soft_targets<kMaxS>(a, NS, nullptr, p);
-#pragma unroll
-  for (uint32_t r = 0; r < kWR; ++r) {
-    const uint32_t rl = w + kW * r;      // row within the chunk (wave-uniform)
-    if (co0 + rl < co1) {
-      const float d = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(dl), rl));
-      const float z = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(zl), rl));
-      alpha_accumulate<NS>(fw[r], h[r], d, z, gy[r], p, lo, hi, acc);
-    }
-  }
-#pragma unroll
-  for (int i = 0; i < NS; ++i) red[threadIdx.x * NS + i] = acc[i];
-  __syncthreads();
-  double tot[kMaxS];
-#pragma unroll
-  for (int i = 0; i < NS; ++i) tot[i] = 0.0;
-  if (w == 0) {
-    // lane l adds column l's 4 wave partials (all loads first), then lane t < nci adds its
-    // input channel's K columns; both in fixed order
-    double v[kW][NS];
-#pragma unroll
-    for (uint32_t ww = 0; ww < kW; ++ww)
-#pragma unroll
-      for (int i = 0; i < NS; ++i) v[ww][i] = red[(ww * kWave + lane) * NS + i];
-#pragma unroll
-    for (int i = 0; i < NS; ++i) {
-      double c = v[0][i];
-#pragma unroll
-      for (uint32_t ww = 1; ww < kW; ++ww) c += v[ww][i];
-      red[lane * NS + i] = c;
-    }
-    __builtin_amdgcn_wave_barrier();
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
-    if (lane < nci) {
-      constexpr uint32_t kUnK = 9;   // 3x3 taps unrolled (loads issued together); others loop
-      if (g.K <= kUnK) {
-        double vk[kUnK][NS];
-#pragma unroll
-        for (uint32_t k = 0; k < kUnK; ++k)
-#pragma unroll
-          for (int i = 0; i < NS; ++i) vk[k][i] = k < g.K ? red[(lane * g.K + k) * NS + i] : 0.0;
-#pragma unroll
-        for (int i = 0; i < NS; ++i) {
-          double sum = vk[0][i];
-#pragma unroll
-          for (uint32_t k = 1; k < kUnK; ++k)
-            if (k < g.K) sum += vk[k][i];
-          tot[i] = sum;
-        }
-      } else {
-#pragma unroll
-        for (int i = 0; i < NS; ++i) {
-          double sum = 0.0;
-          for (uint32_t k = 0; k < g.K; ++k) sum += red[(lane * g.K + k) * NS + i];
-          tot[i] = sum;
-        }
-      }
-    }
-  }
-  if (fin_lane) alpha_finalize<NS>(sg, ac, ci0 + lane, af, tot, reg_lambda, reg_b);
-}
-
-// Form 3: input channel ci of the segment in one workgroup (see bwd_tiling_prep).
+// Input channel ci of the segment in one workgroup (bwd_tiling_prep form 3).
 template <int NS>
 __device__ __forceinline__ void alpha_bwd_channel(const PrepSeg& sg, const AdamConst& ac,
                                                   uint32_t ci, double* red, float reg_lambda,
@@ -566,82 +365,7 @@ __device__ __forceinline__ void alpha_bwd_channel(const PrepSeg& sg, const AdamC
   }
 }
 
-// Form 2's in-launch stage 2 (run by the last arriving workgroup of a column block): thread
-// c takes input channel ci0 + c; every load it needs -- the alpha row, the armed Adam state,
-// the channel's nchunk partials (one contiguous run, write-through loads) -- is issued before
-// any math; the partials are added in chunk order and the channel finalised (regulariser,
-// softmax / clamp backward, the Adam step): one global round trip.
-template <int NS>
-__device__ __forceinline__ void alpha_reduce_chunks(const PrepSeg& sg, const AdamConst& ac,
-                                                    uint32_t ci0, uint32_t nci, float reg_lambda,
-                                                    float reg_b, const float* __restrict__ reg_dev) {
-  const uint32_t nchunk = sg.tl.nchunk;
-  if (reg_dev) {
-    reg_lambda = reg_dev[0];
-    reg_b = reg_dev[1];
-  }
-  for (uint32_t c = threadIdx.x; c < nci; c += kBlock) {
-    const uint32_t ci = ci0 + c;
-    float a[kMaxS], pp[kMaxS], pm[kMaxS], pv[kMaxS];
-    load_row(sg.alpha, ci, NS, a);
-    if (sg.am) {
-#pragma unroll
-      for (int i = 0; i < NS; ++i) {
-        pp[i] = sg.alpha_w[(size_t)ci * NS + i];
-        pm[i] = sg.am[(size_t)ci * NS + i];
-        pv[i] = sg.av[(size_t)ci * NS + i];
-      }
-    }
-    const double* src = sg.part + (size_t)ci * nchunk * NS;
-    constexpr uint32_t kB = 8;       // chunks per load batch (registers of the host kernel)
-    double tot[kMaxS];
-#pragma unroll
-    for (int i = 0; i < NS; ++i) tot[i] = 0.0;
-    for (uint32_t k0 = 0; k0 < nchunk; k0 += kB) {
-      double v[kB][NS];
-#pragma unroll
-      for (uint32_t k = 0; k < kB; ++k)
-#pragma unroll
-        for (int i = 0; i < NS; ++i)
-          v[k][i] = k0 + k < nchunk ? ld_sc1(src + (k0 + k) * NS + i) : 0.0;
-#pragma unroll
-      for (int i = 0; i < NS; ++i) {
-        double t = k0 == 0 ? v[0][i] : tot[i] + v[0][i];
-#pragma unroll
-        for (uint32_t k = 1; k < kB; ++k)
-          if (k0 + k < nchunk) t += v[k][i];
-        tot[i] = t;
-      }
-    }
-    // alpha_finalize with the Adam state already loaded
-    float sm[kMaxS], p[kMaxS], ga[kMaxS];
-    soft_targets<kMaxS>(a, NS, sm, p);
-    float reg = 0.0f;
-    if (reg_lambda != 0.0f) {
-      double racc = 0.0;
-#pragma unroll
-      for (int i = 0; i < NS; ++i) {
-        double rv, rg;
-        reg_term(p[i], reg_lambda, reg_b, 0, rv, rg);
-        racc += rv;
-        tot[i] += rg;
-      }
-      reg = (float)((double)reg_lambda * racc);
-    }
-    softmax_clamp_bwd(sm, NS, tot, ga);
-#pragma unroll
-    for (int i = 0; i < NS; ++i) sg.galpha[(size_t)ci * NS + i] = ga[i];
-    if (sg.reg_vals) sg.reg_vals[ci] = reg;
-    if (sg.am) {
-      const AdamRef r{sg.alpha_w, sg.am, sg.av};
-#pragma unroll
-      for (int i = 0; i < NS; ++i)
-        adam_apply_loaded(ac, r, (uint32_t)(ci * NS + i), ga[i], pp[i], pm[i], pv[i]);
-    }
-  }
-}
-
-// Backward, one launch for every segment: wave-column segments finish here; the
+// Backward, one launch for every segment: per-channel segments finish here; the
 // thread-column stage 1 of the others writes sums of g_int * F_i per (chunk, ci) into
 // part[(ci*nchunk + chunk)*S + i] (input-channel-major: stage 2 reads one coalesced run).
 template <int NS>
@@ -660,11 +384,7 @@ __global__ __launch_bounds__(kBlock) void alpha_bwd_prep(PrepTable tab, float re
   const PrepSeg& sg = tab.s[find_seg<false>(tab, bid)];
   const Geo& g = sg.g;
   const uint32_t local = bid - sg.blk0;
-  if (sg.tl.form == 1) {             // uniform per workgroup
-    alpha_bwd_wavecol<NS>(sg, tab.ac, local, red, reg_lambda, reg_b, reg_dev);
-    return;
-  }
-  if (sg.tl.form == 3) {
+  if (sg.tl.form == 3) {             // uniform per workgroup
     alpha_bwd_channel<NS>(sg, tab.ac, local, red, reg_lambda, reg_b, reg_dev);
     return;
   }
@@ -728,21 +448,14 @@ __global__ __launch_bounds__(kBlock) void alpha_bwd_prep(PrepTable tab, float re
 #pragma unroll
   for (int i = 0; i < NS; ++i) red[t * NS + i] = acc[i];
   __syncthreads();
-  const bool onel = sg.tl.form == 2;
   if (t < nci) {
 #pragma unroll
     for (int i = 0; i < NS; ++i) {
       double sum = 0.0;
       for (uint32_t k = 0; k < g.K; ++k) sum += red[(t * g.K + k) * NS + i];
-      double* dst = sg.part + ((size_t)(ci0 + t) * sg.tl.nchunk + by) * NS + i;
-      if (onel) st_sc1(dst, sum);      // write-through: read back by the last arriver
-      else *dst = sum;
+      sg.part[((size_t)(ci0 + t) * sg.tl.nchunk + by) * NS + i] = sum;
     }
   }
-  if (!onel) return;
-  // form 2: the last workgroup of this column block reduces its chunks and finalises
-  if (!arrive_last(&g_k6p_tickets[sg.ticket0 + bx], sg.tl.nchunk, (int*)red)) return;
-  alpha_reduce_chunks<NS>(sg, tab.ac, ci0, nci, reg_lambda, reg_b, reg_dev);
 }
 
 // Stage 2 (thread-column segments): one wave per (segment, input channel).  Every load the wave needs (alpha row, the device (lambda, b)
@@ -855,7 +568,6 @@ static int make_seg(const SegArgs& a, int i, PrepSeg& sg, const char* what) {
   sg.galpha = nullptr;
   sg.reg_vals = nullptr;
   sg.alpha_w = sg.am = sg.av = nullptr;
-  sg.ticket0 = 0;
   sg.divK = make_fastdiv(sg.g.K);
   sg.tl = col_tiling_prep(sg.g);
   sg.lo = (float)a.qmin[i];
@@ -1066,7 +778,6 @@ extern "C" int ssq_adashift_bwd_prepared_multi(
       sg.blk0 = blk;
       blk += sg.tl.ncolblk * sg.tl.nchunk;
       sg.stage2 = sg.tl.form == 0;
-      sg.ticket0 = (uint32_t)k * kMaxTicketBlk;
       sg.wave0 = waves;
       if (sg.stage2) waves += sg.g.Ci;
     }

@@ -19,6 +19,15 @@ tail -1 $OUT/smoke_$TAG.log
 timeout -k 10 600 python bench.py > $OUT/bench_$TAG.log 2>&1 || { echo "bench failed"; tail -20 $OUT/bench_$TAG.log; exit 1; }
 tail -1 $OUT/bench_$TAG.log | cut -c1-300
 cd /tmp && export TMPDIR=/tmp
+# K6p A/B with cold caches: thread-column everywhere (0), the default per-channel form (3),
+# and the per-channel form without its row cap (3, SSQ_K6P_CHAN_CO=4096)
+for V in "0 256" "3 256" "3 4096"; do
+  set -- $V
+  SSQ_K6P_FORM=$1 SSQ_K6P_CHAN_CO=$2 timeout -k 10 200 rocprofv3 --kernel-trace --output-format csv -d $OUT/k6p_${TAG}_$1_$2 -o t -- python3 $R/tools/alpha_cold.py 30 > $OUT/k6p_${TAG}_$1_$2.log 2>&1 || { echo "alpha_cold $V failed"; tail -5 $OUT/k6p_${TAG}_$1_$2.log; exit 1; }
+  KT=$(find $OUT/k6p_${TAG}_$1_$2 -name "*kernel_trace.csv" | head -1)
+  python3 $R/tools/trace_avg.py "$KT" alpha_bwd --groups=5 > $OUT/k6p_${TAG}_$1_$2.txt 2>&1
+  rm -f "$KT"
+done
 timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/prof_$TAG -o bench -- python3 $R/bench.py --no-cpu-baseline --no-validate --recon-iters 100 > $OUT/prof_bench_$TAG.log 2>&1 || { echo "rocprof failed"; tail -20 $OUT/prof_bench_$TAG.log; exit 1; }
 KT=$(find $OUT/prof_$TAG -name "*kernel_trace.csv" | head -1)
 python3 $R/tools/k1_trace_stats.py "$KT" > $OUT/k1_trace_$TAG.json 2>&1
