@@ -358,13 +358,16 @@ int ssq_epilogue_bwd(const float* g, const float* y, const float* bias, const fl
                      float* gres, float* ggamma, float* gphi, float* gdelta, float* gzp, void* ws,
                      size_t ws_bytes, ssq_stream_t stream);
 /* The fused tail of a reconstruction iteration: the block's final epilogue forward, the
- * p = 2 reconstruction loss against the cached target rows and the epilogue backward, in
- * one pass (layer_recon_fused_shiftedScale.py's quant_out -> lp_loss -> backward).  The
- * output is recomputed from y with the forward's ops and never stored; dL/d(output) is
- * ssq_lp_loss_rows's gradient (mean over M) bit for bit; the loss value Sum|out - tgt|^2 / M
- * (row partials summed in row order) goes to loss_out.  tgt_cache is [*, C, hw], idx holds
- * the N cached rows of this batch.  Outputs and workspace as ssq_epilogue_bwd. */
-int ssq_epilogue_loss_bwd(const float* tgt_cache, const int64_t* idx, int64_t M, float* loss_out,
+ * reconstruction loss (power p: 2 in the shifted-scale loops, 2.4 in BRECQ's act phase)
+ * against the cached target rows and the epilogue backward, in one pass
+ * (layer_recon_fused_shiftedScale.py's quant_out -> lp_loss -> backward; block_recon.py's
+ * act branch).  The output is recomputed from y with the forward's ops and never stored;
+ * dL/d(output) is ssq_lp_loss_rows's gradient at the same p (mean over M) bit for bit; the
+ * loss value Sum|out - tgt|^p / M (row partials summed in row order) goes to loss_out.
+ * tgt_cache is [*, C, hw], idx holds the N cached rows of this batch.  Outputs and
+ * workspace as ssq_epilogue_bwd. */
+int ssq_epilogue_loss_bwd(const float* tgt_cache, const int64_t* idx, int64_t M, float p,
+                          float* loss_out,
                           const float* y, const float* bias, const float* gamma, const float* phi,
                           const float* res, int64_t N, int64_t C, int64_t hw, int relu,
                           const float* delta, const float* zp, int qmin, int qmax, float* gy,

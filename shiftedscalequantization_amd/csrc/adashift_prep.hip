@@ -114,9 +114,11 @@ static ColTiling bwd_tiling_prep(const Geo& g) {
   // 0 = thread-column stage 1 + stage 2 everywhere
   static const uint32_t kForm = prep_env("SSQ_K6P_FORM", 3);
   // rows per channel: a thread's elements sit one row (Ci*K floats) apart, so a 1x1 weight
-  // with many rows is read as Co scattered words per workgroup (r4, layer4.0's 512x256x1x1
-  // downsample: its launch 21.5 -> 26.5 us in this form); SSQ_K6P_CHAN_CO for A/B
-  static const uint32_t kMaxCo = prep_env("SSQ_K6P_CHAN_CO", 256);
+  // with many rows is read as Co scattered words per workgroup (r4, cold whole-block launches:
+  // layer4.0 with its 512-row downsample here 20.1 -> 26.3 us, layer3.0 with its 256-row one
+  // 9.2 -> 11.8 us; layer2.0's 128-row one in a single launch 13.0 -> 9.8 us, stage 2
+  // included); SSQ_K6P_CHAN_CO for A/B
+  static const uint32_t kMaxCo = prep_env("SSQ_K6P_CHAN_CO", 128);
   if (kForm != 3 || g.Co * g.K > kChanElems || g.Co > kMaxCo) return col_tiling_prep(g);
   ColTiling t;
   t.form = 3;
@@ -477,6 +479,15 @@ __global__ __launch_bounds__(kBlock) void alpha_bwd_prep_stage2(PrepTable tab, f
   const uint32_t nchunk = sg.tl.nchunk;
   float a[kMaxS];
   load_row(sg.alpha, ci, NS, a);
+  float ap[kMaxS], am[kMaxS], av[kMaxS];   // the armed Adam state, loaded with the partials
+  if (sg.am && lane == 0) {
+#pragma unroll
+    for (int i = 0; i < NS; ++i) {
+      ap[i] = sg.alpha_w[(size_t)ci * NS + i];
+      am[i] = sg.am[(size_t)ci * NS + i];
+      av[i] = sg.av[(size_t)ci * NS + i];
+    }
+  }
   if (reg_dev) {
     reg_lambda = reg_dev[0];
     reg_b = reg_dev[1];
@@ -531,7 +542,8 @@ __global__ __launch_bounds__(kBlock) void alpha_bwd_prep_stage2(PrepTable tab, f
   if (sg.am) {                        // the fused optimizer step
     const AdamRef r{sg.alpha_w, sg.am, sg.av};
 #pragma unroll
-    for (int i = 0; i < NS; ++i) adam_apply(tab.ac, r, (uint32_t)(ci * NS + i), ga[i]);
+    for (int i = 0; i < NS; ++i)
+      adam_apply_loaded(tab.ac, r, (uint32_t)(ci * NS + i), ga[i], ap[i], am[i], av[i]);
   }
 }
 

@@ -114,6 +114,17 @@ __device__ __forceinline__ void fin_epi(uint32_t bid, const double* __restrict__
     __shared__ double wsum[4][kEpiChan][2];
     const uint32_t cl = threadIdx.x % kEpiChan, w = threadIdx.x / kEpiChan;
     const uint32_t c = bid * kEpiChan + cl;
+    // the fused Adam steps' state, loaded with the partials (one memory round trip, not two)
+    float st[2][3] = {{0.0f, 0.0f, 0.0f}, {0.0f, 0.0f, 0.0f}};
+    if (w == 0 && c < C) {
+#pragma unroll
+      for (int j = 0; j < 2; ++j)
+        if (ad[j].p) {
+          st[j][0] = ad[j].p[c];
+          st[j][1] = ad[j].m[c];
+          st[j][2] = ad[j].v[c];
+        }
+    }
     double sg = 0, sp = 0;
     if (c < C) {
 #pragma unroll 8
@@ -130,8 +141,8 @@ __device__ __forceinline__ void fin_epi(uint32_t bid, const double* __restrict__
       sp = wsum[0][cl][1] + wsum[1][cl][1] + wsum[2][cl][1] + wsum[3][cl][1];
       if (ggamma) ggamma[c] = (float)sg;
       if (gphi) gphi[c] = (float)sp;
-      if (ad[0].p) adam_apply(ac, ad[0], c, (float)sg);
-      if (ad[1].p) adam_apply(ac, ad[1], c, (float)sp);
+      if (ad[0].p) adam_apply_loaded(ac, ad[0], c, (float)sg, st[0][0], st[0][1], st[0][2]);
+      if (ad[1].p) adam_apply_loaded(ac, ad[1], c, (float)sp, st[1][0], st[1][1], st[1][2]);
     }
     return;
   }

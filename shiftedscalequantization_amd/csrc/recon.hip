@@ -274,10 +274,10 @@ struct EpiRow {
   float b, ga, ph;                                   // bias[c], gamma[c], phi[c]
   double sg = 0, sp = 0, a0 = 0, a1 = 0, a2 = 0, a3 = 0, la = 0;
 };
-template <bool RES, int ACT, bool QUANT, bool AFFINE, bool LOSS, bool BIAS>
+template <bool RES, int ACT, bool QUANT, bool AFFINE, int LOSS, bool BIAS>
 __device__ __forceinline__ void epi_elem(EpiRow& w, float d, float z, float lo, float hi,
-                                         float inv_m, float yv, float gv_or_tgt, float rv,
-                                         float& oy, float& orr) {
+                                         float inv_m, float lp, float yv, float gv_or_tgt,
+                                         float rv, float& oy, float& orr) {
   const float pre = BIAS ? __fadd_rn(yv, w.b) : yv;
   float t = AFFINE ? __fadd_rn(__fmul_rn(pre, w.ga), w.ph) : pre;
   if (RES) t = __fadd_rn(t, rv);
@@ -293,7 +293,7 @@ __device__ __forceinline__ void epi_elem(EpiRow& w, float d, float z, float lo, 
   float gv = gv_or_tgt;
   if (LOSS) {   // the forward's output (fq1's dequant), then the loss gradient wrt it
     const float o = QUANT ? __fmul_rn(__fsub_rn(q, z), d) : t;
-    gv = lp_elem<0>(o, gv_or_tgt, 2.0f, inv_m, 1.0f, 0, w.la);
+    gv = lp_elem<LOSS == 1 ? 0 : 2>(o, gv_or_tgt, LOSS == 1 ? 2.0f : lp, inv_m, 1.0f, 0, w.la);
   }
   float gt = gv;
   if (QUANT) {
@@ -313,7 +313,7 @@ __device__ __forceinline__ void epi_elem(EpiRow& w, float d, float z, float lo, 
 }
 
 // the row's sums over the wave (fixed shuffle tree), written by lane 0 to its kEpiParts slots
-template <bool QUANT, bool LOSS>
+template <bool QUANT, int LOSS>
 __device__ __forceinline__ void epi_row_sums(EpiRow& w, uint32_t lane, double* __restrict__ o) {
   w.sg = wave_sum(w.sg);
   w.sp = wave_sum(w.sp);
@@ -349,18 +349,19 @@ __device__ __forceinline__ void epi_row_sums(EpiRow& w, uint32_t lane, double* _
 // the waves.  The pre-activation values are recomputed from y with the forward's fp32
 // operations (bit-identical masks), nothing of the forward is stored.
 // LOSS (the fused tail, ssq_epilogue_loss_bwd): g is the cache of target rows instead of
-// dL/d(output); the output is recomputed (the forward's ops) and dL/d(output) is the p = 2
-// lp_loss gradient of K11 (lp_elem, identical ops), the loss partial goes to slot 6.
+// dL/d(output); the output is recomputed (the forward's ops) and dL/d(output) is the
+// lp_loss gradient of K11 (lp_elem, identical ops: LOSS 1 for p = 2, 2 for a general p such
+// as the act phase's 2.4), the loss partial goes to slot 6.
 // The wave's RPW rows (bid: the workgroup among the launch's main ones); returns the wave's
 // loss sum (LOSS: its rows' totals in row order), 0 for a wave past the last row.
-template <bool RES, int ACT, bool QUANT, bool AFFINE, bool VEC, bool LOSS, int RPW>
+template <bool RES, int ACT, bool QUANT, bool AFFINE, bool VEC, int LOSS, int RPW>
 __device__ __forceinline__ double epilogue_rows_body(
     const float* __restrict__ g, const float* __restrict__ y, const float* __restrict__ bias,
     const float* __restrict__ gamma, const float* __restrict__ phi, const float* __restrict__ res,
     uint32_t rows, uint32_t C, uint32_t hw, const float* __restrict__ qdelta,
     const float* __restrict__ qzp, float lo, float hi, float* __restrict__ gy,
     float* __restrict__ gres, double* __restrict__ part, const int64_t* __restrict__ lidx,
-    float inv_m, uint32_t bid) {
+    float inv_m, float lp, uint32_t bid) {
   const uint32_t lane = threadIdx.x & (kWave - 1);
   const uint32_t r0 = (bid * (kBlock / kWave) + threadIdx.x / kWave) * RPW;
   if (r0 >= rows) return 0.0;
@@ -375,8 +376,8 @@ __device__ __forceinline__ double epilogue_rows_body(
     w[k].ph = (AFFINE && ok) ? phi[c] : 0.0f;
   }
   auto elem = [&](EpiRow& wr, float yv, float gv, float rv, float& oy, float& orr) {
-    if (bias) epi_elem<RES, ACT, QUANT, AFFINE, LOSS, true>(wr, d, z, lo, hi, inv_m, yv, gv, rv, oy, orr);
-    else epi_elem<RES, ACT, QUANT, AFFINE, LOSS, false>(wr, d, z, lo, hi, inv_m, yv, gv, rv, oy, orr);
+    if (bias) epi_elem<RES, ACT, QUANT, AFFINE, LOSS, true>(wr, d, z, lo, hi, inv_m, lp, yv, gv, rv, oy, orr);
+    else epi_elem<RES, ACT, QUANT, AFFINE, LOSS, false>(wr, d, z, lo, hi, inv_m, lp, yv, gv, rv, oy, orr);
   };
   // LOSS: row (n, c)'s target is row c of cached sample idx[n] ([*, C, hw] cache)
   auto gbase_of = [&](uint32_t r) -> int64_t {
@@ -473,14 +474,14 @@ __device__ __forceinline__ double epilogue_rows_body(
   return wl;
 }
 
-template <bool RES, int ACT, bool QUANT, bool AFFINE, bool VEC, bool LOSS, int RPW>
+template <bool RES, int ACT, bool QUANT, bool AFFINE, bool VEC, int LOSS, int RPW>
 __global__ __launch_bounds__(kBlock) void epilogue_bwd_rows(
     const float* __restrict__ g, const float* __restrict__ y, const float* __restrict__ bias,
     const float* __restrict__ gamma, const float* __restrict__ phi, const float* __restrict__ res,
     uint32_t rows, uint32_t C, uint32_t hw, const float* __restrict__ qdelta,
     const float* __restrict__ qzp, float lo, float hi, float* __restrict__ gy,
     float* __restrict__ gres, double* __restrict__ part, FinTable fin, uint32_t nmain,
-    const int64_t* __restrict__ lidx, float inv_m) {
+    const int64_t* __restrict__ lidx, float inv_m, float lp) {
   // queued finalize tasks ride on this launch: its first workgroups (dispatched first, so
   // they run beside the main work instead of after it)
   (void)nmain;
@@ -491,7 +492,7 @@ __global__ __launch_bounds__(kBlock) void epilogue_bwd_rows(
   const uint32_t bid = blockIdx.x - fin.nwg;
   const double wl = epilogue_rows_body<RES, ACT, QUANT, AFFINE, VEC, LOSS, RPW>(
       g, y, bias, gamma, phi, res, rows, C, hw, qdelta, qzp, lo, hi, gy, gres, part, lidx, inv_m,
-      bid);
+      lp, bid);
   if (!LOSS) return;
   // the fused tail's loss: one partial per workgroup (its waves in order) after the rows'
   // records, so the finalize sums rows / (4 RPW) values instead of every row's
@@ -866,17 +867,19 @@ extern "C" size_t ssq_epilogue_bwd_workspace_size(int64_t rows) {
 }
 
 // ssq_epilogue_bwd (g = dL/d(output)) and its fused-tail form ssq_epilogue_loss_bwd
-// (tgt = the cache of target rows, idx = this batch's rows: dL/d(output) of the p = 2
-// lp_loss computed in the pass, its value finalised into loss_out).
+// (tgt = the cache of target rows, idx = this batch's rows: dL/d(output) of the lp_loss
+// (power lp) computed in the pass, its value finalised into loss_out).
 static int epilogue_bwd(const char* what, const float* g, const float* y, const float* bias,
                         const float* gamma, const float* phi, const float* res, int64_t N,
                         int64_t C, int64_t hw, int relu, const float* delta, const float* zp,
-                        int qmin, int qmax, const int64_t* lidx, int64_t M, float* loss_out,
-                        float* gy, float* gres, float* ggamma, float* gphi, float* gdelta,
+                        int qmin, int qmax, const int64_t* lidx, int64_t M, float lp,
+                        float* loss_out, float* gy, float* gres, float* ggamma, float* gphi, float* gdelta,
                         float* gzp, void* ws, size_t ws_bytes, hipStream_t s) {
   const bool loss = lidx != nullptr;
   SSQ_REQUIRE(g && y && gy && N >= 1 && C >= 1 && hw >= 1, SSQ_E_ARG, "%s: bad args", what);
   SSQ_REQUIRE(!loss || (loss_out && M >= 1), SSQ_E_ARG, "%s: loss_out and M required", what);
+  SSQ_REQUIRE(!loss || lp > 0.0f, SSQ_E_ARG, "%s: loss power p must be > 0", what);
+  const bool lp2 = lp == 2.0f;
   SSQ_REQUIRE(!gamma == !phi && (!(ggamma || gphi) || gamma), SSQ_E_ARG,
               "%s: gamma/phi gradients need gamma and phi", what);
   SSQ_REQUIRE(!delta || (zp && qmin < qmax), SSQ_E_ARG, "%s: act quantizer", what);
@@ -906,12 +909,14 @@ static int epilogue_bwd(const char* what, const float* g, const float* y, const 
 #define SSQ_EB0(R, A, Q, F, V, L, P)                                                              \
   hipLaunchKernelGGL((epilogue_bwd_rows<R, A, Q, F, V, L, P>), grid, dim3(kBlock), 0, s, g, y,    \
                      bias, gamma, phi, res, (uint32_t)rows, (uint32_t)C, (uint32_t)hw, delta, zp, \
-                     lo, hi, gy, gres, part, fin, nmain, lidx, inv_m)
+                     lo, hi, gy, gres, part, fin, nmain, lidx, inv_m, lp)
 #define SSQ_EB(R, A, Q, F, V, L) \
   if (multi) SSQ_EB0(R, A, Q, F, V, L, ((Q) ? 1 : 4)); else SSQ_EB0(R, A, Q, F, V, L, 1);
+#define SSQ_EBL(R, A, Q, F, V) \
+  if (lp2) { SSQ_EB(R, A, Q, F, V, 1) } else { SSQ_EB(R, A, Q, F, V, 2) }
 #define SSQ_EB1(R, A, Q, F) \
-  if (loss) { if (vec) { SSQ_EB(R, A, Q, F, true, true) } else { SSQ_EB(R, A, Q, F, false, true) } } \
-  else if (vec) { SSQ_EB(R, A, Q, F, true, false) } else { SSQ_EB(R, A, Q, F, false, false) }
+  if (loss) { if (vec) { SSQ_EBL(R, A, Q, F, true) } else { SSQ_EBL(R, A, Q, F, false) } } \
+  else if (vec) { SSQ_EB(R, A, Q, F, true, 0) } else { SSQ_EB(R, A, Q, F, false, 0) }
 #define SSQ_EB2(R, A, Q) \
   if (gamma) { SSQ_EB1(R, A, Q, true) } else { SSQ_EB1(R, A, Q, false) }
 #define SSQ_EB3(R, A) \
@@ -924,6 +929,7 @@ static int epilogue_bwd(const char* what, const float* g, const float* y, const 
 #undef SSQ_EB3
 #undef SSQ_EB2
 #undef SSQ_EB1
+#undef SSQ_EBL
 #undef SSQ_EB
 #undef SSQ_EB0
   int rc = check_launch(what);
@@ -982,12 +988,12 @@ extern "C" int ssq_epilogue_bwd(const float* g, const float* y, const float* bia
                                 float* ggamma, float* gphi, float* gdelta, float* gzp, void* ws,
                                 size_t ws_bytes, ssq_stream_t stream) {
   return epilogue_bwd("ssq_epilogue_bwd", g, y, bias, gamma, phi, res, N, C, hw, relu, delta, zp,
-                      qmin, qmax, nullptr, 0, nullptr, gy, gres, ggamma, gphi, gdelta, gzp, ws,
+                      qmin, qmax, nullptr, 0, 2.0f, nullptr, gy, gres, ggamma, gphi, gdelta, gzp, ws,
                       ws_bytes, (hipStream_t)stream);
 }
 
 extern "C" int ssq_epilogue_loss_bwd(const float* tgt_cache, const int64_t* idx, int64_t M,
-                                     float* loss_out, const float* y, const float* bias,
+                                     float p, float* loss_out, const float* y, const float* bias,
                                      const float* gamma, const float* phi, const float* res,
                                      int64_t N, int64_t C, int64_t hw, int relu,
                                      const float* delta, const float* zp, int qmin, int qmax,
@@ -996,7 +1002,7 @@ extern "C" int ssq_epilogue_loss_bwd(const float* tgt_cache, const int64_t* idx,
                                      ssq_stream_t stream) {
   SSQ_REQUIRE(idx, SSQ_E_ARG, "ssq_epilogue_loss_bwd: idx is required");
   return epilogue_bwd("ssq_epilogue_loss_bwd", tgt_cache, y, bias, gamma, phi, res, N, C, hw,
-                      relu, delta, zp, qmin, qmax, idx, M, loss_out, gy, gres, ggamma, gphi,
+                      relu, delta, zp, qmin, qmax, idx, M, p, loss_out, gy, gres, ggamma, gphi,
                       gdelta, gzp, ws, ws_bytes, (hipStream_t)stream);
 }
 

@@ -1147,9 +1147,9 @@ def epilogue(y, bias, gamma, phi, res, relu, q=None, lazy=False):
                             q.sym)
 
 
-def epilogue_loss_bwd(tail, tgt, M):
+def epilogue_loss_bwd(tail, tgt, M, p=2.0):
     """The fused tail (ssq_epilogue_loss_bwd): for a lazy epilogue placeholder's inputs and a
-    Rows target, the p = 2 lp_loss value (1-element device tensor, mean over M) and the
+    Rows target, the lp_loss value at power p (1-element device tensor, mean over M) and the
     gradients the epilogue's backward returns -- (loss, gy, gres, ggamma, gphi, gdelta, gzp),
     None where the input needs none -- bit-identical to epilogue -> lp_loss_and_grad ->
     backward."""
@@ -1179,9 +1179,9 @@ def epilogue_loss_bwd(tail, tgt, M):
     gd = torch.empty(1, device=dev_) if (q is not None and q.delta.requires_grad) else None
     gz = torch.empty(1, device=dev_) if (q is not None and q.zero_point.requires_grad) else None
     ws, wsn = workspace(query("ssq_epilogue_bwd_workspace_size", N * C_), dev_, _epi_slot())
-    call("ssq_epilogue_loss_bwd", cp, _vp(idx), int(M), _vp(loss), yp, bp, _vp(gm), _vp(ph), rp,
-         N, C_, hw, int(relu), _vp(d), _vp(z), lo, hi, _vp(gy), _vp(gres), _vp(ggm), _vp(gph),
-         _vp(gd), _vp(gz), ws, wsn, stream_of(y))
+    call("ssq_epilogue_loss_bwd", cp, _vp(idx), int(M), float(p), _vp(loss), yp, bp, _vp(gm),
+         _vp(ph), rp, N, C_, hw, int(relu), _vp(d), _vp(z), lo, hi, _vp(gy), _vp(gres), _vp(ggm),
+         _vp(gph), _vp(gd), _vp(gz), ws, wsn, stream_of(y))
     # a gradient written into its GRAD_INTO slice is not handed back (already in place)
     return loss, gy, gres, None if gm_into else ggm, None if ph_into else gph, gd, gz
 

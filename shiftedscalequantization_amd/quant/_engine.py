@@ -76,6 +76,37 @@ class BatchFeeder:
         return self.inp[:n], self.out[:n]
 
 
+def backward_tail(tail, grads):
+    """Resume autograd at a fused tail's inputs: the conv output y and the residual through
+    their graphs; gamma^z / phi^z / the act quantizer's delta and zero point are leaves here
+    (or views of leaves), accumulated as autograd would."""
+    y, bias, gamma, phi, res, relu, q = tail
+    _, gy, gres, ggm, gph, gd, gz = grads
+    roots, grs = [y], [gy]
+    if gres is not None:
+        roots.append(res)
+        grs.append(gres)
+    leaves = [(gamma, ggm), (phi, gph)]
+    if q is not None:
+        leaves += [(q.delta, gd), (q.zero_point, gz)]
+    for t, g in leaves:
+        if g is None:
+            continue
+        g = g.view(t.shape)
+        if t.is_leaf:
+            if t.grad is None:
+                t.grad = g
+            else:
+                # g may be a deferred-finalize output (fin_tasks.h): make it final before
+                # another kernel reads it
+                K.flush_finalize(g.device)
+                t.grad.add_(g)
+        else:
+            roots.append(t)
+            grs.append(g)
+    torch.autograd.backward(roots, grs)
+
+
 def stash_block_weights(quantizers):
     """The adaShift What of every prepared conv quantizer of a block in ONE launch (their
     alpha backward then runs as one two-launch reduction): they depend only on alpha,

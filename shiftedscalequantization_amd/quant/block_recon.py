@@ -8,16 +8,18 @@ multi_gpu=True all-reduces (SUM, as the reference's link.allreduce) every optimi
 gradient each iteration -- here as ONE flat RCCL bucket (parallel_dp.GradBucket); the
 reference's call crashes because `link` is never imported (block_recon.py:2,102).
 """
+import contextlib
+
 import torch
 
 from .. import kernels as K
 from ..parallel_dp import GradBucket, world
-from ._engine import (BatchFeeder, IterationGraph, LazyValue, SsqAdam, as_float, frozen_except,
-                      probe)
+from ._engine import (BatchFeeder, IterationGraph, LazyValue, SsqAdam, as_float, backward_tail,
+                      frozen_except, probe)
 from .adaptive_rounding import AdaRoundQuantizer
 from .data_utils import save_grad_data, save_inp_oup_data
 from .quant_block import BaseQuantBlock
-from .quant_layer import QuantModule, StraightThrough
+from .quant_layer import QuantModule, StraightThrough, pinned_weights
 from .quant_model import QuantModel
 
 
@@ -36,6 +38,15 @@ def block_reconstruction(model: QuantModel, block: BaseQuantBlock, cali_data: to
 
 GRAPH_WARMUP = 3     # eager iterations before the iteration body is captured
 ITER_HOOK = None     # optional callable(i, iters) at the top of every device-loop iteration (tools)
+# A/B knobs of the device loop, bit-identical either way (tests/test_recon_gpu.py):
+# the loss / epilogue finalizes ride on the next backward launch (csrc/fin_tasks.h; world 1)
+DEFER_FINALIZE = True
+# a block's final epilogue, the loss (p = 2 weight phase, 2.4 act phase) and the epilogue's
+# backward in one pass (K.epilogue_loss_bwd)
+FUSE_TAIL = True
+# act phase: every weight quantizer's W_hat computed once for the loop (the weights are
+# frozen there; quant_layer.pinned_weights)
+PIN_WEIGHTS = True
 
 
 def _reconstruct(model, block, qmodules, cali_data, batch_size, iters, weight, opt_mode, asym,
@@ -128,6 +139,10 @@ def _fast_loop(block, qmodules, opt_params, loss_func, feeder, bucket, iters, ac
     if ITER_HOOK is not None:
         ITER_HOOK(-1, iters)
     use_graph = bool(graph and iters > GRAPH_WARMUP + 1)
+    defer = DEFER_FINALIZE and bucket is None
+    fuse_tail = FUSE_TAIL and isinstance(block, BaseQuantBlock)
+    wq_params = {id(t) for m in qmodules for t in m.weight_quantizer.parameters()}
+    pin = PIN_WEIGHTS and act_quant and not any(id(t) in wq_params for t in opt_params)
     if act_quant:
         optimizer = SsqAdam(opt_params, lr=lr)
         # the reference's cosine schedule, stepped by torch's own scheduler on a shadow
@@ -144,8 +159,28 @@ def _fast_loop(block, qmodules, opt_params, loss_func, feeder, bucket, iters, ac
     last = {}
 
     def body_pre():
+        with K.deferred_finalize(defer):
+            _body_pre()
+
+    def _body_pre():
         cur_inp, cur_out = feeder.gather_lazy()
-        out = block(cur_inp)
+        K.TAIL_LAZY[0] = block if fuse_tail else None
+        try:
+            out = block(cur_inp)
+        finally:
+            K.TAIL_LAZY[0] = None
+        tail = getattr(out, '_ssq_tail', None)
+        if tail is not None:
+            # the block's final epilogue, the loss and the epilogue's backward in one pass;
+            # autograd resumes at the epilogue's inputs
+            grads = K.epilogue_loss_bwd(tail, cur_out, K._lp_M(out, "none"), p)
+            y, _, gamma, phi, res, _, q = tail
+            live = [y, res, gamma, phi] + ([q.delta, q.zero_point] if q is not None else [])
+            last['rec'] = grads[0]
+            last['step'] = any(t is not None and t.requires_grad for t in live)
+            if last['step']:
+                backward_tail(tail, grads)
+            return
         relu_in = getattr(out, '_ssq_relu_inputs', None)
         if not out.requires_grad:
             # no optimised parameter reaches the output (e.g. the act delta of a layer whose
@@ -167,7 +202,15 @@ def _fast_loop(block, qmodules, opt_params, loss_func, feeder, bucket, iters, ac
         if last['step']:
             optimizer.step(hyper=hyper)
 
-    graph_obj, ws_cache = None, {}
+    ws_cache = {}
+    with (pinned_weights(qmodules) if pin else contextlib.nullcontext()):
+        _run(iters, loss_func, feeder, optimizer, scheduler, shadow if act_quant else None, use_graph,
+             bucket, body_pre, body_post, last, opt_params, ada, ws_cache)
+
+
+def _run(iters, loss_func, feeder, optimizer, scheduler, shadow, use_graph, bucket, body_pre,
+         body_post, last, opt_params, ada, ws_cache):
+    graph_obj = None
     try:
         for i in range(iters):
             if ITER_HOOK is not None:

@@ -40,6 +40,34 @@ def frozen_weight_cache():
         _FROZEN_W = prev
 
 
+# Weights pinned for a loop in which no weight quantizer learns (pinned_weights):
+# module -> W_hat.
+_PINNED_W = None
+
+
+@contextlib.contextmanager
+def pinned_weights(modules):
+    """Inside this context every QuantModule of `modules` that quantizes its weight uses the
+    W_hat computed once on entry.  For a reconstruction loop whose optimised parameters do
+    not reach any weight quantizer (BRECQ's act-delta phase, block_recon.py:62-73, after
+    the weight phase has fixed the rounding): every iteration's weight q/dq is then the same
+    computation on the same frozen inputs, so reusing its result is bit-identical and saves
+    the per-iteration weight launches (also inside a captured HIP graph).  The caller
+    guarantees that nothing the weight quantizers read changes inside the context."""
+    global _PINNED_W
+    prev = _PINNED_W
+    pinned = {} if prev is None else dict(prev)
+    with torch.no_grad():
+        for m in modules:
+            if m.use_weight_quant and m.cache_features == 'none':
+                pinned[m] = m.weight_quantizer(m.weight)
+    _PINNED_W = pinned
+    try:
+        yield
+    finally:
+        _PINNED_W = prev
+
+
 _STATE_FLAGS = ('soft_targets', 'hard_round', 'hard_targets', 'opt_mode', 'shiftedScale',
                 'round_mode', 'n_bits')
 
@@ -257,7 +285,9 @@ class QuantModule(nn.Module):
 
     def _weight_bias(self):
         if self.use_weight_quant and self.cache_features == 'none':
-            if _FROZEN_W is not None and not torch.is_grad_enabled():
+            if _PINNED_W is not None and self in _PINNED_W:
+                weight = _PINNED_W[self]
+            elif _FROZEN_W is not None and not torch.is_grad_enabled():
                 key = (id(self.weight_quantizer), id(self.weight), self.weight._version,
                        _quantizer_state(self.weight_quantizer))
                 hit = _FROZEN_W.get(self)

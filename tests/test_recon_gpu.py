@@ -302,6 +302,101 @@ def test_brecq_block_reconstruction_matches_reference(Q, golden, graph, wgrad):
 
 
 @pytest.mark.parametrize("graph", [False, True])
+@pytest.mark.parametrize("affine", [False, True])
+def test_brecq_loop_knobs_bit_identical(Q, golden, graph, affine, det_convs):
+    """block_recon._fast_loop's launch savings -- deferred finalizes, the fused tail (p = 2
+    weight phase, p = 2.4 act phase) and the act phase's pinned weights -- against the plain
+    loop: AdaRound V, the act deltas and the Adam moments bit-identical after each phase,
+    per-iteration losses equal to the last float ulps (row-wise vs block-wise loss partials).
+    affine: gamma^z / phi^z live (the --bias_cal flow's act phase: the general K13 epilogue,
+    whose delta gradient the fused tail and the deferred finalize produce)."""
+    import importlib
+    BR = importlib.import_module("shiftedscalequantization_amd.quant.block_recon")
+    E = importlib.import_module("shiftedscalequantization_amd.quant._engine")
+    g = golden("recon_brecq")
+    cali = dev(g["cali"])
+    runs, used = [], []
+    for on in (False, True):
+        qnn = build_qnn(Q, g)
+        block = qnn.model[3]
+        if affine:
+            gen = torch.Generator().manual_seed(7)
+            for n in ("conv1", "conv2", "downsample"):
+                m = getattr(block, n)
+                with torch.no_grad():
+                    m.alpha_out.copy_(1 + 0.05 * torch.randn(m.alpha_out.shape, generator=gen))
+                    m.beta_out.copy_(0.02 * torch.randn(m.beta_out.shape, generator=gen))
+        seen, opts, tails, pins = [], [], [], []
+        orig_rec, orig_init = BR.LossFunction.record, E.SsqAdam.__init__
+        orig_tail, orig_pin = BR.K.epilogue_loss_bwd, BR.pinned_weights
+
+        def spy(self, rec, rnd, b):
+            r = orig_rec(self, rec, rnd, b)
+            seen.append(float(r))
+            return r
+
+        def init(self, *a, **k):
+            orig_init(self, *a, **k)
+            opts.append(self)
+
+        def tail(*a, **k):
+            tails.append(1)
+            return orig_tail(*a, **k)
+
+        def pin(mods):
+            pins.append(1)
+            return orig_pin(mods)
+
+        knobs = {k: getattr(BR, k) for k in ("DEFER_FINALIZE", "FUSE_TAIL", "PIN_WEIGHTS")}
+        BR.LossFunction.record, E.SsqAdam.__init__, BR.K.epilogue_loss_bwd = spy, init, tail
+        BR.pinned_weights = pin
+        orig_fast = BR._fast_loop
+        BR._fast_loop = lambda *a: orig_fast(*(a[:-1] + (a[-1] and graph,)))
+        for k in knobs:
+            setattr(BR, k, on)
+        out = {}
+        try:
+            torch.manual_seed(1005)
+            Q.block_reconstruction(qnn, block, cali, batch_size=8, iters=12, weight=0.01,
+                                   asym=True, b_range=(20, 2), warmup=0.2, act_quant=False,
+                                   opt_mode="mse")
+            out["w_rec"] = np.array(seen)
+            for n in ("conv1", "conv2", "downsample"):
+                out[n + "_V"] = getattr(block, n).weight_quantizer.alpha.detach().cpu().numpy()
+            qnn.set_quant_state(True, True)
+            with torch.no_grad():
+                qnn(cali[:8])
+            qnn.disable_network_output_quantization()
+            seen.clear()
+            torch.manual_seed(1005)
+            Q.block_reconstruction(qnn, block, cali, batch_size=8, iters=12, act_quant=True,
+                                   opt_mode="mse", lr=4e-4, p=2.4)
+            out["a_rec"] = np.array(seen)
+            aqs = [block.act_quantizer] + [m.act_quantizer for m in (block.conv1, block.conv2,
+                                                                      block.downsample)
+                                           if m.act_quantizer.delta is not None]
+            out["a_delta"] = np.array([float(q.delta) for q in aqs])
+            for k, o in enumerate(opts):
+                for j, p_ in enumerate(o.params):
+                    out[f"opt{k}_m{j}"] = o.state[p_]["exp_avg"].cpu().numpy()
+                    out[f"opt{k}_v{j}"] = o.state[p_]["exp_avg_sq"].cpu().numpy()
+        finally:
+            BR.LossFunction.record, E.SsqAdam.__init__, BR.K.epilogue_loss_bwd = orig_rec, orig_init, orig_tail
+            BR.pinned_weights, BR._fast_loop = orig_pin, orig_fast
+            for k, v in knobs.items():
+                setattr(BR, k, v)
+        runs.append(out)
+        used.append((len(tails), len(pins)))
+    assert used[0] == (0, 0) and used[1][0] > 0 and used[1][1] == 1, used
+    assert runs[0].keys() == runs[1].keys()
+    for k in runs[0]:
+        if k.endswith("_rec"):
+            np.testing.assert_allclose(runs[1][k], runs[0][k], rtol=1e-6, err_msg=k)
+        else:
+            np.testing.assert_array_equal(runs[1][k], runs[0][k], err_msg=k)
+
+
+@pytest.mark.parametrize("graph", [False, True])
 def test_brecq_layer_reconstruction_matches_reference(Q, golden, graph):
     """a22, BRECQ's per-layer path (layer_recon.py:10-104 + its LossFunction :107-170) as
     recon_model calls it for QuantModules: the block's conv1 then the fc (whose captured
