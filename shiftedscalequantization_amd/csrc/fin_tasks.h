@@ -18,11 +18,14 @@
 //     gives lp_loss its own slot and alternates the epilogue backward between two), and
 //     every producer entry first hands pending tasks to its own launch, so at most one
 //     task per producer is pending;
-//   * ssq_adam (which reads gamma^z / phi^z / delta gradients), the lp_loss entry points
-//     and ssq_flush_finalize launch whatever is still pending as one standalone kernel
-//     first; ssq_set_deferred_finalize(0) only flips the flag (it has no stream), so the
-//     caller flushes before turning deferral off -- the recon loop flushes at the end of
-//     its body (kernels.deferred_finalize).
+//   * ssq_adam (which reads gamma^z / phi^z / delta gradients) attaches its update to the
+//     pending tasks when it can (each parameter's step where its gradient is finalised, or
+//     as a kind-3 task when that gradient is already final) and launches them as ONE
+//     kernel -- no Adam launch of its own; otherwise it, the lp_loss entry points and
+//     ssq_flush_finalize launch whatever is still pending as one standalone kernel first;
+//     ssq_set_deferred_finalize(0) only flips the flag (it has no stream), so the caller
+//     flushes before turning deferral off -- the recon loop flushes at the end of its body
+//     (kernels.deferred_finalize).
 #pragma once
 
 #include "ssq_common.h"
@@ -70,7 +73,7 @@ struct FinTask {
   uint32_t a, b, c;          // loss: nblk; epilogue: N, C, nb; rows loss: rows; adam: n
   double m;                  // loss: M
   float* o[4];               // loss: o[0]; epilogue: ggamma, gphi, gdelta, gzp; adam: grad
-  AdamRef ad[2];             // epilogue: the gamma / phi step fused in; adam: ad[0]
+  AdamRef ad[3];             // epilogue: the gamma / phi / delta steps fused in; adam: ad[0]
 };
 constexpr int kMaxFin = 12;
 constexpr int kMaxAdamSegs = 8;      // alpha segments of one prepared alpha-backward launch
@@ -146,6 +149,12 @@ __device__ __forceinline__ void fin_epi(uint32_t bid, const double* __restrict__
     }
     return;
   }
+  float sd[3] = {0.0f, 0.0f, 0.0f};    // the delta step's state, loaded with the sums
+  if (ad[2].p && threadIdx.x == 0) {
+    sd[0] = ad[2].p[0];
+    sd[1] = ad[2].m[0];
+    sd[2] = ad[2].v[0];
+  }
   double a[4] = {0, 0, 0, 0};
   constexpr uint32_t kB = kFinBatch / 4;   // 4 sums per row: keep the registers of the
                                             // host kernels this rides on (occupancy) low
@@ -165,8 +174,10 @@ __device__ __forceinline__ void fin_epi(uint32_t bid, const double* __restrict__
   }
   for (int k = 0; k < 4; ++k) a[k] = block_sum(a[k], red);
   if (threadIdx.x == 0) {
-    if (gdelta) gdelta[0] = (float)(a[0] - a[1]);
+    const float gd = (float)(a[0] - a[1]);
+    if (gdelta) gdelta[0] = gd;
     if (gzp) gzp[0] = (float)(a[2] - a[3]);
+    if (ad[2].p) adam_apply_loaded(ac, ad[2], 0, gd, sd[0], sd[1], sd[2]);
   }
 }
 

@@ -514,7 +514,7 @@ __global__ __launch_bounds__(kBlock) void epilogue_bwd_finalize(
     const double* __restrict__ part, uint32_t N, uint32_t C, uint32_t nb,
     float* __restrict__ ggamma, float* __restrict__ gphi, float* __restrict__ gdelta,
     float* __restrict__ gzp) {
-  const AdamRef none[2] = {AdamRef{}, AdamRef{}};
+  const AdamRef none[3] = {AdamRef{}, AdamRef{}, AdamRef{}};
   fin_epi(blockIdx.x, part, N, C, nb, ggamma, gphi, gdelta, gzp, AdamConst{}, none);
 }
 
@@ -1064,11 +1064,77 @@ extern "C" int ssq_adam_take(ssq_stream_t stream) {
   return done;
 }
 
+// ssq_adam's update riding on the stream's pending finalize tasks (fin_tasks.h): every
+// segment's step is attached where its gradient is finalised (a kind-1 task's gamma / phi /
+// delta output) or, for a gradient some earlier launch finished, as a kind-3 task; the table
+// is then launched as one kernel.  False (nothing launched, nothing taken) when a segment
+// cannot ride: no device hyper, no pending task, a gradient too large for a kind-3 task, or
+// a full table.
+static bool adam_ride(hipStream_t s, int nseg, float* const* p, const float* const* g,
+                      float* const* m, float* const* v, const int64_t* n, const AdamConst& c) {
+  if (!c.hyper) return false;
+  int npend = 0;
+  for (int i = 0; i < g_fin_npending; ++i) npend += g_fin_pending[i].s == s;
+  if (npend == 0 || npend > kMaxFin) return false;
+  FinTable ft = fin_take(s);
+  const int nt = ft.n;
+  bool ok = true;
+  for (int i = 0; i < nseg && ok; ++i) {
+    const AdamRef r{p[i], m[i], v[i]};
+    bool placed = false;
+    for (int t = 0; t < nt && !placed; ++t) {
+      FinTask& k = ft.t[t];
+      if (k.kind != 1) continue;
+      for (int j = 0; j < 4 && !placed && ok; ++j) {
+        if (!k.o[j] || k.o[j] != g[i]) continue;
+        if (j < 3 && (j < 2 ? n[i] == (int64_t)k.b : n[i] == 1)) {
+          k.ad[j] = r;
+          placed = true;
+        } else {
+          ok = false;
+        }
+      }
+    }
+    if (placed || !ok) continue;
+    // a gradient none of the pending tasks writes: final already
+    if (n[i] > (int64_t)kMaxRideAdam || ft.n >= kMaxFin) {
+      ok = false;
+      break;
+    }
+    FinTask t{};
+    t.kind = 3;
+    t.nwg = 1;
+    t.a = (uint32_t)n[i];
+    t.o[0] = (float*)g[i];
+    t.ad[0] = r;
+    ft.t[ft.n++] = t;
+    ft.nwg += 1;
+  }
+  if (!ok) {
+    // put the pending tasks back untouched (same order) for the plain path
+    for (int t = 0; t < nt; ++t) {
+      FinTask k = ft.t[t];
+      k.ad[0] = k.ad[1] = k.ad[2] = AdamRef{};
+      g_fin_pending[g_fin_npending++] = PendingFin{s, k};
+    }
+    return false;
+  }
+  ft.ac = c;
+  hipLaunchKernelGGL(fin_tasks_kernel, dim3(ft.nwg), dim3(kBlock), 0, s, ft);
+  return true;
+}
+
 extern "C" int ssq_adam(int nseg, float* const* p, const float* const* g, float* const* m,
                         float* const* v, const int64_t* n, float one_minus_beta1, float beta2,
                         float one_minus_beta2, float eps, const float* hyper, float neg_step_size,
                         float bias_correction2_sqrt, ssq_stream_t stream) {
   SSQ_REQUIRE(nseg >= 1 && p && g && m && v && n, SSQ_E_ARG, "ssq_adam: bad arrays");
+  for (int i = 0; i < nseg; ++i)
+    SSQ_REQUIRE(p[i] && g[i] && m[i] && v[i] && n[i] >= 1 && n[i] < (1ll << 31), SSQ_E_ARG,
+                "ssq_adam: bad segment %d", i);
+  if (adam_ride((hipStream_t)stream, nseg, p, g, m, v, n,
+                AdamConst{one_minus_beta1, beta2, one_minus_beta2, eps, hyper}))
+    return check_launch("ssq_adam (riding on the pending finalizes)");
   {  // queued gamma / phi / delta gradient finalizes must land before the update reads them
     const int rc = fin_flush((hipStream_t)stream);
     if (rc) return rc;

@@ -161,6 +161,10 @@ def _fast_loop(block, qmodules, opt_params, loss_func, feeder, bucket, iters, ac
     def body_pre():
         with K.deferred_finalize(defer):
             _body_pre()
+            if bucket is None:
+                # world 1: the step inside the deferral, so it rides on the last pending
+                # finalizes (ssq_adam: one launch for both)
+                _step()
 
     def _body_pre():
         cur_inp, cur_out = feeder.gather_lazy()
@@ -198,9 +202,13 @@ def _fast_loop(block, qmodules, opt_params, loss_func, feeder, bucket, iters, ac
         last['rec'] = rec
         last['step'] = True
 
-    def body_post():
+    def _step():
         if last['step']:
             optimizer.step(hyper=hyper)
+
+    def body_post():
+        if bucket is not None:
+            _step()
 
     ws_cache = {}
     with (pinned_weights(qmodules) if pin else contextlib.nullcontext()):
