@@ -349,7 +349,8 @@ int ssq_epilogue_fwd(const float* y, const float* bias, const float* gamma, cons
 /* Its backward from g = dL/d(output), recomputing the pre-activation from y (NCHW, N x C
  * planes of hw): gy = g_t * gamma[c] (or g_t), gres = g_t, ggamma[c] = sum g_t*(y+bias[c]),
  * gphi[c] = sum g_t, gdelta/gzp as ssq_fq_bwd, where g_t is the act quantizer's STE and the
- * ReLU mask applied to g.  Outputs other than gy may be NULL.  Per-(n, c) partials in ws
+ * ReLU mask applied to g.  Every output may be NULL (gy: dL/dy not wanted, only the
+ * per-channel / quantizer sums are produced).  Per-(n, c) partials in ws
  * (ssq_epilogue_bwd_workspace_size(N*C)), reduced in a fixed order.                     */
 size_t ssq_epilogue_bwd_workspace_size(int64_t rows);
 int ssq_epilogue_bwd(const float* g, const float* y, const float* bias, const float* gamma,

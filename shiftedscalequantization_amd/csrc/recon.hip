@@ -390,7 +390,7 @@ __device__ __forceinline__ double epilogue_rows_body(
       const f32x4* Y = (const f32x4*)(y + base);
       const f32x4* G = (const f32x4*)(g + gbase);
       const f32x4* R = RES ? (const f32x4*)(res + base) : nullptr;
-      f32x4* GY = (f32x4*)(gy + base);
+      f32x4* GY = gy ? (f32x4*)(gy + base) : nullptr;
       f32x4* GR = gres ? (f32x4*)(gres + base) : nullptr;
       for (uint32_t v = lane; v < hw / 4; v += kWave) {
         const f32x4 yv = Y[v], gv = G[v];
@@ -401,14 +401,14 @@ __device__ __forceinline__ double epilogue_rows_body(
         elem(wr, yv.y, gv.y, rv.y, oy[1], orr[1]);
         elem(wr, yv.z, gv.z, rv.z, oy[2], orr[2]);
         elem(wr, yv.w, gv.w, rv.w, oy[3], orr[3]);
-        GY[v] = f32x4{oy[0], oy[1], oy[2], oy[3]};
+        if (GY) GY[v] = f32x4{oy[0], oy[1], oy[2], oy[3]};
         if (GR) GR[v] = f32x4{orr[0], orr[1], orr[2], orr[3]};
       }
     } else {
       for (uint32_t j = lane; j < hw; j += kWave) {
         float oy, orr;
         elem(wr, y[base + j], g[gbase + j], RES ? res[base + j] : 0.0f, oy, orr);
-        gy[base + j] = oy;
+        if (gy) gy[base + j] = oy;
         if (gres) gres[base + j] = orr;
       }
     }
@@ -440,7 +440,7 @@ __device__ __forceinline__ double epilogue_rows_body(
         elem(w[k], yv[k].z, gv[k].z, rv[k].z, oy[2], orr[2]);
         elem(w[k], yv[k].w, gv[k].w, rv[k].w, oy[3], orr[3]);
         const int64_t base = (int64_t)(r0 + k) * hw;
-        ((f32x4*)(gy + base))[lane] = f32x4{oy[0], oy[1], oy[2], oy[3]};
+        if (gy) ((f32x4*)(gy + base))[lane] = f32x4{oy[0], oy[1], oy[2], oy[3]};
         if (gres) ((f32x4*)(gres + base))[lane] = f32x4{orr[0], orr[1], orr[2], orr[3]};
       }
       epi_row_sums<QUANT, LOSS>(w[k], lane, part + (int64_t)(r0 + k) * kEpiParts);
@@ -464,7 +464,7 @@ __device__ __forceinline__ double epilogue_rows_body(
         float oy, orr;
         elem(w[k], yv[k], gv[k], rv[k], oy, orr);
         const int64_t base = (int64_t)(r0 + k) * hw;
-        gy[base + lane] = oy;
+        if (gy) gy[base + lane] = oy;
         if (gres) gres[base + lane] = orr;
       }
       epi_row_sums<QUANT, LOSS>(w[k], lane, part + (int64_t)(r0 + k) * kEpiParts);
@@ -876,7 +876,9 @@ static int epilogue_bwd(const char* what, const float* g, const float* y, const 
                         float* loss_out, float* gy, float* gres, float* ggamma, float* gphi, float* gdelta,
                         float* gzp, void* ws, size_t ws_bytes, hipStream_t s) {
   const bool loss = lidx != nullptr;
-  SSQ_REQUIRE(g && y && gy && N >= 1 && C >= 1 && hw >= 1, SSQ_E_ARG, "%s: bad args", what);
+  // gy may be null: dL/dy not wanted (the conv's weight and input are frozen, e.g. the first
+  // conv of a block in BRECQ's act phase) -- only the per-row sums are produced
+  SSQ_REQUIRE(g && y && N >= 1 && C >= 1 && hw >= 1, SSQ_E_ARG, "%s: bad args", what);
   SSQ_REQUIRE(!loss || (loss_out && M >= 1), SSQ_E_ARG, "%s: loss_out and M required", what);
   SSQ_REQUIRE(!loss || lp > 0.0f, SSQ_E_ARG, "%s: loss power p must be > 0", what);
   const bool lp2 = lp == 2.0f;
@@ -890,7 +892,7 @@ static int epilogue_bwd(const char* what, const float* g, const float* y, const 
   SSQ_REQUIRE(ws && ws_bytes >= ssq_epilogue_bwd_workspace_size(rows), SSQ_E_WS,
               "%s: workspace too small", what);
   auto al = [](const void* q) { return ((uintptr_t)q & 15u) == 0; };
-  const bool vec = hw % 4 == 0 && al(g) && al(y) && al(gy) && (!res || al(res)) &&
+  const bool vec = hw % 4 == 0 && al(g) && al(y) && (!gy || al(gy)) && (!res || al(res)) &&
                    (!gres || al(gres));
   SSQ_REQUIRE(relu >= 0 && relu <= 2, SSQ_E_ARG, "%s: activation code %d", what, relu);
   // small planes (<= 64 elements or float4s per row): 4 rows per wave (same bits); not with

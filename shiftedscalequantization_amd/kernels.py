@@ -1047,7 +1047,7 @@ class EpilogueFn(torch.autograd.Function):
             return None if t is None else t.detach().reshape(-1).contiguous()
         b, gm, ph, r = flat(bias), flat(gamma), flat(phi), res
         d, z = flat(delta), flat(zp)
-        gy = torch.empty_like(g)
+        gy = torch.empty_like(g) if need[0] else None
         gres = torch.empty_like(g) if (res is not None and need[4]) else None
         ggm, gm_into = _grad_dest(gamma, C_, dev_, need[2])
         gph, ph_into = _grad_dest(phi, C_, dev_, need[3])
