@@ -1350,12 +1350,14 @@ def test_hard_weights_from_reference_alpha_bit_exact(K, golden, fixture):
         np.testing.assert_array_equal((c - z.reshape(-1, 1, 1, 1)) * d.reshape(-1, 1, 1, 1), what)
 
 
+@pytest.mark.parametrize("p", [2.0, 2.4])
 @pytest.mark.parametrize("hw", [7, 8])
 @pytest.mark.parametrize("quant", [False, True])
 @pytest.mark.parametrize("relu", [0, 1])
-def test_epilogue_loss_bwd_matches_separate_passes(K, hw, quant, relu):
+def test_epilogue_loss_bwd_matches_separate_passes(K, hw, quant, relu, p):
     """ssq_epilogue_loss_bwd (the fused tail) vs the three passes it replaces -- epilogue
-    forward, lp_loss_rows (p = 2) against the cached target rows, epilogue backward -- on
+    forward, lp_loss_rows (p = 2: the shifted-scale loops; 2.4: BRECQ's act phase) against
+    the cached target rows, epilogue backward -- on
     float4 rows (8x8) and scalar rows (7x7), with gamma^z/phi^z, a residual, ReLU or
     identity (InvertedResidual tails) and optionally the per-tensor act quantizer: every
     gradient bit-identical, the loss value to the last ulps (row vs block partials)."""
@@ -1378,7 +1380,7 @@ def test_epilogue_loss_bwd_matches_separate_passes(K, hw, quant, relu):
     # separate passes
     yr = y.clone().requires_grad_(True)
     out = K.epilogue(yr, bias, gamma, phi, res, relu, q)
-    loss1, g1 = K.lp_loss_and_grad(out, K.Rows(cache, idx), 2.0)
+    loss1, g1 = K.lp_loss_and_grad(out, K.Rows(cache, idx), p)
     out.backward(g1)
     sep = [yr.grad, res.grad, gamma.grad, phi.grad] + ([q.delta.grad, q.zero_point.grad] if quant else [])
     sep = [host(t).copy() for t in sep]
@@ -1390,11 +1392,42 @@ def test_epilogue_loss_bwd_matches_separate_passes(K, hw, quant, relu):
     lazy = K.epilogue(y, bias, gamma, phi, res, relu, q, lazy=True)
     assert hasattr(lazy, "_ssq_tail") == (hw * hw % 4 == 0 or K.TAIL_SCALAR)
     tail = (y, bias, gamma, phi, res, relu, q)
-    loss2, gy, gres, ggm, gph, gd, gz = K.epilogue_loss_bwd(tail, K.Rows(cache, idx), N * hw * hw)
+    loss2, gy, gres, ggm, gph, gd, gz = K.epilogue_loss_bwd(tail, K.Rows(cache, idx), N * hw * hw, p)
     fused = [gy, gres, ggm, gph] + ([gd, gz] if quant else [])
     for a, b in zip(sep, fused):
         np.testing.assert_array_equal(a.reshape(-1).view(np.int32), host(b).reshape(-1).view(np.int32))
     close(host(loss2), host(loss1), rtol=1e-6, atol=0)
+
+
+@pytest.mark.parametrize("quant", [False, True])
+def test_epilogue_bwd_without_dy(K, quant):
+    """The epilogue backward of a frozen conv (dL/dy not wanted: BRECQ's act phase) writes no
+    gy and still produces the gamma^z / phi^z / delta / zero-point sums bit-identical to the
+    pass that does write gy."""
+    from shiftedscalequantization_amd.quant.quant_layer import UniformAffineQuantizer
+    gen = torch.Generator().manual_seed(11 + int(quant))
+    N, C, hw = 4, 12, 8
+    y = torch.randn(N, C, hw, hw, generator=gen).cuda()
+    bias = torch.randn(C, generator=gen).cuda()
+    g = torch.randn(N, C, hw, hw, generator=gen).cuda()
+    runs = []
+    for need_dy in (True, False):
+        gamma = (1 + 0.1 * torch.randn(1, C, 1, 1, generator=torch.Generator().manual_seed(3))).cuda().requires_grad_(True)
+        phi = (0.1 * torch.randn(1, C, 1, 1, generator=torch.Generator().manual_seed(4))).cuda().requires_grad_(True)
+        q = None
+        if quant:
+            q = UniformAffineQuantizer(n_bits=4, channel_wise=False, scale_method="max", leaf_param=True).cuda()
+            q.delta = torch.nn.Parameter(torch.tensor(0.19).cuda())
+            q.zero_point = torch.nn.Parameter(torch.tensor(1.0).cuda())
+            q.inited = True
+        yr = y.clone().requires_grad_(need_dy)
+        out = K.epilogue(yr, bias, gamma, phi, None, 1, q)
+        out.backward(g)
+        assert (yr.grad is not None) == need_dy
+        got = [gamma.grad, phi.grad] + ([q.delta.grad, q.zero_point.grad] if quant else [])
+        runs.append([host(t).reshape(-1).view(np.int32).copy() for t in got])
+    for a, b in zip(*runs):
+        np.testing.assert_array_equal(a, b)
 
 
 def test_armed_adam_falls_back_when_not_covered(K):
