@@ -43,4 +43,12 @@ python3 -c "import json,sys; d=json.load(open(sys.argv[1])); print({k: v.get('hb
 timeout -k 10 900 rocprofv3 --kernel-trace --stats --output-format csv -d /tmp/e2eprof -o e2e -- python3 $R/main_imagenet.py --arch resnet18 --n_bits_w 2 --n_bits_a 4 --weight 1.0 --bias_cal True --bias_ch_quant True > $OUT/e2e_prof_$TAG.log 2>&1 || { echo "e2e failed"; tail -20 $OUT/e2e_prof_$TAG.log; exit 1; }
 cp $(find /tmp/e2eprof -name "*kernel_stats.csv" | head -1) $OUT/e2e_kernel_stats_$TAG.csv
 grep "calibration finished" $OUT/e2e_prof_$TAG.log | cut -c1-200
+# the same calibration unprofiled (its wall time), the act phase's iteration anatomy and
+# the short end-to-end runs of the other model families
+cd $R
+timeout -k 10 600 python main_imagenet.py --arch resnet18 --n_bits_w 2 --n_bits_a 4 --weight 1.0 --bias_cal True --bias_ch_quant True > $OUT/e2e_$TAG.log 2>&1 || { echo "e2e failed"; tail -20 $OUT/e2e_$TAG.log; exit 1; }
+grep "calibration finished" $OUT/e2e_$TAG.log | cut -c1-160
+bash tools/act_anatomy.sh $TAG || exit 1
+cd $R
+bash tools/e2e_session.sh $TAG || exit 1
 exit 0
