@@ -814,8 +814,11 @@ def gen_recon_layer_shift(iters=20, n_cali=16, res=16):
     save("recon_layer_shift", **out)
 
 
-def gen_recon_brecq(iters=10, n_cali=16, res=16):
-    """BRECQ block_reconstruction (AdaRound weights), then the act-delta (LSQ) branch."""
+def gen_recon_brecq(iters=10, n_cali=16, res=16, name="recon_brecq"):
+    """BRECQ block_reconstruction (AdaRound weights), then the act-delta (LSQ) branch.
+    name="recon_brecq_long": the same at a long horizon (iters=400), where the AdaRound b
+    schedule (block_recon.py:185-202) reaches its end and the act phase's cosine LR decays to
+    zero (Brecq/main_imagenet.py's CosineAnnealingLR(T_max=iters))."""
     qnn = _build_tiny_qnn()
     torch.manual_seed(1005)
     cali = torch.randn(n_cali, 3, res, res)
@@ -862,7 +865,8 @@ def gen_recon_brecq(iters=10, n_cali=16, res=16):
     out["a_perms"] = np.stack([p.numpy() for p in spy.perms]).astype(np.int64)
     out["a_total_loss"] = np.array([r[1] for r in spy.rec], np.float64)
     out["a_delta"] = np.array([float(q.delta) for q in aqs], np.float32)
-    save("recon_brecq", **out)
+    out["iters"] = np.array([iters])
+    save(name, **out)
 
 
 def gen_recon_layer_brecq(iters=10, n_cali=16, res=16):
@@ -1631,7 +1635,7 @@ if __name__ == "__main__":
     which = sys.argv[1:] or ["uaq", "channelquant", "adaround", "specials", "inpscale", "loss", "recon",
                              "layershift", "brecq", "blocks", "act", "layerfused", "blockshift", "driver",
                              "wmse", "validate", "real", "recon_biascal", "real_biascal", "long",
-                             "layerbrecq", "reallayer"]
+                             "layerbrecq", "reallayer", "brecq_long"]
     torch.set_num_threads(4)
     if "uaq" in which:
         gen_uaq()
@@ -1653,6 +1657,8 @@ if __name__ == "__main__":
         gen_recon_layer_shift()
     if "brecq" in which:
         gen_recon_brecq()
+    if "brecq_long" in which:
+        gen_recon_brecq(iters=400, name="recon_brecq_long")
     if "blocks" in which:
         gen_recon_blocks()
     if "act" in which:

@@ -238,8 +238,12 @@ def test_layer_recon_shiftedScale_matches_reference(Q, golden):
 
 
 @pytest.mark.parametrize("graph", [False, True])
-def test_brecq_block_reconstruction_matches_reference(Q, golden, graph, wgrad):
-    g = golden("recon_brecq")
+@pytest.mark.parametrize("fixture", ["recon_brecq", "recon_brecq_long"])
+def test_brecq_block_reconstruction_matches_reference(Q, golden, graph, wgrad, fixture):
+    """a22 BRECQ block_reconstruction, AdaRound weight phase then the act-delta phase, against
+    the reference's trajectory: 10 iterations, and 400 (recon_brecq_long: the b schedule's
+    end, the act phase's cosine LR decayed to zero)."""
+    g = golden(fixture)
     qnn = build_qnn(Q, g)
     block = qnn.model[3]
     cali = dev(g["cali"])
@@ -293,7 +297,7 @@ def test_brecq_block_reconstruction_matches_reference(Q, golden, graph, wgrad):
         stats["a_total_rel_err"] = np.max(np.abs(np.array(seen) - g["a_total_loss"]) / np.abs(g["a_total_loss"]))
         stats["a_delta_rel_err"] = np.max(np.abs(np.array([float(q.delta) for q in aqs]) - g["a_delta"]) /
                                           np.abs(g["a_delta"]))
-        parity_report(f"a22_brecq_basic[graph={graph},wgrad={wgrad}]", **stats)
+        parity_report(f"a22_brecq_basic[{fixture},graph={graph},wgrad={wgrad}]", **stats)
         np.testing.assert_allclose(seen, g["a_total_loss"], rtol=1e-5)
         np.testing.assert_allclose([float(q.delta) for q in aqs], g["a_delta"], rtol=5e-6)
     finally:
