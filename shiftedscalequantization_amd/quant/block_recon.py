@@ -9,6 +9,7 @@ gradient each iteration -- here as ONE flat RCCL bucket (parallel_dp.GradBucket)
 reference's call crashes because `link` is never imported (block_recon.py:2,102).
 """
 import contextlib
+import os
 
 import torch
 
@@ -38,15 +39,17 @@ def block_reconstruction(model: QuantModel, block: BaseQuantBlock, cali_data: to
 
 GRAPH_WARMUP = 3     # eager iterations before the iteration body is captured
 ITER_HOOK = None     # optional callable(i, iters) at the top of every device-loop iteration (tools)
-# A/B knobs of the device loop, bit-identical either way (tests/test_recon_gpu.py):
+# A/B knobs of the device loop, bit-identical either way (tests/test_recon_gpu.py); the
+# environment's SSQ_BRECQ_FAST=0 starts with all three off (end-to-end A/B runs):
+_FAST = os.environ.get("SSQ_BRECQ_FAST", "1") != "0"
 # the loss / epilogue finalizes ride on the next backward launch (csrc/fin_tasks.h; world 1)
-DEFER_FINALIZE = True
+DEFER_FINALIZE = _FAST
 # a block's final epilogue, the loss (p = 2 weight phase, 2.4 act phase) and the epilogue's
 # backward in one pass (K.epilogue_loss_bwd)
-FUSE_TAIL = True
+FUSE_TAIL = _FAST
 # act phase: every weight quantizer's W_hat computed once for the loop (the weights are
 # frozen there; quant_layer.pinned_weights)
-PIN_WEIGHTS = True
+PIN_WEIGHTS = _FAST
 
 
 def _reconstruct(model, block, qmodules, cali_data, batch_size, iters, weight, opt_mode, asym,
