@@ -48,6 +48,8 @@ grep "calibration finished" $OUT/e2e_prof_$TAG.log | cut -c1-200
 cd $R
 timeout -k 10 600 python main_imagenet.py --arch resnet18 --n_bits_w 2 --n_bits_a 4 --weight 1.0 --bias_cal True --bias_ch_quant True > $OUT/e2e_$TAG.log 2>&1 || { echo "e2e failed"; tail -20 $OUT/e2e_$TAG.log; exit 1; }
 grep "calibration finished" $OUT/e2e_$TAG.log | cut -c1-160
+SSQ_BRECQ_FAST=0 timeout -k 10 600 python main_imagenet.py --arch resnet18 --n_bits_w 2 --n_bits_a 4 --weight 1.0 --bias_cal True --bias_ch_quant True > $OUT/e2e_brecq_plain_$TAG.log 2>&1 || { echo "e2e (plain BRECQ loop) failed"; tail -20 $OUT/e2e_brecq_plain_$TAG.log; exit 1; }
+grep "calibration finished" $OUT/e2e_brecq_plain_$TAG.log | cut -c1-160
 bash tools/act_anatomy.sh $TAG || exit 1
 cd $R
 bash tools/e2e_session.sh $TAG || exit 1
