@@ -814,11 +814,14 @@ def gen_recon_layer_shift(iters=20, n_cali=16, res=16):
     save("recon_layer_shift", **out)
 
 
-def gen_recon_brecq(iters=10, n_cali=16, res=16, name="recon_brecq"):
+def gen_recon_brecq(iters=10, n_cali=16, res=16, name="recon_brecq", affine=False):
     """BRECQ block_reconstruction (AdaRound weights), then the act-delta (LSQ) branch.
     name="recon_brecq_long": the same at a long horizon (iters=400), where the AdaRound b
     schedule (block_recon.py:185-202) reaches its end and the act phase's cosine LR decays to
-    zero (Brecq/main_imagenet.py's CosineAnnealingLR(T_max=iters))."""
+    zero (Brecq/main_imagenet.py's CosineAnnealingLR(T_max=iters)).  affine=True
+    ("recon_brecq_affine"): the block's QuantModules carry seeded non-identity gamma^z /
+    phi^z (alpha_out / beta_out, quant_layer.py:231-238, applied at :258-259) -- the state the
+    act phase meets after a --bias_cal weight phase."""
     qnn = _build_tiny_qnn()
     torch.manual_seed(1005)
     cali = torch.randn(n_cali, 3, res, res)
@@ -827,6 +830,15 @@ def gen_recon_brecq(iters=10, n_cali=16, res=16, name="recon_brecq"):
         qnn(cali[:8])
     block = qnn.model[3]
     out = {"cali": t2n(cali)}
+    if affine:
+        gen = torch.Generator().manual_seed(7)
+        for n in CONVS:
+            m = getattr(block, n)
+            with torch.no_grad():
+                m.alpha_out.copy_(1 + 0.05 * torch.randn(m.alpha_out.shape, generator=gen))
+                m.beta_out.copy_(0.02 * torch.randn(m.beta_out.shape, generator=gen))
+            out[n + "_gamma"] = t2n(m.alpha_out)
+            out[n + "_phi"] = t2n(m.beta_out)
     _dump_block(out, block)
     qms = [m for m in qnn.modules() if isinstance(m, QuantModule)]
     for k, m in enumerate(qms):   # whole-network state: asym capture runs the stem too
@@ -1635,7 +1647,7 @@ if __name__ == "__main__":
     which = sys.argv[1:] or ["uaq", "channelquant", "adaround", "specials", "inpscale", "loss", "recon",
                              "layershift", "brecq", "blocks", "act", "layerfused", "blockshift", "driver",
                              "wmse", "validate", "real", "recon_biascal", "real_biascal", "long",
-                             "layerbrecq", "reallayer", "brecq_long"]
+                             "layerbrecq", "reallayer", "brecq_long", "brecq_affine"]
     torch.set_num_threads(4)
     if "uaq" in which:
         gen_uaq()
@@ -1659,6 +1671,8 @@ if __name__ == "__main__":
         gen_recon_brecq()
     if "brecq_long" in which:
         gen_recon_brecq(iters=400, name="recon_brecq_long")
+    if "brecq_affine" in which:
+        gen_recon_brecq(iters=50, name="recon_brecq_affine", affine=True)
     if "blocks" in which:
         gen_recon_blocks()
     if "act" in which:

@@ -238,14 +238,22 @@ def test_layer_recon_shiftedScale_matches_reference(Q, golden):
 
 
 @pytest.mark.parametrize("graph", [False, True])
-@pytest.mark.parametrize("fixture", ["recon_brecq", "recon_brecq_long"])
+@pytest.mark.parametrize("fixture", ["recon_brecq", "recon_brecq_long", "recon_brecq_affine"])
 def test_brecq_block_reconstruction_matches_reference(Q, golden, graph, wgrad, fixture):
     """a22 BRECQ block_reconstruction, AdaRound weight phase then the act-delta phase, against
-    the reference's trajectory: 10 iterations, and 400 (recon_brecq_long: the b schedule's
-    end, the act phase's cosine LR decayed to zero)."""
+    the reference's trajectory: 10 iterations, 400 (recon_brecq_long: the b schedule's end,
+    the act phase's cosine LR decayed to zero), and 50 with non-identity gamma^z / phi^z
+    (recon_brecq_affine: the --bias_cal flow's act phase -- general K13 epilogue, fused tail
+    at p = 2.4, deferred delta finalize with the riding Adam step, pinned weights)."""
     g = golden(fixture)
     qnn = build_qnn(Q, g)
     block = qnn.model[3]
+    if "conv1_gamma" in g:
+        for n in ("conv1", "conv2", "downsample"):
+            m = getattr(block, n)
+            with torch.no_grad():
+                m.alpha_out.copy_(dev(g[n + "_gamma"]))
+                m.beta_out.copy_(dev(g[n + "_phi"]))
     cali = dev(g["cali"])
     import importlib
     BR = importlib.import_module("shiftedscalequantization_amd.quant.block_recon")
