@@ -82,7 +82,9 @@ def classify(name, sz):
         res = a[0] == "true"
         return "K13_epilogue_fwd", (8 + 4 * res) * A
     if "epilogue_bwd_rows" in name:
-        res, loss = a[0] == "true", a[5] == "true"
+        # RES / LOSS print as bool or int (LOSS: 0 none, 1 p = 2, 2 general p; RES 2: the
+        # downsample's epilogue folded in -- the same bytes, its raw output in place of res)
+        res, loss = a[0] not in ("false", "0"), a[5] not in ("false", "0")
         gres = res and sz["ds"]
         b = (12 + 4 * res + 4 * gres) * A
         return ("K11t_fused_tail" if loss else "K13b_epilogue_bwd"), b
