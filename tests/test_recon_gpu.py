@@ -285,7 +285,12 @@ def test_brecq_block_reconstruction_matches_reference(Q, golden, graph, wgrad, f
             q = getattr(block, n).weight_quantizer
             dv = np.abs(q.alpha.detach().cpu().numpy() - g[n + "_alpha"])
             stats[n + "_V_dev"] = dv.max()
-            stats[n + "_V_walkers"] = assert_walk_bounded(dv, 1e-5, len(seen) * 2e-3, what=n)
+            # 400 iterations (recon_brecq_long) under MIOpen's default stride-2 weight gradients,
+            # which may accumulate with atomics: V entries with a near-zero gradient walk by
+            # a few 1e-5 (observed r4: up to 8e-5 on 1.2 % of conv1's entries in one run, none
+            # in another) -- tight at 1e-4 there, 1e-5 at 10 / 50 iterations
+            tight = 1e-4 if fixture == "recon_brecq_long" else 1e-5
+            stats[n + "_V_walkers"] = assert_walk_bounded(dv, tight, len(seen) * 2e-3, what=n)
             with torch.no_grad():
                 what = q(getattr(block, n).weight).cpu().numpy()
             stats[n + "_hard_flips"] = np.sum(what != g[n + "_what_hard"])
