@@ -366,13 +366,18 @@ int ssq_epilogue_bwd(const float* g, const float* y, const float* bias, const fl
  * dL/d(output) is ssq_lp_loss_rows's gradient at the same p (mean over M) bit for bit; the
  * loss value Sum|out - tgt|^p / M (row partials summed in row order) goes to loss_out.
  * tgt_cache is [*, C, hw], idx holds the N cached rows of this batch.  Outputs and
- * workspace as ssq_epilogue_bwd. */
+ * workspace as ssq_epilogue_bwd.  res_bias / res_gamma+res_phi (any may be NULL; ReLU or
+ * identity only): res is the raw output of the block's downsample conv and its own epilogue
+ * (bias add, gamma^z/phi^z, no activation: ssq_epilogue_fwd's ops) is applied in the pass;
+ * gres is then dL/d(that raw output) and gres_gamma / gres_phi its gamma / phi gradients --
+ * bit-identical to running that epilogue forward and backward as two more passes. */
 int ssq_epilogue_loss_bwd(const float* tgt_cache, const int64_t* idx, int64_t M, float p,
-                          float* loss_out,
-                          const float* y, const float* bias, const float* gamma, const float* phi,
-                          const float* res, int64_t N, int64_t C, int64_t hw, int relu,
-                          const float* delta, const float* zp, int qmin, int qmax, float* gy,
-                          float* gres, float* ggamma, float* gphi, float* gdelta, float* gzp,
+                          float* loss_out, const float* y, const float* bias, const float* gamma,
+                          const float* phi, const float* res, const float* res_bias,
+                          const float* res_gamma, const float* res_phi, int64_t N, int64_t C,
+                          int64_t hw, int relu, const float* delta, const float* zp, int qmin,
+                          int qmax, float* gy, float* gres, float* ggamma, float* gphi,
+                          float* gres_gamma, float* gres_phi, float* gdelta, float* gzp,
                           void* ws, size_t ws_bytes, ssq_stream_t stream);
 
 /* ---------------------------------------------------------------- Adam

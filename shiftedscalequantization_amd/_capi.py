@@ -78,8 +78,9 @@ SIGNATURES = {
     "ssq_epilogue_bwd_workspace_size": (_sz, [_i64]),
     "ssq_epilogue_bwd": (_i, [_p, _p, _p, _p, _p, _p, _i64, _i64, _i64, _i, _p, _p, _i, _i, _p,
                               _p, _p, _p, _p, _p, _p, _sz, _p]),
-    "ssq_epilogue_loss_bwd": (_i, [_p, _p, _i64, _f, _p, _p, _p, _p, _p, _p, _i64, _i64, _i64, _i,
-                                   _p, _p, _i, _i, _p, _p, _p, _p, _p, _p, _p, _sz, _p]),
+    "ssq_epilogue_loss_bwd": (_i, [_p, _p, _i64, _f, _p, _p, _p, _p, _p, _p, _p, _p, _p, _i64,
+                                   _i64, _i64, _i, _p, _p, _i, _i, _p, _p, _p, _p, _p, _p, _p,
+                                   _p, _p, _sz, _p]),
     "ssq_adam": (_i, [_i, _p, _p, _p, _p, _p, _f, _f, _f, _f, _p, _f, _f, _p]),
     "ssq_adam_arm": (_i, [_i, _p, _p, _p, _p, _f, _f, _f, _f, _p, _p]),
     "ssq_adam_take": (_i, [_p]),

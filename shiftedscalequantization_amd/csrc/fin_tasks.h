@@ -34,8 +34,9 @@ namespace ssq {
 
 constexpr int kLossBlocks = 1024;   // lp_loss workgroup partials
 constexpr uint32_t kFinBatch = 16;  // loads in flight per thread in the row-walking finalizes
-constexpr int kEpiParts = 7;        // doubles per (n, c) row of the epilogue backward
-                                    // (slot 6: the fused tail's row loss)
+constexpr int kEpiParts = 9;        // doubles per (n, c) row of the epilogue backward
+                                    // (slot 6: the fused tail's row loss; 7 / 8: its
+                                    // residual epilogue's gamma / phi sums)
 
 // The recon loop's optimizer step applied where each gradient is finalised (ssq_adam_arm):
 // ssq_adam's update, torch.optim.Adam's single-tensor step, op for op.
@@ -71,6 +72,7 @@ struct FinTask {
   uint32_t nwg;              // workgroups the task takes
   const double* part;
   uint32_t a, b, c;          // loss: nblk; epilogue: N, C, nb; rows loss: rows; adam: n
+  uint32_t s0;               // epilogue: the row records' gamma / phi slot pair (0, or 7)
   double m;                  // loss: M
   float* o[4];               // loss: o[0]; epilogue: ggamma, gphi, gdelta, gzp; adam: grad
   AdamRef ad[3];             // epilogue: the gamma / phi / delta steps fused in; adam: ad[0]
@@ -108,7 +110,8 @@ __device__ __forceinline__ void fin_loss(const double* __restrict__ part, int nb
 // (rows in a fixed order, as fq_bwd_finalize)
 constexpr uint32_t kEpiChan = kBlock / 4;
 __device__ __forceinline__ void fin_epi(uint32_t bid, const double* __restrict__ part, uint32_t N,
-                                        uint32_t C, uint32_t nb, float* __restrict__ ggamma,
+                                        uint32_t C, uint32_t nb, uint32_t s0,
+                                        float* __restrict__ ggamma,
                                         float* __restrict__ gphi, float* __restrict__ gdelta,
                                         float* __restrict__ gzp, const AdamConst& ac,
                                         const AdamRef* ad) {
@@ -132,8 +135,8 @@ __device__ __forceinline__ void fin_epi(uint32_t bid, const double* __restrict__
     if (c < C) {
 #pragma unroll 8
       for (uint32_t n = w; n < N; n += 4) {
-        sg += part[((int64_t)n * C + c) * kEpiParts + 0];
-        sp += part[((int64_t)n * C + c) * kEpiParts + 1];
+        sg += part[((int64_t)n * C + c) * kEpiParts + s0];
+        sp += part[((int64_t)n * C + c) * kEpiParts + s0 + 1];
       }
     }
     wsum[w][cl][0] = sg;
@@ -217,7 +220,7 @@ __device__ __forceinline__ void run_fin(const FinTable& ft, uint32_t k) {
       if (t.kind == 0)
         fin_loss(t.part, (int)t.a, t.m, t.o[0]);
       else if (t.kind == 1)
-        fin_epi(k, t.part, t.a, t.b, t.c, t.o[0], t.o[1], t.o[2], t.o[3], ft.ac, t.ad);
+        fin_epi(k, t.part, t.a, t.b, t.c, t.s0, t.o[0], t.o[1], t.o[2], t.o[3], ft.ac, t.ad);
       else if (t.kind == 2)
         fin_loss_rows(t.part, t.a, t.m, t.o[0]);
       else

@@ -272,14 +272,30 @@ __global__ __launch_bounds__(kBlock) void adam_kernel(AdamTable tab, float w1, f
 // the forward's fp32 operations, then dL/d(pre-activation) and the per-row sums.
 struct EpiRow {
   float b, ga, ph;                                   // bias[c], gamma[c], phi[c]
-  double sg = 0, sp = 0, a0 = 0, a1 = 0, a2 = 0, a3 = 0, la = 0;
+  float rb, rga, rph;                                // RES 2: the residual's own epilogue
+  double sg = 0, sp = 0, a0 = 0, a1 = 0, a2 = 0, a3 = 0, la = 0, sgr = 0, spr = 0;
 };
-template <bool RES, int ACT, bool QUANT, bool AFFINE, int LOSS, bool BIAS>
+// Residual epilogue (RES 2): the residual is the raw output of the block's downsample conv,
+// and its own K13 epilogue -- bias add, gamma^z/phi^z, no activation, the ops of
+// bias_act_kernel<false, 0, false, *> -- is applied here (rbias / raffine: which of them the
+// downsample has, uniform).
+struct ResEpi {
+  const float* bias;
+  const float* gamma;
+  const float* phi;
+};
+template <int RES, int ACT, bool QUANT, bool AFFINE, int LOSS, bool BIAS>
 __device__ __forceinline__ void epi_elem(EpiRow& w, float d, float z, float lo, float hi,
-                                         float inv_m, float lp, float yv, float gv_or_tgt,
-                                         float rv, float& oy, float& orr) {
+                                         float inv_m, float lp, bool rbias, bool raffine,
+                                         float yv, float gv_or_tgt, float rv, float& oy,
+                                         float& orr) {
   const float pre = BIAS ? __fadd_rn(yv, w.b) : yv;
   float t = AFFINE ? __fadd_rn(__fmul_rn(pre, w.ga), w.ph) : pre;
+  float prer = rv;
+  if (RES == 2) {
+    prer = rbias ? __fadd_rn(rv, w.rb) : rv;
+    rv = raffine ? __fadd_rn(__fmul_rn(prer, w.rga), w.rph) : prer;
+  }
   if (RES) t = __fadd_rn(t, rv);
   t = act_fwd<ACT>(t);
   float tq = 0.0f, q = 0.0f;
@@ -310,13 +326,22 @@ __device__ __forceinline__ void epi_elem(EpiRow& w, float d, float z, float lo, 
   orr = gt;
   w.sg += (double)gt * (double)pre;
   w.sp += (double)gt;
+  if (RES == 2) {   // the residual epilogue's backward (epi_elem<false, 0, false, *> of g_t)
+    if (raffine) orr = __fmul_rn(gt, w.rga);
+    w.sgr += (double)gt * (double)prer;
+    w.spr += (double)gt;
+  }
 }
 
 // the row's sums over the wave (fixed shuffle tree), written by lane 0 to its kEpiParts slots
-template <bool QUANT, int LOSS>
+template <bool QUANT, int LOSS, int RES>
 __device__ __forceinline__ void epi_row_sums(EpiRow& w, uint32_t lane, double* __restrict__ o) {
   w.sg = wave_sum(w.sg);
   w.sp = wave_sum(w.sp);
+  if (RES == 2) {
+    w.sgr = wave_sum(w.sgr);
+    w.spr = wave_sum(w.spr);
+  }
   if (QUANT) {
     w.a0 = wave_sum(w.a0);
     w.a1 = wave_sum(w.a1);
@@ -332,6 +357,10 @@ __device__ __forceinline__ void epi_row_sums(EpiRow& w, uint32_t lane, double* _
     o[4] = w.a2;
     o[5] = w.a3;
     o[6] = w.la;
+    if (RES == 2) {
+      o[7] = w.sgr;
+      o[8] = w.spr;
+    }
   }
 }
 
@@ -352,20 +381,23 @@ __device__ __forceinline__ void epi_row_sums(EpiRow& w, uint32_t lane, double* _
 // dL/d(output); the output is recomputed (the forward's ops) and dL/d(output) is the
 // lp_loss gradient of K11 (lp_elem, identical ops: LOSS 1 for p = 2, 2 for a general p such
 // as the act phase's 2.4), the loss partial goes to slot 6.
+// RES 2 (fused tail only): res is the downsample conv's raw output and re its epilogue; gres
+// then receives dL/d(that raw output) and the row records' slots 7 / 8 its gamma / phi sums.
 // The wave's RPW rows (bid: the workgroup among the launch's main ones); returns the wave's
 // loss sum (LOSS: its rows' totals in row order), 0 for a wave past the last row.
-template <bool RES, int ACT, bool QUANT, bool AFFINE, bool VEC, int LOSS, int RPW>
+template <int RES, int ACT, bool QUANT, bool AFFINE, bool VEC, int LOSS, int RPW>
 __device__ __forceinline__ double epilogue_rows_body(
     const float* __restrict__ g, const float* __restrict__ y, const float* __restrict__ bias,
     const float* __restrict__ gamma, const float* __restrict__ phi, const float* __restrict__ res,
     uint32_t rows, uint32_t C, uint32_t hw, const float* __restrict__ qdelta,
     const float* __restrict__ qzp, float lo, float hi, float* __restrict__ gy,
     float* __restrict__ gres, double* __restrict__ part, const int64_t* __restrict__ lidx,
-    float inv_m, float lp, uint32_t bid) {
+    float inv_m, float lp, const ResEpi& re, uint32_t bid) {
   const uint32_t lane = threadIdx.x & (kWave - 1);
   const uint32_t r0 = (bid * (kBlock / kWave) + threadIdx.x / kWave) * RPW;
   if (r0 >= rows) return 0.0;
   const float d = QUANT ? qdelta[0] : 1.0f, z = QUANT ? qzp[0] : 0.0f;
+  const bool rbias = RES == 2 && re.bias, raffine = RES == 2 && re.gamma;
   EpiRow w[RPW];
 #pragma unroll
   for (int k = 0; k < RPW; ++k) {
@@ -374,10 +406,13 @@ __device__ __forceinline__ double epilogue_rows_body(
     w[k].b = (bias && ok) ? bias[c] : 0.0f;
     w[k].ga = (AFFINE && ok) ? gamma[c] : 1.0f;
     w[k].ph = (AFFINE && ok) ? phi[c] : 0.0f;
+    w[k].rb = (rbias && ok) ? re.bias[c] : 0.0f;
+    w[k].rga = (raffine && ok) ? re.gamma[c] : 1.0f;
+    w[k].rph = (raffine && ok) ? re.phi[c] : 0.0f;
   }
   auto elem = [&](EpiRow& wr, float yv, float gv, float rv, float& oy, float& orr) {
-    if (bias) epi_elem<RES, ACT, QUANT, AFFINE, LOSS, true>(wr, d, z, lo, hi, inv_m, lp, yv, gv, rv, oy, orr);
-    else epi_elem<RES, ACT, QUANT, AFFINE, LOSS, false>(wr, d, z, lo, hi, inv_m, lp, yv, gv, rv, oy, orr);
+    if (bias) epi_elem<RES, ACT, QUANT, AFFINE, LOSS, true>(wr, d, z, lo, hi, inv_m, lp, rbias, raffine, yv, gv, rv, oy, orr);
+    else epi_elem<RES, ACT, QUANT, AFFINE, LOSS, false>(wr, d, z, lo, hi, inv_m, lp, rbias, raffine, yv, gv, rv, oy, orr);
   };
   // LOSS: row (n, c)'s target is row c of cached sample idx[n] ([*, C, hw] cache)
   auto gbase_of = [&](uint32_t r) -> int64_t {
@@ -412,7 +447,7 @@ __device__ __forceinline__ double epilogue_rows_body(
         if (gres) gres[base + j] = orr;
       }
     }
-    epi_row_sums<QUANT, LOSS>(wr, lane, part + (int64_t)r0 * kEpiParts);
+    epi_row_sums<QUANT, LOSS, RES>(wr, lane, part + (int64_t)r0 * kEpiParts);
     return wr.la;
   }
   // RPW rows, one element (float4) per lane and row, all loads first
@@ -443,7 +478,7 @@ __device__ __forceinline__ double epilogue_rows_body(
         if (gy) ((f32x4*)(gy + base))[lane] = f32x4{oy[0], oy[1], oy[2], oy[3]};
         if (gres) ((f32x4*)(gres + base))[lane] = f32x4{orr[0], orr[1], orr[2], orr[3]};
       }
-      epi_row_sums<QUANT, LOSS>(w[k], lane, part + (int64_t)(r0 + k) * kEpiParts);
+      epi_row_sums<QUANT, LOSS, RES>(w[k], lane, part + (int64_t)(r0 + k) * kEpiParts);
       wl += w[k].la;
     }
   } else {
@@ -467,21 +502,21 @@ __device__ __forceinline__ double epilogue_rows_body(
         if (gy) gy[base + lane] = oy;
         if (gres) gres[base + lane] = orr;
       }
-      epi_row_sums<QUANT, LOSS>(w[k], lane, part + (int64_t)(r0 + k) * kEpiParts);
+      epi_row_sums<QUANT, LOSS, RES>(w[k], lane, part + (int64_t)(r0 + k) * kEpiParts);
       wl += w[k].la;
     }
   }
   return wl;
 }
 
-template <bool RES, int ACT, bool QUANT, bool AFFINE, bool VEC, int LOSS, int RPW>
+template <int RES, int ACT, bool QUANT, bool AFFINE, bool VEC, int LOSS, int RPW>
 __global__ __launch_bounds__(kBlock) void epilogue_bwd_rows(
     const float* __restrict__ g, const float* __restrict__ y, const float* __restrict__ bias,
     const float* __restrict__ gamma, const float* __restrict__ phi, const float* __restrict__ res,
     uint32_t rows, uint32_t C, uint32_t hw, const float* __restrict__ qdelta,
     const float* __restrict__ qzp, float lo, float hi, float* __restrict__ gy,
     float* __restrict__ gres, double* __restrict__ part, FinTable fin, uint32_t nmain,
-    const int64_t* __restrict__ lidx, float inv_m, float lp) {
+    const int64_t* __restrict__ lidx, float inv_m, float lp, ResEpi re) {
   // queued finalize tasks ride on this launch: its first workgroups (dispatched first, so
   // they run beside the main work instead of after it)
   (void)nmain;
@@ -492,7 +527,7 @@ __global__ __launch_bounds__(kBlock) void epilogue_bwd_rows(
   const uint32_t bid = blockIdx.x - fin.nwg;
   const double wl = epilogue_rows_body<RES, ACT, QUANT, AFFINE, VEC, LOSS, RPW>(
       g, y, bias, gamma, phi, res, rows, C, hw, qdelta, qzp, lo, hi, gy, gres, part, lidx, inv_m,
-      lp, bid);
+      lp, re, bid);
   if (!LOSS) return;
   // the fused tail's loss: one partial per workgroup (its waves in order) after the rows'
   // records, so the finalize sums rows / (4 RPW) values instead of every row's
@@ -515,7 +550,7 @@ __global__ __launch_bounds__(kBlock) void epilogue_bwd_finalize(
     float* __restrict__ ggamma, float* __restrict__ gphi, float* __restrict__ gdelta,
     float* __restrict__ gzp) {
   const AdamRef none[3] = {AdamRef{}, AdamRef{}, AdamRef{}};
-  fin_epi(blockIdx.x, part, N, C, nb, ggamma, gphi, gdelta, gzp, AdamConst{}, none);
+  fin_epi(blockIdx.x, part, N, C, nb, 0, ggamma, gphi, gdelta, gzp, AdamConst{}, none);
 }
 
 // the queued finalize tasks of a stream as one standalone launch
@@ -870,12 +905,20 @@ extern "C" size_t ssq_epilogue_bwd_workspace_size(int64_t rows) {
 // (tgt = the cache of target rows, idx = this batch's rows: dL/d(output) of the lp_loss
 // (power lp) computed in the pass, its value finalised into loss_out).
 static int epilogue_bwd(const char* what, const float* g, const float* y, const float* bias,
-                        const float* gamma, const float* phi, const float* res, int64_t N,
-                        int64_t C, int64_t hw, int relu, const float* delta, const float* zp,
-                        int qmin, int qmax, const int64_t* lidx, int64_t M, float lp,
-                        float* loss_out, float* gy, float* gres, float* ggamma, float* gphi, float* gdelta,
-                        float* gzp, void* ws, size_t ws_bytes, hipStream_t s) {
+                        const float* gamma, const float* phi, const float* res, const ResEpi& re,
+                        int64_t N, int64_t C, int64_t hw, int relu, const float* delta,
+                        const float* zp, int qmin, int qmax, const int64_t* lidx, int64_t M,
+                        float lp, float* loss_out, float* gy, float* gres, float* ggamma,
+                        float* gphi, float* grgamma, float* grphi, float* gdelta, float* gzp,
+                        void* ws, size_t ws_bytes, hipStream_t s) {
   const bool loss = lidx != nullptr;
+  // the residual's own epilogue folded in (fused tail only)
+  const bool res2 = res && (re.bias || re.gamma);
+  SSQ_REQUIRE(!re.gamma == !re.phi && (!(grgamma || grphi) || re.gamma), SSQ_E_ARG,
+              "%s: residual gamma/phi go together (and their gradients need them)", what);
+  SSQ_REQUIRE(!(re.bias || re.gamma) || (res && loss && relu <= 1), SSQ_E_ARG,
+              "%s: a residual epilogue needs the residual, the fused loss and ReLU / identity",
+              what);
   // gy may be null: dL/dy not wanted (the conv's weight and input are frozen, e.g. the first
   // conv of a block in BRECQ's act phase) -- only the per-row sums are produced
   SSQ_REQUIRE(g && y && N >= 1 && C >= 1 && hw >= 1, SSQ_E_ARG, "%s: bad args", what);
@@ -897,7 +940,8 @@ static int epilogue_bwd(const char* what, const float* g, const float* y, const 
   SSQ_REQUIRE(relu >= 0 && relu <= 2, SSQ_E_ARG, "%s: activation code %d", what, relu);
   // small planes (<= 64 elements or float4s per row): 4 rows per wave (same bits); not with
   // the act quantizer's four extra sums per row (3-4 waves per SIMD instead of 7-8)
-  const bool multi = (vec ? hw / 4 : hw) <= kWave && !delta && epi_multi_row() >= (loss ? 2 : 1);
+  const bool multi = (vec ? hw / 4 : hw) <= kWave && !delta && !res2 &&
+                     epi_multi_row() >= (loss ? 2 : 1);
   const int64_t rpw = multi ? 4 : 1;
   const int64_t waves = (rows + rpw - 1) / rpw;
   const uint32_t nmain = (uint32_t)((waves + kBlock / kWave - 1) / (kBlock / kWave));
@@ -911,7 +955,7 @@ static int epilogue_bwd(const char* what, const float* g, const float* y, const 
 #define SSQ_EB0(R, A, Q, F, V, L, P)                                                              \
   hipLaunchKernelGGL((epilogue_bwd_rows<R, A, Q, F, V, L, P>), grid, dim3(kBlock), 0, s, g, y,    \
                      bias, gamma, phi, res, (uint32_t)rows, (uint32_t)C, (uint32_t)hw, delta, zp, \
-                     lo, hi, gy, gres, part, fin, nmain, lidx, inv_m, lp)
+                     lo, hi, gy, gres, part, fin, nmain, lidx, inv_m, lp, re2)
 #define SSQ_EB(R, A, Q, F, V, L) \
   if (multi) SSQ_EB0(R, A, Q, F, V, L, ((Q) ? 1 : 4)); else SSQ_EB0(R, A, Q, F, V, L, 1);
 #define SSQ_EBL(R, A, Q, F, V) \
@@ -923,11 +967,27 @@ static int epilogue_bwd(const char* what, const float* g, const float* y, const 
   if (gamma) { SSQ_EB1(R, A, Q, true) } else { SSQ_EB1(R, A, Q, false) }
 #define SSQ_EB3(R, A) \
   if (delta) { SSQ_EB2(R, A, true) } else { SSQ_EB2(R, A, false) }
-  if (res) {
+// RES 2: the fused tail only, ReLU / identity, one row per wave
+#define SSQ_EBLR(A, Q, F, V) \
+  if (lp2) { SSQ_EB0(2, A, Q, F, V, 1, 1); } else { SSQ_EB0(2, A, Q, F, V, 2, 1); }
+#define SSQ_EBR1(A, Q, F) \
+  if (vec) { SSQ_EBLR(A, Q, F, true) } else { SSQ_EBLR(A, Q, F, false) }
+#define SSQ_EBR2(A, Q) \
+  if (gamma) { SSQ_EBR1(A, Q, true) } else { SSQ_EBR1(A, Q, false) }
+#define SSQ_EBR3(A) \
+  if (delta) { SSQ_EBR2(A, true) } else { SSQ_EBR2(A, false) }
+  const ResEpi re2 = res2 ? re : ResEpi{nullptr, nullptr, nullptr};
+  if (res2) {
+    if (relu) { SSQ_EBR3(1) } else { SSQ_EBR3(0) }
+  } else if (res) {
     if (relu == 2) { SSQ_EB3(true, 2) } else if (relu) { SSQ_EB3(true, 1) } else { SSQ_EB3(true, 0) }
   } else {
     if (relu == 2) { SSQ_EB3(false, 2) } else if (relu) { SSQ_EB3(false, 1) } else { SSQ_EB3(false, 0) }
   }
+#undef SSQ_EBR3
+#undef SSQ_EBR2
+#undef SSQ_EBR1
+#undef SSQ_EBLR
 #undef SSQ_EB3
 #undef SSQ_EB2
 #undef SSQ_EB1
@@ -957,6 +1017,31 @@ static int epilogue_bwd(const char* what, const float* g, const float* y, const 
     if (rc) return rc;
   }
   adam_log(s, gamma, phi, ggamma, gphi);
+  if (res2 && (grgamma || grphi)) {
+    // the residual epilogue's gamma / phi: its own finalize task over slots 7 / 8
+    adam_log(s, re.gamma, re.phi, grgamma, grphi);
+    FinTask t{};
+    t.kind = 1;
+    t.nwg = (unsigned)((C + kEpiChan - 1) / kEpiChan);
+    t.part = part;
+    t.a = (uint32_t)N;
+    t.b = (uint32_t)C;
+    t.c = t.nwg;
+    t.s0 = 7;
+    t.o[0] = grgamma;
+    t.o[1] = grphi;
+    if (fin_defer_on()) {
+      rc = fin_push(s, t);
+    } else {
+      FinTable one{};
+      one.t[0] = t;
+      one.n = 1;
+      one.nwg = t.nwg;
+      hipLaunchKernelGGL(fin_tasks_kernel, dim3(one.nwg), dim3(kBlock), 0, s, one);
+      rc = check_launch(what);
+    }
+    if (rc) return rc;
+  }
   if (ggamma || gphi || gdelta || gzp) {
     // blocks [0, nb) only when gamma / phi are wanted; block nb (the act quantizer's four
     // sums over every row, one workgroup) only when delta / zp are
@@ -989,23 +1074,26 @@ extern "C" int ssq_epilogue_bwd(const float* g, const float* y, const float* bia
                                 const float* zp, int qmin, int qmax, float* gy, float* gres,
                                 float* ggamma, float* gphi, float* gdelta, float* gzp, void* ws,
                                 size_t ws_bytes, ssq_stream_t stream) {
-  return epilogue_bwd("ssq_epilogue_bwd", g, y, bias, gamma, phi, res, N, C, hw, relu, delta, zp,
-                      qmin, qmax, nullptr, 0, 2.0f, nullptr, gy, gres, ggamma, gphi, gdelta, gzp, ws,
-                      ws_bytes, (hipStream_t)stream);
+  return epilogue_bwd("ssq_epilogue_bwd", g, y, bias, gamma, phi, res,
+                      ResEpi{nullptr, nullptr, nullptr}, N, C, hw, relu, delta, zp, qmin, qmax,
+                      nullptr, 0, 2.0f, nullptr, gy, gres, ggamma, gphi, nullptr, nullptr, gdelta,
+                      gzp, ws, ws_bytes, (hipStream_t)stream);
 }
 
 extern "C" int ssq_epilogue_loss_bwd(const float* tgt_cache, const int64_t* idx, int64_t M,
                                      float p, float* loss_out, const float* y, const float* bias,
                                      const float* gamma, const float* phi, const float* res,
-                                     int64_t N, int64_t C, int64_t hw, int relu,
-                                     const float* delta, const float* zp, int qmin, int qmax,
-                                     float* gy, float* gres, float* ggamma, float* gphi,
-                                     float* gdelta, float* gzp, void* ws, size_t ws_bytes,
-                                     ssq_stream_t stream) {
+                                     const float* res_bias, const float* res_gamma,
+                                     const float* res_phi, int64_t N, int64_t C, int64_t hw,
+                                     int relu, const float* delta, const float* zp, int qmin,
+                                     int qmax, float* gy, float* gres, float* ggamma, float* gphi,
+                                     float* gres_gamma, float* gres_phi, float* gdelta,
+                                     float* gzp, void* ws, size_t ws_bytes, ssq_stream_t stream) {
   SSQ_REQUIRE(idx, SSQ_E_ARG, "ssq_epilogue_loss_bwd: idx is required");
-  return epilogue_bwd("ssq_epilogue_loss_bwd", tgt_cache, y, bias, gamma, phi, res, N, C, hw,
-                      relu, delta, zp, qmin, qmax, idx, M, p, loss_out, gy, gres, ggamma, gphi,
-                      gdelta, gzp, ws, ws_bytes, (hipStream_t)stream);
+  return epilogue_bwd("ssq_epilogue_loss_bwd", tgt_cache, y, bias, gamma, phi, res,
+                      ResEpi{res_bias, res_gamma, res_phi}, N, C, hw, relu, delta, zp, qmin, qmax,
+                      idx, M, p, loss_out, gy, gres, ggamma, gphi, gres_gamma, gres_phi, gdelta,
+                      gzp, ws, ws_bytes, (hipStream_t)stream);
 }
 
 template <int ACT>

@@ -900,6 +900,33 @@ class BiasActFn(torch.autograd.Function):
         return gin, None, (gin if ctx.needs_input_grad[2] else None), None
 
 
+class LazyRes:
+    """A block's downsample branch whose epilogue is deferred to the block's fused tail: the
+    downsample conv's raw output y and its epilogue's inputs (bias, gamma^z / phi^z, no
+    activation, no act quantizer).  The tail's pass applies that epilogue itself
+    (ssq_epilogue_loss_bwd's res_* arguments) and returns dL/dy; anywhere else the residual is
+    materialised with exactly the ops QuantModule.forward runs for it."""
+
+    def __init__(self, y, bias, gamma, phi):
+        self.y, self.bias, self.gamma, self.phi = y, bias, gamma, phi
+
+    def materialize(self):
+        if self.gamma is not None:
+            return epilogue(self.y, self.bias, self.gamma, self.phi, None, 0, None)
+        if self.bias is not None:
+            return bias_act(self.y, self.bias, None, 0)
+        return self.y
+
+
+def materialize(res):
+    return res.materialize() if isinstance(res, LazyRes) else res
+
+
+# A/B knob: the downsample branch's epilogue deferred into the block's fused tail (LazyRes;
+# bit-identical either way)
+FOLD_RESIDUAL = os.environ.get("SSQ_FOLD_RESIDUAL", "1") != "0"
+
+
 # The fused tail also on planes whose rows are not float4 rows (ResNet-18 layer4's 7x7), in
 # the kernel's scalar-row form: layer4.1 2114 it/s against 2085 with the three separate
 # passes, layer4.0 unchanged (profiles/r3_ab_knobs.txt).  A/B knob: SSQ_TAIL_SCALAR=0.
@@ -909,6 +936,8 @@ TAIL_SCALAR = os.environ.get("SSQ_TAIL_SCALAR", "1") != "0"
 def _tail_ok(y, res):
     """The fused tail (epilogue_loss_bwd) takes contiguous NCHW float4 rows (hw % 4 == 0,
     16-B aligned), and scalar rows when TAIL_SCALAR is set."""
+    if isinstance(res, LazyRes):
+        res = res.y
     if not (y.dim() == 4 and y.is_contiguous() and (res is None or res.is_contiguous())):
         return False
     if TAIL_SCALAR:
@@ -924,6 +953,7 @@ def bias_act(y, bias=None, res=None, relu=True, lazy=False):
         out = torch.empty_like(y)
         out._ssq_tail = (y, bias, None, None, res, int(relu), None)
         return out
+    res = materialize(res)
     out = BiasActFn.apply(y, bias, res, int(relu))
     if int(relu) == 1:
         # lets a loss that folds the ReLU backward into its own pass (lp_loss relu_mask)
@@ -998,6 +1028,7 @@ class BiasActQuantFn(torch.autograd.Function):
 
 def bias_act_quant(y, bias, res, relu, delta, zp, n_bits, sym=False):
     """bias_act followed by fake_quant(delta, zp) in one pass (per-tensor quantizer)."""
+    res = materialize(res)
     keep = torch.is_grad_enabled() and any(
         t is not None and t.requires_grad for t in (y, res, delta, zp))
     return BiasActQuantFn.apply(y, bias, res, delta, zp, int(relu), n_bits, sym, keep)
@@ -1137,10 +1168,11 @@ TAIL_LAZY = [None]
 def epilogue(y, bias, gamma, phi, res, relu, q=None, lazy=False):
     """EpilogueFn with q an (initialised, per-tensor) act quantizer or None.  lazy: see
     TAIL_LAZY (the placeholder must only reach epilogue_loss_bwd)."""
-    if lazy and _tail_ok(y, res):
+    if lazy and int(relu) in (0, 1) and _tail_ok(y, res):
         out = torch.empty_like(y)
         out._ssq_tail = (y, bias, gamma, phi, res, int(relu), q)
         return out
+    res = materialize(res)
     if q is None:
         return EpilogueFn.apply(y, bias, gamma, phi, res, None, None, int(relu), 8, False)
     return EpilogueFn.apply(y, bias, gamma, phi, res, q.delta, q.zero_point, int(relu), q.n_bits,
@@ -1150,12 +1182,17 @@ def epilogue(y, bias, gamma, phi, res, relu, q=None, lazy=False):
 def epilogue_loss_bwd(tail, tgt, M, p=2.0):
     """The fused tail (ssq_epilogue_loss_bwd): for a lazy epilogue placeholder's inputs and a
     Rows target, the lp_loss value at power p (1-element device tensor, mean over M) and the
-    gradients the epilogue's backward returns -- (loss, gy, gres, ggamma, gphi, gdelta, gzp),
-    None where the input needs none -- bit-identical to epilogue -> lp_loss_and_grad ->
-    backward."""
+    gradients the epilogue's backward returns -- (loss, gy, gres, ggamma, gphi, gdelta, gzp,
+    gres_gamma, gres_phi), None where the input needs none -- bit-identical to epilogue ->
+    lp_loss_and_grad -> backward.  A LazyRes residual (the downsample's deferred epilogue) is
+    applied in the same pass: gres is then dL/d(its raw conv output) and gres_gamma /
+    gres_phi its gamma^z / phi^z gradients."""
     y, bias, gamma, phi, res, relu, q = tail
     if not isinstance(tgt, Rows):
         raise A.SSQError("epilogue_loss_bwd: the target must be a Rows view of the cache")
+    lres = res if isinstance(res, LazyRes) else None
+    if lres is not None:
+        res = lres.y
     y, yp, bp, rp, C_, hw, _ = _epilogue_layout(y, bias, res)
     dev_ = y.device
     cache, cp = fptr(tgt.cache.detach(), "tgt cache")
@@ -1176,14 +1213,30 @@ def epilogue_loss_bwd(tail, tgt, M, p=2.0):
     gres = torch.empty_like(y) if (res is not None and res.requires_grad) else None
     ggm, gm_into = _grad_dest(gamma, C_, dev_, gamma is not None and gamma.requires_grad)
     gph, ph_into = _grad_dest(phi, C_, dev_, phi is not None and phi.requires_grad)
+    rbp = rgp = rphp = None
+    grg, grph, rg_into, rph_into = None, None, False, False
+    if lres is not None:
+        if lres.bias is not None:
+            rb, rbp = fptr(lres.bias.detach().reshape(-1), "residual bias")
+            if rb.numel() != C_:
+                raise A.SSQError("epilogue_loss_bwd: residual bias must have one value per channel")
+        if lres.gamma is not None:
+            rg, rgp = fptr(lres.gamma.detach().reshape(-1), "residual gamma")
+            rph_, rphp = fptr(lres.phi.detach().reshape(-1), "residual phi")
+            if rg.numel() != C_ or rph_.numel() != C_:
+                raise A.SSQError("epilogue_loss_bwd: residual gamma / phi must have one value per channel")
+            grg, rg_into = _grad_dest(lres.gamma, C_, dev_, lres.gamma.requires_grad)
+            grph, rph_into = _grad_dest(lres.phi, C_, dev_, lres.phi.requires_grad)
     gd = torch.empty(1, device=dev_) if (q is not None and q.delta.requires_grad) else None
     gz = torch.empty(1, device=dev_) if (q is not None and q.zero_point.requires_grad) else None
     ws, wsn = workspace(query("ssq_epilogue_bwd_workspace_size", N * C_), dev_, _epi_slot())
     call("ssq_epilogue_loss_bwd", cp, _vp(idx), int(M), float(p), _vp(loss), yp, bp, _vp(gm),
-         _vp(ph), rp, N, C_, hw, int(relu), _vp(d), _vp(z), lo, hi, _vp(gy), _vp(gres), _vp(ggm),
-         _vp(gph), _vp(gd), _vp(gz), ws, wsn, stream_of(y))
+         _vp(ph), rp, rbp, rgp, rphp, N, C_, hw, int(relu), _vp(d), _vp(z), lo, hi, _vp(gy),
+         _vp(gres), _vp(ggm), _vp(gph), _vp(grg), _vp(grph), _vp(gd), _vp(gz), ws, wsn,
+         stream_of(y))
     # a gradient written into its GRAD_INTO slice is not handed back (already in place)
-    return loss, gy, gres, None if gm_into else ggm, None if ph_into else gph, gd, gz
+    return (loss, gy, gres, None if gm_into else ggm, None if ph_into else gph, gd, gz,
+            None if rg_into else grg, None if rph_into else grph)
 
 
 def adam_step(params, grads, exp_avgs, exp_avg_sqs, beta1, beta2, eps, hyper=None,

@@ -81,12 +81,17 @@ def backward_tail(tail, grads):
     their graphs; gamma^z / phi^z / the act quantizer's delta and zero point are leaves here
     (or views of leaves), accumulated as autograd would."""
     y, bias, gamma, phi, res, relu, q = tail
-    _, gy, gres, ggm, gph, gd, gz = grads
+    _, gy, gres, ggm, gph, gd, gz, grg, grph = grads
     roots, grs = [y], [gy]
+    leaves = [(gamma, ggm), (phi, gph)]
+    if isinstance(res, K.LazyRes):
+        # the downsample's deferred epilogue: gres is dL/d(its conv output); its gamma^z /
+        # phi^z are leaves like the block's own
+        leaves += [(res.gamma, grg), (res.phi, grph)]
+        res = res.y
     if gres is not None:
         roots.append(res)
         grs.append(gres)
-    leaves = [(gamma, ggm), (phi, gph)]
     if q is not None:
         leaves += [(q.delta, gd), (q.zero_point, gz)]
     for t, g in leaves:

@@ -182,7 +182,8 @@ def _fast_loop(block, qmodules, opt_params, loss_func, feeder, bucket, iters, ac
             # autograd resumes at the epilogue's inputs
             grads = K.epilogue_loss_bwd(tail, cur_out, K._lp_M(out, "none"), p)
             y, _, gamma, phi, res, _, q = tail
-            live = [y, res, gamma, phi] + ([q.delta, q.zero_point] if q is not None else [])
+            live = [y, gamma, phi] + ([q.delta, q.zero_point] if q is not None else [])
+            live += [res.y, res.gamma, res.phi] if isinstance(res, K.LazyRes) else [res]
             last['rec'] = grads[0]
             last['step'] = any(t is not None and t.requires_grad for t in live)
             if last['step']:

@@ -73,6 +73,21 @@ class BaseQuantBlock(nn.Module):
             out = self.act_quantizer(out)
         return out
 
+    def _residual(self, ds, x):
+        """ds(x), the downsample branch.  For the block the recon loop fuses (K.TAIL_LAZY)
+        and a downsample whose forward ends in its K13 epilogue alone (bias, gamma^z/phi^z,
+        no activation, no act quantizer), the conv's raw output and that epilogue's inputs
+        instead (K.LazyRes): the block tail's fused pass applies the epilogue -- the same ops
+        -- and runs its backward, two activation-sized launches fewer; anything else
+        materialises it exactly as ds.forward would."""
+        if (K.FOLD_RESIDUAL and K.TAIL_LAZY[0] is self and not self._forward_hooks
+                and not ds._forward_hooks and ds.epilogue_fusable(x) and ds.act_code() == 0
+                and not (ds.use_act_quant and not ds.disable_act_quant)):
+            raw, bias = ds.forward_raw(x)
+            gamma, phi = ds.affine()
+            return K.LazyRes(raw, bias, gamma, phi)
+        return ds(x)
+
     def _tail(self, last, inp, residual):
         """last(inp) (+ residual) -> block activation -> block act quant.  When `last` has
         no activation of its own and the block's is ReLU / identity, its bias add, the
@@ -103,6 +118,7 @@ class BaseQuantBlock(nn.Module):
             if self.use_act_quant:
                 out = self.act_quantizer(out)
             return out
+        residual = K.materialize(residual)
         out = last(inp)
         if residual is not None:
             out = out + residual
@@ -126,7 +142,7 @@ class QuantBasicBlock(BaseQuantBlock):
     def forward(self, x):
         if self.cache_features == 'if':
             self.cached_inp_features += [self._cache(x)]
-        residual = x if self.downsample is None else self.downsample(x)
+        residual = x if self.downsample is None else self._residual(self.downsample, x)
         out = self._tail(self.conv2, self.conv1(x), residual)
         if self.cache_features == 'of':
             self.cached_out_features += [self._cache(out)]
@@ -157,7 +173,7 @@ class QuantBottleneck(BaseQuantBlock):
     def forward(self, x):
         if self.cache_features == 'if':
             self.cached_inp_features += [self._cache(x)]
-        residual = x if self.downsample is None else self.downsample(x)
+        residual = x if self.downsample is None else self._residual(self.downsample, x)
         out = self._tail(self.conv3, self.conv2(self.conv1(x)), residual)
         if self.cache_features == 'of':
             self.cached_out_features += [self._cache(out)]
@@ -183,7 +199,7 @@ class QuantResBottleneckBlock(BaseQuantBlock):
     def forward(self, x):
         if self.cache_features == 'if':
             self.cached_inp_features += [self._cache(x)]
-        residual = self.downsample(x) if self.proj_block else x
+        residual = self._residual(self.downsample, x) if self.proj_block else x
         out = self._tail(self.conv3, self.conv2(self.conv1(x)), residual)
         if self.cache_features == 'of':
             self.cached_out_features += [self._cache(out)]

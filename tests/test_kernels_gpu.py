@@ -1350,17 +1350,21 @@ def test_hard_weights_from_reference_alpha_bit_exact(K, golden, fixture):
         np.testing.assert_array_equal((c - z.reshape(-1, 1, 1, 1)) * d.reshape(-1, 1, 1, 1), what)
 
 
+@pytest.mark.parametrize("resepi", [False, True])
 @pytest.mark.parametrize("p", [2.0, 2.4])
 @pytest.mark.parametrize("hw", [7, 8])
 @pytest.mark.parametrize("quant", [False, True])
 @pytest.mark.parametrize("relu", [0, 1])
-def test_epilogue_loss_bwd_matches_separate_passes(K, hw, quant, relu, p):
+def test_epilogue_loss_bwd_matches_separate_passes(K, hw, quant, relu, p, resepi):
     """ssq_epilogue_loss_bwd (the fused tail) vs the three passes it replaces -- epilogue
     forward, lp_loss_rows (p = 2: the shifted-scale loops; 2.4: BRECQ's act phase) against
     the cached target rows, epilogue backward -- on
     float4 rows (8x8) and scalar rows (7x7), with gamma^z/phi^z, a residual, ReLU or
     identity (InvertedResidual tails) and optionally the per-tensor act quantizer: every
-    gradient bit-identical, the loss value to the last ulps (row vs block partials)."""
+    gradient bit-identical, the loss value to the last ulps (row vs block partials).
+    resepi: the residual is a downsample branch whose own epilogue (bias, gamma^z/phi^z, no
+    activation) the tail applies (K.LazyRes) instead of two more passes: dL/d(its conv
+    output) and its gamma / phi gradients bit-identical too."""
     from shiftedscalequantization_amd.quant.quant_layer import UniformAffineQuantizer
     gen = torch.Generator().manual_seed(hw * 4 + int(quant) * 2 + relu)
     N, C = 6, 20
@@ -1371,6 +1375,11 @@ def test_epilogue_loss_bwd_matches_separate_passes(K, hw, quant, relu, p):
     phi = (0.1 * torch.randn(1, C, 1, 1, generator=gen)).cuda().requires_grad_(True)
     cache = torch.randn(15, C, hw, hw, generator=gen).relu().cuda()
     idx = torch.tensor([3, 14, 0, 7, 7, 9], dtype=torch.int64).cuda()
+    if resepi:
+        yds = torch.randn(N, C, hw, hw, generator=gen).cuda().requires_grad_(True)
+        bds = torch.randn(C, generator=gen).cuda()
+        gds = (1 + 0.1 * torch.randn(1, C, 1, 1, generator=gen)).cuda().requires_grad_(True)
+        pds = (0.1 * torch.randn(1, C, 1, 1, generator=gen)).cuda().requires_grad_(True)
     q = None
     if quant:
         q = UniformAffineQuantizer(n_bits=4, channel_wise=False, scale_method="max", leaf_param=True).cuda()
@@ -1379,21 +1388,27 @@ def test_epilogue_loss_bwd_matches_separate_passes(K, hw, quant, relu, p):
         q.inited = True
     # separate passes
     yr = y.clone().requires_grad_(True)
-    out = K.epilogue(yr, bias, gamma, phi, res, relu, q)
+    res_in = K.epilogue(yds, bds, gds, pds, None, 0, None) if resepi else res
+    out = K.epilogue(yr, bias, gamma, phi, res_in, relu, q)
     loss1, g1 = K.lp_loss_and_grad(out, K.Rows(cache, idx), p)
     out.backward(g1)
-    sep = [yr.grad, res.grad, gamma.grad, phi.grad] + ([q.delta.grad, q.zero_point.grad] if quant else [])
+    sep = [yr.grad, yds.grad if resepi else res.grad, gamma.grad, phi.grad] + \
+        ([q.delta.grad, q.zero_point.grad] if quant else []) + ([gds.grad, pds.grad] if resepi else [])
     sep = [host(t).copy() for t in sep]
-    for t in [res, gamma, phi] + ([q.delta, q.zero_point] if quant else []):
+    for t in [res, gamma, phi] + ([q.delta, q.zero_point] if quant else []) + \
+            ([yds, gds, pds] if resepi else []):
         t.grad = None
+    if resepi:
+        res = K.LazyRes(yds, bds, gds, pds)
     # fused
     # the lazy placeholder carries exactly these inputs (taken on float4 rows, and on
     # scalar rows while K.TAIL_SCALAR is set)
     lazy = K.epilogue(y, bias, gamma, phi, res, relu, q, lazy=True)
     assert hasattr(lazy, "_ssq_tail") == (hw * hw % 4 == 0 or K.TAIL_SCALAR)
     tail = (y, bias, gamma, phi, res, relu, q)
-    loss2, gy, gres, ggm, gph, gd, gz = K.epilogue_loss_bwd(tail, K.Rows(cache, idx), N * hw * hw, p)
-    fused = [gy, gres, ggm, gph] + ([gd, gz] if quant else [])
+    loss2, gy, gres, ggm, gph, gd, gz, grg, grph = K.epilogue_loss_bwd(tail, K.Rows(cache, idx),
+                                                                        N * hw * hw, p)
+    fused = [gy, gres, ggm, gph] + ([gd, gz] if quant else []) + ([grg, grph] if resepi else [])
     for a, b in zip(sep, fused):
         np.testing.assert_array_equal(a.reshape(-1).view(np.int32), host(b).reshape(-1).view(np.int32))
     close(host(loss2), host(loss1), rtol=1e-6, atol=0)
