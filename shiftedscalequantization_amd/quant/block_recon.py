@@ -20,7 +20,7 @@ from ._engine import (BatchFeeder, IterationGraph, LazyValue, SsqAdam, as_float,
 from .adaptive_rounding import AdaRoundQuantizer
 from .data_utils import save_grad_data, save_inp_oup_data
 from .quant_block import BaseQuantBlock
-from .quant_layer import QuantModule, StraightThrough, pinned_weights
+from .quant_layer import QuantModule, StraightThrough, cached_convs, pinned_weights
 from .quant_model import QuantModel
 
 
@@ -50,6 +50,29 @@ FUSE_TAIL = _FAST
 # act phase: every weight quantizer's W_hat computed once for the loop (the weights are
 # frozen there; quant_layer.pinned_weights)
 PIN_WEIGHTS = _FAST
+# act phase: the convs that read the block input (conv1, the downsample) computed once for
+# every cached sample; each iteration gathers its batch's rows (quant_layer.cached_convs)
+CACHE_CONVS = _FAST
+
+
+def _input_convs(block, qmodules, x):
+    """The QuantModules whose conv reads the block input x directly and runs through
+    forward_raw (the fused-epilogue path), found by one probing forward."""
+    hits = []
+
+    def pre(m, args):
+        if args and isinstance(args[0], torch.Tensor) and args[0].data_ptr() == x.data_ptr() \
+                and m.epilogue_fusable(args[0]):
+            hits.append(m)
+
+    hs = [m.register_forward_pre_hook(pre) for m in qmodules]
+    try:
+        with torch.no_grad():
+            block(x)
+    finally:
+        for h in hs:
+            h.remove()
+    return [m for m in qmodules if m in hits]
 
 
 def _reconstruct(model, block, qmodules, cali_data, batch_size, iters, weight, opt_mode, asym,
@@ -215,7 +238,14 @@ def _fast_loop(block, qmodules, opt_params, loss_func, feeder, bucket, iters, ac
             _step()
 
     ws_cache = {}
-    with (pinned_weights(qmodules) if pin else contextlib.nullcontext()):
+    with contextlib.ExitStack() as stack:
+        if pin:
+            stack.enter_context(pinned_weights(qmodules))
+            if CACHE_CONVS and feeder.N % feeder.bs == 0:
+                convs = _input_convs(block, qmodules, feeder.cur_inp)
+                if convs:
+                    stack.enter_context(cached_convs(convs, feeder.cur_inp, feeder.inp,
+                                                     feeder.didx))
         _run(iters, loss_func, feeder, optimizer, scheduler, shadow if act_quant else None, use_graph,
              bucket, body_pre, body_post, last, opt_params, ada, ws_cache)
 

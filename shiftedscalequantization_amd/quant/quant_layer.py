@@ -68,6 +68,40 @@ def pinned_weights(modules):
         _PINNED_W = prev
 
 
+# Frozen convolutions of a reconstruction loop (cached_convs): module -> (the loop's batch
+# input data_ptr, its shape, the conv's raw outputs for every cached sample, the device
+# batch indices, the batch output buffer).
+_CONV_CACHE = None
+
+
+@contextlib.contextmanager
+def cached_convs(modules, batch_input, source, idx):
+    """Inside this context each QuantModule of `modules`, when its forward gets the loop's
+    batch buffer `batch_input`, returns the rows idx of its raw conv output precomputed for
+    every sample of `source` (the cached block inputs) instead of running the conv.  For a
+    loop in which the conv's input and weight are frozen -- BRECQ's act phase
+    (block_recon.py:62-73): the block input comes from the cache and the weights are pinned
+    (pinned_weights) -- the batch conv computes exactly those rows.  They are precomputed in
+    batches of the loop's own size, the same conv call on the same shapes, so the gathered
+    rows are the loop's bits (test_brecq_loop_knobs_bit_identical).  The caller guarantees
+    that the weights do not change inside the context."""
+    global _CONV_CACHE
+    prev = _CONV_CACHE
+    cache = {} if prev is None else dict(prev)
+    bs = batch_input.shape[0]
+    with torch.no_grad():
+        for m in modules:
+            outs = [m.forward_raw(source[i:i + bs])[0] for i in range(0, source.shape[0], bs)]
+            cache[m] = (batch_input.data_ptr(), tuple(batch_input.shape), torch.cat(outs), idx,
+                        torch.empty_like(outs[0]))
+            del outs
+    _CONV_CACHE = cache
+    try:
+        yield
+    finally:
+        _CONV_CACHE = prev
+
+
 _STATE_FLAGS = ('soft_targets', 'hard_round', 'hard_targets', 'opt_mode', 'shiftedScale',
                 'round_mode', 'n_bits')
 
@@ -340,6 +374,11 @@ class QuantModule(nn.Module):
         """(conv(input, W_hat) without bias, bias): for a parent block that fuses this
         module's bias add with its residual add and activation (see epilogue_fusable)."""
         weight, bias = self._weight_bias()
+        if _CONV_CACHE is not None:
+            hit = _CONV_CACHE.get(self)
+            if hit is not None and hit[0] == input.data_ptr() and hit[1] == tuple(input.shape):
+                K.gather_rows2(hit[2], hit[3], out0=hit[4])
+                return hit[4], bias
         return self._conv(input, weight), bias
 
     def forward(self, input: torch.Tensor):

@@ -342,7 +342,8 @@ def test_brecq_block_reconstruction_matches_reference(Q, golden, graph, wgrad, f
 @pytest.mark.parametrize("affine", [False, True])
 def test_brecq_loop_knobs_bit_identical(Q, golden, graph, affine, det_convs):
     """block_recon._fast_loop's launch savings -- deferred finalizes, the fused tail (p = 2
-    weight phase, p = 2.4 act phase) and the act phase's pinned weights -- against the plain
+    weight phase, p = 2.4 act phase), the act phase's pinned weights and its precomputed
+    block-input convs (conv1, the downsample: gathered rows instead of the conv) -- against the plain
     loop: AdaRound V, the act deltas and the Adam moments bit-identical after each phase,
     per-iteration losses equal to the last float ulps (row-wise vs block-wise loss partials).
     affine: gamma^z / phi^z live (the --bias_cal flow's act phase: the general K13 epilogue,
@@ -363,9 +364,9 @@ def test_brecq_loop_knobs_bit_identical(Q, golden, graph, affine, det_convs):
                 with torch.no_grad():
                     m.alpha_out.copy_(1 + 0.05 * torch.randn(m.alpha_out.shape, generator=gen))
                     m.beta_out.copy_(0.02 * torch.randn(m.beta_out.shape, generator=gen))
-        seen, opts, tails, pins = [], [], [], []
+        seen, opts, tails, pins, cconvs = [], [], [], [], []
         orig_rec, orig_init = BR.LossFunction.record, E.SsqAdam.__init__
-        orig_tail, orig_pin = BR.K.epilogue_loss_bwd, BR.pinned_weights
+        orig_tail, orig_pin, orig_cc = BR.K.epilogue_loss_bwd, BR.pinned_weights, BR.cached_convs
 
         def spy(self, rec, rnd, b):
             r = orig_rec(self, rec, rnd, b)
@@ -384,9 +385,14 @@ def test_brecq_loop_knobs_bit_identical(Q, golden, graph, affine, det_convs):
             pins.append(1)
             return orig_pin(mods)
 
-        knobs = {k: getattr(BR, k) for k in ("DEFER_FINALIZE", "FUSE_TAIL", "PIN_WEIGHTS")}
+        def cc(mods, *a):
+            cconvs.append(len(mods))
+            return orig_cc(mods, *a)
+
+        knobs = {k: getattr(BR, k) for k in ("DEFER_FINALIZE", "FUSE_TAIL", "PIN_WEIGHTS",
+                                             "CACHE_CONVS")}
         BR.LossFunction.record, E.SsqAdam.__init__, BR.K.epilogue_loss_bwd = spy, init, tail
-        BR.pinned_weights = pin
+        BR.pinned_weights, BR.cached_convs = pin, cc
         orig_fast = BR._fast_loop
         BR._fast_loop = lambda *a: orig_fast(*(a[:-1] + (a[-1] and graph,)))
         for k in knobs:
@@ -419,12 +425,13 @@ def test_brecq_loop_knobs_bit_identical(Q, golden, graph, affine, det_convs):
                     out[f"opt{k}_v{j}"] = o.state[p_]["exp_avg_sq"].cpu().numpy()
         finally:
             BR.LossFunction.record, E.SsqAdam.__init__, BR.K.epilogue_loss_bwd = orig_rec, orig_init, orig_tail
-            BR.pinned_weights, BR._fast_loop = orig_pin, orig_fast
+            BR.pinned_weights, BR._fast_loop, BR.cached_convs = orig_pin, orig_fast, orig_cc
             for k, v in knobs.items():
                 setattr(BR, k, v)
         runs.append(out)
-        used.append((len(tails), len(pins)))
-    assert used[0] == (0, 0) and used[1][0] > 0 and used[1][1] == 1, used
+        used.append((len(tails), len(pins), cconvs))
+    # the act phase caches conv1 and the downsample (both read the block input)
+    assert used[0] == (0, 0, []) and used[1][0] > 0 and used[1][1] == 1 and used[1][2] == [2], used
     assert runs[0].keys() == runs[1].keys()
     for k in runs[0]:
         if k.endswith("_rec"):
