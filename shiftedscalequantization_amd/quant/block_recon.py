@@ -52,7 +52,7 @@ FUSE_TAIL = _FAST
 PIN_WEIGHTS = _FAST
 # act phase: the convs that read the block input (conv1, the downsample) computed once for
 # every cached sample; each iteration gathers its batch's rows (quant_layer.cached_convs)
-CACHE_CONVS = _FAST
+CACHE_CONVS = _FAST and os.environ.get("SSQ_BRECQ_CACHE_CONVS", "1") != "0"
 
 
 def _input_convs(block, qmodules, x):
