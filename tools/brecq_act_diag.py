@@ -21,6 +21,12 @@ name = sys.argv[1] if len(sys.argv) > 1 else "recon_brecq_long"
 g = np.load(os.path.join(R, "tests", "golden", name + ".npz"))
 qnn = T.build_qnn(Q, g)
 block = qnn.model[3]
+if "conv1_gamma" in g.files:
+    for n in ("conv1", "conv2", "downsample"):
+        m = getattr(block, n)
+        with torch.no_grad():
+            m.alpha_out.copy_(T.dev(g[n + "_gamma"]))
+            m.beta_out.copy_(T.dev(g[n + "_phi"]))
 cali = T.dev(g["cali"])
 seen = []
 orig_rec = BR.LossFunction.record
@@ -51,7 +57,7 @@ torch.manual_seed(1005)
 Q.block_reconstruction(qnn, block, cali, batch_size=8, iters=len(g["a_total_loss"]), act_quant=True,
                        opt_mode="mse", lr=4e-4, p=2.4)
 E.ITER_PROBE[0] = None
-out = os.path.join(R, "gpurun_out", "brecq_act_diag_%s.npz" % name)
+out = os.path.join(R, "gpurun_out", "brecq_act_diag_%s%s.npz" % (name, os.environ.get("DIAG_TAG", "")))
 os.makedirs(os.path.dirname(out), exist_ok=True)
 np.savez(out, w_seen=np.array(w_seen), a_seen=np.array(seen), deltas=np.array(deltas),
          grads=np.array(grads))
