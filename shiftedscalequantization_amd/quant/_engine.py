@@ -61,10 +61,13 @@ class BatchFeeder:
         K.gather_rows2(self.inp, self.didx, self.out, out0=self.cur_inp, out1=self.cur_out)
         return self.cur_inp, self.cur_out
 
-    def gather_lazy(self):
+    def gather_lazy(self, input_needed=True):
         """The batch input gathered (the conv needs it contiguous); the batch target as a
-        K.Rows view that the loss pass reads in place."""
-        K.gather_rows2(self.inp, self.didx, out0=self.cur_inp)
+        K.Rows view that the loss pass reads in place.  input_needed=False: every reader of
+        the batch input serves it from elsewhere (quant_layer.cached_convs), so only the
+        buffer's identity is handed on."""
+        if input_needed:
+            K.gather_rows2(self.inp, self.didx, out0=self.cur_inp)
         return self.cur_inp, K.Rows(self.out, self.didx)
 
     def next(self, perm=None):

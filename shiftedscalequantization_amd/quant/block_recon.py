@@ -183,6 +183,7 @@ def _fast_loop(block, qmodules, opt_params, loss_func, feeder, bucket, iters, ac
         for q in ada:
             q._fused_reg = (0.0, 0.0, regp)
     last = {}
+    need_input = [True]     # False once cached_convs serves every reader of the block input
 
     def body_pre():
         with K.deferred_finalize(defer):
@@ -193,7 +194,7 @@ def _fast_loop(block, qmodules, opt_params, loss_func, feeder, bucket, iters, ac
                 _step()
 
     def _body_pre():
-        cur_inp, cur_out = feeder.gather_lazy()
+        cur_inp, cur_out = feeder.gather_lazy(input_needed=need_input[0])
         K.TAIL_LAZY[0] = block if fuse_tail else None
         try:
             out = block(cur_inp)
@@ -246,6 +247,9 @@ def _fast_loop(block, qmodules, opt_params, loss_func, feeder, bucket, iters, ac
                 if convs:
                     stack.enter_context(cached_convs(convs, feeder.cur_inp, feeder.inp,
                                                      feeder.didx))
+                    readers = block.input_readers() if isinstance(block, BaseQuantBlock) \
+                        else [block]
+                    need_input[0] = not (readers and all(m in convs for m in readers))
         _run(iters, loss_func, feeder, optimizer, scheduler, shadow if act_quant else None, use_graph,
              bucket, body_pre, body_post, last, opt_params, ada, ws_cache)
 

@@ -73,6 +73,11 @@ class BaseQuantBlock(nn.Module):
             out = self.act_quantizer(out)
         return out
 
+    def input_readers(self):
+        """The QuantModules that read the block input and nothing else does (no identity
+        residual), or None when the input is also used directly."""
+        return None
+
     def _residual(self, ds, x):
         """ds(x), the downsample branch.  For the block the recon loop fuses (K.TAIL_LAZY)
         and a downsample whose forward ends in its K13 epilogue alone (bias, gamma^z/phi^z,
@@ -148,6 +153,9 @@ class QuantBasicBlock(BaseQuantBlock):
             self.cached_out_features += [self._cache(out)]
         return out
 
+    def input_readers(self):
+        return None if self.downsample is None else [self.conv1, self.downsample]
+
     def toggleHardTarget(self):
         for m in (self.conv1, self.conv2, self.downsample):
             if m is not None:
@@ -169,6 +177,9 @@ class QuantBottleneck(BaseQuantBlock):
         self.downsample = None if bottleneck.downsample is None else QuantModule(
             bottleneck.downsample[0], weight_quant_params, act_quant_params, disable_act_quant=True)
         self.stride = bottleneck.stride
+
+    def input_readers(self):
+        return None if self.downsample is None else [self.conv1, self.downsample]
 
     def forward(self, x):
         if self.cache_features == 'if':
@@ -195,6 +206,9 @@ class QuantResBottleneckBlock(BaseQuantBlock):
         self.downsample = QuantModule(bottleneck.proj, weight_quant_params, act_quant_params,
                                       disable_act_quant=True) if bottleneck.proj_block else None
         self.proj_block = bottleneck.proj_block
+
+    def input_readers(self):
+        return [self.conv1, self.downsample] if self.proj_block else None
 
     def forward(self, x):
         if self.cache_features == 'if':
@@ -227,6 +241,9 @@ class QuantInvertedResidual(BaseQuantBlock):
                             disable_act_quant=True))
             self.conv[0].activation_function = nn.ReLU6()
             self.conv[1].activation_function = nn.ReLU6()
+
+    def input_readers(self):
+        return None if self.use_res_connect else [self.conv[0]]
 
     def forward(self, x):
         if self.cache_features == 'if':

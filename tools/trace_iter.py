@@ -4,12 +4,16 @@ iteration), and for each iteration window sums kernel busy time by kernel family
 wall (gather-to-gather) vs GPU-busy time."""
 import collections
 import csv
+import os
 import sys
 
 rows = list(csv.DictReader(open(sys.argv[1])))
 rows.sort(key=lambda r: int(r["Start_Timestamp"]))
-gi = [i for i, r in enumerate(rows) if "gather2_kernel" in r["Kernel_Name"] or
-      "gather_shift_fwd" in r["Kernel_Name"]]
+# iteration marker: the batch gather (default), or MARKER=<substring> (e.g. copyBuffer, the
+# one index copy per iteration, when an iteration gathers several tensors)
+MARK = os.environ.get("MARKER")
+gi = [i for i, r in enumerate(rows) if (MARK in r["Kernel_Name"]) if MARK else
+      ("gather2_kernel" in r["Kernel_Name"] or "gather_shift_fwd" in r["Kernel_Name"])]
 # split into the two recon blocks by large gaps
 segments, cur = [], [gi[0]]
 for a, b in zip(gi, gi[1:]):
