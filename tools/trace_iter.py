@@ -12,8 +12,15 @@ rows.sort(key=lambda r: int(r["Start_Timestamp"]))
 # iteration marker: the batch gather (default), or MARKER=<substring> (e.g. copyBuffer, the
 # one index copy per iteration, when an iteration gathers several tensors)
 MARK = os.environ.get("MARKER")
-gi = [i for i, r in enumerate(rows) if (MARK in r["Kernel_Name"]) if MARK else
-      ("gather2_kernel" in r["Kernel_Name"] or "gather_shift_fwd" in r["Kernel_Name"])]
+
+
+def is_mark(name):
+    if MARK:
+        return MARK in name
+    return "gather2_kernel" in name or "gather_shift_fwd" in name
+
+
+gi = [i for i, r in enumerate(rows) if is_mark(r["Kernel_Name"])]
 # split into the two recon blocks by large gaps
 segments, cur = [], [gi[0]]
 for a, b in zip(gi, gi[1:]):
