@@ -9,6 +9,7 @@ LazyValue: the reference calls .item() on the loss every iteration (a device->ho
 layer_recon_fused_shiftedScale.py:296-298); here loss values stay on the device and are
 read only when reported.
 """
+import numpy as np
 import torch
 
 from .. import kernels as K
@@ -28,6 +29,8 @@ class BatchFeeder:
         # riding on the same H2D copy (the loop's (lambda_S, b2) schedule pair)
         self.ring = [torch.zeros(self.bs + extra_words, dtype=torch.int64, pin_memory=pin)
                      for _ in range(self.RING)]
+        # numpy views of the pinned slots: the per-iteration host writes without torch ops
+        self.ring_np = [r.numpy() for r in self.ring]
         self.done = [None] * self.RING
         self.k = 0
         self._dev = torch.zeros(self.bs + extra_words, dtype=torch.int64, device=device)
@@ -46,10 +49,11 @@ class BatchFeeder:
         slot = self.k % self.RING
         if self.done[slot] is not None:
             self.done[slot].synchronize()
-        h = self.ring[slot]
-        h[:self.bs].copy_(perm)
+        h, hn = self.ring[slot], self.ring_np[slot]
+        hn[:self.bs] = perm.numpy()
         if extra is not None:
-            h[self.bs:].view(torch.float32).copy_(torch.as_tensor(extra, dtype=torch.float32))
+            # float64 -> float32 round to nearest, as torch.as_tensor(extra, dtype=float32)
+            hn[self.bs:].view(np.float32)[:len(extra)] = np.asarray(extra, dtype=np.float64)
         self._dev.copy_(h, non_blocking=True)
         ev = torch.cuda.Event()
         ev.record()
