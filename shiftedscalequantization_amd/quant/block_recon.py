@@ -161,7 +161,10 @@ def _fast_loop(block, qmodules, opt_params, loss_func, feeder, bucket, iters, ac
     AdaRound backward, fused Adam.  After GRAPH_WARMUP eager iterations the body is
     replayed from a HIP graph (at world > 1 as two graphs around the bucket all-reduce,
     _engine.IterationGraph).  The cosine LR schedule is stepped by the
-    reference's own torch scheduler on a shadow optimizer and copied into Adam's device lr."""
+    reference's own torch scheduler on a shadow optimizer and copied into Adam's device lr.
+    Launch savings (module knobs above, bit-identical on or off): deferred finalizes with the
+    Adam step riding on them, the block's fused tail, and in the act phase pinned weights and
+    the block-input convs precomputed for every cached sample."""
     if ITER_HOOK is not None:
         ITER_HOOK(-1, iters)
     use_graph = bool(graph and iters > GRAPH_WARMUP + 1)
