@@ -15,8 +15,8 @@ import torch
 
 from .. import kernels as K
 from ..parallel_dp import GradBucket, world
-from ._engine import (BatchFeeder, IterationGraph, LazyValue, SsqAdam, as_float, backward_tail,
-                      frozen_except, probe)
+from ._engine import (ITER_PROBE, BatchFeeder, IterationGraph, LazyValue, SsqAdam, as_float,
+                      backward_tail, frozen_except, probe)
 from .adaptive_rounding import AdaRoundQuantizer
 from .data_utils import save_grad_data, save_inp_oup_data
 from .quant_block import BaseQuantBlock
@@ -53,6 +53,12 @@ PIN_WEIGHTS = _FAST
 # act phase: the convs that read the block input (conv1, the downsample) computed once for
 # every cached sample; each iteration gathers its batch's rows (quant_layer.cached_convs)
 CACHE_CONVS = _FAST and os.environ.get("SSQ_BRECQ_CACHE_CONVS", "1") != "0"
+# a loop in which nothing learns (the act phase of a layer whose act quantizer is the
+# disabled network output: no optimised parameter reaches its output) runs only the
+# iterations whose loss is reported (every 500th, and the last); the others keep only the
+# reference's randperm draw and schedule steps, so every printed value, the final state and
+# the RNG stream are unchanged
+SKIP_FROZEN = _FAST
 
 
 def _input_convs(block, qmodules, x):
@@ -260,13 +266,24 @@ def _fast_loop(block, qmodules, opt_params, loss_func, feeder, bucket, iters, ac
 def _run(iters, loss_func, feeder, optimizer, scheduler, shadow, use_graph, bucket, body_pre,
          body_post, last, opt_params, ada, ws_cache):
     graph_obj = None
+    skip_ok = (SKIP_FROZEN and bucket is None and ITER_HOOK is None and
+               ITER_PROBE[0] is None and not loss_func.track_values)
     try:
         for i in range(iters):
             if ITER_HOOK is not None:
                 ITER_HOOK(i, iters)
             probe(i, opt_params)
             b, lam, active = loss_func.schedule()
-            feeder.stage(feeder.draw(), extra=(lam, float(b)) + optimizer.next_hyper())
+            perm = feeder.draw()
+            hyp = optimizer.next_hyper()
+            if (skip_ok and last.get('step') is False and loss_func.count % 500 != 0
+                    and i != iters - 1):
+                if scheduler is not None:
+                    shadow.step()
+                    scheduler.step()
+                    optimizer.param_groups[0]['lr'] = shadow.param_groups[0]['lr']
+                continue
+            feeder.stage(perm, extra=(lam, float(b)) + hyp)
             # the round-loss value (reporting only) from alpha before this step, as the
             # reference's forward computes it
             rnd = loss_func.round_value(b) if (active and loss_func.wants_value()) else 0.0

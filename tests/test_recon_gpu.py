@@ -527,6 +527,44 @@ def test_brecq_layer_reconstruction_matches_reference(Q, golden, graph):
         parity_report(f"a22_layer_reconstruction[graph={graph}]", **stats)
 
 
+def test_brecq_frozen_loop_skips_unreported_iterations(Q, golden):
+    """A loop in which nothing learns (the fc's act phase: its act quantizer is the disabled
+    network output) runs only its reported iterations (SKIP_FROZEN): the same printed
+    losses (every 500th count, and the last), the same final state, and the CPU RNG left
+    where the full loop leaves it (the reference draws a randperm every iteration)."""
+    import importlib
+    BR = importlib.import_module("shiftedscalequantization_amd.quant.block_recon")
+    g = golden("recon_layer_brecq")
+    cali = dev(g["cali"])
+    runs = []
+    for skip in (False, True):
+        qnn = build_qnn(Q, g)
+        fc = qnn.model[6]
+        qnn.set_quant_state(True, True)
+        with torch.no_grad():
+            qnn(cali[:8])
+        qnn.disable_network_output_quantization()
+        reported, orig_rec, prev = [], BR.LossFunction.record, BR.SKIP_FROZEN
+
+        def spy(self, rec, rnd, b):
+            r = orig_rec(self, rec, rnd, b)
+            if self.count % 500 == 0 or self.count == 1001:
+                reported.append((self.count, float(r)))
+            return r
+
+        BR.LossFunction.record, BR.SKIP_FROZEN = spy, skip
+        try:
+            torch.manual_seed(1005)
+            Q.layer_reconstruction(qnn, fc, cali, batch_size=8, iters=1001, act_quant=True,
+                                   opt_mode="mse", lr=4e-4, p=2.4)
+            nxt = torch.randint(0, 1 << 30, (4,)).tolist()
+        finally:
+            BR.LossFunction.record, BR.SKIP_FROZEN = orig_rec, prev
+        runs.append((reported, nxt, float(fc.act_quantizer.delta)))
+    assert [c for c, _ in runs[0][0]] == [500, 1000, 1001]
+    assert runs[0] == runs[1]
+
+
 # ------------------------------------------------------------------ other block types
 def block_net(kind):
     from shiftedscalequantization_amd import nets
