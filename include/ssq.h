@@ -259,6 +259,20 @@ int ssq_adaround_bwd(const float* gWhat, const float* W, const float* beta,
                      const float* delta, int delta_per_ci, const float* zp, float scale,
                      int64_t Co, int64_t Ci, int64_t K, int qmin, int qmax, float reg_lambda,
                      float reg_b, const float* reg_dev, float* gbeta, ssq_stream_t stream);
+/* Several AdaRound weights (a block's quantizers) in one launch each way: arrays of nseg
+ * (<= 8) per-weight arguments as in ssq_adaround_fwd / _bwd (scale, qmin, qmax per weight);
+ * results bit-identical to one call per weight. */
+int ssq_adaround_fwd_multi(int nseg, const float* const* W, const float* const* beta,
+                           const float* const* delta, const int* delta_per_ci,
+                           const float* const* zp, const float* scale, const int64_t* Co,
+                           const int64_t* Ci, const int64_t* K, int hard_round, const int* qmin,
+                           const int* qmax, float* const* What, ssq_stream_t stream);
+int ssq_adaround_bwd_multi(int nseg, const float* const* gWhat, const float* const* W,
+                           const float* const* beta, const float* const* delta,
+                           const int* delta_per_ci, const float* const* zp, const float* scale,
+                           const int64_t* Co, const int64_t* Ci, const int64_t* K, const int* qmin,
+                           const int* qmax, float reg_lambda, float reg_b, const float* reg_dev,
+                           float* const* gbeta, ssq_stream_t stream);
 
 /* Rounding regulariser lambda*sum(1-|2h(v)-1|^b) over h = rect_sigmoid(v)
  * (layer_recon_fused_shiftedScale.py:278-279, block_recon.py:171-174,

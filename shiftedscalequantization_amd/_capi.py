@@ -61,6 +61,9 @@ SIGNATURES = {
     "ssq_adaround_fwd": (_i, [_p, _p, _p, _i, _p, _f, _i64, _i64, _i64, _i, _i, _i, _p, _p, _p]),
     "ssq_adaround_bwd": (_i, [_p, _p, _p, _p, _i, _p, _f, _i64, _i64, _i64, _i, _i, _f, _f, _p,
                               _p, _p]),
+    "ssq_adaround_fwd_multi": (_i, [_i, _p, _p, _p, _p, _p, _p, _p, _p, _p, _i, _p, _p, _p, _p]),
+    "ssq_adaround_bwd_multi": (_i, [_i, _p, _p, _p, _p, _p, _p, _p, _p, _p, _p, _p, _p, _f, _f,
+                                    _p, _p, _p]),
     "ssq_round_reg_workspace_size": (_sz, [_i64]),
     "ssq_round_reg": (_i, [_p, _i64, _f, _f, _p, _p, _p, _sz, _p]),
     "ssq_inpscale_search": (_i, [_p, _p, _p, _i64, _i64, _i, _i, _f, _p, _p]),

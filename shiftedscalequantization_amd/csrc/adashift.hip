@@ -191,6 +191,73 @@ __global__ __launch_bounds__(kBlock) void adaround_bwd_kernel(
   }
 }
 
+// Several weights in one launch (the AdaRound quantizers of a block, BRECQ's weight phase):
+// a table of segments, each a contiguous run of kAdaTile-element tiles; every element runs
+// the single-weight kernels' exact ops, so the results are bit-identical to one launch per
+// weight.
+constexpr int kMaxAdaSeg = 8;
+constexpr uint32_t kAdaTile = 4096;
+struct AdaSeg {
+  const float* W;
+  const float* beta;
+  const float* delta;
+  const float* zp;
+  const float* gWhat;   // backward
+  float* out;           // forward: What; backward: gbeta
+  Geo g;
+  uint32_t n, blk0;
+  int per_ci;
+  float scale, lo, hi;
+};
+struct AdaTable {
+  AdaSeg s[kMaxAdaSeg];
+  int nseg;
+};
+
+__device__ __forceinline__ const AdaSeg& ada_seg(const AdaTable& tab, uint32_t& t0, uint32_t& t1) {
+  int si = 0;
+  while (si + 1 < tab.nseg && blockIdx.x >= tab.s[si + 1].blk0) ++si;
+  const AdaSeg& sg = tab.s[si];
+  t0 = (blockIdx.x - sg.blk0) * kAdaTile;
+  t1 = min(t0 + kAdaTile, sg.n);
+  return sg;
+}
+
+__global__ __launch_bounds__(kBlock) void adaround_fwd_multi_kernel(AdaTable tab, int hard_r) {
+  uint32_t t0, t1;
+  const AdaSeg& sg = ada_seg(tab, t0, t1);
+  for (uint32_t e = t0 + threadIdx.x; e < t1; e += kBlock) {
+    uint32_t co, ci;
+    decompose(e, sg.g, co, ci);
+    const float d = __fmul_rn(delta_at(sg.delta, sg.per_ci, sg.g, co, ci), sg.scale), z = sg.zp[co];
+    const float b = sg.beta[e];
+    const float hr = hard_r ? (b >= 0.0f ? 1.0f : 0.0f) : rect_sigmoid(b);
+    const float q = clampf(__fadd_rn(__fadd_rn(floorf(sg.W[e] / d), hr), z), sg.lo, sg.hi);
+    sg.out[e] = __fmul_rn(__fsub_rn(q, z), d);
+  }
+}
+
+__global__ __launch_bounds__(kBlock) void adaround_bwd_multi_kernel(AdaTable tab, float reg_lambda,
+                                                                    float reg_b,
+                                                                    const float* __restrict__ reg_dev) {
+  if (reg_dev) {
+    reg_lambda = reg_dev[0];
+    reg_b = reg_dev[1];
+  }
+  uint32_t t0, t1;
+  const AdaSeg& sg = ada_seg(tab, t0, t1);
+  for (uint32_t e = t0 + threadIdx.x; e < t1; e += kBlock) {
+    uint32_t co, ci;
+    decompose(e, sg.g, co, ci);
+    const float d = __fmul_rn(delta_at(sg.delta, sg.per_ci, sg.g, co, ci), sg.scale), z = sg.zp[co];
+    const float b = sg.beta[e];
+    const float u = __fadd_rn(__fadd_rn(floorf(sg.W[e] / d), rect_sigmoid(b)), z);
+    const float gi = (u >= sg.lo && u <= sg.hi) ? __fmul_rn(sg.gWhat[e], d) : 0.0f;
+    const float ga = rect_sigmoid_grad(b, gi);
+    sg.out[e] = reg_lambda != 0.0f ? __fadd_rn(ga, round_reg_grad(b, reg_lambda, reg_b)) : ga;
+  }
+}
+
 // ------------------------------------------------------------------ inits
 // -log((zeta-gamma)/(rest-gamma) - 1); python_float/tensor == reciprocal(tensor)*float
 __device__ __forceinline__ float rect_inverse(float w, float d) {
@@ -744,6 +811,77 @@ extern "C" int ssq_adaround_bwd(const float* gWhat, const float* W, const float*
                      (hipStream_t)stream, gWhat, W, beta, delta, delta_per_ci, zp, scale, g, n,
                      (float)qmin, (float)qmax, reg_lambda, reg_b, reg_dev, gbeta);
   return check_launch("ssq_adaround_bwd");
+}
+
+static int ada_table(const char* what, int nseg, const float* const* gWhat, const float* const* W,
+                     const float* const* beta, const float* const* delta,
+                     const int* delta_per_ci, const float* const* zp, const float* scale,
+                     const int64_t* Co, const int64_t* Ci, const int64_t* K, const int* qmin,
+                     const int* qmax, float* const* out, AdaTable& tab, uint32_t& nblk) {
+  SSQ_REQUIRE(nseg >= 1 && nseg <= kMaxAdaSeg, SSQ_E_ARG, "%s: 1 <= nseg <= %d", what, kMaxAdaSeg);
+  SSQ_REQUIRE(W && beta && delta && delta_per_ci && zp && scale && Co && Ci && K && qmin && qmax &&
+              out, SSQ_E_ARG, "%s: null array", what);
+  tab.nseg = nseg;
+  int64_t blk = 0;
+  for (int i = 0; i < nseg; ++i) {
+    AdaSeg& sg = tab.s[i];
+    {
+      const int r = make_geo(Co[i], Ci[i], K[i], 0, sg.g);
+      if (r) return r;
+    }
+    SSQ_REQUIRE(W[i] && beta[i] && delta[i] && zp[i] && out[i] && (!gWhat || gWhat[i]), SSQ_E_ARG,
+                "%s: segment %d has a null pointer", what, i);
+    sg.W = W[i];
+    sg.beta = beta[i];
+    sg.delta = delta[i];
+    sg.zp = zp[i];
+    sg.gWhat = gWhat ? gWhat[i] : nullptr;
+    sg.out = out[i];
+    sg.n = sg.g.Co * sg.g.CiK;
+    sg.blk0 = (uint32_t)blk;
+    sg.per_ci = delta_per_ci[i];
+    sg.scale = scale[i];
+    sg.lo = (float)qmin[i];
+    sg.hi = (float)qmax[i];
+    blk += (sg.n + kAdaTile - 1) / kAdaTile;
+  }
+  SSQ_REQUIRE(blk < (1ll << 31), SSQ_E_ARG, "%s: too many tiles", what);
+  nblk = (uint32_t)blk;
+  return SSQ_OK;
+}
+
+extern "C" int ssq_adaround_fwd_multi(int nseg, const float* const* W, const float* const* beta,
+                                      const float* const* delta, const int* delta_per_ci,
+                                      const float* const* zp, const float* scale,
+                                      const int64_t* Co, const int64_t* Ci, const int64_t* K,
+                                      int hard_round, const int* qmin, const int* qmax,
+                                      float* const* What, ssq_stream_t stream) {
+  AdaTable tab;
+  uint32_t nblk = 0;
+  const int rc = ada_table("ssq_adaround_fwd_multi", nseg, nullptr, W, beta, delta, delta_per_ci,
+                           zp, scale, Co, Ci, K, qmin, qmax, What, tab, nblk);
+  if (rc) return rc;
+  hipLaunchKernelGGL(adaround_fwd_multi_kernel, dim3(nblk), dim3(kBlock), 0, (hipStream_t)stream,
+                     tab, hard_round);
+  return check_launch("ssq_adaround_fwd_multi");
+}
+
+extern "C" int ssq_adaround_bwd_multi(int nseg, const float* const* gWhat, const float* const* W,
+                                      const float* const* beta, const float* const* delta,
+                                      const int* delta_per_ci, const float* const* zp,
+                                      const float* scale, const int64_t* Co, const int64_t* Ci,
+                                      const int64_t* K, const int* qmin, const int* qmax,
+                                      float reg_lambda, float reg_b, const float* reg_dev,
+                                      float* const* gbeta, ssq_stream_t stream) {
+  SSQ_REQUIRE(gWhat, SSQ_E_ARG, "ssq_adaround_bwd_multi: null gWhat");
+  AdaTable tab;
+  uint32_t nblk = 0;
+  const int rc = ada_table("ssq_adaround_bwd_multi", nseg, gWhat, W, beta, delta, delta_per_ci,
+                           zp, scale, Co, Ci, K, qmin, qmax, gbeta, tab, nblk);
+  if (rc) return rc;
+  hipLaunchKernelGGL(adaround_bwd_multi_kernel, dim3(nblk), dim3(kBlock), 0, (hipStream_t)stream,
+                     tab, reg_lambda, reg_b, reg_dev);
+  return check_launch("ssq_adaround_bwd_multi");
 }
 
 extern "C" int ssq_rect_init(const float* W, const float* delta, int delta_per_ci, int64_t Co,

@@ -663,6 +663,64 @@ class AdaRoundFn(torch.autograd.Function):
         return (gb, None, None, None, None, None, None, None, None)
 
 
+class AdaRoundMultiFn(torch.autograd.Function):
+    """AdaRoundFn for several weights (a block's AdaRound quantizers) in one launch each way
+    (ssq_adaround_fwd_multi / _bwd_multi; bit-identical to one launch per weight).
+    cfg = (hard_r, reg, entries), entries[i] = (w, delta, zp, n_bits, sym, scale); inputs =
+    the betas; outputs = the Whats."""
+
+    @staticmethod
+    def forward(ctx, cfg, *betas):
+        hard_r, reg, entries = cfg
+        n = len(entries)
+        ws, bs, ds, zs, outs, geo, pc, sc, lo_, hi_ = [], [], [], [], [], [], [], [], [], []
+        for b, (w, d, z, n_bits, sym, scale) in zip(betas, entries):
+            w, _ = fptr(w.detach(), "weight")
+            b, _ = fptr(b.detach(), "beta")
+            d, _ = fptr(d.detach(), "delta")
+            z, _ = fptr(z.detach(), "zero_point")
+            Co, Ci, K, _ = geometry(w)
+            ws.append(w)
+            bs.append(b)
+            ds.append(d)
+            zs.append(z)
+            outs.append(torch.empty_like(w))
+            geo.append((Co, Ci, K))
+            pc.append(_delta_per_ci(d, Co, Ci))
+            sc.append(float(scale))
+            lo, hi = qrange(n_bits, sym)
+            lo_.append(lo)
+            hi_.append(hi)
+        arr = (C.c_int64 * n)
+        args = (arr(*[g[0] for g in geo]), arr(*[g[1] for g in geo]), arr(*[g[2] for g in geo]))
+        ints = ((C.c_int * n)(*pc), (C.c_float * n)(*sc), (C.c_int * n)(*lo_), (C.c_int * n)(*hi_))
+        call("ssq_adaround_fwd_multi", n, _ptrs(ws), _ptrs(bs), _ptrs(ds), ints[0], _ptrs(zs),
+             ints[1], *args, int(hard_r), ints[2], ints[3], _ptrs(outs), stream_of(ws[0]))
+        ctx.save_for_backward(*bs, *ws, *ds, *zs)
+        ctx.cfg = (hard_r, reg, n, args, ints)
+        return tuple(outs)
+
+    @staticmethod
+    def backward(ctx, *gs):
+        hard_r, reg, n, args, ints = ctx.cfg
+        if hard_r or not any(ctx.needs_input_grad[1:]):
+            return (None,) * (n + 1)
+        saved = ctx.saved_tensors
+        bs, ws, ds, zs = saved[:n], saved[n:2 * n], saved[2 * n:3 * n], saved[3 * n:]
+        gs = [torch.zeros_like(w) if g is None else g.contiguous() for g, w in zip(gs, ws)]
+        gb = [torch.empty_like(w) for w in ws]
+        lam, bb, reg_dev = (0.0, 0.0, None) if reg is None else reg
+        call("ssq_adaround_bwd_multi", n, _ptrs(gs), _ptrs(ws), _ptrs(bs), _ptrs(ds), ints[0],
+             _ptrs(zs), ints[1], *args, ints[2], ints[3], float(lam), float(bb), _vp(reg_dev),
+             _ptrs(gb), stream_of(ws[0]))
+        return (None,) + tuple(g if need else None for g, need in zip(gb, ctx.needs_input_grad[1:]))
+
+
+def adaround_multi(betas, entries, hard_r, reg=None):
+    """Several AdaRound weights in one launch (AdaRoundMultiFn)."""
+    return AdaRoundMultiFn.apply((bool(hard_r), reg, tuple(entries)), *betas)
+
+
 def adaround(beta, w, delta, zp, n_bits, sym, hard_r, scale=1.0, reg=None):
     """reg = (lambda, b, reg_dev) folds the rounding regulariser's gradient into the
     backward ((lambda, b) from the device pair reg_dev when given)."""

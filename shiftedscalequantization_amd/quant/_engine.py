@@ -145,6 +145,32 @@ def stash_block_weights(quantizers):
             q._stash = w
 
 
+def stash_adaround(modules):
+    """The AdaRound W_hat of every module of a block in ONE launch (and their backward in
+    one, AdaRoundMultiFn): BRECQ's weight phase learns only the rounding variables, and
+    every weight's W_hat depends on its own alone.  Each quantizer's next forward on its
+    module's weight returns the stashed W_hat.  Graph-capturable (device work only)."""
+    qs = [m for m in modules if getattr(m.weight_quantizer, 'round_mode', None) == 'learned_hard_sigmoid'
+          and m.use_weight_quant and m.weight.dim() == 4]
+    if len(qs) < 2 or len(qs) > 8:
+        return
+    q0 = qs[0].weight_quantizer
+    hard = not q0.soft_targets
+
+    def reg_key(q):
+        r = getattr(q, '_fused_reg', None)
+        return None if r is None else (r[0], r[1], id(r[2]))
+
+    if any((not m.weight_quantizer.soft_targets) != hard or
+           reg_key(m.weight_quantizer) != reg_key(q0) for m in qs):
+        return
+    entries = [(m.weight, m.weight_quantizer.delta, m.weight_quantizer.zero_point,
+                m.weight_quantizer.n_bits, False, 1.0) for m in qs]
+    outs = K.adaround_multi([m.weight_quantizer.alpha for m in qs], entries, hard, reg=q0._fused_reg)
+    for m, w in zip(qs, outs):
+        m.weight_quantizer._stash = (m.weight, w)
+
+
 def clear_stash(quantizers):
     for q in quantizers:
         if getattr(q, '_stash', None) is not None:

@@ -41,6 +41,9 @@ class AdaRoundQuantizer(nn.Module):
             x_quant = torch.clamp(x_int + self.zero_point, 0, self.n_levels - 1)
             return (x_quant - self.zero_point) * self.delta
         elif self.round_mode == 'learned_hard_sigmoid':
+            stash = getattr(self, '_stash', None)
+            if stash is not None and stash[0] is x:
+                return stash[1]            # computed with the block's others (stash_adaround)
             # adaptive_rounding.py:64 clamps to [0, n_levels-1] regardless of sym
             return K.adaround(self.alpha, x, self.delta, self.zero_point, self.n_bits, False,
                               not self.soft_targets, reg=self._fused_reg)

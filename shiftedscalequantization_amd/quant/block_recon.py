@@ -16,7 +16,7 @@ import torch
 from .. import kernels as K
 from ..parallel_dp import GradBucket, world
 from ._engine import (ITER_PROBE, BatchFeeder, IterationGraph, LazyValue, SsqAdam, as_float,
-                      backward_tail, frozen_except, probe)
+                      backward_tail, clear_stash, frozen_except, probe, stash_adaround)
 from .adaptive_rounding import AdaRoundQuantizer
 from .data_utils import save_grad_data, save_inp_oup_data
 from .quant_block import BaseQuantBlock
@@ -59,6 +59,9 @@ CACHE_CONVS = _FAST and os.environ.get("SSQ_BRECQ_CACHE_CONVS", "1") != "0"
 # reference's randperm draw and schedule steps, so every printed value, the final state and
 # the RNG stream are unchanged
 SKIP_FROZEN = _FAST
+# weight phase: the block's AdaRound forwards in one launch and their backwards in one
+# (_engine.stash_adaround)
+STASH_ADAROUND = _FAST
 
 
 def _input_convs(block, qmodules, x):
@@ -178,6 +181,7 @@ def _fast_loop(block, qmodules, opt_params, loss_func, feeder, bucket, iters, ac
     fuse_tail = FUSE_TAIL and isinstance(block, BaseQuantBlock)
     wq_params = {id(t) for m in qmodules for t in m.weight_quantizer.parameters()}
     pin = PIN_WEIGHTS and act_quant and not any(id(t) in wq_params for t in opt_params)
+    stash_ada = STASH_ADAROUND and not act_quant and isinstance(block, BaseQuantBlock)
     if act_quant:
         optimizer = SsqAdam(opt_params, lr=lr)
         # the reference's cosine schedule, stepped by torch's own scheduler on a shadow
@@ -204,11 +208,15 @@ def _fast_loop(block, qmodules, opt_params, loss_func, feeder, bucket, iters, ac
 
     def _body_pre():
         cur_inp, cur_out = feeder.gather_lazy(input_needed=need_input[0])
+        if stash_ada:
+            stash_adaround(qmodules)
         K.TAIL_LAZY[0] = block if fuse_tail else None
         try:
             out = block(cur_inp)
         finally:
             K.TAIL_LAZY[0] = None
+            if stash_ada:
+                clear_stash([m.weight_quantizer for m in qmodules])
         tail = getattr(out, '_ssq_tail', None)
         if tail is not None:
             # the block's final epilogue, the loss and the epilogue's backward in one pass;

@@ -373,9 +373,10 @@ def test_brecq_loop_knobs_bit_identical(Q, golden, graph, affine, det_convs):
                 with torch.no_grad():
                     m.alpha_out.copy_(1 + 0.05 * torch.randn(m.alpha_out.shape, generator=gen))
                     m.beta_out.copy_(0.02 * torch.randn(m.beta_out.shape, generator=gen))
-        seen, opts, tails, pins, cconvs = [], [], [], [], []
+        seen, opts, tails, pins, cconvs, stashed = [], [], [], [], [], []
         orig_rec, orig_init = BR.LossFunction.record, E.SsqAdam.__init__
         orig_tail, orig_pin, orig_cc = BR.K.epilogue_loss_bwd, BR.pinned_weights, BR.cached_convs
+        orig_stash = BR.stash_adaround
 
         def spy(self, rec, rnd, b):
             r = orig_rec(self, rec, rnd, b)
@@ -398,10 +399,14 @@ def test_brecq_loop_knobs_bit_identical(Q, golden, graph, affine, det_convs):
             cconvs.append(len(mods))
             return orig_cc(mods, *a)
 
+        def stash(mods):
+            orig_stash(mods)
+            stashed.append(sum(getattr(m.weight_quantizer, "_stash", None) is not None for m in mods))
+
         knobs = {k: getattr(BR, k) for k in ("DEFER_FINALIZE", "FUSE_TAIL", "PIN_WEIGHTS",
-                                             "CACHE_CONVS")}
+                                             "CACHE_CONVS", "STASH_ADAROUND")}
         BR.LossFunction.record, E.SsqAdam.__init__, BR.K.epilogue_loss_bwd = spy, init, tail
-        BR.pinned_weights, BR.cached_convs = pin, cc
+        BR.pinned_weights, BR.cached_convs, BR.stash_adaround = pin, cc, stash
         orig_fast = BR._fast_loop
         BR._fast_loop = lambda *a: orig_fast(*(a[:-1] + (a[-1] and graph,)))
         for k in knobs:
@@ -435,12 +440,15 @@ def test_brecq_loop_knobs_bit_identical(Q, golden, graph, affine, det_convs):
         finally:
             BR.LossFunction.record, E.SsqAdam.__init__, BR.K.epilogue_loss_bwd = orig_rec, orig_init, orig_tail
             BR.pinned_weights, BR._fast_loop, BR.cached_convs = orig_pin, orig_fast, orig_cc
+            BR.stash_adaround = orig_stash
             for k, v in knobs.items():
                 setattr(BR, k, v)
         runs.append(out)
-        used.append((len(tails), len(pins), cconvs))
-    # the act phase caches conv1 and the downsample (both read the block input)
-    assert used[0] == (0, 0, []) and used[1][0] > 0 and used[1][1] == 1 and used[1][2] == [2], used
+        used.append((len(tails), len(pins), cconvs, sorted(set(stashed))))
+    # the act phase caches conv1 and the downsample (both read the block input); the weight
+    # phase computes the block's three AdaRound weights in one launch every iteration
+    assert used[0] == (0, 0, [], []) and used[1][0] > 0 and used[1][1] == 1 \
+        and used[1][2] == [2] and used[1][3] == [3], used
     assert runs[0].keys() == runs[1].keys()
     for k in runs[0]:
         if k.endswith("_rec"):
