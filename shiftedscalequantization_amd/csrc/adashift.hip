@@ -196,7 +196,7 @@ __global__ __launch_bounds__(kBlock) void adaround_bwd_kernel(
 // the single-weight kernels' exact ops, so the results are bit-identical to one launch per
 // weight.
 constexpr int kMaxAdaSeg = 8;
-constexpr uint32_t kAdaTile = 4096;
+constexpr uint32_t kAdaTile = 512;   // 2 elements per thread: as many workgroups as the single launches
 struct AdaSeg {
   const float* W;
   const float* beta;
