@@ -74,6 +74,16 @@ class BatchFeeder:
             K.gather_rows2(self.inp, self.didx, out0=self.cur_inp)
         return self.cur_inp, K.Rows(self.out, self.didx)
 
+    def gather_many(self, pairs, input_needed=True):
+        """gather_lazy for a loop that also gathers other per-sample row sources (the
+        precomputed block-input convs, quant_layer.cached_convs(gathered=True)) by the same
+        indices: the batch input and those sources two per ssq_gather_rows2 launch."""
+        srcs = ([(self.inp, self.cur_inp)] if input_needed else []) + list(pairs)
+        for k in range(0, len(srcs), 2):
+            (s0, d0), (s1, d1) = srcs[k], srcs[k + 1] if k + 1 < len(srcs) else (None, None)
+            K.gather_rows2(s0, self.didx, s1, out0=d0, out1=d1)
+        return self.cur_inp, K.Rows(self.out, self.didx)
+
     def next(self, perm=None):
         self.stage(self.draw() if perm is None else perm)
         return self.gather()

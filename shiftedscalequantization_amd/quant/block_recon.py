@@ -40,7 +40,7 @@ def block_reconstruction(model: QuantModel, block: BaseQuantBlock, cali_data: to
 GRAPH_WARMUP = 3     # eager iterations before the iteration body is captured
 ITER_HOOK = None     # optional callable(i, iters) at the top of every device-loop iteration (tools)
 # A/B knobs of the device loop, bit-identical either way (tests/test_recon_gpu.py); the
-# environment's SSQ_BRECQ_FAST=0 starts with all three off (end-to-end A/B runs):
+# environment's SSQ_BRECQ_FAST=0 starts with all of them off (end-to-end A/B runs):
 _FAST = os.environ.get("SSQ_BRECQ_FAST", "1") != "0"
 # the loss / epilogue finalizes ride on the next backward launch (csrc/fin_tasks.h; world 1)
 DEFER_FINALIZE = _FAST
@@ -62,6 +62,9 @@ SKIP_FROZEN = _FAST
 # weight phase: the block's AdaRound forwards in one launch and their backwards in one
 # (_engine.stash_adaround)
 STASH_ADAROUND = _FAST
+# act phase with CACHE_CONVS: the batch input (when still read) and the cached convs' rows
+# gathered two sources per launch (_engine.BatchFeeder.gather_many)
+GATHER_ONCE = _FAST and os.environ.get("SSQ_BRECQ_GATHER_ONCE", "1") != "0"
 
 
 def _input_convs(block, qmodules, x):
@@ -197,6 +200,7 @@ def _fast_loop(block, qmodules, opt_params, loss_func, feeder, bucket, iters, ac
             q._fused_reg = (0.0, 0.0, regp)
     last = {}
     need_input = [True]     # False once cached_convs serves every reader of the block input
+    conv_rows = []          # cached_convs' (all rows, batch buffer) pairs, gathered with the input
 
     def body_pre():
         with K.deferred_finalize(defer):
@@ -207,7 +211,10 @@ def _fast_loop(block, qmodules, opt_params, loss_func, feeder, bucket, iters, ac
                 _step()
 
     def _body_pre():
-        cur_inp, cur_out = feeder.gather_lazy(input_needed=need_input[0])
+        if conv_rows:
+            cur_inp, cur_out = feeder.gather_many(conv_rows, input_needed=need_input[0])
+        else:
+            cur_inp, cur_out = feeder.gather_lazy(input_needed=need_input[0])
         if stash_ada:
             stash_adaround(qmodules)
         K.TAIL_LAZY[0] = block if fuse_tail else None
@@ -262,8 +269,10 @@ def _fast_loop(block, qmodules, opt_params, loss_func, feeder, bucket, iters, ac
             if CACHE_CONVS and feeder.N % feeder.bs == 0:
                 convs = _input_convs(block, qmodules, feeder.cur_inp)
                 if convs:
-                    stack.enter_context(cached_convs(convs, feeder.cur_inp, feeder.inp,
-                                                     feeder.didx))
+                    conv_rows[:] = stack.enter_context(cached_convs(
+                        convs, feeder.cur_inp, feeder.inp, feeder.didx, gathered=GATHER_ONCE))
+                    if not GATHER_ONCE:
+                        conv_rows.clear()
                     readers = block.input_readers() if isinstance(block, BaseQuantBlock) \
                         else [block]
                     need_input[0] = not (readers and all(m in convs for m in readers))

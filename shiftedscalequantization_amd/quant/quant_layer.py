@@ -70,12 +70,12 @@ def pinned_weights(modules):
 
 # Frozen convolutions of a reconstruction loop (cached_convs): module -> (the loop's batch
 # input data_ptr, its shape, the conv's raw outputs for every cached sample, the device
-# batch indices, the batch output buffer).
+# batch indices, the batch output buffer, whether the caller gathers into it).
 _CONV_CACHE = None
 
 
 @contextlib.contextmanager
-def cached_convs(modules, batch_input, source, idx):
+def cached_convs(modules, batch_input, source, idx, gathered=False):
     """Inside this context each QuantModule of `modules`, when its forward gets the loop's
     batch buffer `batch_input`, returns the rows idx of its raw conv output precomputed for
     every sample of `source` (the cached block inputs) instead of running the conv.  For a
@@ -84,7 +84,10 @@ def cached_convs(modules, batch_input, source, idx):
     (pinned_weights) -- the batch conv computes exactly those rows.  They are precomputed in
     batches of the loop's own size, the same conv call on the same shapes, so the gathered
     rows are the loop's bits (test_brecq_loop_knobs_bit_identical).  The caller guarantees
-    that the weights do not change inside the context."""
+    that the weights do not change inside the context.  gathered=True: the caller gathers
+    the rows itself (the context yields each module's (all rows, batch buffer) pair, e.g. for
+    one launch per iteration that also gathers the batch input) and forward only hands the
+    batch buffer on."""
     global _CONV_CACHE
     prev = _CONV_CACHE
     cache = {} if prev is None else dict(prev)
@@ -93,11 +96,11 @@ def cached_convs(modules, batch_input, source, idx):
         for m in modules:
             outs = [m.forward_raw(source[i:i + bs])[0] for i in range(0, source.shape[0], bs)]
             cache[m] = (batch_input.data_ptr(), tuple(batch_input.shape), torch.cat(outs), idx,
-                        torch.empty_like(outs[0]))
+                        torch.empty_like(outs[0]), gathered)
             del outs
     _CONV_CACHE = cache
     try:
-        yield
+        yield [(cache[m][2], cache[m][4]) for m in modules]
     finally:
         _CONV_CACHE = prev
 
@@ -377,7 +380,8 @@ class QuantModule(nn.Module):
         if _CONV_CACHE is not None:
             hit = _CONV_CACHE.get(self)
             if hit is not None and hit[0] == input.data_ptr() and hit[1] == tuple(input.shape):
-                K.gather_rows2(hit[2], hit[3], out0=hit[4])
+                if not hit[5]:
+                    K.gather_rows2(hit[2], hit[3], out0=hit[4])
                 return hit[4], bias
         return self._conv(input, weight), bias
 

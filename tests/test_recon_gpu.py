@@ -395,16 +395,22 @@ def test_brecq_loop_knobs_bit_identical(Q, golden, graph, affine, det_convs):
             pins.append(1)
             return orig_pin(mods)
 
-        def cc(mods, *a):
+        def cc(mods, *a, **k):
             cconvs.append(len(mods))
-            return orig_cc(mods, *a)
+            return orig_cc(mods, *a, **k)
+
+        orig_gather, pairs = BR.K.gather_rows2, []
+
+        def gather(src0, idx, src1=None, **k):
+            pairs.append(src1 is not None)
+            return orig_gather(src0, idx, src1, **k)
 
         def stash(mods):
             orig_stash(mods)
             stashed.append(sum(getattr(m.weight_quantizer, "_stash", None) is not None for m in mods))
 
         knobs = {k: getattr(BR, k) for k in ("DEFER_FINALIZE", "FUSE_TAIL", "PIN_WEIGHTS",
-                                             "CACHE_CONVS", "STASH_ADAROUND")}
+                                             "CACHE_CONVS", "STASH_ADAROUND", "GATHER_ONCE")}
         BR.LossFunction.record, E.SsqAdam.__init__, BR.K.epilogue_loss_bwd = spy, init, tail
         BR.pinned_weights, BR.cached_convs, BR.stash_adaround = pin, cc, stash
         orig_fast = BR._fast_loop
@@ -426,8 +432,10 @@ def test_brecq_loop_knobs_bit_identical(Q, golden, graph, affine, det_convs):
             qnn.disable_network_output_quantization()
             seen.clear()
             torch.manual_seed(1005)
+            BR.K.gather_rows2 = gather
             Q.block_reconstruction(qnn, block, cali, batch_size=8, iters=12, act_quant=True,
                                    opt_mode="mse", lr=4e-4, p=2.4)
+            BR.K.gather_rows2 = orig_gather
             out["a_rec"] = np.array(seen)
             aqs = [block.act_quantizer] + [m.act_quantizer for m in (block.conv1, block.conv2,
                                                                       block.downsample)
@@ -440,15 +448,16 @@ def test_brecq_loop_knobs_bit_identical(Q, golden, graph, affine, det_convs):
         finally:
             BR.LossFunction.record, E.SsqAdam.__init__, BR.K.epilogue_loss_bwd = orig_rec, orig_init, orig_tail
             BR.pinned_weights, BR._fast_loop, BR.cached_convs = orig_pin, orig_fast, orig_cc
-            BR.stash_adaround = orig_stash
+            BR.stash_adaround, BR.K.gather_rows2 = orig_stash, orig_gather
             for k, v in knobs.items():
                 setattr(BR, k, v)
         runs.append(out)
-        used.append((len(tails), len(pins), cconvs, sorted(set(stashed))))
-    # the act phase caches conv1 and the downsample (both read the block input); the weight
-    # phase computes the block's three AdaRound weights in one launch every iteration
-    assert used[0] == (0, 0, [], []) and used[1][0] > 0 and used[1][1] == 1 \
-        and used[1][2] == [2] and used[1][3] == [3], used
+        used.append((len(tails), len(pins), cconvs, sorted(set(stashed)), sorted(set(pairs))))
+    # the act phase caches conv1 and the downsample (both read the block input) and gathers
+    # both their rows in one launch per iteration (the plain loop: the batch input only); the
+    # weight phase computes the block's three AdaRound weights in one launch every iteration
+    assert used[0] == (0, 0, [], [], [False]) and used[1][0] > 0 and used[1][1] == 1 \
+        and used[1][2] == [2] and used[1][3] == [3] and used[1][4] == [True], used
     assert runs[0].keys() == runs[1].keys()
     for k in runs[0]:
         if k.endswith("_rec"):
