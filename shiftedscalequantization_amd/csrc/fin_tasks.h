@@ -106,15 +106,34 @@ __device__ __forceinline__ void fin_loss(const double* __restrict__ part, int nb
 // epilogue backward: workgroups [0, nb) the per-channel gamma / phi gradients, kEpiChan
 // channels per workgroup, the samples n split over its 4 waves (wave w sums n = w, w + 4,
 // ... in order, then the 4 wave sums are added in wave order: every load of a channel in
-// flight at once); workgroup nb (when launched) the act quantizer's delta / zp gradients
-// (rows in a fixed order, as fq_bwd_finalize)
+// flight at once); workgroups [nb, nb + nd) (when launched) the act quantizer's delta / zp
+// gradients: workgroup nb + j sums the j-th of nd contiguous row ranges in a fixed order,
+// and the last to arrive adds the nd partials in range order (deterministic, as
+// fq_bwd_finalize; one range below kDeltaRows rows -- a single workgroup walking 16K
+// strided row records was 12 us of load latency on ResNet-18 layer4)
 constexpr uint32_t kEpiChan = kBlock / 4;
+constexpr uint32_t kDeltaRows = 1024;   // rows per delta workgroup (one batch of loads)
+constexpr uint32_t kMaxDeltaWg = 16;
+__host__ __device__ inline uint32_t delta_wgs(uint32_t rows) {
+  const uint32_t d = (rows + kDeltaRows - 1) / kDeltaRows;
+  return d < 1 ? 1 : (d > kMaxDeltaWg ? kMaxDeltaWg : d);
+}
+// the delta partials: after the row records and the fused tail's loss partials
+// (ssq_epilogue_bwd_workspace_size)
+__host__ __device__ inline size_t delta_part_offset(size_t rows) {
+  return rows * kEpiParts + (rows + 3) / 4;
+}
+// last-arriver counters of the delta reduction, one per task slot of a table (a table's
+// tasks run in one launch; launches on a stream run in order).  Per translation unit:
+// every kernel that runs tasks is in the TU whose counters it uses, each reset to zero by
+// its last arriver.
+static __device__ unsigned g_fin_ticket[kMaxFin + 1];
 __device__ __forceinline__ void fin_epi(uint32_t bid, const double* __restrict__ part, uint32_t N,
-                                        uint32_t C, uint32_t nb, uint32_t s0,
+                                        uint32_t C, uint32_t nb, uint32_t nd, uint32_t s0,
                                         float* __restrict__ ggamma,
                                         float* __restrict__ gphi, float* __restrict__ gdelta,
                                         float* __restrict__ gzp, const AdamConst& ac,
-                                        const AdamRef* ad) {
+                                        const AdamRef* ad, unsigned* ticket) {
   __shared__ double red[16];
   if (bid < nb) {
     __shared__ double wsum[4][kEpiChan][2];
@@ -158,24 +177,42 @@ __device__ __forceinline__ void fin_epi(uint32_t bid, const double* __restrict__
     sd[1] = ad[2].m[0];
     sd[2] = ad[2].v[0];
   }
+  const uint32_t rows = N * C, j = bid - nb;
+  const uint32_t per = (rows + nd - 1) / nd, lo = j * per, hi = min(rows, lo + per);
   double a[4] = {0, 0, 0, 0};
   constexpr uint32_t kB = kFinBatch / 4;   // 4 sums per row: keep the registers of the
                                             // host kernels this rides on (occupancy) low
-  for (uint32_t r0 = threadIdx.x; r0 < N * C; r0 += kB * kBlock) {
+  for (uint32_t r0 = lo + threadIdx.x; r0 < hi; r0 += kB * kBlock) {
     double v[kB][4];
 #pragma unroll
-    for (uint32_t j = 0; j < kB; ++j) {
-      const uint32_t r = r0 + j * kBlock;
+    for (uint32_t b = 0; b < kB; ++b) {
+      const uint32_t r = r0 + b * kBlock;
 #pragma unroll
-      for (int k = 0; k < 4; ++k) v[j][k] = r < N * C ? part[(int64_t)r * kEpiParts + 2 + k] : 0.0;
+      for (int k = 0; k < 4; ++k) v[b][k] = r < hi ? part[(int64_t)r * kEpiParts + 2 + k] : 0.0;
     }
 #pragma unroll
-    for (uint32_t j = 0; j < kB; ++j)
-      if (r0 + j * kBlock < N * C)
+    for (uint32_t b = 0; b < kB; ++b)
+      if (r0 + b * kBlock < hi)
 #pragma unroll
-        for (int k = 0; k < 4; ++k) a[k] += v[j][k];
+        for (int k = 0; k < 4; ++k) a[k] += v[b][k];
   }
   for (int k = 0; k < 4; ++k) a[k] = block_sum(a[k], red);
+  if (nd > 1) {
+    double* dp = const_cast<double*>(part) + delta_part_offset(rows);
+    if (threadIdx.x == 0)
+      for (int k = 0; k < 4; ++k) st_sc1(dp + 4 * j + k, a[k]);
+    __shared__ int last;
+    __shared__ double dps[4 * kMaxDeltaWg];
+    if (!arrive_last(ticket, nd, &last)) return;
+    if (threadIdx.x < 4 * nd) dps[threadIdx.x] = ld_sc1(dp + threadIdx.x);
+    __syncthreads();
+    if (threadIdx.x == 0)
+      for (int k = 0; k < 4; ++k) {
+        double t = 0.0;
+        for (uint32_t i = 0; i < nd; ++i) t += dps[4 * i + k];
+        a[k] = t;
+      }
+  }
   if (threadIdx.x == 0) {
     const float gd = (float)(a[0] - a[1]);
     if (gdelta) gdelta[0] = gd;
@@ -220,7 +257,8 @@ __device__ __forceinline__ void run_fin(const FinTable& ft, uint32_t k) {
       if (t.kind == 0)
         fin_loss(t.part, (int)t.a, t.m, t.o[0]);
       else if (t.kind == 1)
-        fin_epi(k, t.part, t.a, t.b, t.c, t.s0, t.o[0], t.o[1], t.o[2], t.o[3], ft.ac, t.ad);
+        fin_epi(k, t.part, t.a, t.b, t.c, t.nwg - t.c, t.s0, t.o[0], t.o[1], t.o[2], t.o[3],
+                ft.ac, t.ad, &g_fin_ticket[i]);
       else if (t.kind == 2)
         fin_loss_rows(t.part, t.a, t.m, t.o[0]);
       else

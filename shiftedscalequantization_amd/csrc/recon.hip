@@ -550,7 +550,8 @@ __global__ __launch_bounds__(kBlock) void epilogue_bwd_finalize(
     float* __restrict__ ggamma, float* __restrict__ gphi, float* __restrict__ gdelta,
     float* __restrict__ gzp) {
   const AdamRef none[3] = {AdamRef{}, AdamRef{}, AdamRef{}};
-  fin_epi(blockIdx.x, part, N, C, nb, 0, ggamma, gphi, gdelta, gzp, AdamConst{}, none);
+  fin_epi(blockIdx.x, part, N, C, nb, gridDim.x - nb, 0, ggamma, gphi, gdelta, gzp, AdamConst{},
+          none, &g_fin_ticket[kMaxFin]);
 }
 
 // the queued finalize tasks of a stream as one standalone launch
@@ -897,8 +898,9 @@ extern "C" int ssq_epilogue_fwd(const float* y, const float* bias, const float* 
 }
 
 extern "C" size_t ssq_epilogue_bwd_workspace_size(int64_t rows) {
-  // the rows' records, then (fused tail) one loss partial per workgroup: <= ceil(rows / 4)
-  return ((size_t)rows * kEpiParts + (size_t)(rows + 3) / 4) * sizeof(double);
+  // the rows' records, then (fused tail) one loss partial per workgroup: <= ceil(rows / 4),
+  // then the delta reduction's workgroup partials (fin_epi)
+  return (delta_part_offset((size_t)rows) + 4 * kMaxDeltaWg) * sizeof(double);
 }
 
 // ssq_epilogue_bwd (g = dL/d(output)) and its fused-tail form ssq_epilogue_loss_bwd
@@ -1043,10 +1045,11 @@ static int epilogue_bwd(const char* what, const float* g, const float* y, const 
     if (rc) return rc;
   }
   if (ggamma || gphi || gdelta || gzp) {
-    // blocks [0, nb) only when gamma / phi are wanted; block nb (the act quantizer's four
-    // sums over every row, one workgroup) only when delta / zp are
+    // blocks [0, nb) only when gamma / phi are wanted; blocks [nb, nb + nq) (the act
+    // quantizer's four sums over every row, kDeltaRows rows per workgroup) only when delta /
+    // zp are
     const unsigned nb = (ggamma || gphi) ? (unsigned)((C + kEpiChan - 1) / kEpiChan) : 0u;
-    const unsigned nq = (gdelta || gzp) ? 1u : 0u;
+    const unsigned nq = (gdelta || gzp) ? delta_wgs((uint32_t)rows) : 0u;
     if (fin_defer_on()) {
       FinTask t{};
       t.kind = 1;

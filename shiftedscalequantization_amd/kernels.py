@@ -1160,6 +1160,11 @@ _EPI_SLOT = [0]
 
 def _epi_slot():
     _EPI_SLOT[0] ^= 1
+    return _epi_slot_name()
+
+
+def _epi_slot_name():
+    """The workspace slot of the last epilogue backward (tests read its row records)."""
     return "epi%d" % _EPI_SLOT[0]
 
 

@@ -1445,6 +1445,57 @@ def test_epilogue_bwd_without_dy(K, quant):
         np.testing.assert_array_equal(a, b)
 
 
+@pytest.mark.parametrize("shape", [(8, 125, 5), (11, 100, 8), (40, 500, 7)])
+def test_epilogue_bwd_delta_split(K, shape):
+    """The act quantizer's delta / zero-point sums of the epilogue backward over many rows:
+    one workgroup per 1024 rows (<= 16), the last to arrive adding the partials in range
+    order (csrc/fin_tasks.h fin_epi).  1000 rows (one workgroup), 1100 (two), 20000 (16).
+    Against the float64 sum of the launch's own row records; deferred (riding on a later
+    launch) and standalone bit-identical; repeated calls identical (the counter resets); and
+    the unfused epilogue + fake-quant composition within the affine epilogue's tolerance."""
+    from shiftedscalequantization_amd import _capi as A
+    from shiftedscalequantization_amd.quant.quant_layer import UniformAffineQuantizer
+    N, C, hw = shape
+    gen = torch.Generator().manual_seed(N + C)
+    y = torch.randn(N, C, hw, hw, generator=gen).cuda()
+    bias = (0.1 * torch.randn(C, generator=gen)).cuda()
+    g = torch.randn(N, C, hw, hw, generator=gen).cuda()
+    gm0 = (1 + 0.1 * torch.randn(1, C, 1, 1, generator=gen)).cuda()
+    ph0 = (0.1 * torch.randn(1, C, 1, 1, generator=gen)).cuda()
+
+    def run(defer, fused=True):
+        gamma, phi = gm0.clone().requires_grad_(True), ph0.clone().requires_grad_(True)
+        q = UniformAffineQuantizer(n_bits=4, channel_wise=False, scale_method="max", leaf_param=True).cuda()
+        q.delta = torch.nn.Parameter(torch.tensor(0.23).cuda())
+        q.zero_point = torch.nn.Parameter(torch.tensor(3.0).cuda())
+        q.inited = True
+        cache = {}
+        with A.workspace_scope(cache), K.deferred_finalize(defer):
+            if fused:
+                out = K.epilogue(y, bias, gamma, phi, None, 1, q)
+            else:
+                out = q(K.epilogue(y, bias, gamma, phi, None, 1, None))
+            out.backward(g)
+        torch.cuda.synchronize()
+        ws = [b for k, b in cache.items() if k[2] == K._epi_slot_name()] if fused else []
+        return [host(t).reshape(-1).copy() for t in (q.delta.grad, q.zero_point.grad, gamma.grad,
+                                                     phi.grad)], ws
+
+    base, ws = run(False)
+    rows = N * C
+    rec = ws[0][:rows * 9 * 8].view(torch.float64).view(rows, 9).cpu().numpy()
+    a = rec[:, 2:6].sum(axis=0)
+    np.testing.assert_allclose(base[0], [a[0] - a[1]], rtol=1e-6, atol=0)
+    np.testing.assert_allclose(base[1], [a[2] - a[3]], rtol=1e-6, atol=1e-6)
+    for defer in (True, False, True):
+        got, _ = run(defer)
+        for x, b in zip(got, base):
+            np.testing.assert_array_equal(x.view(np.int32), b.view(np.int32))
+    unf, _ = run(False, fused=False)
+    for x, b in zip(base, unf):      # (x/d)/d vs (x/d)*(1/d): see _compare_fused_unfused
+        np.testing.assert_allclose(x, b, rtol=1e-4, atol=1e-3 * max(1.0, float(np.abs(b).max())))
+
+
 def test_armed_adam_falls_back_when_not_covered(K):
     """An armed step the alpha backward cannot take entirely (a parameter whose gradient
     no launch of the stream produced) is left alone: adam_take() is False and nothing was
