@@ -544,6 +544,89 @@ def test_brecq_layer_reconstruction_matches_reference(Q, golden, graph):
         parity_report(f"a22_layer_reconstruction[graph={graph}]", **stats)
 
 
+@pytest.mark.parametrize("affine", [False, True])
+def test_brecq_act_identity_block_gathers_input_with_conv(Q, affine, det_convs):
+    """BRECQ's act phase on a block with an identity residual (no downsample, e.g. ResNet-18
+    layer1.1): the block input is still read (the residual), so each iteration gathers it
+    together with the cached conv1 rows in ONE ssq_gather_rows2 launch (GATHER_ONCE); act
+    deltas and Adam moments bit-identical to the plain loop (every knob off), losses to the
+    last ulps."""
+    import importlib
+    from shiftedscalequantization_amd import nets
+    BR = importlib.import_module("shiftedscalequantization_amd.quant.block_recon")
+    E = importlib.import_module("shiftedscalequantization_amd.quant._engine")
+    knobs = ("DEFER_FINALIZE", "FUSE_TAIL", "PIN_WEIGHTS", "CACHE_CONVS", "STASH_ADAROUND",
+             "GATHER_ONCE")
+    gen = torch.Generator().manual_seed(21)
+    cali = torch.randn(32, 3, 12, 12, generator=gen).cuda()
+    runs, pairs = [], []
+    for on in (False, True):
+        torch.manual_seed(5)
+        net = nn.Sequential(nn.Conv2d(3, 16, 3, padding=1, bias=False), nn.BatchNorm2d(16),
+                            nn.ReLU(), nets.BasicBlock(16, 16), nn.AdaptiveAvgPool2d(1),
+                            nn.Flatten(), nn.Linear(16, 10)).eval()
+        qnn = Q.QuantModel(net, {"n_bits": 2, "channel_wise": True, "scale_method": "max"},
+                           {"n_bits": 4, "channel_wise": False, "scale_method": "mse",
+                            "leaf_param": True}).cuda().eval()
+        qnn.set_first_last_layer_to_8bit()
+        block = qnn.model[3]
+        if affine:
+            g2 = torch.Generator().manual_seed(7)
+            for n in ("conv1", "conv2"):
+                m = getattr(block, n)
+                with torch.no_grad():
+                    m.alpha_out.copy_(1 + 0.05 * torch.randn(m.alpha_out.shape, generator=g2))
+                    m.beta_out.copy_(0.02 * torch.randn(m.beta_out.shape, generator=g2))
+        qnn.set_quant_state(True, True)
+        with torch.no_grad():
+            qnn(cali[:8])
+        seen, opts, got = [], [], []
+        orig_rec, orig_init, orig_gather = BR.LossFunction.record, E.SsqAdam.__init__, BR.K.gather_rows2
+
+        def spy(self, rec, rnd, b):
+            r = orig_rec(self, rec, rnd, b)
+            seen.append(float(r))
+            return r
+
+        def init(self, *a, **k):
+            orig_init(self, *a, **k)
+            opts.append(self)
+
+        def gather(src0, idx, src1=None, **k):
+            got.append(src1 is not None)
+            return orig_gather(src0, idx, src1, **k)
+
+        prev = {k: getattr(BR, k) for k in knobs}
+        BR.LossFunction.record, E.SsqAdam.__init__, BR.K.gather_rows2 = spy, init, gather
+        for k in knobs:
+            setattr(BR, k, on)
+        try:
+            torch.manual_seed(1005)
+            Q.block_reconstruction(qnn, block, cali, batch_size=8, iters=12, act_quant=True,
+                                   opt_mode="mse", lr=4e-4, p=2.4)
+        finally:
+            BR.LossFunction.record, E.SsqAdam.__init__, BR.K.gather_rows2 = orig_rec, orig_init, orig_gather
+            for k, v in prev.items():
+                setattr(BR, k, v)
+        out = {"rec": np.array(seen),
+               "delta": np.array([float(q.delta) for q in
+                                  [block.act_quantizer, block.conv1.act_quantizer,
+                                   block.conv2.act_quantizer] if q.delta is not None])}
+        for k, o in enumerate(opts):
+            for j, p_ in enumerate(o.params):
+                out[f"opt{k}_m{j}"] = o.state[p_]["exp_avg"].cpu().numpy()
+                out[f"opt{k}_v{j}"] = o.state[p_]["exp_avg_sq"].cpu().numpy()
+        runs.append(out)
+        pairs.append(sorted(set(got)))
+    assert pairs == [[False], [True]], pairs
+    assert runs[0].keys() == runs[1].keys() and len(runs[0]["rec"]) == 12
+    for k in runs[0]:
+        if k == "rec":
+            np.testing.assert_allclose(runs[1][k], runs[0][k], rtol=1e-6, err_msg=k)
+        else:
+            np.testing.assert_array_equal(runs[1][k], runs[0][k], err_msg=k)
+
+
 def test_brecq_frozen_loop_skips_unreported_iterations(Q, golden):
     """A loop in which nothing learns (the fc's act phase: its act quantizer is the disabled
     network output) runs only its reported iterations (SKIP_FROZEN): the same printed
