@@ -246,15 +246,22 @@ struct AdamTable {
 
 __global__ __launch_bounds__(kBlock) void adam_kernel(AdamTable tab, float w1, float b2, float w2,
                                                       float eps, const float* __restrict__ hyper,
-                                                      float nss, float bc2s) {
+                                                      float nss, float bc2s, FinTable fin) {
+  // queued finalize tasks that write none of the gradients read here ride on the launch
+  // (its first workgroups; ssq_adam)
+  if (blockIdx.x < fin.nwg) {
+    run_fin(fin, blockIdx.x);
+    return;
+  }
+  const uint32_t bid = blockIdx.x - fin.nwg;
   if (hyper) {
     nss = hyper[0];
     bc2s = hyper[1];
   }
   int si = 0;
-  while (si + 1 < tab.nseg && blockIdx.x >= tab.s[si + 1].blk0) ++si;
+  while (si + 1 < tab.nseg && bid >= tab.s[si + 1].blk0) ++si;
   const AdamSeg& sg = tab.s[si];
-  const uint32_t t0 = (blockIdx.x - sg.blk0) * (uint32_t)kAdamTile;
+  const uint32_t t0 = (bid - sg.blk0) * (uint32_t)kAdamTile;
   const uint32_t t1 = min(t0 + (uint32_t)kAdamTile, sg.n);
   for (uint32_t e = t0 + threadIdx.x; e < t1; e += blockDim.x) {
     const float g = sg.g[e];
@@ -1228,9 +1235,33 @@ extern "C" int ssq_adam(int nseg, float* const* p, const float* const* g, float*
   if (adam_ride((hipStream_t)stream, nseg, p, g, m, v, n,
                 AdamConst{one_minus_beta1, beta2, one_minus_beta2, eps, hyper}))
     return check_launch("ssq_adam (riding on the pending finalizes)");
-  {  // queued gamma / phi / delta gradient finalizes must land before the update reads them
-    const int rc = fin_flush((hipStream_t)stream);
-    if (rc) return rc;
+  // queued finalizes: those that write a gradient read here (gamma / phi / delta) must land
+  // before the update -- launched first, standalone; the others (e.g. the loss value) ride
+  // on the update's first launch
+  FinTable ride{};
+  {
+    bool disjoint = true;
+    for (int t = 0; t < g_fin_npending && disjoint; ++t) {
+      const PendingFin& pf = g_fin_pending[t];
+      if (pf.s != (hipStream_t)stream) continue;
+      for (int j = 0; j < 4; ++j) {
+        if (!pf.t.o[j]) continue;
+        // what the task writes: gamma / phi gradients (C floats) or one float
+        const int64_t len = (pf.t.kind == 1 && j < 2) ? (int64_t)pf.t.b
+                            : (pf.t.kind == 3 ? (int64_t)pf.t.a : 1);
+        const float* lo = pf.t.o[j];
+        for (int i = 0; i < nseg; ++i)
+          if (lo < g[i] + n[i] && g[i] < lo + len) disjoint = false;
+      }
+    }
+    int npend = 0;
+    for (int t = 0; t < g_fin_npending; ++t) npend += g_fin_pending[t].s == (hipStream_t)stream;
+    if (disjoint && npend <= kMaxFin) {
+      ride = fin_take((hipStream_t)stream);
+    } else {
+      const int rc = fin_flush((hipStream_t)stream);
+      if (rc) return rc;
+    }
   }
   for (int base = 0; base < nseg; base += kMaxAdamSeg) {
     AdamTable tab;
@@ -1244,11 +1275,12 @@ extern "C" int ssq_adam(int nseg, float* const* p, const float* const* g, float*
       blk += (n[i] + kAdamTile - 1) / kAdamTile;
     }
     SSQ_REQUIRE(blk < (1ll << 31), SSQ_E_ARG, "ssq_adam: too many tiles");
-    hipLaunchKernelGGL(adam_kernel, dim3((unsigned)blk), dim3(kBlock), 0, (hipStream_t)stream, tab,
-                       one_minus_beta1, beta2, one_minus_beta2, eps, hyper, neg_step_size,
-                       bias_correction2_sqrt);
+    hipLaunchKernelGGL(adam_kernel, dim3((unsigned)(blk + ride.nwg)), dim3(kBlock), 0,
+                       (hipStream_t)stream, tab, one_minus_beta1, beta2, one_minus_beta2, eps, hyper,
+                       neg_step_size, bias_correction2_sqrt, ride);
     const int rc = check_launch("ssq_adam");
     if (rc) return rc;
+    ride = FinTable{};
   }
   return SSQ_OK;
 }
