@@ -3,6 +3,10 @@
     python bench.py [--gpus N] [--steps K] [--warmup W]
     python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N ...
 
+`--gpus N` alone starts its own N rank processes (shiftedscalequantization_amd/launch.py, as
+the reference's mp.spawn, Brecq/main_imagenet_dist.py:268-271); under an external launcher
+(WORLD_SIZE set) this process is one rank.
+
 One step (configs[1], ResNet-18 W2A4, 1024 calibration samples, synthetic data) =
   * A4 per-tensor q/dq of the block-input activation cache [1024,64,56,56] fp32
     (205.5 M elements, 822 MB >> the 256 MB Infinity Cache), delta/zp from the 'mse'
@@ -24,6 +28,15 @@ import sys
 import tempfile
 import time
 
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+if __name__ == "__main__":
+    # --gpus N > 1 without an external launcher: start N rank processes of this script now,
+    # before torch (and the HIP runtime) is loaded in this parent (launch.py)
+    from shiftedscalequantization_amd.launch import maybe_spawn
+    maybe_spawn(os.path.abspath(__file__))
+
 # MIOpen persists its solver choices in a per-user find-db that outlives the process: a
 # test run that convolved under cudnn.deterministic would otherwise hand its (slow,
 # deterministic) solvers to this bench's recon loops on the same box.  Fresh db per run.
@@ -31,9 +44,6 @@ os.environ.setdefault("MIOPEN_USER_DB_PATH", tempfile.mkdtemp(prefix="ssq_bench_
 
 import torch  # noqa: E402
 import torch.distributed as dist  # noqa: E402
-
-ROOT = os.path.dirname(os.path.abspath(__file__))
-sys.path.insert(0, ROOT)
 
 from shiftedscalequantization_amd import kernels as K  # noqa: E402
 
@@ -71,6 +81,9 @@ def setup(backend="nccl"):
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     ndev = torch.cuda.device_count()
+    if world > 1 and backend == "nccl" and world > ndev:
+        raise SystemExit(f"bench.py: {world} ranks over RCCL need {world} GPUs, {ndev} visible "
+                         f"(rehearse with --dist-backend gloo: ranks then share devices)")
     dev = torch.device("cuda", local % max(ndev, 1))
     torch.cuda.set_device(dev)
     if world > 1:
@@ -280,6 +293,9 @@ def cpu_baseline(act_dev, d_a, z_a, seconds, recon_state=None):
 def main():
     args = parse()
     rank, world, dev = setup(args.dist_backend)
+    if world > 1 and args.gpus not in (1, world):
+        print(f"bench.py: --gpus {args.gpus} but the launcher started {world} ranks; "
+              f"reporting {world}", file=sys.stderr)
     if args.variant >= 0:
         K.set_variant(args.variant)
     act, d_a, z_a, weights, dws, zws, bits = make_workload(dev, rank, args.n_cali)
@@ -391,6 +407,12 @@ def main():
                                "per-tensor q/dq of act [1024,64,56,56] + W2 per-channel q/dq of "
                                "all 21 conv/fc weights (8-bit stem/head)",
                    "elems_per_step_per_rank": elems_per_step, "parallelism": f"dp{world}"},
+        # how the ranks came to be and what the process group saw (n_gpus is the latter)
+        "launch": {"launcher": os.environ.get("SSQ_LAUNCHER",
+                                              "external" if "WORLD_SIZE" in os.environ else "none"),
+                   "world_size_backend": dist.get_world_size() if world > 1 else 1,
+                   "allreduce_backend": dist.get_backend() if world > 1 else None,
+                   "devices_visible": torch.cuda.device_count()},
         "roofline": {"bound": "hbm",
                      "kernel": "fq_fwd_pt_ride (ssq_fq_fwd per-tensor A4 with the 21 weights' "
                                "ssq_fq_fwd_multi tiles riding on the launch: the whole step)",

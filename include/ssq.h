@@ -323,6 +323,15 @@ int ssq_lp_loss_rows(const float* pred, const float* tgt_cache, const int64_t* i
 int ssq_gather_rows2(const float* src0, float* dst0, int64_t row0, const float* src1,
                      float* dst1, int64_t row1, const int64_t* idx, int64_t nidx,
                      ssq_stream_t stream);
+/* The same gather with the indices read from `slot` (one iteration's row of a device ring
+ * the host filled for several iterations at once: nidx indices, then the iteration's other
+ * words) and slot[0:stage_words] copied to stage_dst in the same launch -- the static words
+ * the iteration's later launches read (the loss rows' indices, Adam's step constants).  A
+ * loop captured as several iterations per graph replay starts each with this launch
+ * (quant/block_recon.py).                                                              */
+int ssq_gather_rows2_staged(const float* src0, float* dst0, int64_t row0, const float* src1,
+                            float* dst1, int64_t row1, const int64_t* slot, int64_t nidx,
+                            int64_t* stage_dst, int64_t stage_words, ssq_stream_t stream);
 
 /* ---------------------------------------------------------------- K13 fused epilogue
  * QuantModule conv bias add (quant_layer.py:250), the block's residual add and ReLU

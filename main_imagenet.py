@@ -14,17 +14,24 @@ Flow (the README flags mapped onto the snapshot's code):
      "Full quantization (W{w}A{a}) accuracy"); otherwise the reconstruction losses.
 Data: --data_path may hold cali.pt ([N,3,224,224] float) and val.pt ((images, labels));
 without it synthetic N(0,1) calibration images are used (no network access here).
-Multi-GPU: launch with torch.distributed.run; each rank calibrates on its shard of the
-calibration set and the per-iteration gradients are all-reduced over RCCL.
+Multi-GPU: `--gpus N` spawns N rank processes (as the reference's mp.spawn,
+Brecq/main_imagenet_dist.py:268-271), or launch with torch.distributed.run; each rank
+calibrates on its shard of the calibration set and the per-iteration gradients are
+all-reduced over RCCL.
 """
 import os
 import sys
 import time
 
-import torch
-import torch.distributed as dist
-
 sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+
+if __name__ == '__main__':
+    # before torch is imported: the parent of the spawned ranks never loads the HIP runtime
+    from shiftedscalequantization_amd.launch import maybe_spawn
+    maybe_spawn(os.path.abspath(__file__))
+
+import torch  # noqa: E402
+import torch.distributed as dist  # noqa: E402
 
 from shiftedscalequantization_amd import drivers as D  # noqa: E402
 from shiftedscalequantization_amd.cli import parse_args, seed_all, validate_model  # noqa: E402

@@ -84,7 +84,10 @@ def fake_quant_bwd(x, delta, zp, n_bits, sym, gy):
 
 # ----------------------------------------------------------------- K3 / K4  (quant_layer.py:100-175)
 def _py_round(v):
-    """Python's round(): half-to-even on a double."""
+    """Python's round(): half-to-even on a double; round(nan) raises ValueError (the
+    reference's 'max' init on a NaN row or x_min = -inf, quant_layer.py:140)."""
+    if np.isnan(v):
+        raise ValueError("cannot convert float NaN to integer")
     return float(np.rint(v))
 
 
@@ -117,7 +120,11 @@ def _quantize_cand(x, mx, mn, n_bits):
 
 def init_scale_mse(x, n_bits, sym=False, return_scores=False):
     """'mse' branch, quant_layer.py:144-162: 80 shrink candidates, Lp(2.4) score, first strict min."""
-    x = _f(x)
+    with np.errstate(all="ignore"):   # constant / infinite rows: x/0, inf/inf -> NaN scores
+        return _init_scale_mse(_f(x), n_bits, sym, return_scores)
+
+
+def _init_scale_mse(x, n_bits, sym, return_scores):
     x_max, x_min = F32(x.max()), F32(x.min())
     if sym:
         x_absmax = max(abs(x_min), x_max)
@@ -149,10 +156,16 @@ def init_scale(x, n_bits, sym=False, channel_wise=False, method="max"):
     if channel_wise:
         rows = x.reshape(x.shape[0], -1)
         res = [fn(r, n_bits, sym, **kw) for r in rows]
+        if any(v[0] is None for v in res):
+            # 'mse' found no candidate for a row: the reference assigns its None delta into
+            # the channel's slot, a TypeError (quant_layer.py:114)
+            raise TypeError("a row has no 'mse' quantization scale (delta None)")
         shape = (-1,) + (1,) * (x.ndim - 1)
         d, z, r = (np.array([v[i] for v in res], F32).reshape(shape) for i in range(3))
         return d, z, r
     d, z, r = fn(x, n_bits, sym, **kw)
+    if d is None:
+        return None, None, None   # per-tensor 'mse' without a candidate: the reference's None
     return F32(d), F32(z), F32(r)
 
 

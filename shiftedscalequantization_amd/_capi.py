@@ -72,6 +72,7 @@ SIGNATURES = {
     "ssq_lp_loss": (_i, [_p, _p, _i64, _i64, _f, _p, _p, _p, _i, _p, _sz, _p]),
     "ssq_lp_loss_rows": (_i, [_p, _p, _p, _i64, _i64, _i64, _f, _p, _p, _p, _i, _p, _sz, _p]),
     "ssq_gather_rows2": (_i, [_p, _p, _i64, _p, _p, _i64, _p, _i64, _p]),
+    "ssq_gather_rows2_staged": (_i, [_p, _p, _i64, _p, _p, _i64, _p, _i64, _p, _i64, _p]),
     "ssq_bias_act": (_i, [_p, _p, _p, _p, _i64, _i64, _i64, _i, _p]),
     "ssq_relu_bwd": (_i, [_p, _p, _p, _i64, _p]),
     "ssq_relu6_bwd": (_i, [_p, _p, _p, _i64, _p]),

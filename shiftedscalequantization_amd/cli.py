@@ -68,7 +68,11 @@ def build_parser():
     p.add_argument('--keep_features_on_host', default=False, type=bool)
     p.add_argument('--deterministic', default=1, type=int,
                    help='1 (reference): deterministic MIOpen conv solvers; 0: fastest solvers')
-    # data parallel (one process per GPU under torch.distributed.run)
+    # data parallel: one process per GPU, spawned by main_imagenet.py itself with --gpus N
+    # (the reference's mp.spawn, Brecq/main_imagenet_dist.py:268-271) or by an external
+    # torch.distributed.run
+    p.add_argument('--gpus', default=1, type=int,
+                   help='ranks to spawn on this node (one per GPU) when no launcher set WORLD_SIZE')
     p.add_argument('--dist_backend', default='nccl', type=str,
                    help="torch.distributed backend for world > 1: 'nccl' (= RCCL over xGMI); "
                         "'gloo' rehearses several ranks on one GPU")

@@ -123,17 +123,19 @@ __host__ __device__ inline uint32_t delta_wgs(uint32_t rows) {
 __host__ __device__ inline size_t delta_part_offset(size_t rows) {
   return rows * kEpiParts + (rows + 3) / 4;
 }
-// last-arriver counters of the delta reduction, one per task slot of a table (a table's
-// tasks run in one launch; launches on a stream run in order).  Per translation unit:
-// every kernel that runs tasks is in the TU whose counters it uses, each reset to zero by
-// its last arriver.
-static __device__ unsigned g_fin_ticket[kMaxFin + 1];
+// the delta reduction's last-arriver counter: one word after its partials, in the calling
+// epilogue backward's own workspace -- so two calls (other streams, other workspaces) never
+// share a counter.  The launch that writes the rows' records stores zero there (it runs
+// before any finalize of those records, in stream order), the last arriver resets it.
+__host__ __device__ inline size_t delta_ticket_offset(size_t rows) {
+  return delta_part_offset(rows) + 4 * kMaxDeltaWg;
+}
 __device__ __forceinline__ void fin_epi(uint32_t bid, const double* __restrict__ part, uint32_t N,
                                         uint32_t C, uint32_t nb, uint32_t nd, uint32_t s0,
                                         float* __restrict__ ggamma,
                                         float* __restrict__ gphi, float* __restrict__ gdelta,
                                         float* __restrict__ gzp, const AdamConst& ac,
-                                        const AdamRef* ad, unsigned* ticket) {
+                                        const AdamRef* ad) {
   __shared__ double red[16];
   if (bid < nb) {
     __shared__ double wsum[4][kEpiChan][2];
@@ -203,6 +205,7 @@ __device__ __forceinline__ void fin_epi(uint32_t bid, const double* __restrict__
       for (int k = 0; k < 4; ++k) st_sc1(dp + 4 * j + k, a[k]);
     __shared__ int last;
     __shared__ double dps[4 * kMaxDeltaWg];
+    unsigned* ticket = (unsigned*)(const_cast<double*>(part) + delta_ticket_offset(rows));
     if (!arrive_last(ticket, nd, &last)) return;
     if (threadIdx.x < 4 * nd) dps[threadIdx.x] = ld_sc1(dp + threadIdx.x);
     __syncthreads();
@@ -258,7 +261,7 @@ __device__ __forceinline__ void run_fin(const FinTable& ft, uint32_t k) {
         fin_loss(t.part, (int)t.a, t.m, t.o[0]);
       else if (t.kind == 1)
         fin_epi(k, t.part, t.a, t.b, t.c, t.nwg - t.c, t.s0, t.o[0], t.o[1], t.o[2], t.o[3],
-                ft.ac, t.ad, &g_fin_ticket[i]);
+                ft.ac, t.ad);
       else if (t.kind == 2)
         fin_loss_rows(t.part, t.a, t.m, t.o[0]);
       else

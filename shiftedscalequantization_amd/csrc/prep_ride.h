@@ -22,6 +22,11 @@ struct GatherArgs {
   const int64_t* idx;
   uint32_t gx;      // workgroups per batch row
   uint32_t nrows;   // batch rows
+  // staged form (ssq_gather_rows2_staged): idx is one slot of a device ring of iterations'
+  // words; its first stage_n words are also copied to stage_dst (the loop's static slot,
+  // read by the iteration's later launches), by the workgroup of (bx, r) = (0, 0)
+  int64_t* stage_dst;
+  uint32_t stage_n;
 };
 
 // dst[k] = src[k] for k = k0, k0 + stride, ... < n: kGatherU loads in flight per lane
@@ -49,6 +54,8 @@ __device__ __forceinline__ void gather2_body(const GatherArgs& a, uint32_t bx, u
   typedef typename std::conditional<VEC, f32x4, float>::type T;
   const int64_t w = VEC ? 4 : 1;
   const int64_t r0 = a.row0 / w, r1 = a.s1 ? a.row1 / w : 0;
+  if (a.stage_dst && bx == 0 && r == 0)
+    for (uint32_t k = threadIdx.x; k < a.stage_n; k += blockDim.x) a.stage_dst[k] = a.idx[k];
   const int64_t src = a.idx[r];
   const T* a0 = (const T*)a.s0 + src * r0;
   T* b0 = (T*)a.d0 + (int64_t)r * r0;

@@ -532,6 +532,11 @@ __global__ __launch_bounds__(kBlock) void epilogue_bwd_rows(
     return;
   }
   const uint32_t bid = blockIdx.x - fin.nwg;
+  // the act quantizer's delta reduction (fin_epi, a later launch) counts its workgroups in
+  // this call's workspace: start it at zero
+  if (QUANT && bid == 0 && threadIdx.x == 0)
+    __hip_atomic_store((gu32_t*)(part + delta_ticket_offset(rows)), 0u, __ATOMIC_RELAXED,
+                       __HIP_MEMORY_SCOPE_AGENT);
   const double wl = epilogue_rows_body<RES, ACT, QUANT, AFFINE, VEC, LOSS, RPW>(
       g, y, bias, gamma, phi, res, rows, C, hw, qdelta, qzp, lo, hi, gy, gres, part, lidx, inv_m,
       lp, re, bid);
@@ -558,7 +563,7 @@ __global__ __launch_bounds__(kBlock) void epilogue_bwd_finalize(
     float* __restrict__ gzp) {
   const AdamRef none[3] = {AdamRef{}, AdamRef{}, AdamRef{}};
   fin_epi(blockIdx.x, part, N, C, nb, gridDim.x - nb, 0, ggamma, gphi, gdelta, gzp, AdamConst{},
-          none, &g_fin_ticket[kMaxFin]);
+          none);
 }
 
 // the queued finalize tasks of a stream as one standalone launch
@@ -815,9 +820,9 @@ extern "C" int ssq_lp_loss_rows(const float* pred, const float* tgt_cache, const
                  relu_mask, ws, ws_bytes, (hipStream_t)stream);
 }
 
-extern "C" int ssq_gather_rows2(const float* src0, float* dst0, int64_t row0, const float* src1,
-                                float* dst1, int64_t row1, const int64_t* idx, int64_t nidx,
-                                ssq_stream_t stream) {
+static int gather_rows2(const float* src0, float* dst0, int64_t row0, const float* src1,
+                        float* dst1, int64_t row1, const int64_t* idx, int64_t nidx,
+                        int64_t* stage_dst, int64_t stage_n, hipStream_t stream) {
   SSQ_REQUIRE(src0 && dst0 && idx && row0 >= 1 && nidx >= 1, SSQ_E_ARG,
               "ssq_gather_rows2: bad args");
   SSQ_REQUIRE(!src1 || (dst1 && row1 >= 1), SSQ_E_ARG, "ssq_gather_rows2: bad second source");
@@ -830,10 +835,30 @@ extern "C" int ssq_gather_rows2(const float* src0, float* dst0, int64_t row0, co
   const int64_t need = (per + kBlock - 1) / kBlock;
   if (gx > need) gx = need;
   if (gx < 1) gx = 1;
-  GatherArgs a{src0, dst0, row0, src1, dst1, row1, idx, (uint32_t)gx, (uint32_t)nidx};
-  const int rc = launch_gather((hipStream_t)stream, a, vec);
+  GatherArgs a{src0, dst0, row0, src1, dst1, row1, idx, (uint32_t)gx, (uint32_t)nidx,
+               stage_dst, (uint32_t)stage_n};
+  const int rc = launch_gather(stream, a, vec);
   if (rc) return rc;
   return check_launch("ssq_gather_rows2");
+}
+
+extern "C" int ssq_gather_rows2(const float* src0, float* dst0, int64_t row0, const float* src1,
+                                float* dst1, int64_t row1, const int64_t* idx, int64_t nidx,
+                                ssq_stream_t stream) {
+  return gather_rows2(src0, dst0, row0, src1, dst1, row1, idx, nidx, nullptr, 0,
+                      (hipStream_t)stream);
+}
+
+extern "C" int ssq_gather_rows2_staged(const float* src0, float* dst0, int64_t row0,
+                                       const float* src1, float* dst1, int64_t row1,
+                                       const int64_t* slot, int64_t nidx, int64_t* stage_dst,
+                                       int64_t stage_words, ssq_stream_t stream) {
+  SSQ_REQUIRE(slot && stage_dst && stage_words >= nidx && stage_words <= 65536, SSQ_E_ARG,
+              "ssq_gather_rows2_staged: the slot holds the nidx indices first, <= 65536 words");
+  SSQ_REQUIRE(stage_dst + stage_words <= slot || slot + stage_words <= stage_dst, SSQ_E_ARG,
+              "ssq_gather_rows2_staged: slot and stage_dst overlap");
+  return gather_rows2(src0, dst0, row0, src1, dst1, row1, slot, nidx, stage_dst, stage_words,
+                      (hipStream_t)stream);
 }
 
 // A/B knob SSQ_EPI_MULTI_ROW: 4 rows per wave on small planes for the epilogue backward
@@ -906,8 +931,8 @@ extern "C" int ssq_epilogue_fwd(const float* y, const float* bias, const float* 
 
 extern "C" size_t ssq_epilogue_bwd_workspace_size(int64_t rows) {
   // the rows' records, then (fused tail) one loss partial per workgroup: <= ceil(rows / 4),
-  // then the delta reduction's workgroup partials (fin_epi)
-  return (delta_part_offset((size_t)rows) + 4 * kMaxDeltaWg) * sizeof(double);
+  // then the delta reduction's workgroup partials and its counter (fin_epi)
+  return (delta_ticket_offset((size_t)rows) + 1) * sizeof(double);
 }
 
 // ssq_epilogue_bwd (g = dL/d(output)) and its fused-tail form ssq_epilogue_loss_bwd

@@ -16,6 +16,21 @@ namespace ssq {
 constexpr int kCand = 80;
 constexpr int kSlice = 8192;  // elements of one row handled by one workgroup (32 KB LDS)
 
+// torch.min / torch.max propagate NaN (the reference's x.min() / x.max(),
+// quant_layer.py:124-125,145-146): IEEE 754-2019 minimum / maximum, not fminf / fmaxf
+__device__ __forceinline__ float nan_min(float a, float b) { return __builtin_elementwise_minimum(a, b); }
+__device__ __forceinline__ float nan_max(float a, float b) { return __builtin_elementwise_maximum(a, b); }
+__device__ __forceinline__ float wave_nan_min(float v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v = nan_min(v, __shfl_xor(v, o, kWave));
+  return v;
+}
+__device__ __forceinline__ float wave_nan_max(float v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v = nan_max(v, __shfl_xor(v, o, kWave));
+  return v;
+}
+
 __global__ __launch_bounds__(kBlock) void minmax_stage(const float* __restrict__ x, int64_t inner,
                                                        int nslice, float* __restrict__ pmin,
                                                        float* __restrict__ pmax) {
@@ -26,11 +41,11 @@ __global__ __launch_bounds__(kBlock) void minmax_stage(const float* __restrict__
   float mn = INFINITY, mx = -INFINITY;
   for (int64_t k = s0 + threadIdx.x; k < s1; k += blockDim.x) {
     const float v = r[k];
-    mn = fminf(mn, v);
-    mx = fmaxf(mx, v);
+    mn = nan_min(mn, v);
+    mx = nan_max(mx, v);
   }
-  mn = wave_min(mn);
-  mx = wave_max(mx);
+  mn = wave_nan_min(mn);
+  mx = wave_nan_max(mx);
   const int lane = threadIdx.x & (kWave - 1), w = threadIdx.x / kWave;
   if (lane == 0) {
     smin[w] = mn;
@@ -39,11 +54,11 @@ __global__ __launch_bounds__(kBlock) void minmax_stage(const float* __restrict__
   __syncthreads();
   if (threadIdx.x == 0) {
     for (int i = 1; i < kBlock / kWave; ++i) {
-      mn = fminf(mn, smin[i]);
-      mx = fmaxf(mx, smax[i]);
+      mn = nan_min(mn, smin[i]);
+      mx = nan_max(mx, smax[i]);
     }
-    mn = fminf(smin[0], mn);
-    mx = fmaxf(smax[0], mx);
+    mn = nan_min(smin[0], mn);
+    mx = nan_max(smax[0], mx);
     pmin[row * nslice + blockIdx.x] = mn;
     pmax[row * nslice + blockIdx.x] = mx;
   }
@@ -54,12 +69,15 @@ __device__ __forceinline__ void row_minmax(const float* pmin, const float* pmax,
   mn = pmin[row * nslice];
   mx = pmax[row * nslice];
   for (int i = 1; i < nslice; ++i) {
-    mn = fminf(mn, pmin[row * nslice + i]);
-    mx = fmaxf(mx, pmax[row * nslice + i]);
+    mn = nan_min(mn, pmin[row * nslice + i]);
+    mx = nan_max(mx, pmax[row * nslice + i]);
   }
 }
 
-// 'max' finalize: host Python fp64 arithmetic (quant_layer.py:124-142).
+// 'max' finalize: host Python fp64 arithmetic (quant_layer.py:124-142).  A row the
+// reference cannot initialise -- a NaN extremum, or x_min = -inf, where its
+// round(-x_min / delta) is round(nan) and raises ValueError (:140) -- gets delta = zp =
+// raw_zp = NaN, which the host layer turns into that error (kernels.scale_init).
 __global__ void finalize_max(const float* __restrict__ pmin, const float* __restrict__ pmax,
                              int64_t rows, int nslice, int n_bits, int sym, int scale_flag,
                              float* __restrict__ delta, float* __restrict__ zp,
@@ -81,6 +99,10 @@ __global__ void finalize_max(const float* __restrict__ pmin, const float* __rest
   double d = (x_max - x_min) / (double)((1 << n_bits) - 1);
   if (d < 1e-8) d = 1e-8;
   const double z = rint(-x_min / d);  // Python round(): half-to-even
+  if (isnan(fmn) || isnan(fmx) || isnan(z)) {
+    delta[row] = zp[row] = raw_zp[row] = NAN;
+    return;
+  }
   delta[row] = (float)d;
   zp[row] = (float)z;
   raw_zp[row] = (float)(-x_min);
@@ -100,8 +122,10 @@ __device__ __forceinline__ void candidate(float mx, float mn, int i, int n_bits,
   z = rintf(-nmin / d);
 }
 
+// |e|^2.4 with NaN kept NaN (torch.pow): a candidate whose error is NaN anywhere scores NaN
+// and is never the strict minimum, as in the reference (quant_layer.py:157-158)
 __device__ __forceinline__ float pow24(float a) {
-  return a > 0.0f ? exp2f(2.4f * log2f(a)) : 0.0f;
+  return a > 0.0f ? exp2f(2.4f * log2f(a)) : (a == 0.0f ? 0.0f : a);
 }
 
 __global__ __launch_bounds__(kBlock) void mse_stage(const float* __restrict__ x, int64_t inner,
@@ -168,6 +192,9 @@ __global__ void finalize_mse(const double* __restrict__ part, const float* __res
     mn = mn < 0.0f ? -a : 0.0f;
     mx = a;
   }
+  // no candidate with a score below 1e10 (a NaN row, an infinite extremum, a constant row:
+  // every score NaN) leaves the reference's delta None (quant_layer.py:147-162), which it
+  // cannot use: NaN here, raised by the host layer
   double best = 1e10;
   float bd = NAN, bz = NAN, br = NAN;
   for (int c = 0; c < kCand; ++c) {

@@ -298,10 +298,21 @@ class deferred_fq_multi:
 
 
 # ------------------------------------------------------------------ K3/K4
-def scale_init(x, n_bits, sym=False, channel_wise=False, method="max", return_scores=False):
+class ScaleInitError(A.SSQError, ValueError):
+    """A row the reference's init_quantization_scale cannot initialise."""
+
+
+def scale_init(x, n_bits, sym=False, channel_wise=False, method="max", return_scores=False,
+               check=True):
     """init_quantization_scale (quant_layer.py:100-166) on the device.
     Returns (delta, zero_point, raw_zero_point) shaped like the reference's:
-    (Co,1,1,1)/(Co,1) for channel_wise, 0-dim otherwise."""
+    (Co,1,1,1)/(Co,1) for channel_wise, 0-dim otherwise.
+
+    A row holding NaN (or, for 'max', -inf; for 'mse', any infinity or a constant row) has no
+    init in the reference: 'max' raises ValueError at round(nan) (:140), 'mse' never assigns
+    delta (:147-162) and fails where it is used.  ssq_scale_init marks such rows NaN and this
+    raises ScaleInitError (an SSQError and a ValueError) naming them -- one host sync, as the
+    reference's own .item() calls; check=False skips it (the caller inspects the NaN rows)."""
     x, xp = fptr(x.detach(), "x")
     if "max" in method:
         m, sflag = 0, int("scale" in method)
@@ -319,6 +330,13 @@ def scale_init(x, n_bits, sym=False, channel_wise=False, method="max", return_sc
     ws, wsn = workspace(wsb, x.device)
     call("ssq_scale_init", xp, rows, inner, n_bits, int(sym), m, sflag, _vp(d), _vp(z), _vp(r),
          _vp(sc), ws, wsn, stream_of(x))
+    if check:
+        bad = torch.isnan(d) | torch.isnan(z)
+        if bool(bad.any()):
+            rows_bad = bad.nonzero().flatten()[:8].tolist()
+            raise ScaleInitError(f"ssq_scale_init ({method}): {int(bad.sum())} of {rows} rows have "
+                                 f"no quantization scale (NaN / infinite input; rows {rows_bad}...), "
+                                 f"as the reference's init_quantization_scale raises there")
     if channel_wise:
         shape = (-1,) + (1,) * (x.dim() - 1)
         out = d.view(shape), z.view(shape), r.view(shape)
@@ -468,23 +486,30 @@ def _ptrs(ts):
 # gamma^z / phi^z: their module's epilogue).
 GRAD_INTO = {}
 INTO_WRITES = [0]       # gradients written straight into a GRAD_INTO slice (test counter)
+_INTO_SEEN = set()      # the parameters already written into inside the current context
 
 
 class grads_into:
-    """Context: GRAD_INTO = mapping (param.data_ptr() -> destination) inside."""
+    """Context: GRAD_INTO = mapping (param.data_ptr() -> destination) inside.  One context
+    spans one iteration's backward: a second kernel producing the same parameter's gradient
+    inside it would overwrite the first's contribution instead of adding to it, so it
+    raises SSQError instead."""
 
     def __init__(self, mapping):
         self.mapping = mapping or {}
 
     def __enter__(self):
-        self.prev = dict(GRAD_INTO)
+        self.prev = dict(GRAD_INTO), set(_INTO_SEEN)
         GRAD_INTO.clear()
         GRAD_INTO.update(self.mapping)
+        _INTO_SEEN.clear()
         return self
 
     def __exit__(self, *exc):
         GRAD_INTO.clear()
-        GRAD_INTO.update(self.prev)
+        GRAD_INTO.update(self.prev[0])
+        _INTO_SEEN.clear()
+        _INTO_SEEN.update(self.prev[1])
 
 
 def _grad_dest(param, numel, device, need=True):
@@ -496,6 +521,10 @@ def _grad_dest(param, numel, device, need=True):
     if d is not None:
         if d.numel() != numel or not d.is_contiguous():
             raise A.SSQError("grads_into: destination does not match the parameter")
+        if param.data_ptr() in _INTO_SEEN:
+            raise A.SSQError("grads_into: a second kernel produces the gradient of the same "
+                             "parameter in one iteration (it would overwrite, not add)")
+        _INTO_SEEN.add(param.data_ptr())
         INTO_WRITES[0] += 1
         return d.view(-1), True
     return torch.empty(numel, device=device), False
@@ -912,6 +941,26 @@ def gather_rows2(src0, idx, src1=None, out0=None, out1=None):
     else:
         s1, p1, row1, d1 = None, None, 0, None
     call("ssq_gather_rows2", p0, _vp(d0), row0, p1, _vp(d1), row1, _vp(idx), n, stream_of(s0))
+    return d0, d1
+
+
+def gather_rows2_staged(src0, slot, n, stage_dst, src1=None, out0=None, out1=None):
+    """gather_rows2 with the indices slot[:n] of a device ring row, which the same launch
+    also copies whole into stage_dst (ssq_gather_rows2_staged)."""
+    s0, p0 = fptr(src0, "src0")
+    if slot.dtype != torch.int64 or not slot.is_contiguous() or stage_dst.dtype != torch.int64 \
+            or stage_dst.numel() != slot.numel() or slot.device != s0.device:
+        raise A.SSQError("gather_rows2_staged: int64 contiguous slot and stage_dst of one size")
+    row0 = s0[0].numel()
+    d0 = torch.empty((n,) + tuple(s0.shape[1:]), dtype=s0.dtype, device=s0.device) if out0 is None else out0
+    if src1 is not None:
+        s1, p1 = fptr(src1, "src1")
+        row1 = s1[0].numel()
+        d1 = torch.empty((n,) + tuple(s1.shape[1:]), dtype=s1.dtype, device=s1.device) if out1 is None else out1
+    else:
+        s1, p1, row1, d1 = None, None, 0, None
+    call("ssq_gather_rows2_staged", p0, _vp(d0), row0, p1, _vp(d1), row1, _vp(slot), n,
+         _vp(stage_dst), slot.numel(), stream_of(s0))
     return d0, d1
 
 

@@ -34,6 +34,9 @@ class BatchFeeder:
         self.done = [None] * self.RING
         self.k = 0
         self._dev = torch.zeros(self.bs + extra_words, dtype=torch.int64, device=device)
+        self.extra_words = extra_words
+        self.slot = None          # chunk capture: this iteration's row of chunk_dev
+        self.chunk_dev = None
         self.didx = self._dev[:self.bs]
         self.extra = self._dev[self.bs:].view(torch.float32)      # 2*extra_words floats
         self.cur_inp = torch.empty((self.bs,) + tuple(self.inp.shape[1:]), device=device)
@@ -43,6 +46,54 @@ class BatchFeeder:
         """One reference-identical draw: torch.randperm(N)[:batch_size] on the CPU."""
         return torch.randperm(self.N)[:self.bs]
 
+    def _write_slot(self, hn, perm, extra):
+        hn[:self.bs] = perm.numpy()
+        if extra is not None:
+            # float64 -> float32 round to nearest, as torch.as_tensor(extra, dtype=float32)
+            hn[self.bs:].view(np.float32)[:len(extra)] = np.asarray(extra, dtype=np.float64)
+
+    def enable_chunks(self, n):
+        """Several iterations per graph replay (quant/block_recon.py ChunkGraph): a device
+        ring of n iterations' words (indices + the iteration's extra words), filled by one
+        H2D copy per chunk from one of two pinned host buffers."""
+        w = self.bs + self.extra_words
+        pin = torch.cuda.is_available()
+        self.chunk_dev = torch.zeros(n, w, dtype=torch.int64, device=self.device)
+        self.chunk_host = [torch.zeros(n, w, dtype=torch.int64, pin_memory=pin) for _ in range(2)]
+        self.chunk_np = [t.numpy() for t in self.chunk_host]
+        self.chunk_done = [None, None]
+        self.chunk_k = 0
+
+    def stage_chunk(self, perms, extras):
+        """The words of len(perms) consecutive iterations into chunk_dev (one H2D copy)."""
+        j = self.chunk_k % 2
+        if self.chunk_done[j] is not None:
+            self.chunk_done[j].synchronize()
+        hn = self.chunk_np[j]
+        for k, (perm, extra) in enumerate(zip(perms, extras)):
+            self._write_slot(hn[k], perm, extra)
+        n = len(perms)
+        self.chunk_dev[:n].copy_(self.chunk_host[j][:n], non_blocking=True)
+        ev = torch.cuda.Event()
+        ev.record()
+        self.chunk_done[j] = ev
+        self.chunk_k += 1
+
+    def _gather2(self, s0, s1, d0, d1, first):
+        """One ssq_gather_rows2 launch by the static indices; the iteration's first one,
+        inside a chunk capture, reads its slot of chunk_dev and copies the slot into the
+        static words the iteration's later launches read (ssq_gather_rows2_staged)."""
+        if first and self.slot is not None:
+            K.gather_rows2_staged(s0, self.chunk_dev[self.slot], self.bs, self._dev, s1,
+                                  out0=d0, out1=d1)
+        else:
+            K.gather_rows2(s0, self.didx, s1, out0=d0, out1=d1)
+
+    def _stage_only(self):
+        """Chunk capture, an iteration without a gather launch: the slot's words by copy."""
+        if self.slot is not None:
+            self._dev.copy_(self.chunk_dev[self.slot])
+
     def stage(self, perm, extra=None):
         """One host -> device copy of the batch indices (and, optionally, fp32 values into
         self.extra) into the static device buffer."""
@@ -50,10 +101,7 @@ class BatchFeeder:
         if self.done[slot] is not None:
             self.done[slot].synchronize()
         h, hn = self.ring[slot], self.ring_np[slot]
-        hn[:self.bs] = perm.numpy()
-        if extra is not None:
-            # float64 -> float32 round to nearest, as torch.as_tensor(extra, dtype=float32)
-            hn[self.bs:].view(np.float32)[:len(extra)] = np.asarray(extra, dtype=np.float64)
+        self._write_slot(hn, perm, extra)
         self._dev.copy_(h, non_blocking=True)
         ev = torch.cuda.Event()
         ev.record()
@@ -71,7 +119,9 @@ class BatchFeeder:
         the batch input serves it from elsewhere (quant_layer.cached_convs), so only the
         buffer's identity is handed on."""
         if input_needed:
-            K.gather_rows2(self.inp, self.didx, out0=self.cur_inp)
+            self._gather2(self.inp, None, self.cur_inp, None, True)
+        else:
+            self._stage_only()
         return self.cur_inp, K.Rows(self.out, self.didx)
 
     def gather_many(self, pairs, input_needed=True):
@@ -79,9 +129,11 @@ class BatchFeeder:
         precomputed block-input convs, quant_layer.cached_convs(gathered=True)) by the same
         indices: the batch input and those sources two per ssq_gather_rows2 launch."""
         srcs = ([(self.inp, self.cur_inp)] if input_needed else []) + list(pairs)
+        if not srcs:
+            self._stage_only()
         for k in range(0, len(srcs), 2):
             (s0, d0), (s1, d1) = srcs[k], srcs[k + 1] if k + 1 < len(srcs) else (None, None)
-            K.gather_rows2(s0, self.didx, s1, out0=d0, out1=d1)
+            self._gather2(s0, s1, d0, d1, k == 0)
         return self.cur_inp, K.Rows(self.out, self.didx)
 
     def next(self, perm=None):

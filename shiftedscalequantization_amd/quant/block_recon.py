@@ -15,8 +15,9 @@ import torch
 
 from .. import kernels as K
 from ..parallel_dp import GradBucket, world
-from ._engine import (ITER_PROBE, BatchFeeder, IterationGraph, LazyValue, SsqAdam, as_float,
-                      backward_tail, clear_stash, frozen_except, probe, stash_adaround)
+from ._engine import (GRAPH_REPLAYS, ITER_PROBE, BatchFeeder, IterationGraph, LazyValue,
+                      SsqAdam, as_float, backward_tail, clear_stash, frozen_except, probe,
+                      stash_adaround)
 from .adaptive_rounding import AdaRoundQuantizer
 from .data_utils import save_grad_data, save_inp_oup_data
 from .quant_block import BaseQuantBlock
@@ -65,26 +66,42 @@ STASH_ADAROUND = _FAST
 # act phase with CACHE_CONVS: the batch input (when still read) and the cached convs' rows
 # gathered two sources per launch (_engine.BatchFeeder.gather_many)
 GATHER_ONCE = _FAST and os.environ.get("SSQ_BRECQ_GATHER_ONCE", "1") != "0"
+# world 1, after the warm-up: this many iterations per graph replay (ChunkGraph), staged by
+# one H2D copy -- for loops whose iteration is cheaper on the GPU than on the host (the
+# fc's 20000-iteration AdaRound loop); 1 = one iteration per replay
+CHUNK_ITERS = int(os.environ.get("SSQ_BRECQ_CHUNK", "25")) if _FAST else 1
 
 
 def _input_convs(block, qmodules, x):
     """The QuantModules whose conv reads the block input x directly and runs through
-    forward_raw (the fused-epilogue path), found by one probing forward."""
-    hits = []
+    forward_raw (the fused-epilogue path), found by one probing forward, with the number of
+    output elements per sample of each."""
+    hits, per_sample = [], {}
 
     def pre(m, args):
         if args and isinstance(args[0], torch.Tensor) and args[0].data_ptr() == x.data_ptr() \
                 and m.epilogue_fusable(args[0]):
             hits.append(m)
 
+    def post(m, args, out):
+        if m in hits and isinstance(out, torch.Tensor):
+            per_sample[m] = out[0].numel()
+
     hs = [m.register_forward_pre_hook(pre) for m in qmodules]
+    hs += [m.register_forward_hook(post) for m in qmodules]
     try:
         with torch.no_grad():
             block(x)
     finally:
         for h in hs:
             h.remove()
-    return [m for m in qmodules if m in hits]
+    return [(m, per_sample.get(m, 0)) for m in qmodules if m in hits]
+
+
+# cached_convs holds every cached sample's raw output of each input conv (822 MB per
+# ResNet-18 layer1 conv at 1024 samples): only when all of them fit in this fraction of
+# the device's free memory; otherwise the loop runs those convs every iteration as before
+CACHE_CONVS_MEM_FRAC = 0.5
 
 
 def _reconstruct(model, block, qmodules, cali_data, batch_size, iters, weight, opt_mode, asym,
@@ -267,7 +284,10 @@ def _fast_loop(block, qmodules, opt_params, loss_func, feeder, bucket, iters, ac
         if pin:
             stack.enter_context(pinned_weights(qmodules))
             if CACHE_CONVS and feeder.N % feeder.bs == 0:
-                convs = _input_convs(block, qmodules, feeder.cur_inp)
+                found = _input_convs(block, qmodules, feeder.cur_inp)
+                need = sum(n for _, n in found) * feeder.N * 4
+                free = torch.cuda.mem_get_info(feeder.inp.device)[0]
+                convs = [m for m, _ in found] if need <= CACHE_CONVS_MEM_FRAC * free else []
                 if convs:
                     conv_rows[:] = stack.enter_context(cached_convs(
                         convs, feeder.cur_inp, feeder.inp, feeder.didx, gathered=GATHER_ONCE))
@@ -280,13 +300,95 @@ def _fast_loop(block, qmodules, opt_params, loss_func, feeder, bucket, iters, ac
              bucket, body_pre, body_post, last, opt_params, ada, ws_cache)
 
 
+class ChunkGraph:
+    """`n` consecutive iterations of a world-1 loop captured in ONE HIP graph: the host draws
+    the n iterations' batch permutations (the reference's torch.randperm on the CPU
+    generator, in order), schedules and Adam step constants ahead, stages them with one H2D
+    copy (BatchFeeder.stage_chunk) and replays once -- a loop whose iteration is a few
+    microseconds of GPU work per launch (the fc's AdaRound layer loop: 9 small launches)
+    is no longer paced by the host's per-iteration work.  Iteration k of the graph starts
+    with ssq_gather_rows2_staged on slot k; the kernels, their order and their operands are
+    the single-iteration graph's, so the results are the same bits
+    (test_brecq_chunked_loop_bit_identical)."""
+
+    def __init__(self, body, optimizer, feeder, n, ws_cache, last):
+        self.n, self.recs = n, []
+        g = torch.cuda.CUDAGraph()
+        try:
+            with K.A.workspace_scope(ws_cache):
+                with torch.cuda.graph(g):
+                    for k in range(n):
+                        # autograd steals each iteration's gradient into .grad (none is
+                        # accumulated across iterations, as the eager loop's zero_grad)
+                        optimizer.zero_grad(set_to_none=True)
+                        feeder.slot = k
+                        body()
+                        self.recs.append(last['rec'])
+        finally:
+            feeder.slot = None
+        self.graph = g
+        self.grads = [p.grad for p in optimizer.params]
+
+    def replay(self):
+        self.graph.replay()
+        GRAPH_REPLAYS["chunk"] = GRAPH_REPLAYS.get("chunk", 0) + 1
+
+
 def _run(iters, loss_func, feeder, optimizer, scheduler, shadow, use_graph, bucket, body_pre,
          body_post, last, opt_params, ada, ws_cache):
     graph_obj = None
+    chunk_obj = None
+    grads_of = {}        # the .grad tensors of each graph (restored for the one replayed last)
     skip_ok = (SKIP_FROZEN and bucket is None and ITER_HOOK is None and
                ITER_PROBE[0] is None and not loss_func.track_values)
+    chunk_ok = (use_graph and CHUNK_ITERS > 1 and bucket is None and ITER_HOOK is None and
+                ITER_PROBE[0] is None and not loss_func.track_values)
+    last_graph = [None]
+    if chunk_ok:
+        feeder.enable_chunks(CHUNK_ITERS)
+
+    def body():
+        body_pre()
+        body_post()
+
+    def run_chunk(n):
+        """Iterations i .. i + n - 1 from the chunk graph (n == CHUNK_ITERS)."""
+        nonlocal chunk_obj
+        perms, extras, sched = [], [], []
+        rnd = 0.0
+        for k in range(n):
+            b, lam, active = loss_func.schedule()
+            perms.append(feeder.draw())
+            extras.append((lam, float(b)) + optimizer.next_hyper())
+            sched.append((b, loss_func.count))
+            if k == 0 and active and loss_func.wants_value():
+                # the round-loss value from alpha before this step (the chunk's first)
+                rnd = loss_func.round_value(b)
+            if scheduler is not None:
+                shadow.step()
+                scheduler.step()
+                optimizer.param_groups[0]['lr'] = shadow.param_groups[0]['lr']
+        feeder.stage_chunk(perms, extras)
+        if chunk_obj is None:
+            chunk_obj = ChunkGraph(body, optimizer, feeder, n, ws_cache, last)
+            grads_of['chunk'] = chunk_obj.grads
+        chunk_obj.replay()
+        last_graph[0] = 'chunk'
+        for k, (b, count) in enumerate(sched):
+            loss_func.record(chunk_obj.recs[k][0], rnd if k == 0 else 0.0, b, count=count)
+
     try:
-        for i in range(iters):
+        i = 0
+        while i < iters:
+            if chunk_ok and graph_obj is not None and last.get('step'):
+                # the chunk never spans an iteration whose value is reported (count % 500)
+                # except as its first
+                r = (loss_func.count + 1) % 500
+                n = min(CHUNK_ITERS, iters - i, 500 - r if r else 500)
+                if n == CHUNK_ITERS:
+                    run_chunk(n)
+                    i += n
+                    continue
             if ITER_HOOK is not None:
                 ITER_HOOK(i, iters)
             probe(i, opt_params)
@@ -309,8 +411,10 @@ def _run(iters, loss_func, feeder, optimizer, scheduler, shadow, use_graph, buck
                     optimizer.zero_grad(set_to_none=True)
                 # world > 1: two graphs around the eager bucket all-reduce (IterationGraph)
                 graph_obj = IterationGraph(body_pre, body_post, bucket, ws_cache)
+                grads_of['single'] = [p_.grad for p_ in opt_params]
             if graph_obj is not None:
                 graph_obj.replay()
+                last_graph[0] = 'single'
             else:
                 optimizer.zero_grad()
                 if bucket is not None:
@@ -325,6 +429,7 @@ def _run(iters, loss_func, feeder, optimizer, scheduler, shadow, use_graph, buck
                 shadow.step()
                 scheduler.step()
                 optimizer.param_groups[0]['lr'] = shadow.param_groups[0]['lr']
+            i += 1
         if ITER_HOOK is not None:
             ITER_HOOK(iters, iters)
         probe(iters, opt_params)
@@ -333,10 +438,15 @@ def _run(iters, loss_func, feeder, optimizer, scheduler, shadow, use_graph, buck
             q._fused_reg = None
         if graph_obj is not None:
             torch.cuda.current_stream().synchronize()
+            if last_graph[0] in grads_of:
+                # the gradients the last replayed graph wrote
+                for p_, g_ in zip(opt_params, grads_of[last_graph[0]]):
+                    p_.grad = g_
             for p_ in opt_params:       # detach the grads from the graph's private pool
                 p_.grad = None if p_.grad is None else p_.grad.clone()
             graph_obj.release()
             del graph_obj
+            chunk_obj = None
 
 
 class LossFunction:
@@ -384,15 +494,17 @@ class LossFunction:
             total = total + K.round_reg_value(m.weight_quantizer.alpha, self.weight, b)
         return total
 
-    def record(self, rec_loss, round_loss, b):
+    def record(self, rec_loss, round_loss, b, count=None):
+        """count: the iteration's own count when the host scheduled ahead (ChunkGraph)."""
+        count = self.count if count is None else count
         # no tensor op when there is no round term (keeps the device loop launch-free)
         total_loss = rec_loss if isinstance(round_loss, (int, float)) and round_loss == 0 \
             else rec_loss + round_loss
         self.last_total = LazyValue(total_loss.detach() if isinstance(total_loss, torch.Tensor)
                                     else total_loss)
-        if self.count % 500 == 0:
+        if count % 500 == 0:
             print('Total loss:\t{:.3f} (rec:{:.3f}, round:{:.3f})\tb={:.2f}\tcount={}'.format(
-                float(total_loss), float(rec_loss), float(round_loss), b, self.count))
+                float(total_loss), float(rec_loss), float(round_loss), b, count))
         return total_loss
 
     def __call__(self, pred, tgt, grad=None):

@@ -94,10 +94,17 @@ def cached_convs(modules, batch_input, source, idx, gathered=False):
     bs = batch_input.shape[0]
     with torch.no_grad():
         for m in modules:
-            outs = [m.forward_raw(source[i:i + bs])[0] for i in range(0, source.shape[0], bs)]
-            cache[m] = (batch_input.data_ptr(), tuple(batch_input.shape), torch.cat(outs), idx,
-                        torch.empty_like(outs[0]), gathered)
-            del outs
+            # one buffer for every sample's rows, written batch by batch (no list + cat: the
+            # peak stays one copy of the cached outputs)
+            first = m.forward_raw(source[:bs])[0]
+            rows = torch.empty((source.shape[0],) + tuple(first.shape[1:]), dtype=first.dtype,
+                               device=first.device)
+            rows[:bs].copy_(first)
+            for i in range(bs, source.shape[0], bs):
+                rows[i:i + bs].copy_(m.forward_raw(source[i:i + bs])[0])
+            cache[m] = (batch_input.data_ptr(), tuple(batch_input.shape), rows, idx,
+                        torch.empty_like(first), gathered)
+            del first
     _CONV_CACHE = cache
     try:
         yield [(cache[m][2], cache[m][4]) for m in modules]

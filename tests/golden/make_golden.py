@@ -284,6 +284,55 @@ def gen_uaq_specials():
     save("uaq_specials", **out)
 
 
+def gen_init_specials():
+    """init_quantization_scale (quant_layer.py:100-166) on inputs holding SPECIALS BEFORE the
+    init.  Per case: status 0 = the reference returns a usable scale (delta / zp / raw_zp
+    recorded per row), 1 = it raises (its exception's type name recorded: round(nan) is a
+    ValueError at :140; a None delta assigned into a channel's slot a TypeError at :114),
+    2 = it returns delta None (per-tensor 'mse' when no candidate scores below 1e10,
+    :147-162), which the quantizer cannot use."""
+    g = torch.Generator().manual_seed(31337)
+    out, names = {}, []
+    shape = (6, 5, 3, 3)
+    plants = {"nan": float("nan"), "pinf": float("inf"), "ninf": -float("inf"),
+              "big": 3.0e38, "const": None, "zero": None}
+    for method in ("max", "mse"):
+        for cw in (True, False):
+            for sym in (False, True):
+                for pname, val in plants.items():
+                    x = edge_tensor(g, shape, 0.2)
+                    if not cw and not sym:
+                        x = torch.relu(x)
+                    if pname == "const":
+                        x[3] = 0.375
+                    elif pname == "zero":
+                        x[3] = 0.0
+                    else:
+                        x[3, 2, 1, 0] = val
+                    tag = f"{method}_{'cw' if cw else 'pt'}_{'sym' if sym else 'asym'}_{pname}"
+                    q = UniformAffineQuantizer(n_bits=4, symmetric=sym, channel_wise=cw,
+                                               scale_method=method, ch=shape)
+                    out[tag + "_x"] = t2n(x)
+                    try:
+                        d, z, r = q.init_quantization_scale(x.clone(), channel_wise=cw)
+                    except Exception as e:  # the reference's own failure, recorded as data
+                        out[tag + "_status"] = np.array([1], np.int32)
+                        out[tag + "_exc"] = np.array([type(e).__name__])
+                        names.append(tag)
+                        continue
+                    if d is None:
+                        out[tag + "_status"] = np.array([2], np.int32)
+                        names.append(tag)
+                        continue
+                    out[tag + "_status"] = np.array([0], np.int32)
+                    for k, v in (("delta", d), ("zp", z), ("rawzp", r)):
+                        out[tag + "_" + k] = f32(v.detach().reshape(-1).numpy()
+                                                 if torch.is_tensor(v) else [v])
+                    names.append(tag)
+    out["cases"] = np.array(names)
+    save("init_specials", **out)
+
+
 # --------------------------------------------------------------------------- K5-K9 ChannelQuant
 def _mk_uaq(w, bits=2, method="max"):
     q = UniformAffineQuantizer(n_bits=bits, channel_wise=True, scale_method=method, ch=w.shape)
@@ -1558,8 +1607,12 @@ def gen_real_layer_shift(case="r18_layer1_0", iters=20):
     with torch.no_grad():
         out["shift_what_sha"] = np.array([RS.sha(t2n(q(m.weight)))])
     q.hard_targets = False
-    with _Spy(LRS.ScaleLossFunction) as spy:
+    # the AdaRound phase's beta gradients (ScaleLossFunction's lp term + the rounding term,
+    # :297-338,414-486) at the same steps, with their float64 truth
+    with _Spy(LRS.ScaleLossFunction) as spy, \
+            _GradSpy((0, 5, iters - 1), _layer_truth(m, spy, 0.01, iters, True)) as gspy:
         l2 = LRS.layer_recon_shiftedScale(m, iters, 0.01, qnn, None, adaround=True)
+    gspy.dump(out, "ar_")
     out["ar_perms"] = np.stack([p.numpy() for p in spy.perms]).astype(np.int64)
     out["ar_total_loss"] = np.array([r[1] for r in spy.rec], np.float64)
     out["ar_final"] = np.array(l2, np.float64)
@@ -1647,7 +1700,7 @@ if __name__ == "__main__":
     which = sys.argv[1:] or ["uaq", "channelquant", "adaround", "specials", "inpscale", "loss", "recon",
                              "layershift", "brecq", "blocks", "act", "layerfused", "blockshift", "driver",
                              "wmse", "validate", "real", "recon_biascal", "real_biascal", "long",
-                             "layerbrecq", "reallayer", "brecq_long", "brecq_affine"]
+                             "layerbrecq", "reallayer", "brecq_long", "brecq_affine", "init_specials"]
     torch.set_num_threads(4)
     if "uaq" in which:
         gen_uaq()
@@ -1659,6 +1712,8 @@ if __name__ == "__main__":
         gen_uaq_specials()
         gen_channelquant(specials=True)
         gen_adaround(specials=True)
+    if "init_specials" in which:
+        gen_init_specials()
     if "inpscale" in which:
         gen_inpscale()
     if "loss" in which:

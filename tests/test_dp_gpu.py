@@ -140,3 +140,32 @@ def test_validation_world2_whole_set_top1(tmp_path):
     assert int(r0["n_local"][0]) != len(g["labels"])
     assert float(r0["top1"][0]) == float(g["top1"][0])
     assert float(r1["top1"][0]) == float(g["top1"][0])
+
+
+@pytest.mark.timeout(600)
+def test_bench_self_launches_two_ranks():
+    """`python bench.py --gpus 2` with no launcher in the environment starts its own two
+    rank processes (launch.py; the reference's mp.spawn, Brecq/main_imagenet_dist.py:268-271),
+    and rank 0's line reports what the process group saw.  Over gloo here: RCCL needs one
+    GPU per rank and this box has one, so the two ranks share cuda:0."""
+    import json
+    if not torch.cuda.is_available():
+        pytest.skip("no HIP device")
+    env = {k: v for k, v in os.environ.items()
+           if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_ADDR", "MASTER_PORT")}
+    root = os.path.dirname(HERE)
+    r = subprocess.run([sys.executable, os.path.join(root, "bench.py"), "--gpus", "2",
+                        "--dist-backend", "gloo", "--steps", "2", "--warmup", "1",
+                        "--no-cpu-baseline", "--no-validate", "--recon-iters", "8"],
+                       env=env, cwd=root, capture_output=True, text=True, timeout=540)
+    assert r.returncode == 0, (r.stdout[-2000:], r.stderr[-4000:])
+    lines = [json.loads(x) for x in r.stdout.splitlines() if x.startswith("{")]
+    assert len(lines) == 1, r.stdout[-2000:]          # rank 0 only
+    out = lines[0]
+    assert out["n_gpus"] == 2 and out["config"]["parallelism"] == "dp2"
+    assert out["launch"] == {"launcher": "self-spawned", "world_size_backend": 2,
+                             "allreduce_backend": "gloo",
+                             "devices_visible": torch.cuda.device_count()}
+    assert out["recon"]["n_gpus"] == 2 and out["value"] > 0
+    print(json.dumps({"self_launch_world2": {k: out[k] for k in ("value", "ms_per_step")},
+                      "recon_all_blocks_it_s": out["recon"].get("resnet18_all_blocks_iters_per_s")}))

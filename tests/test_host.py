@@ -204,3 +204,88 @@ def test_dwconv_support_query_covers_both_stages():
     assert A.query("ssq_dwconv_supported", 2, 32, 56, 56, 5, 5, 2, 2) == 1
     assert A.query("ssq_dwconv_supported", 2, 32, 178, 178, 3, 3, 1, 1) == 0
     assert A.query("ssq_dwconv_supported", 2, 32, 180, 180, 3, 3, 1, 1) == 0
+
+
+# ---- self-launch (--gpus N without an external launcher; launch.py) --------------------
+
+def _dryrun(script, args):
+    """Run an entry point with --gpus 2 and no launcher in the environment; the ranks stop
+    before importing torch (SSQ_LAUNCH_DRYRUN) and print their rendezvous environment."""
+    import json
+    import subprocess
+    import sys
+    env = {k: v for k, v in os.environ.items()
+           if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_ADDR", "MASTER_PORT")}
+    env["SSQ_LAUNCH_DRYRUN"] = "1"
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    r = subprocess.run([sys.executable, os.path.join(root, script)] + args, env=env,
+                       capture_output=True, text=True, timeout=120, cwd=root)
+    assert r.returncode == 0, r.stderr
+    lines = [json.loads(x) for x in r.stdout.splitlines() if x.startswith("{")]
+    parent = [x["launcher_parent"] for x in lines if "launcher_parent" in x]
+    ranks = sorted((x["rank_env"] for x in lines if "rank_env" in x), key=lambda e: e["RANK"])
+    return parent, ranks
+
+
+@pytest.mark.parametrize("script,args", [
+    ("bench.py", ["--gpus", "2", "--dist-backend", "gloo", "--steps", "2", "--warmup", "1"]),
+    ("main_imagenet.py", ["--gpus", "2", "--dist_backend", "gloo", "--arch", "resnet18"])])
+def test_entry_points_spawn_ranks_before_touching_gpu(script, args):
+    """`--gpus 2` alone starts two rank processes with torch.distributed.run's environment
+    (the reference's mp.spawn, Brecq/main_imagenet_dist.py:268-271), from a parent that has
+    not imported torch nor mapped the HIP runtime."""
+    parent, ranks = _dryrun(script, args)
+    assert parent == [{"torch_imported": False, "cuda_initialized": False,
+                       "hip_runtime_mapped": False, "libssq_loaded": False}]
+    assert [e["RANK"] for e in ranks] == ["0", "1"]
+    assert [e["LOCAL_RANK"] for e in ranks] == ["0", "1"]
+    assert all(e["WORLD_SIZE"] == "2" and e["MASTER_ADDR"] == "127.0.0.1" for e in ranks)
+    assert len({e["MASTER_PORT"] for e in ranks}) == 1
+    assert all(e["SSQ_LAUNCHER"] == "self-spawned" for e in ranks)
+
+
+def test_spawn_ranks_propagates_failure(tmp_path):
+    """A failing rank's exit code is the job's, and the other ranks are stopped."""
+    import time as _time
+    from shiftedscalequantization_amd.launch import spawn_ranks
+    script = tmp_path / "rank.py"
+    script.write_text("import os, sys, time\n"
+                      "if os.environ['RANK'] == '1':\n    sys.exit(3)\n"
+                      "time.sleep(60)\n")
+    t0 = _time.time()
+    assert spawn_ranks(str(script), [], 2, check_parent=False) == 3
+    assert _time.time() - t0 < 30
+    ok = tmp_path / "ok.py"
+    ok.write_text("import os\nassert os.environ['WORLD_SIZE'] == '3'\n")
+    assert spawn_ranks(str(ok), [], 3, check_parent=False) == 0
+
+
+def test_no_spawn_under_external_launcher(monkeypatch):
+    from shiftedscalequantization_amd import launch
+    monkeypatch.setenv("WORLD_SIZE", "4")
+    monkeypatch.delenv("SSQ_LAUNCH_DRYRUN", raising=False)
+    called = []
+    monkeypatch.setattr(launch, "spawn_ranks", lambda *a: called.append(a))
+    launch.maybe_spawn("x.py", ["--gpus", "4"])
+    monkeypatch.delenv("WORLD_SIZE")
+    launch.maybe_spawn("x.py", ["--gpus", "1"])
+    assert called == []
+
+
+def test_grads_into_one_write_per_parameter():
+    """Inside one grads_into context (one iteration's backward) each parameter's gradient
+    slice may be written by one kernel only: a second producer would overwrite the first
+    contribution, so _grad_dest raises; a new context starts afresh."""
+    from shiftedscalequantization_amd import _capi as A
+    from shiftedscalequantization_amd import kernels as K
+    p, q = torch.zeros(6), torch.zeros(4)
+    bucket = torch.zeros(10)
+    into = {p.data_ptr(): bucket[:6], q.data_ptr(): bucket[6:]}
+    for _ in range(2):
+        with K.grads_into(into):
+            d, written = K._grad_dest(p, 6, p.device)
+            assert written and d.data_ptr() == bucket.data_ptr()
+            K._grad_dest(q, 4, q.device)
+            with pytest.raises(A.SSQError):
+                K._grad_dest(p, 6, p.device)
+    assert not K.GRAD_INTO

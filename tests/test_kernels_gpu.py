@@ -158,6 +158,36 @@ def test_scale_init_per_tensor_mse(K):
     assert host(d) == rd and host(z) == rz and host(r) == rr
 
 
+def test_scale_init_specials_golden(K, golden):
+    """NaN / +-inf / 3e38 / constant / zero rows planted BEFORE the init
+    (make_golden.gen_init_specials, the reference's init_quantization_scale,
+    quant_layer.py:100-166).  Where the reference returns a usable scale ssq_scale_init's is
+    bit-identical (delta = inf for a +inf row included); where the reference raises or returns
+    None, K.scale_init raises ScaleInitError -- and with check=False the NaN-marked rows are
+    exactly the planted row (3; per-tensor: the one row)."""
+    d = golden("init_specials")
+    n_raise = 0
+    for tag in d["cases"]:
+        tag = str(tag)
+        method, cw, sym = tag.split("_")[:3]
+        cw, sym = cw == "cw", sym == "sym"
+        x = dev(d[tag + "_x"])
+        status = int(d[tag + "_status"][0])
+        if status != 0:
+            with pytest.raises(K.ScaleInitError):
+                K.scale_init(x, 4, sym, cw, method)
+            dl, zp, _ = K.scale_init(x, 4, sym, cw, method, check=False)
+            bad = (torch.isnan(dl) | torch.isnan(zp)).flatten().nonzero().flatten().tolist()
+            assert bad == ([3] if cw else [0]), (tag, bad)
+            n_raise += 1
+            continue
+        dl, zp, rz = K.scale_init(x, 4, sym, cw, method)
+        np.testing.assert_array_equal(host(dl).ravel(), d[tag + "_delta"], err_msg=tag)
+        np.testing.assert_array_equal(host(zp).ravel(), d[tag + "_zp"], err_msg=tag)
+        np.testing.assert_array_equal(host(rz).ravel(), d[tag + "_rawzp"], err_msg=tag)
+    assert n_raise == sum(int(d[str(t) + "_status"][0]) != 0 for t in d["cases"]) > 10
+
+
 @pytest.mark.parametrize("n", [0, 1, 3, 4, 5, 1023, 4097, 1 << 20])
 def test_fq_ragged_sizes(K, n):
     gen = torch.Generator().manual_seed(n)
@@ -1494,6 +1524,55 @@ def test_epilogue_bwd_delta_split(K, shape):
     unf, _ = run(False, fused=False)
     for x, b in zip(base, unf):      # (x/d)/d vs (x/d)*(1/d): see _compare_fused_unfused
         np.testing.assert_allclose(x, b, rtol=1e-4, atol=1e-3 * max(1.0, float(np.abs(b).max())))
+
+
+@pytest.mark.parametrize("defer", [False, True])
+def test_epilogue_bwd_delta_split_two_streams(K, defer):
+    """The delta reduction's last-arriver counter lives in each call's workspace
+    (fin_tasks.h delta_ticket_offset), so epilogue backwards running at the same time on two
+    streams (20000 rows each: 16 delta workgroups apiece) cannot count each other's
+    workgroups: every gradient equals the one-stream result bit for bit."""
+    from shiftedscalequantization_amd import _capi as A
+    from shiftedscalequantization_amd.quant.quant_layer import UniformAffineQuantizer
+    N, C, hw = 40, 500, 7
+    gen = torch.Generator().manual_seed(4242)
+    ys = [torch.randn(N, C, hw, hw, generator=gen).cuda() for _ in range(2)]
+    gs = [torch.randn(N, C, hw, hw, generator=gen).cuda() for _ in range(2)]
+    bias = (0.1 * torch.randn(C, generator=gen)).cuda()
+    gm0 = (1 + 0.1 * torch.randn(1, C, 1, 1, generator=gen)).cuda()
+    ph0 = (0.1 * torch.randn(1, C, 1, 1, generator=gen)).cuda()
+
+    def launch(i):
+        gamma, phi = gm0.clone().requires_grad_(True), ph0.clone().requires_grad_(True)
+        q = UniformAffineQuantizer(n_bits=4, channel_wise=False, scale_method="max", leaf_param=True).cuda()
+        q.delta = torch.nn.Parameter(torch.tensor(0.23).cuda())
+        q.zero_point = torch.nn.Parameter(torch.tensor(3.0).cuda())
+        q.inited = True
+        with A.workspace_scope({}), K.deferred_finalize(defer):
+            out = K.epilogue(ys[i], bias, gamma, phi, None, 1, q)
+            out.backward(gs[i])
+        return q, gamma, phi
+
+    def grads(r):
+        q, gamma, phi = r
+        return [host(t).reshape(-1).view(np.int32).copy()
+                for t in (q.delta.grad, q.zero_point.grad, gamma.grad, phi.grad)]
+
+    base = []
+    for i in range(2):
+        r = launch(i)
+        torch.cuda.synchronize()
+        base.append(grads(r))
+    streams = [torch.cuda.Stream(), torch.cuda.Stream()]
+    for _ in range(8):
+        res = []
+        for i in range(2):
+            with torch.cuda.stream(streams[i]):
+                res.append(launch(i))
+        torch.cuda.synchronize()
+        for i in range(2):
+            for x, b in zip(grads(res[i]), base[i]):
+                np.testing.assert_array_equal(x, b)
 
 
 def test_armed_adam_falls_back_when_not_covered(K):

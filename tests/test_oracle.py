@@ -50,6 +50,33 @@ def test_uaq_zero_range_channel(golden):
     np.testing.assert_array_equal(y, g["zero_y"])
 
 
+def _init_case(d, tag):
+    method, cw, sym = tag.split("_")[:3]
+    return d[tag + "_x"], method, cw == "cw", sym == "sym", int(d[tag + "_status"][0])
+
+
+def test_init_specials(golden):
+    """init_quantization_scale with NaN / +-inf / 3e38 / constant / zero rows planted BEFORE
+    the init (quant_layer.py:100-166): where the reference returns a scale the oracle's is
+    bit-identical; where it raises, the oracle raises the same exception type; where it
+    returns None (per-tensor 'mse'), so does the oracle."""
+    d = golden("init_specials")
+    for tag in d["cases"]:
+        x, method, cw, sym, status = _init_case(d, tag)
+        if status == 1:
+            exc = {"ValueError": ValueError, "TypeError": TypeError}[str(d[tag + "_exc"][0])]
+            with pytest.raises(exc):
+                R.init_scale(x, 4, sym, cw, method)
+            continue
+        dl, zp, rz = R.init_scale(x, 4, sym, cw, method)
+        if status == 2:
+            assert dl is None, tag
+            continue
+        np.testing.assert_array_equal(np.ravel(dl), d[tag + "_delta"], err_msg=tag)
+        np.testing.assert_array_equal(np.ravel(zp), d[tag + "_zp"], err_msg=tag)
+        np.testing.assert_array_equal(np.ravel(rz), d[tag + "_rawzp"], err_msg=tag)
+
+
 def test_uaq_backward(golden):
     g = golden("uaq")
     for t in tags(g, "_gdelta"):

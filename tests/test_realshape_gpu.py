@@ -505,7 +505,24 @@ def test_real_layer_shift_w4a8_matches_reference(Q, golden):
         wh = RS.sha(host(q(m.weight)))
     stats["shift_hard_identical"] = float(wh == str(g["shift_what_sha"][0]))
     q.hard_targets = False
-    l2 = Q.layer_recon_shiftedScale(m, iters, 0.01, qnn, None, adaround=True, verbose=False)
+    # the AdaRound phase, teacher-forced the same way: beta set to the reference's value at
+    # the recorded steps, the gradient (ScaleLossFunction's lp term + the rounding term,
+    # layer_recon_shiftedScale.py:297-338,414-486) held to its float64 truth
+    ar_steps = [int(s_) for s_ in g["ar_grad_steps"]]
+    probe, ar_got, ar_before = grad_recorder(ar_steps, {s_: [g[f"ar_gs{s_}_p0"]] for s_ in ar_steps})
+    E.ITER_PROBE[0] = probe
+    try:
+        l2 = Q.layer_recon_shiftedScale(m, iters, 0.01, qnn, None, adaround=True, verbose=False)
+    finally:
+        E.ITER_PROBE[0] = None
+    ar_worst = 0.0
+    for s_ in ar_steps:
+        ar_worst = max(ar_worst, grad_stats(stats, f"ar_g{s_}", ar_got[s_], [g[f"ar_gs{s_}_g0"]],
+                                            truths(g, "ar_", s_, 1)))
+    stats["ar_grad_worst_over_bound"] = ar_worst
+    # beta at step 0 is init_beta of the selected deltas: forced to the reference's, so the
+    # overwrite must have been (almost) a no-op
+    stats["ar_init_dev"] = np.abs(ar_before[0][0].reshape(-1) - g["ar_gs0_p0"].reshape(-1)).max()
     stats["ar_final_rel_err"] = np.max(np.abs(np.array(l2) - g["ar_final"]) / np.abs(g["ar_final"]))
     d = host(q.delta)
     stats["ar_delta_flips"] = int(np.sum(d != g["ar_delta"]))
@@ -516,19 +533,32 @@ def test_real_layer_shift_w4a8_matches_reference(Q, golden):
     stats["ar_beta_walk_frac"] = float(np.mean(db > 2e-4))
     decided = np.abs(g["ar_beta"]) > budget
     stats["ar_undecided_frac"] = float(np.mean(~decided))
+    flip = (bq >= 0) != (g["ar_beta"] >= 0)
+    stats["ar_round_flips"] = int(flip.sum())
+    stats["ar_flips_max_abs_ref_beta"] = float(np.abs(g["ar_beta"][flip]).max(initial=0.0))
     with torch.no_grad():
         wh2 = RS.sha(host(q(m.weight)))
     stats["ar_hard_identical"] = float(wh2 == str(g["ar_what_sha"][0]))
+    # the final losses: rtol 1e-5 (north_star) when no beta walked; a walked beta moves the
+    # soft-rounded output, and with it the loss, by the walk's own size (observed r4: 1.5 %
+    # of the entries by <= 1.1e-3 -> 2e-5 relative), which is the bound then
+    rtol = 1e-5 if stats["ar_beta_walk_frac"] == 0.0 else 1e-4
+    stats["ar_final_rtol_applied"] = rtol
     parity_report("real_layer_shift_w4a8[r18_layer1_0]", **stats)
-    # the AdaRound phase's beta: entries whose rounding-loss gradient nearly cancels are
-    # walked by Adam in +-lr steps (observed r4: 1.5 % of them, by <= 1.1e-3, inside the
-    # budget), which moves the final loss by ~2e-5 relative
-    np.testing.assert_allclose(l2, g["ar_final"], rtol=1e-4)
-    assert worst <= 1.0, stats
-    assert stats["shift_init_dev"] <= 5e-7
-    assert np.mean(d != g["ar_delta"]) <= 0.005
-    assert db.max() <= budget and np.mean(db > 2e-4) <= 0.05
-    assert np.all((bq >= 0)[decided] == (g["ar_beta"] >= 0)[decided])
+    assert worst <= 1.0 and ar_worst <= 1.0, stats
+    assert stats["shift_init_dev"] <= 5e-7 and stats["ar_init_dev"] <= 5e-7, stats
+    assert stats["ar_delta_flips"] == 0, stats
+    # beta: teacher-forced gradients at the exact-gradient bound (above); between the forced
+    # steps Adam's first moves are +-lr whatever the gradient's size, so an entry whose
+    # gradient is at the fp32 noise floor of the dL/dW sum takes the sign that summation
+    # order gives it -- in the reference as here.  Those walk by <= 2 lr per step; the
+    # rounding decision may flip only inside that budget, and with no flip the hard weights
+    # are the reference's bit for bit.
+    assert db.max() <= budget and np.mean(db > 2e-4) <= 0.05, stats
+    assert np.all(np.abs(g["ar_beta"][flip]) <= budget), stats
+    if not flip.any():
+        assert stats["ar_hard_identical"] == 1.0, stats
+    np.testing.assert_allclose(l2, g["ar_final"], rtol=rtol)
     if stats["shift_alpha_walkers"] == 0:
         assert stats["shift_hard_identical"] == 1.0
 
