@@ -333,6 +333,25 @@ int ssq_gather_rows2_staged(const float* src0, float* dst0, int64_t row0, const 
                             float* dst1, int64_t row1, const int64_t* slot, int64_t nidx,
                             int64_t* stage_dst, int64_t stage_words, ssq_stream_t stream);
 
+/* ---------------------------------------------------------------- K19 fused fc iteration
+ * One BRECQ AdaRound iteration of a Linear layer (the network's last layer: layer_recon.py
+ * :10-104 with its LossFunction :107-170, adaptive_rounding.py:38-67, lp_loss p = 2,
+ * quant_layer.py:25-32) in two launches: y = x[idx] W^T + bias with W^ = AdaRound(W, V)
+ * (per-row delta / zp, soft rounding, clamp to [qmin, qmax]) computed on the fly, the loss
+ * gradient g = dL/dy; then dW = g^T x[idx], V's gradient (AdaRound backward + the rounding
+ * regulariser) and V's Adam step (exp_avg / exp_avg_sq; ssq_adam's ops), and the loss
+ * value into loss_out.  `slot` (device) holds the bs batch indices (rows of x_cache
+ * [N, Ci] and tgt_cache [N, Co]) followed by the iteration's words as fp32 pairs: (lambda,
+ * b) of the regulariser, then Adam's (-lr/bc1, sqrt(bc2)).  g ([bs, Co]) is scratch (and
+ * readable); gv_out may receive V's gradient.  1 <= bs <= 64, Ci <= 4096.             */
+size_t ssq_fc_recon_workspace_size(int64_t Co, int64_t Ci, int64_t bs);
+int ssq_fc_recon_iter(const float* x_cache, const float* tgt_cache, const int64_t* slot,
+                      int64_t bs, const float* W, float* V, const float* delta, const float* zp,
+                      int qmin, int qmax, const float* bias, int64_t Co, int64_t Ci,
+                      float one_minus_beta1, float beta2, float one_minus_beta2, float eps,
+                      float* exp_avg, float* exp_avg_sq, float* g, float* gv_out, float* loss_out,
+                      void* ws, size_t ws_bytes, ssq_stream_t stream);
+
 /* ---------------------------------------------------------------- K13 fused epilogue
  * QuantModule conv bias add (quant_layer.py:250), the block's residual add and ReLU
  * (quant_block.py:99-117) in one pass, in the reference's op order:
@@ -490,6 +509,17 @@ int ssq_conv_wgrad(const float* x, const float* dy, int64_t Nb, int64_t C, int64
 int ssq_wgrad_gemm_operands(const float* x, const float* dy, int64_t Nb, int64_t C, int64_t H,
                             int64_t W, int64_t Co, int64_t R, int64_t S, int64_t stride,
                             int64_t pad, float* col, float* dy2, ssq_stream_t stream);
+/* The im2col matrix col (N*OH*OW x C*R*S) of epilogue(y): y is the previous conv's raw
+ * output and the epilogue the K13 one (ssq_epilogue_fwd's bias, gamma^z / phi^z, activation
+ * and per-tensor act fake-quant, each optional: bias / gamma+phi / delta+zp may be NULL),
+ * applied on the fly with the same fp32 ops -- col is bit for bit the im2col of the
+ * materialised epilogue output, which is never written (ResNet BasicBlock conv1 -> conv2 on
+ * the small planes: quant_layer.py:250-272 then conv2's F.conv2d, quant_block.py:99-117). */
+int ssq_gemm_col_epilogue(const float* y, const float* bias, const float* gamma,
+                          const float* phi, int relu, const float* delta, const float* zp,
+                          int qmin, int qmax, int64_t Nb, int64_t C, int64_t H, int64_t W,
+                          int64_t R, int64_t S, int64_t stride, int64_t pad, float* col,
+                          ssq_stream_t stream);
 
 /* ---------------------------------------------------------------- K18 depthwise conv
  * Depthwise (groups == C == Co) fp32 NCHW conv, dilation 1, R*S <= 25, zero padding:

@@ -19,7 +19,7 @@ LIB = os.path.join(HERE, "libssq.so")
 ARCH = os.environ.get("SSQ_OFFLOAD_ARCH", "gfx950")
 
 SOURCES = ["fq.hip", "adashift.hip", "adashift_prep.hip", "scale_init.hip", "recon.hip", "pack.hip", "conv_wgrad.hip",
-           "dwconv.hip"]
+           "dwconv.hip", "fc_recon.hip"]
 HEADERS = ["ssq_common.h", "adashift_common.h", "fin_tasks.h", "prep_ride.h", os.path.join("..", "..", "include", "ssq.h")]
 CFLAGS = ["-O3", f"--offload-arch={ARCH}", "-fPIC", "-std=c++17", "-ffp-contract=off",
           "-fhip-fp32-correctly-rounded-divide-sqrt", "-Wall", "-Wno-unused-function"]

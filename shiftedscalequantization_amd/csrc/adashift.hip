@@ -157,16 +157,6 @@ __global__ __launch_bounds__(kBlock) void adaround_fwd_kernel(
   }
 }
 
-// d/dv of the rounding regulariser lambda*(1-|2h(v)-1|^b) (round_reg_kernel's gradient)
-__device__ __forceinline__ float round_reg_grad(float v, float lambda, float b) {
-  if (lambda == 0.0f || b == 0.0f) return 0.0f;
-  const float h = rect_sigmoid(v);
-  const float r = __fmul_rn(fabsf(__fsub_rn(h, 0.5f)), 2.0f);
-  const float sg = h > 0.5f ? 1.0f : (h < 0.5f ? -1.0f : 0.0f);
-  const float gh = -lambda * b * powf(r, b - 1.0f) * 2.0f * sg;
-  return rect_sigmoid_grad(v, gh);
-}
-
 // reg_dev != null: the rounding regulariser's gradient (lambda, b = reg_dev[0..1]) is added
 // (BRECQ's round loss, block_recon.py:171-174, folded into this backward).
 __global__ __launch_bounds__(kBlock) void adaround_bwd_kernel(

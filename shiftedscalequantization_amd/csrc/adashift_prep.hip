@@ -106,8 +106,9 @@ static ColTiling col_tiling_prep(const Geo& g) {
 // 6-13 us slower than the stage-2 launch they save; and this form with 9 elements per thread
 // (up to Co*K = 2304, layer3 3x3) -- equal on layer3 (16.0 vs 15.8 us) but its registers
 // (97 VGPRs) cost the other forms' occupancy.
-constexpr uint32_t kChanPer = 5;                      // elements per thread
-constexpr uint32_t kChanElems = kChanPer * kBlock;    // 1280
+constexpr uint32_t kChanPer = 5;                      // elements per thread per batch
+constexpr uint32_t kChanElems = kChanPer * kBlock;    // 1280: one batch
+constexpr uint32_t kChanBatches = 4;                  // batches in the per-channel form
 
 static ColTiling bwd_tiling_prep(const Geo& g) {
   // SSQ_K6P_FORM (A/B): 3 = the per-channel form where it fits, else thread-column (default);
@@ -119,7 +120,13 @@ static ColTiling bwd_tiling_prep(const Geo& g) {
   // 9.2 -> 11.8 us; layer2.0's 128-row one in a single launch 13.0 -> 9.8 us, stage 2
   // included); SSQ_K6P_CHAN_CO for A/B
   static const uint32_t kMaxCo = prep_env("SSQ_K6P_CHAN_CO", 128);
-  if (kForm != 3 || g.Co * g.K > kChanElems || g.Co > kMaxCo) return col_tiling_prep(g);
+  // elements per input channel the per-channel form takes: up to kChanBatches batches of
+  // kChanPer per thread, each batch's loads issued while the previous one is summed
+  // (SSQ_K6P_CHAN_ELEMS, A/B; r4: one batch, 1280)
+  static const uint32_t kMaxElems = prep_env("SSQ_K6P_CHAN_ELEMS", kChanElems);
+  if (kForm != 3 || g.Co * g.K > kMaxElems || g.Co * g.K > kChanBatches * kChanElems ||
+      (g.Co > kMaxCo && g.K == 1))
+    return col_tiling_prep(g);
   ColTiling t;
   t.form = 3;
   t.threads = kBlock;
@@ -302,29 +309,48 @@ __device__ __forceinline__ void alpha_bwd_channel(const PrepSeg& sg, const AdamC
   }
   uint32_t fw[kChanPer];
   float h[kChanPer], gy[kChanPer], d[kChanPer], z[kChanPer];
+  // batch b: elements t + (b * kChanPer + e) * kBlock
+  auto fetch = [&](uint32_t b) {
 #pragma unroll
-  for (uint32_t e = 0; e < kChanPer; ++e) {
-    const uint32_t f = t + e * kBlock;
-    fw[e] = 0u;
-    h[e] = gy[e] = d[e] = z[e] = 0.0f;
-    if (f < n) {
-      const uint32_t co = fdiv(f, sg.divK);
-      const uint32_t idx = co * g.CiK + ci * g.K + (f - co * g.K);
-      fw[e] = sg.fpack[idx];
-      h[e] = sg.hterm[idx];
-      gy[e] = sg.gWhat[idx];
-      d[e] = sg.delta[co];
-      z[e] = sg.zp[co];
+    for (uint32_t e = 0; e < kChanPer; ++e) {
+      const uint32_t f = t + (b * kChanPer + e) * kBlock;
+      fw[e] = 0u;
+      h[e] = gy[e] = d[e] = z[e] = 0.0f;
+      if (f < n) {
+        const uint32_t co = fdiv(f, sg.divK);
+        const uint32_t idx = co * g.CiK + ci * g.K + (f - co * g.K);
+        fw[e] = sg.fpack[idx];
+        h[e] = sg.hterm[idx];
+        gy[e] = sg.gWhat[idx];
+        d[e] = sg.delta[co];
+        z[e] = sg.zp[co];
+      }
     }
-  }
+  };
+  fetch(0);
   float p[kMaxS];
   soft_targets<kMaxS>(a, NS, nullptr, p);
   double acc[NS];
 #pragma unroll
   for (int i = 0; i < NS; ++i) acc[i] = 0.0;
+  const uint32_t nb = (n + kChanElems - 1) / kChanElems;   // uniform per workgroup
+  for (uint32_t b = 0; b < nb; ++b) {
+    uint32_t fw1[kChanPer];
+    float h1[kChanPer], gy1[kChanPer], d1[kChanPer], z1[kChanPer];
 #pragma unroll
-  for (uint32_t e = 0; e < kChanPer; ++e)
-    if (t + e * kBlock < n) alpha_accumulate<NS>(fw[e], h[e], d[e], z[e], gy[e], p, sg.lo, sg.hi, acc);
+    for (uint32_t e = 0; e < kChanPer; ++e) {
+      fw1[e] = fw[e];
+      h1[e] = h[e];
+      gy1[e] = gy[e];
+      d1[e] = d[e];
+      z1[e] = z[e];
+    }
+    if (b + 1 < nb) fetch(b + 1);
+#pragma unroll
+    for (uint32_t e = 0; e < kChanPer; ++e)
+      if (t + (b * kChanPer + e) * kBlock < n)
+        alpha_accumulate<NS>(fw1[e], h1[e], d1[e], z1[e], gy1[e], p, sg.lo, sg.hi, acc);
+  }
 #pragma unroll
   for (int i = 0; i < NS; ++i) acc[i] = wave_sum(acc[i]);
   if (lane == 0) {

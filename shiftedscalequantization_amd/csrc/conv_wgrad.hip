@@ -1361,6 +1361,88 @@ __global__ __launch_bounds__(kBlock) void wgrad_gemm_operands(
   }
 }
 
+// The im2col matrix of a conv whose input is the previous conv's K13 epilogue output, the
+// epilogue applied on the fly (ResNet BasicBlock conv1 -> conv2 on the small planes, where
+// conv2's forward and weight gradient are GEMMs over this matrix): x = epilogue(y),
+//   t = y + bias[c]; t = t * gamma[c] + phi[c]; t = act(t); t = fq(t)   (each step optional)
+// -- the very fp32 ops of bias_act_kernel (recon.hip), so col is bit for bit the im2col of
+// the materialised epilogue output, which is never written.  Padding stays 0 (the conv pads
+// the epilogue's output).
+template <int ACT>
+__device__ __forceinline__ float epi_in(float v, uint32_t c, const float* __restrict__ bias,
+                                        const float* __restrict__ gamma,
+                                        const float* __restrict__ phi, bool quant,
+                                        const QParams& qp) {
+  float t = bias ? __fadd_rn(v, bias[c]) : v;
+  if (gamma) t = __fadd_rn(__fmul_rn(t, gamma[c]), phi[c]);
+  t = act_fwd<ACT>(t);
+  if (quant) {
+    float q;
+    t = fq1(t, qp, &q);
+  }
+  return t;
+}
+
+template <int ACT>
+__global__ __launch_bounds__(kBlock) void gemm_col_epi(
+    const float* __restrict__ y, const float* __restrict__ bias, const float* __restrict__ gamma,
+    const float* __restrict__ phi, const float* __restrict__ qdelta,
+    const float* __restrict__ qzp, float qlo, float qhi, uint32_t C, uint32_t H, uint32_t W,
+    uint32_t R, uint32_t S, uint32_t st, int pad, uint32_t OW, uint32_t NP, FastDiv dCRS,
+    FastDiv dRS, FastDiv dS, FastDiv dP, FastDiv dOW, uint32_t CRS, uint32_t P,
+    float* __restrict__ col) {
+  const bool quant = qdelta != nullptr;
+  QParams qp{1.0f, 0.0f, qlo, qhi};
+  if (quant) {
+    qp.d = qdelta[0];
+    qp.z = qzp[0];
+  }
+  const uint32_t n1 = NP * CRS;
+  for (uint32_t e = blockIdx.x * kBlock + threadIdx.x; e < n1; e += gridDim.x * kBlock) {
+    const uint32_t row = fdiv(e, dCRS), k = e - row * CRS;
+    const uint32_t n = fdiv(row, dP), p = row - n * P;
+    const uint32_t oh = fdiv(p, dOW), ow = p - oh * OW;
+    const uint32_t ci = fdiv(k, dRS), rs = k - ci * R * S;
+    const uint32_t r = fdiv(rs, dS), s = rs - r * S;
+    const int ih = (int)(oh * st + r) - pad, iw = (int)(ow * st + s) - pad;
+    float v = 0.0f;
+    if (ih >= 0 && ih < (int)H && iw >= 0 && iw < (int)W)
+      v = epi_in<ACT>(y[(((size_t)n * C + ci) * H + ih) * W + iw], ci, bias, gamma, phi, quant,
+                      qp);
+    col[e] = v;
+  }
+}
+
+extern "C" int ssq_gemm_col_epilogue(const float* y, const float* bias, const float* gamma,
+                                     const float* phi, int relu, const float* delta,
+                                     const float* zp, int qmin, int qmax, int64_t Nb, int64_t C,
+                                     int64_t H, int64_t W, int64_t R, int64_t S, int64_t stride,
+                                     int64_t pad, float* col, ssq_stream_t stream) {
+  SSQ_REQUIRE(y && col, SSQ_E_ARG, "ssq_gemm_col_epilogue: null pointer");
+  SSQ_REQUIRE(!gamma == !phi, SSQ_E_ARG, "ssq_gemm_col_epilogue: gamma and phi go together");
+  SSQ_REQUIRE(!delta || (zp && qmin < qmax), SSQ_E_ARG, "ssq_gemm_col_epilogue: act quantizer");
+  SSQ_REQUIRE(relu >= 0 && relu <= 2, SSQ_E_ARG, "ssq_gemm_col_epilogue: activation code %d", relu);
+  SSQ_REQUIRE(Nb >= 1 && C >= 1 && H >= 1 && W >= 1 && R >= 1 && S >= 1 && stride >= 1 &&
+                  pad >= 0, SSQ_E_ARG, "ssq_gemm_col_epilogue: bad geometry");
+  const int64_t OH = (H + 2 * pad - R) / stride + 1, OW = (W + 2 * pad - S) / stride + 1;
+  SSQ_REQUIRE(OH >= 1 && OW >= 1, SSQ_E_ARG, "ssq_gemm_col_epilogue: empty output plane");
+  const int64_t P = OH * OW, NP = Nb * P, CRS = C * R * S;
+  SSQ_REQUIRE(NP * CRS < (1ll << 31) && Nb * C * H * W < (1ll << 31), SSQ_E_ARG,
+              "ssq_gemm_col_epilogue: operands exceed 2^31 elements");
+  const uint32_t nb = (uint32_t)std::min<int64_t>((NP * CRS + kBlock - 1) / kBlock, 8192);
+#define SSQ_GCE(A)                                                                          \
+  hipLaunchKernelGGL(gemm_col_epi<A>, dim3(nb), dim3(kBlock), 0, (hipStream_t)stream, y, bias, \
+                     gamma, phi, delta, zp, (float)qmin, (float)qmax, (uint32_t)C, (uint32_t)H, \
+                     (uint32_t)W, (uint32_t)R, (uint32_t)S, (uint32_t)stride, (int)pad,         \
+                     (uint32_t)OW, (uint32_t)NP, make_fastdiv((uint32_t)CRS),                   \
+                     make_fastdiv((uint32_t)(R * S)), make_fastdiv((uint32_t)S),                \
+                     make_fastdiv((uint32_t)P), make_fastdiv((uint32_t)OW), (uint32_t)CRS,      \
+                     (uint32_t)P, col)
+  if (relu == 2) SSQ_GCE(2); else if (relu == 1) SSQ_GCE(1); else SSQ_GCE(0);
+#undef SSQ_GCE
+  return check_launch("ssq_gemm_col_epilogue");
+}
+
 extern "C" int ssq_wgrad_gemm_operands(const float* x, const float* dy, int64_t Nb, int64_t C,
                                        int64_t H, int64_t W, int64_t Co, int64_t R, int64_t S,
                                        int64_t stride, int64_t pad, float* col, float* dy2,

@@ -274,4 +274,50 @@ __device__ __forceinline__ float fq1(float x, const QParams& p, float* qout, flo
   return __fmul_rn(__fsub_rn(q, p.z), p.d);  // (x_quant - zp) * delta
 }
 
+// ---------------------------------------------------------------- loss / regulariser terms
+// (lp_loss_kernel and the fused tail in recon.hip, the fused fc iteration in fc_recon.hip)
+// |d|^p and its derivative p*|d|^(p-1) for one element.
+template <int PMODE>  // 0: p == 2, 1: p == 1, 2: general p
+__device__ __forceinline__ void lp_term(float a, float p, float& pw, float& dp) {
+  if (PMODE == 0) {
+    pw = __fmul_rn(a, a);
+    dp = __fmul_rn(2.0f, a);
+  } else if (PMODE == 1) {
+    pw = a;
+    dp = 1.0f;
+  } else {
+    // both powers from one hardware log2 and two hardware exp2 (about 1e-6 relative; the
+    // loss and gradient tolerance is 1e-5).  No divide and no ocml powf: those made this
+    // pass VALU-bound.  a == 0: log2 = -inf gives pow's own values (0 for p > 1; inf for
+    // p - 1 < 0, so the gradient is inf * sgn(0) = NaN, as torch's)
+    const float l = __builtin_amdgcn_logf(a);
+    pw = __builtin_amdgcn_exp2f(__fmul_rn(p, l));
+    dp = __fmul_rn(p, __builtin_amdgcn_exp2f(__fmul_rn(__fsub_rn(p, 1.0f), l)));
+  }
+}
+
+template <int PMODE>
+__device__ __forceinline__ float lp_elem(float x, float t, float p, float inv_m, float gs,
+                                         int relu_mask, double& acc) {
+  const float d = __fsub_rn(x, t);
+  float pw, dp;
+  lp_term<PMODE>(fabsf(d), p, pw, dp);
+  acc += (double)pw;
+  const float sg = d > 0.0f ? 1.0f : (d < 0.0f ? -1.0f : 0.0f);
+  const float gv = __fmul_rn(__fmul_rn(__fmul_rn(inv_m, dp), sg), gs);
+  // relu_mask: pred is a ReLU output; the gradient is written at the ReLU's input
+  // (torch threshold_backward: out <= 0 -> 0)
+  return (relu_mask && x <= 0.0f) ? 0.0f : gv;
+}
+
+// d/dv of the rounding regulariser lambda*(1-|2h(v)-1|^b) (round_reg_kernel's gradient)
+__device__ __forceinline__ float round_reg_grad(float v, float lambda, float b) {
+  if (lambda == 0.0f || b == 0.0f) return 0.0f;
+  const float h = rect_sigmoid(v);
+  const float r = __fmul_rn(fabsf(__fsub_rn(h, 0.5f)), 2.0f);
+  const float sg = h > 0.5f ? 1.0f : (h < 0.5f ? -1.0f : 0.0f);
+  const float gh = -lambda * b * powf(r, b - 1.0f) * 2.0f * sg;
+  return rect_sigmoid_grad(v, gh);
+}
+
 }  // namespace ssq

@@ -1177,31 +1177,37 @@ class EpilogueFn(torch.autograd.Function):
     def backward(ctx, g):
         y, bias, gamma, phi, res, delta, zp = ctx.saved_tensors
         relu, lo, hi, quant, C_, hw = ctx.cfg
-        g, gp = fptr(g.contiguous(), "grad")
-        need = ctx.needs_input_grad
-        dev_ = g.device
+        return _epilogue_backward(g, y, bias, gamma, phi, res, delta, zp, relu, lo, hi, quant,
+                                  C_, hw, ctx.needs_input_grad)
 
-        def flat(t):
-            return None if t is None else t.detach().reshape(-1).contiguous()
-        b, gm, ph, r = flat(bias), flat(gamma), flat(phi), res
-        d, z = flat(delta), flat(zp)
-        gy = torch.empty_like(g) if need[0] else None
-        gres = torch.empty_like(g) if (res is not None and need[4]) else None
-        ggm, gm_into = _grad_dest(gamma, C_, dev_, need[2])
-        gph, ph_into = _grad_dest(phi, C_, dev_, need[3])
-        gd = torch.empty(1, device=dev_) if (quant and need[5]) else None
-        gz = torch.empty(1, device=dev_) if (quant and need[6]) else None
-        N = g.numel() // (C_ * hw)
-        # two alternating slots: a queued finalize of the previous call still reads its own
-        ws, wsn = workspace(query("ssq_epilogue_bwd_workspace_size", N * C_), dev_, _epi_slot())
-        call("ssq_epilogue_bwd", gp, _vp(y), _vp(b), _vp(gm), _vp(ph),
-             _vp(r.contiguous() if r is not None else None), N, C_, hw, int(relu), _vp(d), _vp(z),
-             lo, hi, _vp(gy), _vp(gres), _vp(ggm), _vp(gph), _vp(gd), _vp(gz), ws, wsn,
-             stream_of(g))
-        shape = (lambda t, o: None if o is None else o.view(t.shape))
-        return (gy if need[0] else None, None, None if gm_into else shape(gamma, ggm),
-                None if ph_into else shape(phi, gph), gres, shape(delta, gd), shape(zp, gz), None,
-                None, None)
+
+def _epilogue_backward(g, y, bias, gamma, phi, res, delta, zp, relu, lo, hi, quant, C_, hw, need):
+    """ssq_epilogue_bwd for EpilogueFn (need = its needs_input_grad) and EpiConvGemmFn:
+    EpilogueFn.backward's return tuple."""
+    g, gp = fptr(g.contiguous(), "grad")
+    dev_ = g.device
+
+    def flat(t):
+        return None if t is None else t.detach().reshape(-1).contiguous()
+    b, gm, ph, r = flat(bias), flat(gamma), flat(phi), res
+    d, z = flat(delta), flat(zp)
+    gy = torch.empty_like(g) if need[0] else None
+    gres = torch.empty_like(g) if (res is not None and need[4]) else None
+    ggm, gm_into = _grad_dest(gamma, C_, dev_, need[2])
+    gph, ph_into = _grad_dest(phi, C_, dev_, need[3])
+    gd = torch.empty(1, device=dev_) if (quant and need[5]) else None
+    gz = torch.empty(1, device=dev_) if (quant and need[6]) else None
+    N = g.numel() // (C_ * hw)
+    # two alternating slots: a queued finalize of the previous call still reads its own
+    ws, wsn = workspace(query("ssq_epilogue_bwd_workspace_size", N * C_), dev_, _epi_slot())
+    call("ssq_epilogue_bwd", gp, _vp(y), _vp(b), _vp(gm), _vp(ph),
+         _vp(r.contiguous() if r is not None else None), N, C_, hw, int(relu), _vp(d), _vp(z),
+         lo, hi, _vp(gy), _vp(gres), _vp(ggm), _vp(gph), _vp(gd), _vp(gz), ws, wsn,
+         stream_of(g))
+    shape = (lambda t, o: None if o is None else o.view(t.shape))
+    return (gy if need[0] else None, None, None if gm_into else shape(gamma, ggm),
+            None if ph_into else shape(phi, gph), gres, shape(delta, gd), shape(zp, gz), None,
+            None, None)
 
 
 _EPI_SLOT = [0]
@@ -1275,6 +1281,115 @@ class deferred_prep_fwd:
 # epilogue in one pass (epilogue_loss_bwd).  Only consumed by BaseQuantBlock._tail, and
 # only by the block identical to TAIL_LAZY[0] (nested blocks and hooked blocks run eagerly).
 TAIL_LAZY = [None]
+
+
+# ------------------------------------------------------------------ K13 epilogue into an im2col GEMM
+# A ResNet BasicBlock's conv1 epilogue feeds only conv2.  Where conv2's forward and weight
+# gradient run as GEMMs over one im2col matrix (ResNet-18 layer3 / layer4: _use_fwd_gemm),
+# the block marks conv2 as the consumer (EPI_CONSUMER) while conv1 runs; conv1 then returns
+# a placeholder carrying its raw output and its epilogue's inputs (LazyEpi), and conv2 builds
+# its im2col matrix from them with the epilogue applied on the fly (ssq_gemm_col_epilogue):
+# the epilogue's forward launch and its activation-sized output are gone, the bits are the
+# same (col is the im2col of the same values; the backward runs the same ssq_epilogue_bwd on
+# the same input gradient).  Any other consumer materialises the placeholder with exactly
+# the ops QuantModule.forward runs.  A/B knob: SSQ_EPI_GEMM=0.
+EPI_INTO_GEMM = os.environ.get("SSQ_EPI_GEMM", "1") != "0"
+EPI_CONSUMER = [None]
+
+
+class LazyEpi:
+    """conv1's raw output y and its K13 epilogue's inputs (QuantModule.forward's fused
+    branch: bias, gamma^z / phi^z, activation code, per-tensor act quantizer)."""
+
+    def __init__(self, y, bias, gamma, phi, relu, q):
+        self.y, self.bias, self.gamma, self.phi, self.relu, self.q = y, bias, gamma, phi, relu, q
+
+    def materialize(self):
+        y, bias, gamma, phi, relu, q = self.y, self.bias, self.gamma, self.phi, self.relu, self.q
+        if gamma is not None:
+            return epilogue(y, bias, gamma, phi, None, relu, q)
+        if q is not None:
+            return bias_act_quant(y, bias, None, relu, q.delta, q.zero_point, q.n_bits, q.sym)
+        if bias is not None or relu:
+            return bias_act(y, bias, None, relu)
+        return y
+
+
+def lazy_epilogue(y, bias, gamma, phi, relu, q):
+    out = torch.empty_like(y)
+    out._ssq_epi = LazyEpi(y, bias, gamma, phi, int(relu), q)
+    return out
+
+
+def materialize_epi(x):
+    epi = getattr(x, "_ssq_epi", None)
+    return x if epi is None else epi.materialize()
+
+
+class EpiConvGemmFn(torch.autograd.Function):
+    """conv2d(epilogue(y), W) (no bias, ungrouped, dilation 1) as ONE im2col build with the
+    epilogue folded in (ssq_gemm_col_epilogue) + the strided-batched GEMM of conv_fwd_gemm.
+    Backward: the input gradient on MIOpen (the input's values are not read), the weight
+    gradient as conv_wgrad_gemm over the saved im2col matrix, then the epilogue's backward
+    (ssq_epilogue_bwd) on that input gradient -- the unfused path's kernels and operands."""
+
+    @staticmethod
+    def forward(ctx, y, bias, gamma, phi, delta, zp, weight, cfg):
+        relu, n_bits, sym, stride, padding = cfg
+        Nb, C_, H, W, Co, R, S, st, pad, OH, OW = _gemm_geo(y.shape, weight.shape, stride, padding)
+        y, yp = fptr(y.detach(), "conv output")
+        flat = (lambda t, nm: (None, None) if t is None else fptr(t.detach().reshape(-1), nm))
+        b, bp = flat(bias, "bias")
+        gm, gmp = flat(gamma, "gamma")
+        ph, php = flat(phi, "phi")
+        d, dp = flat(delta, "delta")
+        z, zpp = flat(zp, "zero_point")
+        for t, nm in ((b, "bias"), (gm, "gamma"), (ph, "phi")):
+            if t is not None and t.numel() != C_:
+                raise A.SSQError(f"epilogue into GEMM: {nm} must have one value per channel")
+        quant = d is not None
+        lo, hi = qrange(n_bits, sym) if quant else (0, 1)
+        NP, CRS = Nb * OH * OW, C_ * R * S
+        col = torch.empty(NP, CRS, dtype=torch.float32, device=y.device)
+        call("ssq_gemm_col_epilogue", yp, bp, gmp, php, int(relu), dp, zpp, lo, hi, Nb, C_, H, W,
+             R, S, st, pad, _vp(col), stream_of(y))
+        out = torch.matmul(weight.detach().reshape(Co, CRS), col.view(Nb, OH * OW, CRS).transpose(1, 2))
+        ctx.save_for_backward(y, bias, gamma, phi, delta, zp, weight, col)
+        ctx.cfg = (int(relu), lo, hi, quant, C_, H * W, stride, padding)
+        return out.view(Nb, Co, OH, OW)
+
+    @staticmethod
+    def backward(ctx, g):
+        y, bias, gamma, phi, delta, zp, weight, col = ctx.saved_tensors
+        relu, lo, hi, quant, C_, hw, stride, padding = ctx.cfg
+        need = ctx.needs_input_grad
+        g = g.contiguous()
+        # the conv's input: only its shape matters to the input gradient and the dy operand
+        x_like = torch.empty(y.shape, dtype=y.dtype, device=y.device)
+        gw = None
+        if need[6]:
+            _, dy2 = gemm_operands(x_like, g, weight.shape, stride, padding, want_col=False,
+                                   want_dy2=True)
+            gw = torch.matmul(dy2, col).view(tuple(weight.shape))
+        if not any(need[:6]):
+            return None, None, None, None, None, None, gw, None
+        gx = torch.ops.aten.convolution_backward(
+            g, x_like, weight, None, _pair(stride), _pair(padding), [1, 1], False, [0, 0], 1,
+            (True, False, False))[0]
+        gy, _, ggm, gph, _, gd, gz, _, _, _ = _epilogue_backward(
+            gx, y, bias, gamma, phi, None, delta, zp, relu, lo, hi, quant, C_, hw,
+            (need[0], False, need[2], need[3], False, need[4], need[5]))
+        return gy, None, ggm, gph, gd, gz, gw, None
+
+
+def epi_conv_gemm(x, weight, stride, padding):
+    """conv2d of a LazyEpi placeholder x through EpiConvGemmFn."""
+    e = x._ssq_epi
+    q = e.q
+    cfg = (e.relu, q.n_bits if q is not None else 8, q.sym if q is not None else False,
+           stride, padding)
+    return EpiConvGemmFn.apply(e.y, e.bias, e.gamma, e.phi, None if q is None else q.delta,
+                               None if q is None else q.zero_point, weight, cfg)
 
 
 def epilogue(y, bias, gamma, phi, res, relu, q=None, lazy=False):
@@ -1368,6 +1483,37 @@ def adam_step(params, grads, exp_avgs, exp_avg_sqs, beta1, beta2, eps, hyper=Non
         na[k] = p_.numel()
     call("ssq_adam", n, pa, ga, ma, va, na, float(1 - beta1), float(beta2), float(1 - beta2),
          float(eps), _vp(hyper), float(neg_step_size), float(bc2_sqrt), stream_of(params[0]))
+
+
+def fc_recon_iter(x_cache, tgt_cache, slot, bs, w, v, delta, zp, n_bits, bias, exp_avg,
+                  exp_avg_sq, beta1, beta2, eps, g=None, gv_out=None, loss_out=None):
+    """One fused BRECQ AdaRound iteration of a Linear layer (ssq_fc_recon_iter, K19): the
+    forward with W^ = AdaRound(w, v) on the fly, the p = 2 loss and its gradient, then dW,
+    V's gradient with the rounding regulariser and V's Adam step, in two launches.  slot:
+    int64 device words (bs indices, then (lambda, b, -lr/bc1, sqrt(bc2)) as fp32).
+    Returns (loss, g)."""
+    xc, xp = fptr(x_cache, "x cache")
+    tc, tp = fptr(tgt_cache, "target cache")
+    Co, Ci = int(w.shape[0]), int(w.shape[1])
+    if xc.shape[1:].numel() != Ci or tc.shape[1:].numel() != Co or slot.dtype != torch.int64 \
+            or not slot.is_contiguous() or slot.numel() < bs + 2:
+        raise A.SSQError("fc_recon_iter: shapes / slot")
+    for t, nm in ((w, "weight"), (v, "V"), (exp_avg, "exp_avg"), (exp_avg_sq, "exp_avg_sq")):
+        A.check(t, nm)
+        if not t.is_contiguous() or t.numel() != Co * Ci:
+            raise A.SSQError(f"fc_recon_iter: {nm} must be contiguous [Co, Ci]")
+    d, dp = fptr(delta.detach().reshape(-1), "delta")
+    z, zpp = fptr(zp.detach().reshape(-1), "zero_point")
+    bp = fptr(bias.detach().reshape(-1), "bias")[1] if bias is not None else None
+    dev_ = w.device
+    g = torch.empty(bs, Co, device=dev_) if g is None else g
+    loss = torch.empty(1, device=dev_) if loss_out is None else loss_out
+    ws, wsn = workspace(query("ssq_fc_recon_workspace_size", Co, Ci, bs), dev_, "fc")
+    call("ssq_fc_recon_iter", xp, tp, _vp(slot), bs, _vp(w), _vp(v), dp, zpp, 0,
+         2 ** n_bits - 1, bp, Co, Ci, float(1 - beta1), float(beta2), float(1 - beta2),
+         float(eps), _vp(exp_avg), _vp(exp_avg_sq), _vp(g), _vp(gv_out), _vp(loss), ws, wsn,
+         stream_of(w))
+    return loss, g
 
 
 def adam_arm(params, exp_avgs, exp_avg_sqs, beta1, beta2, eps, hyper):
@@ -1798,7 +1944,14 @@ DWCONV_POLICY = "auto"
 def conv2d(x, weight, stride=1, padding=0, dilation=1, groups=1):
     """F.conv2d without bias: depthwise convs on K18/K17 (DWCONV_POLICY), otherwise MIOpen
     with the K17 weight gradient when the weight needs one (WGRAD_POLICY); 1x1 stride-2
-    forwards as one batched GEMM (FWD_1X1_GEMM)."""
+    forwards as one batched GEMM (FWD_1X1_GEMM); a LazyEpi input (a BasicBlock's conv1
+    epilogue) folded into the im2col GEMM of conv_fwd_gemm's shapes, else materialised."""
+    if getattr(x, "_ssq_epi", None) is not None:
+        if (weight.requires_grad and torch.is_grad_enabled() and groups == 1 and
+                (dilation if isinstance(dilation, int) else max(dilation)) == 1 and
+                _use_fwd_gemm(x, weight, stride, padding, groups)):
+            return epi_conv_gemm(x, weight, stride, padding)
+        x = materialize_epi(x)
     if DWCONV_POLICY == "auto" and dwconv_supported(x, weight, stride, padding, dilation, groups) \
             and x.is_contiguous():
         if torch.is_grad_enabled() and (x.requires_grad or weight.requires_grad):

@@ -182,6 +182,59 @@ def _eager_loop(opt_params, loss_func, feeder, bucket, cached_grads, block, iter
     probe(iters, opt_params)
 
 
+# BRECQ's layer loop on a Linear layer (the network's last layer, 20000 iterations in the
+# end-to-end flow), AdaRound weight phase at world 1: the whole iteration as the fused K19
+# pair (kernels.fc_recon_iter) instead of gather / AdaRound / GEMM / loss / GEMM / AdaRound
+# backward / Adam launches.  A/B knob: SSQ_FUSE_FC=0.
+FUSE_FC = _FAST and os.environ.get("SSQ_FUSE_FC", "1") != "0"
+
+
+def _fc_fused_body(layer, qmodules, act_quant, p, bucket, feeder, optimizer, last):
+    """The fused fc iteration's body, or None when the loop is not one it covers: a
+    Linear QuantModule alone, soft AdaRound with per-row delta, no activation, no act
+    quantizer, no gamma^z / phi^z affine, p = 2, world 1, batch <= 64, C_in <= 4096."""
+    import torch.nn.functional as F
+    if not (FUSE_FC and not act_quant and bucket is None and float(p) == 2.0
+            and len(qmodules) == 1 and qmodules[0] is layer and isinstance(layer, QuantModule)):
+        return None
+    m = layer
+    q = m.weight_quantizer
+    if not (m.fwd_func is F.linear and m.use_weight_quant and m.cache_features == 'none'
+            and m.se_module is None and isinstance(m.activation_function, StraightThrough)
+            and (not m.use_act_quant or m.disable_act_quant) and m._affine_is_identity()
+            and isinstance(q, AdaRoundQuantizer) and q.round_mode == 'learned_hard_sigmoid'
+            and q.soft_targets and getattr(q, '_stash', None) is None):
+        return None
+    w, v = m.weight, q.alpha
+    if w.dim() != 2:
+        return None
+    Co, Ci = int(w.shape[0]), int(w.shape[1])
+    if not (w.is_cuda and w.is_contiguous() and v.is_contiguous()
+            and q.delta.numel() == Co and q.zero_point.numel() == Co
+            and feeder.inp.dim() == 2 and feeder.inp.shape[1] == Ci
+            and feeder.out.dim() == 2 and feeder.out.shape[1] == Co
+            and 1 <= feeder.bs <= 64 and Ci <= 4096 and feeder.bs * Ci * 4 <= 96 * 1024):
+        return None
+    if optimizer.params != [v]:
+        return None
+    st = optimizer.state[v]
+    b1, b2 = optimizer.param_groups[0]["betas"]
+    eps = optimizer.param_groups[0]["eps"]
+    bias = m.bias if (m.bias is None or m.train_bias) else m.bias.detach()
+    gbuf = torch.empty(feeder.bs, Co, device=w.device)
+    gv = torch.zeros_like(v)        # V's gradient, for anyone reading .grad (test probes)
+
+    def body():
+        src = feeder.chunk_dev[feeder.slot] if feeder.slot is not None else feeder._dev
+        loss, _ = K.fc_recon_iter(feeder.inp, feeder.out, src, feeder.bs, w.detach(), v.data,
+                                  q.delta, q.zero_point, q.n_bits, bias, st["exp_avg"],
+                                  st["exp_avg_sq"], b1, b2, eps, g=gbuf, gv_out=gv)
+        v.grad = gv
+        last['rec'] = loss
+        last['step'] = True
+    return body
+
+
 def _fast_loop(block, qmodules, opt_params, loss_func, feeder, bucket, iters, act_quant, lr, p,
                graph):
     """Same iteration, device only: one H2D copy (batch indices + this iteration's
@@ -278,6 +331,10 @@ def _fast_loop(block, qmodules, opt_params, loss_func, feeder, bucket, iters, ac
     def body_post():
         if bucket is not None:
             _step()
+
+    fc_body = _fc_fused_body(block, qmodules, act_quant, p, bucket, feeder, optimizer, last)
+    if fc_body is not None:
+        body_pre = fc_body          # gather, forward, loss, backward and Adam: two launches
 
     ws_cache = {}
     with contextlib.ExitStack() as stack:
@@ -401,6 +458,7 @@ def _run(iters, loss_func, feeder, optimizer, scheduler, shadow, use_graph, buck
                     shadow.step()
                     scheduler.step()
                     optimizer.param_groups[0]['lr'] = shadow.param_groups[0]['lr']
+                i += 1
                 continue
             feeder.stage(perm, extra=(lam, float(b)) + hyp)
             # the round-loss value (reporting only) from alpha before this step, as the

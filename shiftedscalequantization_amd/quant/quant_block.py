@@ -5,6 +5,7 @@ kept as in the reference.  setPathName is defined on BaseQuantBlock so every blo
 works with QuantModel (the reference defines it only on QuantBasicBlock, so QuantModel
 crashes on ResNet-50 / MobileNetV2 / RegNetX: quant_model.py:30 vs quant_block.py:119).
 """
+import torch
 import torch.nn as nn
 
 from .. import kernels as K
@@ -148,7 +149,18 @@ class QuantBasicBlock(BaseQuantBlock):
         if self.cache_features == 'if':
             self.cached_inp_features += [self._cache(x)]
         residual = x if self.downsample is None else self._residual(self.downsample, x)
-        out = self._tail(self.conv2, self.conv1(x), residual)
+        # conv1's output feeds conv2 only: its epilogue may fold into conv2's im2col GEMM
+        # (kernels.EPI_CONSUMER; conv2 materialises it when it does not run as that GEMM)
+        fold = (K.EPI_INTO_GEMM and torch.is_grad_enabled() and x.is_cuda
+                and not self._forward_hooks and not self._forward_pre_hooks
+                and not self.conv2._forward_pre_hooks and self.conv2.cache_features == 'none')
+        prev = K.EPI_CONSUMER[0]
+        K.EPI_CONSUMER[0] = self.conv2 if fold else None
+        try:
+            out1 = self.conv1(x)
+        finally:
+            K.EPI_CONSUMER[0] = prev
+        out = self._tail(self.conv2, out1, residual)
         if self.cache_features == 'of':
             self.cached_out_features += [self._cache(out)]
         return out

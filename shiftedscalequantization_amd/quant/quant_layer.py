@@ -374,11 +374,12 @@ class QuantModule(nn.Module):
 
     def _conv(self, input, weight, bias=None):
         """The layer's conv / linear; a conv whose weight needs a gradient goes through
-        K.conv2d (deterministic K17 weight gradient, see kernels.WGRAD_POLICY)."""
+        K.conv2d (deterministic K17 weight gradient, see kernels.WGRAD_POLICY; a LazyEpi
+        input folded into its im2col GEMM there)."""
         if self.fwd_func is F.conv2d and input.is_cuda and weight.requires_grad:
             out = K.conv2d(input, weight, **self.fwd_kwargs)
             return out if bias is None else out + bias.view(1, -1, 1, 1)
-        return self.fwd_func(input, weight, bias, **self.fwd_kwargs)
+        return self.fwd_func(K.materialize_epi(input), weight, bias, **self.fwd_kwargs)
 
     def forward_raw(self, input):
         """(conv(input, W_hat) without bias, bias): for a parent block that fuses this
@@ -401,6 +402,14 @@ class QuantModule(nn.Module):
             relu = self.act_code()
             q = fusable_act_quantizer(self.act_quantizer, act_q)
             gamma, phi = self.affine()
+            # (with an act quantizer only in the affine epilogue's form: the plain bias+act+q
+            # pass has its own backward kernel, whose delta sums are not the affine one's)
+            if (K.EPI_CONSUMER[0] is not None and (q is not None or not act_q)
+                    and (q is None or gamma is not None)
+                    and self.cache_features == 'none' and not self._forward_hooks):
+                # the parent block's next conv folds this epilogue into its im2col GEMM
+                # (kernels.EPI_CONSUMER); anything else materialises it
+                return K.lazy_epilogue(out, bias, gamma, phi, relu, q)
             if gamma is not None:
                 out = K.epilogue(out, bias, gamma, phi, None, relu, q)
                 act_q = act_q and q is None

