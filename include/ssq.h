@@ -336,21 +336,25 @@ int ssq_gather_rows2_staged(const float* src0, float* dst0, int64_t row0, const 
 /* ---------------------------------------------------------------- K19 fused fc iteration
  * One BRECQ AdaRound iteration of a Linear layer (the network's last layer: layer_recon.py
  * :10-104 with its LossFunction :107-170, adaptive_rounding.py:38-67, lp_loss p = 2,
- * quant_layer.py:25-32) in two launches: y = x[idx] W^T + bias with W^ = AdaRound(W, V)
- * (per-row delta / zp, soft rounding, clamp to [qmin, qmax]) computed on the fly, the loss
- * gradient g = dL/dy; then dW = g^T x[idx], V's gradient (AdaRound backward + the rounding
- * regulariser) and V's Adam step (exp_avg / exp_avg_sq; ssq_adam's ops), and the loss
- * value into loss_out.  `slot` (device) holds the bs batch indices (rows of x_cache
- * [N, Ci] and tgt_cache [N, Co]) followed by the iteration's words as fp32 pairs: (lambda,
- * b) of the regulariser, then Adam's (-lr/bc1, sqrt(bc2)).  g ([bs, Co]) is scratch (and
- * readable); gv_out may receive V's gradient.  1 <= bs <= 64, Ci <= 4096.             */
+ * quant_layer.py:25-32) in two launches: y = x[idx] What^T + bias and the loss gradient
+ * g = dL/dy; then dW = g^T x[idx], V's gradient (AdaRound backward + the rounding
+ * regulariser), V's Adam step (exp_avg / exp_avg_sq; ssq_adam's ops), What = AdaRound(W, V)
+ * of the updated V for the next call (per-row delta / zp, soft rounding, clamp to
+ * [qmin, qmax]; ssq_adaround_fwd's ops -- which also provides the first call's What), and
+ * the loss value into loss_out.  `slot` (device) holds the bs batch indices (rows of
+ * x_cache [N, Ci] and tgt_cache [N, Co]) followed by the iteration's words as fp32 pairs:
+ * (lambda, b) of the regulariser, then Adam's (-lr/bc1, sqrt(bc2)).  g ([bs, Co]) is
+ * scratch (and readable); gv_out may receive V's gradient.  1 <= bs <= 64, Ci a multiple
+ * of 64 up to 4096; x_cache and What 16-B aligned.  fp32 MFMA (v_mfma_f32_16x16x4_f32):
+ * the forward as 16 x 16 output tiles with the K range split over 8 waves, the weight
+ * gradient as one 16 x 16 tile per wave; fixed summation orders.                      */
 size_t ssq_fc_recon_workspace_size(int64_t Co, int64_t Ci, int64_t bs);
 int ssq_fc_recon_iter(const float* x_cache, const float* tgt_cache, const int64_t* slot,
-                      int64_t bs, const float* W, float* V, const float* delta, const float* zp,
-                      int qmin, int qmax, const float* bias, int64_t Co, int64_t Ci,
-                      float one_minus_beta1, float beta2, float one_minus_beta2, float eps,
-                      float* exp_avg, float* exp_avg_sq, float* g, float* gv_out, float* loss_out,
-                      void* ws, size_t ws_bytes, ssq_stream_t stream);
+                      int64_t bs, const float* W, float* V, float* What, const float* delta,
+                      const float* zp, int qmin, int qmax, const float* bias, int64_t Co,
+                      int64_t Ci, float one_minus_beta1, float beta2, float one_minus_beta2,
+                      float eps, float* exp_avg, float* exp_avg_sq, float* g, float* gv_out,
+                      float* loss_out, void* ws, size_t ws_bytes, ssq_stream_t stream);
 
 /* ---------------------------------------------------------------- K13 fused epilogue
  * QuantModule conv bias add (quant_layer.py:250), the block's residual add and ReLU

@@ -74,8 +74,8 @@ SIGNATURES = {
     "ssq_gather_rows2": (_i, [_p, _p, _i64, _p, _p, _i64, _p, _i64, _p]),
     "ssq_gemm_col_epilogue": (_i, [_p, _p, _p, _p, _i, _p, _p, _i, _i] + [_i64] * 8 + [_p, _p]),
     "ssq_fc_recon_workspace_size": (_sz, [_i64, _i64, _i64]),
-    "ssq_fc_recon_iter": (_i, [_p, _p, _p, _i64, _p, _p, _p, _p, _i, _i, _p, _i64, _i64, _f, _f, _f,
-                               _f, _p, _p, _p, _p, _p, _p, _sz, _p]),
+    "ssq_fc_recon_iter": (_i, [_p, _p, _p, _i64, _p, _p, _p, _p, _p, _i, _i, _p, _i64, _i64, _f, _f,
+                               _f, _f, _p, _p, _p, _p, _p, _p, _sz, _p]),
     "ssq_gather_rows2_staged": (_i, [_p, _p, _i64, _p, _p, _i64, _p, _i64, _p, _i64, _p]),
     "ssq_bias_act": (_i, [_p, _p, _p, _p, _i64, _i64, _i64, _i, _p]),
     "ssq_relu_bwd": (_i, [_p, _p, _p, _i64, _p]),

@@ -7,34 +7,36 @@
 // adaptive_rounding.py:38-67, then F.linear), the loss (lp_loss p = 2 + the rounding
 // regulariser, block_recon.py:119-182 / layer_recon.py:107-170), its backward and Adam.
 // Each of those is microseconds of GPU work on this layer, so as separate launches the loop
-// is bound by launch boundaries (r4: 9 launches, 45 us of GPU time per iteration).  Here:
+// is bound by dependent-launch boundaries (r5: 8 launches, 40 us per iteration).  Here:
 //
-//   fc_fwd_loss  (one workgroup per 32 output channels): the batch rows x[idx[r]] staged in
-//     LDS, W^ = AdaRound(W, V) of the workgroup's rows computed on the fly into LDS (the
-//     adaround_fwd_kernel ops), y = x W^T + bias (fp32 FMA, ci in order), the lp_loss p = 2
-//     term and gradient of every output (lp_elem: the lp_loss_kernel ops) -> g = dL/dy and
-//     one double loss partial per workgroup;
-//   fc_bwd_adam  (one workgroup per 8 output channels): dW = g^T x (r in order), AdaRound's
-//     backward with the rounding regulariser folded in (the adaround_bwd_kernel ops, lambda
-//     and b from the iteration's device words), and the Adam step of V (ssq_adam's ops);
-//     workgroup 0 also sums the loss partials in order (the loss value).
+//   fc_fwd_loss  (one workgroup per 16 x 16 tile of y, 8 waves splitting C_in): y = x W^T
+//     + bias on fp32 MFMA (v_mfma_f32_16x16x4_f32, every operand load of a wave issued
+//     before its first MFMA), the 8 partial tiles added in wave order, then the lp_loss
+//     p = 2 term and gradient of every output (lp_elem: the lp_loss_kernel ops) -> g = dL/dy
+//     and one double loss partial per workgroup;
+//   fc_bwd_adam  (one workgroup per 16 x 16 tile of dW): dW = g^T x on the same MFMA, then
+//     per element (one a thread) AdaRound's backward with the rounding regulariser folded in (the
+//     adaround_bwd_kernel ops, lambda and b from the iteration's device words), V's Adam step
+//     (ssq_adam's ops), and W^ of the NEXT iteration from the updated V (the
+//     adaround_fwd_kernel ops) -- so the forward reads W^ instead of evaluating the soft
+//     rounding (a divide and an exp per weight) itself; workgroup 0 also sums the loss
+//     partials.
 //
-// The batch indices and the iteration's scalars are read from one device slot (the
-// BatchFeeder's words: idx, then (lambda, b), then Adam's (-lr/bc1, sqrt(bc2))), so a
-// graph of several iterations reads one slot each (quant/block_recon.py ChunkGraph).
-// Deterministic: fixed summation orders, no atomics.  The GEMMs' summation order is this
-// kernel's, not hipBLASLt's: values agree with the unfused path to fp32 rounding
-// (tests/test_recon_gpu.py::test_fc_fused_iteration_matches_unfused).
+// W^ of the first iteration comes from ssq_adaround_fwd (the caller's).  The batch indices
+// and the iteration's scalars are read from one device slot (BatchFeeder's words: idx, then
+// (lambda, b), then Adam's (-lr/bc1, sqrt(bc2))), so a graph of several iterations reads one
+// slot each (quant/block_recon.py ChunkGraph).  Deterministic: fixed summation orders, no
+// atomics.  The GEMMs' summation order is this kernel's, not hipBLASLt's: values agree with
+// the unfused launches to fp32 rounding (tests/test_recon_gpu.py).
 #include "fin_tasks.h"
 #include "ssq_common.h"
 
 namespace ssq {
 
-constexpr uint32_t kFcCo = 32;        // output channels per forward workgroup
 constexpr uint32_t kFcRows = 64;      // max batch rows
-constexpr uint32_t kFcCi = 128;       // ci chunk staged per step (forward)
-constexpr uint32_t kFcBwdCo = 8;      // output channels per backward workgroup
-constexpr uint32_t kFcMaxCi = 4096;   // x rows staged whole in the backward (LDS)
+constexpr uint32_t kFcMaxCi = 4096;
+constexpr uint32_t kFcKW = 8;         // forward: waves per output tile = K chunks
+constexpr uint32_t kFcBwdW = 4;       // backward: waves per workgroup (one 16x16 dW tile)
 
 // W^ of one element: adaround_fwd_kernel's ops (per-row delta, scale 1)
 __device__ __forceinline__ float fc_what(float w, float v, float d, float z, float lo, float hi) {
@@ -42,117 +44,155 @@ __device__ __forceinline__ float fc_what(float w, float v, float d, float z, flo
   return __fmul_rn(__fsub_rn(q, z), d);
 }
 
-// Forward: workgroup b owns output channels [b*32, b*32+32); thread t -> channel t % 32,
-// rows (t / 32) + 8 j.  Every output's dot product runs ci = 0, 1, ... in order.
-__global__ __launch_bounds__(kBlock) void fc_fwd_loss(
+// 16 consecutive floats (4 x 16 B) from a 16-B aligned row, or zeros
+__device__ __forceinline__ void ld16(const float* p, bool ok, f32x4* v) {
+#pragma unroll
+  for (int u = 0; u < 4; ++u) v[u] = ok ? ((const f32x4*)p)[u] : f32x4{0.0f, 0.0f, 0.0f, 0.0f};
+}
+
+// Forward: workgroup = one 16 x 16 tile of y (rows r0.., columns o0..), 8 waves; wave w
+// sums k in its chunk [w*ck, (w+1)*ck) with v_mfma_f32_16x16x4_f32 (A = x rows, B = W^^T),
+// 64 k per round: lane l (k slot q = l >> 4) feeds k = k0 + 16 q + s at step s, so its 16
+// A and 16 B values are 4 float4 loads each, all issued before the first MFMA.  The 8
+// partial tiles are added in wave order through LDS, then the epilogue: bias, the lp_loss
+// p = 2 term and gradient (lp_elem), one loss partial per workgroup.
+__global__ __launch_bounds__(kBlock * 2) void fc_fwd_loss(
     const float* __restrict__ x, const int64_t* __restrict__ slot, uint32_t bs,
-    const float* __restrict__ W, const float* __restrict__ V, const float* __restrict__ delta,
-    const float* __restrict__ zp, float lo, float hi, const float* __restrict__ bias,
-    uint32_t Co, uint32_t Ci, const float* __restrict__ tgt, float inv_m, float* __restrict__ g,
+    const float* __restrict__ what, const float* __restrict__ bias, uint32_t Co, uint32_t Ci,
+    uint32_t ck, const float* __restrict__ tgt, float inv_m, float* __restrict__ g,
     double* __restrict__ part) {
-  __shared__ float xs[kFcRows][kFcCi + 1];
-  __shared__ float ws[kFcCo][kFcCi + 1];
-  __shared__ double red[kBlock / kWave];
-  const uint32_t t = threadIdx.x, cl = t % kFcCo, rg = t / kFcCo;   // rg in [0, 8)
-  const uint32_t co0 = blockIdx.x * kFcCo, co = co0 + cl;
-  constexpr uint32_t kRpt = kFcRows / (kBlock / kFcCo);             // 8 rows per thread
-  float acc[kRpt];
+  __shared__ f32x4 red[kFcKW][kWave];
+  __shared__ double lred[kWave];
+  const uint32_t lane = threadIdx.x & (kWave - 1), w = threadIdx.x / kWave;
+  const uint32_t i16 = lane & 15, q = lane >> 4;
+  const uint32_t o0 = blockIdx.x * 16, r0 = blockIdx.y * 16;
+  const uint32_t ra = r0 + i16, ob = o0 + i16;          // this lane's A row / B column
+  const bool aok = ra < bs, bok = ob < Co;
+  const float* xr = x + (aok ? slot[ra] : 0) * (int64_t)Ci;
+  const float* wr = what + (int64_t)(bok ? ob : 0) * Ci;
+  f32x4 acc = {0.0f, 0.0f, 0.0f, 0.0f};
+  const uint32_t k1 = min(Ci, (w + 1) * ck);
+  for (uint32_t k0 = w * ck; k0 < k1; k0 += 64) {
+    const uint32_t kq = k0 + 16 * q;
+    const bool in = kq < k1;                          // Ci % 64 == 0 -> whole 16-runs
+    f32x4 av[4], bv[4];
+    ld16(xr + kq, aok && in, av);
+    ld16(wr + kq, bok && in, bv);
 #pragma unroll
-  for (uint32_t j = 0; j < kRpt; ++j) acc[j] = 0.0f;
-  for (uint32_t c0 = 0; c0 < Ci; c0 += kFcCi) {
-    const uint32_t nc = min(kFcCi, Ci - c0);
-    // stage x[idx[r], c0:c0+nc] and W^[co0:co0+32, c0:c0+nc]
-    for (uint32_t e = t; e < bs * kFcCi; e += kBlock) {
-      const uint32_t r = e / kFcCi, c = e % kFcCi;
-      xs[r][c] = c < nc ? x[slot[r] * (int64_t)Ci + c0 + c] : 0.0f;
+    for (int u = 0; u < 4; ++u) {
+      acc = __builtin_amdgcn_mfma_f32_16x16x4f32(av[u].x, bv[u].x, acc, 0, 0, 0);
+      acc = __builtin_amdgcn_mfma_f32_16x16x4f32(av[u].y, bv[u].y, acc, 0, 0, 0);
+      acc = __builtin_amdgcn_mfma_f32_16x16x4f32(av[u].z, bv[u].z, acc, 0, 0, 0);
+      acc = __builtin_amdgcn_mfma_f32_16x16x4f32(av[u].w, bv[u].w, acc, 0, 0, 0);
     }
-    for (uint32_t e = t; e < kFcCo * kFcCi; e += kBlock) {
-      const uint32_t r = e / kFcCi, c = e % kFcCi, o = co0 + r;
-      float wv = 0.0f;
-      if (o < Co && c < nc) {
-        const int64_t i = (int64_t)o * Ci + c0 + c;
-        wv = fc_what(W[i], V[i], delta[o], zp[o], lo, hi);
-      }
-      ws[r][c] = wv;
-    }
-    __syncthreads();
-    for (uint32_t c = 0; c < nc; ++c) {
-      const float wv = ws[cl][c];
-#pragma unroll
-      for (uint32_t j = 0; j < kRpt; ++j) acc[j] = __fmaf_rn(xs[rg + 8 * j][c], wv, acc[j]);
-    }
-    __syncthreads();
   }
-  double la = 0.0;
-  if (co < Co) {
-    const float b = bias ? bias[co] : 0.0f;
+  red[w][lane] = acc;
+  __syncthreads();
+  if (w != 0) return;
+  f32x4 y = red[0][lane];
 #pragma unroll
-    for (uint32_t j = 0; j < kRpt; ++j) {
-      const uint32_t r = rg + 8 * j;
+  for (uint32_t k = 1; k < kFcKW; ++k) {
+    const f32x4 t = red[k][lane];
+    y.x = __fadd_rn(y.x, t.x);
+    y.y = __fadd_rn(y.y, t.y);
+    y.z = __fadd_rn(y.z, t.z);
+    y.w = __fadd_rn(y.w, t.w);
+  }
+  // D layout: column o = o0 + (lane & 15), rows r0 + 4 (lane >> 4) + v
+  const uint32_t o = o0 + i16;
+  double la = 0.0;
+  if (o < Co) {
+    const float b = bias ? bias[o] : 0.0f;
+    float yv[4] = {y.x, y.y, y.z, y.w};
+#pragma unroll
+    for (int v = 0; v < 4; ++v) {
+      const uint32_t r = r0 + 4 * q + v;
       if (r < bs) {
-        const float y = bias ? __fadd_rn(acc[j], b) : acc[j];
-        g[(int64_t)r * Co + co] = lp_elem<0>(y, tgt[slot[r] * (int64_t)Co + co], 2.0f, inv_m,
-                                             1.0f, 0, la);
+        const float yy = bias ? __fadd_rn(yv[v], b) : yv[v];
+        g[(int64_t)r * Co + o] = lp_elem<0>(yy, tgt[slot[r] * (int64_t)Co + o], 2.0f, inv_m, 1.0f, 0,
+                                            la);
       }
     }
   }
   la = wave_sum(la);
-  if ((t & (kWave - 1)) == 0) red[t / kWave] = la;
-  __syncthreads();
-  if (t == 0) {
-    double s = red[0];
-#pragma unroll
-    for (int k = 1; k < kBlock / kWave; ++k) s += red[k];
-    part[blockIdx.x] = s;
-  }
+  if (lane == 0) part[blockIdx.y * gridDim.x + blockIdx.x] = la;
 }
 
-// Backward + Adam: workgroup b owns output channels [b*8, b*8+8) x every ci; the batch's x
-// rows and g columns staged in LDS; thread t walks elements t, t + 256, ... of the tile.
+// Backward + Adam + the next W^: workgroup = one 16 x 16 tile of dW (rows o0.., columns
+// c0..), 4 waves.  Wave 0 forms dW = g^T x over the batch rows with v_mfma_f32_16x16x4_f32
+// (lane slot q feeds rows r = 4 s + q in a fixed order) and puts the tile in LDS; then each
+// of the 4 waves takes 4 of its rows, one element per lane: AdaRound's backward with the
+// rounding regulariser (adaround_bwd_kernel's ops, lambda and b from the iteration's words),
+// V's Adam step (ssq_adam's ops) and W^ of the updated V (adaround_fwd_kernel's ops) for the
+// next iteration.  The per-element math (a divide, two exps, a pow, a sqrt, Adam's divides)
+// is most of the kernel, so it is spread over 4x the waves of a wave-per-tile form (measured:
+// DESIGN §5).  Every load of a wave is issued before its first use.
+// Workgroup 0 also sums the forward's loss partials in order.
 __global__ __launch_bounds__(kBlock) void fc_bwd_adam(
     const float* __restrict__ x, const int64_t* __restrict__ slot, uint32_t bs,
     const float* __restrict__ g, const float* __restrict__ W, float* __restrict__ V,
     const float* __restrict__ delta, const float* __restrict__ zp, float lo, float hi,
     uint32_t Co, uint32_t Ci, const float* __restrict__ regp, AdamConst ac,
     float* __restrict__ m, float* __restrict__ v, float* __restrict__ gv_out,
-    const double* __restrict__ part, uint32_t nparts, double M, float* __restrict__ loss_out) {
-  extern __shared__ float sm[];
-  float* xs = sm;                        // [bs][Ci]
-  float* gs = sm + (size_t)bs * Ci;      // [bs][8]
-  const uint32_t t = threadIdx.x;
-  if (blockIdx.x == 0 && t == 0) {
+    float* __restrict__ what, const double* __restrict__ part, uint32_t nparts, double M,
+    float* __restrict__ loss_out) {
+  __shared__ float tile_dw[16][17];
+  const uint32_t lane = threadIdx.x & (kWave - 1), w = threadIdx.x / kWave;
+  if (blockIdx.x == 0 && threadIdx.x == 0) {
     // the loss value: the forward's workgroup partials in order
     double s = 0.0;
     for (uint32_t k = 0; k < nparts; ++k) s += part[k];
     loss_out[0] = (float)(s / M);
   }
-  const uint32_t co0 = blockIdx.x * kFcBwdCo;
-  for (uint32_t e = t; e < bs * Ci; e += kBlock) {
-    const uint32_t r = e / Ci, c = e - r * Ci;
-    xs[e] = x[slot[r] * (int64_t)Ci + c];
-  }
-  for (uint32_t e = t; e < bs * kFcBwdCo; e += kBlock) {
-    const uint32_t r = e / kFcBwdCo, o = co0 + e % kFcBwdCo;
-    gs[e] = o < Co ? g[(int64_t)r * Co + o] : 0.0f;
+  const uint32_t nct = Ci / 16;                       // column tiles (Ci % 16 == 0)
+  const uint32_t o0 = (blockIdx.x / nct) * 16, c0 = (blockIdx.x % nct) * 16;
+  const uint32_t i16 = lane & 15, q = lane >> 4;
+  // this thread's element: row o = o0 + 4 w + q, column c = c0 + i16
+  const uint32_t o = o0 + 4 * w + q, c = c0 + i16;
+  const bool ok = o < Co;
+  const int64_t i = (int64_t)(ok ? o : 0) * Ci + c;
+  const float wv = ok ? W[i] : 0.0f, b = ok ? V[i] : 0.0f;
+  const float mv = ok ? m[i] : 0.0f, vv = ok ? v[i] : 0.0f;
+  const float d = ok ? delta[o] : 1.0f, z = ok ? zp[o] : 0.0f;
+  const float lam = regp[0], rb = regp[1];
+  if (w == 0) {
+    // the operands: A[i][k] = g[r][o0 + i], B[k][j] = x[idx[r]][c0 + j], r = 4 s + q over
+    // the 16 steps (bs <= 64)
+    float av[16], bv[16];
+    const uint32_t oa = o0 + i16;
+#pragma unroll
+    for (int s = 0; s < 16; ++s) {
+      const uint32_t r = 4 * s + q;
+      const bool rk = r < bs;
+      av[s] = (rk && oa < Co) ? g[(int64_t)r * Co + oa] : 0.0f;
+      bv[s] = rk ? x[slot[r] * (int64_t)Ci + c0 + i16] : 0.0f;
+    }
+    f32x4 acc = {0.0f, 0.0f, 0.0f, 0.0f};
+    const uint32_t steps = (bs + 3) / 4;               // uniform
+    for (uint32_t s = 0; s < 16; ++s)
+      if (s < steps) acc = __builtin_amdgcn_mfma_f32_16x16x4f32(av[s], bv[s], acc, 0, 0, 0);
+    // D layout: column i16, rows 4 q + e
+    tile_dw[4 * q + 0][i16] = acc.x;
+    tile_dw[4 * q + 1][i16] = acc.y;
+    tile_dw[4 * q + 2][i16] = acc.z;
+    tile_dw[4 * q + 3][i16] = acc.w;
   }
   __syncthreads();
-  const float lam = regp[0], rb = regp[1];
-  const AdamRef ar{V, m, v};
-  for (uint32_t e = t; e < kFcBwdCo * Ci; e += kBlock) {
-    const uint32_t ol = e / Ci, c = e - ol * Ci, o = co0 + ol;
-    if (o >= Co) continue;
-    float dw = 0.0f;
-    for (uint32_t r = 0; r < bs; ++r) dw = __fmaf_rn(gs[r * kFcBwdCo + ol], xs[r * Ci + c], dw);
-    const int64_t i = (int64_t)o * Ci + c;
-    const float d = delta[o], z = zp[o], b = V[i];
-    // adaround_bwd_kernel's ops
-    const float u = __fadd_rn(__fadd_rn(floorf(W[i] / d), rect_sigmoid(b)), z);
-    const float gi = (u >= lo && u <= hi) ? __fmul_rn(dw, d) : 0.0f;
-    const float ga = rect_sigmoid_grad(b, gi);
-    const float gb = lam != 0.0f ? __fadd_rn(ga, round_reg_grad(b, lam, rb)) : ga;
-    if (gv_out) gv_out[i] = gb;
-    adam_apply_loaded(ac, ar, (uint32_t)i, gb, b, m[i], v[i]);
-  }
+  if (!ok) return;
+  const float dwv = tile_dw[4 * w + q][i16];
+  // adaround_bwd_kernel's ops
+  const float u0 = __fadd_rn(__fadd_rn(floorf(wv / d), rect_sigmoid(b)), z);
+  const float gi = (u0 >= lo && u0 <= hi) ? __fmul_rn(dwv, d) : 0.0f;
+  const float ga = rect_sigmoid_grad(b, gi);
+  const float gb = lam != 0.0f ? __fadd_rn(ga, round_reg_grad(b, lam, rb)) : ga;
+  if (gv_out) gv_out[i] = gb;
+  float pn = b, mn = mv, vn = vv;
+  adam_update(ac, gb, pn, mn, vn);            // ssq_adam's ops
+  V[i] = pn;
+  m[i] = mn;
+  v[i] = vn;
+  // the next iteration's W^ from the updated V (adaround_fwd_kernel's ops)
+  what[i] = fc_what(wv, pn, d, z, lo, hi);
 }
 
 }  // namespace ssq
@@ -161,47 +201,45 @@ using namespace ssq;
 
 extern "C" size_t ssq_fc_recon_workspace_size(int64_t Co, int64_t Ci, int64_t bs) {
   (void)Ci;
-  (void)bs;
-  const size_t nwg = (size_t)((Co + kFcCo - 1) / kFcCo);
+  const size_t nwg = (size_t)((Co + 15) / 16) * (size_t)((bs + 15) / 16);
   return nwg * sizeof(double);
 }
 
 extern "C" int ssq_fc_recon_iter(const float* x_cache, const float* tgt_cache,
                                  const int64_t* slot, int64_t bs, const float* W, float* V,
-                                 const float* delta, const float* zp, int qmin, int qmax,
-                                 const float* bias, int64_t Co, int64_t Ci, float one_minus_beta1,
-                                 float beta2, float one_minus_beta2, float eps, float* exp_avg,
-                                 float* exp_avg_sq, float* g, float* gv_out, float* loss_out,
-                                 void* ws, size_t ws_bytes, ssq_stream_t stream) {
-  SSQ_REQUIRE(x_cache && tgt_cache && slot && W && V && delta && zp && exp_avg && exp_avg_sq && g &&
-                  loss_out, SSQ_E_ARG, "ssq_fc_recon_iter: null pointer");
-  SSQ_REQUIRE(bs >= 1 && bs <= (int64_t)kFcRows && Co >= 1 && Ci >= 1 && Ci <= (int64_t)kFcMaxCi &&
-                  Co * Ci < (1ll << 31) && qmin < qmax, SSQ_E_ARG,
-              "ssq_fc_recon_iter: 1 <= batch <= %u, Ci <= %u", kFcRows, kFcMaxCi);
+                                 float* What, const float* delta, const float* zp, int qmin,
+                                 int qmax, const float* bias, int64_t Co, int64_t Ci,
+                                 float one_minus_beta1, float beta2, float one_minus_beta2,
+                                 float eps, float* exp_avg, float* exp_avg_sq, float* g,
+                                 float* gv_out, float* loss_out, void* ws, size_t ws_bytes,
+                                 ssq_stream_t stream) {
+  SSQ_REQUIRE(x_cache && tgt_cache && slot && W && V && What && delta && zp && exp_avg &&
+                  exp_avg_sq && g && loss_out, SSQ_E_ARG, "ssq_fc_recon_iter: null pointer");
+  SSQ_REQUIRE(bs >= 1 && bs <= (int64_t)kFcRows && Co >= 1 && Ci >= 64 && Ci % 64 == 0 &&
+                  Ci <= (int64_t)kFcMaxCi && Co * Ci < (1ll << 31) && qmin < qmax, SSQ_E_ARG,
+              "ssq_fc_recon_iter: 1 <= batch <= %u, 64 <= C_in <= %u, C_in %% 64 == 0", kFcRows,
+              kFcMaxCi);
+  auto al = [](const void* p) { return ((uintptr_t)p & 15u) == 0; };
+  SSQ_REQUIRE(al(x_cache) && al(What), SSQ_E_ARG, "ssq_fc_recon_iter: 16-B aligned x / W^");
   SSQ_REQUIRE(ws && ws_bytes >= ssq_fc_recon_workspace_size(Co, Ci, bs), SSQ_E_WS,
               "ssq_fc_recon_iter: workspace too small");
   hipStream_t s = (hipStream_t)stream;
-  const uint32_t nf = (uint32_t)((Co + kFcCo - 1) / kFcCo);
+  // K chunk per wave: C_in / 8 rounded up to whole 64-k rounds
+  const uint32_t ck = (uint32_t)(((Ci + kFcKW - 1) / kFcKW + 63) / 64 * 64);
+  const dim3 gf((unsigned)((Co + 15) / 16), (unsigned)((bs + 15) / 16));
   double* part = (double*)ws;
   // the slot: bs indices, then (lambda, b) and Adam's (-lr/bc1, sqrt(bc2)) as fp32 pairs
   const float* words = (const float*)(slot + bs);
-  hipLaunchKernelGGL(fc_fwd_loss, dim3(nf), dim3(kBlock), 0, s, x_cache, slot, (uint32_t)bs, W, V,
-                     delta, zp, (float)qmin, (float)qmax, bias, (uint32_t)Co, (uint32_t)Ci,
-                     tgt_cache, 1.0f / (float)bs, g, part);
+  hipLaunchKernelGGL(fc_fwd_loss, gf, dim3(kWave * kFcKW), 0, s, x_cache, slot, (uint32_t)bs,
+                     What, bias, (uint32_t)Co, (uint32_t)Ci, ck, tgt_cache, 1.0f / (float)bs, g,
+                     part);
   int rc = check_launch("ssq_fc_recon_iter (forward)");
   if (rc) return rc;
-  const uint32_t nb = (uint32_t)((Co + kFcBwdCo - 1) / kFcBwdCo);
-  const size_t lds = ((size_t)bs * Ci + (size_t)bs * kFcBwdCo) * sizeof(float);
-  SSQ_REQUIRE(lds <= 160 * 1024, SSQ_E_ARG, "ssq_fc_recon_iter: batch x Ci exceeds the LDS");
-  static bool attr = false;
-  if (!attr) {
-    hipFuncSetAttribute((const void*)fc_bwd_adam, hipFuncAttributeMaxDynamicSharedMemorySize,
-                        160 * 1024);
-    attr = true;
-  }
+  const uint32_t ntile = (uint32_t)(((Co + 15) / 16) * (Ci / 16));
   const AdamConst ac{one_minus_beta1, beta2, one_minus_beta2, eps, words + 2};
-  hipLaunchKernelGGL(fc_bwd_adam, dim3(nb), dim3(kBlock), lds, s, x_cache, slot, (uint32_t)bs, g, W,
-                     V, delta, zp, (float)qmin, (float)qmax, (uint32_t)Co, (uint32_t)Ci, words, ac,
-                     exp_avg, exp_avg_sq, gv_out, part, nf, (double)bs, loss_out);
-  return check_launch("ssq_fc_recon_iter (backward + Adam)");
+  hipLaunchKernelGGL(fc_bwd_adam, dim3(ntile), dim3(kWave * kFcBwdW), 0,
+                     s, x_cache, slot, (uint32_t)bs, g, W, V, delta, zp, (float)qmin, (float)qmax,
+                     (uint32_t)Co, (uint32_t)Ci, words, ac, exp_avg, exp_avg_sq, gv_out, What,
+                     part, gf.x * gf.y, (double)bs, loss_out);
+  return check_launch("ssq_fc_recon_iter (backward + Adam + next W^)");
 }

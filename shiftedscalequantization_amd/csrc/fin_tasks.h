@@ -49,14 +49,20 @@ struct AdamRef {
   float* m;
   float* v;
 };
-// the update of one entry from its loaded (p, m, v)
-__device__ __forceinline__ void adam_apply_loaded(const AdamConst& c, const AdamRef& r, uint32_t e,
-                                                  float g, float p, float m, float v) {
+// the update of one entry: (p, m, v) -> the new values, in place
+__device__ __forceinline__ void adam_update(const AdamConst& c, float g, float& p, float& m,
+                                            float& v) {
   const float nss = c.hyper[0], bc2s = c.hyper[1];
   m = __fadd_rn(m, __fmul_rn(c.w1, __fsub_rn(g, m)));
   v = __fadd_rn(__fmul_rn(v, c.b2), __fmul_rn(__fmul_rn(c.w2, g), g));
   const float denom = __fadd_rn(__fdiv_rn(__fsqrt_rn(v), bc2s), c.eps);
-  r.p[e] = __fadd_rn(p, __fdiv_rn(__fmul_rn(nss, m), denom));
+  p = __fadd_rn(p, __fdiv_rn(__fmul_rn(nss, m), denom));
+}
+// the update of one entry from its loaded (p, m, v)
+__device__ __forceinline__ void adam_apply_loaded(const AdamConst& c, const AdamRef& r, uint32_t e,
+                                                  float g, float p, float m, float v) {
+  adam_update(c, g, p, m, v);
+  r.p[e] = p;
   r.m[e] = m;
   r.v[e] = v;
 }

@@ -1485,11 +1485,12 @@ def adam_step(params, grads, exp_avgs, exp_avg_sqs, beta1, beta2, eps, hyper=Non
          float(eps), _vp(hyper), float(neg_step_size), float(bc2_sqrt), stream_of(params[0]))
 
 
-def fc_recon_iter(x_cache, tgt_cache, slot, bs, w, v, delta, zp, n_bits, bias, exp_avg,
+def fc_recon_iter(x_cache, tgt_cache, slot, bs, w, v, what, delta, zp, n_bits, bias, exp_avg,
                   exp_avg_sq, beta1, beta2, eps, g=None, gv_out=None, loss_out=None):
     """One fused BRECQ AdaRound iteration of a Linear layer (ssq_fc_recon_iter, K19): the
-    forward with W^ = AdaRound(w, v) on the fly, the p = 2 loss and its gradient, then dW,
-    V's gradient with the rounding regulariser and V's Adam step, in two launches.  slot:
+    forward on what = AdaRound(w, v) (the first call's from adaround(), every later one's
+    written by the previous call), the p = 2 loss and its gradient, then dW, V's gradient
+    with the rounding regulariser, V's Adam step and the next what, in two launches.  slot:
     int64 device words (bs indices, then (lambda, b, -lr/bc1, sqrt(bc2)) as fp32).
     Returns (loss, g)."""
     xc, xp = fptr(x_cache, "x cache")
@@ -1498,7 +1499,8 @@ def fc_recon_iter(x_cache, tgt_cache, slot, bs, w, v, delta, zp, n_bits, bias, e
     if xc.shape[1:].numel() != Ci or tc.shape[1:].numel() != Co or slot.dtype != torch.int64 \
             or not slot.is_contiguous() or slot.numel() < bs + 2:
         raise A.SSQError("fc_recon_iter: shapes / slot")
-    for t, nm in ((w, "weight"), (v, "V"), (exp_avg, "exp_avg"), (exp_avg_sq, "exp_avg_sq")):
+    for t, nm in ((w, "weight"), (v, "V"), (what, "W^"), (exp_avg, "exp_avg"),
+                  (exp_avg_sq, "exp_avg_sq")):
         A.check(t, nm)
         if not t.is_contiguous() or t.numel() != Co * Ci:
             raise A.SSQError(f"fc_recon_iter: {nm} must be contiguous [Co, Ci]")
@@ -1509,7 +1511,7 @@ def fc_recon_iter(x_cache, tgt_cache, slot, bs, w, v, delta, zp, n_bits, bias, e
     g = torch.empty(bs, Co, device=dev_) if g is None else g
     loss = torch.empty(1, device=dev_) if loss_out is None else loss_out
     ws, wsn = workspace(query("ssq_fc_recon_workspace_size", Co, Ci, bs), dev_, "fc")
-    call("ssq_fc_recon_iter", xp, tp, _vp(slot), bs, _vp(w), _vp(v), dp, zpp, 0,
+    call("ssq_fc_recon_iter", xp, tp, _vp(slot), bs, _vp(w), _vp(v), _vp(what), dp, zpp, 0,
          2 ** n_bits - 1, bp, Co, Ci, float(1 - beta1), float(beta2), float(1 - beta2),
          float(eps), _vp(exp_avg), _vp(exp_avg_sq), _vp(g), _vp(gv_out), _vp(loss), ws, wsn,
          stream_of(w))

@@ -192,9 +192,11 @@ FUSE_FC = _FAST and os.environ.get("SSQ_FUSE_FC", "1") != "0"
 def _fc_fused_body(layer, qmodules, act_quant, p, bucket, feeder, optimizer, last):
     """The fused fc iteration's body, or None when the loop is not one it covers: a
     Linear QuantModule alone, soft AdaRound with per-row delta, no activation, no act
-    quantizer, no gamma^z / phi^z affine, p = 2, world 1, batch <= 64, C_in <= 4096."""
+    quantizer, no gamma^z / phi^z affine, p = 2, world 1, batch <= 64, C_in a multiple of 64
+    up to 4096."""
     import torch.nn.functional as F
     if not (FUSE_FC and not act_quant and bucket is None and float(p) == 2.0
+            and ITER_PROBE[0] is None      # a probe may rewrite V: W^ is carried over
             and len(qmodules) == 1 and qmodules[0] is layer and isinstance(layer, QuantModule)):
         return None
     m = layer
@@ -213,7 +215,8 @@ def _fc_fused_body(layer, qmodules, act_quant, p, bucket, feeder, optimizer, las
             and q.delta.numel() == Co and q.zero_point.numel() == Co
             and feeder.inp.dim() == 2 and feeder.inp.shape[1] == Ci
             and feeder.out.dim() == 2 and feeder.out.shape[1] == Co
-            and 1 <= feeder.bs <= 64 and Ci <= 4096 and feeder.bs * Ci * 4 <= 96 * 1024):
+            and 1 <= feeder.bs <= 64 and Ci % 64 == 0 and 64 <= Ci <= 4096
+            and feeder.inp.data_ptr() % 16 == 0):
         return None
     if optimizer.params != [v]:
         return None
@@ -222,12 +225,15 @@ def _fc_fused_body(layer, qmodules, act_quant, p, bucket, feeder, optimizer, las
     eps = optimizer.param_groups[0]["eps"]
     bias = m.bias if (m.bias is None or m.train_bias) else m.bias.detach()
     gbuf = torch.empty(feeder.bs, Co, device=w.device)
-    gv = torch.zeros_like(v)        # V's gradient, for anyone reading .grad (test probes)
+    gv = torch.zeros_like(v)        # V's gradient, for anyone reading .grad
+    # W^ of the first iteration (every later one is written by the previous iteration)
+    with torch.no_grad():
+        what = K.adaround(v, w, q.delta, q.zero_point, q.n_bits, False, False).detach().clone()
 
     def body():
         src = feeder.chunk_dev[feeder.slot] if feeder.slot is not None else feeder._dev
         loss, _ = K.fc_recon_iter(feeder.inp, feeder.out, src, feeder.bs, w.detach(), v.data,
-                                  q.delta, q.zero_point, q.n_bits, bias, st["exp_avg"],
+                                  what, q.delta, q.zero_point, q.n_bits, bias, st["exp_avg"],
                                   st["exp_avg_sq"], b1, b2, eps, g=gbuf, gv_out=gv)
         v.grad = gv
         last['rec'] = loss

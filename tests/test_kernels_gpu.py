@@ -1631,7 +1631,8 @@ def test_epilogue_bwd_delta_split_two_streams(K, defer):
                 np.testing.assert_array_equal(x, b)
 
 
-@pytest.mark.parametrize("bs,Co,Ci,lam", [(32, 1000, 512, 0.01), (8, 10, 32, 0.0), (64, 37, 300, 0.01)])
+@pytest.mark.parametrize("bs,Co,Ci,lam", [(32, 1000, 512, 0.01), (8, 10, 64, 0.0), (64, 37, 320, 0.01),
+                                          (33, 70, 256, 0.01), (1, 16, 4096, 0.01)])
 def test_fc_recon_iter_vs_reference(K, bs, Co, Ci, lam):
     """K19 ssq_fc_recon_iter, one iteration against its parts: the loss and dL/dy against the
     float64 evaluation of x[idx] W^T + bias with W^ the AdaRound forward (bit-exact kernel);
@@ -1656,10 +1657,16 @@ def test_fc_recon_iter_vs_reference(K, bs, Co, Ci, lam):
     slot = slot.cuda()
     v0, m0, s0 = v.clone(), m.clone(), s2.clone()
     gv = torch.empty_like(v)
-    loss, g = K.fc_recon_iter(x, tgt, slot, bs, w, v, d, z, 8, bias, m, s2, 0.9, 0.999, 1e-8, gv_out=gv)
+    what_in = K.adaround(v0, w, d, z, 8, False, False).detach().clone()
+    what_buf = what_in.clone()
+    loss, g = K.fc_recon_iter(x, tgt, slot, bs, w, v, what_buf, d, z, 8, bias, m, s2, 0.9, 0.999,
+                              1e-8, gv_out=gv)
     torch.cuda.synchronize()
+    # the next iteration's W^: ssq_adaround_fwd of the updated V, bit for bit
+    np.testing.assert_array_equal(host(what_buf).view(np.int32),
+                                  host(K.adaround(v, w, d, z, 8, False, False)).view(np.int32))
     # float64 truth of the forward / loss / gradient
-    what = K.adaround(v0, w, d, z, 8, False, False).detach().double()
+    what = what_in.double()
     xb, tb = x[idx.cuda()].double(), tgt[idx.cuda()].double()
     y = xb @ what.t() + bias.double()
     ref_loss = ((y - tb) ** 2).sum(1).mean().item()

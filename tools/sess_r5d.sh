@@ -6,7 +6,7 @@ R=${GRAFT_REPO_ROOT:-$(pwd)}
 OUT=$R/gpurun_out
 mkdir -p $OUT
 cd $R
-bash tools/sess_tests.sh $TAG "into_gemm or fc_ or chunked or frozen_loop or real_layer_shift or layer_reconstruction"
+bash tools/sess_tests.sh $TAG "${2:-into_gemm or fc_ or chunked or frozen_loop or real_layer_shift or layer_reconstruction}"
 rc=$?
 [ $rc -gt 1 ] && exit $rc
 for V in "0 25" "1 1" "1 25"; do
