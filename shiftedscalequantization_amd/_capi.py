@@ -89,6 +89,13 @@ SIGNATURES = {
     "ssq_epilogue_loss_bwd": (_i, [_p, _p, _i64, _f, _p, _p, _p, _p, _p, _p, _p, _p, _p, _i64,
                                    _i64, _i64, _i, _p, _p, _i, _i, _p, _p, _p, _p, _p, _p, _p,
                                    _p, _p, _sz, _p]),
+    "ssq_epilogue_fwd_rows": (_i, [_p, _p, _p, _p, _p, _p, _p, _p, _i64, _i64, _i64, _i, _p, _p,
+                                   _i, _i, _p]),
+    "ssq_epilogue_bwd_rows": (_i, [_p, _p, _p, _p, _p, _p, _p, _p, _i64, _i64, _i64, _i, _p, _p,
+                                   _i, _i, _p, _p, _p, _p, _p, _p, _p, _sz, _p]),
+    "ssq_epilogue_loss_bwd_rows": (_i, [_p, _p, _i64, _f, _p, _p, _p, _p, _p, _p, _p, _p, _p, _p,
+                                        _p, _i64, _i64, _i64, _i, _p, _p, _i, _i, _p, _p, _p, _p,
+                                        _p, _p, _p, _p, _p, _sz, _p]),
     "ssq_adam": (_i, [_i, _p, _p, _p, _p, _p, _f, _f, _f, _f, _p, _f, _f, _p]),
     "ssq_adam_arm": (_i, [_i, _p, _p, _p, _p, _f, _f, _f, _f, _p, _p]),
     "ssq_adam_take": (_i, [_p]),
@@ -167,11 +174,29 @@ def ptr(t):
     return None if t is None else C.c_void_p(t.data_ptr())
 
 
+# In-place row views (kernels.rows_view): data_ptr of a batch buffer -> (buffer, cache, idx)
+# while the buffer stands for cache[idx] without having been gathered.
+ROW_VIEWS = {}
+
+
+def materialize_rows(t):
+    """Gather a registered row view into its buffer (one ssq_gather_rows2) and unregister it;
+    a no-op for any other tensor."""
+    e = ROW_VIEWS.pop(t.data_ptr(), None)
+    if e is not None:
+        buf, cache, idx = e
+        call("ssq_gather_rows2", ptr(cache), ptr(buf), cache[0].numel(), None, None, 0, ptr(idx),
+             idx.numel(), stream_of(buf))
+
+
 def fptr(t, name="tensor"):
-    """Device pointer of a contiguous fp32 tensor (made contiguous if needed)."""
+    """Device pointer of a contiguous fp32 tensor (made contiguous if needed).  A row view
+    is gathered first: a kernel that does not read the rows in place sees the batch."""
     if t is None:
         return None, None
     check(t, name)
+    if ROW_VIEWS:
+        materialize_rows(t)
     t = t.contiguous()
     return t, C.c_void_p(t.data_ptr())
 

@@ -100,7 +100,9 @@ __global__ void lp_loss_finalize(const double* __restrict__ part, int nblk, doub
 // ------------------------------------------------------------------ K13 fused epilogue
 // out = act(y + bias[c] (+ res)),  c = (i / hw) % C, in the reference's op order (conv
 // bias add, residual add, ReLU: three separate fp32 roundings -> bit-identical to the
-// eager sequence), one pass instead of three.
+// eager sequence), one pass instead of three.  yrows (optional): y is a cache of per-sample
+// [C, hw] rows and sample n of this batch is its row yrows[n] (BRECQ's act phase reads the
+// frozen conv's precomputed outputs in place instead of a gathered copy).
 template <bool RES, int ACT, bool QUANT, bool AFFINE>
 __global__ __launch_bounds__(kBlock) void bias_act_kernel(const float* __restrict__ y,
                                                           const float* __restrict__ bias,
@@ -113,9 +115,17 @@ __global__ __launch_bounds__(kBlock) void bias_act_kernel(const float* __restric
                                                           const float* __restrict__ qzp,
                                                           float qlo, float qhi,
                                                           const float* __restrict__ gamma,
-                                                          const float* __restrict__ phi) {
+                                                          const float* __restrict__ phi,
+                                                          const int64_t* __restrict__ yrows,
+                                                          uint32_t chw) {
   const uint32_t stride = gridDim.x * blockDim.x;
   QParams qp{1.0f, 0.0f, qlo, qhi};
+  // element i of the batch -> its offset in y (yrows: sample n = i / chw is row yrows[n])
+  auto yoff = [&](uint32_t i) -> int64_t {
+    if (!yrows) return (int64_t)i;
+    const uint32_t nn = fdiv(fdiv(i, div_hw), div_c);
+    return yrows[nn] * (int64_t)chw + (int64_t)(i - nn * chw);
+  };
   if (QUANT) {
     qp.d = qdelta[0];
     qp.z = qzp[0];
@@ -135,7 +145,7 @@ __global__ __launch_bounds__(kBlock) void bias_act_kernel(const float* __restric
   if (vec) {
     const uint32_t n4 = n / 4;
     for (uint32_t v = blockIdx.x * blockDim.x + threadIdx.x; v < n4; v += stride) {
-      const f32x4 a = ((const f32x4*)y)[v];
+      const f32x4 a = *(const f32x4*)(y + yoff(4 * v));   // hw % 4 == 0 with yrows
       f32x4 rr = {0.0f, 0.0f, 0.0f, 0.0f};
       if (RES) rr = ((const f32x4*)res)[v];
       f32x4 o;
@@ -155,7 +165,7 @@ __global__ __launch_bounds__(kBlock) void bias_act_kernel(const float* __restric
     }
   } else {
     for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
-      const float t = one(i, y[i], RES ? res[i] : 0.0f);
+      const float t = one(i, y[yoff(i)], RES ? res[i] : 0.0f);
       if (!QUANT || out) out[i] = t;
       if (QUANT) yq[i] = fq(t);
     }
@@ -365,7 +375,8 @@ __device__ __forceinline__ double epilogue_rows_body(
     uint32_t rows, uint32_t C, uint32_t hw, const float* __restrict__ qdelta,
     const float* __restrict__ qzp, float lo, float hi, float* __restrict__ gy,
     float* __restrict__ gres, double* __restrict__ part, const int64_t* __restrict__ lidx,
-    float inv_m, float lp, const ResEpi& re, uint32_t bid) {
+    float inv_m, float lp, const ResEpi& re, uint32_t bid, const int64_t* __restrict__ yrows,
+    const int64_t* __restrict__ rrows) {
   const uint32_t lane = threadIdx.x & (kWave - 1);
   const uint32_t r0 = (bid * (kBlock / kWave) + threadIdx.x / kWave) * RPW;
   if (r0 >= rows) return 0.0;
@@ -387,17 +398,20 @@ __device__ __forceinline__ double epilogue_rows_body(
     if (bias) epi_elem<RES, ACT, QUANT, AFFINE, LOSS, true>(wr, d, z, lo, hi, inv_m, lp, rbias, raffine, yv, gv, rv, oy, orr);
     else epi_elem<RES, ACT, QUANT, AFFINE, LOSS, false>(wr, d, z, lo, hi, inv_m, lp, rbias, raffine, yv, gv, rv, oy, orr);
   };
-  // LOSS: row (n, c)'s target is row c of cached sample idx[n] ([*, C, hw] cache)
-  auto gbase_of = [&](uint32_t r) -> int64_t {
-    return LOSS ? (lidx[r / C] * (int64_t)C + r % C) * hw : (int64_t)r * hw;
+  // row r = (n, c) of a [*, C, hw] cache read through a row map: row c of cached sample
+  // map[n] (LOSS: the target; yrows / rrows: y / res read in place from a cache)
+  auto mapped = [&](const int64_t* map, uint32_t r) -> int64_t {
+    return map ? (map[r / C] * (int64_t)C + r % C) * hw : (int64_t)r * hw;
   };
+  auto gbase_of = [&](uint32_t r) -> int64_t { return mapped(LOSS ? lidx : nullptr, r); };
   if (RPW == 1) {
     EpiRow& wr = w[0];
     const int64_t base = (int64_t)r0 * hw, gbase = gbase_of(r0);
+    const int64_t ybase = mapped(yrows, r0), rbase = mapped(rrows, r0);
     if (VEC) {
-      const f32x4* Y = (const f32x4*)(y + base);
+      const f32x4* Y = (const f32x4*)(y + ybase);
       const f32x4* G = (const f32x4*)(g + gbase);
-      const f32x4* R = RES ? (const f32x4*)(res + base) : nullptr;
+      const f32x4* R = RES ? (const f32x4*)(res + rbase) : nullptr;
       f32x4* GY = gy ? (f32x4*)(gy + base) : nullptr;
       f32x4* GR = gres ? (f32x4*)(gres + base) : nullptr;
       for (uint32_t v = lane; v < hw / 4; v += kWave) {
@@ -415,7 +429,7 @@ __device__ __forceinline__ double epilogue_rows_body(
     } else {
       for (uint32_t j = lane; j < hw; j += kWave) {
         float oy, orr;
-        elem(wr, y[base + j], g[gbase + j], RES ? res[base + j] : 0.0f, oy, orr);
+        elem(wr, y[ybase + j], g[gbase + j], RES ? res[rbase + j] : 0.0f, oy, orr);
         if (gy) gy[base + j] = oy;
         if (gres) gres[base + j] = orr;
       }
@@ -433,9 +447,9 @@ __device__ __forceinline__ double epilogue_rows_body(
     for (int k = 0; k < RPW; ++k) {
       yv[k] = gv[k] = rv[k] = f32x4{0.0f, 0.0f, 0.0f, 0.0f};
       if (on && r0 + k < rows) {
-        yv[k] = ((const f32x4*)(y + (int64_t)(r0 + k) * hw))[lane];
+        yv[k] = ((const f32x4*)(y + mapped(yrows, r0 + k)))[lane];
         gv[k] = ((const f32x4*)(g + gbase_of(r0 + k)))[lane];
-        if (RES) rv[k] = ((const f32x4*)(res + (int64_t)(r0 + k) * hw))[lane];
+        if (RES) rv[k] = ((const f32x4*)(res + mapped(rrows, r0 + k)))[lane];
       }
     }
 #pragma unroll
@@ -460,9 +474,9 @@ __device__ __forceinline__ double epilogue_rows_body(
     for (int k = 0; k < RPW; ++k) {
       yv[k] = gv[k] = rv[k] = 0.0f;
       if (on && r0 + k < rows) {
-        yv[k] = y[(int64_t)(r0 + k) * hw + lane];
+        yv[k] = y[mapped(yrows, r0 + k) + lane];
         gv[k] = g[gbase_of(r0 + k) + lane];
-        if (RES) rv[k] = res[(int64_t)(r0 + k) * hw + lane];
+        if (RES) rv[k] = res[mapped(rrows, r0 + k) + lane];
       }
     }
 #pragma unroll
@@ -489,7 +503,8 @@ __global__ __launch_bounds__(kBlock) void epilogue_bwd_rows(
     uint32_t rows, uint32_t C, uint32_t hw, const float* __restrict__ qdelta,
     const float* __restrict__ qzp, float lo, float hi, float* __restrict__ gy,
     float* __restrict__ gres, double* __restrict__ part, FinTable fin, uint32_t nmain,
-    const int64_t* __restrict__ lidx, float inv_m, float lp, ResEpi re) {
+    const int64_t* __restrict__ lidx, float inv_m, float lp, ResEpi re,
+    const int64_t* __restrict__ yrows, const int64_t* __restrict__ rrows) {
   // queued finalize tasks ride on this launch: its first workgroups (dispatched first, so
   // they run beside the main work instead of after it)
   (void)nmain;
@@ -505,7 +520,7 @@ __global__ __launch_bounds__(kBlock) void epilogue_bwd_rows(
                        __HIP_MEMORY_SCOPE_AGENT);
   const double wl = epilogue_rows_body<RES, ACT, QUANT, AFFINE, VEC, LOSS, RPW>(
       g, y, bias, gamma, phi, res, rows, C, hw, qdelta, qzp, lo, hi, gy, gres, part, lidx, inv_m,
-      lp, re, bid);
+      lp, re, bid, yrows, rrows);
   if (!LOSS) return;
   // the fused tail's loss: one partial per workgroup (its waves in order) after the rows'
   // records, so the finalize sums rows / (4 RPW) values instead of every row's
@@ -840,7 +855,8 @@ static int epi_multi_row() {
 static int bias_act(const char* what, const float* y, const float* bias, const float* res,
                     float* out, float* yq, int64_t n, int64_t hw, int64_t C, int relu,
                     const float* qdelta, const float* qzp, int qmin, int qmax, hipStream_t s,
-                    const float* gamma = nullptr, const float* phi = nullptr) {
+                    const float* gamma = nullptr, const float* phi = nullptr,
+                    const int64_t* yrows = nullptr) {
   SSQ_REQUIRE(!gamma == !phi, SSQ_E_ARG, "%s: gamma and phi go together", what);
   SSQ_REQUIRE(y && n >= 0 && hw >= 1 && C >= 1, SSQ_E_ARG, "%s: bad args", what);
   SSQ_REQUIRE(yq ? (qdelta && qzp && qmin < qmax) : out != nullptr, SSQ_E_ARG, "%s: bad outputs",
@@ -849,13 +865,17 @@ static int bias_act(const char* what, const float* y, const float* bias, const f
               "%s: tensor exceeds 2^31 elements", what);
   if (n == 0) return SSQ_OK;
   auto al = [](const void* q) { return ((uintptr_t)q & 15u) == 0; };
-  const int vec = n % 4 == 0 && al(y) && (!out || al(out)) && (!res || al(res)) && (!yq || al(yq));
+  SSQ_REQUIRE(!yrows || n % (hw * C) == 0, SSQ_E_ARG, "%s: y rows need whole [C, hw] samples",
+              what);
+  const int vec = n % 4 == 0 && al(y) && (!out || al(out)) && (!res || al(res)) &&
+                  (!yq || al(yq)) && (!yrows || hw % 4 == 0);
   const FastDiv dh = make_fastdiv((uint32_t)hw), dc = make_fastdiv((uint32_t)C);
   const dim3 grid(grid_for(vec ? n / 4 : n, kBlock, 2048));
   const float lo = (float)qmin, hi = (float)qmax;
 #define SSQ_BA(R, A, Q, F)                                                                    \
   hipLaunchKernelGGL((bias_act_kernel<R, A, Q, F>), grid, dim3(kBlock), 0, s, y, bias, res, out, \
-                     (uint32_t)n, dh, dc, (uint32_t)C, vec, yq, qdelta, qzp, lo, hi, gamma, phi)
+                     (uint32_t)n, dh, dc, (uint32_t)C, vec, yq, qdelta, qzp, lo, hi, gamma, phi, \
+                     yrows, (uint32_t)(C * hw))
 #define SSQ_BA1(R, A, Q) \
   if (gamma) SSQ_BA(R, A, Q, true); else SSQ_BA(R, A, Q, false);
 #define SSQ_BA2(R, A) \
@@ -895,6 +915,16 @@ extern "C" int ssq_epilogue_fwd(const float* y, const float* bias, const float* 
                   qmax, (hipStream_t)stream, gamma, phi);
 }
 
+extern "C" int ssq_epilogue_fwd_rows(const float* y_cache, const int64_t* y_rows,
+                                     const float* bias, const float* gamma, const float* phi,
+                                     const float* res, float* out, float* yq, int64_t n,
+                                     int64_t hw, int64_t C, int relu, const float* delta,
+                                     const float* zp, int qmin, int qmax, ssq_stream_t stream) {
+  SSQ_REQUIRE(y_rows, SSQ_E_ARG, "ssq_epilogue_fwd_rows: y_rows is required");
+  return bias_act("ssq_epilogue_fwd_rows", y_cache, bias, res, out, yq, n, hw, C, relu, delta,
+                  zp, qmin, qmax, (hipStream_t)stream, gamma, phi, y_rows);
+}
+
 extern "C" size_t ssq_epilogue_bwd_workspace_size(int64_t rows) {
   // the rows' records, then (fused tail) one loss partial per workgroup: <= ceil(rows / 4),
   // then the delta reduction's workgroup partials and its counter (fin_epi)
@@ -910,7 +940,8 @@ static int epilogue_bwd(const char* what, const float* g, const float* y, const 
                         const float* zp, int qmin, int qmax, const int64_t* lidx, int64_t M,
                         float lp, float* loss_out, float* gy, float* gres, float* ggamma,
                         float* gphi, float* grgamma, float* grphi, float* gdelta, float* gzp,
-                        void* ws, size_t ws_bytes, hipStream_t s) {
+                        void* ws, size_t ws_bytes, hipStream_t s,
+                        const int64_t* yrows = nullptr, const int64_t* rrows = nullptr) {
   const bool loss = lidx != nullptr;
   // the residual's own epilogue folded in (fused tail only)
   const bool res2 = res && (re.bias || re.gamma);
@@ -955,7 +986,7 @@ static int epilogue_bwd(const char* what, const float* g, const float* y, const 
 #define SSQ_EB0(R, A, Q, F, V, L, P)                                                              \
   hipLaunchKernelGGL((epilogue_bwd_rows<R, A, Q, F, V, L, P>), grid, dim3(kBlock), 0, s, g, y,    \
                      bias, gamma, phi, res, (uint32_t)rows, (uint32_t)C, (uint32_t)hw, delta, zp, \
-                     lo, hi, gy, gres, part, fin, nmain, lidx, inv_m, lp, re2)
+                     lo, hi, gy, gres, part, fin, nmain, lidx, inv_m, lp, re2, yrows, rrows)
 #define SSQ_EB(R, A, Q, F, V, L) \
   if (multi) SSQ_EB0(R, A, Q, F, V, L, ((Q) ? 1 : 4)); else SSQ_EB0(R, A, Q, F, V, L, 1);
 #define SSQ_EBL(R, A, Q, F, V) \
@@ -1095,6 +1126,38 @@ extern "C" int ssq_epilogue_loss_bwd(const float* tgt_cache, const int64_t* idx,
                       ResEpi{res_bias, res_gamma, res_phi}, N, C, hw, relu, delta, zp, qmin, qmax,
                       idx, M, p, loss_out, gy, gres, ggamma, gphi, gres_gamma, gres_phi, gdelta,
                       gzp, ws, ws_bytes, (hipStream_t)stream);
+}
+
+// the two above with y and / or res read in place from per-sample row caches (y_rows /
+// res_rows: this batch's rows of y / res; either may be null = y / res are the batch itself)
+extern "C" int ssq_epilogue_bwd_rows(const float* g, const float* y, const int64_t* y_rows,
+                                     const float* bias, const float* gamma, const float* phi,
+                                     const float* res, const int64_t* res_rows, int64_t N,
+                                     int64_t C, int64_t hw, int relu, const float* delta,
+                                     const float* zp, int qmin, int qmax, float* gy, float* gres,
+                                     float* ggamma, float* gphi, float* gdelta, float* gzp,
+                                     void* ws, size_t ws_bytes, ssq_stream_t stream) {
+  SSQ_REQUIRE(!res_rows || res, SSQ_E_ARG, "ssq_epilogue_bwd_rows: res_rows without res");
+  return epilogue_bwd("ssq_epilogue_bwd_rows", g, y, bias, gamma, phi, res,
+                      ResEpi{nullptr, nullptr, nullptr}, N, C, hw, relu, delta, zp, qmin, qmax,
+                      nullptr, 0, 2.0f, nullptr, gy, gres, ggamma, gphi, nullptr, nullptr, gdelta,
+                      gzp, ws, ws_bytes, (hipStream_t)stream, y_rows, res_rows);
+}
+
+extern "C" int ssq_epilogue_loss_bwd_rows(
+    const float* tgt_cache, const int64_t* idx, int64_t M, float p, float* loss_out,
+    const float* y, const int64_t* y_rows, const float* bias, const float* gamma,
+    const float* phi, const float* res, const int64_t* res_rows, const float* res_bias,
+    const float* res_gamma, const float* res_phi, int64_t N, int64_t C, int64_t hw, int relu,
+    const float* delta, const float* zp, int qmin, int qmax, float* gy, float* gres,
+    float* ggamma, float* gphi, float* gres_gamma, float* gres_phi, float* gdelta, float* gzp,
+    void* ws, size_t ws_bytes, ssq_stream_t stream) {
+  SSQ_REQUIRE(idx, SSQ_E_ARG, "ssq_epilogue_loss_bwd_rows: idx is required");
+  SSQ_REQUIRE(!res_rows || res, SSQ_E_ARG, "ssq_epilogue_loss_bwd_rows: res_rows without res");
+  return epilogue_bwd("ssq_epilogue_loss_bwd_rows", tgt_cache, y, bias, gamma, phi, res,
+                      ResEpi{res_bias, res_gamma, res_phi}, N, C, hw, relu, delta, zp, qmin, qmax,
+                      idx, M, p, loss_out, gy, gres, ggamma, gphi, gres_gamma, gres_phi, gdelta,
+                      gzp, ws, ws_bytes, (hipStream_t)stream, y_rows, res_rows);
 }
 
 template <int ACT>

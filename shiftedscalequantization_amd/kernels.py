@@ -874,6 +874,41 @@ class Rows:
         return gather_rows2(self.cache, self.idx)[0]
 
 
+# ------------------------------------------------------------------ in-place row views
+# BRECQ's act phase reads its frozen convs' precomputed outputs and the cached block input
+# by the batch indices (quant/block_recon.py ROWS_IN_PLACE).  Instead of gathering each into
+# a batch buffer, the buffer is registered as a view of cache[idx] (rows_view) and the K13
+# epilogue kernels read the rows in place (ssq_epilogue_*_rows, bit-identical to reading the
+# gathered batch).  Any other kernel call reaching the buffer through fptr gathers it first
+# (_capi.fptr), as does materialize(); the registry lives for one loop (row_views).
+def rows_view(buf, cache, idx):
+    """Register buf (a contiguous batch buffer, never read by torch ops while registered) as
+    cache[idx]; returns buf."""
+    if tuple(buf.shape) != (idx.numel(),) + tuple(cache.shape[1:]) or not buf.is_contiguous() \
+            or idx.dtype != torch.int64 or not cache.is_contiguous():
+        raise A.SSQError("rows_view: buffer, cache and indices do not match")
+    A.ROW_VIEWS[buf.data_ptr()] = (buf, cache, idx)
+    return buf
+
+
+def rows_of(t):
+    """(cache, idx) when t is a registered row view, else None."""
+    if t is None or not A.ROW_VIEWS:
+        return None
+    e = A.ROW_VIEWS.get(t.data_ptr())
+    return None if e is None or e[0].numel() != t.numel() else (e[1], e[2])
+
+
+class row_views:
+    """Context of a loop that registers row views: the registry is emptied on exit."""
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *exc):
+        A.ROW_VIEWS.clear()
+
+
 def lp_loss_and_grad(pred, tgt, p=2.0, reduction="none", want_grad=True, loss_out=None,
                      relu_mask=False):
     """lp_loss value (1-element device tensor) and d/d pred in one fused pass.  With
@@ -972,7 +1007,12 @@ class BiasActFn(torch.autograd.Function):
 
     @staticmethod
     def forward(ctx, y, bias, res, relu):
-        y, yp = fptr(y.detach(), "conv output")
+        yr = rows_of(y)
+        if yr is not None:
+            A.check(y, "conv output")
+            yp = _vp(yr[0])
+        else:
+            y, yp = fptr(y.detach(), "conv output")
         C = y.shape[1] if y.dim() > 1 else 1
         hw = y[0, 0].numel() if y.dim() > 2 else 1
         if bias is not None:
@@ -988,7 +1028,11 @@ class BiasActFn(torch.autograd.Function):
         else:
             rp = None
         out = torch.empty_like(y)
-        call("ssq_bias_act", yp, bp, rp, _vp(out), y.numel(), hw, C, int(relu), stream_of(y))
+        if yr is not None:
+            call("ssq_epilogue_fwd_rows", yp, _vp(yr[1]), bp, None, None, rp, _vp(out), None,
+                 y.numel(), hw, C, int(relu), None, None, 0, 1, stream_of(y))
+        else:
+            call("ssq_bias_act", yp, bp, rp, _vp(out), y.numel(), hw, C, int(relu), stream_of(y))
         ctx.relu = int(relu)
         if relu:
             ctx.save_for_backward(out)
@@ -1026,7 +1070,11 @@ class LazyRes:
 
 
 def materialize(res):
-    return res.materialize() if isinstance(res, LazyRes) else res
+    if isinstance(res, LazyRes):
+        return res.materialize()
+    if res is not None and A.ROW_VIEWS:
+        A.materialize_rows(res)
+    return res
 
 
 # A/B knob: the downsample branch's epilogue deferred into the block's fused tail (LazyRes;
@@ -1069,8 +1117,17 @@ def bias_act(y, bias=None, res=None, relu=True, lazy=False):
     return out
 
 
-def _epilogue_layout(y, bias, res):
-    y, yp = fptr(y.detach(), "conv output")
+def _epilogue_layout(y, bias, res, rows=False):
+    """Pointers and (C, hw) of an epilogue's operands.  rows: y / res may stay row views --
+    their pointers are then their caches' and ROWS holds (y_idx, res_idx) pointers (None for
+    an operand that is the batch itself); otherwise a row view is gathered (fptr)."""
+    yr = rows_of(y) if rows else None
+    rr = rows_of(res) if rows else None
+    if yr is not None:
+        A.check(y, "conv output")
+        yp = _vp(yr[0])
+    else:
+        y, yp = fptr(y.detach(), "conv output")
     C = y.shape[1] if y.dim() > 1 else 1
     hw = y[0, 0].numel() if y.dim() > 2 else 1
     bp = rp = None
@@ -1079,9 +1136,16 @@ def _epilogue_layout(y, bias, res):
         if bias.numel() != C:
             raise A.SSQError("bias_act: bias must have one value per channel")
     if res is not None:
-        res, rp = fptr(res.detach(), "residual")
+        if rr is not None:
+            A.check(res, "residual")
+            rp = _vp(rr[0])
+        else:
+            res, rp = fptr(res.detach(), "residual")
         if res.shape != y.shape:
             raise A.SSQError("bias_act: residual shape mismatch")
+    if rows:
+        return y, yp, bp, rp, C, hw, (bias, res), (None if yr is None else _vp(yr[1]),
+                                                   None if rr is None else _vp(rr[1]))
     return y, yp, bp, rp, C, hw, (bias, res)
 
 
@@ -1094,7 +1158,8 @@ class BiasActQuantFn(torch.autograd.Function):
 
     @staticmethod
     def forward(ctx, y, bias, res, delta, zp, relu, n_bits, sym, keep):
-        y, yp, bp, rp, C_, hw, hold = _epilogue_layout(y, bias, res)
+        materialize(res)
+        y, yp, bp, rp, C_, hw, hold, (yi, _) = _epilogue_layout(y, bias, res, rows=True)
         d, dp = fptr(delta.detach().reshape(-1), "delta")
         z, zpp = fptr(zp.detach().reshape(-1), "zero_point")
         if d.numel() != 1 or z.numel() != 1:
@@ -1102,8 +1167,12 @@ class BiasActQuantFn(torch.autograd.Function):
         lo, hi = qrange(n_bits, sym)
         out = torch.empty_like(y) if keep else None
         yq = torch.empty_like(y)
-        call("ssq_bias_act_fq", yp, bp, rp, _vp(out), _vp(yq), y.numel(), hw, C_, int(relu), dp,
-             zpp, lo, hi, stream_of(y))
+        if yi is not None:
+            call("ssq_epilogue_fwd_rows", yp, yi, bp, None, None, rp, _vp(out), _vp(yq), y.numel(),
+                 hw, C_, int(relu), dp, zpp, lo, hi, stream_of(y))
+        else:
+            call("ssq_bias_act_fq", yp, bp, rp, _vp(out), _vp(yq), y.numel(), hw, C_, int(relu),
+                 dp, zpp, lo, hi, stream_of(y))
         ctx.relu, ctx.q = int(relu), (lo, hi)
         if keep:
             ctx.save_for_backward(out, delta, zp)
@@ -1150,7 +1219,8 @@ class EpilogueFn(torch.autograd.Function):
 
     @staticmethod
     def forward(ctx, y, bias, gamma, phi, res, delta, zp, relu, n_bits, sym):
-        y, yp, bp, rp, C_, hw, _ = _epilogue_layout(y, bias, res)
+        materialize(res)
+        y, yp, bp, rp, C_, hw, _, (yi, _) = _epilogue_layout(y, bias, res, rows=True)
         gm, gmp = fptr(gamma.detach().reshape(-1), "gamma") if gamma is not None else (None, None)
         ph, php = fptr(phi.detach().reshape(-1), "phi") if phi is not None else (None, None)
         if gm is not None and (gm.numel() != C_ or ph.numel() != C_):
@@ -1166,9 +1236,14 @@ class EpilogueFn(torch.autograd.Function):
             dp = zpp = None
             lo, hi = 0, 1
         out = torch.empty_like(y)
-        call("ssq_epilogue_fwd", yp, bp, gmp, php, rp, None if quant else _vp(out),
-             _vp(out) if quant else None, y.numel(), hw, C_, int(relu), dp, zpp, lo, hi,
-             stream_of(y))
+        if yi is not None:
+            call("ssq_epilogue_fwd_rows", yp, yi, bp, gmp, php, rp, None if quant else _vp(out),
+                 _vp(out) if quant else None, y.numel(), hw, C_, int(relu), dp, zpp, lo, hi,
+                 stream_of(y))
+        else:
+            call("ssq_epilogue_fwd", yp, bp, gmp, php, rp, None if quant else _vp(out),
+                 _vp(out) if quant else None, y.numel(), hw, C_, int(relu), dp, zpp, lo, hi,
+                 stream_of(y))
         ctx.cfg = (int(relu), lo, hi, quant, C_, hw)
         ctx.save_for_backward(y, bias, gamma, phi, res, delta, zp)
         return out
@@ -1191,6 +1266,7 @@ def _epilogue_backward(g, y, bias, gamma, phi, res, delta, zp, relu, lo, hi, qua
         return None if t is None else t.detach().reshape(-1).contiguous()
     b, gm, ph, r = flat(bias), flat(gamma), flat(phi), res
     d, z = flat(delta), flat(zp)
+    yr, rr = rows_of(y), rows_of(r)
     gy = torch.empty_like(g) if need[0] else None
     gres = torch.empty_like(g) if (res is not None and need[4]) else None
     ggm, gm_into = _grad_dest(gamma, C_, dev_, need[2])
@@ -1200,10 +1276,17 @@ def _epilogue_backward(g, y, bias, gamma, phi, res, delta, zp, relu, lo, hi, qua
     N = g.numel() // (C_ * hw)
     # two alternating slots: a queued finalize of the previous call still reads its own
     ws, wsn = workspace(query("ssq_epilogue_bwd_workspace_size", N * C_), dev_, _epi_slot())
-    call("ssq_epilogue_bwd", gp, _vp(y), _vp(b), _vp(gm), _vp(ph),
-         _vp(r.contiguous() if r is not None else None), N, C_, hw, int(relu), _vp(d), _vp(z),
-         lo, hi, _vp(gy), _vp(gres), _vp(ggm), _vp(gph), _vp(gd), _vp(gz), ws, wsn,
-         stream_of(g))
+    if yr is not None or rr is not None:
+        call("ssq_epilogue_bwd_rows", gp, _vp(y if yr is None else yr[0]),
+             None if yr is None else _vp(yr[1]), _vp(b), _vp(gm), _vp(ph),
+             _vp(r.contiguous() if (r is not None and rr is None) else (rr[0] if rr else None)),
+             None if rr is None else _vp(rr[1]), N, C_, hw, int(relu), _vp(d), _vp(z), lo, hi,
+             _vp(gy), _vp(gres), _vp(ggm), _vp(gph), _vp(gd), _vp(gz), ws, wsn, stream_of(g))
+    else:
+        call("ssq_epilogue_bwd", gp, _vp(y), _vp(b), _vp(gm), _vp(ph),
+             _vp(r.contiguous() if r is not None else None), N, C_, hw, int(relu), _vp(d),
+             _vp(z), lo, hi, _vp(gy), _vp(gres), _vp(ggm), _vp(gph), _vp(gd), _vp(gz), ws, wsn,
+             stream_of(g))
     shape = (lambda t, o: None if o is None else o.view(t.shape))
     return (gy if need[0] else None, None, None if gm_into else shape(gamma, ggm),
             None if ph_into else shape(phi, gph), gres, shape(delta, gd), shape(zp, gz), None,
@@ -1420,7 +1503,7 @@ def epilogue_loss_bwd(tail, tgt, M, p=2.0):
     lres = res if isinstance(res, LazyRes) else None
     if lres is not None:
         res = lres.y
-    y, yp, bp, rp, C_, hw, _ = _epilogue_layout(y, bias, res)
+    y, yp, bp, rp, C_, hw, _, (yi, ri) = _epilogue_layout(y, bias, res, rows=True)
     dev_ = y.device
     cache, cp = fptr(tgt.cache.detach(), "tgt cache")
     idx = tgt.idx
@@ -1457,10 +1540,16 @@ def epilogue_loss_bwd(tail, tgt, M, p=2.0):
     gd = torch.empty(1, device=dev_) if (q is not None and q.delta.requires_grad) else None
     gz = torch.empty(1, device=dev_) if (q is not None and q.zero_point.requires_grad) else None
     ws, wsn = workspace(query("ssq_epilogue_bwd_workspace_size", N * C_), dev_, _epi_slot())
-    call("ssq_epilogue_loss_bwd", cp, _vp(idx), int(M), float(p), _vp(loss), yp, bp, _vp(gm),
-         _vp(ph), rp, rbp, rgp, rphp, N, C_, hw, int(relu), _vp(d), _vp(z), lo, hi, _vp(gy),
-         _vp(gres), _vp(ggm), _vp(gph), _vp(grg), _vp(grph), _vp(gd), _vp(gz), ws, wsn,
-         stream_of(y))
+    if yi is not None or ri is not None:
+        call("ssq_epilogue_loss_bwd_rows", cp, _vp(idx), int(M), float(p), _vp(loss), yp, yi, bp,
+             _vp(gm), _vp(ph), rp, ri, rbp, rgp, rphp, N, C_, hw, int(relu), _vp(d), _vp(z), lo,
+             hi, _vp(gy), _vp(gres), _vp(ggm), _vp(gph), _vp(grg), _vp(grph), _vp(gd), _vp(gz),
+             ws, wsn, stream_of(y))
+    else:
+        call("ssq_epilogue_loss_bwd", cp, _vp(idx), int(M), float(p), _vp(loss), yp, bp, _vp(gm),
+             _vp(ph), rp, rbp, rgp, rphp, N, C_, hw, int(relu), _vp(d), _vp(z), lo, hi, _vp(gy),
+             _vp(gres), _vp(ggm), _vp(gph), _vp(grg), _vp(grph), _vp(gd), _vp(gz), ws, wsn,
+             stream_of(y))
     # a gradient written into its GRAD_INTO slice is not handed back (already in place)
     return (loss, gy, gres, None if gm_into else ggm, None if ph_into else gph, gd, gz,
             None if rg_into else grg, None if rph_into else grph)

@@ -136,6 +136,19 @@ class BatchFeeder:
             self._gather2(s0, s1, d0, d1, k == 0)
         return self.cur_inp, K.Rows(self.out, self.didx)
 
+    def rows_lazy(self, input_needed=True, input_view=False):
+        """gather_lazy for a loop whose cached rows are read in place (kernels.rows_view):
+        no gather of the cached convs' rows; the batch input is gathered only when it is
+        needed and input_view is off, and with input_view it is handed on as a row view of
+        the cached inputs (its only other reader is the tail's residual, which reads rows)."""
+        if input_needed and not input_view:
+            self._gather2(self.inp, None, self.cur_inp, None, True)
+        else:
+            self._stage_only()
+        if input_view:
+            K.rows_view(self.cur_inp, self.inp, self.didx)
+        return self.cur_inp, K.Rows(self.out, self.didx)
+
     def next(self, perm=None):
         self.stage(self.draw() if perm is None else perm)
         return self.gather()

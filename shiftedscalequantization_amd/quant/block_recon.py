@@ -70,6 +70,10 @@ GATHER_ONCE = _FAST and os.environ.get("SSQ_BRECQ_GATHER_ONCE", "1") != "0"
 # one H2D copy -- for loops whose iteration is cheaper on the GPU than on the host (the
 # fc's 20000-iteration AdaRound loop); 1 = one iteration per replay
 CHUNK_ITERS = int(os.environ.get("SSQ_BRECQ_CHUNK", "25")) if _FAST else 1
+# act phase with CACHE_CONVS: the cached convs' rows and (identity residual) the batch input
+# are not gathered -- the epilogue kernels read them in place by the batch indices
+# (kernels.rows_view, ssq_epilogue_*_rows): no gather launch and no batch copy per iteration
+ROWS_IN_PLACE = CACHE_CONVS and os.environ.get("SSQ_BRECQ_ROWS", "1") != "0"
 
 
 def _input_convs(block, qmodules, x):
@@ -277,6 +281,7 @@ def _fast_loop(block, qmodules, opt_params, loss_func, feeder, bucket, iters, ac
     last = {}
     need_input = [True]     # False once cached_convs serves every reader of the block input
     conv_rows = []          # cached_convs' (all rows, batch buffer) pairs, gathered with the input
+    rows_mode = [False, False]   # (cached rows read in place, the batch input as a row view)
 
     def body_pre():
         with K.deferred_finalize(defer):
@@ -287,7 +292,9 @@ def _fast_loop(block, qmodules, opt_params, loss_func, feeder, bucket, iters, ac
                 _step()
 
     def _body_pre():
-        if conv_rows:
+        if rows_mode[0]:
+            cur_inp, cur_out = feeder.rows_lazy(need_input[0], rows_mode[1])
+        elif conv_rows:
             cur_inp, cur_out = feeder.gather_many(conv_rows, input_needed=need_input[0])
         else:
             cur_inp, cur_out = feeder.gather_lazy(input_needed=need_input[0])
@@ -352,13 +359,22 @@ def _fast_loop(block, qmodules, opt_params, loss_func, feeder, bucket, iters, ac
                 free = torch.cuda.mem_get_info(feeder.inp.device)[0]
                 convs = [m for m, _ in found] if need <= CACHE_CONVS_MEM_FRAC * free else []
                 if convs:
+                    mode = "rows" if ROWS_IN_PLACE else GATHER_ONCE
                     conv_rows[:] = stack.enter_context(cached_convs(
-                        convs, feeder.cur_inp, feeder.inp, feeder.didx, gathered=GATHER_ONCE))
-                    if not GATHER_ONCE:
+                        convs, feeder.cur_inp, feeder.inp, feeder.didx, gathered=mode))
+                    if ROWS_IN_PLACE:
+                        stack.enter_context(K.row_views())
+                        rows_mode[0] = True
+                    if ROWS_IN_PLACE or not GATHER_ONCE:
                         conv_rows.clear()
                     readers = block.input_readers() if isinstance(block, BaseQuantBlock) \
                         else [block]
                     need_input[0] = not (readers and all(m in convs for m in readers))
+                    ident = block.identity_input_convs() if isinstance(block, BaseQuantBlock) \
+                        else None
+                    # an identity residual the only other reader: the input as a row view
+                    rows_mode[1] = bool(ROWS_IN_PLACE and need_input[0] and ident
+                                        and all(m in convs for m in ident))
         _run(iters, loss_func, feeder, optimizer, scheduler, shadow if act_quant else None, use_graph,
              bucket, body_pre, body_post, last, opt_params, ada, ws_cache)
 

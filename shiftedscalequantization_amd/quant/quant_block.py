@@ -79,6 +79,11 @@ class BaseQuantBlock(nn.Module):
         residual), or None when the input is also used directly."""
         return None
 
+    def identity_input_convs(self):
+        """With an identity residual: the QuantModules that read the block input besides the
+        residual add of the block's tail (_tail); None otherwise."""
+        return None
+
     def _residual(self, ds, x):
         """ds(x), the downsample branch.  For the block the recon loop fuses (K.TAIL_LAZY)
         and a downsample whose forward ends in its K13 epilogue alone (bias, gamma^z/phi^z,
@@ -168,6 +173,9 @@ class QuantBasicBlock(BaseQuantBlock):
     def input_readers(self):
         return None if self.downsample is None else [self.conv1, self.downsample]
 
+    def identity_input_convs(self):
+        return [self.conv1] if self.downsample is None else None
+
     def toggleHardTarget(self):
         for m in (self.conv1, self.conv2, self.downsample):
             if m is not None:
@@ -192,6 +200,9 @@ class QuantBottleneck(BaseQuantBlock):
 
     def input_readers(self):
         return None if self.downsample is None else [self.conv1, self.downsample]
+
+    def identity_input_convs(self):
+        return [self.conv1] if self.downsample is None else None
 
     def forward(self, x):
         if self.cache_features == 'if':
@@ -221,6 +232,9 @@ class QuantResBottleneckBlock(BaseQuantBlock):
 
     def input_readers(self):
         return [self.conv1, self.downsample] if self.proj_block else None
+
+    def identity_input_convs(self):
+        return None if self.proj_block else [self.conv1]
 
     def forward(self, x):
         if self.cache_features == 'if':
@@ -256,6 +270,9 @@ class QuantInvertedResidual(BaseQuantBlock):
 
     def input_readers(self):
         return None if self.use_res_connect else [self.conv[0]]
+
+    def identity_input_convs(self):
+        return [self.conv[0]] if self.use_res_connect else None
 
     def forward(self, x):
         if self.cache_features == 'if':

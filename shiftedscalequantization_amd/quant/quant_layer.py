@@ -87,7 +87,9 @@ def cached_convs(modules, batch_input, source, idx, gathered=False):
     that the weights do not change inside the context.  gathered=True: the caller gathers
     the rows itself (the context yields each module's (all rows, batch buffer) pair, e.g. for
     one launch per iteration that also gathers the batch input) and forward only hands the
-    batch buffer on."""
+    batch buffer on.  gathered="rows": nothing gathers them -- forward hands the batch buffer
+    on as a row view of (all rows, idx) (kernels.rows_view), which the epilogue kernels read
+    in place; the caller holds a kernels.row_views() context."""
     global _CONV_CACHE
     prev = _CONV_CACHE
     cache = {} if prev is None else dict(prev)
@@ -388,6 +390,8 @@ class QuantModule(nn.Module):
         if _CONV_CACHE is not None:
             hit = _CONV_CACHE.get(self)
             if hit is not None and hit[0] == input.data_ptr() and hit[1] == tuple(input.shape):
+                if hit[5] == "rows":
+                    return K.rows_view(hit[4], hit[2], hit[3]), bias
                 if not hit[5]:
                     K.gather_rows2(hit[2], hit[3], out0=hit[4])
                 return hit[4], bias
@@ -419,6 +423,8 @@ class QuantModule(nn.Module):
                 act_q = False
             elif bias is not None or relu:
                 out = K.bias_act(out, bias, None, relu)
+            else:
+                out = K.materialize(out)     # a row view leaves as the batch it stands for
         else:
             weight, bias = self._weight_bias()
             out = self._conv(input, weight, bias)

@@ -1531,6 +1531,86 @@ def test_epilogue_bwd_without_dy(K, quant):
         np.testing.assert_array_equal(a, b)
 
 
+@pytest.mark.parametrize("form", ["affine_q", "bias_q", "bias_act"])
+@pytest.mark.parametrize("hw", [7, 8])
+def test_epilogue_rows_in_place_bit_identical(K, hw, form):
+    """ssq_epilogue_*_rows (BRECQ's act phase, block_recon.ROWS_IN_PLACE): the K13 epilogue
+    forward and backward reading a frozen conv's output rows in place from its per-sample
+    cache by the batch indices (duplicates included), and the fused tail reading the
+    residual's rows in place, against the same calls on the gathered batch -- outputs and
+    every gradient bit-identical, nothing gathered behind the call (no fptr fallback).
+    Forms: the --bias_cal affine epilogue + act quantizer (EpilogueFn), bias + ReLU + act
+    quantizer (BiasActQuantFn), bias + ReLU (BiasActFn); float4 rows (8x8), scalar (7x7)."""
+    from shiftedscalequantization_amd import _capi as A
+    from shiftedscalequantization_amd.quant.quant_layer import UniformAffineQuantizer
+    gen = torch.Generator().manual_seed(hw * 3 + len(form))
+    C = 12
+    cache = torch.randn(9, C, hw, hw, generator=gen).cuda()
+    rcache = torch.randn(9, C, hw, hw, generator=gen).cuda()
+    tcache = torch.randn(9, C, hw, hw, generator=gen).relu().cuda()
+    idx = torch.tensor([4, 1, 8, 1, 0], dtype=torch.int64).cuda()
+    N = idx.numel()
+    bias = torch.randn(C, generator=gen).cuda()
+    g = torch.randn(N, C, hw, hw, generator=gen).cuda()
+    y2 = torch.randn(N, C, hw, hw, generator=gen).cuda()     # the tail's conv output
+
+    def quantizer():
+        q = UniformAffineQuantizer(n_bits=4, channel_wise=False, scale_method="max", leaf_param=True).cuda()
+        q.delta = torch.nn.Parameter(torch.tensor(0.23).cuda())
+        q.zero_point = torch.nn.Parameter(torch.tensor(2.0).cuda())
+        q.inited = True
+        return q
+
+    def run(view):
+        gm = (1 + 0.1 * torch.randn(1, C, 1, 1, generator=torch.Generator().manual_seed(5))).cuda().requires_grad_(True)
+        ph = (0.1 * torch.randn(1, C, 1, 1, generator=torch.Generator().manual_seed(6))).cuda().requires_grad_(True)
+        q = quantizer()
+        falls = []
+        orig = A.materialize_rows
+
+        def mat(t):
+            if t.data_ptr() in A.ROW_VIEWS:
+                falls.append(1)
+            return orig(t)
+
+        A.materialize_rows = mat
+        try:
+            with K.row_views():
+                yb = torch.empty(N, C, hw, hw, device="cuda")
+                rb = torch.empty(N, C, hw, hw, device="cuda")
+                if view:
+                    K.rows_view(yb, cache, idx)
+                    K.rows_view(rb, rcache, idx)
+                else:
+                    yb.copy_(cache[idx])
+                    rb.copy_(rcache[idx])
+                if form == "affine_q":
+                    out = K.epilogue(yb, bias, gm, ph, None, 1, q)
+                elif form == "bias_q":
+                    out = K.bias_act_quant(yb, bias, None, 1, q.delta, q.zero_point, 4)
+                else:
+                    gm = ph = None
+                    out = K.bias_act(yb, bias, None, 1)
+                res_out = [host(out).copy()]
+                if out.requires_grad:
+                    out.backward(g)
+                    res_out += [host(t).copy() for t in (gm, ph) if t is not None]
+                    if form != "bias_act":
+                        res_out += [host(q.delta.grad).copy(), host(q.zero_point.grad).copy()]
+                # the fused tail with the residual read in place (its rows' gradient wanted)
+                tail = (y2, bias, None, None, rb, 1, None)
+                loss, gy, gres = K.epilogue_loss_bwd(tail, K.Rows(tcache, idx), N * hw * hw, 2.4)[:3]
+                res_out += [host(loss).copy(), host(gy).copy()]
+        finally:
+            A.materialize_rows = orig
+        return res_out, falls
+
+    (a, fa), (b, fb) = run(False), run(True)
+    assert not fb and len(a) == len(b)
+    for u, v in zip(a, b):
+        np.testing.assert_array_equal(u.reshape(-1).view(np.int32), v.reshape(-1).view(np.int32))
+
+
 @pytest.mark.parametrize("shape", [(8, 125, 5), (11, 100, 8), (40, 500, 7)])
 def test_epilogue_bwd_delta_split(K, shape):
     """The act quantizer's delta / zero-point sums of the epilogue backward over many rows:

@@ -348,20 +348,24 @@ def test_brecq_block_reconstruction_matches_reference(Q, golden, graph, wgrad, f
         BR._fast_loop = orig_fast
 
 
+@pytest.mark.parametrize("rows", [False, True])
 @pytest.mark.parametrize("graph", [False, True])
 @pytest.mark.parametrize("affine", [False, True])
-def test_brecq_loop_knobs_bit_identical(Q, golden, graph, affine, det_convs):
+def test_brecq_loop_knobs_bit_identical(Q, golden, graph, affine, rows, det_convs):
     """block_recon._fast_loop's launch savings -- deferred finalizes, the fused tail (p = 2
     weight phase, p = 2.4 act phase), the act phase's pinned weights and its precomputed
     block-input convs (conv1, the downsample: gathered rows instead of the conv) -- against the plain
     loop: AdaRound V, the act deltas and the Adam moments bit-identical after each phase,
     per-iteration losses equal to the last float ulps (row-wise vs block-wise loss partials).
     affine: gamma^z / phi^z live (the --bias_cal flow's act phase: the general K13 epilogue,
-    whose delta gradient the fused tail and the deferred finalize produce)."""
+    whose delta gradient the fused tail and the deferred finalize produce).  rows: the cached
+    convs' rows read in place by the epilogue kernels (ROWS_IN_PLACE: no gather launch at all
+    in the act phase, no row view gathered behind the loop's back) instead of gathered."""
     import importlib
     BR = importlib.import_module("shiftedscalequantization_amd.quant.block_recon")
     E = importlib.import_module("shiftedscalequantization_amd.quant._engine")
     g = golden("recon_brecq")
+    views, fallbacks = [], []
     cali = dev(g["cali"])
     runs, used = [], []
     for on in (False, True):
@@ -411,13 +415,26 @@ def test_brecq_loop_knobs_bit_identical(Q, golden, graph, affine, det_convs):
             stashed.append(sum(getattr(m.weight_quantizer, "_stash", None) is not None for m in mods))
 
         knobs = {k: getattr(BR, k) for k in ("DEFER_FINALIZE", "FUSE_TAIL", "PIN_WEIGHTS",
-                                             "CACHE_CONVS", "STASH_ADAROUND", "GATHER_ONCE")}
+                                             "CACHE_CONVS", "STASH_ADAROUND", "GATHER_ONCE",
+                                             "ROWS_IN_PLACE")}
         BR.LossFunction.record, E.SsqAdam.__init__, BR.K.epilogue_loss_bwd = spy, init, tail
         BR.pinned_weights, BR.cached_convs, BR.stash_adaround = pin, cc, stash
         orig_fast = BR._fast_loop
         BR._fast_loop = lambda *a: orig_fast(*(a[:-1] + (a[-1] and graph,)))
+        orig_view, orig_mat = BR.K.rows_view, BR.K.A.materialize_rows
+
+        def view(*a):
+            views.append(1)
+            return orig_view(*a)
+
+        def mat(t):
+            if t.data_ptr() in BR.K.A.ROW_VIEWS:
+                fallbacks.append(1)
+            return orig_mat(t)
+
+        BR.K.rows_view, BR.K.A.materialize_rows = view, mat
         for k in knobs:
-            setattr(BR, k, on)
+            setattr(BR, k, on and (rows or k != "ROWS_IN_PLACE"))
         out = {}
         try:
             torch.manual_seed(1005)
@@ -450,15 +467,18 @@ def test_brecq_loop_knobs_bit_identical(Q, golden, graph, affine, det_convs):
             BR.LossFunction.record, E.SsqAdam.__init__, BR.K.epilogue_loss_bwd = orig_rec, orig_init, orig_tail
             BR.pinned_weights, BR._fast_loop, BR.cached_convs = orig_pin, orig_fast, orig_cc
             BR.stash_adaround, BR.K.gather_rows2 = orig_stash, orig_gather
+            BR.K.rows_view, BR.K.A.materialize_rows = orig_view, orig_mat
             for k, v in knobs.items():
                 setattr(BR, k, v)
         runs.append(out)
         used.append((len(tails), len(pins), cconvs, sorted(set(stashed)), sorted(set(pairs))))
     # the act phase caches conv1 and the downsample (both read the block input) and gathers
-    # both their rows in one launch per iteration (the plain loop: the batch input only); the
-    # weight phase computes the block's three AdaRound weights in one launch every iteration
+    # both their rows in one launch per iteration (the plain loop: the batch input only) --
+    # or, rows, gathers nothing (the input is not read; the epilogues read the cached rows in
+    # place); the weight phase computes the block's three AdaRound weights in one launch
     assert used[0] == (0, 0, [], [], [False]) and used[1][0] > 0 and used[1][1] == 1 \
-        and used[1][2] == [2] and used[1][3] == [3] and used[1][4] == [True], used
+        and used[1][2] == [2] and used[1][3] == [3] and used[1][4] == ([] if rows else [True]), used
+    assert (len(views) > 0) == rows and not fallbacks, (len(views), len(fallbacks))
     assert runs[0].keys() == runs[1].keys()
     for k in runs[0]:
         if k.endswith("_rec"):
@@ -546,20 +566,23 @@ def test_brecq_layer_reconstruction_matches_reference(Q, golden, graph):
         parity_report(f"a22_layer_reconstruction[graph={graph}]", **stats)
 
 
+@pytest.mark.parametrize("rows", [False, True])
 @pytest.mark.parametrize("affine", [False, True])
-def test_brecq_act_identity_block_gathers_input_with_conv(Q, affine, det_convs):
+def test_brecq_act_identity_block_gathers_input_with_conv(Q, affine, rows, det_convs):
     """BRECQ's act phase on a block with an identity residual (no downsample, e.g. ResNet-18
     layer1.1): the block input is still read (the residual), so each iteration gathers it
-    together with the cached conv1 rows in ONE ssq_gather_rows2 launch (GATHER_ONCE); act
-    deltas and Adam moments bit-identical to the plain loop (every knob off), losses to the
-    last ulps."""
+    together with the cached conv1 rows in ONE ssq_gather_rows2 launch (GATHER_ONCE) -- or,
+    rows (ROWS_IN_PLACE), gathers nothing: conv1's epilogue reads the cached conv1 rows and
+    the fused tail the residual's cached input rows in place; act deltas and Adam moments
+    bit-identical to the plain loop (every knob off), losses to the last ulps."""
     import importlib
     from shiftedscalequantization_amd import nets
     BR = importlib.import_module("shiftedscalequantization_amd.quant.block_recon")
     E = importlib.import_module("shiftedscalequantization_amd.quant._engine")
     knobs = ("DEFER_FINALIZE", "FUSE_TAIL", "PIN_WEIGHTS", "CACHE_CONVS", "STASH_ADAROUND",
-             "GATHER_ONCE")
+             "GATHER_ONCE", "ROWS_IN_PLACE")
     gen = torch.Generator().manual_seed(21)
+    fallbacks = []
     cali = torch.randn(32, 3, 12, 12, generator=gen).cuda()
     runs, pairs = [], []
     for on in (False, True):
@@ -598,16 +621,25 @@ def test_brecq_act_identity_block_gathers_input_with_conv(Q, affine, det_convs):
             got.append(src1 is not None)
             return orig_gather(src0, idx, src1, **k)
 
+        orig_mat = BR.K.A.materialize_rows
+
+        def mat(t):
+            if t.data_ptr() in BR.K.A.ROW_VIEWS:
+                fallbacks.append(1)
+            return orig_mat(t)
+
         prev = {k: getattr(BR, k) for k in knobs}
         BR.LossFunction.record, E.SsqAdam.__init__, BR.K.gather_rows2 = spy, init, gather
+        BR.K.A.materialize_rows = mat
         for k in knobs:
-            setattr(BR, k, on)
+            setattr(BR, k, on and (rows or k != "ROWS_IN_PLACE"))
         try:
             torch.manual_seed(1005)
             Q.block_reconstruction(qnn, block, cali, batch_size=8, iters=12, act_quant=True,
                                    opt_mode="mse", lr=4e-4, p=2.4)
         finally:
             BR.LossFunction.record, E.SsqAdam.__init__, BR.K.gather_rows2 = orig_rec, orig_init, orig_gather
+            BR.K.A.materialize_rows = orig_mat
             for k, v in prev.items():
                 setattr(BR, k, v)
         out = {"rec": np.array(seen),
@@ -620,7 +652,8 @@ def test_brecq_act_identity_block_gathers_input_with_conv(Q, affine, det_convs):
                 out[f"opt{k}_v{j}"] = o.state[p_]["exp_avg_sq"].cpu().numpy()
         runs.append(out)
         pairs.append(sorted(set(got)))
-    assert pairs == [[False], [True]], pairs
+    assert pairs == [[False], [] if rows else [True]], pairs
+    assert not fallbacks
     assert runs[0].keys() == runs[1].keys() and len(runs[0]["rec"]) == 12
     for k in runs[0]:
         if k == "rec":
