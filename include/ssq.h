@@ -425,17 +425,17 @@ int ssq_epilogue_loss_bwd(const float* tgt_cache, const int64_t* idx, int64_t M,
                           int qmax, float* gy, float* gres, float* ggamma, float* gphi,
                           float* gres_gamma, float* gres_phi, float* gdelta, float* gzp,
                           void* ws, size_t ws_bytes, ssq_stream_t stream);
-/* The three above reading y (and res) in place from per-sample row caches: y_cache /
- * res are [*, C, hw] caches and sample n of the batch is their row y_rows[n] / res_rows[n]
+/* The three above reading y and / or res in place from per-sample row caches: with a map,
+ * y / res is a [*, C, hw] cache and sample n of the batch is its row y_rows[n] / res_rows[n]
  * (either map may be NULL: that operand is the batch itself).  BRECQ's act phase hands its
  * frozen convs' precomputed outputs and the cached block input to the epilogues this way
  * instead of gathering a batch copy of each (block_recon.py:62-73's cached[idx]); the values
  * and their order are those of the gathered batch, so the results are bit-identical.       */
-int ssq_epilogue_fwd_rows(const float* y_cache, const int64_t* y_rows, const float* bias,
-                          const float* gamma, const float* phi, const float* res, float* out,
-                          float* yq, int64_t n, int64_t hw, int64_t C, int relu,
-                          const float* delta, const float* zp, int qmin, int qmax,
-                          ssq_stream_t stream);
+int ssq_epilogue_fwd_rows(const float* y, const int64_t* y_rows, const float* bias,
+                          const float* gamma, const float* phi, const float* res,
+                          const int64_t* res_rows, float* out, float* yq, int64_t n, int64_t hw,
+                          int64_t C, int relu, const float* delta, const float* zp, int qmin,
+                          int qmax, ssq_stream_t stream);
 int ssq_epilogue_bwd_rows(const float* g, const float* y, const int64_t* y_rows,
                           const float* bias, const float* gamma, const float* phi,
                           const float* res, const int64_t* res_rows, int64_t N, int64_t C,

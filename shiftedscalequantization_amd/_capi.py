@@ -89,8 +89,8 @@ SIGNATURES = {
     "ssq_epilogue_loss_bwd": (_i, [_p, _p, _i64, _f, _p, _p, _p, _p, _p, _p, _p, _p, _p, _i64,
                                    _i64, _i64, _i, _p, _p, _i, _i, _p, _p, _p, _p, _p, _p, _p,
                                    _p, _p, _sz, _p]),
-    "ssq_epilogue_fwd_rows": (_i, [_p, _p, _p, _p, _p, _p, _p, _p, _i64, _i64, _i64, _i, _p, _p,
-                                   _i, _i, _p]),
+    "ssq_epilogue_fwd_rows": (_i, [_p, _p, _p, _p, _p, _p, _p, _p, _p, _i64, _i64, _i64, _i, _p,
+                                   _p, _i, _i, _p]),
     "ssq_epilogue_bwd_rows": (_i, [_p, _p, _p, _p, _p, _p, _p, _p, _i64, _i64, _i64, _i, _p, _p,
                                    _i, _i, _p, _p, _p, _p, _p, _p, _p, _sz, _p]),
     "ssq_epilogue_loss_bwd_rows": (_i, [_p, _p, _i64, _f, _p, _p, _p, _p, _p, _p, _p, _p, _p, _p,

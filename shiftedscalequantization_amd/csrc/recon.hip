@@ -117,14 +117,16 @@ __global__ __launch_bounds__(kBlock) void bias_act_kernel(const float* __restric
                                                           const float* __restrict__ gamma,
                                                           const float* __restrict__ phi,
                                                           const int64_t* __restrict__ yrows,
+                                                          const int64_t* __restrict__ rrows,
                                                           uint32_t chw) {
   const uint32_t stride = gridDim.x * blockDim.x;
   QParams qp{1.0f, 0.0f, qlo, qhi};
-  // element i of the batch -> its offset in y (yrows: sample n = i / chw is row yrows[n])
-  auto yoff = [&](uint32_t i) -> int64_t {
-    if (!yrows) return (int64_t)i;
+  // element i of the batch -> its offset in y / res (a row map: sample n = i / chw is row
+  // map[n] of the cache)
+  auto off = [&](const int64_t* map, uint32_t i) -> int64_t {
+    if (!map) return (int64_t)i;
     const uint32_t nn = fdiv(fdiv(i, div_hw), div_c);
-    return yrows[nn] * (int64_t)chw + (int64_t)(i - nn * chw);
+    return map[nn] * (int64_t)chw + (int64_t)(i - nn * chw);
   };
   if (QUANT) {
     qp.d = qdelta[0];
@@ -145,9 +147,9 @@ __global__ __launch_bounds__(kBlock) void bias_act_kernel(const float* __restric
   if (vec) {
     const uint32_t n4 = n / 4;
     for (uint32_t v = blockIdx.x * blockDim.x + threadIdx.x; v < n4; v += stride) {
-      const f32x4 a = *(const f32x4*)(y + yoff(4 * v));   // hw % 4 == 0 with yrows
+      const f32x4 a = *(const f32x4*)(y + off(yrows, 4 * v));   // hw % 4 == 0 with a map
       f32x4 rr = {0.0f, 0.0f, 0.0f, 0.0f};
-      if (RES) rr = ((const f32x4*)res)[v];
+      if (RES) rr = *(const f32x4*)(res + off(rrows, 4 * v));
       f32x4 o;
       o.x = one(4 * v, a.x, rr.x);
       o.y = one(4 * v + 1, a.y, rr.y);
@@ -165,7 +167,7 @@ __global__ __launch_bounds__(kBlock) void bias_act_kernel(const float* __restric
     }
   } else {
     for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
-      const float t = one(i, y[yoff(i)], RES ? res[i] : 0.0f);
+      const float t = one(i, y[off(yrows, i)], RES ? res[off(rrows, i)] : 0.0f);
       if (!QUANT || out) out[i] = t;
       if (QUANT) yq[i] = fq(t);
     }
@@ -856,7 +858,7 @@ static int bias_act(const char* what, const float* y, const float* bias, const f
                     float* out, float* yq, int64_t n, int64_t hw, int64_t C, int relu,
                     const float* qdelta, const float* qzp, int qmin, int qmax, hipStream_t s,
                     const float* gamma = nullptr, const float* phi = nullptr,
-                    const int64_t* yrows = nullptr) {
+                    const int64_t* yrows = nullptr, const int64_t* rrows = nullptr) {
   SSQ_REQUIRE(!gamma == !phi, SSQ_E_ARG, "%s: gamma and phi go together", what);
   SSQ_REQUIRE(y && n >= 0 && hw >= 1 && C >= 1, SSQ_E_ARG, "%s: bad args", what);
   SSQ_REQUIRE(yq ? (qdelta && qzp && qmin < qmax) : out != nullptr, SSQ_E_ARG, "%s: bad outputs",
@@ -865,17 +867,18 @@ static int bias_act(const char* what, const float* y, const float* bias, const f
               "%s: tensor exceeds 2^31 elements", what);
   if (n == 0) return SSQ_OK;
   auto al = [](const void* q) { return ((uintptr_t)q & 15u) == 0; };
-  SSQ_REQUIRE(!yrows || n % (hw * C) == 0, SSQ_E_ARG, "%s: y rows need whole [C, hw] samples",
-              what);
+  SSQ_REQUIRE((!yrows && !rrows) || n % (hw * C) == 0, SSQ_E_ARG,
+              "%s: row maps need whole [C, hw] samples", what);
+  SSQ_REQUIRE(!rrows || res, SSQ_E_ARG, "%s: res_rows without res", what);
   const int vec = n % 4 == 0 && al(y) && (!out || al(out)) && (!res || al(res)) &&
-                  (!yq || al(yq)) && (!yrows || hw % 4 == 0);
+                  (!yq || al(yq)) && ((!yrows && !rrows) || hw % 4 == 0);
   const FastDiv dh = make_fastdiv((uint32_t)hw), dc = make_fastdiv((uint32_t)C);
   const dim3 grid(grid_for(vec ? n / 4 : n, kBlock, 2048));
   const float lo = (float)qmin, hi = (float)qmax;
 #define SSQ_BA(R, A, Q, F)                                                                    \
   hipLaunchKernelGGL((bias_act_kernel<R, A, Q, F>), grid, dim3(kBlock), 0, s, y, bias, res, out, \
                      (uint32_t)n, dh, dc, (uint32_t)C, vec, yq, qdelta, qzp, lo, hi, gamma, phi, \
-                     yrows, (uint32_t)(C * hw))
+                     yrows, rrows, (uint32_t)(C * hw))
 #define SSQ_BA1(R, A, Q) \
   if (gamma) SSQ_BA(R, A, Q, true); else SSQ_BA(R, A, Q, false);
 #define SSQ_BA2(R, A) \
@@ -915,14 +918,13 @@ extern "C" int ssq_epilogue_fwd(const float* y, const float* bias, const float* 
                   qmax, (hipStream_t)stream, gamma, phi);
 }
 
-extern "C" int ssq_epilogue_fwd_rows(const float* y_cache, const int64_t* y_rows,
-                                     const float* bias, const float* gamma, const float* phi,
-                                     const float* res, float* out, float* yq, int64_t n,
+extern "C" int ssq_epilogue_fwd_rows(const float* y, const int64_t* y_rows, const float* bias,
+                                     const float* gamma, const float* phi, const float* res,
+                                     const int64_t* res_rows, float* out, float* yq, int64_t n,
                                      int64_t hw, int64_t C, int relu, const float* delta,
                                      const float* zp, int qmin, int qmax, ssq_stream_t stream) {
-  SSQ_REQUIRE(y_rows, SSQ_E_ARG, "ssq_epilogue_fwd_rows: y_rows is required");
-  return bias_act("ssq_epilogue_fwd_rows", y_cache, bias, res, out, yq, n, hw, C, relu, delta,
-                  zp, qmin, qmax, (hipStream_t)stream, gamma, phi, y_rows);
+  return bias_act("ssq_epilogue_fwd_rows", y, bias, res, out, yq, n, hw, C, relu, delta, zp,
+                  qmin, qmax, (hipStream_t)stream, gamma, phi, y_rows, res_rows);
 }
 
 extern "C" size_t ssq_epilogue_bwd_workspace_size(int64_t rows) {

@@ -1007,29 +1007,10 @@ class BiasActFn(torch.autograd.Function):
 
     @staticmethod
     def forward(ctx, y, bias, res, relu):
-        yr = rows_of(y)
-        if yr is not None:
-            A.check(y, "conv output")
-            yp = _vp(yr[0])
-        else:
-            y, yp = fptr(y.detach(), "conv output")
-        C = y.shape[1] if y.dim() > 1 else 1
-        hw = y[0, 0].numel() if y.dim() > 2 else 1
-        if bias is not None:
-            bias, bp = fptr(bias.detach().reshape(-1), "bias")
-            if bias.numel() != C:
-                raise A.SSQError("bias_act: bias must have one value per channel")
-        else:
-            bp = None
-        if res is not None:
-            res, rp = fptr(res.detach(), "residual")
-            if res.shape != y.shape:
-                raise A.SSQError("bias_act: residual shape mismatch")
-        else:
-            rp = None
+        y, yp, bp, rp, C, hw, _, (yi, ri) = _epilogue_layout(y, bias, res, rows=True)
         out = torch.empty_like(y)
-        if yr is not None:
-            call("ssq_epilogue_fwd_rows", yp, _vp(yr[1]), bp, None, None, rp, _vp(out), None,
+        if yi is not None or ri is not None:
+            call("ssq_epilogue_fwd_rows", yp, yi, bp, None, None, rp, ri, _vp(out), None,
                  y.numel(), hw, C, int(relu), None, None, 0, 1, stream_of(y))
         else:
             call("ssq_bias_act", yp, bp, rp, _vp(out), y.numel(), hw, C, int(relu), stream_of(y))
@@ -1070,11 +1051,18 @@ class LazyRes:
 
 
 def materialize(res):
+    """A residual as a tensor with its values: a LazyRes materialised, a row view gathered."""
     if isinstance(res, LazyRes):
         return res.materialize()
     if res is not None and A.ROW_VIEWS:
         A.materialize_rows(res)
     return res
+
+
+def _unlazy(res):
+    """A LazyRes materialised for an epilogue kernel; a row view stays one (the K13 kernels
+    read it in place)."""
+    return res.materialize() if isinstance(res, LazyRes) else res
 
 
 # A/B knob: the downsample branch's epilogue deferred into the block's fused tail (LazyRes;
@@ -1108,7 +1096,7 @@ def bias_act(y, bias=None, res=None, relu=True, lazy=False):
         out = torch.empty_like(y)
         out._ssq_tail = (y, bias, None, None, res, int(relu), None)
         return out
-    res = materialize(res)
+    res = _unlazy(res)
     out = BiasActFn.apply(y, bias, res, int(relu))
     if int(relu) == 1:
         # lets a loss that folds the ReLU backward into its own pass (lp_loss relu_mask)
@@ -1158,8 +1146,7 @@ class BiasActQuantFn(torch.autograd.Function):
 
     @staticmethod
     def forward(ctx, y, bias, res, delta, zp, relu, n_bits, sym, keep):
-        materialize(res)
-        y, yp, bp, rp, C_, hw, hold, (yi, _) = _epilogue_layout(y, bias, res, rows=True)
+        y, yp, bp, rp, C_, hw, hold, (yi, ri) = _epilogue_layout(y, bias, res, rows=True)
         d, dp = fptr(delta.detach().reshape(-1), "delta")
         z, zpp = fptr(zp.detach().reshape(-1), "zero_point")
         if d.numel() != 1 or z.numel() != 1:
@@ -1167,9 +1154,9 @@ class BiasActQuantFn(torch.autograd.Function):
         lo, hi = qrange(n_bits, sym)
         out = torch.empty_like(y) if keep else None
         yq = torch.empty_like(y)
-        if yi is not None:
-            call("ssq_epilogue_fwd_rows", yp, yi, bp, None, None, rp, _vp(out), _vp(yq), y.numel(),
-                 hw, C_, int(relu), dp, zpp, lo, hi, stream_of(y))
+        if yi is not None or ri is not None:
+            call("ssq_epilogue_fwd_rows", yp, yi, bp, None, None, rp, ri, _vp(out), _vp(yq),
+                 y.numel(), hw, C_, int(relu), dp, zpp, lo, hi, stream_of(y))
         else:
             call("ssq_bias_act_fq", yp, bp, rp, _vp(out), _vp(yq), y.numel(), hw, C_, int(relu),
                  dp, zpp, lo, hi, stream_of(y))
@@ -1204,7 +1191,7 @@ class BiasActQuantFn(torch.autograd.Function):
 
 def bias_act_quant(y, bias, res, relu, delta, zp, n_bits, sym=False):
     """bias_act followed by fake_quant(delta, zp) in one pass (per-tensor quantizer)."""
-    res = materialize(res)
+    res = _unlazy(res)
     keep = torch.is_grad_enabled() and any(
         t is not None and t.requires_grad for t in (y, res, delta, zp))
     return BiasActQuantFn.apply(y, bias, res, delta, zp, int(relu), n_bits, sym, keep)
@@ -1219,8 +1206,7 @@ class EpilogueFn(torch.autograd.Function):
 
     @staticmethod
     def forward(ctx, y, bias, gamma, phi, res, delta, zp, relu, n_bits, sym):
-        materialize(res)
-        y, yp, bp, rp, C_, hw, _, (yi, _) = _epilogue_layout(y, bias, res, rows=True)
+        y, yp, bp, rp, C_, hw, _, (yi, ri) = _epilogue_layout(y, bias, res, rows=True)
         gm, gmp = fptr(gamma.detach().reshape(-1), "gamma") if gamma is not None else (None, None)
         ph, php = fptr(phi.detach().reshape(-1), "phi") if phi is not None else (None, None)
         if gm is not None and (gm.numel() != C_ or ph.numel() != C_):
@@ -1236,8 +1222,8 @@ class EpilogueFn(torch.autograd.Function):
             dp = zpp = None
             lo, hi = 0, 1
         out = torch.empty_like(y)
-        if yi is not None:
-            call("ssq_epilogue_fwd_rows", yp, yi, bp, gmp, php, rp, None if quant else _vp(out),
+        if yi is not None or ri is not None:
+            call("ssq_epilogue_fwd_rows", yp, yi, bp, gmp, php, rp, ri, None if quant else _vp(out),
                  _vp(out) if quant else None, y.numel(), hw, C_, int(relu), dp, zpp, lo, hi,
                  stream_of(y))
         else:
@@ -1482,7 +1468,7 @@ def epilogue(y, bias, gamma, phi, res, relu, q=None, lazy=False):
         out = torch.empty_like(y)
         out._ssq_tail = (y, bias, gamma, phi, res, int(relu), q)
         return out
-    res = materialize(res)
+    res = _unlazy(res)
     if q is None:
         return EpilogueFn.apply(y, bias, gamma, phi, res, None, None, int(relu), 8, False)
     return EpilogueFn.apply(y, bias, gamma, phi, res, q.delta, q.zero_point, int(relu), q.n_bits,

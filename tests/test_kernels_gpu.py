@@ -1538,7 +1538,8 @@ def test_epilogue_rows_in_place_bit_identical(K, hw, form):
     forward and backward reading a frozen conv's output rows in place from its per-sample
     cache by the batch indices (duplicates included), and the fused tail reading the
     residual's rows in place, against the same calls on the gathered batch -- outputs and
-    every gradient bit-identical, nothing gathered behind the call (no fptr fallback).
+    every gradient bit-identical, nothing gathered behind the call (no fptr fallback); the
+    forwards take a row-view residual too (the non-fused block tail of the act phase).
     Forms: the --bias_cal affine epilogue + act quantizer (EpilogueFn), bias + ReLU + act
     quantizer (BiasActQuantFn), bias + ReLU (BiasActFn); float4 rows (8x8), scalar (7x7)."""
     from shiftedscalequantization_amd import _capi as A
@@ -1585,12 +1586,12 @@ def test_epilogue_rows_in_place_bit_identical(K, hw, form):
                     yb.copy_(cache[idx])
                     rb.copy_(rcache[idx])
                 if form == "affine_q":
-                    out = K.epilogue(yb, bias, gm, ph, None, 1, q)
+                    out = K.epilogue(yb, bias, gm, ph, rb, 1, q)
                 elif form == "bias_q":
-                    out = K.bias_act_quant(yb, bias, None, 1, q.delta, q.zero_point, 4)
+                    out = K.bias_act_quant(yb, bias, rb, 1, q.delta, q.zero_point, 4)
                 else:
                     gm = ph = None
-                    out = K.bias_act(yb, bias, None, 1)
+                    out = K.bias_act(yb, bias, rb, 1)
                 res_out = [host(out).copy()]
                 if out.requires_grad:
                     out.backward(g)

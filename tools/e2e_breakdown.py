@@ -62,7 +62,10 @@ def _hook(i, iters):
             _marks.clear()
 
 
-BR.ITER_HOOK = _hook
+# the per-iteration hook turns the loops' chunked graph replays off (block_recon.ChunkGraph
+# needs ITER_HOOK unset): SSQ_BREAKDOWN_HOOK=0 keeps the per-call times only
+if os.environ.get("SSQ_BREAKDOWN_HOOK", "1") != "0":
+    BR.ITER_HOOK = _hook
 t0 = time.perf_counter()
 main_imagenet.main(sys.argv[1:])
 torch.cuda.synchronize()
