@@ -349,6 +349,50 @@ __device__ __forceinline__ void epi_row_sums(EpiRow& w, uint32_t lane, double* _
   }
 }
 
+// Small planes (<= 64 elements or float4s per row: ResNet layer3 / layer4, 14x14 / 7x7):
+// 4 rows per wave, 16 lanes per row (RPW = kG16).  Each lane sums its elements of the row in
+// order (j = l16, l16 + 16, ...), then the 16 lanes of a row are added by one xor tree
+// (8, 4, 2, 1) that reduces the wave's 4 rows at once -- 4 shuffle steps per quantity for 4
+// rows, where a row per wave takes 6 for 1.  Every path that produces these rows' records
+// (the plain backward, the fused tail) takes this form for the same shape, so they agree bit
+// for bit; the order differs from the row-per-wave form's only in how the doubles are
+// grouped.
+constexpr int kG16 = 16;
+__device__ __forceinline__ double group16_sum(double v) {
+#pragma unroll
+  for (int o = 8; o > 0; o >>= 1) v += __shfl_xor(v, o, kWave);
+  return v;
+}
+template <bool QUANT, int LOSS, int RES>
+__device__ __forceinline__ void epi_row_sums16(EpiRow& w, bool writer, double* __restrict__ o) {
+  w.sg = group16_sum(w.sg);
+  w.sp = group16_sum(w.sp);
+  if (RES == 2) {
+    w.sgr = group16_sum(w.sgr);
+    w.spr = group16_sum(w.spr);
+  }
+  if (QUANT) {
+    w.a0 = group16_sum(w.a0);
+    w.a1 = group16_sum(w.a1);
+    w.a2 = group16_sum(w.a2);
+    w.a3 = group16_sum(w.a3);
+  }
+  if (LOSS) w.la = group16_sum(w.la);
+  if (writer) {
+    o[0] = w.sg;
+    o[1] = w.sp;
+    o[2] = w.a0;
+    o[3] = w.a1;
+    o[4] = w.a2;
+    o[5] = w.a3;
+    o[6] = w.la;
+    if (RES == 2) {
+      o[7] = w.sgr;
+      o[8] = w.spr;
+    }
+  }
+}
+
 // Backward of the K13 epilogue (optionally with gamma^z/phi^z and the act quantizer):
 // t = (y + bias[c]) [*gamma[c] + phi[c]] [+ res] [-> ReLU] [-> fq]; given g = dL/d(output)
 //   g_t = dL/d(pre-ReLU t): the STE of the act quantizer (fq_bwd_pt's formulas), then the
@@ -380,13 +424,17 @@ __device__ __forceinline__ double epilogue_rows_body(
     float inv_m, float lp, const ResEpi& re, uint32_t bid, const int64_t* __restrict__ yrows,
     const int64_t* __restrict__ rrows) {
   const uint32_t lane = threadIdx.x & (kWave - 1);
-  const uint32_t r0 = (bid * (kBlock / kWave) + threadIdx.x / kWave) * RPW;
+  constexpr uint32_t kRows = RPW == kG16 ? 4u : (uint32_t)RPW;     // rows per wave
+  const uint32_t r0 = (bid * (kBlock / kWave) + threadIdx.x / kWave) * kRows;
   if (r0 >= rows) return 0.0;
   const float d = QUANT ? qdelta[0] : 1.0f, z = QUANT ? qzp[0] : 0.0f;
   const bool rbias = RES == 2 && re.bias, raffine = RES == 2 && re.gamma;
-  EpiRow w[RPW];
+  // per-row constants of the row-per-wave / 4-rows forms (the 16-lane form loads its own)
+  constexpr int kW = RPW == kG16 ? 1 : RPW;
+  EpiRow w[kW];
 #pragma unroll
-  for (int k = 0; k < RPW; ++k) {
+  for (int k = 0; k < kW; ++k) {
+    if (RPW == kG16) break;
     const uint32_t c = (r0 + k) % C;
     const bool ok = r0 + k < rows;
     w[k].b = (bias && ok) ? bias[c] : 0.0f;
@@ -406,6 +454,81 @@ __device__ __forceinline__ double epilogue_rows_body(
     return map ? (map[r / C] * (int64_t)C + r % C) * hw : (int64_t)r * hw;
   };
   auto gbase_of = [&](uint32_t r) -> int64_t { return mapped(LOSS ? lidx : nullptr, r); };
+  if (RPW == kG16) {
+    // row r0 + (lane >> 4), this lane's elements l16, l16 + 16, ... (<= 4 of them: every
+    // load issued before any math)
+    const uint32_t l16 = lane & 15, r = r0 + (lane >> 4);
+    const bool ok = r < rows;
+    const uint32_t rr = ok ? r : r0;
+    const uint32_t c = rr % C;
+    EpiRow wr;
+    wr.b = bias ? bias[c] : 0.0f;
+    wr.ga = AFFINE ? gamma[c] : 1.0f;
+    wr.ph = AFFINE ? phi[c] : 0.0f;
+    wr.rb = rbias ? re.bias[c] : 0.0f;
+    wr.rga = raffine ? re.gamma[c] : 1.0f;
+    wr.rph = raffine ? re.phi[c] : 0.0f;
+    const int64_t base = (int64_t)rr * hw, gbase = gbase_of(rr);
+    const int64_t ybase = mapped(yrows, rr), rbase = mapped(rrows, rr);
+    const uint32_t nv = VEC ? hw / 4 : hw;     // <= 64 (host-checked)
+    if (VEC) {
+      f32x4 yv[4], gv[4], rv[4];
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        const uint32_t v = l16 + 16 * k;
+        yv[k] = gv[k] = rv[k] = f32x4{0.0f, 0.0f, 0.0f, 0.0f};
+        if (ok && v < nv) {
+          yv[k] = ((const f32x4*)(y + ybase))[v];
+          gv[k] = ((const f32x4*)(g + gbase))[v];
+          if (RES) rv[k] = ((const f32x4*)(res + rbase))[v];
+        }
+      }
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        const uint32_t v = l16 + 16 * k;
+        if (!(ok && v < nv)) continue;
+        float oy[4], orr[4];
+        elem(wr, yv[k].x, gv[k].x, rv[k].x, oy[0], orr[0]);
+        elem(wr, yv[k].y, gv[k].y, rv[k].y, oy[1], orr[1]);
+        elem(wr, yv[k].z, gv[k].z, rv[k].z, oy[2], orr[2]);
+        elem(wr, yv[k].w, gv[k].w, rv[k].w, oy[3], orr[3]);
+        if (gy) ((f32x4*)(gy + base))[v] = f32x4{oy[0], oy[1], oy[2], oy[3]};
+        if (gres) ((f32x4*)(gres + base))[v] = f32x4{orr[0], orr[1], orr[2], orr[3]};
+      }
+    } else {
+      float yv[4], gv[4], rv[4];
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        const uint32_t j = l16 + 16 * k;
+        yv[k] = gv[k] = rv[k] = 0.0f;
+        if (ok && j < nv) {
+          yv[k] = y[ybase + j];
+          gv[k] = g[gbase + j];
+          if (RES) rv[k] = res[rbase + j];
+        }
+      }
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        const uint32_t j = l16 + 16 * k;
+        if (!(ok && j < nv)) continue;
+        float oy, orr;
+        elem(wr, yv[k], gv[k], rv[k], oy, orr);
+        if (gy) gy[base + j] = oy;
+        if (gres) gres[base + j] = orr;
+      }
+    }
+    epi_row_sums16<QUANT, LOSS, RES>(wr, ok && l16 == 0, part + (int64_t)rr * kEpiParts);
+    // the wave's loss sum: its rows' totals in row order (lane 0's value is the one used)
+    double wl = 0.0;
+    if (LOSS) {
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        const double t = __shfl(wr.la, 16 * k, kWave);
+        if (r0 + k < rows) wl += t;
+      }
+    }
+    return wl;
+  }
   if (RPW == 1) {
     EpiRow& wr = w[0];
     const int64_t base = (int64_t)r0 * hw, gbase = gbase_of(r0);
@@ -846,6 +969,14 @@ extern "C" int ssq_gather_rows2_staged(const float* src0, float* dst0, int64_t r
 
 // A/B knob SSQ_EPI_MULTI_ROW: 4 rows per wave on small planes for the epilogue backward
 // (1, the default), also for its fused-tail form (2), or never (0)
+static bool epi_g16() {
+  static const bool on = [] {
+    const char* e = getenv("SSQ_EPI_G16");
+    return !(e && *e && atoi(e) == 0);
+  }();
+  return on;
+}
+
 static int epi_multi_row() {
   static const int mode = [] {
     const char* e = getenv("SSQ_EPI_MULTI_ROW");
@@ -973,9 +1104,14 @@ static int epilogue_bwd(const char* what, const float* g, const float* y, const 
   SSQ_REQUIRE(relu >= 0 && relu <= 2, SSQ_E_ARG, "%s: activation code %d", what, relu);
   // small planes (<= 64 elements or float4s per row): 4 rows per wave (same bits); not with
   // the act quantizer's four extra sums per row (3-4 waves per SIMD instead of 7-8)
-  const bool multi = (vec ? hw / 4 : hw) <= kWave && !delta && !res2 &&
-                     epi_multi_row() >= (loss ? 2 : 1);
-  const int64_t rpw = multi ? 4 : 1;
+  // rows of <= 64 elements or float4s: 4 rows per wave, 16 lanes each (kG16; every variant,
+  // the same form for the plain backward and the fused tail); SSQ_EPI_G16=0 for A/B: the r4
+  // forms (4 rows per wave with a lane per element where the registers allow, else a row
+  // per wave)
+  const bool small = (vec ? hw / 4 : hw) <= kWave;
+  const bool g16 = small && epi_g16();
+  const bool multi = !g16 && small && !delta && !res2 && epi_multi_row() >= (loss ? 2 : 1);
+  const int64_t rpw = (g16 || multi) ? 4 : 1;
   const int64_t waves = (rows + rpw - 1) / rpw;
   const uint32_t nmain = (uint32_t)((waves + kBlock / kWave - 1) / (kBlock / kWave));
   int frc = SSQ_OK;
@@ -990,7 +1126,8 @@ static int epilogue_bwd(const char* what, const float* g, const float* y, const 
                      bias, gamma, phi, res, (uint32_t)rows, (uint32_t)C, (uint32_t)hw, delta, zp, \
                      lo, hi, gy, gres, part, fin, nmain, lidx, inv_m, lp, re2, yrows, rrows)
 #define SSQ_EB(R, A, Q, F, V, L) \
-  if (multi) SSQ_EB0(R, A, Q, F, V, L, ((Q) ? 1 : 4)); else SSQ_EB0(R, A, Q, F, V, L, 1);
+  if (g16) SSQ_EB0(R, A, Q, F, V, L, kG16); \
+  else if (multi) SSQ_EB0(R, A, Q, F, V, L, ((Q) ? 1 : 4)); else SSQ_EB0(R, A, Q, F, V, L, 1);
 #define SSQ_EBL(R, A, Q, F, V) \
   if (lp2) { SSQ_EB(R, A, Q, F, V, 1) } else { SSQ_EB(R, A, Q, F, V, 2) }
 #define SSQ_EB1(R, A, Q, F) \
@@ -1002,7 +1139,8 @@ static int epilogue_bwd(const char* what, const float* g, const float* y, const 
   if (delta) { SSQ_EB2(R, A, true) } else { SSQ_EB2(R, A, false) }
 // RES 2: the fused tail only, ReLU / identity, one row per wave
 #define SSQ_EBLR(A, Q, F, V) \
-  if (lp2) { SSQ_EB0(2, A, Q, F, V, 1, 1); } else { SSQ_EB0(2, A, Q, F, V, 2, 1); }
+  if (g16) { if (lp2) { SSQ_EB0(2, A, Q, F, V, 1, kG16); } else { SSQ_EB0(2, A, Q, F, V, 2, kG16); } } \
+  else if (lp2) { SSQ_EB0(2, A, Q, F, V, 1, 1); } else { SSQ_EB0(2, A, Q, F, V, 2, 1); }
 #define SSQ_EBR1(A, Q, F) \
   if (vec) { SSQ_EBLR(A, Q, F, true) } else { SSQ_EBLR(A, Q, F, false) }
 #define SSQ_EBR2(A, Q) \

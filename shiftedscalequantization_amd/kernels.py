@@ -1361,8 +1361,12 @@ TAIL_LAZY = [None]
 # the epilogue's forward launch and its activation-sized output are gone, the bits are the
 # same (col is the im2col of the same values; the backward runs the same ssq_epilogue_bwd on
 # the same input gradient).  Any other consumer materialises the placeholder with exactly
-# the ops QuantModule.forward runs.  A/B knob: SSQ_EPI_GEMM=0.
-EPI_INTO_GEMM = os.environ.get("SSQ_EPI_GEMM", "1") != "0"
+# the ops QuantModule.forward runs.  Off by default (SSQ_EPI_GEMM=1 turns it on): the im2col
+# build evaluates the epilogue once per column entry, R*S = 9 times per activation, and that
+# costs more than the launch it saves -- bench.py's recon loops, ABAB on one box (r5j,
+# profiles/r5_epi_gemm_ab.txt): layer3.0 1980 vs 2001 it/s, layer3.1 2012 vs 2029, layer4.0
+# 2341 vs 2344, layer4.1 2196 vs 2215 with the fold on vs off.
+EPI_INTO_GEMM = os.environ.get("SSQ_EPI_GEMM", "0") == "1"
 EPI_CONSUMER = [None]
 
 
