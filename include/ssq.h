@@ -431,11 +431,16 @@ int ssq_epilogue_loss_bwd(const float* tgt_cache, const int64_t* idx, int64_t M,
  * frozen convs' precomputed outputs and the cached block input to the epilogues this way
  * instead of gathering a batch copy of each (block_recon.py:62-73's cached[idx]); the values
  * and their order are those of the gathered batch, so the results are bit-identical.       */
+/* stage_dst (may be NULL): workgroup 0 also copies stage_n int64 words (<= 4096) from
+ * stage_src to stage_dst -- a loop replaying several iterations per graph hands each
+ * iteration's device words (a ring row, from which this launch takes its row maps) to the
+ * static slot its later launches read, without a copy launch of its own.                  */
 int ssq_epilogue_fwd_rows(const float* y, const int64_t* y_rows, const float* bias,
                           const float* gamma, const float* phi, const float* res,
                           const int64_t* res_rows, float* out, float* yq, int64_t n, int64_t hw,
                           int64_t C, int relu, const float* delta, const float* zp, int qmin,
-                          int qmax, ssq_stream_t stream);
+                          int qmax, const int64_t* stage_src, int64_t* stage_dst,
+                          int64_t stage_n, ssq_stream_t stream);
 int ssq_epilogue_bwd_rows(const float* g, const float* y, const int64_t* y_rows,
                           const float* bias, const float* gamma, const float* phi,
                           const float* res, const int64_t* res_rows, int64_t N, int64_t C,

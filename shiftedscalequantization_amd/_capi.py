@@ -90,7 +90,7 @@ SIGNATURES = {
                                    _i64, _i64, _i, _p, _p, _i, _i, _p, _p, _p, _p, _p, _p, _p,
                                    _p, _p, _sz, _p]),
     "ssq_epilogue_fwd_rows": (_i, [_p, _p, _p, _p, _p, _p, _p, _p, _p, _i64, _i64, _i64, _i, _p,
-                                   _p, _i, _i, _p]),
+                                   _p, _i, _i, _p, _p, _i64, _p]),
     "ssq_epilogue_bwd_rows": (_i, [_p, _p, _p, _p, _p, _p, _p, _p, _i64, _i64, _i64, _i, _p, _p,
                                    _i, _i, _p, _p, _p, _p, _p, _p, _p, _sz, _p]),
     "ssq_epilogue_loss_bwd_rows": (_i, [_p, _p, _i64, _f, _p, _p, _p, _p, _p, _p, _p, _p, _p, _p,
@@ -179,9 +179,27 @@ def ptr(t):
 ROW_VIEWS = {}
 
 
+# A pending stage of a chunk-replayed iteration's device words: (ring row, static slot).  The
+# iteration's first K13 row-view forward performs it (ssq_epilogue_fwd_rows stage_*) and
+# reads its row maps from the ring row; any other kernel call first performs it as a copy.
+ROW_STAGE = []
+
+
+def flush_row_stage():
+    if ROW_STAGE:
+        src, dst = ROW_STAGE.pop()
+        dst.copy_(src)
+
+
+def take_row_stage():
+    """(ring row, static slot) of the pending stage, now the caller's to perform, or None."""
+    return ROW_STAGE.pop() if ROW_STAGE else None
+
+
 def materialize_rows(t):
     """Gather a registered row view into its buffer (one ssq_gather_rows2) and unregister it;
     a no-op for any other tensor."""
+    flush_row_stage()
     e = ROW_VIEWS.pop(t.data_ptr(), None)
     if e is not None:
         buf, cache, idx = e
@@ -195,6 +213,8 @@ def fptr(t, name="tensor"):
     if t is None:
         return None, None
     check(t, name)
+    if ROW_STAGE:
+        flush_row_stage()
     if ROW_VIEWS:
         materialize_rows(t)
     t = t.contiguous()

@@ -118,8 +118,15 @@ __global__ __launch_bounds__(kBlock) void bias_act_kernel(const float* __restric
                                                           const float* __restrict__ phi,
                                                           const int64_t* __restrict__ yrows,
                                                           const int64_t* __restrict__ rrows,
-                                                          uint32_t chw) {
+                                                          uint32_t chw,
+                                                          const int64_t* __restrict__ stage_src,
+                                                          int64_t* __restrict__ stage_dst,
+                                                          uint32_t stage_n) {
   const uint32_t stride = gridDim.x * blockDim.x;
+  // the iteration's device words (a chunk ring row) copied into the loop's static slot, which
+  // the iteration's later launches read (this launch reads its row maps from the ring row)
+  if (stage_dst && blockIdx.x == 0)
+    for (uint32_t k = threadIdx.x; k < stage_n; k += blockDim.x) stage_dst[k] = stage_src[k];
   QParams qp{1.0f, 0.0f, qlo, qhi};
   // element i of the batch -> its offset in y / res (a row map: sample n = i / chw is row
   // map[n] of the cache)
@@ -989,18 +996,22 @@ static int bias_act(const char* what, const float* y, const float* bias, const f
                     float* out, float* yq, int64_t n, int64_t hw, int64_t C, int relu,
                     const float* qdelta, const float* qzp, int qmin, int qmax, hipStream_t s,
                     const float* gamma = nullptr, const float* phi = nullptr,
-                    const int64_t* yrows = nullptr, const int64_t* rrows = nullptr) {
+                    const int64_t* yrows = nullptr, const int64_t* rrows = nullptr,
+                    const int64_t* stage_src = nullptr, int64_t* stage_dst = nullptr,
+                    int64_t stage_n = 0) {
   SSQ_REQUIRE(!gamma == !phi, SSQ_E_ARG, "%s: gamma and phi go together", what);
   SSQ_REQUIRE(y && n >= 0 && hw >= 1 && C >= 1, SSQ_E_ARG, "%s: bad args", what);
   SSQ_REQUIRE(yq ? (qdelta && qzp && qmin < qmax) : out != nullptr, SSQ_E_ARG, "%s: bad outputs",
               what);
   SSQ_REQUIRE(n < (1ll << 31) && hw < (1ll << 31) && C < (1ll << 31), SSQ_E_ARG,
               "%s: tensor exceeds 2^31 elements", what);
-  if (n == 0) return SSQ_OK;
+  if (n == 0 && !stage_dst) return SSQ_OK;
   auto al = [](const void* q) { return ((uintptr_t)q & 15u) == 0; };
   SSQ_REQUIRE((!yrows && !rrows) || n % (hw * C) == 0, SSQ_E_ARG,
               "%s: row maps need whole [C, hw] samples", what);
   SSQ_REQUIRE(!rrows || res, SSQ_E_ARG, "%s: res_rows without res", what);
+  SSQ_REQUIRE(!stage_dst || (stage_src && stage_n > 0 && stage_n <= 4096), SSQ_E_ARG,
+              "%s: staging needs a source and 1..4096 words", what);
   const int vec = n % 4 == 0 && al(y) && (!out || al(out)) && (!res || al(res)) &&
                   (!yq || al(yq)) && ((!yrows && !rrows) || hw % 4 == 0);
   const FastDiv dh = make_fastdiv((uint32_t)hw), dc = make_fastdiv((uint32_t)C);
@@ -1009,7 +1020,7 @@ static int bias_act(const char* what, const float* y, const float* bias, const f
 #define SSQ_BA(R, A, Q, F)                                                                    \
   hipLaunchKernelGGL((bias_act_kernel<R, A, Q, F>), grid, dim3(kBlock), 0, s, y, bias, res, out, \
                      (uint32_t)n, dh, dc, (uint32_t)C, vec, yq, qdelta, qzp, lo, hi, gamma, phi, \
-                     yrows, rrows, (uint32_t)(C * hw))
+                     yrows, rrows, (uint32_t)(C * hw), stage_src, stage_dst, (uint32_t)stage_n)
 #define SSQ_BA1(R, A, Q) \
   if (gamma) SSQ_BA(R, A, Q, true); else SSQ_BA(R, A, Q, false);
 #define SSQ_BA2(R, A) \
@@ -1053,9 +1064,12 @@ extern "C" int ssq_epilogue_fwd_rows(const float* y, const int64_t* y_rows, cons
                                      const float* gamma, const float* phi, const float* res,
                                      const int64_t* res_rows, float* out, float* yq, int64_t n,
                                      int64_t hw, int64_t C, int relu, const float* delta,
-                                     const float* zp, int qmin, int qmax, ssq_stream_t stream) {
+                                     const float* zp, int qmin, int qmax,
+                                     const int64_t* stage_src, int64_t* stage_dst,
+                                     int64_t stage_n, ssq_stream_t stream) {
   return bias_act("ssq_epilogue_fwd_rows", y, bias, res, out, yq, n, hw, C, relu, delta, zp,
-                  qmin, qmax, (hipStream_t)stream, gamma, phi, y_rows, res_rows);
+                  qmin, qmax, (hipStream_t)stream, gamma, phi, y_rows, res_rows, stage_src,
+                  stage_dst, stage_n);
 }
 
 extern "C" size_t ssq_epilogue_bwd_workspace_size(int64_t rows) {

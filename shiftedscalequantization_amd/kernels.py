@@ -1007,11 +1007,12 @@ class BiasActFn(torch.autograd.Function):
 
     @staticmethod
     def forward(ctx, y, bias, res, relu):
-        y, yp, bp, rp, C, hw, _, (yi, ri) = _epilogue_layout(y, bias, res, rows=True)
+        y, yp, bp, rp, C, hw, _, (yi, ri), stg = _epilogue_layout(y, bias, res, rows=True,
+                                                                 stage=True)
         out = torch.empty_like(y)
         if yi is not None or ri is not None:
             call("ssq_epilogue_fwd_rows", yp, yi, bp, None, None, rp, ri, _vp(out), None,
-                 y.numel(), hw, C, int(relu), None, None, 0, 1, stream_of(y))
+                 y.numel(), hw, C, int(relu), None, None, 0, 1, *stg, stream_of(y))
         else:
             call("ssq_bias_act", yp, bp, rp, _vp(out), y.numel(), hw, C, int(relu), stream_of(y))
         ctx.relu = int(relu)
@@ -1105,10 +1106,19 @@ def bias_act(y, bias=None, res=None, relu=True, lazy=False):
     return out
 
 
-def _epilogue_layout(y, bias, res, rows=False):
+def _epilogue_layout(y, bias, res, rows=False, stage=False):
     """Pointers and (C, hw) of an epilogue's operands.  rows: y / res may stay row views --
-    their pointers are then their caches' and ROWS holds (y_idx, res_idx) pointers (None for
-    an operand that is the batch itself); otherwise a row view is gathered (fptr)."""
+    their pointers are then their caches' and the result ends with their row maps' pointers
+    (None for an operand that is the batch itself); otherwise a row view is gathered (fptr).
+    stage (the K13 forward): a pending stage of the iteration's device words (_capi.ROW_STAGE)
+    is taken over by the caller's launch -- the maps then point into the ring row it copies
+    from -- and the result ends with (src, dst, n) pointers for ssq_epilogue_fwd_rows, or
+    (None, None, 0); without a row map the stage is performed here as a copy."""
+    st = None
+    if rows and stage:
+        st = A.take_row_stage()
+    elif A.ROW_STAGE:
+        A.flush_row_stage()
     yr = rows_of(y) if rows else None
     rr = rows_of(res) if rows else None
     if yr is not None:
@@ -1132,8 +1142,19 @@ def _epilogue_layout(y, bias, res, rows=False):
         if res.shape != y.shape:
             raise A.SSQError("bias_act: residual shape mismatch")
     if rows:
-        return y, yp, bp, rp, C, hw, (bias, res), (None if yr is None else _vp(yr[1]),
-                                                   None if rr is None else _vp(rr[1]))
+        def rmap(t):
+            # the static slot's indices are read from the ring row this launch copies
+            if st is not None and t.data_ptr() == st[1].data_ptr():
+                return _vp(st[0])
+            return _vp(t)
+        maps = (None if yr is None else rmap(yr[1]), None if rr is None else rmap(rr[1]))
+        if st is not None and maps == (None, None):
+            st[1].copy_(st[0])
+            st = None
+        if stage:
+            stg = (None, None, 0) if st is None else (_vp(st[0]), _vp(st[1]), st[0].numel())
+            return y, yp, bp, rp, C, hw, (bias, res), maps, stg
+        return y, yp, bp, rp, C, hw, (bias, res), maps
     return y, yp, bp, rp, C, hw, (bias, res)
 
 
@@ -1146,7 +1167,8 @@ class BiasActQuantFn(torch.autograd.Function):
 
     @staticmethod
     def forward(ctx, y, bias, res, delta, zp, relu, n_bits, sym, keep):
-        y, yp, bp, rp, C_, hw, hold, (yi, ri) = _epilogue_layout(y, bias, res, rows=True)
+        y, yp, bp, rp, C_, hw, hold, (yi, ri), stg = _epilogue_layout(y, bias, res, rows=True,
+                                                                     stage=True)
         d, dp = fptr(delta.detach().reshape(-1), "delta")
         z, zpp = fptr(zp.detach().reshape(-1), "zero_point")
         if d.numel() != 1 or z.numel() != 1:
@@ -1156,7 +1178,7 @@ class BiasActQuantFn(torch.autograd.Function):
         yq = torch.empty_like(y)
         if yi is not None or ri is not None:
             call("ssq_epilogue_fwd_rows", yp, yi, bp, None, None, rp, ri, _vp(out), _vp(yq),
-                 y.numel(), hw, C_, int(relu), dp, zpp, lo, hi, stream_of(y))
+                 y.numel(), hw, C_, int(relu), dp, zpp, lo, hi, *stg, stream_of(y))
         else:
             call("ssq_bias_act_fq", yp, bp, rp, _vp(out), _vp(yq), y.numel(), hw, C_, int(relu),
                  dp, zpp, lo, hi, stream_of(y))
@@ -1206,7 +1228,8 @@ class EpilogueFn(torch.autograd.Function):
 
     @staticmethod
     def forward(ctx, y, bias, gamma, phi, res, delta, zp, relu, n_bits, sym):
-        y, yp, bp, rp, C_, hw, _, (yi, ri) = _epilogue_layout(y, bias, res, rows=True)
+        y, yp, bp, rp, C_, hw, _, (yi, ri), stg = _epilogue_layout(y, bias, res, rows=True,
+                                                                  stage=True)
         gm, gmp = fptr(gamma.detach().reshape(-1), "gamma") if gamma is not None else (None, None)
         ph, php = fptr(phi.detach().reshape(-1), "phi") if phi is not None else (None, None)
         if gm is not None and (gm.numel() != C_ or ph.numel() != C_):
@@ -1225,7 +1248,7 @@ class EpilogueFn(torch.autograd.Function):
         if yi is not None or ri is not None:
             call("ssq_epilogue_fwd_rows", yp, yi, bp, gmp, php, rp, ri, None if quant else _vp(out),
                  _vp(out) if quant else None, y.numel(), hw, C_, int(relu), dp, zpp, lo, hi,
-                 stream_of(y))
+                 *stg, stream_of(y))
         else:
             call("ssq_epilogue_fwd", yp, bp, gmp, php, rp, None if quant else _vp(out),
                  _vp(out) if quant else None, y.numel(), hw, C_, int(relu), dp, zpp, lo, hi,

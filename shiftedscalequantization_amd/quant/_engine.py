@@ -17,6 +17,9 @@ from .. import kernels as K
 
 class BatchFeeder:
     RING = 4
+    # chunk capture with rows read in place: the iteration's words staged by its first K13
+    # row-view forward (False: by a copy launch, as the gathering loops' _stage_only)
+    STAGE_IN_K13 = True
 
     def __init__(self, cached_inp, cached_out, batch_size, device, extra_words=1):
         self.inp = cached_inp.to(device).contiguous()
@@ -143,8 +146,13 @@ class BatchFeeder:
         the cached inputs (its only other reader is the tail's residual, which reads rows)."""
         if input_needed and not input_view:
             self._gather2(self.inp, None, self.cur_inp, None, True)
-        else:
+        elif self.slot is not None and not self.STAGE_IN_K13:
             self._stage_only()
+        elif self.slot is not None:
+            # chunk capture: the iteration's first K13 row-view forward copies the ring row
+            # into the static words (ssq_epilogue_fwd_rows stage_*), reading its row maps from
+            # the ring row; any other kernel call first performs it as a copy (_capi.fptr)
+            K.A.ROW_STAGE[:] = [(self.chunk_dev[self.slot], self._dev)]
         if input_view:
             K.rows_view(self.cur_inp, self.inp, self.didx)
         return self.cur_inp, K.Rows(self.out, self.didx)

@@ -286,6 +286,7 @@ def _fast_loop(block, qmodules, opt_params, loss_func, feeder, bucket, iters, ac
     def body_pre():
         with K.deferred_finalize(defer):
             _body_pre()
+            K.A.flush_row_stage()      # (no kernel took the iteration's stage: a copy)
             if bucket is None:
                 # world 1: the step inside the deferral, so it rides on the last pending
                 # finalizes (ssq_adam: one launch for both)
@@ -416,6 +417,7 @@ class ChunkGraph:
 def _run(iters, loss_func, feeder, optimizer, scheduler, shadow, use_graph, bucket, body_pre,
          body_post, last, opt_params, ada, ws_cache):
     graph_obj = None
+    graph_last = {}
     chunk_obj = None
     grads_of = {}        # the .grad tensors of each graph (restored for the one replayed last)
     skip_ok = (SKIP_FROZEN and bucket is None and ITER_HOOK is None and
@@ -492,7 +494,11 @@ def _run(iters, loss_func, feeder, optimizer, scheduler, shadow, use_graph, buck
                 # world > 1: two graphs around the eager bucket all-reduce (IterationGraph)
                 graph_obj = IterationGraph(body_pre, body_post, bucket, ws_cache)
                 grads_of['single'] = [p_.grad for p_ in opt_params]
+                # the graph's own loss buffer and step flag (a chunk graph captured later
+                # leaves `last` pointing at its last iteration's)
+                graph_last = dict(last)
             if graph_obj is not None:
+                last.update(graph_last)
                 graph_obj.replay()
                 last_graph[0] = 'single'
             else:

@@ -718,6 +718,92 @@ def test_brecq_chunked_loop_bit_identical(Q, golden, det_convs):
             np.testing.assert_array_equal(runs[1][k], runs[0][k], err_msg=k)
 
 
+@pytest.mark.parametrize("stage", [False, True])
+@pytest.mark.parametrize("affine", [False, True])
+def test_brecq_act_chunked_rows_bit_identical(Q, affine, stage, det_convs):
+    """BRECQ's act phase on an identity-residual block with the cached rows read in place
+    (ROWS_IN_PLACE) and 25 iterations per graph replay: each replayed iteration's first
+    launch -- conv1's K13 row-view forward -- copies its ring row into the static words
+    (ssq_epilogue_fwd_rows stage_*; no copy launch of its own) and takes its row maps from
+    the ring row.  Act deltas, Adam moments and every reported loss bit-identical to one
+    iteration per replay; the stage taken by the forward in every chunked iteration (stage) or
+    done by a copy launch (the gathering loops' form)."""
+    import importlib
+    from shiftedscalequantization_amd import nets
+    BR = importlib.import_module("shiftedscalequantization_amd.quant.block_recon")
+    E = importlib.import_module("shiftedscalequantization_amd.quant._engine")
+    A = BR.K.A
+    gen = torch.Generator().manual_seed(23)
+    cali = torch.randn(32, 3, 12, 12, generator=gen).cuda()
+    runs, taken = [], []
+    for chunk in (1, 25):
+        torch.manual_seed(5)
+        net = nn.Sequential(nn.Conv2d(3, 16, 3, padding=1, bias=False), nn.BatchNorm2d(16),
+                            nn.ReLU(), nets.BasicBlock(16, 16), nn.AdaptiveAvgPool2d(1),
+                            nn.Flatten(), nn.Linear(16, 10)).eval()
+        qnn = Q.QuantModel(net, {"n_bits": 2, "channel_wise": True, "scale_method": "max"},
+                           {"n_bits": 4, "channel_wise": False, "scale_method": "mse",
+                            "leaf_param": True}).cuda().eval()
+        qnn.set_first_last_layer_to_8bit()
+        block = qnn.model[3]
+        if affine:
+            g2 = torch.Generator().manual_seed(7)
+            for n in ("conv1", "conv2"):
+                m = getattr(block, n)
+                with torch.no_grad():
+                    m.alpha_out.copy_(1 + 0.05 * torch.randn(m.alpha_out.shape, generator=g2))
+                    m.beta_out.copy_(0.02 * torch.randn(m.beta_out.shape, generator=g2))
+        qnn.set_quant_state(True, True)
+        with torch.no_grad():
+            qnn(cali[:8])
+        seen, opts, took = [], [], [0]
+        orig_rec, orig_init, orig_take = BR.LossFunction.record, E.SsqAdam.__init__, A.take_row_stage
+
+        def spy(self, rec, rnd, b, **k):
+            r = orig_rec(self, rec, rnd, b, **k)
+            seen.append(float(r))
+            return r
+
+        def init(self, *a, **k):
+            orig_init(self, *a, **k)
+            opts.append(self)
+
+        def take():
+            st = orig_take()
+            took[0] += st is not None
+            return st
+
+        prev, prev_st = BR.CHUNK_ITERS, E.BatchFeeder.STAGE_IN_K13
+        BR.LossFunction.record, E.SsqAdam.__init__, A.take_row_stage = spy, init, take
+        BR.CHUNK_ITERS, E.BatchFeeder.STAGE_IN_K13 = chunk, stage
+        n0 = E.GRAPH_REPLAYS.get("chunk", 0)
+        try:
+            torch.manual_seed(1005)
+            Q.block_reconstruction(qnn, block, cali, batch_size=8, iters=120, act_quant=True,
+                                   opt_mode="mse", lr=4e-4, p=2.4)
+        finally:
+            BR.LossFunction.record, E.SsqAdam.__init__, A.take_row_stage = orig_rec, orig_init, orig_take
+            BR.CHUNK_ITERS, E.BatchFeeder.STAGE_IN_K13 = prev, prev_st
+        out = {"rec": np.array(seen),
+               "delta": np.array([float(q.delta) for q in
+                                  [block.act_quantizer, block.conv1.act_quantizer,
+                                   block.conv2.act_quantizer] if q.delta is not None])}
+        for k, o in enumerate(opts):
+            for j, p_ in enumerate(o.params):
+                out[f"opt{k}_m{j}"] = o.state[p_]["exp_avg"].cpu().numpy()
+                out[f"opt{k}_v{j}"] = o.state[p_]["exp_avg_sq"].cpu().numpy()
+        runs.append(out)
+        taken.append((took[0], E.GRAPH_REPLAYS.get("chunk", 0) - n0))
+    # chunk 25: the stage is taken once per captured iteration (the graph holds 25) and the
+    # loop replays the chunk graph at least 4 times (120 iterations after a 4-iteration warm-up)
+    assert taken[0] == (0, 0) and taken[1][0] == (25 if stage else 0) and taken[1][1] >= 4, taken
+    assert runs[0].keys() == runs[1].keys()
+    bad = np.nonzero(runs[1]["rec"] != runs[0]["rec"])[0]
+    assert bad.size == 0, ("iterations whose loss differs", bad.tolist())
+    for k in runs[0]:
+        np.testing.assert_array_equal(runs[1][k], runs[0][k], err_msg=k)
+
+
 @pytest.mark.parametrize("bits", [4, 8])
 def test_fc_fused_iteration_matches_unfused(Q, det_convs, bits):
     """K19 (kernels.fc_recon_iter, block_recon.FUSE_FC): BRECQ's layer loop on a Linear
