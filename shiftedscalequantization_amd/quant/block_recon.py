@@ -380,6 +380,13 @@ def _fast_loop(block, qmodules, opt_params, loss_func, feeder, bucket, iters, ac
              bucket, body_pre, body_post, last, opt_params, ada, ws_cache)
 
 
+# tools: when CHUNK_PROBE[0] is not None, the loop's chunk graph is timed once right after
+# its capture (ChunkGraph.probe: back-to-back replays, which repeat its iterations' device
+# work on the same staged words -- the loop's results are then not the reference's; timing
+# runs only) and the µs per iteration are left here
+CHUNK_PROBE = [None]
+
+
 class ChunkGraph:
     """`n` consecutive iterations of a world-1 loop captured in ONE HIP graph: the host draws
     the n iterations' batch permutations (the reference's torch.randperm on the CPU
@@ -412,6 +419,17 @@ class ChunkGraph:
     def replay(self):
         self.graph.replay()
         GRAPH_REPLAYS["chunk"] = GRAPH_REPLAYS.get("chunk", 0) + 1
+
+    def probe(self, reps=20):
+        """µs per iteration of back-to-back replays (GPU work and launch boundaries only)."""
+        self.graph.replay()
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record()
+        for _ in range(reps):
+            self.graph.replay()
+        e1.record()
+        e1.synchronize()
+        return e0.elapsed_time(e1) * 1e3 / (reps * self.n)
 
 
 def _run(iters, loss_func, feeder, optimizer, scheduler, shadow, use_graph, bucket, body_pre,
@@ -452,6 +470,8 @@ def _run(iters, loss_func, feeder, optimizer, scheduler, shadow, use_graph, buck
         feeder.stage_chunk(perms, extras)
         if chunk_obj is None:
             chunk_obj = ChunkGraph(body, optimizer, feeder, n, ws_cache, last)
+            if CHUNK_PROBE[0] is not None:
+                CHUNK_PROBE[0] = chunk_obj.probe()
             grads_of['chunk'] = chunk_obj.grads
         chunk_obj.replay()
         last_graph[0] = 'chunk'

@@ -49,6 +49,16 @@ def main():
     us = (t[2200] - t[200]) / 2000 * 1e6
     out = {"fc_adaround_us_per_iter": round(us, 2), "it_per_s": round(1e6 / us, 1)}
     print(json.dumps(out))
+    # the chunk graph's own replay time (GPU work + launch boundaries, no host work between
+    # iterations): 20 back-to-back replays of the loop's last chunk graph, HIP events
+    from shiftedscalequantization_amd.quant import block_recon as BR
+    BR.CHUNK_PROBE[0] = False
+    run(dev, cali, 300)
+    us_chunk = BR.CHUNK_PROBE[0]
+    BR.CHUNK_PROBE[0] = None
+    if us_chunk:
+        print(json.dumps({"chunk_replay_us_per_iter": round(us_chunk, 2),
+                          "iters_per_chunk": BR.CHUNK_ITERS}))
     pr = cProfile.Profile()
     pr.enable()
     run(dev, cali, 2200)
