@@ -7,7 +7,8 @@
 // adaptive_rounding.py:38-67, then F.linear), the loss (lp_loss p = 2 + the rounding
 // regulariser, block_recon.py:119-182 / layer_recon.py:107-170), its backward and Adam.
 // Each of those is microseconds of GPU work on this layer, so as separate launches the loop
-// is bound by dependent-launch boundaries (r5: 8 launches, 40 us per iteration).  Here:
+// is bound by dependent-launch boundaries (8 launches: 32 us per iteration replayed back to
+// back; in two launches 19.5 us, profiles/r5_fc_replay_probe.txt).  Here:
 //
 //   fc_fwd_loss  (one workgroup per 16 x 16 tile of y, 8 waves splitting C_in): y = x W^T
 //     + bias on fp32 MFMA (v_mfma_f32_16x16x4_f32, every operand load of a wave issued
@@ -15,8 +16,8 @@
 //     p = 2 term and gradient of every output (lp_elem: the lp_loss_kernel ops) -> g = dL/dy
 //     and one double loss partial per workgroup;
 //   fc_bwd_adam  (one workgroup per 16 x 16 tile of dW): dW = g^T x on the same MFMA, then
-//     per element (one a thread) AdaRound's backward with the rounding regulariser folded in (the
-//     adaround_bwd_kernel ops, lambda and b from the iteration's device words), V's Adam step
+//     per element (one a thread) AdaRound's backward with the rounding regulariser folded in
+//     (the adaround_bwd_kernel ops, lambda and b from the iteration's device words), V's Adam step
 //     (ssq_adam's ops), and W^ of the NEXT iteration from the updated V (the
 //     adaround_fwd_kernel ops) -- so the forward reads W^ instead of evaluating the soft
 //     rounding (a divide and an exp per weight) itself; workgroup 0 also sums the loss
@@ -125,8 +126,9 @@ __global__ __launch_bounds__(kBlock * 2) void fc_fwd_loss(
 // rounding regulariser (adaround_bwd_kernel's ops, lambda and b from the iteration's words),
 // V's Adam step (ssq_adam's ops) and W^ of the updated V (adaround_fwd_kernel's ops) for the
 // next iteration.  The per-element math (a divide, two exps, a pow, a sqrt, Adam's divides)
-// is most of the kernel, so it is spread over 4x the waves of a wave-per-tile form (measured:
-// DESIGN §5).  Every load of a wave is issued before its first use.
+// is most of the kernel, so it is spread over 4x the waves of a wave-per-tile form (traced on
+// the ResNet-18 fc: 13.1-15.1 -> 11.7-13.1 us, profiles/r5_fc_anatomy_wavetile.txt vs
+// r5_fc_anatomy.txt).  Every load of a wave is issued before its first use.
 // Workgroup 0 also sums the forward's loss partials in order.
 __global__ __launch_bounds__(kBlock) void fc_bwd_adam(
     const float* __restrict__ x, const int64_t* __restrict__ slot, uint32_t bs,
