@@ -88,11 +88,12 @@ static ColTiling col_tiling_prep(const Geo& g) {
   return t;
 }
 
-// Alpha-backward tiling.  Weights with Co*K <= kChanElems (ResNet-18 layer1 / layer2 3x3
-// convs and every 1x1 downsample, the ResNet-50 1x1 convs up to Co = 1280) take one
-// workgroup per input channel (alpha_bwd_channel): its 256 threads take the channel's Co*K
-// (row, tap) elements -- thread t: elements t, t + 256, ... (<= kChanPer), every load issued
-// before any math -- and reduce them in the workgroup (fixed shuffle tree per wave, then the
+// Alpha-backward tiling.  Weights with Co*K <= 2304 (ResNet-18 layer1 - layer3 3x3 convs)
+// and 1x1 weights with Co <= 256 take one workgroup per input channel (alpha_bwd_channel,
+// channels in XCD-aware order): its 256 threads take the channel's Co*K (row, tap) elements
+// -- thread t: elements t, t + 256, ..., kChanPer per batch, every load of a batch issued
+// before any math, the next batch while the current one is summed -- and reduce them in the
+// workgroup (fixed shuffle tree per wave, then the
 // 4 waves in order): one launch, no partials, and as many workgroups as input channels.
 // Larger weights keep the thread-column tiling of the forward (chunks of rows) and a stage-2
 // launch that sums the chunk partials.  The tiling depends only on the weight's own shape, so
@@ -110,6 +111,16 @@ constexpr uint32_t kChanPer = 5;                      // elements per thread per
 constexpr uint32_t kChanElems = kChanPer * kBlock;    // 1280: one batch
 constexpr uint32_t kChanBatches = 4;                  // batches in the per-channel form
 
+// XCD-aware channel order of the per-channel form: workgroups b and b + 8 share an XCD (and
+// its L2), and neighbouring input channels share cache lines (K = 9: a row's 36 B of channel
+// ci sit next to ci + 1's; K = 1: 32 channels per 128-B line), so the workgroups one XCD
+// runs take a contiguous run of channels: local workgroup j -> the (j / 8)-th channel of
+// run j % 8.  A bijection on [0, n) for any n; per-channel sums are unchanged.
+__device__ __forceinline__ uint32_t xcd_channel(uint32_t j, uint32_t n) {
+  const uint32_t q = n >> 3, rem = n & 7, r = j & 7;
+  return r * q + min(r, rem) + (j >> 3);
+}
+
 static ColTiling bwd_tiling_prep(const Geo& g) {
   // SSQ_K6P_FORM (A/B): 3 = the per-channel form where it fits, else thread-column (default);
   // 0 = thread-column stage 1 + stage 2 everywhere
@@ -118,12 +129,18 @@ static ColTiling bwd_tiling_prep(const Geo& g) {
   // with many rows is read as Co scattered words per workgroup (r4, cold whole-block launches:
   // layer4.0 with its 512-row downsample here 20.1 -> 26.3 us, layer3.0 with its 256-row one
   // 9.2 -> 11.8 us; layer2.0's 128-row one in a single launch 13.0 -> 9.8 us, stage 2
-  // included); SSQ_K6P_CHAN_CO for A/B
-  static const uint32_t kMaxCo = prep_env("SSQ_K6P_CHAN_CO", 128);
+  // included) -- before the XCD-aware channel order (xcd_channel), which puts the 32
+  // channels sharing a 1x1 row's cache line on one XCD; SSQ_K6P_CHAN_CO for A/B
+  static const uint32_t kMaxCo = prep_env("SSQ_K6P_CHAN_CO", 256);
   // elements per input channel the per-channel form takes: up to kChanBatches batches of
   // kChanPer per thread, each batch's loads issued while the previous one is summed
-  // (SSQ_K6P_CHAN_ELEMS, A/B; r4: one batch, 1280)
-  static const uint32_t kMaxElems = prep_env("SSQ_K6P_CHAN_ELEMS", kChanElems);
+  // (SSQ_K6P_CHAN_ELEMS, A/B).  r4: one batch (1280); r5: 2304 = ResNet-18 layer3's 3x3
+  // convs in two batches, so layer3 blocks take one launch.  Cold whole-block launches
+  // (profiles/r5_k6p_xcd_ab.txt), XCD order on: layer3.0 15.4 us in one launch vs 9.4 + 6.3
+  // in two; layer4 (Co*K = 4608, four batches) 29-34 us vs 20.4-24.1 + 6.2, so layer4 keeps
+  // two.  In the loop (bench.py recon, r5y): layer3.0 / 3.1 alpha backward 13.4 / 13.1 us vs
+  // 14.5 / 14.7, it/s 1996-1999 / 2024-2031 vs 1990-1991 / 2014-2023.
+  static const uint32_t kMaxElems = prep_env("SSQ_K6P_CHAN_ELEMS", 2304);
   if (kForm != 3 || g.Co * g.K > kMaxElems || g.Co * g.K > kChanBatches * kChanElems ||
       (g.Co > kMaxCo && g.K == 1))
     return col_tiling_prep(g);
@@ -134,7 +151,9 @@ static ColTiling bwd_tiling_prep(const Geo& g) {
   t.ncolblk = g.Ci;
   t.R = g.Co;
   t.nchunk = 1;
-  t.whole = 1;
+  // SSQ_K6P_XCD (A/B): 1 = XCD-aware channel order (whole = 2), 0 = channel = workgroup
+  static const uint32_t kXcd = prep_env("SSQ_K6P_XCD", 1);
+  t.whole = kXcd ? 2 : 1;
   return t;
 }
 
@@ -413,7 +432,8 @@ __global__ __launch_bounds__(kBlock) void alpha_bwd_prep(PrepTable tab, float re
   const Geo& g = sg.g;
   const uint32_t local = bid - sg.blk0;
   if (sg.tl.form == 3) {             // uniform per workgroup
-    alpha_bwd_channel<NS>(sg, tab.ac, local, red, reg_lambda, reg_b, reg_dev);
+    const uint32_t ci = sg.tl.whole == 2 ? xcd_channel(local, g.Ci) : local;
+    alpha_bwd_channel<NS>(sg, tab.ac, ci, red, reg_lambda, reg_b, reg_dev);
     return;
   }
   const uint32_t bx = local % sg.tl.ncolblk, by = local / sg.tl.ncolblk;
