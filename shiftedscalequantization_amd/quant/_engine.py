@@ -9,6 +9,8 @@ LazyValue: the reference calls .item() on the loss every iteration (a device->ho
 layer_recon_fused_shiftedScale.py:296-298); here loss values stay on the device and are
 read only when reported.
 """
+import math
+
 import numpy as np
 import torch
 
@@ -351,6 +353,38 @@ class SsqAdam:
         K.adam_step(live, [p.grad for p in live], [self.state[p]["exp_avg"] for p in live],
                     [self.state[p]["exp_avg_sq"] for p in live], b1, b2, g["eps"], hyper=hyper,
                     neg_step_size=nss, bc2_sqrt=bc2s)
+
+
+class CosineLR:
+    """The lr sequence of torch.optim.lr_scheduler.CosineAnnealingLR(T_max, eta_min) as the
+    reference's act phase steps it once per iteration (Brecq block_recon.py:56-58): the
+    scheduler's chainable recursion (CosineAnnealingLR.get_lr, torch 2.10) with the same
+    expressions in the same order, so every value is the same double
+    (tests/test_host.py pins it against torch's scheduler).  It replaces a shadow
+    torch.optim.Adam + scheduler: constructing the first torch optimizer of a process
+    imports torch._dynamo (0.78 s in the ResNet-18 flow's first act phase,
+    profiles/r5_e2e_setup_probe.txt), and each shadow step cost ~30 us of host time."""
+
+    def __init__(self, lr, T_max, eta_min=0.0):
+        self.base_lr = self.lr = lr
+        self.T_max = T_max
+        self.eta_min = eta_min
+        self.last_epoch = 0        # after the scheduler's initial step
+        self._step_count = 1
+
+    def step(self):
+        """One scheduler.step(); returns the new lr."""
+        self._step_count += 1
+        self.last_epoch += 1
+        e, T, m = self.last_epoch, self.T_max, self.eta_min
+        if self._step_count == 1 and e > 0:
+            self.lr = m + (self.base_lr - m) * (1 + math.cos((e) * math.pi / T)) / 2
+        elif (e - 1 - T) % (2 * T) == 0:
+            self.lr = self.lr + (self.base_lr - m) * (1 - math.cos(math.pi / T)) / 2
+        else:
+            self.lr = ((1 + math.cos(math.pi * e / T)) / (1 + math.cos(math.pi * (e - 1) / T))
+                       * (self.lr - m) + m)
+        return self.lr
 
 
 class frozen_except:

@@ -16,8 +16,8 @@ import torch
 from .. import kernels as K
 from ..parallel_dp import GradBucket, world
 from ._engine import (GRAPH_REPLAYS, ITER_PROBE, BatchFeeder, IterationGraph, LazyValue,
-                      SsqAdam, as_float, backward_tail, clear_stash, frozen_except, probe,
-                      stash_adaround)
+                      CosineLR, SsqAdam, as_float, backward_tail, clear_stash, frozen_except,
+                      probe, stash_adaround)
 from .adaptive_rounding import AdaRoundQuantizer
 from .data_utils import save_grad_data, save_inp_oup_data
 from .quant_block import BaseQuantBlock
@@ -252,8 +252,8 @@ def _fast_loop(block, qmodules, opt_params, loss_func, feeder, bucket, iters, ac
     final fused-epilogue ReLU), backward with the round loss's gradient folded into the
     AdaRound backward, fused Adam.  After GRAPH_WARMUP eager iterations the body is
     replayed from a HIP graph (at world > 1 as two graphs around the bucket all-reduce,
-    _engine.IterationGraph).  The cosine LR schedule is stepped by the
-    reference's own torch scheduler on a shadow optimizer and copied into Adam's device lr.
+    _engine.IterationGraph).  The cosine LR schedule (_engine.CosineLR: torch's
+    CosineAnnealingLR recursion, value for value) is copied into Adam's device lr.
     Launch savings (module knobs above, bit-identical on or off): deferred finalizes with the
     Adam step riding on them, the block's fused tail, and in the act phase pinned weights and
     the block-input convs precomputed for every cached sample."""
@@ -267,10 +267,9 @@ def _fast_loop(block, qmodules, opt_params, loss_func, feeder, bucket, iters, ac
     stash_ada = STASH_ADAROUND and not act_quant and isinstance(block, BaseQuantBlock)
     if act_quant:
         optimizer = SsqAdam(opt_params, lr=lr)
-        # the reference's cosine schedule, stepped by torch's own scheduler on a shadow
-        # optimizer so every lr value is the one the reference uses
-        shadow = torch.optim.Adam([torch.zeros(1, requires_grad=True)], lr=lr)
-        scheduler = torch.optim.lr_scheduler.CosineAnnealingLR(shadow, T_max=max(iters, 1), eta_min=0.)
+        # the reference's cosine schedule (CosineAnnealingLR(T_max=iters, eta_min=0)), value
+        # for value (_engine.CosineLR)
+        scheduler = CosineLR(lr, max(iters, 1), 0.)
     else:
         optimizer, scheduler = SsqAdam(opt_params), None
     regp, hyper = feeder.extra[0:2], feeder.extra[2:4]
@@ -376,7 +375,7 @@ def _fast_loop(block, qmodules, opt_params, loss_func, feeder, bucket, iters, ac
                     # an identity residual the only other reader: the input as a row view
                     rows_mode[1] = bool(ROWS_IN_PLACE and need_input[0] and ident
                                         and all(m in convs for m in ident))
-        _run(iters, loss_func, feeder, optimizer, scheduler, shadow if act_quant else None, use_graph,
+        _run(iters, loss_func, feeder, optimizer, scheduler, use_graph,
              bucket, body_pre, body_post, last, opt_params, ada, ws_cache)
 
 
@@ -432,7 +431,7 @@ class ChunkGraph:
         return e0.elapsed_time(e1) * 1e3 / (reps * self.n)
 
 
-def _run(iters, loss_func, feeder, optimizer, scheduler, shadow, use_graph, bucket, body_pre,
+def _run(iters, loss_func, feeder, optimizer, scheduler, use_graph, bucket, body_pre,
          body_post, last, opt_params, ada, ws_cache):
     graph_obj = None
     graph_last = {}
@@ -464,9 +463,7 @@ def _run(iters, loss_func, feeder, optimizer, scheduler, shadow, use_graph, buck
                 # the round-loss value from alpha before this step (the chunk's first)
                 rnd = loss_func.round_value(b)
             if scheduler is not None:
-                shadow.step()
-                scheduler.step()
-                optimizer.param_groups[0]['lr'] = shadow.param_groups[0]['lr']
+                optimizer.param_groups[0]['lr'] = scheduler.step()
         feeder.stage_chunk(perms, extras)
         if chunk_obj is None:
             chunk_obj = ChunkGraph(body, optimizer, feeder, n, ws_cache, last)
@@ -499,9 +496,7 @@ def _run(iters, loss_func, feeder, optimizer, scheduler, shadow, use_graph, buck
             if (skip_ok and last.get('step') is False and loss_func.count % 500 != 0
                     and i != iters - 1):
                 if scheduler is not None:
-                    shadow.step()
-                    scheduler.step()
-                    optimizer.param_groups[0]['lr'] = shadow.param_groups[0]['lr']
+                    optimizer.param_groups[0]['lr'] = scheduler.step()
                 i += 1
                 continue
             feeder.stage(perm, extra=(lam, float(b)) + hyp)
@@ -532,9 +527,7 @@ def _run(iters, loss_func, feeder, optimizer, scheduler, shadow, use_graph, buck
             rec = last['rec'][0]
             loss_func.record(rec, rnd, b)
             if scheduler is not None:
-                shadow.step()
-                scheduler.step()
-                optimizer.param_groups[0]['lr'] = shadow.param_groups[0]['lr']
+                optimizer.param_groups[0]['lr'] = scheduler.step()
             i += 1
         if ITER_HOOK is not None:
             ITER_HOOK(iters, iters)

@@ -73,6 +73,22 @@ def test_schedules_match_reference(golden):
         assert lsh(t) == g["sched_lsh"][t]
 
 
+@pytest.mark.parametrize("lr,T", [(4e-5, 5000), (4e-4, 20000), (1e-3, 1), (4e-5, 7), (3e-3, 100)])
+def test_cosine_lr_matches_torch_scheduler(lr, T):
+    """The act phase's lr sequence (_engine.CosineLR) is the reference's
+    CosineAnnealingLR(T_max=iters, eta_min=0.) stepped once per iteration
+    (Brecq/quant/block_recon.py:56-58), equal as doubles at every step (a few past T_max
+    too: the scheduler's restart branch)."""
+    from shiftedscalequantization_amd.quant._engine import CosineLR
+    opt = torch.optim.Adam([torch.zeros(1, requires_grad=True)], lr=lr)
+    sch = torch.optim.lr_scheduler.CosineAnnealingLR(opt, T_max=T, eta_min=0.)
+    mine = CosineLR(lr, T, 0.)
+    for k in range(T + 3):
+        opt.step()
+        sch.step()
+        assert mine.step() == opt.param_groups[0]["lr"], k
+
+
 def test_quant_model_structure_resnet18():
     """QuantModel wraps the 21 conv/fc layers, 8 BasicBlocks, sets 8-bit stem/head and
     path names exactly as the reference (quant_model.py:15-69)."""

@@ -1237,8 +1237,11 @@ def test_channel_quant_act_golden(K, golden):
 
 
 # ------------------------------------------------------------------ round 2: prepared adaShift
+# (256, 64, 3, 3) and (200, 37, 3, 3): the alpha backward's per-channel form in two load
+# batches (Co*K 1281-2304), the latter with Ci not a multiple of the 8 XCDs (xcd_channel)
 PREP_SHAPES = [(8, 6, 3, 3), (64, 64, 3, 3), (96, 48, 3, 3), (128, 64, 1, 1), (33, 5, 5, 5),
-               (24, 1, 3, 3), (512, 512, 3, 3), (256, 128, 1, 1), (7, 300, 1, 1)]
+               (24, 1, 3, 3), (512, 512, 3, 3), (256, 128, 1, 1), (7, 300, 1, 1),
+               (256, 64, 3, 3), (200, 37, 3, 3)]
 
 
 @pytest.mark.parametrize("shape", PREP_SHAPES)
@@ -1289,7 +1292,8 @@ def test_adashift_prepared_multi_equals_single(K):
     more in further launches) give each weight's single-launch What and alpha gradient
     bit for bit, with per-weight regulariser values."""
     shapes = [(64, 64, 3, 3), (128, 64, 3, 3), (128, 64, 1, 1), (7, 300, 1, 1), (24, 1, 3, 3),
-              (33, 5, 5, 5), (96, 48, 3, 3), (512, 256, 3, 3), (16, 16, 3, 3), (40, 24, 1, 1)]
+              (33, 5, 5, 5), (96, 48, 3, 3), (512, 256, 3, 3), (16, 16, 3, 3), (40, 24, 1, 1),
+              (256, 128, 3, 3), (256, 100, 1, 1)]
     gen = torch.Generator().manual_seed(11)
     regp = dev([0.1, 7.5])
     alphas, entries, gys, singles = [], [], [], []
