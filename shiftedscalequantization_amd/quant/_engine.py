@@ -168,6 +168,33 @@ class BatchFeeder:
         return self.inp[:n], self.out[:n]
 
 
+try:
+    from torch.autograd.graph import _engine_run_backward
+except ImportError:         # another torch: its public entry point
+    _engine_run_backward = None
+
+
+def run_backward(roots, grads):
+    """torch.autograd.backward(roots, grads) for gradients the loop built to match their roots
+    (shape, dtype and device checked here), handed straight to the autograd engine as
+    torch.autograd.backward hands them after its own check.  That check (_make_grads)
+    imports torch.fx's symbolic-shape module on its first call with a gradient tensor: 0.78 s
+    in the flow's first shift loop (profiles/r5_e2e_setup_probe.txt); the reference's
+    backward starts from a scalar loss and never pays it."""
+    roots, grads = tuple(roots), tuple(grads)
+    if len(roots) != len(grads):
+        raise RuntimeError("run_backward: one gradient per root")
+    for r, g in zip(roots, grads):
+        if r.shape != g.shape or r.dtype != g.dtype or r.device != g.device:
+            raise RuntimeError(f"run_backward: gradient {tuple(g.shape)} {g.dtype} {g.device} "
+                               f"for a root {tuple(r.shape)} {r.dtype} {r.device}")
+    if _engine_run_backward is None:
+        torch.autograd.backward(roots, grads)
+        return
+    _engine_run_backward(roots, grads, False, False, (), allow_unreachable=True,
+                         accumulate_grad=True)
+
+
 def backward_tail(tail, grads):
     """Resume autograd at a fused tail's inputs: the conv output y and the residual through
     their graphs; gamma^z / phi^z / the act quantizer's delta and zero point are leaves here
@@ -201,7 +228,7 @@ def backward_tail(tail, grads):
         else:
             roots.append(t)
             grs.append(g)
-    torch.autograd.backward(roots, grs)
+    run_backward(roots, grs)
 
 
 def stash_block_weights(quantizers):

@@ -17,7 +17,7 @@ from .. import kernels as K
 from ..parallel_dp import GradBucket, world
 from ._engine import (GRAPH_REPLAYS, ITER_PROBE, BatchFeeder, IterationGraph, LazyValue,
                       CosineLR, SsqAdam, as_float, backward_tail, clear_stash, frozen_except,
-                      probe, stash_adaround)
+                      probe, run_backward, stash_adaround)
 from .adaptive_rounding import AdaRoundQuantizer
 from .data_utils import save_grad_data, save_inp_oup_data
 from .quant_block import BaseQuantBlock
@@ -330,10 +330,10 @@ def _fast_loop(block, qmodules, opt_params, loss_func, feeder, bucket, iters, ac
             return
         if relu_in:
             rec, g = K.lp_loss_and_grad(out, cur_out, p, relu_mask=True)
-            torch.autograd.backward(list(relu_in), [g] * len(relu_in))
+            run_backward(list(relu_in), [g] * len(relu_in))
         else:
             rec, g = K.lp_loss_and_grad(out, cur_out, p)
-            out.backward(g)
+            run_backward([out], [g])
         last['rec'] = rec
         last['step'] = True
 

@@ -20,7 +20,7 @@ from tqdm import tqdm
 from .. import kernels as K
 from ..parallel_dp import GradBucket, world
 from ._engine import (BatchFeeder, IterationGraph, LazyValue, SsqAdam, as_float, backward_tail,
-                      clear_stash, probe, stash_block_weights)
+                      clear_stash, probe, run_backward, stash_block_weights)
 from .quant_block import BaseQuantBlock
 from .quant_layer import QuantModule
 
@@ -151,10 +151,10 @@ def _fused_loop(block, modules, iters, lmda, model, p, lr, bias_cal, batch_size,
             # the block ends in the fused epilogue's ReLU: the loss pass writes the gradient
             # at the ReLU's input and backward starts from the epilogue's inputs
             rec, g_pre = loss_func.loss_and_grad(quant_out, cur_out, relu_mask=True)
-            torch.autograd.backward(list(relu_in), [g_pre] * len(relu_in))
+            run_backward(list(relu_in), [g_pre] * len(relu_in))
         else:
             rec, g_out = loss_func.loss_and_grad(quant_out, cur_out)
-            quant_out.backward(g_out)
+            run_backward([quant_out], [g_out])
         last['rec'] = rec
 
     def body_post():
