@@ -139,19 +139,51 @@ __global__ __launch_bounds__(kBlock) void bias_act_kernel(const float* __restric
     qp.d = qdelta[0];
     qp.z = qzp[0];
   }
+  // channel c's operands applied to one element (the reference's op order)
+  auto epi = [&](float v, float rv, float bc, float gc, float pc) {
+    float t = bias ? __fadd_rn(v, bc) : v;
+    if (AFFINE) t = __fadd_rn(__fmul_rn(t, gc), pc);  // out*alpha_out + beta_out
+    if (RES) t = __fadd_rn(t, rv);
+    return act_fwd<ACT>(t);  // torch clamp: keeps -0 and NaN
+  };
   auto one = [&](uint32_t i, float v, float rv) {
     const uint32_t q = fdiv(i, div_hw);
     const uint32_t c = q - fdiv(q, div_c) * C;
-    float t = bias ? __fadd_rn(v, bias[c]) : v;
-    if (AFFINE) t = __fadd_rn(__fmul_rn(t, gamma[c]), phi[c]);  // out*alpha_out + beta_out
-    if (RES) t = __fadd_rn(t, rv);
-    return act_fwd<ACT>(t);  // torch clamp: keeps -0 and NaN
+    return epi(v, rv, bias ? bias[c] : 0.0f, AFFINE ? gamma[c] : 1.0f, AFFINE ? phi[c] : 0.0f);
   };
   auto fq = [&](float t) {
     float q;
     return fq1(t, qp, &q);
   };
-  if (vec) {
+  if (vec == 2) {
+    // hw % 4 == 0: a float4 lies in one (n, c) plane -- one channel lookup, one row-map
+    // lookup and one set of channel operands per float4 instead of per element (the
+    // act-quant form of this pass is VALU-bound: the divide of the fake quant)
+    const uint32_t n4 = n / 4;
+    for (uint32_t v = blockIdx.x * blockDim.x + threadIdx.x; v < n4; v += stride) {
+      const uint32_t i = 4 * v, q = fdiv(i, div_hw), nn = fdiv(q, div_c), c = q - nn * C;
+      const uint32_t inrow = i - nn * chw;
+      const f32x4 a = *(const f32x4*)(y + (yrows ? yrows[nn] * (int64_t)chw + inrow : (int64_t)i));
+      f32x4 rr = {0.0f, 0.0f, 0.0f, 0.0f};
+      if (RES) rr = *(const f32x4*)(res + (rrows ? rrows[nn] * (int64_t)chw + inrow : (int64_t)i));
+      const float bc = bias ? bias[c] : 0.0f;
+      const float gc = AFFINE ? gamma[c] : 1.0f, pc = AFFINE ? phi[c] : 0.0f;
+      f32x4 o;
+      o.x = epi(a.x, rr.x, bc, gc, pc);
+      o.y = epi(a.y, rr.y, bc, gc, pc);
+      o.z = epi(a.z, rr.z, bc, gc, pc);
+      o.w = epi(a.w, rr.w, bc, gc, pc);
+      if (!QUANT || out) ((f32x4*)out)[v] = o;
+      if (QUANT) {
+        f32x4 r;
+        r.x = fq(o.x);
+        r.y = fq(o.y);
+        r.z = fq(o.z);
+        r.w = fq(o.w);
+        ((f32x4*)yq)[v] = r;
+      }
+    }
+  } else if (vec) {
     const uint32_t n4 = n / 4;
     for (uint32_t v = blockIdx.x * blockDim.x + threadIdx.x; v < n4; v += stride) {
       const f32x4 a = *(const f32x4*)(y + off(yrows, 4 * v));   // hw % 4 == 0 with a map
@@ -1012,8 +1044,12 @@ static int bias_act(const char* what, const float* y, const float* bias, const f
   SSQ_REQUIRE(!rrows || res, SSQ_E_ARG, "%s: res_rows without res", what);
   SSQ_REQUIRE(!stage_dst || (stage_src && stage_n > 0 && stage_n <= 4096), SSQ_E_ARG,
               "%s: staging needs a source and 1..4096 words", what);
-  const int vec = n % 4 == 0 && al(y) && (!out || al(out)) && (!res || al(res)) &&
-                  (!yq || al(yq)) && ((!yrows && !rrows) || hw % 4 == 0);
+  // vec 2: float4s that never straddle an (n, c) plane (SSQ_K13_PLANE4=0: the per-element
+  // channel form, for A/B)
+  static const bool kPlane4 = !getenv("SSQ_K13_PLANE4") || atoi(getenv("SSQ_K13_PLANE4")) != 0;
+  int vec = n % 4 == 0 && al(y) && (!out || al(out)) && (!res || al(res)) &&
+            (!yq || al(yq)) && ((!yrows && !rrows) || hw % 4 == 0);
+  if (vec && hw % 4 == 0 && kPlane4) vec = 2;
   const FastDiv dh = make_fastdiv((uint32_t)hw), dc = make_fastdiv((uint32_t)C);
   const dim3 grid(grid_for(vec ? n / 4 : n, kBlock, 2048));
   const float lo = (float)qmin, hi = (float)qmax;
