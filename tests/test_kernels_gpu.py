@@ -696,6 +696,19 @@ def _set_affine(qb):
 
 
 def _compare_fused_unfused(qb, x, act, affine=()):
+    # under the reference's cudnn.deterministic (as the folded-epilogue test): MIOpen's solver
+    # choice, and with it the forward's values, then no longer varies from box to box -- the
+    # affine act-delta bound below is cancellation-sensitive to those values (r5ev5: one box
+    # 3.6e-3 off on ~18 where others stay inside 2.8e-3)
+    det = torch.backends.cudnn.deterministic
+    torch.backends.cudnn.deterministic = True
+    try:
+        _compare_fused_unfused_det(qb, x, act, affine)
+    finally:
+        torch.backends.cudnn.deterministic = det
+
+
+def _compare_fused_unfused_det(qb, x, act, affine=()):
     from shiftedscalequantization_amd import quant as Q
     outs = []
     g = torch.randn(1, generator=torch.Generator().manual_seed(1))
