@@ -269,9 +269,20 @@ __global__ __launch_bounds__(kBlock) void shift_fwd_prep(PrepTable tab) {
 
 // The iteration start (prep_ride.h): workgroups [0, ngw) gather the batch rows, the rest
 // run the queued prepared forward.
+// nfwd > 0: the forward's nfwd workgroups come first (dispatched first, so their short,
+// latency-bound bodies run beside the gather's stream instead of after it); 0: after.
 template <bool VEC, int NS, int HARD_T>
 __global__ __launch_bounds__(kBlock) void gather_shift_fwd(GatherArgs ga, uint32_t ngw,
-                                                           PrepTable tab) {
+                                                           PrepTable tab, uint32_t nfwd) {
+  if (nfwd) {
+    if (blockIdx.x < nfwd) {
+      shift_fwd_body<NS, HARD_T>(tab, blockIdx.x);
+      return;
+    }
+    const uint32_t b = blockIdx.x - nfwd;
+    gather2_body<VEC>(ga, b % ga.gx, b / ga.gx);
+    return;
+  }
   if (blockIdx.x < ngw) {
     gather2_body<VEC>(ga, blockIdx.x % ga.gx, blockIdx.x / ga.gx);
     return;
@@ -686,12 +697,20 @@ int launch_gather(hipStream_t s, const GatherArgs& a, bool vec) {
   g_fwd_pend.on = false;
   const uint32_t ngw = a.gx * a.nrows;
   const dim3 grid(ngw + f.blk);
+  // The forward's workgroups first in the grid when they are a short tail beside the gather
+  // (at most half its workgroups: ResNet-18 layer1 - layer3); after it when the forward is
+  // the launch's bulk (layer4: 56 MB of weights against a 13 MB batch), so the What the
+  // next conv reads are the launch's last writes.  bench.py's recon loops (r5k5, ABAB):
+  // forward first, traced start launch 0.4-1.2 us shorter on every block and layer3 it/s
+  // +0.7 %, but layer4.0 / 4.1 -0.6 / -1.6 %.  SSQ_K5P_FIRST=0: always after (A/B).
+  static const bool kFirst = prep_env("SSQ_K5P_FIRST", 1) != 0;
+  const uint32_t nfwd = kFirst && 2 * f.blk <= ngw ? f.blk : 0;
 #define SSQ_GF(V, NS)                                                                        \
   do {                                                                                       \
     if (f.hard)                                                                              \
-      hipLaunchKernelGGL((gather_shift_fwd<V, NS, 1>), grid, dim3(kBlock), 0, s, a, ngw, f.tab); \
+      hipLaunchKernelGGL((gather_shift_fwd<V, NS, 1>), grid, dim3(kBlock), 0, s, a, ngw, f.tab, nfwd); \
     else                                                                                     \
-      hipLaunchKernelGGL((gather_shift_fwd<V, NS, 0>), grid, dim3(kBlock), 0, s, a, ngw, f.tab); \
+      hipLaunchKernelGGL((gather_shift_fwd<V, NS, 0>), grid, dim3(kBlock), 0, s, a, ngw, f.tab, nfwd); \
   } while (0)
 #define SSQ_GFS(V)                    \
   switch (f.S) {                      \
