@@ -732,8 +732,11 @@ def _compare_fused_unfused_det(qb, x, act, affine=()):
         if affine:
             # the affine epilogue reduces the act-delta sums per (n, c) row and takes the
             # (x/d)/d term exactly as torch's div backward; the float4 fq backward uses
-            # (x/d)*(1/d): one ulp per term of two sums of ~1e2 that cancel to ~1e-2
-            np.testing.assert_allclose(a, b, rtol=1e-4, atol=1e-3)
+            # (x/d)*(1/d): one ulp per term of two sums of ~1e2 that cancel to ~1e-2.
+            # The forward's values (MIOpen's solver pick) differ between box types, and with
+            # them the cancellation: observed up to 2.0e-4 relative on one type (r5ev5,
+            # r5ev7b: 18.1153 vs 18.1189), < 1e-4 on the others
+            np.testing.assert_allclose(a, b, rtol=1e-3, atol=1e-3)
         else:
             np.testing.assert_array_equal(a, b)
     for a, b in zip(outs[0][3], outs[1][3]):   # gamma / phi: double vs torch's fp32 sums
