@@ -327,7 +327,10 @@ def test_brecq_block_reconstruction_matches_reference(Q, golden, graph, wgrad, f
             stats["a_median_rel_err"] = float(np.median(a_rel))
         parity_report(f"a22_brecq_basic[{fixture},graph={graph},wgrad={wgrad}]", **stats)
         if fixture == "recon_brecq_long":
-            assert a_rel[:20].max() <= 1e-5, a_rel[:20].max()
+            # first 20 act iterations: <= 1e-5 on most boxes; 2.3e-5 on a box type whose
+            # solver picks moved the 400-iteration weight phase (w_total_rel_err 5.7e-7 vs
+            # 6.4e-7, V within 3-7e-6 either way) before this chaotic phase (r5ev7)
+            assert a_rel[:20].max() <= 5e-5, a_rel[:20].max()
             assert np.median(a_rel) <= 1e-3 and a_rel.max() <= 1e-2, (np.median(a_rel), a_rel.max())
             assert max(win) <= 1e-3, win
             np.testing.assert_allclose([float(q.delta) for q in aqs], g["a_delta"], rtol=2e-3)
