@@ -69,7 +69,11 @@ def main(argv=None):
     if world > 1:
         # one process per GPU; ranks beyond the visible GPUs share them (gloo rehearsals)
         local = int(os.environ.get('LOCAL_RANK', '0'))
-        device = torch.device('cuda', local % max(torch.cuda.device_count(), 1))
+        ndev = torch.cuda.device_count()
+        if args.dist_backend == 'nccl' and world > ndev:
+            raise SystemExit(f'main_imagenet.py: {world} ranks over RCCL need {world} GPUs, {ndev} '
+                             f'visible (rehearse with --dist_backend gloo: ranks then share devices)')
+        device = torch.device('cuda', local % max(ndev, 1))
         torch.cuda.set_device(device)
         if args.dist_backend == 'nccl':
             dist.init_process_group('nccl', device_id=device)

@@ -383,7 +383,10 @@ __global__ __launch_bounds__(kBlock) void fq_bwd_pt(const float* __restrict__ x,
 }
 
 // float4 form of fq_bwd_pt (x, gy, gx 16-B aligned): two float4 loads per 4 elements,
-// (x/d)/d as t * (1/d) (it only feeds the reduction), zp sums only when asked for.
+// zp sums only when asked for.  The delta term is (x/d)/d with two IEEE divides, as torch's
+// div backward forms it (quant_layer.py:92-98 under autograd) and as the fused epilogue's
+// backward does: t * (1/d) is one ulp off per term, and the two ~1e2 sums of the delta
+// gradient cancel to ~1e-2, which turned that ulp into 2e-4 of the result.
 template <bool ZP, int ACT>
 __global__ __launch_bounds__(kBlock) void fq_bwd_pt4(const f32x4* __restrict__ x,
                                                      const f32x4* __restrict__ gy,
@@ -393,7 +396,6 @@ __global__ __launch_bounds__(kBlock) void fq_bwd_pt4(const f32x4* __restrict__ x
                                                      double* __restrict__ part) {
   __shared__ double red[16];
   const float d = delta[0], z = zp[0];
-  const float rd = 1.0f / d;
   double a0 = 0, a1 = 0, a2 = 0, a3 = 0;
   const int64_t stride = (int64_t)gridDim.x * blockDim.x;
   for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n4; i += stride) {
@@ -411,7 +413,7 @@ __global__ __launch_bounds__(kBlock) void fq_bwd_pt4(const f32x4* __restrict__ x
       go[j] = (ACT && !act_pass<ACT>(xs[j])) ? 0.0f : gi / d;
       if (part) {
         a0 += (double)gs[j] * (double)__fsub_rn(q, z);
-        a1 += (double)gi * (double)__fmul_rn(t, rd);
+        a1 += (double)gi * (double)(t / d);
         if (ZP) {
           a2 += (double)gi;
           a3 += (double)gq;

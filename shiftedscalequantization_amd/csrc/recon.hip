@@ -16,8 +16,6 @@
 
 namespace ssq {
 
-__device__ unsigned g_loss_ticket;   // lp_loss_kernel's last-arriver counter (zero at rest)
-
 // Target rows: tgt itself, or (GATHER) rows idx[r] of a [N, row] cache, r = i / row, so the
 // loop's batch target is never materialised.
 struct TgtRows {
@@ -44,7 +42,8 @@ __global__ __launch_bounds__(kBlock) void lp_loss_kernel(const float* __restrict
                                                          int relu_mask, int vec, TgtRows tr4,
                                                          TgtRows tr1,
                                                          double* __restrict__ part, double m,
-                                                         float* __restrict__ loss_out) {
+                                                         float* __restrict__ loss_out,
+                                                         unsigned* __restrict__ ticket) {
   __shared__ double red[16];
   double acc = 0.0;
   const float gs = gscale ? gscale[0] : 1.0f;
@@ -76,8 +75,10 @@ __global__ __launch_bounds__(kBlock) void lp_loss_kernel(const float* __restrict
     return;
   }
   if (threadIdx.x == 0) st_sc1(part + blockIdx.x, acc);
-  // one-launch form: the last workgroup to finish sums the partials in index order
-  if (!arrive_last(&g_loss_ticket, gridDim.x, (int*)red)) return;
+  // one-launch form: the last workgroup to finish sums the partials in index order.  The
+  // counter is the call's own (a word of its workspace after the partials), so calls in
+  // flight on other streams with other workspaces never count each other's workgroups
+  if (!arrive_last(ticket, gridDim.x, (int*)red)) return;
   double v[kLossBlocks / kBlock];
 #pragma unroll
   for (int k = 0; k < kLossBlocks / kBlock; ++k) {
@@ -889,9 +890,13 @@ static FinTable fin_take_for_host(hipStream_t s, const void* w0, size_t wn, int*
 
 using namespace ssq;
 
+// the partials, then the one-launch form's last-arriver counter (lp_loss_ticket)
 extern "C" size_t ssq_lp_loss_workspace_size(int64_t n) {
   (void)n;
-  return kLossBlocks * sizeof(double);
+  return kLossBlocks * sizeof(double) + sizeof(double);
+}
+static unsigned* lp_loss_ticket(void* ws) {
+  return (unsigned*)((char*)ws + kLossBlocks * sizeof(double));
 }
 
 static int lp_loss(const char* what, const float* pred, const float* tgt, const int64_t* idx,
@@ -930,7 +935,8 @@ static int lp_loss(const char* what, const float* pred, const float* tgt, const 
   }();
   const bool fuse = one && loss_out;
   hipLaunchKernelGGL(k, dim3(grid), dim3(kBlock), 0, s, pred, tgt, n, p, inv_m, grad, gscale,
-                     relu_mask, vec, tr4, tr1, part, (double)M, fuse ? loss_out : nullptr);
+                     relu_mask, vec, tr4, tr1, part, (double)M, fuse ? loss_out : nullptr,
+                     fuse ? lp_loss_ticket(ws) : nullptr);
   if (loss_out && !fuse) {
     if (fin_defer_on()) {
       FinTask t{};

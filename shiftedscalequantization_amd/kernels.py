@@ -900,13 +900,16 @@ def rows_of(t):
 
 
 class row_views:
-    """Context of a loop that registers row views: the registry is emptied on exit."""
+    """Context of a loop that registers row views: the registry and any stage still pending
+    (a capture that raised between rows_lazy and the kernel that takes it) are emptied on
+    exit, so no later call performs an old loop's copy."""
 
     def __enter__(self):
         return self
 
     def __exit__(self, *exc):
         A.ROW_VIEWS.clear()
+        A.ROW_STAGE.clear()
 
 
 def lp_loss_and_grad(pred, tgt, p=2.0, reduction="none", want_grad=True, loss_out=None,

@@ -222,7 +222,7 @@ def _fc_fused_body(layer, qmodules, act_quant, p, bucket, feeder, optimizer, las
             and 1 <= feeder.bs <= 64 and Ci % 64 == 0 and 64 <= Ci <= 4096
             and feeder.inp.data_ptr() % 16 == 0):
         return None
-    if optimizer.params != [v]:
+    if len(optimizer.params) != 1 or optimizer.params[0] is not v:
         return None
     st = optimizer.state[v]
     b1, b2 = optimizer.param_groups[0]["betas"]
@@ -412,6 +412,7 @@ class ChunkGraph:
                         self.recs.append(last['rec'])
         finally:
             feeder.slot = None
+            K.A.ROW_STAGE.clear()      # a stage queued by a capture that raised
         self.graph = g
         self.grads = [p.grad for p in optimizer.params]
 

@@ -919,12 +919,48 @@ def gen_recon_brecq(iters=10, n_cali=16, res=16, name="recon_brecq", affine=Fals
                                    if m.act_quantizer.delta is not None]
     out["a_delta0"] = np.array([float(q.delta) for q in aqs], np.float32)
     out["a_zp0"] = np.array([float(q.zero_point) for q in aqs], np.float32)
+    # act_truth > 0: the first act_truth act iterations' loss also in float64 at the fp32 run's
+    # own state and batch -- the reference's distance from exact arithmetic, activation
+    # rounding decisions included (recon_brecq_long)
+    act_truth = 20 if name == "recon_brecq_long" else 0
+    cache, l64s = {}, []
+    orig_save = BR.save_inp_oup_data
+
+    def save_io(*a, **k):
+        r = orig_save(*a, **k)
+        cache["inp"], cache["out"] = r
+        return r
+
     torch.manual_seed(1005)
-    with _Spy(BR.LossFunction) as spy:
-        BR.block_reconstruction(qnn, block, cali, batch_size=8, iters=iters, act_quant=True,
-                                opt_mode="mse", lr=4e-4, p=2.4)
+    BR.save_inp_oup_data = save_io
+    try:
+        with _Spy(BR.LossFunction) as spy:
+            if act_truth:
+                orig_call = BR.LossFunction.__call__
+
+                def call64(lf, pred, tgt, grad=None):
+                    r = orig_call(lf, pred, tgt, grad)
+                    if len(l64s) < act_truth:
+                        import copy
+                        b64 = _to64(copy.deepcopy(block))
+                        perm = spy.perms[-1][:8]
+                        with torch.no_grad():
+                            y64 = b64(cache["inp"][perm].double())
+                            l64s.append(float(BR.lp_loss(y64, cache["out"][perm].double(), p=2.4)))
+                    return r
+                BR.LossFunction.__call__ = call64
+            try:
+                BR.block_reconstruction(qnn, block, cali, batch_size=8, iters=iters, act_quant=True,
+                                        opt_mode="mse", lr=4e-4, p=2.4)
+            finally:
+                if act_truth:
+                    BR.LossFunction.__call__ = orig_call
+    finally:
+        BR.save_inp_oup_data = orig_save
     out["a_perms"] = np.stack([p.numpy() for p in spy.perms]).astype(np.int64)
     out["a_total_loss"] = np.array([r[1] for r in spy.rec], np.float64)
+    if act_truth:
+        out["a_total_loss64"] = np.array(l64s, np.float64)
     out["a_delta"] = np.array([float(q.delta) for q in aqs], np.float32)
     out["iters"] = np.array([iters])
     save(name, **out)
@@ -980,6 +1016,115 @@ def gen_recon_layer_brecq(iters=10, n_cali=16, res=16):
         out["logits"] = t2n(qnn(cali))
     out["iters"] = np.array([iters])
     save("recon_layer_brecq", **out)
+
+
+FC_GRAD_STEPS = (0, 45, 199)
+
+
+def gen_recon_layer_brecq_fc(iters=200, n_cali=64, bs=32, grad_steps=FC_GRAD_STEPS):
+    """a22 on the fc loop as production runs it (the fused K19 pair, taken when C_in % 64 ==
+    0): layer_reconstruction (quant/layer_recon.py:10-104, LossFunction :107-168) on the last
+    layer of Linear(64, 512) -> ReLU -> Linear(512, 40) (40 = 2.5 16-row tiles: a
+    partial tile as ResNet-18's 1000 outputs have), 8-bit by set_first_last_layer_to_8bit
+    (quant_model.py:58-68) as ResNet-18's fc, asym capture (its input carries the first
+    layer's 8-bit weights and the ReLU, as the fc's avgpool features do), batch 32 of 64
+    cached samples, 200 iterations: the b schedule's warm-up (40 iterations), its decay and
+    its end.  Recorded: the captured input / target, every batch draw, every iteration's
+    rec (lp_loss) and total loss with the float64 rec loss at the fp32 run's own state (the
+    reference's distance from exact arithmetic), V and its gradient before the Adam steps in
+    grad_steps with the float64 gradient there, the final V and the hard W^."""
+    import copy
+    from quant import layer_recon as LR
+    torch.manual_seed(1005)
+    net = nn.Sequential(nn.Linear(64, 512), nn.ReLU(), nn.Linear(512, 40)).eval()
+    wq = {"n_bits": 4, "channel_wise": True, "scale_method": "max", "tune_delta_zero": False,
+          "symmetric": False}
+    aq = {"n_bits": 8, "channel_wise": False, "scale_method": "max", "tune_delta_zero": False,
+          "leaf_param": True, "symmetric": False}
+    qnn = QuantModel(model=net, weight_quant_params=wq, act_quant_params=aq)
+    qnn.eval()
+    qnn.set_first_last_layer_to_8bit()
+    torch.manual_seed(1005)
+    cali = torch.randn(n_cali, 64)
+    qnn.set_quant_state(True, False)
+    with torch.no_grad():
+        qnn(cali[:8])
+    layer = qnn.model[2]
+    assert isinstance(layer, QuantModule) and layer.weight_quantizer.n_bits == 8
+    out = {"cali": t2n(cali)}
+    _dump_qms(out, qnn, "")
+    cache, recs, busy = {}, [], [False]
+    orig_save, orig_lp = LR.save_inp_oup_data, LR.lp_loss
+
+    def save_io(*a, **k):
+        r = orig_save(*a, **k)
+        cache["inp"], cache["out"] = r[0].clone(), r[1].clone()
+        return r
+
+    def lp(pred, tgt, p=2.0, reduction="none"):
+        r = orig_lp(pred, tgt, p=p, reduction=reduction)
+        if not busy[0]:
+            busy[0] = True
+            try:      # the same loss in float64 at this iteration's state and batch
+                l64 = _to64(copy.deepcopy(layer))
+                perm = spy.perms[-1][:bs]
+                with torch.no_grad():
+                    r64 = orig_lp(l64(cache["inp"][perm].double()), cache["out"][perm].double(),
+                                  p=p, reduction=reduction)
+                recs.append((float(r.item()), float(r64.item())))
+            finally:
+                busy[0] = False
+        return r
+
+    def truth(step):
+        busy[0] = True
+        try:
+            l64 = _to64(copy.deepcopy(layer))
+            q = l64.weight_quantizer
+            q.alpha.grad = None
+            lf = LR.LossFunction(l64, round_loss="relaxation", weight=0.01, max_count=iters,
+                                 rec_loss="mse", b_range=(20, 2), decay_start=0, warmup=0.2, p=2.0)
+            lf.count = step
+            perm = spy.perms[-1][:bs]
+            spy.orig_call(lf, l64(cache["inp"][perm].double()),
+                          cache["out"][perm].double()).backward()
+            return [np.asarray(q.alpha.grad.detach().numpy(), np.float64).copy()]
+        finally:
+            busy[0] = False
+
+    LR.save_inp_oup_data, LR.lp_loss = save_io, lp
+    try:
+        torch.manual_seed(1005)
+        with _Spy(LR.LossFunction) as spy, _GradSpy(grad_steps, truth) as gspy:
+            LR.layer_reconstruction(qnn, layer, cali, batch_size=bs, iters=iters, weight=0.01,
+                                    asym=True, b_range=(20, 2), warmup=0.2, act_quant=False,
+                                    opt_mode="mse")
+    finally:
+        LR.save_inp_oup_data, LR.lp_loss = orig_save, orig_lp
+    out["cached_inp"], out["cached_out"] = t2n(cache["inp"]), t2n(cache["out"])
+    # the draws of N = 64: the batch is each draw's first bs entries
+    out["perms"] = np.stack([p.numpy()[:bs] for p in spy.perms]).astype(np.int16)
+    out["total_loss"] = np.array([r[1] for r in spy.rec], np.float64)
+    out["rec_loss"] = np.array([r[0] for r in recs], np.float64)
+    out["rec_loss64"] = np.array([r[1] for r in recs], np.float64)
+    for s, (ps, gs) in sorted(gspy.rec.items()):
+        out[f"gs{s}_V"], out[f"gs{s}_g"] = ps[0], gs[0]
+        # the float64 gradient as its offset from the reference's fp32 one (fp32 holds the
+        # offset to ~1e-7 of itself: far below either side's distance from it)
+        out[f"gs{s}_t_minus_g"] = f32(gspy.rec64[s][0] - gs[0].astype(np.float64))
+    out["grad_steps"] = np.array(sorted(gspy.rec), np.int64)
+    q = layer.weight_quantizer
+    out["V"] = t2n(q.alpha)
+    with torch.no_grad():
+        what = t2n(q(layer.weight))
+    # the hard W^ as its 8-bit codes: (code - zp) * delta in fp32 gives it back bit for bit
+    d, z = out["qm1_delta"][:, None], out["qm1_zp"][:, None]
+    codes = np.rint(what / d + z)
+    assert codes.min() >= 0 and codes.max() <= 255
+    assert np.array_equal(((codes.astype(np.float32) - z) * d).view(np.int32), what.view(np.int32))
+    out["what_hard_codes"] = codes.astype(np.uint8)
+    out["iters"], out["bs"] = np.array([iters]), np.array([bs])
+    save("recon_layer_brecq_fc", **out)
 
 
 # ------------------------------------------------------------------ other block types
@@ -1700,7 +1845,8 @@ if __name__ == "__main__":
     which = sys.argv[1:] or ["uaq", "channelquant", "adaround", "specials", "inpscale", "loss", "recon",
                              "layershift", "brecq", "blocks", "act", "layerfused", "blockshift", "driver",
                              "wmse", "validate", "real", "recon_biascal", "real_biascal", "long",
-                             "layerbrecq", "reallayer", "brecq_long", "brecq_affine", "init_specials"]
+                             "layerbrecq", "reallayer", "brecq_long", "brecq_affine", "init_specials",
+                             "layerbrecq_fc"]
     torch.set_num_threads(4)
     if "uaq" in which:
         gen_uaq()
@@ -1748,6 +1894,8 @@ if __name__ == "__main__":
         gen_real_layer_shift()
     if "layerbrecq" in which:
         gen_recon_layer_brecq()
+    if "layerbrecq_fc" in which:
+        gen_recon_layer_brecq_fc()
     if "recon_biascal" in which:
         gen_recon_fused(bias_cal=True)
     if "real_biascal" in which:

@@ -72,10 +72,10 @@ def tiny_net():
                          nn.AdaptiveAvgPool2d(1), nn.Flatten(), nn.Linear(32, 10)).eval()
 
 
-def build_qnn(Q, g, bits_w=2, bits_a=4):
+def build_qnn(Q, g, bits_w=2, bits_a=4, net=None):
     wq = {"n_bits": bits_w, "channel_wise": True, "scale_method": "max"}
     aq = {"n_bits": bits_a, "channel_wise": False, "scale_method": "mse", "leaf_param": True}
-    qnn = Q.QuantModel(tiny_net(), wq, aq).cuda().eval()
+    qnn = Q.QuantModel(tiny_net() if net is None else net, wq, aq).cuda().eval()
     qnn.set_first_last_layer_to_8bit()
     qms = [m for m in qnn.modules() if isinstance(m, Q.QuantModule)]
     for k, m in enumerate(qms):
@@ -304,6 +304,17 @@ def test_brecq_block_reconstruction_matches_reference(Q, golden, graph, wgrad, f
         aqs = [block.act_quantizer] + [m.act_quantizer for m in (block.conv1, block.conv2, block.downsample)
                                        if m.act_quantizer.delta is not None]
         np.testing.assert_allclose([float(q.delta) for q in aqs], g["a_delta0"], rtol=1e-6)
+        stats["a_delta0_rel_err"] = np.max(np.abs(np.array([float(q.delta) for q in aqs]) - g["a_delta0"]) /
+                                           g["a_delta0"])
+        if fixture == "recon_brecq_long":
+            # the act phase from the reference's own start state: its weight phase's V (the
+            # hard W^ then bit-identical, flips or not) and its act-delta init, so the act
+            # comparison below measures the act phase only
+            with torch.no_grad():
+                for n in ("conv1", "conv2", "downsample"):
+                    getattr(block, n).weight_quantizer.alpha.copy_(dev(g[n + "_alpha"]))
+                for q, d0 in zip(aqs, g["a_delta0"]):
+                    q.delta.fill_(float(d0))
         seen.clear()
         torch.manual_seed(1005)
         Q.block_reconstruction(qnn, block, cali, batch_size=8, iters=len(g["a_total_loss"]),
@@ -325,12 +336,21 @@ def test_brecq_block_reconstruction_matches_reference(Q, golden, graph, wgrad, f
                    np.mean(g["a_total_loss"][i:i + 100]) for i in range(0, len(seen), 100)]
             stats["a_window_mean_rel_err"] = max(win)
             stats["a_median_rel_err"] = float(np.median(a_rel))
+            l64 = g["a_total_loss64"]
+            k = len(l64)
+            stats["a_first20_rel_err"] = a_rel[:k].max()
+            stats["a_first20_argmax"] = int(a_rel[:k].argmax())
+            stats["a_first20_ours_vs_f64"] = np.max(np.abs(np.array(seen[:k]) - l64) / l64)
+            stats["a_first20_ref_vs_f64"] = np.max(np.abs(g["a_total_loss"][:k] - l64) / l64)
         parity_report(f"a22_brecq_basic[{fixture},graph={graph},wgrad={wgrad}]", **stats)
         if fixture == "recon_brecq_long":
-            # first 20 act iterations: <= 1e-5 on most boxes; 2.3e-5 on a box type whose
-            # solver picks moved the 400-iteration weight phase (w_total_rel_err 5.7e-7 vs
-            # 6.4e-7, V within 3-7e-6 either way) before this chaotic phase (r5ev7)
-            assert a_rel[:20].max() <= 5e-5, a_rel[:20].max()
+            # first 20 act iterations, from the reference's start state (above): the
+            # reference is within 1.2e-7 of float64 there (a_total_loss64, no activation
+            # rounding decided differently), so 1e-5 leaves room only for the convs'
+            # summation order.  r5 held 5e-5 after one box type reached 2.3e-5 while the act
+            # phase started from our own delta init (rtol 1e-6 of the reference's) -- not from
+            # the weight phase, whose hard W^ had no flip: 0 of every conv's decisions
+            assert a_rel[:20].max() <= 1e-5, a_rel[:20].max()
             assert np.median(a_rel) <= 1e-3 and a_rel.max() <= 1e-2, (np.median(a_rel), a_rel.max())
             assert max(win) <= 1e-3, win
             np.testing.assert_allclose([float(q.delta) for q in aqs], g["a_delta"], rtol=2e-3)
@@ -883,6 +903,211 @@ def test_fc_fused_iteration_matches_unfused(Q, det_convs, bits):
         assert dv.max() <= iters * 2e-3, dv.max()
     stats["hard_flips"] = ahf(w1, w0, v1, v0, iters * 2e-3, "fc")
     parity_report(f"k19_fc_fused_vs_unfused[w{bits}]", **stats)
+
+
+def fc_mlp():
+    """make_golden.gen_recon_layer_brecq_fc's network (weights from the fixture)."""
+    return nn.Sequential(nn.Linear(64, 512), nn.ReLU(), nn.Linear(512, 40)).eval()
+
+
+def fc_slot(bs, perm, lam, b, step):
+    """The device words of BRECQ iteration `step` (0-based) as BatchFeeder stages them: the
+    batch indices, (lambda, b), Adam's (-lr/bc1, sqrt(bc2)) at lr 1e-3, betas (0.9, 0.999)."""
+    slot = torch.zeros(bs + 2, dtype=torch.int64)
+    slot[:bs] = torch.as_tensor(perm.astype(np.int64))
+    t = step + 1
+    words = np.array([lam, b, -1e-3 / (1 - 0.9 ** t), (1 - 0.999 ** t) ** 0.5], np.float32)
+    slot[bs:] = torch.from_numpy(words.view(np.int64))
+    return slot.cuda()
+
+
+def test_fc_loop_matches_reference(Q, golden):
+    """K19, the fc loop as production runs it (FUSE_FC, CHUNK_ITERS iterations per graph
+    replay, no per-iteration value tracking), against the reference's own trajectory
+    (recon_layer_brecq_fc.npz: layer_reconstruction, quant/layer_recon.py:10-104, on an
+    8-bit Linear(512, 40) -- C_in % 64 == 0, so K19 is taken; 40 outputs leave a partial
+    16-row tile as ResNet-18's 1000 do -- 200 iterations over the b schedule's warm-up,
+    decay and end).  The captured input / target are the reference's (teacher-forced: the
+    first layer's GEMM order is not the loop under test; ours is checked against them too).
+      * every batch draw identical;
+      * every iteration's rec loss within max(1e-5, 2x the reference's own largest
+        distance from float64) of the reference's, and as close to the float64 loss as the
+        reference is (2x) -- at 8 bits the loss is a sum of squares of y - t ~ 4e-3 |y|,
+        so a GEMM's fp32 summation order moves it by ~1e-5 (the reference's own distance
+        from float64: max 9.5e-6, median 2.2e-6);
+      * V walk-bounded, hard rounding flipped only inside the walk budget;
+      * teacher-forced V gradients at steps 0 / 45 / 199 (K19's gv_out at the reference's V
+        and batch) within 2x the reference's own distance from the float64 gradient."""
+    import importlib
+    from conftest import assert_hard_flips_bounded as ahf
+    BR = importlib.import_module("shiftedscalequantization_amd.quant.block_recon")
+    E = importlib.import_module("shiftedscalequantization_amd.quant._engine")
+    g = golden("recon_layer_brecq_fc")
+    iters, bs = int(g["iters"][0]), int(g["bs"][0])
+    qnn = build_qnn(Q, g, net=fc_mlp())
+    fc = [m for m in qnn.modules() if isinstance(m, Q.QuantModule)][-1]
+    assert fc.weight_quantizer.n_bits == 8 and tuple(fc.weight.shape) == (40, 512)
+    cali = dev(g["cali"])
+    seen, draws, calls, cap = [], [], [], {}
+    orig = (BR.LossFunction.record, BR.K.fc_recon_iter, BR.save_inp_oup_data, E.BatchFeeder.draw)
+
+    def spy(self, rec, rnd, b, count=None):
+        seen.append((self.count if count is None else count, float(rec)))
+        return orig[0](self, rec, rnd, b, count=count)
+
+    def fcs(*a, **k):
+        calls.append(1)
+        return orig[1](*a, **k)
+
+    def save_io(*a, **k):
+        inp, out = orig[2](*a, **k)
+        cap["inp_rel"] = (inp.cpu().numpy() - g["cached_inp"]).__abs__().max() / np.abs(g["cached_inp"]).max()
+        cap["out_rel"] = (out.cpu().numpy() - g["cached_out"]).__abs__().max() / np.abs(g["cached_out"]).max()
+        return dev(g["cached_inp"]), dev(g["cached_out"])
+
+    def draw(self):
+        p = orig[3](self)
+        draws.append(p.numpy().copy())
+        return p
+
+    BR.LossFunction.record, BR.K.fc_recon_iter, BR.save_inp_oup_data, E.BatchFeeder.draw = \
+        spy, fcs, save_io, draw
+    n0 = E.GRAPH_REPLAYS.get("chunk", 0)
+    try:
+        assert BR.FUSE_FC and BR.CHUNK_ITERS > 1, "production knobs"
+        torch.manual_seed(1005)
+        Q.layer_reconstruction(qnn, fc, cali, batch_size=bs, iters=iters, weight=0.01, asym=True,
+                               b_range=(20, 2), warmup=0.2, act_quant=False, opt_mode="mse")
+    finally:
+        BR.LossFunction.record, BR.K.fc_recon_iter, BR.save_inp_oup_data, E.BatchFeeder.draw = orig
+    chunks = E.GRAPH_REPLAYS.get("chunk", 0) - n0
+    # K19 engaged (the eager warm-up calls, one single-iteration capture, one chunk capture)
+    # and the loop ran on chunk replays
+    assert len(calls) >= 2 and chunks >= 5, (len(calls), chunks)
+    # our capture of the same input / target: the first layer's GEMM order only
+    assert cap["inp_rel"] <= 1e-6 and cap["out_rel"] <= 1e-6, cap
+    np.testing.assert_array_equal(np.stack(draws), g["perms"].astype(np.int64))
+    assert [c for c, _ in seen] == list(range(1, iters + 1))
+    rec = np.array([v for _, v in seen])
+    ref, ref64 = g["rec_loss"], g["rec_loss64"]
+    rel = np.abs(rec - ref) / np.abs(ref)
+    ref_self = np.abs(ref - ref64) / np.abs(ref64)
+    our_self = np.abs(rec - ref64) / np.abs(ref64)
+    stats = {"loss_rel_err": rel.max(), "loss_rel_median": np.median(rel),
+             "ref_vs_f64_max": ref_self.max(), "ours_vs_f64_max": our_self.max(),
+             "ours_vs_f64_median": np.median(our_self), "ref_vs_f64_median": np.median(ref_self),
+             "chunk_replays": chunks, "capture_inp_rel": cap["inp_rel"]}
+    q = fc.weight_quantizer
+    v = q.alpha.detach().cpu().numpy()
+    dv = np.abs(v - g["V"])
+    stats["V_dev"] = dv.max()
+    stats["V_walkers"] = int((dv > 1e-5).sum())
+    q.soft_targets = False
+    with torch.no_grad():
+        what = q(fc.weight).cpu().numpy()
+    d, z = g["qm1_delta"][:, None], g["qm1_zp"][:, None]
+    what_ref = (g["what_hard_codes"].astype(np.float32) - z) * d
+    stats["hard_flips"] = ahf(what, what_ref, v, g["V"], iters * 2e-3, "fc")
+    # teacher-forced V gradients
+    w = fc.weight.detach().contiguous()
+    dq, zq = q.delta.detach(), q.zero_point.detach()
+    decay = BR.LinearTempDecay(iters, rel_start_decay=0.2, start_b=20, end_b=2)
+    for s in g["grad_steps"]:
+        s = int(s)
+        V = dev(g[f"gs{s}_V"]).contiguous()
+        lam = 0.01 if (s + 1) >= 0.2 * iters else 0.0
+        slot = fc_slot(bs, g["perms"][s], lam, float(decay(s + 1)) if lam else 0.0, s)
+        what_s = K_adaround(Q, V, w, dq, zq)
+        gv = torch.empty_like(V)
+        m_, v_ = torch.zeros_like(V), torch.zeros_like(V)
+        BR.K.fc_recon_iter(dev(g["cached_inp"]), dev(g["cached_out"]), slot, bs, w, V.clone(),
+                           what_s, dq, zq, 8, fc.bias.detach(), m_, v_, 0.9, 0.999, 1e-8, gv_out=gv)
+        gr = g[f"gs{s}_g"].astype(np.float64)
+        truth = gr + g[f"gs{s}_t_minus_g"].astype(np.float64)
+        ours = np.abs(gv.cpu().numpy().astype(np.float64) - truth).max()
+        theirs = np.abs(gr - truth).max()
+        stats[f"gs{s}_ours_vs_f64"], stats[f"gs{s}_ref_vs_f64"] = ours, theirs
+        stats[f"gs{s}_maxabs"] = np.abs(truth).max()
+    parity_report("k19_fc_loop_vs_reference", **stats)
+    tol = max(1e-5, 2 * ref_self.max())
+    assert rel.max() <= tol, (rel.max(), tol, int(rel.argmax()))
+    assert our_self.max() <= 2 * ref_self.max(), (our_self.max(), ref_self.max())
+    assert_walk_bounded(dv, 1e-5, iters * 2e-3, frac=0.05, what="fc V")
+    for s in g["grad_steps"]:
+        assert stats[f"gs{s}_ours_vs_f64"] <= 2 * stats[f"gs{s}_ref_vs_f64"], \
+            (int(s), stats[f"gs{s}_ours_vs_f64"], stats[f"gs{s}_ref_vs_f64"])
+
+
+def K_adaround(Q, V, w, d, z):
+    """W^ = AdaRound's soft forward (ssq_adaround_fwd), the first K19 call's input."""
+    from shiftedscalequantization_amd import kernels as K
+    return K.adaround(V, w, d, z, 8, False, False).detach().clone()
+
+
+@pytest.mark.parametrize("shape", [(512, 1000), (512, 40)])
+def test_fc_chunked_loop_bit_identical(Q, det_convs, shape):
+    """The production fc loop -- K19 inside ChunkGraph replays, track_values off, so the
+    iteration reads its words straight from the chunk ring row (feeder.chunk_dev[slot]) --
+    against one iteration per replay (CHUNK_ITERS = 1): V, Adam's moments, every recorded
+    rec loss and the CPU RNG's position bit-identical, at ResNet-18's fc shape (512 -> 1000)
+    and the fixture's (512 -> 40)."""
+    import copy
+    import importlib
+    BR = importlib.import_module("shiftedscalequantization_amd.quant.block_recon")
+    E = importlib.import_module("shiftedscalequantization_amd.quant._engine")
+    ci, co = shape
+    torch.manual_seed(11)
+    lin = nn.Linear(ci, co)
+    cali = torch.relu(torch.randn(256, ci)).cuda()
+    runs = []
+    for chunk in (1, 25):
+        qnn = Q.QuantModel(nn.Sequential(copy.deepcopy(lin)),
+                           {"n_bits": 8, "channel_wise": True, "scale_method": "max"},
+                           {"n_bits": 8, "channel_wise": False, "scale_method": "max"}).cuda().eval()
+        qnn.set_quant_state(True, False)
+        with torch.no_grad():
+            qnn(cali[:64])
+        fc = [m for m in qnn.modules() if isinstance(m, Q.QuantModule)][-1]
+        seen, opts, calls = [], [], []
+        orig_rec, orig_init, orig_fc, prev = (BR.LossFunction.record, E.SsqAdam.__init__,
+                                              BR.K.fc_recon_iter, BR.CHUNK_ITERS)
+
+        def spy(self, rec, rnd, b, count=None):
+            seen.append(float(rec))
+            return orig_rec(self, rec, rnd, b, count=count)
+
+        def init(self, *a, **k):
+            orig_init(self, *a, **k)
+            opts.append(self)
+
+        def fcs(*a, **k):
+            calls.append(1)
+            return orig_fc(*a, **k)
+
+        BR.LossFunction.record, E.SsqAdam.__init__, BR.K.fc_recon_iter, BR.CHUNK_ITERS = \
+            spy, init, fcs, chunk
+        n0 = E.GRAPH_REPLAYS.get("chunk", 0)
+        try:
+            torch.manual_seed(1005)
+            Q.layer_reconstruction(qnn, fc, cali, batch_size=32, iters=160, weight=0.01,
+                                   asym=True, b_range=(20, 2), warmup=0.2, act_quant=False,
+                                   opt_mode="mse")
+        finally:
+            BR.LossFunction.record, E.SsqAdam.__init__, BR.K.fc_recon_iter, BR.CHUNK_ITERS = \
+                orig_rec, orig_init, orig_fc, prev
+        out = {"rec": np.array(seen), "V": fc.weight_quantizer.alpha.detach().cpu().numpy(),
+               "rng": np.array(torch.randint(0, 1 << 30, (4,)).tolist()),
+               "replays": E.GRAPH_REPLAYS.get("chunk", 0) - n0, "fused": len(calls)}
+        for j, p_ in enumerate(opts[0].params):
+            out[f"m{j}"] = opts[0].state[p_]["exp_avg"].cpu().numpy()
+            out[f"v{j}"] = opts[0].state[p_]["exp_avg_sq"].cpu().numpy()
+        runs.append(out)
+    assert runs[0]["replays"] == 0 and runs[1]["replays"] >= 5, runs[1]["replays"]
+    assert runs[0]["fused"] >= 2 and runs[1]["fused"] >= 2
+    assert len(runs[0]["rec"]) == len(runs[1]["rec"]) == 160
+    for k in runs[0]:
+        if k not in ("replays", "fused"):
+            np.testing.assert_array_equal(runs[1][k], runs[0][k], err_msg=k)
 
 
 def test_brecq_frozen_loop_skips_unreported_iterations(Q, golden):
