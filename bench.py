@@ -69,6 +69,8 @@ def parse():
     p.add_argument("--no-recon", action="store_true")
     p.add_argument("--recon-iters", type=int, default=200)
     p.add_argument("--no-validate", action="store_true")
+    p.add_argument("--no-recon-configs", action="store_true",
+                   help="skip BASELINE configs 3-5's loops (recon_configs)")
     p.add_argument("--variant", type=int, default=-1, help="streaming cache policy A/B")
     p.add_argument("--dist-backend", default="nccl",
                    help="nccl (= RCCL over xGMI, the default) or gloo (rehearsing N > 1 ranks "
@@ -139,7 +141,7 @@ def _stamp(d):
 
 def pmc_traffic(kernel="fq_fwd_pt"):
     """(HBM bytes per launch of `kernel`, provenance) from the committed rocprofv3 PMC passes
-    (tools/pmc_session.sh: FETCH_SIZE and WRITE_SIZE in separate passes, read side doubled
+    (tools/session.sh TAG pmc: FETCH_SIZE and WRITE_SIZE in separate passes, read side doubled
     per the gfx950 correction), or (None, None) if they were not collected."""
     path = os.path.join(os.path.dirname(os.path.abspath(__file__)), PMC_FILE)
     try:
@@ -167,6 +169,24 @@ def recon_roofline():
     out["source_file"] = RECON_ROOFLINE_FILE + " (a committed trace, not this run)"
     out.update(_stamp(d))
     out["per_block_gbs"] = {b: v["achieved_gbs"] for b, v in d.get("blocks", {}).items()}
+    return out
+
+
+RECON_CONFIGS_ROOFLINE_FILE = "profiles/recon_configs_roofline.json"
+
+
+def recon_configs_roofline():
+    """Configs 3-5's ssq-set rooflines: the summary tools/recon_roofline.py --configs wrote
+    from a rocprofv3 kernel trace of these loops, or None."""
+    path = os.path.join(os.path.dirname(os.path.abspath(__file__)), RECON_CONFIGS_ROOFLINE_FILE)
+    try:
+        with open(path) as f:
+            d = json.load(f)
+    except (OSError, ValueError):
+        return None
+    out = {k: v for k, v in d.items() if k != "provenance"}
+    out["source_file"] = RECON_CONFIGS_ROOFLINE_FILE + " (a committed trace, not this run)"
+    out.update(_stamp(d))
     return out
 
 
@@ -375,12 +395,16 @@ def main():
 
     recon = None
     recon_state = None
+    recon_configs = None
     if not args.no_recon:
         from shiftedscalequantization_amd.recon_bench import run_recon_bench
         want_cpu = world == 1 and rank == 0 and not args.no_cpu_baseline
         recon = run_recon_bench(dev, world, rank, iters=args.recon_iters,
                                 cpu_sample=64 if want_cpu else 0)
         recon_state = recon.pop("_cpu_state", None)
+        if not args.no_recon_configs:
+            from shiftedscalequantization_amd.recon_bench import run_recon_configs
+            recon_configs = run_recon_configs(dev, world, rank, iters=args.recon_iters)
 
     validation = None
     if not args.no_validate:
@@ -447,6 +471,14 @@ def main():
         if rr is not None:
             out["roofline_recon"] = rr
         out["recon"] = recon
+    if recon_configs is not None:
+        rc = recon_configs_roofline()
+        for k, v in recon_configs.items():
+            if rc is not None and k in rc.get("configs", {}):
+                v["roofline"] = rc["configs"][k]
+        if rc is not None:
+            recon_configs["roofline_source"] = {kk: vv for kk, vv in rc.items() if kk != "configs"}
+        out["recon_configs"] = recon_configs
     if validation is not None:
         out["validation"] = validation
     if world == 1 and rank == 0 and not args.no_cpu_baseline:

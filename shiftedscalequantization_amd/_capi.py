@@ -146,8 +146,15 @@ def load():
     return lib
 
 
+# tools (tools/recon_configs_trace.py): when set, CALL_HOOK(name, args) sees every entry
+# point call before it is made (the per-iteration ledger of algorithmic bytes)
+CALL_HOOK = None
+
+
 def call(name, *args):
     lib = load()
+    if CALL_HOOK is not None:
+        CALL_HOOK(name, args)
     rc = getattr(lib, name)(*args)
     if rc != 0:
         msg = lib.ssq_last_error().decode(errors="replace")

@@ -386,7 +386,10 @@ __global__ __launch_bounds__(kBlock) void fq_bwd_pt(const float* __restrict__ x,
 // zp sums only when asked for.  The delta term is (x/d)/d with two IEEE divides, as torch's
 // div backward forms it (quant_layer.py:92-98 under autograd) and as the fused epilogue's
 // backward does: t * (1/d) is one ulp off per term, and the two ~1e2 sums of the delta
-// gradient cancel to ~1e-2, which turned that ulp into 2e-4 of the result.
+// gradient cancel to ~1e-2, which turned that ulp into 2e-4 of the result (r5).  The pass
+// runs at ~5.3 TB/s (ResNet-50 layer1.0's act phase): HBM-bound, so the divides cost nothing
+// here -- a form with two float4 pairs in flight per thread and the reciprocal-form divides
+// under a wave-uniform range test measured 82.7 vs 79.1 us per three launches (r6, not kept).
 template <bool ZP, int ACT>
 __global__ __launch_bounds__(kBlock) void fq_bwd_pt4(const f32x4* __restrict__ x,
                                                      const f32x4* __restrict__ gy,

@@ -40,6 +40,10 @@ def block_reconstruction(model: QuantModel, block: BaseQuantBlock, cali_data: to
 
 GRAPH_WARMUP = 3     # eager iterations before the iteration body is captured
 ITER_HOOK = None     # optional callable(i, iters) at the top of every device-loop iteration (tools)
+# optional callable(i) before iteration i is issued -- once per chunk replay (i its first
+# iteration) -- and (iters) after the last: unlike ITER_HOOK it keeps the chunked replays,
+# so the loop timed through it is the production loop (recon_bench)
+TIMING_HOOK = None
 # A/B knobs of the device loop, bit-identical either way (tests/test_recon_gpu.py); the
 # environment's SSQ_BRECQ_FAST=0 starts with all of them off (end-to-end A/B runs):
 _FAST = os.environ.get("SSQ_BRECQ_FAST", "1") != "0"
@@ -479,6 +483,8 @@ def _run(iters, loss_func, feeder, optimizer, scheduler, use_graph, bucket, body
     try:
         i = 0
         while i < iters:
+            if TIMING_HOOK is not None:
+                TIMING_HOOK(i)
             if chunk_ok and graph_obj is not None and last.get('step'):
                 # the chunk never spans an iteration whose value is reported (count % 500)
                 # except as its first
@@ -532,6 +538,8 @@ def _run(iters, loss_func, feeder, optimizer, scheduler, use_graph, bucket, body
             i += 1
         if ITER_HOOK is not None:
             ITER_HOOK(iters, iters)
+        if TIMING_HOOK is not None:
+            TIMING_HOOK(iters)
         probe(iters, opt_params)
     finally:
         for q in ada:

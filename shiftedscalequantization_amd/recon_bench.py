@@ -27,6 +27,24 @@ BLOCKS = {"layer1.0": (64, 56, 56), "layer1.1": (64, 56, 56), "layer2.0": (64, 5
           "layer4.0": (256, 14, 14), "layer4.1": (512, 7, 7)}
 
 
+# tools/recon_configs_trace.py: MARK[0] = callable(n) launches a marker kernel at the start
+# (n None) and the end (n = timed iterations) of every timed region, for a kernel trace
+MARK = [None]
+# tools/recon_configs_trace.py: ITER_NOTE[0] = callable(i) is told the index of every
+# iteration the loop issues on the host (eager, captured, or a chunk's first)
+ITER_NOTE = [None]
+
+
+def _mark(n):
+    if MARK[0] is not None:
+        MARK[0](n)
+
+
+def _note(i):
+    if ITER_NOTE[0] is not None:
+        ITER_NOTE[0](i)
+
+
 def graph_time_ms(fn, reps=20, rounds=5):
     """Device time per call of `fn`: `reps` calls captured in one HIP graph (no host
     launch cost), replayed `rounds` times, median of the per-replay averages (HIP events on
@@ -119,9 +137,11 @@ def run_block(dev, name, n_cali=1024, iters=200, warmup=20, rank=0, bias_cal=Tru
     stamps = {}
 
     def hook(i):
+        _note(i)
         if i in (warmup, warmup + iters):
             torch.cuda.synchronize(dev)
             stamps[i] = time.perf_counter()
+            _mark(i - warmup if i == warmup + iters else None)
 
     import builtins
     from . import parallel_dp as P
@@ -142,6 +162,108 @@ def run_block(dev, name, n_cali=1024, iters=200, warmup=20, rank=0, bias_cal=Tru
         P.TIMING = None
     res["ips"] = iters / (stamps[warmup + iters] - stamps[warmup])
     return res
+
+
+def run_brecq_block(dev, arch, name, n_cali=1024, iters=200, warmup=20, rank=0, act=True):
+    """BRECQ block_reconstruction (quant/block_recon.py:10-116) on one block of `arch` as
+    Brecq/main_imagenet.py's recon_model runs it for config 3: the AdaRound weight phase (asym,
+    weight 0.01, b (20, 2), warm-up 0.2), then after the act-delta init the act phase (lr 4e-4,
+    p 2.4); batch 32 drawn from the block features of n_cali synthetic 224x224 images
+    (captured by the loop itself, save_inp_oup_data).  The iterations are timed on the
+    production loop -- chunked graph replays -- through block_recon.TIMING_HOOK, from the first
+    replay that starts at or after `warmup`."""
+    from .quant import block_recon as BRm
+    from .quant import block_reconstruction
+    torch.manual_seed(1005 + rank)
+    cnn = nets.ARCHS[arch]().eval().to(dev)
+    qnn = QuantModel(cnn, {"n_bits": 2, "channel_wise": True, "scale_method": "max"},
+                     {"n_bits": 4, "channel_wise": False, "scale_method": "mse", "leaf_param": True})
+    qnn.to(dev).eval()
+    qnn.set_first_last_layer_to_8bit()
+    g = torch.Generator(device=dev).manual_seed(1005 + rank)
+    cali = torch.empty(n_cali, 3, 224, 224, device=dev).normal_(generator=g)
+    qnn.set_quant_state(True, False)
+    with torch.no_grad():
+        qnn(cali[:32])                      # every weight quantizer's 'max' init
+    block = _block(qnn, name)
+    total = warmup + iters
+    res = {}
+
+    def timed(phase, **kw):
+        st = {}
+
+        def hook(i):
+            _note(i)
+            if "t0" not in st and i >= warmup:
+                torch.cuda.synchronize(dev)
+                st["t0"], st["i0"] = time.perf_counter(), i
+                _mark(None)
+            elif i == total and "t0" in st:
+                torch.cuda.synchronize(dev)
+                st["t1"] = time.perf_counter()
+                _mark(total - st["i0"])
+
+        BRm.TIMING_HOOK = hook
+        try:
+            block_reconstruction(qnn, block, cali, batch_size=32, iters=total, **kw)
+        finally:
+            BRm.TIMING_HOOK = None
+        res[phase] = (total - st["i0"]) / (st["t1"] - st["t0"])
+
+    timed("weight", weight=0.01, asym=True, b_range=(20, 2), warmup=0.2, act_quant=False,
+          opt_mode="mse")
+    if act:
+        qnn.set_quant_state(True, True)
+        with torch.no_grad():
+            qnn(cali[:64])                  # act-delta init (Brecq/main_imagenet.py:231-236)
+        qnn.disable_network_output_quantization()
+        timed("act", act_quant=True, opt_mode="mse", lr=4e-4, p=2.4)
+    del qnn, cnn, cali
+    torch.cuda.empty_cache()
+    return res
+
+
+# BASELINE configs 3-5 beside ResNet-18's blocks: (config, arch, block, loop).  Config 3 runs
+# BRECQ (Brecq/main_imagenet.py's recon_model); configs 4 and 5 run the --bias_ch_quant flow's
+# fused shifted-scale loop with bias_cal, on the block the real-shape parity cases pin
+# (tests/golden/realshape.py: mbv2_960, rgx_g9).
+RECON_CONFIGS = (("3", "resnet50", "layer1.0", "brecq"),
+                 ("4", "mobilenetv2", "features.16", "fused"),
+                 ("5", "regnetx_3200m", "s3.b1", "fused"))
+
+
+def run_recon_configs(dev, world, rank, iters=200, configs=RECON_CONFIGS):
+    """iters/s of BASELINE configs 3-5's reconstruction loops under cudnn.deterministic (the
+    reference's seed_all), one block each, batch 32 per rank."""
+    cudnn = torch.backends.cudnn
+    saved = (cudnn.benchmark, cudnn.deterministic)
+    out = {}
+    import builtins
+    _print = builtins.print
+    try:
+        cudnn.benchmark, cudnn.deterministic = False, True
+        for cfg, arch, name, loop in configs:
+            t0 = time.perf_counter()
+            builtins.print = lambda *a, **k: None     # silence the loops' init prints
+            try:
+                if loop == "brecq":
+                    r = run_brecq_block(dev, arch, name, iters=iters, rank=rank)
+                    ips = {"weight_phase": round(_slowest(r["weight"], world, dev), 2),
+                           "act_phase": round(_slowest(r["act"], world, dev), 2)}
+                    what = ("BRECQ block_reconstruction: AdaRound weight phase, then the act "
+                            "phase (p 2.4)")
+                else:
+                    r = run_block(dev, name, iters=iters, rank=rank, arch=arch)
+                    ips = {"fused_loop": round(_slowest(r["ips"], world, dev), 2)}
+                    what = "block_recon_fused_shiftedScale, W2 S=3, bias_cal"
+            finally:
+                builtins.print = _print
+            out[f"config{cfg}"] = {"arch": arch, "block": name, "loop": what,
+                                   "iters_per_s": ips, "timed_iters": iters,
+                                   "setup_and_run_s": round(time.perf_counter() - t0, 1)}
+    finally:
+        cudnn.benchmark, cudnn.deterministic = saved
+    return out
 
 
 def _slowest(ips, world, dev):

@@ -305,3 +305,122 @@ def test_grads_into_one_write_per_parameter():
             with pytest.raises(A.SSQError):
                 K._grad_dest(p, 6, p.device)
     assert not K.GRAD_INTO
+
+
+# ---- the first RCCL run (the driver's 8-GPU node), rehearsed on the host ------------------
+
+def test_eight_rccl_ranks_map_to_distinct_devices(monkeypatch):
+    """`bench.py --gpus 8 --dist-backend nccl` / `main_imagenet.py --gpus 8`: the self-spawner
+    gives the 8 ranks LOCAL_RANK 0..7, and with 8 devices visible (mocked here) each rank
+    binds cuda:LOCAL_RANK and initialises RCCL with that device -- no two ranks share a GPU.
+    With fewer devices than ranks, RCCL is refused with a pointer to gloo."""
+    import importlib
+    import sys
+    import torch.distributed as dist
+    sys.path.insert(0, ROOT)
+    for script, args in (("bench.py", ["--gpus", "8", "--dist-backend", "nccl"]),
+                         ("main_imagenet.py", ["--gpus", "8", "--dist_backend", "nccl"])):
+        parent, ranks = _dryrun(script, args)
+        assert [e["LOCAL_RANK"] for e in ranks] == [str(r) for r in range(8)]
+        mod = importlib.import_module(script[:-3])
+        bound = []
+
+        class _Stop(Exception):
+            pass
+
+        def init_pg(backend, device_id=None, **k):
+            bound.append((backend, device_id))
+            if script == "main_imagenet.py":
+                raise _Stop()          # main() goes on to build the model: stop at RCCL
+
+        monkeypatch.setattr(torch.cuda, "device_count", lambda: 8)
+        monkeypatch.setattr(torch.cuda, "set_device", lambda d: None)
+        monkeypatch.setattr(dist, "init_process_group", init_pg)
+        for e in ranks:
+            for k in ("RANK", "LOCAL_RANK", "WORLD_SIZE", "MASTER_ADDR", "MASTER_PORT"):
+                monkeypatch.setenv(k, e[k])
+            if script == "bench.py":
+                monkeypatch.setattr(sys, "argv", [script] + args)
+                mod.setup(mod.parse().dist_backend)
+            else:
+                with pytest.raises(_Stop):
+                    mod.main(args)
+        assert [b for b, _ in bound] == ["nccl"] * 8, bound
+        assert [d for _, d in bound] == [torch.device("cuda", r) for r in range(8)], bound
+        # 8 ranks over RCCL on a 4-GPU box: refused (gloo rehearses shared devices)
+        monkeypatch.setattr(torch.cuda, "device_count", lambda: 4)
+        with pytest.raises(SystemExit, match="gloo"):
+            if script == "bench.py":
+                mod.setup("nccl")
+            else:
+                mod.main(args)
+    for k in ("RANK", "LOCAL_RANK", "WORLD_SIZE", "MASTER_ADDR", "MASTER_PORT"):
+        monkeypatch.delenv(k, raising=False)
+
+
+def test_collective_stays_outside_graph_capture(monkeypatch):
+    """At world > 1 the reconstruction iteration is captured as two HIP graphs around the
+    gradient bucket's all-reduce (_engine.IterationGraph): the body's kernels are captured,
+    the collective never is -- RCCL's all-reduce runs eagerly between the two replays, in
+    the iteration's order (pre replay, all-reduce, post replay).  Graph capture and the
+    collective are mocked (host only); the bucket and the graph split are the product's."""
+    import torch.distributed as dist
+    from shiftedscalequantization_amd import parallel_dp as P
+    from shiftedscalequantization_amd.quant import _engine as E
+    state, log = {"capturing": False}, []
+
+    class Graph:
+        def __init__(self):
+            self.body = None
+
+        def pool(self):
+            return None
+
+        def replay(self):
+            log.append(("replay", self.body))
+
+    class capture:
+        def __init__(self, g, pool=None):
+            self.g = g
+
+        def __enter__(self):
+            state["capturing"] = True
+            state["graph"] = self.g
+
+        def __exit__(self, *exc):
+            state["capturing"] = False
+
+    def all_reduce(t, op=None):
+        assert not state["capturing"], "collective inside a graph capture"
+        log.append(("all_reduce", t.numel()))
+
+    monkeypatch.setattr(torch.cuda, "CUDAGraph", Graph)
+    monkeypatch.setattr(torch.cuda, "graph", capture)
+    monkeypatch.setattr(dist, "all_reduce", all_reduce)
+    monkeypatch.setattr(P, "world", lambda: 8)
+    a, b = torch.zeros(5, requires_grad=True), torch.zeros(3, requires_grad=True)
+    bucket = P.GradBucket([a, b])
+    a.grad, b.grad = torch.ones(5), torch.ones(3)
+    bucket.allreduce_()                       # builds the flat bucket (8 elements)
+    assert bucket.active and log == [("all_reduce", 8)]
+    log.clear()
+
+    def pre():
+        assert state["capturing"]
+        state["graph"].body = "pre"
+
+    def post():
+        assert state["capturing"]
+        state["graph"].body = "post"
+
+    ig = E.IterationGraph(pre, post, bucket, {})
+    assert len(ig.graphs) == 2 and log == []
+    for _ in range(3):
+        ig.replay()
+    assert log == [("replay", "pre"), ("all_reduce", 8), ("replay", "post")] * 3, log
+    # world 1: one graph, no collective
+    monkeypatch.setattr(P, "world", lambda: 1)
+    log.clear()
+    ig1 = E.IterationGraph(pre, lambda: None, P.GradBucket([a]), {})
+    ig1.replay()
+    assert len(ig1.graphs) == 1 and log == [("replay", "pre")]

@@ -875,6 +875,34 @@ def test_fq_bwd_per_tensor_vs_oracle(K, n):
     close(host(zz.grad).reshape(-1), np.reshape(rgz, -1), rtol=1e-5, atol=1e-6)
 
 
+@pytest.mark.parametrize("d", [0.21, 2.0 ** -40, 3.0e9])
+def test_fq_bwd_extreme_values_bit_exact(K, d):
+    """fq_bwd_pt4 (the float4 STE backward) with values planted far outside the usual range
+    (tiny, huge, zeros, inf, NaN) and deltas from 2^-40 to 3e9: gx bit-exact against numpy's
+    IEEE fp32, the delta / zero-point gradients (the (x/d)/d term with two IEEE divides) as
+    the oracle's float64 sums."""
+    n = 1 << 20
+    gen = torch.Generator().manual_seed(int(d * 1e3) % 1000 + 7)
+    x = (torch.randn(n, generator=gen) * 4 * d).float()
+    gy = torch.randn(n, generator=gen)
+    pos = torch.randperm(n, generator=gen)[:24]
+    specials = torch.tensor([1e-38, -3e-39, 2.0 ** -31, 2.0 ** 31, 1e30, -1e33, 0.0, -0.0,
+                             float("inf"), float("-inf"), float("nan"), 1e-20])
+    x[pos[:12]] = specials * (d if d < 1 else 1.0)
+    gy[pos[12:]] = specials
+    d_t, z_t = torch.tensor(np.float32(d)), torch.tensor(3.0)
+    xr = x.cuda().requires_grad_(True)
+    dd, zz = d_t.cuda().requires_grad_(True), z_t.cuda().requires_grad_(True)
+    K.fake_quant(xr, dd, zz, 4, False).backward(gy.cuda())
+    rgx, rgd, rgz = R.fake_quant_bwd(x.numpy(), d_t.numpy(), z_t.numpy(), 4, False, gy.numpy())
+    np.testing.assert_array_equal(host(xr.grad).view(np.int32), np.asarray(rgx, np.float32).view(np.int32))
+    for got, ref in ((host(dd.grad), rgd), (host(zz.grad), rgz)):
+        got, ref = np.reshape(got, -1), np.reshape(ref, -1)
+        assert np.array_equal(np.isnan(got), np.isnan(ref))
+        ok = ~np.isnan(ref)
+        close(got[ok], ref[ok], rtol=1e-5, atol=1e-6)
+
+
 @pytest.mark.parametrize("level,threshold", [(1024, 2.0), (64, 1.0), (1, 1.5), (333, 0.5)])
 def test_inpscale_search_binary_search_equals_scan(K, level, threshold):
     """The kernel's binary search over k returns exactly the reference's linear scan

@@ -157,6 +157,82 @@ def analyse(path, warmup=20):
             "frac": round(ach / HBM_PEAK_GBS, 4), "blocks": out}
 
 
+def _short(name):
+    n = name.split("(")[0]
+    n = n.replace("void ", "").replace("ssq::", "")
+    return n[:60]
+
+
+def analyse_configs(trace, side_path):
+    """BASELINE configs 3-5 (tools/recon_configs_trace.py): each timed region lies between two
+    marker launches (write_probe); its ssq-set launches (tools/ssq_bytes.ssq_kernel) are timed
+    from the trace, and priced with the algorithmic bytes of the entry points one iteration
+    calls (the side file's ledger, from the iteration the loop captured and replays)."""
+    sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+    import ssq_bytes
+    side = json.load(open(side_path))
+    rows = list(csv.DictReader(open(trace)))
+    rows.sort(key=lambda r: int(r["Start_Timestamp"]))
+    marks = [i for i, r in enumerate(rows) if "write_probe" in r["Kernel_Name"]]
+    pairs = list(zip(marks[0::2], marks[1::2]))
+    regions = side["regions"]
+    if len(pairs) != len(regions):
+        raise SystemExit(f"expected {len(regions)} marked regions, found {len(pairs)}")
+    out, tot_b, tot_us = {}, 0.0, 0.0
+    for (a, b), reg in zip(pairs, regions):
+        n_it = reg["iterations"]
+        us, cnt, conv_us, other_us = collections.Counter(), collections.Counter(), 0.0, 0.0
+        for r in rows[a + 1:b]:
+            d = (int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e3
+            name = r["Kernel_Name"]
+            if ssq_bytes.ssq_kernel(name):
+                us[_short(name)] += d
+                cnt[_short(name)] += 1
+            elif "ssq::" in name or "wgrad_gemm_operands" in name:
+                conv_us += d
+            else:
+                other_us += d
+        wall = (int(rows[b]["Start_Timestamp"]) - int(rows[a]["End_Timestamp"])) / 1e3
+        ssq_us = sum(us.values()) / n_it
+        by = reg["bytes_per_iteration"]
+        key = reg["config"] + ("" if reg["phase"] == "fused_loop" else "_" + reg["phase"])
+        out[key] = {
+            "arch": reg["arch"], "block": reg["block"], "phase": reg["phase"], "iterations": n_it,
+            "wall_us_per_iteration": round(wall / n_it, 1),
+            "ssq_set_us": round(ssq_us, 2), "ssq_set_bytes": int(by),
+            "achieved": round(by / (ssq_us * 1e-6) / 1e9, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+            "frac": round(by / (ssq_us * 1e-6) / 1e9 / HBM_PEAK_GBS, 4),
+            "conv_side_ssq_kernels_us": round(conv_us / n_it, 1),
+            "library_convs_gemms_other_us": round(other_us / n_it, 1),
+            "kernels": {k: {"us": round(v / n_it, 2), "launches": round(cnt[k] / n_it, 2)}
+                        for k, v in us.most_common()},
+            "ledger": reg["ledger"]}
+        tot_b += by
+        tot_us += ssq_us
+    return {"bound": "hbm", "source": "rocprofv3 --kernel-trace of tools/recon_configs_trace.py "
+                                      "(configs 3-5's loops, deterministic solvers, timed iterations)",
+            "kernels": "every ssq:: launch of the loop iteration except conv arithmetic (K17 weight "
+                       "gradients, K18 depthwise convs, im2col operands); bytes: the iteration's "
+                       "entry points' operands (tools/ssq_bytes.py)",
+            "configs": out}
+
+
+if __name__ == "__main__" and sys.argv[1] == "--configs":
+    res = analyse_configs(sys.argv[2], sys.argv[3])
+    sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+    from shiftedscalequantization_amd.build import provenance
+    res["provenance"] = provenance()
+    with open(sys.argv[4], "w") as f:
+        f.write(json.dumps(res, indent=1) + "\n")
+    for k, v in res["configs"].items():
+        print(f"{k} {v['arch']} {v['block']} {v['phase']}: wall {v['wall_us_per_iteration']} us/it, "
+              f"ssq set {v['ssq_set_us']} us {v['ssq_set_bytes'] / 1e6:.2f} MB = {v['achieved']} GB/s "
+              f"({v['frac']}), conv-side ssq {v['conv_side_ssq_kernels_us']} us, library/other "
+              f"{v['library_convs_gemms_other_us']} us")
+        for c, kk in v["kernels"].items():
+            print(f"    {c:60s} {kk['us']:8.2f} us x{kk['launches']}")
+    sys.exit(0)
+
 if __name__ == "__main__":
     res = analyse(sys.argv[1])
     sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
