@@ -1916,6 +1916,8 @@ class Conv2dFn(torch.autograd.Function):
         if ctx.needs_input_grad[1]:
             if _use_wgrad_gemm(x, weight, stride, padding, groups):
                 gw = conv_wgrad_gemm(x, g, weight.shape, stride, padding, col=col)
+            elif _use_wgrad_bmm(x, weight, stride, padding, groups):
+                gw = conv_wgrad_1x1_bmm(x, g, weight.shape)
             else:
                 gw = conv_wgrad(x, g, weight.shape, stride, padding, groups)
         return gx, gw, None, None, None, None
@@ -1975,6 +1977,36 @@ def _use_wgrad_gemm(x, weight, stride, padding, groups=1):
         # 44 / 44; layer2.0's (28x28 plane) stays on K17 (84 vs 42; tools/ds_gemm_probe.py)
         return Co >= 256
     return Co >= 128 and C_ * R * S >= 1152
+
+
+# 1x1 stride-1 convs on large planes (OH*OW >= 400: ResNet-50's bottleneck 1x1s and layer1
+# downsample, MobileNetV2's expand / project convs, RegNetX's 'a' convs on 28x28 and up): the
+# weight gradient as ONE strided-batched library GEMM, sum_n dy[n] @ x[n]^T, then the batch
+# summed in order (conv_wgrad_1x1_bmm), instead of K17's 1x1 kernel, whose per-lane 4-B
+# LDS-DMA staging holds it at 11-31 TF there.  tools/wgrad1x1_probe.py
+# (profiles/r6_wgrad1x1_probe.jsonl), batch 32: ResNet-50 layer1.0 conv1 / conv3 / downsample
+# 74.6 / 120.8 / 120.9 -> 20.9 / 35.3 / 35.0 us, RegNetX-3200M s3.b1 'a' 133.7 -> 54.3 us;
+# bit-identical run to run, within 1e-6 of float64 (K17: 3e-7).  Planes <= 196 pixels keep
+# the im2col GEMM (_use_wgrad_gemm) or K17.  A/B knob: SSQ_WGRAD_1X1_BMM=0.
+WGRAD_1X1_BMM = os.environ.get("SSQ_WGRAD_1X1_BMM", "1") != "0"
+
+
+def _use_wgrad_bmm(x, weight, stride, padding, groups=1):
+    if not WGRAD_1X1_BMM or WGRAD_POLICY != "auto" or groups != 1 \
+            or tuple(weight.shape[2:]) != (1, 1):
+        return False
+    if _pair(stride) != [1, 1] or _pair(padding) != [0, 0]:
+        return False
+    return x.dim() == 4 and x.shape[2] * x.shape[3] >= 400
+
+
+def conv_wgrad_1x1_bmm(x, dy, w_shape):
+    """d loss / d weight of a 1x1 / stride 1 / pad 0 ungrouped conv: sum_n dy[n] @ x[n]^T as
+    one strided-batched GEMM (torch.matmul -> hipBLASLt) and an in-order batch sum."""
+    n, c = int(x.shape[0]), int(x.shape[1])
+    co, p = int(w_shape[0]), int(x.shape[2] * x.shape[3])
+    gw = torch.matmul(dy.detach().reshape(n, co, p), x.detach().reshape(n, c, p).transpose(1, 2))
+    return gw.sum(0).view(tuple(w_shape))
 
 
 def _use_fwd_gemm(x, weight, stride, padding, groups=1):

@@ -1108,6 +1108,43 @@ def test_conv1x1_stride2_forward_gemm(K, cfg):
 
 
 @pytest.mark.parametrize("cfg", [
+    # (Nb, C, H, Co): ResNet-50 layer1.0's conv1 / conv3+downsample, RegNetX-3200M s3.b1 'a',
+    # MobileNetV2's 56x56 expand, ragged sizes at the 400-pixel edge
+    (32, 64, 56, 64), (32, 64, 56, 256), (32, 192, 28, 432), (32, 24, 56, 144), (3, 37, 20, 29),
+    (4, 16, 19, 8)])
+def test_conv_wgrad_1x1_bmm_matches_fp64(K, cfg):
+    """The 1x1 stride-1 weight gradient on planes >= 400 pixels as one strided-batched GEMM
+    and an in-order batch sum (K.conv_wgrad_1x1_bmm, WGRAD_1X1_BMM): vs the fp64 CPU gradient
+    within the fp32 accumulation bound, bit-identical run to run, and what K.conv2d's
+    training path (Conv2dFn under cudnn.deterministic) hands the weight -- below 400 pixels,
+    or with the policy forced, K17 / the im2col GEMM as before."""
+    Nb, C, H, Co = cfg
+    gen = torch.Generator().manual_seed(sum(cfg))
+    x = torch.relu(torch.randn(Nb, C, H, H, generator=gen))
+    w = torch.randn(Co, C, 1, 1, generator=gen) * 0.1
+    dy = torch.randn(Nb, Co, H, H, generator=gen)
+    ref = torch.nn.grad.conv2d_weight(x.double(), w.shape, dy.double(), 1, 0)
+    mag = torch.nn.grad.conv2d_weight(x.double().abs(), w.shape, dy.double().abs(), 1, 0)
+    xd, dyd = x.cuda(), dy.cuda()
+    dw1, dw2 = K.conv_wgrad_1x1_bmm(xd, dyd, w.shape), K.conv_wgrad_1x1_bmm(xd, dyd, w.shape)
+    np.testing.assert_array_equal(host(dw1).view(np.int32), host(dw2).view(np.int32))
+    err = (dw1.double().cpu() - ref).abs()
+    assert bool((err <= 1e-5 * mag + 1e-30).all()), float((err / mag.clamp_min(1e-30)).max())
+    wd = w.cuda()
+    assert K._use_wgrad_bmm(xd, wd, 1, 0) == (H * H >= 400)
+    old_det = torch.backends.cudnn.deterministic
+    torch.backends.cudnn.deterministic = True
+    try:
+        wg = wd.clone().requires_grad_(True)
+        K.conv2d(xd, wg, 1, 0).backward(dyd)
+    finally:
+        torch.backends.cudnn.deterministic = old_det
+    if H * H >= 400:
+        np.testing.assert_array_equal(host(wg.grad).view(np.int32), host(dw1).view(np.int32))
+    assert bool(((wg.grad.double().cpu() - ref).abs() <= 1e-5 * mag + 1e-30).all())
+
+
+@pytest.mark.parametrize("cfg", [
     # (Nb, C, H, Co, k, stride, pad): ResNet-18 layer3 / layer3.0 s2 / layer4 / layer4.0 s2
     # at batch 32 (the shapes the GEMM policy takes), a 5x5 and ragged sizes
     (32, 256, 14, 256, 3, 1, 1), (32, 128, 28, 256, 3, 2, 1), (32, 512, 7, 512, 3, 1, 1),
