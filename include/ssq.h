@@ -15,12 +15,11 @@
  *
  * Streams and workspaces (every entry point): calls on one stream run in issue order;
  * calls on different streams may run concurrently provided no two calls in flight share a
- * workspace (`ws`) or an output buffer.  The library holds no device-global counters: the
- * one-launch reductions keep their last-arriver counter in the call's own workspace (the
- * size functions include it).  Workspaces are zero-filled once when allocated (hipMemset,
- * torch.zeros) and every call leaves its counters zero again -- the same rule as a
- * semaphore workspace.  The host-state deferrals and the armed step below are per stream
- * but not thread-safe: issue them from one host thread.
+ * workspace (`ws`) or an output buffer.  The library holds no device-global state: every
+ * reduction's partials -- and the one in-launch last-arriver counter (the epilogue
+ * backward's act-delta reduction, zeroed by the launch that writes its partials) -- live in
+ * the call's own workspace, which needs no initialisation.  The host-state deferrals and
+ * the armed step below are per stream but not thread-safe: issue them from one host thread.
  *
  * The reference (jai1215snu/ShiftedScaleQuantization) is pure PyTorch: it has no FFI.
  * Each entry point below replaces the eager-op sequence cited beside it; the reference
@@ -311,9 +310,8 @@ int ssq_inpscale_fwd(const float* W, const float* inp_scale, const float* delta,
  * loss_out / grad / gscale (a DEVICE scalar, the upstream gradient) may each be NULL.
  * relu_mask != 0: pred is the output of a ReLU and grad is written at the ReLU's input
  * (grad = 0 where pred <= 0, torch's threshold_backward) -- the block's final ReLU
- * backward folded into the loss pass.  The loss reduction is deterministic.
- * ws: ssq_lp_loss_workspace_size(n) bytes, zero-filled at allocation (the one-launch form,
- * SSQ_LOSS_ONE_LAUNCH=1, keeps its last-arriver counter after the partials and leaves it 0). */
+ * backward folded into the loss pass.  The loss reduction is deterministic: workgroup
+ * partials in ws, summed in index order by a finalize launch (or task, with deferral on). */
 size_t ssq_lp_loss_workspace_size(int64_t n);
 int ssq_lp_loss(const float* pred, const float* tgt, int64_t n, int64_t M, float p,
                 float* loss_out, float* grad, const float* gscale, int relu_mask, void* ws,

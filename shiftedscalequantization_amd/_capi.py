@@ -265,9 +265,7 @@ def workspace(nbytes, device, slot=None):
     key = (device.index, torch.cuda.current_stream(device).cuda_stream, slot)
     buf = cache.get(key)
     if buf is None or buf.numel() < nbytes:
-        # zero-filled once (include/ssq.h: one-launch reductions keep their last-arriver
-        # counters in the call's workspace and leave them zero)
-        buf = torch.zeros(max(int(nbytes), 1 << 16), dtype=torch.uint8, device=device)
+        buf = torch.empty(max(int(nbytes), 1 << 16), dtype=torch.uint8, device=device)
         cache[key] = buf
     return C.c_void_p(buf.data_ptr()), buf.numel()
 

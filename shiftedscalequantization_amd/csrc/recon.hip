@@ -4,7 +4,7 @@
 // lp_loss (quant_layer.py:25-32) is five eager launches plus five more in autograd; here
 // one pass reads pred and tgt and writes d loss/d pred (12 B/elem), with a deterministic
 // reduction of the loss value (workgroup partials summed in index order by a 1-workgroup
-// finalize launch, or by the last workgroup to finish: SSQ_LOSS_ONE_LAUNCH).  For p == 2
+// finalize launch, or by a finalize task riding on a later launch: fin_tasks.h).  For p == 2
 // the gradient is bit-identical to PyTorch's: (1/M) * (2*|d|) * sgn(d).
 #include <stdlib.h>
 
@@ -41,9 +41,7 @@ __global__ __launch_bounds__(kBlock) void lp_loss_kernel(const float* __restrict
                                                          const float* __restrict__ gscale,
                                                          int relu_mask, int vec, TgtRows tr4,
                                                          TgtRows tr1,
-                                                         double* __restrict__ part, double m,
-                                                         float* __restrict__ loss_out,
-                                                         unsigned* __restrict__ ticket) {
+                                                         double* __restrict__ part) {
   __shared__ double red[16];
   double acc = 0.0;
   const float gs = gscale ? gscale[0] : 1.0f;
@@ -70,29 +68,10 @@ __global__ __launch_bounds__(kBlock) void lp_loss_kernel(const float* __restrict
   }
   if (!part) return;
   acc = block_sum(acc, red);
-  if (!loss_out) {                     // two-launch form: lp_loss_finalize sums the partials
-    if (threadIdx.x == 0) part[blockIdx.x] = acc;
-    return;
-  }
-  if (threadIdx.x == 0) st_sc1(part + blockIdx.x, acc);
-  // one-launch form: the last workgroup to finish sums the partials in index order.  The
-  // counter is the call's own (a word of its workspace after the partials), so calls in
-  // flight on other streams with other workspaces never count each other's workgroups
-  if (!arrive_last(ticket, gridDim.x, (int*)red)) return;
-  double v[kLossBlocks / kBlock];
-#pragma unroll
-  for (int k = 0; k < kLossBlocks / kBlock; ++k) {
-    const int i = threadIdx.x + k * kBlock;
-    v[k] = i < (int)gridDim.x ? ld_sc1(part + i) : 0.0;
-  }
-  double a = 0.0;
-#pragma unroll
-  for (int k = 0; k < kLossBlocks / kBlock; ++k) a += v[k];
-  a = block_sum(a, red);
-  if (threadIdx.x == 0) loss_out[0] = (float)(a / m);
+  if (threadIdx.x == 0) part[blockIdx.x] = acc;   // lp_loss_finalize / a finalize task sums them
 }
 
-// two-launch form: the block partials summed in index order (every load issued first)
+// the block partials summed in index order (every load issued first)
 __global__ void lp_loss_finalize(const double* __restrict__ part, int nblk, double m,
                                  float* __restrict__ out) {
   fin_loss(part, nblk, m, out);
@@ -890,13 +869,9 @@ static FinTable fin_take_for_host(hipStream_t s, const void* w0, size_t wn, int*
 
 using namespace ssq;
 
-// the partials, then the one-launch form's last-arriver counter (lp_loss_ticket)
 extern "C" size_t ssq_lp_loss_workspace_size(int64_t n) {
   (void)n;
-  return kLossBlocks * sizeof(double) + sizeof(double);
-}
-static unsigned* lp_loss_ticket(void* ws) {
-  return (unsigned*)((char*)ws + kLossBlocks * sizeof(double));
+  return kLossBlocks * sizeof(double);
 }
 
 static int lp_loss(const char* what, const float* pred, const float* tgt, const int64_t* idx,
@@ -927,17 +902,9 @@ static int lp_loss(const char* what, const float* pred, const float* tgt, const 
                                : (p == 1.0f ? lp_loss_kernel<1, true> : lp_loss_kernel<2, true>))
                   : (p == 2.0f ? lp_loss_kernel<0, false>
                                : (p == 1.0f ? lp_loss_kernel<1, false> : lp_loss_kernel<2, false>));
-  // A/B knob SSQ_LOSS_ONE_LAUNCH: 1 finalises the loss value in the same launch (last
-  // workgroup to arrive), 0 in a 1-workgroup finalize launch
-  static const bool one = [] {
-    const char* e = getenv("SSQ_LOSS_ONE_LAUNCH");
-    return e && *e ? atoi(e) != 0 : false;
-  }();
-  const bool fuse = one && loss_out;
   hipLaunchKernelGGL(k, dim3(grid), dim3(kBlock), 0, s, pred, tgt, n, p, inv_m, grad, gscale,
-                     relu_mask, vec, tr4, tr1, part, (double)M, fuse ? loss_out : nullptr,
-                     fuse ? lp_loss_ticket(ws) : nullptr);
-  if (loss_out && !fuse) {
+                     relu_mask, vec, tr4, tr1, part);
+  if (loss_out) {
     if (fin_defer_on()) {
       FinTask t{};
       t.kind = 0;

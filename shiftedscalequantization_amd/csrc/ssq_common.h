@@ -212,9 +212,10 @@ __device__ __forceinline__ double block_sum(double v, double* lds /* >= 16 */) {
 // (relaxed agent-scope fetch_add on a per-reduction counter); the workgroup that draws
 // the last ticket reads every partial with sc1 loads (each of them: no acquire fence
 // needed) in a fixed order -- deterministic -- and resets the counter for the next
-// launch.  Every counter is a word of the calling launch's own workspace (zero-filled at
-// allocation, include/ssq.h), so two launches in flight with different workspaces -- e.g. on
-// two streams -- never share one; no counter is a device global.
+// launch.  The one counter (fin_epi's act-delta reduction) is a word of the calling launch's
+// own workspace, zeroed by the launch that writes the partials it counts, so two launches in
+// flight with different workspaces -- e.g. on two streams -- never share one; no counter is a
+// device global.
 typedef __attribute__((address_space(1))) unsigned long long gu64_t;
 typedef __attribute__((address_space(1))) unsigned int gu32_t;
 

@@ -1802,20 +1802,48 @@ def test_epilogue_bwd_delta_split_two_streams(K, defer):
                 np.testing.assert_array_equal(x, b)
 
 
-def test_lp_loss_one_launch_two_streams(K):
-    """ssq_lp_loss's one-launch form keeps its last-arriver counter in the call's workspace
-    (csrc/recon.hip lp_loss_ticket; no device-global counter left in the library): two
-    calls in flight on two streams give the one-stream values and gradients bit for bit.
-    The form is an env knob read once per process, so it runs in a process of its own."""
-    import os
-    import subprocess
-    import sys
-    here = os.path.dirname(os.path.abspath(__file__))
-    env = dict(os.environ, SSQ_LOSS_ONE_LAUNCH="1")
-    r = subprocess.run([sys.executable, os.path.join(here, "lp_loss_streams_worker.py")], env=env,
-                       stdout=subprocess.PIPE, stderr=subprocess.STDOUT, timeout=240)
-    out = r.stdout.decode(errors="replace")
-    assert r.returncode == 0 and "LP_LOSS_STREAMS_OK" in out, out[-3000:]
+@pytest.mark.parametrize("defer", [False, True])
+def test_lp_loss_two_streams(K, defer):
+    """ssq_lp_loss keeps no device-global state (its one-launch form and the counter it
+    needed are gone): the partials live in the call's workspace, one per stream, so two loss
+    passes in flight on two streams -- standalone finalize or finalize tasks queued on each
+    stream and flushed there -- give the one-stream values and gradients bit for bit, and the
+    value is the float64 loss to 1e-6."""
+    from shiftedscalequantization_amd import _capi as A
+    gen = torch.Generator().manual_seed(77)
+    # 1024 workgroups apiece (the launch's cap): both grids fill the chip together
+    preds = [torch.randn(64, 256, 28, 28, generator=gen).cuda() for _ in range(2)]
+    tgts = [torch.randn(64, 256, 28, 28, generator=gen).cuda() for _ in range(2)]
+
+    def run(i, p):
+        with K.deferred_finalize(defer):
+            loss, g = K.lp_loss_and_grad(preds[i], tgts[i], p)
+        return loss, g
+
+    def bits(r):
+        return [host(t).reshape(-1).view(np.int32).copy() for t in r]
+
+    for p in (2.0, 2.4):
+        base = []
+        for i in range(2):
+            r = run(i, p)
+            torch.cuda.synchronize()
+            base.append(bits(r))
+        streams = [torch.cuda.Stream(), torch.cuda.Stream()]
+        for _ in range(8):
+            res = []
+            for i in range(2):
+                with torch.cuda.stream(streams[i]), A.workspace_scope({}):
+                    res.append(run(i, p))
+            torch.cuda.synchronize()
+            for i in range(2):
+                for a, b in zip(bits(res[i]), base[i]):
+                    np.testing.assert_array_equal(a, b)
+        if p == 2.0:
+            for i in range(2):
+                ref = (preds[i] - tgts[i]).double().abs().pow(p).sum(1).mean().item()
+                got = float(base[i][0].view(np.float32)[0])
+                assert abs(got - ref) <= 1e-6 * abs(ref), (got, ref)
 
 
 @pytest.mark.parametrize("bs,Co,Ci,lam", [(32, 1000, 512, 0.01), (8, 10, 64, 0.0), (64, 37, 320, 0.01),
