@@ -473,10 +473,16 @@ def main():
         out["recon"] = recon
     if recon_configs is not None:
         rc = recon_configs_roofline()
-        for k, v in recon_configs.items():
-            if rc is not None and k in rc.get("configs", {}):
-                v["roofline"] = rc["configs"][k]
         if rc is not None:
+            keep = ("wall_us_per_iteration", "ssq_set_us", "ssq_set_bytes", "achieved", "peak",
+                    "unit", "frac", "conv_side_ssq_kernels_us", "library_convs_gemms_other_us")
+            for k, v in recon_configs.items():
+                # one roofline per loop: config3's two phases, the fused loop of configs 4 / 5
+                loops = {kk: vv for kk, vv in rc.get("configs", {}).items()
+                         if kk == k or kk.startswith(k + "_")}
+                if loops:
+                    v["roofline"] = {kk[len(k) + 1:] or "fused_loop":
+                                     {f: vv[f] for f in keep if f in vv} for kk, vv in loops.items()}
             recon_configs["roofline_source"] = {kk: vv for kk, vv in rc.items() if kk != "configs"}
         out["recon_configs"] = recon_configs
     if validation is not None:

@@ -1918,6 +1918,8 @@ class Conv2dFn(torch.autograd.Function):
                 gw = conv_wgrad_gemm(x, g, weight.shape, stride, padding, col=col)
             elif _use_wgrad_bmm(x, weight, stride, padding, groups):
                 gw = conv_wgrad_1x1_bmm(x, g, weight.shape)
+            elif _use_wgrad_grouped_gemm(x, weight, stride, padding, groups):
+                gw = conv_wgrad_grouped_gemm(x, g, weight.shape, stride, padding, groups)
             else:
                 gw = conv_wgrad(x, g, weight.shape, stride, padding, groups)
         return gx, gw, None, None, None, None
@@ -2007,6 +2009,46 @@ def conv_wgrad_1x1_bmm(x, dy, w_shape):
     co, p = int(w_shape[0]), int(x.shape[2] * x.shape[3])
     gw = torch.matmul(dy.detach().reshape(n, co, p), x.detach().reshape(n, c, p).transpose(1, 2))
     return gw.sum(0).view(tuple(w_shape))
+
+
+# Grouped (not depthwise) convs on small output planes (OH*OW <= 196: RegNetX-3200M's g = 9 /
+# 21 'b' convs of stages 3 and 4): the weight gradient as the im2col operands of every channel
+# (ssq_wgrad_gemm_operands) and ONE strided-batched library GEMM over the groups,
+# dW[g] = dy2[g rows] @ col[:, g columns] (conv_wgrad_grouped_gemm), instead of K17's implicit
+# GEMM, which runs at 6-11 TF there.  tools/wgrad_grouped_probe.py
+# (profiles/r6_wgrad_grouped_probe.jsonl), batch 32: s3.b1 268.6 -> 115.5 us, s3.b2 205.4 ->
+# 91.0, s4.b1 243.9 -> 70.3, s4.b2 121.7 -> 57.6; on the larger planes of stages 1-2 (g = 2,
+# 4) K17 stays faster and keeps them.  Bit-identical run to run, within 1e-6 of float64.
+# A/B knob: SSQ_WGRAD_GROUPED_GEMM=0.
+WGRAD_GROUPED_GEMM = os.environ.get("SSQ_WGRAD_GROUPED_GEMM", "1") != "0"
+
+
+def _use_wgrad_grouped_gemm(x, weight, stride, padding, groups=1):
+    if not WGRAD_GROUPED_GEMM or WGRAD_POLICY != "auto" or groups <= 1 or weight.shape[1] <= 1:
+        return False
+    if isinstance(stride, (tuple, list)) and len(set(stride)) != 1:
+        return False
+    if isinstance(padding, str) or (isinstance(padding, (tuple, list)) and len(set(padding)) != 1):
+        return False
+    oh, ow = _out_plane(x, weight, stride, padding)
+    Co, Cig, R, S = (int(v) for v in weight.shape)
+    NP = x.shape[0] * oh * ow
+    if NP * Cig * groups * R * S >= (1 << 31) or Co * NP >= (1 << 31):
+        return False
+    return oh * ow <= 196
+
+
+def conv_wgrad_grouped_gemm(x, dy, w_shape, stride, padding, groups):
+    """d loss / d weight of a grouped conv: the im2col matrix of every input channel and the
+    permuted gradient (ssq_wgrad_gemm_operands, as for an ungrouped conv of C_in = Cig * G),
+    then one strided-batched GEMM over the groups (group g: its Cog rows of dy2 against its
+    Cig * R * S columns of col)."""
+    Co, Cig, R, S = (int(v) for v in w_shape)
+    col, dy2 = gemm_operands(x, dy, (Co, Cig * groups, R, S), stride, padding)
+    NP = col.shape[0]
+    a = dy2.view(groups, Co // groups, NP)
+    b = col.view(NP, groups, Cig * R * S).transpose(0, 1)
+    return torch.matmul(a, b).reshape(tuple(w_shape))
 
 
 def _use_fwd_gemm(x, weight, stride, padding, groups=1):
@@ -2099,6 +2141,7 @@ def conv2d(x, weight, stride=1, padding=0, dilation=1, groups=1):
     if weight.requires_grad and torch.is_grad_enabled() and \
             (dilation if isinstance(dilation, int) else max(dilation)) == 1 and \
             (_use_wgrad_gemm(x, weight, stride, padding, groups) or
+             _use_wgrad_grouped_gemm(x, weight, stride, padding, groups) or
              (conv_wgrad_supported(x, weight, stride, padding, dilation, groups) and
               _use_k17(x, weight, stride, padding, groups))):
         return Conv2dFn.apply(x, weight, stride, padding, dilation, groups)

@@ -1145,6 +1145,46 @@ def test_conv_wgrad_1x1_bmm_matches_fp64(K, cfg):
 
 
 @pytest.mark.parametrize("cfg", [
+    # (Nb, C, H, stride, groups): RegNetX-3200M s3.b1 / s3.b2 / s4.b2 'b' convs (group width
+    # 48), a ragged one, and s2.b2's 28x28 plane (K17 keeps it)
+    (32, 432, 28, 2, 9), (32, 432, 14, 1, 9), (32, 1008, 7, 1, 21), (3, 36, 9, 1, 3),
+    (8, 192, 28, 1, 4)])
+def test_conv_wgrad_grouped_gemm_matches_fp64(K, cfg):
+    """Grouped-conv weight gradients on output planes <= 196 pixels as the im2col operands of
+    every channel and one strided-batched GEMM over the groups (K.conv_wgrad_grouped_gemm,
+    WGRAD_GROUPED_GEMM): vs the fp64 CPU gradient within the fp32 accumulation bound,
+    bit-identical run to run, and what K.conv2d's training path hands the weight (larger
+    planes: K17 as before)."""
+    Nb, C, H, st, G = cfg
+    gen = torch.Generator().manual_seed(sum(cfg))
+    w_shape = (C, C // G, 3, 3)
+    x = torch.relu(torch.randn(Nb, C, H, H, generator=gen))
+    w = torch.randn(w_shape, generator=gen) * 0.1
+    y = torch.nn.functional.conv2d(x, w, None, st, 1, 1, G)
+    dy = torch.randn(y.shape, generator=gen)
+    ref = torch.nn.grad.conv2d_weight(x.double(), w_shape, dy.double(), st, 1, groups=G)
+    mag = torch.nn.grad.conv2d_weight(x.double().abs(), w_shape, dy.double().abs(), st, 1, groups=G)
+    xd, dyd, wd = x.cuda(), dy.cuda(), w.cuda()
+    small = y.shape[2] * y.shape[3] <= 196
+    assert K._use_wgrad_grouped_gemm(xd, wd, st, 1, G) == small
+    dw1 = K.conv_wgrad_grouped_gemm(xd, dyd, w_shape, st, 1, G)
+    dw2 = K.conv_wgrad_grouped_gemm(xd, dyd, w_shape, st, 1, G)
+    np.testing.assert_array_equal(host(dw1).view(np.int32), host(dw2).view(np.int32))
+    err = (dw1.double().cpu() - ref).abs()
+    assert bool((err <= 1e-5 * mag + 1e-30).all()), float((err / mag.clamp_min(1e-30)).max())
+    old_det = torch.backends.cudnn.deterministic
+    torch.backends.cudnn.deterministic = True
+    try:
+        wg = wd.clone().requires_grad_(True)
+        K.conv2d(xd, wg, st, 1, 1, G).backward(dyd)
+    finally:
+        torch.backends.cudnn.deterministic = old_det
+    if small:
+        np.testing.assert_array_equal(host(wg.grad).view(np.int32), host(dw1).view(np.int32))
+    assert bool(((wg.grad.double().cpu() - ref).abs() <= 1e-5 * mag + 1e-30).all())
+
+
+@pytest.mark.parametrize("cfg", [
     # (Nb, C, H, Co, k, stride, pad): ResNet-18 layer3 / layer3.0 s2 / layer4 / layer4.0 s2
     # at batch 32 (the shapes the GEMM policy takes), a 5x5 and ragged sizes
     (32, 256, 14, 256, 3, 1, 1), (32, 128, 28, 256, 3, 2, 1), (32, 512, 7, 512, 3, 1, 1),

@@ -69,6 +69,7 @@ step_cfgtrace() {
   python3 $R/tools/recon_roofline.py --configs "$KT" $OUT/cfg_side_$TAG.json \
     $OUT/recon_configs_roofline_$TAG.json > $OUT/recon_configs_roofline_$TAG.txt 2>&1 \
     || fail "configs roofline failed" $OUT/recon_configs_roofline_$TAG.txt
+  gzip -c "$KT" > $OUT/cfg_trace_$TAG.csv.gz
   rm -f "$KT"
   cat $OUT/recon_configs_roofline_$TAG.txt | cut -c1-200
 }

@@ -49,7 +49,11 @@ def main():
         forms = {"k17": lambda: K.conv_wgrad(x, dy, w_shape, st, 1, groups),
                  "grouped_gemm": lambda: grouped_gemm(x, dy, w_shape, st, 1, groups)}
         for k, fn in forms.items():
-            a, b = fn(), fn()
+            try:
+                a, b = fn(), fn()
+            except K.A.SSQError as e:          # e.g. K17's LDS tile on 112-wide rows
+                out[k] = {"unsupported": str(e)[:120]}
+                continue
             torch.cuda.synchronize()
             ms = graph_time_ms(fn, reps=20, rounds=5)
             err = ((a.double().cpu() - ref).abs().max() / ref.abs().max()).item()
