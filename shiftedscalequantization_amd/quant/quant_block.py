@@ -121,9 +121,13 @@ class BaseQuantBlock(nn.Module):
                 if q is None and self.use_act_quant:
                     out = self.act_quantizer(out)
                 return out
-            if q is not None:   # + the block's act quant in the same pass
-                return K.bias_act_quant(raw, bias, residual, relu, q.delta, q.zero_point,
-                                        q.n_bits, q.sym)
+            if q is not None:
+                # + the block's act quant in the same pass: the general epilogue with no
+                # gamma^z / phi^z, whose backward sums the act delta per (n, c) row as the
+                # fused tail does -- so the recon loop (BRECQ's act phase without --bias_cal)
+                # takes the block's last epilogue, the loss and its backward as one pass
+                # (lazy), bit-identical to this unfused form
+                return K.epilogue(raw, bias, None, None, residual, relu, q, lazy=lazy_ok)
             lazy = lazy_ok and not self.use_act_quant
             out = K.bias_act(raw, bias, residual, relu, lazy=lazy)
             if self.use_act_quant:

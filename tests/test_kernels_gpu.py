@@ -729,16 +729,14 @@ def _compare_fused_unfused_det(qb, x, act, affine=()):
     np.testing.assert_array_equal(outs[0][1], outs[1][1])
     assert len(outs[0][2]) == len(outs[1][2])
     for a, b in zip(outs[0][2], outs[1][2]):
-        if affine:
-            # the affine epilogue reduces the act-delta sums per (n, c) row, the fq backward
-            # per workgroup: the same fp32 terms -- (x/d)/d with two IEEE divides on both
-            # sides, as torch's div backward -- summed in double in two orders.  Until r6 the
-            # float4 fq backward took (x/d)*(1/d), one ulp per term of two ~1e2 sums that
-            # cancel to ~1e-2, and that ulp reached 2.0e-4 of the result (r5ev5, r5ev7b:
-            # 18.1153 vs 18.1189).  Now only the double sums' order differs: ~1e-16 * 1e4
-            np.testing.assert_allclose(a, b, rtol=1e-6, atol=0)
-        else:
-            np.testing.assert_array_equal(a, b)
+        # the fused epilogue reduces the act-delta sums per (n, c) row (with or without
+        # gamma^z / phi^z since r6), the fq backward per workgroup: the same fp32 terms --
+        # (x/d)/d with two IEEE divides on both sides, as torch's div backward -- summed in
+        # double in two orders.  Until r6 the float4 fq backward took (x/d)*(1/d), one ulp
+        # per term of two ~1e2 sums that cancel to ~1e-2, and that ulp reached 2.0e-4 of the
+        # result (r5ev5, r5ev7b: 18.1153 vs 18.1189).  Now only the double sums' order
+        # differs: ~1e-16 * 1e4 of the result, far below one fp32 ulp
+        np.testing.assert_allclose(a, b, rtol=1e-6, atol=0)
     for a, b in zip(outs[0][3], outs[1][3]):   # gamma / phi: double vs torch's fp32 sums
         np.testing.assert_allclose(a, b, rtol=1e-4, atol=1e-4 * np.abs(b).max())
 
