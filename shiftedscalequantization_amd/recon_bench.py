@@ -216,6 +216,11 @@ def run_brecq_block(dev, arch, name, n_cali=1024, iters=200, warmup=20, rank=0, 
         qnn.set_quant_state(True, True)
         with torch.no_grad():
             qnn(cali[:64])                  # act-delta init (Brecq/main_imagenet.py:231-236)
+        from .parallel_dp import world
+        if world() > 1:
+            # each rank initialised on its own shard: all-average, as main_imagenet.py does
+            # (Brecq/main_imagenet_dist.py:210-211)
+            qnn.synchorize_activation_statistics()
         qnn.disable_network_output_quantization()
         timed("act", act_quant=True, opt_mode="mse", lr=4e-4, p=2.4)
     del qnn, cnn, cali
@@ -259,7 +264,8 @@ def run_recon_configs(dev, world, rank, iters=200, configs=RECON_CONFIGS):
             finally:
                 builtins.print = _print
             out[f"config{cfg}"] = {"arch": arch, "block": name, "loop": what,
-                                   "iters_per_s": ips, "timed_iters": iters,
+                                   "iters_per_s": ips, "batch_per_rank": 32, "n_gpus": world,
+                                   "timed_iters": iters,
                                    "setup_and_run_s": round(time.perf_counter() - t0, 1)}
     finally:
         cudnn.benchmark, cudnn.deterministic = saved
