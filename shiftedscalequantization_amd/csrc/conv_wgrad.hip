@@ -563,20 +563,25 @@ __global__ __launch_bounds__(256) void wgrad_stage2(const float* __restrict__ pa
 // are laid over (output row, output column) once (no per-pixel division), each keeps R*S
 // fp32 partials over its pixels, and the workgroup reduces them in a fixed order (wave
 // shuffle tree, waves in order) into part[split][c][rs].
+constexpr int kPf = 8;  // dy loads in flight per thread in the depthwise product loops
+
 template <int RSMAX>
 __global__ __launch_bounds__(256) void wgrad_dw_stage1(const float* __restrict__ x,
                                                        const float* __restrict__ dy, int C, int H,
                                                        int W, int OH, int OW, int R, int S,
-                                                       int st, int pad, int spl,
-                                                       FastDiv dWp, float* __restrict__ part) {
-  extern __shared__ float xs[];  // [H + 2 pad][W + 2 pad]
+                                                       int st, int pad, int spl, int bh,
+                                                       int nbands, FastDiv dWp,
+                                                       float* __restrict__ part) {
+  extern __shared__ float xs[];  // the band's padded input rows [(bh - 1) st + R][W + 2 pad]
   __shared__ float red[4][RSMAX];
-  const int c = blockIdx.x, split = blockIdx.y;
+  const int c = blockIdx.x, split = blockIdx.y / nbands, band = blockIdx.y - split * nbands;
   const int n0 = split * spl;
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
   const int RS = R * S;
-  const int Hp = H + 2 * pad, Wp = W + 2 * pad;
-  const int HpWp = Hp * Wp;
+  const int Wp = W + 2 * pad;
+  const int oh_lo = band * bh, oh_hi = min(OH, oh_lo + bh);
+  const int prow0 = oh_lo * st;  // first padded input row of the band
+  const int HpWp = ((oh_hi - 1) * st + R - prow0) * Wp;  // elements staged per sample
   // product layout: thread -> (output row o0 + k*op, output column ocw)
   const int ocols = min(OW, 256), orp = 256 / ocols;
   const int or0 = tid / ocols, ocw = tid - or0 * ocols;
@@ -587,7 +592,7 @@ __global__ __launch_bounds__(256) void wgrad_dw_stage1(const float* __restrict__
   for (int n = n0; n < n0 + spl; ++n) {
     const float* xp = x + ((int64_t)n * C + c) * HW;
     const float* dp = dy + ((int64_t)n * C + c) * OHW;
-    __syncthreads();  // the previous sample's products are done with the plane
+    __syncthreads();  // the previous sample's products are done with the rows
     // 8 loads in flight per thread, then the 8 LDS stores
     for (int e0 = tid; e0 < HpWp; e0 += 256 * 8) {
       float v[8];
@@ -595,7 +600,7 @@ __global__ __launch_bounds__(256) void wgrad_dw_stage1(const float* __restrict__
       for (int u = 0; u < 8; ++u) {
         const int e = e0 + 256 * u;
         const int rr = (int)fdiv((uint32_t)e, dWp), cc = e - rr * Wp;
-        const int ih = rr - pad, iw = cc - pad;
+        const int ih = prow0 + rr - pad, iw = cc - pad;
         const bool ok = e < HpWp && ih >= 0 && ih < H && iw >= 0 && iw < W;
         const float t = xp[ok ? ih * W + iw : 0];
         v[u] = ok ? t : 0.0f;
@@ -606,18 +611,120 @@ __global__ __launch_bounds__(256) void wgrad_dw_stage1(const float* __restrict__
     }
     __syncthreads();
     if (or0 < orp) {
-      for (int oh = or0; oh < OH; oh += orp) {
-        for (int ow = ocw; ow < OW; ow += ocols) {
-          const float g = dp[oh * OW + ow];
-          const float* xr = xs + oh * st * Wp + ow * st;
+      // the dy values of kPf rows are loaded together: one load latency per kPf products
+      for (int ow = ocw; ow < OW; ow += ocols) {
+        for (int oh0 = oh_lo + or0; oh0 < oh_hi; oh0 += kPf * orp) {
+          float g[kPf];
 #pragma unroll
-          for (int j = 0; j < RSMAX; ++j) {
-            if (j < RS) {
-              const int r = j / S, q = j - r * S;
-              acc[j] = __fadd_rn(acc[j], __fmul_rn(g, xr[r * Wp + q]));
+          for (int k = 0; k < kPf; ++k) {
+            const int oh = oh0 + k * orp;
+            g[k] = 0.0f;
+            if (oh < oh_hi) g[k] = dp[oh * OW + ow];
+          }
+#pragma unroll 1
+          for (int k = 0; k < kPf; ++k) {  // rolled (g shifts down): no hoisted LDS reads
+            const int oh = oh0 + k * orp;
+            if (oh >= oh_hi) break;
+            const float* xr = xs + (oh * st - prow0) * Wp + ow * st;
+#pragma unroll
+            for (int j = 0; j < RSMAX; ++j) {
+              if (j < RS) {
+                const int r = j / S, q = j - r * S;
+                acc[j] = __fadd_rn(acc[j], __fmul_rn(g[0], xr[r * Wp + q]));
+              }
             }
+#pragma unroll
+            for (int t = 0; t + 1 < kPf; ++t) g[t] = g[t + 1];
           }
         }
+      }
+    }
+  }
+#pragma unroll
+  for (int j = 0; j < RSMAX; ++j) {
+    float v = acc[j];
+#pragma unroll
+    for (int o = 32; o >= 1; o >>= 1) v = __fadd_rn(v, __shfl_xor(v, o));
+    if (lane == 0) red[w][j] = v;
+  }
+  __syncthreads();
+  if (tid < RS)
+    part[((int64_t)blockIdx.y * C + c) * RS + tid] =
+        __fadd_rn(__fadd_rn(__fadd_rn(red[0][tid], red[1][tid]), red[2][tid]), red[3][tid]);
+}
+
+// Depthwise weight gradient on small planes (<= 4 KiB padded: 28x28 and below), where a
+// sample's plane is too few products (49 on 7x7) to hide a load round trip per sample:
+// workgroup (c, split) stages nb samples' zero-padded x planes per pass (16 loads in flight
+// per thread, one barrier pair per pass) and lays its threads over (sample, pixel); dy is
+// read straight from global memory, one independent load per product row.  Partials and
+// their fixed-order reduction as wgrad_dw_stage1.
+template <int RSMAX>
+__global__ __launch_bounds__(256) void wgrad_dw_small(const float* __restrict__ x,
+                                                      const float* __restrict__ dy, int C, int H,
+                                                      int W, int OH, int OW, int R, int S, int st,
+                                                      int pad, int spl, int nb, FastDiv dWp,
+                                                      FastDiv dP, FastDiv dOHW, FastDiv dOW,
+                                                      float* __restrict__ part) {
+  extern __shared__ float xs[];  // [nb][H + 2 pad][W + 2 pad]
+  __shared__ float red[4][RSMAX];
+  const int c = blockIdx.x, split = blockIdx.y;
+  const int n0 = split * spl;
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const int RS = R * S;
+  const int Wp = W + 2 * pad, HpWp = (H + 2 * pad) * Wp;
+  const int OHW = OH * OW, HW = H * W;
+  constexpr int U = 8;
+  float acc[RSMAX];
+#pragma unroll
+  for (int j = 0; j < RSMAX; ++j) acc[j] = 0.0f;
+  for (int n = n0; n < n0 + spl; n += nb) {
+    const int cnt = min(nb, n0 + spl - n);
+    const float* xb = x + ((int64_t)n * C + c) * HW;
+    const float* db = dy + ((int64_t)n * C + c) * OHW;
+    const int tot = cnt * HpWp, totp = cnt * OHW;
+    __syncthreads();  // the previous pass's products are done with the planes
+    for (int e0 = tid; e0 < tot; e0 += 256 * U) {
+      float v[U];
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        const int e = e0 + 256 * u;
+        const int j = (int)fdiv((uint32_t)e, dP), rem = e - j * HpWp;
+        const int rr = (int)fdiv((uint32_t)rem, dWp), cc = rem - rr * Wp;
+        const int ih = rr - pad, iw = cc - pad;
+        v[u] = 0.0f;  // padding and slots past the pass issue no load
+        if (e < tot && ih >= 0 && ih < H && iw >= 0 && iw < W) v[u] = xb[(int64_t)j * C * HW + ih * W + iw];
+      }
+#pragma unroll
+      for (int u = 0; u < U; ++u)
+        if (e0 + 256 * u < tot) xs[e0 + 256 * u] = v[u];
+    }
+    __syncthreads();
+    for (int p0 = tid; p0 < totp; p0 += 256 * kPf) {
+      float g[kPf];
+#pragma unroll
+      for (int k = 0; k < kPf; ++k) {  // the dy values of kPf pixels in one load round
+        const int p = p0 + 256 * k;
+        const int j = (int)fdiv((uint32_t)p, dOHW);
+        g[k] = 0.0f;
+        if (p < totp) g[k] = db[(int64_t)j * C * OHW + (p - j * OHW)];
+      }
+#pragma unroll 1
+      for (int k = 0; k < kPf; ++k) {  // rolled (g shifts down): no hoisted LDS reads
+        const int p = p0 + 256 * k;
+        if (p >= totp) break;
+        const int j = (int)fdiv((uint32_t)p, dOHW), q = p - j * OHW;
+        const int oh = (int)fdiv((uint32_t)q, dOW), ow = q - oh * OW;
+        const float* xr = xs + j * HpWp + oh * st * Wp + ow * st;
+#pragma unroll
+        for (int kk = 0; kk < RSMAX; ++kk) {
+          if (kk < RS) {
+            const int r = kk / S, q2 = kk - r * S;
+            acc[kk] = __fadd_rn(acc[kk], __fmul_rn(g[0], xr[r * Wp + q2]));
+          }
+        }
+#pragma unroll
+        for (int t = 0; t + 1 < kPf; ++t) g[t] = g[t + 1];
       }
     }
   }
@@ -635,6 +742,20 @@ __global__ __launch_bounds__(256) void wgrad_dw_stage1(const float* __restrict__
 }
 
 static bool is_depthwise(int64_t C, int64_t Co, int64_t G) { return G == C && G == Co && G > 1; }
+// samples staged per pass by wgrad_dw_small (0: the plane is over 4 KiB, wgrad_dw_stage1)
+static int dw_stage(int64_t H, int64_t W, int64_t pad, int spl) {
+  const int64_t b = (H + 2 * pad) * (W + 2 * pad) * (int64_t)sizeof(float);
+  if (b > 4096) return 0;
+  return (int)std::max<int64_t>(1, std::min<int64_t>(spl, 32 * 1024 / b));
+}
+// output rows per band of wgrad_dw_stage1: planes over 8 KiB are cut into row bands of
+// <= 8 KiB of staged input each (more, smaller workgroups: a 112x112 plane is 8 bands)
+static int dw_band_rows(int64_t H, int64_t W, int64_t R, int64_t st, int64_t pad, int64_t OH) {
+  const int64_t Wp = W + 2 * pad, row = Wp * (int64_t)sizeof(float);
+  if ((H + 2 * pad) * row <= 8192) return (int)OH;
+  const int64_t rows = std::max<int64_t>(R, 8192 / row);
+  return (int)std::min<int64_t>(OH, (rows - R) / st + 1);
+}
 static bool dw_lds_ok(int64_t H, int64_t W, int64_t pad) {
   return (H + 2 * pad) * (W + 2 * pad) * (int64_t)sizeof(float) <= 128 * 1024;
 }
@@ -1159,7 +1280,13 @@ extern "C" size_t ssq_conv_wgrad_workspace_size(int64_t Nb, int64_t C, int64_t H
   if (is_depthwise(C, Co, groups) && R * S <= 25 && Nb >= 1 && dw_lds_ok(H, W, pad)) {
     int spl;
     const int ns = dw_splits(Nb, C, &spl);
-    return (size_t)ns * (size_t)C * (size_t)(R * S) * sizeof(float);
+    const int64_t OH = (H + 2 * pad - R) / stride + 1;
+    int64_t nbands = 1;
+    if (dw_stage(H, W, pad, spl) == 0 && OH >= 1) {
+      const int bh = dw_band_rows(H, W, R, stride, pad, OH);
+      nbands = (OH + bh - 1) / bh;
+    }
+    return (size_t)ns * (size_t)nbands * (size_t)C * (size_t)(R * S) * sizeof(float);
   }
   {
     BandGeo gb;
@@ -1202,7 +1329,30 @@ extern "C" int ssq_conv_wgrad(const float* x, const float* dy, int64_t Nb, int64
     const size_t need = (size_t)ns * (size_t)C * (size_t)(R * S) * sizeof(float);
     SSQ_REQUIRE(ws && ws_bytes >= need, SSQ_E_WS, "ssq_conv_wgrad: workspace too small");
     const dim3 grid((unsigned)C, (unsigned)ns);
-    const size_t lds = (size_t)(H + 2 * pad) * (W + 2 * pad) * sizeof(float);
+    const int64_t plane = (H + 2 * pad) * (W + 2 * pad);
+    const int nb = dw_stage(H, W, pad, spl);
+    if (nb > 0) {
+      const size_t lds = (size_t)nb * plane * sizeof(float);  // <= 32 KiB
+      const FastDiv dWp = make_fastdiv((uint32_t)(W + 2 * pad)), dP = make_fastdiv((uint32_t)plane),
+                    dOHW = make_fastdiv((uint32_t)(OH * OW)), dOW = make_fastdiv((uint32_t)OW);
+      if (R * S <= 9)
+        hipLaunchKernelGGL(wgrad_dw_small<9>, grid, dim3(256), lds, s, x, dy, (int)C, (int)H,
+                           (int)W, (int)OH, (int)OW, (int)R, (int)S, (int)stride, (int)pad, spl,
+                           nb, dWp, dP, dOHW, dOW, (float*)ws);
+      else
+        hipLaunchKernelGGL(wgrad_dw_small<25>, grid, dim3(256), lds, s, x, dy, (int)C, (int)H,
+                           (int)W, (int)OH, (int)OW, (int)R, (int)S, (int)stride, (int)pad, spl,
+                           nb, dWp, dP, dOHW, dOW, (float*)ws);
+      const int64_t n = C * R * S;
+      hipLaunchKernelGGL(wgrad_stage2, dim3((unsigned)std::min<int64_t>((n + 63) / 64, 4096)),
+                         dim3(256), 0, s, (const float*)ws, ns, n, dw);
+      return check_launch("ssq_conv_wgrad");
+    }
+    const int bh = dw_band_rows(H, W, R, stride, pad, OH);
+    const int nbands = (int)((OH + bh - 1) / bh);
+    SSQ_REQUIRE(ws_bytes >= need * (size_t)nbands, SSQ_E_WS, "ssq_conv_wgrad: workspace too small");
+    const dim3 gridb((unsigned)C, (unsigned)(ns * nbands));
+    const size_t lds = (size_t)(((int64_t)bh - 1) * stride + R) * (W + 2 * pad) * sizeof(float);
     static bool dw_attr = false;
     if (!dw_attr) {  // dynamic LDS beyond 64 KiB must be opted into
       hipFuncSetAttribute((const void*)wgrad_dw_stage1<9>,
@@ -1212,16 +1362,16 @@ extern "C" int ssq_conv_wgrad(const float* x, const float* dy, int64_t Nb, int64
       dw_attr = true;
     }
     if (R * S <= 9)
-      hipLaunchKernelGGL(wgrad_dw_stage1<9>, grid, dim3(256), lds, s, x, dy, (int)C, (int)H, (int)W,
-                         (int)OH, (int)OW, (int)R, (int)S, (int)stride, (int)pad, spl,
+      hipLaunchKernelGGL(wgrad_dw_stage1<9>, gridb, dim3(256), lds, s, x, dy, (int)C, (int)H, (int)W,
+                         (int)OH, (int)OW, (int)R, (int)S, (int)stride, (int)pad, spl, bh, nbands,
                          make_fastdiv((uint32_t)(W + 2 * pad)), (float*)ws);
     else
-      hipLaunchKernelGGL(wgrad_dw_stage1<25>, grid, dim3(256), lds, s, x, dy, (int)C, (int)H, (int)W,
-                         (int)OH, (int)OW, (int)R, (int)S, (int)stride, (int)pad, spl,
+      hipLaunchKernelGGL(wgrad_dw_stage1<25>, gridb, dim3(256), lds, s, x, dy, (int)C, (int)H, (int)W,
+                         (int)OH, (int)OW, (int)R, (int)S, (int)stride, (int)pad, spl, bh, nbands,
                          make_fastdiv((uint32_t)(W + 2 * pad)), (float*)ws);
     const int64_t n = C * R * S;
     hipLaunchKernelGGL(wgrad_stage2, dim3((unsigned)std::min<int64_t>((n + 63) / 64, 4096)),
-                       dim3(256), 0, s, (const float*)ws, ns, n, dw);
+                       dim3(256), 0, s, (const float*)ws, ns * nbands, n, dw);
     return check_launch("ssq_conv_wgrad");
   }
   {

@@ -966,7 +966,14 @@ def wgrad_form(request):
     (2, 300, 7, 130, 1, 1, 0, 1), (2, 48, 12, 96, 1, 1, 0, 2), (4, 16, 5, 24, 1, 2, 0, 1),
     # depthwise path: stride 2, planes wider than a wave, 5x5, odd batch
     (3, 32, 57, 32, 3, 2, 1, 32), (2, 144, 28, 144, 3, 1, 1, 144), (5, 16, 11, 16, 5, 1, 2, 16),
-    (32, 8, 7, 8, 3, 1, 1, 8)])
+    (32, 8, 7, 8, 3, 1, 1, 8),
+    # depthwise, several samples staged per pass: MobileNetV2 features.16 (16 samples of a
+    # 7x7 plane in one pass), a ragged last pass (11 samples, 9 per pass), 5x5 on 14x14
+    (32, 960, 7, 960, 3, 1, 1, 960), (11, 520, 28, 520, 3, 2, 1, 520),
+    (8, 400, 14, 400, 5, 1, 2, 400),
+    # depthwise on planes cut into row bands: 112x112 (8 bands, a short last one), 5x5
+    # stride 2 (3 bands)
+    (2, 16, 112, 16, 3, 1, 1, 16), (2, 8, 64, 8, 5, 2, 2, 8)])
 def test_conv_wgrad_matches_fp64(K, cfg, wgrad_form):
     """K17 weight gradient (both non-depthwise forms) vs the fp64 CPU gradient: error
     within the fp32 accumulation bound, bit-identical run to run, and the autograd wrapper
