@@ -1883,13 +1883,17 @@ def _pair(v):
 
 
 class Conv2dFn(torch.autograd.Function):
-    """F.conv2d whose weight gradient runs on K17 (deterministic, MFMA); the forward and
-    the input gradient stay on MIOpen."""
+    """F.conv2d whose weight gradient runs on K17 (deterministic, MFMA) or a library GEMM
+    form; the forward and the input gradient stay on MIOpen except where a GEMM form is
+    faster (small-plane im2col forwards, 1x1 stride-2 forwards, 1x1 stride-1 input gradients)."""
 
     @staticmethod
-    def forward(ctx, x, weight, stride, padding, dilation, groups):
+    def forward(ctx, x, weight, stride, padding, dilation, groups, lib_wgrad=False):
+        # lib_wgrad: a 1x1 conv taken for its GEMM input gradient only; its weight gradient
+        # (if any) stays on MIOpen
         ctx.cfg = (stride, padding, dilation, groups)
-        if _use_fwd_gemm(x, weight, stride, padding, groups):
+        ctx.lib_wgrad = lib_wgrad
+        if not lib_wgrad and _use_fwd_gemm(x, weight, stride, padding, groups):
             # small planes: the forward as one library GEMM over the im2col matrix, kept
             # for the weight gradient's GEMM
             y, col = conv_fwd_gemm(x, weight, stride, padding)
@@ -1906,14 +1910,20 @@ class Conv2dFn(torch.autograd.Function):
         stride, padding, dilation, groups = ctx.cfg
         g = g.contiguous()
         gx = gw = None
-        if ctx.needs_input_grad[0]:
+        if ctx.needs_input_grad[0] and _use_dgrad_1x1(x, weight, stride, padding, groups):
+            gx = conv1x1_dgrad_gemm(g, weight)
+        elif ctx.needs_input_grad[0]:
             # the saved input itself, not torch.nn.grad.conv2d_input's expanded dummy: the
             # MIOpen backend makes an expanded input contiguous first (one activation-sized
             # copy per call, 8.4 us on a ResNet-18 layer1 batch)
             gx = torch.ops.aten.convolution_backward(
                 g, x, weight, None, _pair(stride), _pair(padding), _pair(dilation), False,
                 [0, 0], groups, (True, False, False))[0]
-        if ctx.needs_input_grad[1]:
+        if ctx.needs_input_grad[1] and ctx.lib_wgrad:
+            gw = torch.ops.aten.convolution_backward(
+                g, x, weight, None, _pair(stride), _pair(padding), _pair(dilation), False,
+                [0, 0], groups, (False, True, False))[1]
+        elif ctx.needs_input_grad[1]:
             if _use_wgrad_gemm(x, weight, stride, padding, groups):
                 gw = conv_wgrad_gemm(x, g, weight.shape, stride, padding, col=col)
             elif _use_wgrad_bmm(x, weight, stride, padding, groups):
@@ -1922,7 +1932,7 @@ class Conv2dFn(torch.autograd.Function):
                 gw = conv_wgrad_grouped_gemm(x, g, weight.shape, stride, padding, groups)
             else:
                 gw = conv_wgrad(x, g, weight.shape, stride, padding, groups)
-        return gx, gw, None, None, None, None
+        return gx, gw, None, None, None, None, None
 
 
 # When the conv weight gradient runs on K17 (tools/wgrad_bench.py, batch 32, MI355X,
@@ -1976,8 +1986,11 @@ def _use_wgrad_gemm(x, weight, stride, padding, groups=1):
         return False
     if R * S == 1:
         # 1x1 (the ResNet downsamples): layer3.0 / layer4.0 33 / 23 us vs K17's 1x1 kernel
-        # 44 / 44; layer2.0's (28x28 plane) stays on K17 (84 vs 42; tools/ds_gemm_probe.py)
-        return Co >= 256
+        # 44 / 44; layer2.0's (28x28 plane) stays on K17 (84 vs 42; tools/ds_gemm_probe.py).
+        # Under cudnn.deterministic also every 1x1 on a 7x7 plane: MIOpen's deterministic
+        # weight gradient takes 74-137 us there (MobileNetV2 960 -> 160: GEMM 25, K17 45;
+        # tools/conv1x1_probe.py, profiles/r6_conv1x1_probe.jsonl)
+        return Co >= 256 or (oh * ow <= 49 and torch.backends.cudnn.deterministic)
     return Co >= 128 and C_ * R * S >= 1152
 
 
@@ -1999,7 +2012,52 @@ def _use_wgrad_bmm(x, weight, stride, padding, groups=1):
         return False
     if _pair(stride) != [1, 1] or _pair(padding) != [0, 0]:
         return False
-    return x.dim() == 4 and x.shape[2] * x.shape[3] >= 400
+    # 14x14 planes too under cudnn.deterministic (MobileNetV2's 14x14 1x1s: 16-27 us vs K17's
+    # 39-44; tools/conv1x1_probe.py) where the im2col GEMM does not take them
+    p = x.shape[2] * x.shape[3] if x.dim() == 4 else 0
+    return p >= 400 or (p >= 100 and torch.backends.cudnn.deterministic)
+
+
+# The input gradient of 1x1 stride-1 convs as ONE strided-batched library GEMM,
+# dx[n] = W^T @ dy[n] (conv1x1_dgrad_gemm), on the shapes where MIOpen's deterministic
+# backward-data solver is slower (tools/conv1x1_probe.py over every 1x1 stride-1 conv of
+# ResNet-50 / MobileNetV2 / RegNetX-3200M at batch 32, profiles/r6_conv1x1_probe.jsonl):
+#   112x112 planes, all (MobileNetV2 16 -> 96: 110 -> 38 us);
+#   7x7 planes with Co <= 4 C (ResNet-50 512 -> 2048: 157 -> 37; MobileNetV2 960 -> 160:
+#       15.1 -> 12.5; 160 -> 960 is slower as a GEMM, 16.5 -> 41.6);
+#   14x14 / 28x28 planes with C >= 128 and Co >= C, and Co >= 2 C on 14x14 (ResNet-50
+#       256 -> 1024: 53 -> 35; RegNetX 192 -> 432: 103 -> 51; 432 -> 432 on 14x14 is not);
+#   56x56 planes never (the GEMM is 1.3-2.5x slower there).
+# A/B knob: SSQ_DGRAD_1X1_GEMM=0.
+DGRAD_1X1_GEMM = os.environ.get("SSQ_DGRAD_1X1_GEMM", "1") != "0"
+
+
+def _use_dgrad_1x1(x, weight, stride, padding, groups=1):
+    if not DGRAD_1X1_GEMM or WGRAD_POLICY == "never" or groups != 1 \
+            or tuple(weight.shape[2:]) != (1, 1) or not torch.backends.cudnn.deterministic:
+        return False
+    if _pair(stride) != [1, 1] or _pair(padding) != [0, 0]:
+        return False
+    if x.dim() != 4 or not x.is_cuda or x.dtype != torch.float32:
+        return False
+    co, c = int(weight.shape[0]), int(weight.shape[1])
+    p = x.shape[2] * x.shape[3]
+    if p >= 12544:
+        return True
+    if p <= 49:
+        return co <= 4 * c
+    if 196 <= p <= 784:
+        return c >= 128 and co >= c and (p >= 784 or co >= 2 * c)
+    return False
+
+
+def conv1x1_dgrad_gemm(dy, weight):
+    """d loss / d input of a 1x1 / stride 1 / pad 0 ungrouped conv: W^T @ dy[n] for every
+    sample as one strided-batched GEMM (torch.matmul -> hipBLASLt)."""
+    n, co, h, w = (int(v) for v in dy.shape)
+    c = int(weight.shape[1])
+    gx = torch.matmul(weight.detach().reshape(co, c).t(), dy.reshape(n, co, h * w))
+    return gx.view(n, c, h, w)
 
 
 def conv_wgrad_1x1_bmm(x, dy, w_shape):
@@ -2145,6 +2203,11 @@ def conv2d(x, weight, stride=1, padding=0, dilation=1, groups=1):
              (conv_wgrad_supported(x, weight, stride, padding, dilation, groups) and
               _use_k17(x, weight, stride, padding, groups))):
         return Conv2dFn.apply(x, weight, stride, padding, dilation, groups)
+    if torch.is_grad_enabled() and x.requires_grad and \
+            _use_dgrad_1x1(x, weight, stride, padding, groups):
+        # a 1x1 conv K17 does not take (an activation-phase conv, or a small plane): its
+        # input gradient as a GEMM, its weight gradient (if any) on MIOpen as before
+        return Conv2dFn.apply(x, weight, stride, padding, dilation, groups, True)
     if _use_fwd_1x1(x, weight, stride, padding, dilation, groups) and \
             not (torch.is_grad_enabled() and (x.requires_grad or weight.requires_grad)):
         return conv1x1_fwd_gemm(x, weight, stride)

@@ -1136,17 +1136,64 @@ def test_conv_wgrad_1x1_bmm_matches_fp64(K, cfg):
     err = (dw1.double().cpu() - ref).abs()
     assert bool((err <= 1e-5 * mag + 1e-30).all()), float((err / mag.clamp_min(1e-30)).max())
     wd = w.cuda()
-    assert K._use_wgrad_bmm(xd, wd, 1, 0) == (H * H >= 400)
     old_det = torch.backends.cudnn.deterministic
-    torch.backends.cudnn.deterministic = True
     try:
+        torch.backends.cudnn.deterministic = False
+        assert K._use_wgrad_bmm(xd, wd, 1, 0) == (H * H >= 400)
+        torch.backends.cudnn.deterministic = True  # 14x14 planes and up there
+        assert K._use_wgrad_bmm(xd, wd, 1, 0) == (H * H >= 100)
         wg = wd.clone().requires_grad_(True)
         K.conv2d(xd, wg, 1, 0).backward(dyd)
     finally:
         torch.backends.cudnn.deterministic = old_det
-    if H * H >= 400:
+    if H * H >= 100:
         np.testing.assert_array_equal(host(wg.grad).view(np.int32), host(dw1).view(np.int32))
     assert bool(((wg.grad.double().cpu() - ref).abs() <= 1e-5 * mag + 1e-30).all())
+
+
+@pytest.mark.parametrize("cfg", [
+    # (Nb, C, H, Co, GEMM?): MobileNetV2 features.16's project (960 -> 160 on 7x7: GEMM) and
+    # expand (MIOpen), features.2's 112x112 expand, ResNet-50 layer3's expand (14x14),
+    # layer1.0 conv3 (56x56: MIOpen), a ragged one
+    (32, 960, 7, 160, True), (32, 160, 7, 960, False), (32, 16, 112, 96, True),
+    (32, 256, 14, 1024, True), (32, 64, 56, 256, False), (3, 37, 9, 29, False)])
+@pytest.mark.parametrize("weight_grad", [True, False], ids=["weight_phase", "act_phase"])
+def test_conv1x1_dgrad_gemm_matches_fp64(K, cfg, weight_grad):
+    """The input gradient of 1x1 stride-1 convs as one strided-batched GEMM
+    (K.conv1x1_dgrad_gemm, DGRAD_1X1_GEMM, on the shapes its rule names): vs the fp64 CPU
+    gradient within the fp32 accumulation bound, bit-identical run to run, and what K.conv2d's
+    autograd hands the input under cudnn.deterministic, with the weight trained (Conv2dFn) and
+    fixed (an activation-phase conv): the GEMM's bits where the rule takes the shape, else
+    MIOpen's within the same bound; and the weight's gradient within it too."""
+    Nb, C, H, Co, gemm = cfg
+    gen = torch.Generator().manual_seed(Nb + C + H + Co + 7)
+    x = torch.relu(torch.randn(Nb, C, H, H, generator=gen))
+    w = torch.randn(Co, C, 1, 1, generator=gen) * 0.1
+    dy = torch.randn(Nb, Co, H, H, generator=gen)
+    ref = torch.nn.grad.conv2d_input(x.shape, w.double(), dy.double(), 1, 0)
+    mag = torch.nn.grad.conv2d_input(x.shape, w.double().abs(), dy.double().abs(), 1, 0)
+    xd, wd, dyd = x.cuda(), w.cuda(), dy.cuda()
+    g1, g2 = K.conv1x1_dgrad_gemm(dyd, wd), K.conv1x1_dgrad_gemm(dyd, wd)
+    np.testing.assert_array_equal(host(g1).view(np.int32), host(g2).view(np.int32))
+    assert bool(((g1.double().cpu() - ref).abs() <= 1e-5 * mag + 1e-30).all())
+    old_det = torch.backends.cudnn.deterministic
+    try:
+        torch.backends.cudnn.deterministic = False
+        assert not K._use_dgrad_1x1(xd, wd, 1, 0)
+        torch.backends.cudnn.deterministic = True
+        assert K._use_dgrad_1x1(xd, wd, 1, 0) == gemm
+        xg = xd.clone().requires_grad_(True)
+        wg = wd.clone().requires_grad_(weight_grad)
+        K.conv2d(xg, wg, 1, 0).backward(dyd)
+    finally:
+        torch.backends.cudnn.deterministic = old_det
+    if gemm:
+        np.testing.assert_array_equal(host(xg.grad).view(np.int32), host(g1).view(np.int32))
+    assert bool(((xg.grad.double().cpu() - ref).abs() <= 1e-5 * mag + 1e-30).all())
+    if weight_grad:
+        rw = torch.nn.grad.conv2d_weight(x.double(), w.shape, dy.double(), 1, 0)
+        mw = torch.nn.grad.conv2d_weight(x.double().abs(), w.shape, dy.double().abs(), 1, 0)
+        assert bool(((wg.grad.double().cpu() - rw).abs() <= 1e-5 * mw + 1e-30).all())
 
 
 @pytest.mark.parametrize("cfg", [
