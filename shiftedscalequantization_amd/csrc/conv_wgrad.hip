@@ -1478,27 +1478,58 @@ extern "C" int ssq_conv_wgrad(const float* x, const float* dy, int64_t Nb, int64
 //   dW[Co, C*R*S] = dy2[Co, N*P] @ col[N*P, C*R*S],  P = OH*OW,
 //   dy2[co][n*P + p] = dy[n][co][p],
 //   col[n*P + p][(ci*R + r)*S + s] = x[n][ci][oh*st + r - pad][ow*st + s - pad] (0 outside).
-// One launch writes both operands (workgroups [0, nb1) col, the rest dy2); writes are
-// coalesced along the rows, the x / dy reads hit L2 (the tensors are a few MB).  The GEMM
+// One launch writes both operands (workgroups [0, nb1) col in 64 x 64 tiles transposed
+// through LDS -- x read along the output pixels, col written along its rows, 16-B stores
+// when a row is a multiple of 4 columns -- the rest dy2); the x / dy reads hit L2.  The GEMM
 // (torch.matmul: hipBLASLt, fp32, one deterministic kernel per shape) is the caller's.
 __global__ __launch_bounds__(kBlock) void wgrad_gemm_operands(
     const float* __restrict__ x, const float* __restrict__ dy, uint32_t C, uint32_t H,
     uint32_t W, uint32_t Co, uint32_t R, uint32_t S, uint32_t st, int pad, uint32_t OW,
     uint32_t NP, FastDiv dCRS, FastDiv dRS, FastDiv dS, FastDiv dP, FastDiv dOW, uint32_t CRS,
-    uint32_t P, uint32_t nb1, float* __restrict__ col, float* __restrict__ dy2) {
+    uint32_t P, uint32_t nb1, uint32_t tiles_k, uint32_t vec4, float* __restrict__ col,
+    float* __restrict__ dy2) {
   if (blockIdx.x < nb1) {
-    const uint32_t n1 = NP * CRS;
-    for (uint32_t e = blockIdx.x * kBlock + threadIdx.x; e < n1; e += nb1 * kBlock) {
-      const uint32_t row = fdiv(e, dCRS), k = e - row * CRS;
-      const uint32_t n = fdiv(row, dP), p = row - n * P;
-      const uint32_t oh = fdiv(p, dOW), ow = p - oh * OW;
-      const uint32_t ci = fdiv(k, dRS), rs = k - ci * R * S;
-      const uint32_t r = fdiv(rs, dS), s = rs - r * S;
-      const int ih = (int)(oh * st + r) - pad, iw = (int)(ow * st + s) - pad;
-      float v = 0.0f;
-      if (ih >= 0 && ih < (int)H && iw >= 0 && iw < (int)W)
-        v = x[(((size_t)n * C + ci) * H + ih) * W + iw];
-      col[e] = v;
+    // 64 rows x 64 columns per workgroup through LDS: the x reads run along the rows (output
+    // pixels: consecutive addresses for stride 1), the col writes along the columns (16-B
+    // stores when vec4)
+    __shared__ float tile[64][65];
+    const uint32_t tk = blockIdx.x % tiles_k, tp = blockIdx.x / tiles_k;
+    const uint32_t row0 = tp * 64, k0 = tk * 64, RS = R * S;
+    // thread -> one row (output pixel) and columns kb, kb + 4, ..: the 16 loads in flight
+    const uint32_t pp = threadIdx.x & 63, kb = threadIdx.x >> 6, row = row0 + pp;
+    const bool rok = row < NP;
+    const uint32_t n = rok ? fdiv(row, dP) : 0u, p = row - n * P;
+    const uint32_t oh = fdiv(p, dOW), ow = p - oh * OW;
+    const int ih0 = (int)(oh * st) - pad, iw0 = (int)(ow * st) - pad;
+    const float* xn = x + (size_t)n * C * H * W;
+    float v[16];
+#pragma unroll
+    for (int j = 0; j < 16; ++j) {
+      const uint32_t k = k0 + kb + 4 * j;
+      const uint32_t ci = fdiv(k, dRS), rs = k - ci * RS;
+      const uint32_t r = fdiv(rs, dS), sc = rs - r * S;
+      const int ih = ih0 + (int)r, iw = iw0 + (int)sc;
+      v[j] = 0.0f;
+      if (rok && k < CRS && ih >= 0 && ih < (int)H && iw >= 0 && iw < (int)W)
+        v[j] = xn[((size_t)ci * H + ih) * W + iw];
+    }
+#pragma unroll
+    for (int j = 0; j < 16; ++j) tile[kb + 4 * j][pp] = v[j];
+    __syncthreads();
+    if (vec4) {
+      for (uint32_t i = threadIdx.x; i < 64 * 16; i += kBlock) {
+        const uint32_t pp = i >> 4, kq = (i & 15) << 2;
+        const uint32_t row = row0 + pp, k = k0 + kq;
+        if (row < NP && k < CRS)  // CRS % 4 == 0: the 4 columns are all in range
+          *reinterpret_cast<float4*>(col + (size_t)row * CRS + k) =
+              make_float4(tile[kq][pp], tile[kq + 1][pp], tile[kq + 2][pp], tile[kq + 3][pp]);
+      }
+    } else {
+      for (uint32_t i = threadIdx.x; i < 64 * 64; i += kBlock) {
+        const uint32_t pp = i >> 6, kk = i & 63;
+        const uint32_t row = row0 + pp, k = k0 + kk;
+        if (row < NP && k < CRS) col[(size_t)row * CRS + k] = tile[kk][pp];
+      }
     }
     return;
   }
@@ -1607,13 +1638,18 @@ extern "C" int ssq_wgrad_gemm_operands(const float* x, const float* dy, int64_t 
   const int64_t P = OH * OW, NP = Nb * P, CRS = C * R * S;
   SSQ_REQUIRE(NP * CRS < (1ll << 31) && Co * NP < (1ll << 31) && Nb * C * H * W < (1ll << 31),
               SSQ_E_ARG, "ssq_wgrad_gemm_operands: operands exceed 2^31 elements");
-  const uint32_t nb1 = col ? (uint32_t)std::min<int64_t>((NP * CRS + kBlock - 1) / kBlock, 8192) : 0u;
+  // col in 64 x 64 tiles (float4 stores when the rows are whole 16-B pieces)
+  const bool vec4 = col && CRS % 4 == 0 && ((uintptr_t)col & 15) == 0;
+  const int64_t tiles_k = (CRS + 63) / 64, tiles = ((NP + 63) / 64) * tiles_k;
+  SSQ_REQUIRE(tiles < (1ll << 31), SSQ_E_ARG, "ssq_wgrad_gemm_operands: too many tiles");
+  const uint32_t nb1 = col ? (uint32_t)tiles : 0u;
   const uint32_t nb2 = dy2 ? (uint32_t)std::min<int64_t>((Co * NP + kBlock - 1) / kBlock, 2048) : 0u;
   hipLaunchKernelGGL(wgrad_gemm_operands, dim3(nb1 + nb2), dim3(kBlock), 0, (hipStream_t)stream,
                      x, dy, (uint32_t)C, (uint32_t)H, (uint32_t)W, (uint32_t)Co, (uint32_t)R,
                      (uint32_t)S, (uint32_t)stride, (int)pad, (uint32_t)OW, (uint32_t)NP,
                      make_fastdiv((uint32_t)CRS), make_fastdiv((uint32_t)(R * S)),
                      make_fastdiv((uint32_t)S), make_fastdiv((uint32_t)P),
-                     make_fastdiv((uint32_t)OW), (uint32_t)CRS, (uint32_t)P, nb1, col, dy2);
+                     make_fastdiv((uint32_t)OW), (uint32_t)CRS, (uint32_t)P, nb1,
+                     (uint32_t)tiles_k, (uint32_t)vec4, col, dy2);
   return check_launch("ssq_wgrad_gemm_operands");
 }

@@ -1899,6 +1899,12 @@ class Conv2dFn(torch.autograd.Function):
             y, col = conv_fwd_gemm(x, weight, stride, padding)
             ctx.save_for_backward(x, weight, col)
             return y
+        if not lib_wgrad and ctx.needs_input_grad[1] and GROUPED_GEMM_FWD and \
+                _use_wgrad_grouped_gemm(x, weight, stride, padding, groups):
+            # the im2col matrix the grouped weight gradient reads, built once, forward first
+            y, col = conv_fwd_grouped_gemm(x, weight, stride, padding, groups)
+            ctx.save_for_backward(x, weight, col)
+            return y
         ctx.save_for_backward(x, weight, None)
         if _use_fwd_1x1(x, weight, stride, padding, dilation, groups):
             return conv1x1_fwd_gemm(x, weight, stride)
@@ -1929,7 +1935,8 @@ class Conv2dFn(torch.autograd.Function):
             elif _use_wgrad_bmm(x, weight, stride, padding, groups):
                 gw = conv_wgrad_1x1_bmm(x, g, weight.shape)
             elif _use_wgrad_grouped_gemm(x, weight, stride, padding, groups):
-                gw = conv_wgrad_grouped_gemm(x, g, weight.shape, stride, padding, groups)
+                gw = conv_wgrad_grouped_gemm(x, g, weight.shape, stride, padding, groups,
+                                             col=col)
             else:
                 gw = conv_wgrad(x, g, weight.shape, stride, padding, groups)
         return gx, gw, None, None, None, None, None
@@ -2079,6 +2086,9 @@ def conv_wgrad_1x1_bmm(x, dy, w_shape):
 # 4) K17 stays faster and keeps them.  Bit-identical run to run, within 1e-6 of float64.
 # A/B knob: SSQ_WGRAD_GROUPED_GEMM=0.
 WGRAD_GROUPED_GEMM = os.environ.get("SSQ_WGRAD_GROUPED_GEMM", "1") != "0"
+# ... and the forward of those convs as one GEMM over the groups on the same im2col matrix,
+# built once, in the forward (conv_fwd_grouped_gemm).  A/B knob: SSQ_GROUPED_GEMM_FWD=0.
+GROUPED_GEMM_FWD = os.environ.get("SSQ_GROUPED_GEMM_FWD", "1") != "0"
 
 
 def _use_wgrad_grouped_gemm(x, weight, stride, padding, groups=1):
@@ -2096,17 +2106,37 @@ def _use_wgrad_grouped_gemm(x, weight, stride, padding, groups=1):
     return oh * ow <= 196
 
 
-def conv_wgrad_grouped_gemm(x, dy, w_shape, stride, padding, groups):
+def conv_wgrad_grouped_gemm(x, dy, w_shape, stride, padding, groups, col=None):
     """d loss / d weight of a grouped conv: the im2col matrix of every input channel and the
     permuted gradient (ssq_wgrad_gemm_operands, as for an ungrouped conv of C_in = Cig * G),
     then one strided-batched GEMM over the groups (group g: its Cog rows of dy2 against its
-    Cig * R * S columns of col)."""
+    Cig * R * S columns of col).  col may be the forward's (conv_fwd_grouped_gemm), saved."""
     Co, Cig, R, S = (int(v) for v in w_shape)
-    col, dy2 = gemm_operands(x, dy, (Co, Cig * groups, R, S), stride, padding)
+    c2, dy2 = gemm_operands(x, dy, (Co, Cig * groups, R, S), stride, padding,
+                            want_col=col is None, want_dy2=True)
+    col = c2 if col is None else col
     NP = col.shape[0]
     a = dy2.view(groups, Co // groups, NP)
     b = col.view(NP, groups, Cig * R * S).transpose(0, 1)
     return torch.matmul(a, b).reshape(tuple(w_shape))
+
+
+def conv_fwd_grouped_gemm(x, weight, stride, padding, groups):
+    """F.conv2d of a grouped conv (no bias) on _use_wgrad_grouped_gemm's shapes as the im2col
+    matrix of every input channel (the one its weight gradient reads: returned, to be saved)
+    and ONE strided-batched GEMM over the groups, Y[g] = W[g] @ col[:, g]^T (G x Cog x N*P),
+    then permuted to NCHW.  RegNetX-3200M s3.b1's 'b' conv (g = 9, stride 2): MIOpen's
+    deterministic forward 102.5 us; here the im2col build moves from the backward to the
+    forward (tools/recon_configs_trace.py).  Returns (y, col)."""
+    Nb, C_, H, W, Co, R, S, st, pad, OH, OW = _gemm_geo(x.shape, weight.shape, stride, padding)
+    C_ = int(weight.shape[1]) * groups
+    k = int(weight.shape[1]) * R * S
+    col, _ = gemm_operands(x, None, (Co, C_, R, S), stride, padding, want_col=True,
+                           want_dy2=False)
+    y = torch.matmul(weight.detach().reshape(groups, Co // groups, k),
+                     col.view(-1, groups, k).permute(1, 2, 0))
+    y = y.view(groups, Co // groups, Nb, OH * OW).permute(2, 0, 1, 3).contiguous()
+    return y.view(Nb, Co, OH, OW), col
 
 
 def _use_fwd_gemm(x, weight, stride, padding, groups=1):

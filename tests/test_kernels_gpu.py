@@ -1206,7 +1206,9 @@ def test_conv_wgrad_grouped_gemm_matches_fp64(K, cfg):
     every channel and one strided-batched GEMM over the groups (K.conv_wgrad_grouped_gemm,
     WGRAD_GROUPED_GEMM): vs the fp64 CPU gradient within the fp32 accumulation bound,
     bit-identical run to run, and what K.conv2d's training path hands the weight (larger
-    planes: K17 as before)."""
+    planes: K17 as before); the forward as one GEMM over the groups on the same im2col
+    matrix (K.conv_fwd_grouped_gemm) likewise, and the weight gradient from its saved
+    matrix bit-identical to the one built in the backward."""
     Nb, C, H, st, G = cfg
     gen = torch.Generator().manual_seed(sum(cfg))
     w_shape = (C, C // G, 3, 3)
@@ -1224,16 +1226,30 @@ def test_conv_wgrad_grouped_gemm_matches_fp64(K, cfg):
     np.testing.assert_array_equal(host(dw1).view(np.int32), host(dw2).view(np.int32))
     err = (dw1.double().cpu() - ref).abs()
     assert bool((err <= 1e-5 * mag + 1e-30).all()), float((err / mag.clamp_min(1e-30)).max())
+    # the forward as one GEMM over the groups on the same im2col matrix (GROUPED_GEMM_FWD)
+    yref = torch.nn.functional.conv2d(x.double(), w.double(), None, st, 1, 1, G)
+    ymag = torch.nn.functional.conv2d(x.double().abs(), w.double().abs(), None, st, 1, 1, G)
+    if small:
+        y1, col = K.conv_fwd_grouped_gemm(xd, wd, st, 1, G)
+        y2, _ = K.conv_fwd_grouped_gemm(xd, wd, st, 1, G)
+        np.testing.assert_array_equal(host(y1).view(np.int32), host(y2).view(np.int32))
+        assert y1.shape == yref.shape and y1.is_contiguous()
+        assert bool(((y1.double().cpu() - yref).abs() <= 1e-5 * ymag + 1e-30).all())
+        dw3 = K.conv_wgrad_grouped_gemm(xd, dyd, w_shape, st, 1, G, col=col)
+        np.testing.assert_array_equal(host(dw3).view(np.int32), host(dw1).view(np.int32))
     old_det = torch.backends.cudnn.deterministic
     torch.backends.cudnn.deterministic = True
     try:
         wg = wd.clone().requires_grad_(True)
-        K.conv2d(xd, wg, st, 1, 1, G).backward(dyd)
+        yo = K.conv2d(xd, wg, st, 1, 1, G)
+        yo.backward(dyd)
     finally:
         torch.backends.cudnn.deterministic = old_det
     if small:
         np.testing.assert_array_equal(host(wg.grad).view(np.int32), host(dw1).view(np.int32))
+        np.testing.assert_array_equal(host(yo.detach()).view(np.int32), host(y1).view(np.int32))
     assert bool(((wg.grad.double().cpu() - ref).abs() <= 1e-5 * mag + 1e-30).all())
+    assert bool(((yo.detach().double().cpu() - yref).abs() <= 1e-5 * ymag + 1e-30).all())
 
 
 @pytest.mark.parametrize("cfg", [
