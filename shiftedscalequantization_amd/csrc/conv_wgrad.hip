@@ -1485,7 +1485,7 @@ extern "C" int ssq_conv_wgrad(const float* x, const float* dy, int64_t Nb, int64
 __global__ __launch_bounds__(kBlock) void wgrad_gemm_operands(
     const float* __restrict__ x, const float* __restrict__ dy, uint32_t C, uint32_t H,
     uint32_t W, uint32_t Co, uint32_t R, uint32_t S, uint32_t st, int pad, uint32_t OW,
-    uint32_t NP, FastDiv dCRS, FastDiv dRS, FastDiv dS, FastDiv dP, FastDiv dOW, uint32_t CRS,
+    uint32_t NP, FastDiv dRS, FastDiv dS, FastDiv dP, FastDiv dOW, uint32_t CRS,
     uint32_t P, uint32_t nb1, uint32_t tiles_k, uint32_t vec4, float* __restrict__ col,
     float* __restrict__ dy2) {
   if (blockIdx.x < nb1) {
@@ -1647,9 +1647,8 @@ extern "C" int ssq_wgrad_gemm_operands(const float* x, const float* dy, int64_t 
   hipLaunchKernelGGL(wgrad_gemm_operands, dim3(nb1 + nb2), dim3(kBlock), 0, (hipStream_t)stream,
                      x, dy, (uint32_t)C, (uint32_t)H, (uint32_t)W, (uint32_t)Co, (uint32_t)R,
                      (uint32_t)S, (uint32_t)stride, (int)pad, (uint32_t)OW, (uint32_t)NP,
-                     make_fastdiv((uint32_t)CRS), make_fastdiv((uint32_t)(R * S)),
-                     make_fastdiv((uint32_t)S), make_fastdiv((uint32_t)P),
-                     make_fastdiv((uint32_t)OW), (uint32_t)CRS, (uint32_t)P, nb1,
-                     (uint32_t)tiles_k, (uint32_t)vec4, col, dy2);
+                     make_fastdiv((uint32_t)(R * S)), make_fastdiv((uint32_t)S),
+                     make_fastdiv((uint32_t)P), make_fastdiv((uint32_t)OW), (uint32_t)CRS,
+                     (uint32_t)P, nb1, (uint32_t)tiles_k, (uint32_t)vec4, col, dy2);
   return check_launch("ssq_wgrad_gemm_operands");
 }
