@@ -10,6 +10,7 @@ Feature caching keeps tensors on the device by default (the reference moves ever
 to the host with .cpu(); quant_layer.py:247,278) -- identical values, no PCIe round trip.
 """
 import contextlib
+import os
 from typing import Union
 
 import torch
@@ -20,6 +21,11 @@ from .. import kernels as K
 
 # Frozen-weight cache of a validation pass (frozen_weight_cache): module -> (key, W_hat).
 _FROZEN_W = None
+
+# A QuantModule's epilogue with an act quantizer and no gamma^z / phi^z (BRECQ's act phase
+# without --bias_cal) through the general epilogue (K.epilogue) rather than bias_act_quant.
+# A/B knob: SSQ_EPI_NONAFFINE_Q=0.
+EPI_NONAFFINE_Q = os.environ.get("SSQ_EPI_NONAFFINE_Q", "1") != "0"
 
 
 @contextlib.contextmanager
@@ -414,7 +420,11 @@ class QuantModule(nn.Module):
                 # the parent block's next conv folds this epilogue into its im2col GEMM
                 # (kernels.EPI_CONSUMER); anything else materialises it
                 return K.lazy_epilogue(out, bias, gamma, phi, relu, q)
-            if gamma is not None:
+            if gamma is not None or (q is not None and EPI_NONAFFINE_Q):
+                # (no gamma^z / phi^z with an act quantizer: the general epilogue too, whose
+                # backward sums the act delta per (n, c) row and hands its finalisation to
+                # the next launch's task list -- bias_act_quant's backward finalises in a
+                # launch of its own)
                 out = K.epilogue(out, bias, gamma, phi, None, relu, q)
                 act_q = act_q and q is None
             elif q is not None:
