@@ -1611,7 +1611,7 @@ def fc_recon_iter(x_cache, tgt_cache, slot, bs, w, v, what, delta, zp, n_bits, b
             raise A.SSQError(f"fc_recon_iter: {nm} must be contiguous [Co, Ci]")
     d, dp = fptr(delta.detach().reshape(-1), "delta")
     z, zpp = fptr(zp.detach().reshape(-1), "zero_point")
-    bp = fptr(bias.detach().reshape(-1), "bias")[1] if bias is not None else None
+    bt, bp = fptr(bias.detach().reshape(-1), "bias") if bias is not None else (None, None)
     dev_ = w.device
     g = torch.empty(bs, Co, device=dev_) if g is None else g
     loss = torch.empty(1, device=dev_) if loss_out is None else loss_out
@@ -1775,8 +1775,10 @@ def gemm_operands(x, dy, w_shape, stride, padding, want_col=True, want_dy2=True)
     dev_ = (x if x is not None else dy).device
     col = torch.empty(NP, C_ * R * S, dtype=torch.float32, device=dev_) if want_col else None
     dy2 = torch.empty(Co, NP, dtype=torch.float32, device=dev_) if want_dy2 else None
-    xp = fptr(x.detach(), "x")[1] if want_col else None
-    dp = fptr(dy.detach(), "dy")[1] if want_dy2 else None
+    # (the contiguous tensors are held to the launch: a copy made here must not be freed
+    # and its block reused by the next one before the kernel has read it)
+    xt, xp = fptr(x.detach(), "x") if want_col else (None, None)
+    dt, dp = fptr(dy.detach(), "dy") if want_dy2 else (None, None)
     call("ssq_wgrad_gemm_operands", xp, dp, Nb, C_, H, W, Co, R, S, st, pad, _vp(col), _vp(dy2),
          stream_of(col if want_col else dy2))
     return col, dy2
