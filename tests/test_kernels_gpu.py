@@ -1151,6 +1151,22 @@ def test_conv_wgrad_1x1_bmm_matches_fp64(K, cfg):
     assert bool(((wg.grad.double().cpu() - ref).abs() <= 1e-5 * mag + 1e-30).all())
 
 
+def test_gemm_operands_noncontiguous_inputs(K):
+    """ssq_wgrad_gemm_operands from non-contiguous x and dy (channels-last x, a transposed
+    view of dy): both are copied to contiguous tensors held until the launch -- the operands
+    equal those of the contiguous inputs, bit for bit."""
+    gen = torch.Generator().manual_seed(11)
+    x = torch.randn(4, 16, 9, 9, generator=gen).cuda()
+    dy = torch.randn(4, 24, 9, 9, generator=gen).cuda()
+    xn = x.to(memory_format=torch.channels_last)
+    dyn = dy.transpose(2, 3).contiguous().transpose(2, 3)
+    assert not xn.is_contiguous() and not dyn.is_contiguous()
+    c1, d1 = K.gemm_operands(x, dy, (24, 16, 3, 3), 1, 1)
+    c2, d2 = K.gemm_operands(xn, dyn, (24, 16, 3, 3), 1, 1)
+    np.testing.assert_array_equal(host(c1).view(np.int32), host(c2).view(np.int32))
+    np.testing.assert_array_equal(host(d1).view(np.int32), host(d2).view(np.int32))
+
+
 @pytest.mark.parametrize("cfg", [
     # (Nb, C, H, Co, GEMM?): MobileNetV2 features.16's project (960 -> 160 on 7x7: GEMM) and
     # expand (MIOpen), features.2's 112x112 expand, ResNet-50 layer3's expand (14x14),
