@@ -1907,9 +1907,13 @@ class Conv2dFn(torch.autograd.Function):
             y, col = conv_fwd_grouped_gemm(x, weight, stride, padding, groups)
             ctx.save_for_backward(x, weight, col)
             return y
-        ctx.save_for_backward(x, weight, None)
         if _use_fwd_1x1(x, weight, stride, padding, dilation, groups):
-            return conv1x1_fwd_gemm(x, weight, stride)
+            y, xs = conv1x1_fwd_gemm(x, weight, stride, keep_xs=True)
+            keep = (not lib_wgrad and ctx.needs_input_grad[1]
+                    and _use_wgrad_bmm_s2(x, weight, stride, padding, groups))
+            ctx.save_for_backward(x, weight, xs if keep else None)
+            return y
+        ctx.save_for_backward(x, weight, None)
         return torch.nn.functional.conv2d(x, weight, None, stride, padding, dilation, groups)
 
     @staticmethod
@@ -1936,6 +1940,8 @@ class Conv2dFn(torch.autograd.Function):
                 gw = conv_wgrad_gemm(x, g, weight.shape, stride, padding, col=col)
             elif _use_wgrad_bmm(x, weight, stride, padding, groups):
                 gw = conv_wgrad_1x1_bmm(x, g, weight.shape)
+            elif col is not None and _use_wgrad_bmm_s2(x, weight, stride, padding, groups):
+                gw = conv_wgrad_1x1_bmm(col, g, weight.shape)   # col: the forward's xs
             elif _use_wgrad_grouped_gemm(x, weight, stride, padding, groups):
                 gw = conv_wgrad_grouped_gemm(x, g, weight.shape, stride, padding, groups,
                                              col=col)
@@ -2176,15 +2182,39 @@ def _use_fwd_1x1(x, weight, stride, padding, dilation, groups):
     return not (100 < oh * ow < 400 and x.shape[0] < 128)
 
 
-def conv1x1_fwd_gemm(x, weight, stride):
+def conv1x1_fwd_gemm(x, weight, stride, keep_xs=False):
     """F.conv2d of a 1x1 / pad 0 / stride s conv as one strided-batched GEMM on the
-    subsampled input (see FWD_1X1_GEMM)."""
+    subsampled input (see FWD_1X1_GEMM); keep_xs: also return that input, contiguous (the
+    weight gradient's operand, conv_wgrad_1x1_bmm)."""
     st = stride if isinstance(stride, int) else stride[0]
-    xs = x[:, :, ::st, ::st]
+    xs = x[:, :, ::st, ::st].contiguous()
     n, c, oh, ow = xs.shape
     co = int(weight.shape[0])
-    y = torch.matmul(weight.detach().reshape(co, c), xs.reshape(n, c, oh * ow))
-    return y.view(n, co, oh, ow)
+    y = torch.matmul(weight.detach().reshape(co, c), xs.view(n, c, oh * ow))
+    y = y.view(n, co, oh, ow)
+    return (y, xs) if keep_xs else y
+
+
+# 1x1 stride-2 weight gradients on output planes >= 400 pixels (the forward GEMM above made
+# the subsampled input contiguous) with channel counts in whole 64s: one strided-batched GEMM
+# + batch sum over that input (conv_wgrad_1x1_bmm) instead of K17's 1x1 kernel.
+# tools/ds_wgrad_probe.py (profiles/r6_ds_wgrad_probe.jsonl), batch 32: ResNet-18 layer2.0
+# 41.1 -> 31.6 us, ResNet-50 layer2.0 138.9 -> 65.3; RegNetX s2.b1 (96 -> 192) is slower as
+# the GEMM (79.3 vs 43.6) and keeps K17; on 14x14 and 7x7 planes the im2col GEMM stays.
+# A/B knob: SSQ_WGRAD_S2_BMM=0.
+WGRAD_S2_BMM = os.environ.get("SSQ_WGRAD_S2_BMM", "1") != "0"
+
+
+def _use_wgrad_bmm_s2(x, weight, stride, padding, groups=1):
+    if not WGRAD_S2_BMM or WGRAD_POLICY != "auto" or groups != 1 \
+            or tuple(weight.shape[2:]) != (1, 1) or _pair(padding) != [0, 0]:
+        return False
+    st = _pair(stride)
+    if st[0] != st[1] or st[0] < 2:
+        return False
+    oh, ow = _out_plane(x, weight, st[0], 0)
+    co, c = int(weight.shape[0]), int(weight.shape[1])
+    return oh * ow >= 400 and c % 64 == 0 and co % 64 == 0
 
 
 def _use_k17(x, weight, stride, padding, groups=1):

@@ -1109,7 +1109,15 @@ def test_conv1x1_stride2_forward_gemm(K, cfg):
         K.FWD_1X1_GEMM = old
         torch.backends.cudnn.deterministic = old_det
     np.testing.assert_array_equal(host(xg.grad).view(np.int32), host(xm.grad).view(np.int32))
-    np.testing.assert_array_equal(host(wg.grad).view(np.int32), host(wm.grad).view(np.int32))
+    if use and K._use_wgrad_bmm_s2(xd, wd, 2, 0):
+        # the weight gradient then runs on the forward's subsampled input (WGRAD_S2_BMM,
+        # test_conv_wgrad_s2_bmm_matches_fp64): another summation order, same bound
+        rw = torch.nn.grad.conv2d_weight(x.double(), w.shape, dy.double().cpu(), 2, 0)
+        mw = torch.nn.grad.conv2d_weight(x.double().abs(), w.shape, dy.double().abs().cpu(), 2, 0)
+        for gw in (wg.grad, wm.grad):
+            assert bool(((gw.double().cpu() - rw).abs() <= 1e-5 * mw + 1e-30).all())
+    else:
+        np.testing.assert_array_equal(host(wg.grad).view(np.int32), host(wm.grad).view(np.int32))
 
 
 @pytest.mark.parametrize("cfg", [
@@ -1149,6 +1157,43 @@ def test_conv_wgrad_1x1_bmm_matches_fp64(K, cfg):
     if H * H >= 100:
         np.testing.assert_array_equal(host(wg.grad).view(np.int32), host(dw1).view(np.int32))
     assert bool(((wg.grad.double().cpu() - ref).abs() <= 1e-5 * mag + 1e-30).all())
+
+
+@pytest.mark.parametrize("cfg", [
+    # (Nb, C, H, Co, bmm?): ResNet-18 layer2.0's downsample (28x28 out), a 64-multiple one at
+    # the 400-pixel edge, RegNetX s2.b1's 96 -> 192 (K17 keeps it), a 14x14 one (im2col GEMM)
+    (32, 64, 56, 128, True), (3, 64, 40, 64, True), (4, 96, 56, 192, False),
+    (4, 128, 28, 256, False)])
+def test_conv_wgrad_s2_bmm_matches_fp64(K, cfg):
+    """1x1 stride-2 weight gradients as one batched GEMM + batch sum over the subsampled
+    input the forward GEMM made contiguous (WGRAD_S2_BMM): K.conv2d's training path under
+    cudnn.deterministic hands the weight exactly K.conv_wgrad_1x1_bmm(xs)'s bits where the
+    rule takes the shape, and every route is within the fp32 bound of the fp64 gradient."""
+    Nb, C, H, Co, bmm = cfg
+    gen = torch.Generator().manual_seed(Nb + C + H + Co)
+    x = torch.relu(torch.randn(Nb, C, H, H, generator=gen))
+    w = torch.randn(Co, C, 1, 1, generator=gen) * 0.1
+    dy = torch.randn(Nb, Co, H // 2, H // 2, generator=gen)
+    ref = torch.nn.grad.conv2d_weight(x.double(), w.shape, dy.double(), 2, 0)
+    mag = torch.nn.grad.conv2d_weight(x.double().abs(), w.shape, dy.double().abs(), 2, 0)
+    xd, wd, dyd = x.cuda(), w.cuda(), dy.cuda()
+    assert K._use_wgrad_bmm_s2(xd, wd, 2, 0) == bmm
+    old_det = torch.backends.cudnn.deterministic
+    torch.backends.cudnn.deterministic = True
+    try:
+        wg = wd.clone().requires_grad_(True)
+        y = K.conv2d(xd, wg, 2, 0)
+        y.backward(dyd)
+    finally:
+        torch.backends.cudnn.deterministic = old_det
+    if bmm:
+        xs = xd[:, :, ::2, ::2].contiguous()
+        gw = K.conv_wgrad_1x1_bmm(xs, dyd, w.shape)
+        np.testing.assert_array_equal(host(wg.grad).view(np.int32), host(gw).view(np.int32))
+    assert bool(((wg.grad.double().cpu() - ref).abs() <= 1e-5 * mag + 1e-30).all())
+    yref = torch.nn.functional.conv2d(x.double(), w.double(), None, 2)
+    ymag = torch.nn.functional.conv2d(x.double().abs(), w.double().abs(), None, 2)
+    assert bool(((y.detach().double().cpu() - yref).abs() <= 1e-5 * ymag + 1e-30).all())
 
 
 def test_gemm_operands_noncontiguous_inputs(K):
